@@ -1,0 +1,85 @@
+"""ctypes binding of the C-ABI library ``libasrx.so`` (declared in ``include/asrx.h``).
+
+The library is built in-tree by ``make -C asr-model_amd`` (``__graft_entry__.build()``).  There is
+no fallback: if the library is missing, or a call is made without a GPU, the call raises.
+
+Every entry point returns 0 on success; a nonzero code is turned into ``RuntimeError`` carrying
+``asrx_last_error()`` (SURVEY.md §8(b) "Errors").
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (loads the HIP runtime first so libasrx binds to the same instance)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libasrx.so")
+
+_i64 = ctypes.c_int64
+_i32 = ctypes.c_int
+_f32 = ctypes.c_float
+_p = ctypes.c_void_p
+_u32 = ctypes.c_uint32
+
+# name -> (restype, argtypes).  Kept in the order of include/asrx.h.
+SIGNATURES = {
+    "asrx_last_error": (ctypes.c_char_p, []),
+    "asrx_abi_version": (_i32, []),
+    "asrx_noise_hash": (_u32, [_u32, _u32]),
+    "asrx_mel_frames": (_i32, [_i64]),
+    "asrx_logmel": (_i32, [_p, _i64, _i64, _i64, _p, _p, _p, _p, _i32, _i64, _p, _p, _i64, _p]),
+    "asrx_gemm": (
+        _i32,
+        [_i32, _p, _i64, _i64, _i32, _i32, _p, _i64, _i64, _i32, _i32, _p, _i64, _i64, _p, _p,
+         _i64, _i64, _i64, _i64, _f32, _f32, _i32, _i64, _i64, _i32, _p],
+    ),
+}
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"asrx native library not found at {LIB_PATH}; build it with `make -C asr-model_amd`"
+            )
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def exported_symbols() -> list[str]:
+    return list(SIGNATURES)
+
+
+def check(rc: int, name: str) -> None:
+    if rc != 0:
+        msg = load().asrx_last_error().decode(errors="replace")
+        raise RuntimeError(f"{name} failed (code {rc}): {msg}")
+
+
+def call(name: str, *args) -> None:
+    check(getattr(load(), name)(*args), name)
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t) -> int | None:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def require_gpu(*tensors) -> None:
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("asrx kernels take device tensors (got a CPU tensor); there is no CPU path")

@@ -1,0 +1,126 @@
+// asrx — MI355X (gfx950 / CDNA4) native kernels for the ASR hot path.
+// Shared device helpers and the C-ABI error plumbing.
+//
+// Conventions (see include/asrx.h):
+//   * every entry point is extern "C", takes raw device pointers, int64 sizes/strides and a
+//     hipStream_t, launches on that stream and returns 0 on success or a nonzero code;
+//   * kernels never allocate; the caller (PyTorch's caching allocator) owns every buffer;
+//   * the last error message is thread-local and read back with asrx_last_error().
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+#include <cstdio>
+#include <cstdarg>
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+namespace asrx {
+
+enum Prec : int { PREC_F32 = 0, PREC_BF16 = 1 };
+
+enum Act : int { ACT_NONE = 0, ACT_GELU = 1, ACT_SILU = 2, ACT_SIGMOID = 3, ACT_RELU = 4 };
+
+void set_error(const char* fmt, ...);
+int check_launch(const char* what);
+
+}  // namespace asrx
+
+#define ASRX_REQUIRE(cond, ...)            \
+  do {                                     \
+    if (!(cond)) {                         \
+      asrx::set_error(__VA_ARGS__);        \
+      return 2;                            \
+    }                                      \
+  } while (0)
+
+#define ASRX_LAUNCHED(name) return asrx::check_launch(name)
+
+// ---------------------------------------------------------------- device helpers
+namespace asrx {
+
+__device__ __forceinline__ float gelu_f(float x) {  // exact (erf) GELU, nn.GELU() default
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+}
+__device__ __forceinline__ float gelu_grad(float x) {
+  float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+  float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+__device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + __expf(-x)); }
+__device__ __forceinline__ float silu_f(float x) { return x * sigmoid_f(x); }
+__device__ __forceinline__ float silu_grad(float x) {
+  float s = sigmoid_f(x);
+  return s * (1.0f + x * (1.0f - s));
+}
+
+__device__ __forceinline__ float apply_act(int act, float x) {
+  switch (act) {
+    case ACT_GELU: return gelu_f(x);
+    case ACT_SILU: return silu_f(x);
+    case ACT_SIGMOID: return sigmoid_f(x);
+    case ACT_RELU: return x > 0.f ? x : 0.f;
+    default: return x;
+  }
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x == NT (multiple of 64). `red` must hold NT/64 floats.
+template <int NT>
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) t += red[i];
+  return t;
+}
+
+// Ordered-int encoding so that atomicMax on int works for any float.
+__host__ __device__ __forceinline__ int float_to_ordered(float f) {
+  int i = __builtin_bit_cast(int, f);
+  return i >= 0 ? i : i ^ 0x7fffffff;
+}
+__host__ __device__ __forceinline__ float ordered_to_float(int i) {
+  return __builtin_bit_cast(float, i >= 0 ? i : i ^ 0x7fffffff);
+}
+
+// ------------------------------------------------------------ counter-based noise
+// The reference draws torch Exp(1) noise inside F.gumbel_softmax (essentials.py:170,
+// model.py:476) and Bernoulli masks inside nn.Dropout (model.py:107,147). Here noise is a pure
+// function of (site key, logical element index): u = (mix(mix(idx ^ k0) + k1) >> 8 + 0.5)/2^24,
+// restated bit-for-bit in oracle/noise.py so the oracle sees the same draws.
+__host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ float noise_uniform(uint32_t key, uint32_t idx) {
+  uint32_t h = mix32(mix32(idx ^ key) + (key * 0x9E3779B9U + 0x632BE5ABU));
+  return ((float)(h >> 8) + 0.5f) * (1.0f / 16777216.0f);
+}
+// Gumbel(0,1) sample g = -log(E), E = -log(u) ~ Exp(1).
+__device__ __forceinline__ float noise_gumbel(uint32_t key, uint32_t idx) {
+  float u = noise_uniform(key, idx);
+  return -logf(-logf(u));
+}
+
+}  // namespace asrx

@@ -1,0 +1,147 @@
+"""GPU parity of the GEMM and log-mel kernels (through the C-ABI)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(A, B):
+    return (A.double() @ B.double()).float()
+
+
+@pytest.mark.parametrize("prec,tol", [(0, 2e-5), (1, 2e-2)])
+@pytest.mark.parametrize("a_kc,b_kc", [(True, True), (True, False), (False, True), (False, False)])
+def test_gemm_layouts(cuda, prec, tol, a_kc, b_kc):
+    from asrx.gemm import gemm
+
+    g = torch.Generator().manual_seed(0)
+    M, N, K = 200, 136, 264
+    A = torch.randn(M, K, generator=g)
+    B = torch.randn(K, N, generator=g)
+    bias = torch.randn(N, generator=g)
+    Ad = (A if a_kc else A.t().contiguous()).to(cuda)
+    Bd = (B.t().contiguous() if b_kc else B).to(cuda)
+    C = torch.empty(M, N, device=cuda)
+    gemm(Ad, Bd, C, M=M, N=N, K=K, lda=K if a_kc else M, ldb=K if b_kc else N, ldc=N, a_kc=a_kc,
+         b_kc=b_kc, bias=bias.to(cuda), precision=prec)
+    ref = _ref(A, B) + bias
+    err = (C.cpu() - ref).abs().max() / ref.abs().max()
+    assert err < tol, err
+
+
+@pytest.mark.parametrize("act", ["gelu", "silu", "sigmoid"])
+def test_gemm_epilogue(cuda, act):
+    from asrx.gemm import gemm
+
+    g = torch.Generator().manual_seed(1)
+    M, N, K = 64, 96, 32
+    A, B = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g)
+    C = torch.empty(M, N, device=cuda)
+    Z = torch.empty(M, N, device=cuda)
+    gemm(A.to(cuda), B.to(cuda), C, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, act=act, Z=Z, precision=0)
+    z = A.double() @ B.double().t()
+    f = {"gelu": torch.nn.functional.gelu, "silu": torch.nn.functional.silu, "sigmoid": torch.sigmoid}[act]
+    assert torch.allclose(Z.cpu().double(), z, atol=1e-4)
+    assert torch.allclose(C.cpu().double(), f(z), atol=1e-4)
+
+
+def test_gemm_splitk_batched_beta(cuda):
+    from asrx.gemm import gemm
+
+    g = torch.Generator().manual_seed(2)
+    Bt, M, N, K = 3, 64, 72, 1000
+    A, B = torch.randn(Bt, M, K, generator=g), torch.randn(Bt, N, K, generator=g)
+    C0 = torch.randn(Bt, M, N, generator=g)
+    C = C0.clone().to(cuda)
+    gemm(A.to(cuda), B.to(cuda), C, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, batch=Bt, sA=M * K, sB=N * K,
+         sC=M * N, beta=1.0, splitk=4, precision=0)
+    ref = C0.double() + A.double() @ B.double().transpose(1, 2)
+    assert torch.allclose(C.cpu().double(), ref, rtol=1e-4, atol=1e-3)
+
+
+def test_conv3_implicit_im2col(cuda):
+    """k3/pad1 Conv1d on channels-last sequences == F.conv1d; dgrad + wgrad via the same kernel."""
+    from asrx.gemm import gemm
+
+    g = torch.Generator().manual_seed(3)
+    Bn, T, Ci, Co = 2, 37, 8, 12
+    x = torch.randn(Bn, Ci, T, generator=g, dtype=torch.float64)
+    W = torch.randn(Co, Ci, 3, generator=g, dtype=torch.float64)
+    ref = torch.nn.functional.conv1d(x, W, padding=1)  # (B, Co, T)
+    xcl = x.transpose(1, 2).contiguous().float().to(cuda)  # (B, T, Ci)
+    Wt = W.permute(0, 2, 1).reshape(Co, 3 * Ci).contiguous().float().to(cuda)  # [o][k*Ci + c]
+    y = torch.empty(Bn * T, Co, device=cuda)
+    gemm(xcl, Wt, y, M=Bn * T, N=Co, K=3 * Ci, lda=Ci, ldb=3 * Ci, ldc=Co, conv_a=True, conv_F=T,
+         conv_C=Ci, precision=0)
+    assert torch.allclose(y.cpu().double().view(Bn, T, Co).transpose(1, 2), ref, atol=1e-4)
+    # wgrad: dW[o, k*Ci + c] = sum_t dy[t, o] x[t + k - 1, c]
+    dy = torch.randn(Bn, Co, T, generator=g, dtype=torch.float64)
+    xr = x.clone().requires_grad_(True)
+    Wr = W.clone().requires_grad_(True)
+    torch.nn.functional.conv1d(xr, Wr, padding=1).backward(dy)
+    dycl = dy.transpose(1, 2).contiguous().float().to(cuda)
+    dW = torch.zeros(Co, 3 * Ci, device=cuda)
+    gemm(dycl, xcl, dW, M=Co, N=3 * Ci, K=Bn * T, lda=Co, ldb=Ci, ldc=3 * Ci, a_kc=False, b_kc=False,
+         conv_b=True, conv_F=T, conv_C=Ci, beta=1.0, splitk=2, precision=0)
+    assert torch.allclose(dW.cpu().double().view(Co, 3, Ci).permute(0, 2, 1), Wr.grad, atol=1e-3)
+    # dgrad: dx = conv3(dy, W~), W~[c][k'*Co + o] = W[o][c][2-k']
+    Wf = W.flip(2).permute(1, 2, 0).reshape(Ci, 3 * Co).contiguous().float().to(cuda)
+    dx = torch.empty(Bn * T, Ci, device=cuda)
+    gemm(dycl, Wf, dx, M=Bn * T, N=Ci, K=3 * Co, lda=Co, ldb=3 * Co, ldc=Ci, conv_a=True, conv_F=T,
+         conv_C=Co, precision=0)
+    assert torch.allclose(dx.cpu().double().view(Bn, T, Ci).transpose(1, 2), xr.grad, atol=1e-3)
+
+
+def test_linear_helpers(cuda):
+    from asrx import gemm as G
+
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(5, 33, 64, generator=g)
+    W = torch.randn(48, 64, generator=g)
+    b = torch.randn(48, generator=g)
+    dy = torch.randn(5, 33, 48, generator=g)
+    with __import__("asrx.prec", fromlist=["x"]).precision("fp32"):
+        y = G.linear_fwd(x.to(cuda), W.to(cuda), b.to(cuda))
+        dx = G.linear_dgrad(dy.to(cuda), W.to(cuda))
+        dW = G.linear_wgrad(dy.to(cuda), x.to(cuda))
+    assert torch.allclose(y.cpu(), x @ W.t() + b, atol=1e-4)
+    assert torch.allclose(dx.cpu(), dy @ W, atol=1e-4)
+    assert torch.allclose(dW.cpu(), dy.reshape(-1, 48).t() @ x.reshape(-1, 64), atol=1e-3)
+
+
+def _clip(n, seed):
+    rng = np.random.default_rng(seed)
+    t = np.arange(n) / 16000.0
+    f = rng.uniform(100, 300)
+    x = 0.5 * np.sin(2 * np.pi * f * t) * (1 + 0.3 * np.sin(2 * np.pi * 3 * t)) + 0.05 * rng.standard_normal(n)
+    return (x / np.abs(x).max()).astype(np.float32)
+
+
+@pytest.mark.parametrize("n", [16000, 480000, 12345])
+def test_logmel_matches_oracle(cuda, n):
+    from asrx.mel import logmel
+    from oracle import mel as omel
+
+    clips = np.stack([_clip(n, s) for s in range(3)])
+    out_bfm = logmel(torch.from_numpy(clips).to(cuda), layout="BFM").cpu().numpy()
+    out_bmf = logmel(torch.from_numpy(clips).to(cuda), layout="BMF").cpu().numpy()
+    for b in range(3):
+        ref = omel.log_mel(clips[b].astype(np.float64))
+        assert out_bmf[b].shape == ref.shape
+        assert np.array_equal(out_bmf[b], out_bfm[b].T)
+        err = np.abs(out_bmf[b] - ref).max()
+        assert err < 2e-4, err
+
+
+def test_logmel_pool_and_silence(cuda):
+    from asrx.mel import logmel
+    from oracle import mel as omel
+
+    clips = np.stack([_clip(480000, 7), np.zeros(480000, np.float32)])
+    out, pooled = logmel(torch.from_numpy(clips).to(cuda), layout="BMF", pool=True)
+    out, pooled = out.cpu().numpy(), pooled.cpu().numpy()
+    assert np.all(out[1] == -1.5)
+    ref = omel.waveform_feature(clips[0].astype(np.float64))[0]
+    assert np.abs(pooled[0] - ref).max() < 1e-6
+    assert np.all(pooled[1] == 0)

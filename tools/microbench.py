@@ -1,0 +1,66 @@
+"""Ad-hoc kernel timing on the GPU box (not part of the product)."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "asr-model_amd")]
+
+import torch  # noqa: E402
+
+
+def timeit(fn, iters=20, warm=3):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e-3
+
+
+def gemm_bench():
+    from asrx import gemm as G
+
+    dev = torch.device("cuda:0")
+    for (M, N, K) in [(96032, 384, 384), (96032, 1152, 384), (96032, 384, 1152), (8192, 40000, 384),
+                      (4096, 4096, 4096)]:
+        x = torch.randn(M, K, device=dev)
+        W = torch.randn(N, K, device=dev)
+        for p in (1, 0):
+            y = torch.empty(M, N, device=dev)
+            t = timeit(lambda: G.gemm(x, W, y, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, precision=p))
+            print(f"gemm prec={p} M={M} N={N} K={K}: {t*1e6:.1f} us  {2*M*N*K/t/1e12:.1f} TF/s", flush=True)
+        dy = torch.randn(M, N, device=dev)
+        t = timeit(lambda: G.linear_wgrad(dy, x))
+        print(f"  wgrad bf16: {t*1e6:.1f} us {2*M*N*K/t/1e12:.1f} TF/s", flush=True)
+        t = timeit(lambda: G.linear_dgrad(dy, W))
+        print(f"  dgrad bf16: {t*1e6:.1f} us {2*M*N*K/t/1e12:.1f} TF/s", flush=True)
+        del x, W, y, dy
+    ref_a = torch.randn(4096, 4096, device=dev, dtype=torch.bfloat16)
+    t = timeit(lambda: ref_a @ ref_a)
+    print(f"torch bf16 4096^3 (hipBLASLt, reference point): {2*4096**3/t/1e12:.1f} TF/s")
+
+
+def mel_bench():
+    from asrx.mel import logmel
+
+    dev = torch.device("cuda:0")
+    B, N = 32, 480000
+    wav = torch.randn(B, N, device=dev)
+    for lay in ("BFM", "BMF"):
+        t = timeit(lambda: logmel(wav, layout=lay, pool=True))
+        F = 1 + N // 160
+        byts = B * (N * 4 + 128 * F * 4 + (N // 160) * 4)
+        print(f"logmel {lay} B={B}: {t*1e6:.1f} us  {byts/t/1e9:.0f} GB/s (algorithmic)", flush=True)
+
+
+if __name__ == "__main__":
+    what = sys.argv[1:] or ["gemm", "mel"]
+    if "mel" in what:
+        mel_bench()
+    if "gemm" in what:
+        gemm_bench()
