@@ -34,6 +34,48 @@ SIGNATURES = {
         [_i32, _p, _i64, _i64, _i32, _i32, _p, _i64, _i64, _i32, _i32, _p, _i64, _i64, _p, _p,
          _i64, _i64, _i64, _i64, _f32, _f32, _i32, _i64, _i64, _i32, _p],
     ),
+    "asrx_abby_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _u32, _i32, _p]),
+    "asrx_abby_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _p]),
+    "asrx_attn_fwd": (_i32, [_i32, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i32, _f32, _p]),
+    "asrx_attn_bwd": (_i32, [_i32, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p,
+                             _i64, _i64, _i64, _i64, _i64, _i32, _f32, _p]),
+    "asrx_layernorm_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _i64, _f32, _p]),
+    "asrx_layernorm_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _p]),
+    "asrx_small_linear_fwd": (_i32, [_p, _p, _p, _p, _i64, _i64, _i64, _i32, _p]),
+    "asrx_small_linear_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i32, _f32, _p]),
+    "asrx_rownorm": (_i32, [_p, _p, _i64, _i64, _p]),
+    "asrx_rownorm_bwd": (_i32, [_p, _p, _p, _p, _i64, _i64, _p]),
+    "asrx_rotary_fwd": (_i32, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _f32, _p]),
+    "asrx_rotary_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _f32, _p]),
+    "asrx_vgate_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _f32, _p]),
+    "asrx_vgate_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p,
+                              _i64, _i64, _i64, _f32, _p]),
+    "asrx_tgate_fwd": (_i32, [_p, _p, _p, _i64, _i64, _p]),
+    "asrx_tgate_bwd": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _p]),
+    "asrx_axpy_row": (_i32, [_p, _p, _p, _p, _i64, _i64, _p]),
+    "asrx_axpy_row_bwd": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _p]),
+    "asrx_jump_select": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p]),
+    "asrx_jump_select_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p]),
+    "asrx_seg_colsum": (_i32, [_p, _p, _i64, _i64, _i64, _f32, _i32, _p]),
+    "asrx_colsum": (_i32, [_p, _p, _i64, _i64, _p]),
+    "asrx_add_rows": (_i32, [_p, _p, _p, _p, _i64, _i64, _i64, _p]),
+    "asrx_lincomb": (_i32, [_p, _p, _p, _f32, _f32, _f32, _p, _i64, _p]),
+    "asrx_act_fwd": (_i32, [_p, _p, _i64, _i32, _p]),
+    "asrx_act_bwd": (_i32, [_p, _p, _p, _i64, _i32, _p]),
+    "asrx_glu_fwd": (_i32, [_p, _p, _i64, _i64, _p]),
+    "asrx_glu_bwd": (_i32, [_p, _p, _p, _i64, _i64, _p]),
+    "asrx_dropout": (_i32, [_p, _p, _i64, _i64, _i64, _i64, _u32, _f32, _p]),
+    "asrx_dwconv_fwd": (_i32, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),
+    "asrx_dwconv_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),
+    "asrx_bn_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _f32, _i32, _p]),
+    "asrx_bn_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p]),
+    "asrx_stem1_fwd": (_i32, [_p, _p, _p, _p, _i64, _i64, _i64, _p]),
+    "asrx_stem1_bwd": (_i32, [_p, _p, _p, _p, _i64, _i64, _i64, _p]),
+    "asrx_embed_fwd": (_i32, [_p, _p, _p, _i64, _i64, _p]),
+    "asrx_embed_bwd": (_i32, [_p, _p, _p, _i64, _i64, _p]),
+    "asrx_ce_fwd": (_i32, [_p, _p, _p, _p, _i64, _i64, _p]),
+    "asrx_ce_bwd": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _p]),
+    "asrx_policy_noise": (_i32, [_p, _i64, _i64, _i64, _u32, _p]),
 }
 
 _lib = None

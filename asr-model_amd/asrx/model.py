@@ -1,0 +1,544 @@
+"""MI355X-native Model with the reference's module tree, parameter names and forward signature
+(model.py:631-672).  `Model(param).state_dict()` is key-compatible with the reference; the forward
+runs the HIP kernels of csrc/ through asrx.ops.
+
+Execution differs from the reference only where batch-1 semantics had to be generalised
+(SURVEY.md §7 "Hard parts"): clips are batched with per-sample BatchNorm statistics, per-sample
+MSheath control flow evaluated on device as masked compute (no .item() syncs), and keyed noise.
+Activations are channels-last (B, T, D) throughout the encoder, so no permutes are needed.
+Blocks 0..L-2 are computed faithfully (the reference recomputes them and discards the result,
+model.py:617-628) under no_grad, since nothing downstream depends on them.
+"""
+from __future__ import annotations
+
+import contextlib
+import math
+
+import torch
+from torch import nn
+from torch.nn.utils.parametrizations import weight_norm
+
+from . import ops
+from .config import Dimensions
+from .noise import NoiseCtx
+
+THETA = 30000.0
+
+# ------------------------------------------------------------------------------- constant tables
+_TABLES: dict = {}
+
+
+def sinusoids(ctx: int, dims: int, device) -> torch.Tensor:
+    """essentials.sinusoids (essentials.py:354-358), evaluated in float32 exactly like the reference
+    and cached on the device."""
+    key = ("pe", ctx, dims, str(device))
+    if key not in _TABLES:
+        tscales = torch.exp(-torch.log(torch.tensor(float(THETA))) / (dims // 2 - 1)
+                            * torch.arange(dims // 2, dtype=torch.float32))
+        scaled = torch.arange(ctx, dtype=torch.float32).unsqueeze(1) * tscales.unsqueeze(0)
+        _TABLES[key] = torch.cat([torch.sin(scaled), torch.cos(scaled)], dim=1).contiguous().to(device)
+    return _TABLES[key]
+
+
+def rotary_freqs(dims: int, head: int, masked: bool, device) -> torch.Tensor:
+    """rotary.compute_f (model.py:191-196) with x=None, float32 like the reference."""
+    key = ("rot", dims, head, masked, str(device))
+    if key not in _TABLES:
+        hd = dims // head
+        if not masked:
+            scale = torch.pow(8000.0 / 200.0, torch.linspace(0, 1, hd // 2, dtype=torch.float32)) * 200.0
+            scale = scale / 1000  # essentials.gammatone
+            f = 200 * scale / 1000
+        else:
+            f = torch.arange(0, hd, 2, dtype=torch.float32) / hd * torch.log(torch.tensor(THETA))
+        _TABLES[key] = f.contiguous().to(device)
+    return _TABLES[key]
+
+
+# ------------------------------------------------------------------------------- norms
+
+
+class AbbyNormal(nn.Module):
+    """essentials.AbbyNormal (essentials.py:140-191)."""
+
+    def __init__(self, dims, size: int = 5, alpha: float = 1e-4, beta: float = 0.75, k: float = 1.0,
+                 threshold: float = 0.8):
+        super().__init__()
+        self.size, self.alpha, self.beta, self.k, self.tx = size, alpha, beta, k, threshold
+        self.mode_router = nn.Sequential(nn.Linear(dims, dims), nn.SiLU(), nn.Linear(dims, 3))
+
+    def run(self, x, noise: NoiseCtx, site: str, sid_base: int, L: int, H: int = 1):
+        return ops.abby_normal(self, x, L, H, sid_base, noise.key(site), True)
+
+
+class LayerNorm(nn.Module):
+    """essentials.LayerNorm (essentials.py:102-113): layer_norm over channels."""
+
+    def __init__(self, dims, eps=1e-5):
+        super().__init__()
+        self.dims, self.eps = dims, eps
+        self.gamma = nn.Parameter(torch.ones(dims))
+        self.beta = nn.Parameter(torch.zeros(dims))
+
+
+def get_norm(n_type: str, dims: int):
+    if n_type != "AbbyNormal":
+        raise NotImplementedError(f"n_type {n_type!r}: only the reachable 'AbbyNormal' path is built "
+                                  "(SURVEY.md §2 #10)")
+    return AbbyNormal(dims, size=5, alpha=1e-4, beta=0.75, k=1.0, threshold=0.8)
+
+
+def get_activation(act: str) -> nn.Module:
+    if act != "gelu":
+        raise NotImplementedError(f"act {act!r}: only 'gelu' (the configured activation) is built")
+    return nn.GELU()
+
+
+# ------------------------------------------------------------------------------- encoder
+
+
+class ConvLite(nn.Module):
+    def __init__(self, dims, kernel_size=15):
+        super().__init__()
+        self.point1 = nn.Conv1d(dims, dims * 2, kernel_size=1)
+        self.glu = nn.GLU(dim=1)
+        self.depth = nn.Conv1d(dims, dims, kernel_size=kernel_size, padding=(kernel_size - 1) // 2, groups=dims)
+        self.bn = nn.BatchNorm1d(dims)
+        self.swish = nn.SiLU()
+        self.point2 = nn.Conv1d(dims, dims, kernel_size=1)
+        self.dropout = nn.Dropout(0.1)
+
+    def run(self, x, noise: NoiseCtx, site: str, sid_base: int):
+        """model.py:109-118 on channels-last (B, T, D)."""
+        D = x.shape[-1]
+        res = x
+        y = ops.linear(x, self.point1.weight.view(2 * D, D), self.point1.bias)
+        y = ops.glu(y)
+        y = ops.DWConv.apply(y, self.depth.weight, self.depth.bias)
+        if self.training:
+            stats = []
+            y = ops.BatchNormPS.apply(y, self.bn.weight, self.bn.bias, self.bn.eps, stats)
+            self._update_running(stats[0], y.shape[1])
+        else:
+            y = ops.batch_norm_eval(y, self.bn.weight, self.bn.bias, self.bn.running_mean, self.bn.running_var,
+                                    self.bn.eps)
+        y = ops.act(y, "silu")
+        y = ops.linear(y, self.point2.weight.view(D, D), self.point2.bias)
+        if self.training:
+            y = ops.Dropout.apply(y, sid_base, noise.key(site + ".cl"), 0.1)
+        return ops.add(res, y)
+
+    @torch.no_grad()
+    def _update_running(self, stats, T):
+        # batch-1 semantics: one update per clip would be applied by the reference; here the mean of
+        # the per-clip statistics is applied once per stream group (running stats do not affect the
+        # train-mode output).
+        mean, rstd = stats
+        var = (1.0 / (rstd * rstd) - self.bn.eps) * (T / max(T - 1, 1))
+        m = self.bn.momentum
+        self.bn.running_mean.mul_(1 - m).add_(mean.mean(0), alpha=m)
+        self.bn.running_var.mul_(1 - m).add_(var.mean(0), alpha=m)
+        self.bn.num_batches_tracked += 1
+
+
+class AudioEncoder(nn.Module):
+    """model.py:120-169 (norm=False, enc=False)."""
+
+    def __init__(self, mels, dims, head, layer, act, n_type, norm=False, enc=False):
+        super().__init__()
+        if norm or enc:
+            raise NotImplementedError("AudioEncoder(norm/enc=True) is not reachable from Model")
+        self.norm = nn.Identity()
+        self.local_norm = nn.Identity()
+        act_fn = get_activation(act)
+        self.conv1 = nn.Sequential(nn.Conv1d(mels, dims, kernel_size=3, stride=1, padding=1), self.norm)
+        self.conv2 = nn.Sequential(nn.Conv1d(1, dims, kernel_size=3, stride=1, padding=1), self.local_norm)
+        self.EncoderLayer = nn.Identity()
+        self.encoder = nn.ModuleList()
+        for _ in range(layer):
+            self.encoder.append(nn.Sequential(
+                act_fn, weight_norm(nn.Conv1d(dims, dims, kernel_size=3, padding=1)),
+                LayerNorm(dims),
+                ConvLite(dims, kernel_size=15),
+                act_fn,
+                nn.Conv1d(dims, dims, kernel_size=3, stride=1, padding=1, groups=dims), act_fn, nn.Dropout(0.1)))
+
+    def stem(self, x):
+        """(B, C, T) -> (B, T, D): Conv1d(mels, D, 3) for C > 1, Conv1d(1, D, 3) otherwise (model.py:150-155)."""
+        if x.dim() == 2:
+            x = x.unsqueeze(0)
+        B, C, T = x.shape
+        if C > 1:
+            xt = x.transpose(1, 2).contiguous()
+            return ops.Conv3.apply(xt, self.conv1[0].weight, self.conv1[0].bias)
+        return ops.Stem1.apply(x.reshape(B, T), self.conv2[0].weight, self.conv2[0].bias)
+
+    def layers(self, x, noise: NoiseCtx, sid_base: int):
+        for l, layer in enumerate(self.encoder):
+            x = ops.act(x, "gelu")
+            x = ops.Conv3.apply(x, layer[1].weight, layer[1].bias)
+            x = ops.layer_norm(x, layer[2].gamma, layer[2].beta, layer[2].eps)
+            x = layer[3].run(x, noise, f"enc.L{l}", sid_base)
+            x = ops.act(x, "gelu")
+            x = ops.DWConv.apply(x, layer[5].weight, layer[5].bias)
+            x = ops.act(x, "gelu")
+            if self.training:
+                x = ops.Dropout.apply(x, sid_base, noise.key(f"enc.L{l}.dr"), 0.1)
+        return ops.add_rows(x, sinusoids(x.shape[1], x.shape[2], x.device))
+
+    def encode(self, streams, noise: NoiseCtx, B: int):
+        """streams: list of 3 (B, C, T) tensors (a, b, c).  Returns 3 (B, T, D) encodings; streams
+        of equal length share one batched pass (sample ids stay s*B + b)."""
+        stems = [self.stem(s) for s in streams]
+        out = [None] * len(stems)
+        i = 0
+        while i < len(stems):
+            j = i + 1
+            while j < len(stems) and stems[j].shape[1] == stems[i].shape[1]:
+                j += 1
+            x = stems[i] if j == i + 1 else torch.cat(stems[i:j], 0)
+            y = self.layers(x, noise, i * B)
+            for s in range(i, j):
+                out[s] = y[(s - i) * B:(s - i + 1) * B]
+            i = j
+        return out
+
+
+# ------------------------------------------------------------------------------- attention
+
+
+class rotary(nn.Module):  # noqa: N801  (reference class name, model.py:171)
+    def __init__(self, dims, head):
+        super().__init__()
+        self.head_dim = dims // head
+        self.head = head
+        self.dims = dims
+        self.lin = nn.Linear(dims, self.head_dim // 2, bias=True)  # constructed, unused (model.py:178)
+
+
+class attention(nn.Module):  # noqa: N801
+    """model.py:234-317 (live path: pt=None, pitch_bias=None, modal=False)."""
+
+    def __init__(self, dims, head, layer, n_type=None, modal=False):
+        super().__init__()
+        self.layer = layer
+        self.head = head
+        self.scale = (dims // head) ** -0.25
+        self.modal = modal
+        self.q = nn.Sequential(get_norm(n_type, dims), nn.Linear(dims, dims), nn.Identity())
+        self.kv = nn.Sequential(get_norm(n_type, dims), nn.Linear(dims, dims * 2), nn.Identity())
+        self.c = nn.Sequential(get_norm(n_type, dims), nn.Linear(dims, dims), nn.Identity())
+        self.out = nn.Sequential(nn.Identity(), nn.Linear(dims, dims))
+        self.conv = nn.Identity()
+        self.ln = get_norm(n_type, dims // head)
+        self.rot = rotary(dims, head)
+
+    def project_kv(self, src, noise, site, sid_base, masked):
+        """k, v of `src` (model.py:261, 304, 306-307 k-side): AbbyNormal -> Linear(D, 2D) split
+        '(kv h d)' -> k: scale + rotary(|src|) + per-head AbbyNormal."""
+        B, L, D = src.shape
+        H, hd = self.head, D // self.head
+        kvn = self.kv[0].run(src, noise, site + ".kv", sid_base, L)
+        W, b = self.kv[1].weight, self.kv[1].bias
+        k = ops.linear(kvn, W[:D], b[:D])
+        v = ops.linear(kvn, W[D:], b[D:])
+        k = ops.rotary(k, src, rotary_freqs(D, H, masked, src.device), hd, self.scale)
+        k = self.ln.run(k.view(B, L, H, hd), noise, site + ".kh", sid_base, L, H)
+        return k, v.view(B, L, H, hd)
+
+    def project_q(self, x, noise, site, sid_base, masked):
+        B, L, D = x.shape
+        H, hd = self.head, D // self.head
+        qn = self.q[0].run(x, noise, site + ".q", sid_base, L)
+        q = ops.linear(qn, self.q[1].weight, self.q[1].bias)
+        q = ops.rotary(q, x, rotary_freqs(D, H, masked, x.device), hd, self.scale)
+        return self.ln.run(q.view(B, L, H, hd), noise, site + ".qh", sid_base, L, H)
+
+    def run(self, x, kv, noise, site, sid_base, masked):
+        """x: attention input (B, Lq, D); kv: None (self attention on x) or (k, v) of the cross
+        source.  Returns the out-projected (B, Lq, D)."""
+        B, L, D = x.shape
+        if kv is None:
+            kv = self.project_kv(x, noise, site, sid_base, masked)
+        q = self.project_q(x, noise, site, sid_base, masked)
+        o = ops.attention(q, kv[0], kv[1], masked)
+        return ops.linear(o.view(B, L, D), self.out[1].weight, self.out[1].bias)
+
+
+# ------------------------------------------------------------------------------- MSheath
+
+
+class AdaptiveSpan(nn.Module):
+    """essentials.AdaptiveSpan (essentials.py:1219-1280): constructed by MSheath but never called;
+    kept for parameter-name compatibility (span_scale)."""
+
+    def __init__(self, dims, head, max_dist, sharpen=True, temp_scale=0.01):
+        super().__init__()
+        self.dims, self.head, self.max_dist = dims, head, max_dist
+        self.sharpen, self.temp_scale = sharpen, temp_scale
+        self.span_scale = nn.Parameter(torch.tensor(1.0))
+
+
+class v_gate(nn.Module):  # noqa: N801  (model.py:336-358)
+    def __init__(self, dims, mem=64, thresh=0.5):
+        super().__init__()
+        self.mkey = nn.Parameter(torch.randn(mem, dims))
+        self.mval = nn.Parameter(torch.randn(mem, 1))
+        self.mlp = nn.Sequential(nn.Linear(dims, dims // 2), nn.SiLU(), nn.Linear(dims // 2, 1))
+        self.tx = nn.Parameter(torch.tensor(thresh, dtype=torch.float32), requires_grad=False)
+        self.concat = nn.Linear(2, 1)
+
+
+class MPNet(nn.Module):
+    def __init__(self, dims, jump=2):
+        super().__init__()
+        self.net = nn.Sequential(nn.Linear(dims, 128), nn.SiLU(), nn.Linear(128, jump + 1))
+
+
+class MSheath(nn.Module):
+    """model.py:387-507."""
+
+    def __init__(self, dims, head, layer, mini_hc=False, rate=2):
+        super().__init__()
+        if mini_hc:
+            raise NotImplementedError("MSheath(mini_hc=True) is not reachable from residual")
+        self.layer = layer
+        self.dims = dims
+        self.l_jump = True
+        self.jstat = {0: 0, 1: 0, 2: 0}
+        self.shared_head = AdaptiveSpan(dims, head, max_dist=1)
+        self.mem_w = nn.Parameter(torch.zeros(1, 1, dims), requires_grad=True)
+        self.mem_gate = nn.Sequential(nn.Linear(dims, 1), nn.Sigmoid())
+        self.jump_s = nn.Parameter(torch.tensor([0.1, 0.05, 0.01]), requires_grad=True)
+        self.layers = nn.ModuleList()
+        for i in range(layer):
+            self.layers.append(nn.ModuleDict({
+                "ln": nn.LayerNorm(dims),
+                "gate": nn.Sequential(nn.Linear(dims, 1), nn.Sigmoid()),
+                "v_gate": v_gate(dims, mem=64, thresh=0.3),
+                "adapter": nn.Linear(dims, dims) if i % 2 == 0 else None,
+                "ranvier": None,
+            }))
+        self.pnet = MPNet(dims, jump=2)
+        self.mlp_gate = nn.Sequential(nn.Linear(dims, 1), nn.Sigmoid())
+        self.mlp = nn.Sequential(nn.Linear(dims, dims * 4), nn.SiLU(), nn.Linear(dims * 4, dims))
+        self.mlp_ln = nn.LayerNorm(dims)
+
+    def run(self, x, noise: NoiseCtx, site: str, sid_base: int):
+        """Batched MSheath.forward with batch-1 semantics per sample: every sample follows its own
+        layer/jump trajectory, evaluated as masked compute on device (no host syncs)."""
+        B, L, D = x.shape
+        dev = x.device
+        orig = x
+        mem_w = self.mem_w.reshape(1, D).expand(B, D)
+        pooled = ops.seg_mean(x)
+        h = ops.linear(pooled, self.pnet.net[0].weight, self.pnet.net[0].bias, act="silu")
+        policy = torch.softmax(ops.small_linear(h, self.pnet.net[2].weight, self.pnet.net[2].bias), dim=-1)
+        gpol = ops.policy_noise(B, self.layer, sid_base, noise.key(site), dev)
+        next_i = torch.zeros(B, device=dev)
+        for i in range(self.layer):
+            lay = self.layers[i]
+            active = (next_i == i).to(torch.float32)
+            ion = ops.v_gate(lay["v_gate"], x)  # (B, L)
+            px = ops.layer_norm(x, lay["ln"].weight, lay["ln"].bias, lay["ln"].eps)
+            out = ops.linear(px, lay["adapter"].weight, lay["adapter"].bias) if lay["adapter"] is not None else px
+            g_val = ops.small_linear(px, lay["gate"][0].weight, lay["gate"][0].bias, act="sigmoid")  # (B, L, 1)
+            x_new = ops.axpy_row(x, (g_val.reshape(B, L) * ion).contiguous(), out)
+            mem = ops.seg_mean(x_new)
+            mem_v = ops.small_linear(mem, self.mem_gate[0].weight, self.mem_gate[0].bias, act="sigmoid")  # (B, 1)
+            mem_w_new = mem_v * mem_w + (1 - mem_v) * mem
+            potential = ion.mean(dim=1)
+            if i < self.layer - 1:
+                ys = torch.softmax(policy + gpol[:, i], dim=-1)
+                a_g = ys.argmax(dim=-1)
+                hard = torch.zeros_like(ys).scatter_(-1, a_g.unsqueeze(-1), 1.0) - ys.detach() + ys
+                jg_g = hard.gather(-1, a_g.unsqueeze(-1)).squeeze(-1)
+                low = potential < 0.1
+                action = torch.where(low, torch.ones_like(a_g), a_g)
+                jump_g = torch.where(low, torch.ones_like(jg_g), jg_g)
+            else:
+                action = torch.zeros(B, dtype=torch.long, device=dev)
+                jump_g = torch.ones(B, device=dev)
+            jumped = action > 0
+            jw = self.jump_s[(action - 1).clamp(0, 2)]
+            alpha = torch.where(jumped, torch.ones_like(jump_g), jump_g)
+            beta = torch.where(jumped, jw * jump_g, torch.zeros_like(jump_g))
+            gam = torch.where(jumped, (1 - jw) * jump_g, torch.zeros_like(jump_g)).unsqueeze(-1) * mem_w_new
+            x = ops.JumpSelect.apply(x_new, orig, x, active, alpha, beta, gam)
+            mem_w = torch.where(active.bool().unsqueeze(-1), mem_w_new, mem_w)
+            step = torch.where(jumped, torch.clamp(i + action + 1, max=self.layer), torch.full_like(action, i + 1))
+            next_i = torch.where(active.bool(), step.to(torch.float32), next_i)
+        gate = ops.small_linear(x, self.mlp_gate[0].weight, self.mlp_gate[0].bias, act="sigmoid")
+        hh = ops.layer_norm(x, self.mlp_ln.weight, self.mlp_ln.bias, self.mlp_ln.eps)
+        hh = ops.linear(hh, self.mlp[0].weight, self.mlp[0].bias, act="silu")
+        hh = ops.linear(hh, self.mlp[2].weight, self.mlp[2].bias)
+        return ops.axpy_row(x, gate.reshape(B, L).contiguous(), hh)
+
+
+# ------------------------------------------------------------------------------- blocks
+
+
+class tgate(nn.Module):  # noqa: N801  (model.py:525-535)
+    def __init__(self, dims, num_types=2):
+        super().__init__()
+        self.ga = nn.ModuleList([nn.Sequential(nn.Linear(dims, dims), nn.Sigmoid()) for _ in range(num_types)])
+        self.cs = nn.Sequential(nn.Linear(dims, num_types), nn.Softmax(dim=-1))
+
+
+class router(nn.Module):  # noqa: N801  (model.py:537-557)
+    """Parameters kept for state_dict compatibility.  router(x, x, x) = sum_k w_k x with
+    sum_k w_k = 1, i.e. the identity (up to one rounding), so the HIP path applies it as identity
+    (tests/test_gpu_model.py checks it against the oracle's full evaluation)."""
+
+    def __init__(self, dims, num_types):
+        super().__init__()
+        self.num_types = num_types
+        self.top = nn.Linear(dims * num_types, num_types)
+        self.soft = nn.Sequential(nn.Linear(dims * num_types, num_types), nn.Softmax(dim=-1))
+        self.alpha = nn.Parameter(torch.ones(1), requires_grad=True)
+
+
+class residual(nn.Module):  # noqa: N801  (model.py:559-583)
+    def __init__(self, dims, head, layer, act, n_type, num_types=3):
+        super().__init__()
+        self.layer = layer - 1
+        self.ln = get_norm(n_type=n_type, dims=dims)
+        self.act_fn = get_activation(act)
+        self.attn = attention(dims, head, layer, n_type=n_type)
+        self.router = router(dims, num_types=num_types)
+        self.jump = MSheath(dims, head, layer)
+        self.mlp = nn.Sequential(self.ln, tgate(dims, num_types=num_types),
+                                 nn.Linear(dims, dims * num_types), get_activation(act),
+                                 nn.Linear(dims * num_types, dims), self.ln)
+
+    def call(self, x, noise: NoiseCtx, site: str, sid_base: int, kv=None, masked=False):
+        """residual.forward with the cross source given as precomputed (k, v) (see xa_side)."""
+        L = x.shape[1]
+        h = self.ln.run(x, noise, site + ".ln0", sid_base, L)
+        x = self.jump.run(h, noise, site + ".jump", sid_base)
+        h = self.ln.run(x, noise, site + ".ln1", sid_base, L)
+        x = ops.add(x, self.attn.run(h, None, noise, site + ".sa", sid_base, masked))
+        if kv is not None:
+            h = self.ln.run(x, noise, site + ".ln2", sid_base, L)
+            x = ops.add(x, self.attn.run(h, kv, noise, site + ".ca", sid_base, False))
+        m = self.ln.run(x, noise, site + ".mlp.ln0", sid_base, L)
+        m = ops.tgate(self.mlp[1], m)
+        m = ops.linear(m, self.mlp[2].weight, self.mlp[2].bias, act="gelu")
+        m = ops.linear(m, self.mlp[4].weight, self.mlp[4].bias)
+        m = self.ln.run(m, noise, site + ".mlp.ln1", sid_base, L)
+        return ops.add(x, m)
+
+    def xa_side(self, xa, noise: NoiseCtx, site: str, sid_base: int):
+        """The cross source of residual.forward (model.py:579-582): xa + PE -> AbbyNormal -> MSheath
+        -> attention k/v projection."""
+        S, D = xa.shape[1], xa.shape[2]
+        xa = ops.add_rows(xa, sinusoids(S, D, xa.device))
+        xa = self.ln.run(xa, noise, site + ".ln", sid_base, S)
+        xa = self.jump.run(xa, noise, site + ".jump", sid_base)
+        return self.attn.project_kv(xa, noise, site + ".ca", sid_base, False)
+
+
+def _split(t, B):
+    return [t[i * B:(i + 1) * B] for i in range(t.shape[0] // B)]
+
+
+class processor(nn.Module):  # noqa: N801  (model.py:585-629)
+    def __init__(self, tokens, mels, dims, head, layer, act, n_type, ctx=2048):
+        super().__init__()
+        self.dims = dims
+        self.ln = get_norm(n_type, dims)
+        self.token = nn.Embedding(tokens, dims)
+        self.pitch_tokens = nn.Embedding(1024, dims)
+        self.position = nn.Parameter(torch.ones(ctx, dims), requires_grad=True)
+        self.blend = nn.Parameter(torch.tensor(0.5), requires_grad=True)
+        self.block = nn.ModuleList([residual(dims, head, layer, act, n_type) for _ in range(layer)])
+
+    def forward(self, x, xa, noise: NoiseCtx, seq=False):
+        B, T = x.shape
+        xe = ops.Embedding.apply(x, self.token.weight)
+        x = ops.add_rows(xe, self.position[:T])
+        A_in = [xa["a"], xa["b"], xa["c"]]
+        nblk = len(self.block)
+        for i, blk in enumerate(self.block):
+            dead = i < nblk - 1 and torch.is_grad_enabled()
+            with torch.no_grad() if dead else contextlib.nullcontext():
+                a = blk.call(x, noise, f"b{i}.ta", 0, masked=True)
+                A = self._audio(blk, A_in, noise, f"b{i}.audio", B, "call")
+                KV = self._audio(blk, A, noise, f"b{i}.xa", B, "xa")
+                b_ = blk.call(a, noise, f"b{i}.tb", 0, kv=KV[0])
+                c_ = blk.call(b_, noise, f"b{i}.tc", 0, kv=KV[1])
+                d = blk.call(c_, noise, f"b{i}.td", 0, kv=KV[2])
+                e = ops.add(a, b_, c_)
+                kve = blk.xa_side(e, noise, f"b{i}.tg.xa", 0)
+                g = blk.call(d, noise, f"b{i}.tg", 0, kv=kve)
+        if seq:
+            out = g
+        else:
+            blend = torch.sigmoid(self.blend)
+            out = blend * d + (1 - blend) * g
+        out = self.ln.run(out.contiguous(), noise, "final.ln", 0, T)
+        return ops.linear(out, self.token.weight)
+
+    @staticmethod
+    def _audio(blk, streams, noise, site, B, kind):
+        """Run blk.call / blk.xa_side on the 3 audio streams, batching streams of equal length."""
+        out = [None, None, None]
+        i = 0
+        while i < 3:
+            j = i + 1
+            while j < 3 and streams[j].shape[1] == streams[i].shape[1]:
+                j += 1
+            x = streams[i] if j == i + 1 else torch.cat(streams[i:j], 0)
+            if kind == "call":
+                y = blk.call(x, noise, site, i * B)
+                for s, part in zip(range(i, j), _split(y, B)):
+                    out[s] = part
+            else:
+                k, v = blk.xa_side(x, noise, site, i * B)
+                for s, kk, vv in zip(range(i, j), _split(k, B), _split(v, B)):
+                    out[s] = (kk, vv)
+            i = j
+        return out
+
+
+class Model(nn.Module):
+    """model.py:631-701."""
+
+    def __init__(self, param: Dimensions):
+        super().__init__()
+        self.param = param
+        self.processor = processor(tokens=param.tokens, mels=param.mels, dims=param.dims, head=param.head,
+                                   layer=param.layer, act=param.act, n_type=param.n_type)
+        self.enc = AudioEncoder(param.mels, param.dims, param.head, param.layer, param.act, param.n_type,
+                                norm=False, enc=False)
+        self.layer = sum(1 for name, _ in self.named_modules() if name != "")
+        self.noise_seed = 0
+        self.noise_step = 0
+
+    def set_noise(self, seed: int, step: int):
+        self.noise_seed, self.noise_step = int(seed), int(step)
+
+    def forward(self, labels=None, text_ids=None, spectrogram=None, pitch=None, waveform=None, pitch_tokens=None):
+        if pitch_tokens is not None:
+            raise NotImplementedError("pitch_tokens: the reference's pitch-token branch calls an undefined "
+                                      "quantize_pitch (model.py:609); out of scope (SURVEY.md §2 #4)")
+        first = next((t for t in (pitch, spectrogram, waveform) if t is not None), None)
+        if first is None or text_ids is None:
+            raise ValueError("forward needs text_ids and at least one of pitch/spectrogram/waveform")
+
+        def aborc(a, b, c):  # essentials.py:25
+            return a if a is not None else (b if b is not None else c)
+
+        streams = [aborc(pitch, spectrogram, waveform), aborc(spectrogram, pitch, waveform),
+                   aborc(waveform, pitch, spectrogram)]
+        streams = [s.to(torch.float32).contiguous() for s in streams]
+        B = first.shape[0]
+        noise = NoiseCtx(self.noise_seed, self.noise_step, self.training)
+        if self.training:
+            self.noise_step += 1
+        enc = self.enc.encode(streams, noise, B)
+        logits = self.processor(text_ids, {"a": enc[0], "b": enc[1], "c": enc[2]}, noise, seq=False)
+        loss = None
+        if labels is not None:
+            loss = ops.CrossEntropy.apply(logits, labels)
+        return {"logits": logits, "loss": loss}

@@ -1,0 +1,764 @@
+"""Autograd functions over the HIP C-ABI.  Forward and backward of every function run asrx kernels
+(csrc/*.hip); PyTorch supplies memory, streams and the autograd tape only.
+
+All activations are contiguous float32 device tensors; "rows" means the flattened leading dims.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import torch
+
+from . import gemm as G
+from . import lib, prec
+
+_E = torch.empty
+_S = lib.stream
+_P = lib.ptr
+
+
+def _c(t):
+    return t if t.is_contiguous() else t.contiguous()
+
+
+def _rows(t):
+    return t.numel() // t.shape[-1]
+
+
+def _zeros_like(t):
+    return torch.zeros_like(t)
+
+
+ACT = G.ACT
+
+# =============================================================================== Linear (GEMM)
+
+
+class Linear(torch.autograd.Function):
+    """y = act(x W^T + b) on MFMA (nn.Linear / 1x1 Conv1d)."""
+
+    @staticmethod
+    def forward(ctx, x, W, b, act="none"):
+        x = _c(x)
+        z = _E(*x.shape[:-1], W.shape[0], device=x.device) if act != "none" else None
+        y = G.linear_fwd(x, W, b, act=act, preact=z)
+        ctx.act = act
+        ctx.has_b = b is not None
+        ctx.save_for_backward(x, W, z)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, W, z = ctx.saved_tensors
+        gy = _c(gy)
+        if ctx.act != "none":
+            gz = _E(gy.shape, device=gy.device)
+            lib.call("asrx_act_bwd", _P(gy), _P(z), _P(gz), gy.numel(), ACT[ctx.act], _S())
+        else:
+            gz = gy
+        dx = G.linear_dgrad(gz, W) if ctx.needs_input_grad[0] else None
+        dW = G.linear_wgrad(gz, x) if ctx.needs_input_grad[1] else None
+        db = colsum(gz) if ctx.has_b and ctx.needs_input_grad[2] else None
+        return dx, dW, db, None
+
+
+def linear(x, W, b=None, act="none"):
+    return Linear.apply(x, W, b, act)
+
+
+def colsum(x2):
+    d = x2.shape[-1]
+    out = torch.zeros(d, device=x2.device)
+    lib.call("asrx_colsum", _P(x2), _P(out), _rows(x2), d, _S())
+    return out
+
+
+class SmallLinear(torch.autograd.Function):
+    """y = act(x W^T + b) for <= 4 outputs (row-dot kernel); act in {none, sigmoid}."""
+
+    @staticmethod
+    def forward(ctx, x, W, b, act="none"):
+        x = _c(x)
+        N, K = W.shape
+        y = _E(*x.shape[:-1], N, device=x.device)
+        lib.call("asrx_small_linear_fwd", _P(x), _P(W), _P(b), _P(y), _rows(x), K, N, ACT[act], _S())
+        ctx.act = act
+        ctx.has_b = b is not None
+        ctx.save_for_backward(x, W, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, W, y = ctx.saved_tensors
+        gy = _c(gy)
+        N, K = W.shape
+        dx = _E(x.shape, device=x.device) if ctx.needs_input_grad[0] else None
+        dW = torch.zeros_like(W)
+        db = torch.zeros(N, device=W.device) if ctx.has_b else None
+        lib.call("asrx_small_linear_bwd", _P(gy), _P(y), _P(x), _P(W), _P(dx), _P(dW), _P(db), _rows(x), K, N,
+                 ACT[ctx.act], 0.0, _S())
+        return dx, dW, db, None
+
+
+def small_linear(x, W, b=None, act="none"):
+    return SmallLinear.apply(x, W, b, act)
+
+
+# =============================================================================== AbbyNormal
+
+
+class AbbyNormalFn(torch.autograd.Function):
+    """essentials.AbbyNormal (essentials.py:155-191): router GEMM on MFMA + fused row kernel."""
+
+    @staticmethod
+    def forward(ctx, x, W1, b1, W2, b2, L, H, sid_base, key, use_noise):
+        x = _c(x)
+        d = x.shape[-1]
+        rows = _rows(x)
+        hpre = G.linear_fwd(x, W1, b1)
+        out = _E(x.shape, device=x.device)
+        ys = _E(rows, 3, device=x.device)
+        idx = _E(rows, dtype=torch.int32, device=x.device)
+        lib.call("asrx_abby_fwd", _P(x), _P(hpre), _P(W2), _P(b2), _P(out), _P(ys), _P(idx), rows, d, L, H,
+                 sid_base, key & 0xFFFFFFFF, int(use_noise), _S())
+        ctx.save_for_backward(x, hpre, W1, W2, ys, idx)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        x, hpre, W1, W2, ys, idx = ctx.saved_tensors
+        gout = _c(gout)
+        d = x.shape[-1]
+        rows = _rows(x)
+        dx = _E(x.shape, device=x.device)
+        dh = _E(x.shape, device=x.device)
+        dW2 = torch.zeros_like(W2)
+        db2 = torch.zeros(3, device=x.device)
+        lib.call("asrx_abby_bwd", _P(gout), _P(x), _P(hpre), _P(W2), _P(ys), _P(idx), _P(dx), _P(dh), _P(dW2),
+                 _P(db2), rows, d, _S())
+        G.linear_dgrad(dh, W1, out=dx, beta=1.0)
+        dW1 = G.linear_wgrad(dh, x)
+        db1 = colsum(dh.view(-1, d))
+        return dx, dW1, db1, dW2, db2, None, None, None, None, None
+
+
+def abby_normal(mod, x, L, H, sid_base, key, use_noise=True):
+    r = mod.mode_router
+    return AbbyNormalFn.apply(x, r[0].weight, r[0].bias, r[2].weight, r[2].bias, L, H, sid_base, key, use_noise)
+
+
+# =============================================================================== LayerNorm
+
+
+class LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, eps):
+        x = _c(x)
+        d = x.shape[-1]
+        rows = _rows(x)
+        y = _E(x.shape, device=x.device)
+        mean = _E(rows, device=x.device)
+        rstd = _E(rows, device=x.device)
+        lib.call("asrx_layernorm_fwd", _P(x), _P(w), _P(b), _P(y), _P(mean), _P(rstd), rows, d, float(eps), _S())
+        ctx.save_for_backward(x, w, mean, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w, mean, rstd = ctx.saved_tensors
+        gy = _c(gy)
+        d = x.shape[-1]
+        dx = _E(x.shape, device=x.device)
+        dw = torch.zeros_like(w)
+        db = torch.zeros_like(w)
+        lib.call("asrx_layernorm_bwd", _P(gy), _P(x), _P(w), _P(mean), _P(rstd), _P(dx), _P(dw), _P(db), _rows(x),
+                 d, _S())
+        return dx, dw, db, None
+
+
+def layer_norm(x, w, b, eps=1e-5):
+    return LayerNormFn.apply(x, w, b, eps)
+
+
+# =============================================================================== attention
+
+
+def _st3(t):
+    """(B, L, H, hd) view -> int64[3] {batch, seq, head} strides."""
+    arr = (ctypes.c_int64 * 3)(t.stride(0), t.stride(1), t.stride(2))
+    return arr
+
+
+def _addr(arr):
+    return ctypes.cast(arr, ctypes.c_void_p)
+
+
+class AttentionFn(torch.autograd.Function):
+    """SDPA(q, k, v, is_causal) (model.py:307) on (B, L, H, 64) views; scale 1/sqrt(64)."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, causal):
+        B, Lq, H, hd = q.shape
+        Lk = k.shape[1]
+        o = _E(B, Lq, H, hd, device=q.device)
+        lse = _E(B, H, Lq, device=q.device)
+        sq, sk, sv, so = _st3(q), _st3(k), _st3(v), _st3(o)
+        p = prec.get()
+        lib.call("asrx_attn_fwd", p, _P(q), _addr(sq), _P(k), _addr(sk), _P(v), _addr(sv), _P(o), _addr(so),
+                 _P(lse), B, H, Lq, Lk, hd, int(causal), 1.0 / math.sqrt(hd), _S())
+        ctx.causal = causal
+        ctx.prec = p
+        ctx.save_for_backward(q, k, v, o, lse)
+        return o
+
+    @staticmethod
+    def backward(ctx, go):
+        q, k, v, o, lse = ctx.saved_tensors
+        go = _c(go)
+        B, Lq, H, hd = q.shape
+        Lk = k.shape[1]
+        dq = _E(q.shape, device=q.device)
+        dk = _E(k.shape, device=q.device)
+        dv = _E(v.shape, device=q.device)
+        delta = _E(B, H, Lq, device=q.device)
+        arrs = [_st3(t) for t in (q, k, v, o, go, dq, dk, dv)]
+        lib.call("asrx_attn_bwd", ctx.prec, _P(q), _addr(arrs[0]), _P(k), _addr(arrs[1]), _P(v), _addr(arrs[2]),
+                 _P(o), _addr(arrs[3]), _P(go), _addr(arrs[4]), _P(lse), _P(delta), _P(dq), _addr(arrs[5]), _P(dk),
+                 _addr(arrs[6]), _P(dv), _addr(arrs[7]), B, H, Lq, Lk, hd, int(ctx.causal), 1.0 / math.sqrt(hd),
+                 _S())
+        return dq, dk, dv, None
+
+
+def attention(q, k, v, causal):
+    return AttentionFn.apply(q, k, v, causal)
+
+
+# =============================================================================== rotary
+
+
+class RotaryFn(torch.autograd.Function):
+    """rotary.forward (model.py:198-214) fused with the hd^-0.25 scale: x, src (B, L, D)."""
+
+    @staticmethod
+    def forward(ctx, x, src, freqs, hd, scale):
+        x = _c(x)
+        src = _c(src)
+        B, L, D = x.shape
+        m = _E(B * L, device=x.device)
+        lib.call("asrx_rownorm", _P(src), _P(m), B * L, D, _S())
+        y = _E(x.shape, device=x.device)
+        lib.call("asrx_rotary_fwd", _P(x), _P(m), _P(freqs), _P(y), B * L, L, D, hd, float(scale), _S())
+        ctx.hd, ctx.scale = hd, scale
+        ctx.save_for_backward(x, src, m, freqs)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, src, m, freqs = ctx.saved_tensors
+        gy = _c(gy)
+        B, L, D = x.shape
+        dx = _E(x.shape, device=x.device)
+        dm = torch.zeros(B * L, device=x.device)
+        lib.call("asrx_rotary_bwd", _P(gy), _P(x), _P(m), _P(freqs), _P(dx), _P(dm), B * L, L, D, ctx.hd,
+                 float(ctx.scale), _S())
+        dsrc = torch.zeros_like(src)
+        lib.call("asrx_rownorm_bwd", _P(dm), _P(src), _P(m), _P(dsrc), B * L, D, _S())
+        return dx, dsrc, None, None, None
+
+
+def rotary(x, src, freqs, hd, scale):
+    return RotaryFn.apply(x, src, freqs, hd, scale)
+
+
+# =============================================================================== v_gate
+
+
+class VGateFn(torch.autograd.Function):
+    """v_gate.forward (model.py:346-351) -> ion (rows,) with the STE backward."""
+
+    @staticmethod
+    def forward(ctx, x, mkeyn, mval, W1, b1, W2, b2, cw, cb, tx):
+        x = _c(x)
+        D = x.shape[-1]
+        rows = _rows(x)
+        M = mkeyn.shape[0]
+        Dh = W1.shape[0]
+        nx = _E(rows, device=x.device)
+        lib.call("asrx_rownorm", _P(x), _P(nx), rows, D, _S())
+        S = G.linear_fwd(x, mkeyn)
+        h = G.linear_fwd(x, W1, b1)
+        ion = _E(rows, device=x.device)
+        xval = _E(rows, device=x.device)
+        kv = _E(rows, device=x.device)
+        m2 = _E(rows, device=x.device)
+        c = 1.0 / math.sqrt(D)
+        lib.call("asrx_vgate_fwd", _P(S), _P(nx), _P(mval), _P(h), _P(W2), _P(b2), _P(cw), _P(cb), _P(tx), _P(ion),
+                 _P(xval), _P(kv), _P(m2), rows, M, Dh, c, _S())
+        ctx.save_for_backward(x, mkeyn, mval, W1, W2, cw, nx, S, h, kv, m2)
+        return ion.view(*x.shape[:-1])
+
+    @staticmethod
+    def backward(ctx, gion):
+        x, mkeyn, mval, W1, W2, cw, nx, S, h, kv, m2 = ctx.saved_tensors
+        gion = _c(gion)
+        D = x.shape[-1]
+        rows = _rows(x)
+        M = mkeyn.shape[0]
+        Dh = W1.shape[0]
+        dS = _E(rows, M, device=x.device)
+        dnx = _E(rows, device=x.device)
+        dh = _E(rows, Dh, device=x.device)
+        dmval = torch.zeros(M, device=x.device)
+        dW2 = torch.zeros_like(W2)
+        db2 = torch.zeros(1, device=x.device)
+        dcw = torch.zeros(2, device=x.device)
+        dcb = torch.zeros(1, device=x.device)
+        lib.call("asrx_vgate_bwd", _P(gion), _P(S), _P(nx), _P(mval), _P(h), _P(W2), _P(cw), _P(kv), _P(m2), _P(dS),
+                 _P(dnx), _P(dh), _P(dmval), _P(dW2), _P(db2), _P(dcw), _P(dcb), rows, M, Dh, 1.0 / math.sqrt(D),
+                 _S())
+        x2 = x.view(rows, D)
+        dx = G.linear_dgrad(dS, mkeyn)
+        G.linear_dgrad(dh, W1, out=dx, beta=1.0)
+        lib.call("asrx_rownorm_bwd", _P(dnx), _P(x2), _P(nx), _P(dx), rows, D, _S())
+        dmkeyn = G.linear_wgrad(dS, x2)
+        dW1 = G.linear_wgrad(dh, x2)
+        db1 = colsum(dh)
+        return (dx.view(x.shape), dmkeyn, dmval.view(M, 1), dW1, db1, dW2.view(1, Dh), db2, dcw.view(1, 2), dcb,
+                None)
+
+
+def v_gate(mod, x):
+    mkeyn = torch.nn.functional.normalize(mod.mkey, p=2, dim=-1)  # parameter-sized (64 x D)
+    return VGateFn.apply(x, mkeyn, mod.mval, mod.mlp[0].weight, mod.mlp[0].bias, mod.mlp[2].weight,
+                         mod.mlp[2].bias, mod.concat.weight, mod.concat.bias, mod.tx)
+
+
+# =============================================================================== tgate
+
+
+class TGateFn(torch.autograd.Function):
+    """tgate (model.py:532-535): one N=3D GEMM with sigmoid epilogue + softmax-weighted combine."""
+
+    @staticmethod
+    def forward(ctx, x, Wcat, bcat, Wcs, bcs):
+        x = _c(x)
+        D = x.shape[-1]
+        rows = _rows(x)
+        Gs = G.linear_fwd(x, Wcat, bcat, act="sigmoid")
+        c = _E(rows, 3, device=x.device)
+        lib.call("asrx_small_linear_fwd", _P(x), _P(Wcs), _P(bcs), _P(c), rows, D, 3, 0, _S())
+        out = _E(x.shape, device=x.device)
+        lib.call("asrx_tgate_fwd", _P(Gs), _P(c), _P(out), rows, D, _S())
+        ctx.save_for_backward(x, Wcat, Wcs, Gs, c)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        x, Wcat, Wcs, Gs, c = ctx.saved_tensors
+        gout = _c(gout)
+        D = x.shape[-1]
+        rows = _rows(x)
+        dGz = _E(rows, 3 * D, device=x.device)
+        dc = _E(rows, 3, device=x.device)
+        lib.call("asrx_tgate_bwd", _P(gout), _P(Gs), _P(c), _P(dGz), _P(dc), rows, D, _S())
+        dx = G.linear_dgrad(dGz, Wcat)
+        dWcs = torch.zeros_like(Wcs)
+        dbcs = torch.zeros(3, device=x.device)
+        lib.call("asrx_small_linear_bwd", _P(dc), None, _P(x), _P(Wcs), _P(dx), _P(dWcs), _P(dbcs), rows, D, 3, 0,
+                 1.0, _S())
+        dWcat = G.linear_wgrad(dGz, x)
+        dbcat = colsum(dGz)
+        return dx.view(x.shape), dWcat, dbcat, dWcs, dbcs
+
+
+def tgate(mod, x):
+    Wcat = torch.cat([g[0].weight for g in mod.ga], 0)
+    bcat = torch.cat([g[0].bias for g in mod.ga], 0)
+    return TGateFn.apply(x, Wcat, bcat, mod.cs[0].weight, mod.cs[0].bias)
+
+
+# =============================================================================== elementwise
+
+
+class AxpyRow(torch.autograd.Function):
+    """out = x + s[row] * y"""
+
+    @staticmethod
+    def forward(ctx, x, s, y):
+        x, s, y = _c(x), _c(s), _c(y)
+        d = x.shape[-1]
+        out = _E(x.shape, device=x.device)
+        lib.call("asrx_axpy_row", _P(x), _P(s), _P(y), _P(out), _rows(x), d, _S())
+        ctx.save_for_backward(s, y)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        s, y = ctx.saved_tensors
+        g = _c(g)
+        d = y.shape[-1]
+        dy = _E(y.shape, device=y.device)
+        ds = _E(s.shape, device=y.device)
+        lib.call("asrx_axpy_row_bwd", _P(g), _P(s), _P(y), _P(dy), _P(ds), _rows(y), d, _S())
+        return g, ds, dy
+
+
+def axpy_row(x, s, y):
+    return AxpyRow.apply(x, s, y)
+
+
+class JumpSelect(torch.autograd.Function):
+    """Per-sample masked MSheath step (model.py:489-501): act ? alpha*xn + beta*orig + gam : xold."""
+
+    @staticmethod
+    def forward(ctx, xn, orig, xold, act, alpha, beta, gam):
+        xn, orig, xold = _c(xn), _c(orig), _c(xold)
+        act, alpha, beta, gam = _c(act), _c(alpha), _c(beta), _c(gam)
+        B, L, d = xn.shape
+        out = _E(xn.shape, device=xn.device)
+        lib.call("asrx_jump_select", _P(xn), _P(orig), _P(xold), _P(act), _P(alpha), _P(beta), _P(gam), _P(out), B,
+                 L, d, _S())
+        ctx.save_for_backward(xn, orig, act, alpha, beta)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        xn, orig, act, alpha, beta = ctx.saved_tensors
+        g = _c(g)
+        B, L, d = xn.shape
+        dxn, dorig, dxold = _E(xn.shape, device=g.device), _E(xn.shape, device=g.device), _E(xn.shape, device=g.device)
+        dalpha = torch.zeros(B, device=g.device)
+        dbeta = torch.zeros(B, device=g.device)
+        dgam = _E(B, d, device=g.device)
+        lib.call("asrx_jump_select_bwd", _P(g), _P(xn), _P(orig), _P(act), _P(alpha), _P(beta), _P(dxn), _P(dorig),
+                 _P(dxold), _P(dalpha), _P(dbeta), _P(dgam), B, L, d, _S())
+        return dxn, dorig, dxold, None, dalpha, dbeta, dgam
+
+
+class SegMean(torch.autograd.Function):
+    """x.mean(dim=1) for (B, L, d) -> (B, d)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        x = _c(x)
+        B, L, d = x.shape
+        out = _E(B, d, device=x.device)
+        lib.call("asrx_seg_colsum", _P(x), _P(out), B, L, d, 1.0 / L, 0, _S())
+        ctx.shape = x.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        B, L, d = ctx.shape
+        u = _c(g) * (1.0 / L)
+        dx = _E(B, L, d, device=g.device)
+        lib.call("asrx_add_rows", None, None, _P(u), _P(dx), B, L, d, _S())
+        return dx
+
+
+def seg_mean(x):
+    return SegMean.apply(x)
+
+
+class AddRows(torch.autograd.Function):
+    """out[b, l] = x[b, l] + t[l]  (t: PE table or the learned position rows)."""
+
+    @staticmethod
+    def forward(ctx, x, t):
+        x, t = _c(x), _c(t)
+        B, L, d = x.shape
+        out = _E(x.shape, device=x.device)
+        lib.call("asrx_add_rows", _P(x), _P(t), None, _P(out), B, L, d, _S())
+        ctx.tshape = t.shape
+        ctx.t_grad = t.requires_grad
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        g = _c(g)
+        dt = None
+        if ctx.needs_input_grad[1]:
+            B = g.shape[0]
+            dt = colsum(g.view(B, -1)).view(ctx.tshape)
+        return g, dt
+
+
+def add_rows(x, t):
+    return AddRows.apply(x, t)
+
+
+class LinComb(torch.autograd.Function):
+    """out = a*x + b*y (+ c*z) with python-float coefficients."""
+
+    @staticmethod
+    def forward(ctx, x, y, z, a, b, c):
+        x, y = _c(x), _c(y)
+        z = _c(z) if z is not None else None
+        out = _E(x.shape, device=x.device)
+        lib.call("asrx_lincomb", _P(x), _P(y), _P(z), float(a), float(b), float(c), _P(out), x.numel(), _S())
+        ctx.coef = (a, b, c)
+        ctx.has_z = z is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b, c = ctx.coef
+        g = _c(g)
+
+        def sc(k):
+            if k == 1.0:
+                return g
+            out = _E(g.shape, device=g.device)
+            lib.call("asrx_lincomb", _P(g), None, None, float(k), 0.0, 0.0, _P(out), g.numel(), _S())
+            return out
+
+        return sc(a), sc(b), (sc(c) if ctx.has_z else None), None, None, None
+
+
+def add(x, y, z=None):
+    return LinComb.apply(x, y, z, 1.0, 1.0, 1.0)
+
+
+class Act(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, act):
+        x = _c(x)
+        y = _E(x.shape, device=x.device)
+        lib.call("asrx_act_fwd", _P(x), _P(y), x.numel(), ACT[act], _S())
+        ctx.act = act
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        g = _c(g)
+        dx = _E(x.shape, device=x.device)
+        lib.call("asrx_act_bwd", _P(g), _P(x), _P(dx), x.numel(), ACT[ctx.act], _S())
+        return dx, None
+
+
+def act(x, name):
+    return Act.apply(x, name)
+
+
+class GLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = _c(x)
+        C = x.shape[-1] // 2
+        y = _E(*x.shape[:-1], C, device=x.device)
+        lib.call("asrx_glu_fwd", _P(x), _P(y), _rows(x), C, _S())
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        dx = _E(x.shape, device=x.device)
+        lib.call("asrx_glu_bwd", _P(_c(g)), _P(x), _P(dx), _rows(x), x.shape[-1] // 2, _S())
+        return dx
+
+
+def glu(x):
+    return GLU.apply(x)
+
+
+class Dropout(torch.autograd.Function):
+    """nn.Dropout(p) in train mode with keyed masks on channels-last (B, T, C)."""
+
+    @staticmethod
+    def forward(ctx, x, sid_base, key, p):
+        x = _c(x)
+        B, T, C = x.shape
+        y = _E(x.shape, device=x.device)
+        lib.call("asrx_dropout", _P(x), _P(y), B, T, C, sid_base, key & 0xFFFFFFFF, float(p), _S())
+        ctx.args = (sid_base, key, p)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        sid_base, key, p = ctx.args
+        g = _c(g)
+        B, T, C = g.shape
+        dx = _E(g.shape, device=g.device)
+        lib.call("asrx_dropout", _P(g), _P(dx), B, T, C, sid_base, key & 0xFFFFFFFF, float(p), _S())
+        return dx, None, None, None
+
+
+class DWConv(torch.autograd.Function):
+    """Depthwise Conv1d (groups=C, padding K//2) on channels-last (B, T, C); w (C, 1, K)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        x = _c(x)
+        B, T, C = x.shape
+        K = w.shape[-1]
+        y = _E(x.shape, device=x.device)
+        lib.call("asrx_dwconv_fwd", _P(x), _P(w), _P(b), _P(y), B, T, C, K, _S())
+        ctx.save_for_backward(x, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        g = _c(g)
+        B, T, C = x.shape
+        K = w.shape[-1]
+        dx = _E(x.shape, device=x.device)
+        dw = torch.zeros_like(w)
+        db = torch.zeros(C, device=x.device)
+        lib.call("asrx_dwconv_bwd", _P(g), _P(x), _P(w), _P(dx), _P(dw), _P(db), B, T, C, K, _S())
+        return dx, dw, db
+
+
+class BatchNormPS(torch.autograd.Function):
+    """BatchNorm1d in train mode with per-sample statistics (batch-1 semantics) on (B, T, C)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, eps, stats):
+        x = _c(x)
+        B, T, C = x.shape
+        mean = _E(B, C, device=x.device)
+        rstd = _E(B, C, device=x.device)
+        y = _E(x.shape, device=x.device)
+        lib.call("asrx_bn_fwd", _P(x), _P(w), _P(b), _P(y), _P(mean), _P(rstd), B, T, C, float(eps), 1, _S())
+        if stats is not None:
+            stats.append((mean, rstd))
+        ctx.save_for_backward(x, w, mean, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w, mean, rstd = ctx.saved_tensors
+        g = _c(g)
+        B, T, C = x.shape
+        sg = _E(B, C, device=x.device)
+        sgx = _E(B, C, device=x.device)
+        dx = _E(x.shape, device=x.device)
+        dw = torch.zeros_like(w)
+        db = torch.zeros_like(w)
+        lib.call("asrx_bn_bwd", _P(g), _P(x), _P(mean), _P(rstd), _P(w), _P(sg), _P(sgx), _P(dx), _P(dw), _P(db), B,
+                 T, C, _S())
+        return dx, dw, db, None, None
+
+
+def batch_norm_eval(x, w, b, rm, rv, eps):
+    x = _c(x)
+    B, T, C = x.shape
+    rstd = torch.rsqrt(rv + eps)
+    y = _E(x.shape, device=x.device)
+    lib.call("asrx_bn_fwd", _P(x), _P(w), _P(b), _P(y), _P(_c(rm)), _P(rstd), B, T, C, float(eps), 0, _S())
+    return y
+
+
+class Conv3(torch.autograd.Function):
+    """k3 / padding-1 Conv1d on channels-last (B, T, Cin) -> (B, T, Cout) via implicit-im2col GEMM.
+    W (Cout, Cin, 3) like nn.Conv1d."""
+
+    @staticmethod
+    def forward(ctx, x, W, b):
+        x = _c(x)
+        B, T, Ci = x.shape
+        Co = W.shape[0]
+        Wt = W.permute(0, 2, 1).reshape(Co, 3 * Ci).contiguous()
+        y = _E(B, T, Co, device=x.device)
+        G.gemm(x, Wt, y, M=B * T, N=Co, K=3 * Ci, lda=Ci, ldb=3 * Ci, ldc=Co, bias=b, conv_a=True, conv_F=T,
+               conv_C=Ci)
+        ctx.save_for_backward(x, W)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, W = ctx.saved_tensors
+        g = _c(g)
+        B, T, Ci = x.shape
+        Co = W.shape[0]
+        dx = None
+        if ctx.needs_input_grad[0]:
+            Wf = W.flip(2).permute(1, 2, 0).reshape(Ci, 3 * Co).contiguous()
+            dx = _E(x.shape, device=x.device)
+            G.gemm(g, Wf, dx, M=B * T, N=Ci, K=3 * Co, lda=Co, ldb=3 * Co, ldc=Ci, conv_a=True, conv_F=T, conv_C=Co)
+        dWt = torch.zeros(Co, 3 * Ci, device=x.device)
+        tiles = ((Co + 127) // 128) * ((3 * Ci + 127) // 128)
+        G.gemm(g, x, dWt, M=Co, N=3 * Ci, K=B * T, lda=Co, ldb=Ci, ldc=3 * Ci, a_kc=False, b_kc=False, conv_b=True,
+               conv_F=T, conv_C=Ci, beta=1.0, splitk=G._splitk_for(B * T, tiles))
+        dW = dWt.view(Co, 3, Ci).permute(0, 2, 1).contiguous()
+        db = colsum(g.view(-1, Co))
+        return dx, dW, db
+
+
+class Stem1(torch.autograd.Function):
+    """Conv1d(1, D, 3, padding=1) (model.py:133) on (B, T) single-channel streams -> (B, T, D)."""
+
+    @staticmethod
+    def forward(ctx, x, W, b):
+        x = _c(x)
+        B, T = x.shape
+        D = W.shape[0]
+        y = _E(B, T, D, device=x.device)
+        lib.call("asrx_stem1_fwd", _P(x), _P(W), _P(b), _P(y), B, T, D, _S())
+        ctx.save_for_backward(x, W)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, W = ctx.saved_tensors
+        B, T = x.shape
+        D = W.shape[0]
+        dW = torch.zeros_like(W)
+        db = torch.zeros(D, device=x.device)
+        lib.call("asrx_stem1_bwd", _P(_c(g)), _P(x), _P(dW), _P(db), B, T, D, _S())
+        return None, dW, db
+
+
+class Embedding(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, E):
+        ids = _c(ids)
+        d = E.shape[1]
+        y = _E(*ids.shape, d, device=E.device)
+        lib.call("asrx_embed_fwd", _P(ids), _P(E), _P(y), ids.numel(), d, _S())
+        ctx.save_for_backward(ids)
+        ctx.Eshape = E.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        (ids,) = ctx.saved_tensors
+        dE = torch.zeros(ctx.Eshape, device=g.device)
+        lib.call("asrx_embed_bwd", _P(ids), _P(_c(g)), _P(dE), ids.numel(), ctx.Eshape[1], _S())
+        return None, dE
+
+
+class CrossEntropy(torch.autograd.Function):
+    """F.cross_entropy(logits, labels, ignore_index=0), mean over non-ignored rows."""
+
+    @staticmethod
+    def forward(ctx, logits, labels):
+        z = _c(logits)
+        V = z.shape[-1]
+        rows = _rows(z)
+        lab = _c(labels.reshape(-1))
+        loss_r = _E(rows, device=z.device)
+        lse = _E(rows, device=z.device)
+        lib.call("asrx_ce_fwd", _P(z), _P(lab), _P(loss_r), _P(lse), rows, V, _S())
+        count = (lab != 0).sum().clamp_min(1).to(torch.float32)
+        loss = loss_r.sum() / count
+        ctx.save_for_backward(z, lab, lse, count)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        z, lab, lse, count = ctx.saved_tensors
+        scale = (g / count).reshape(1).contiguous()
+        dz = _E(z.shape, device=z.device)
+        lib.call("asrx_ce_bwd", _P(z), _P(lab), _P(lse), _P(scale), _P(dz), _rows(z), z.shape[-1], _S())
+        return dz, None
+
+
+def policy_noise(B, layers, sid_base, key, device):
+    out = _E(B, layers, 3, device=device)
+    lib.call("asrx_policy_noise", _P(out), B, layers, sid_base, key & 0xFFFFFFFF, _S())
+    return out

@@ -1,0 +1,1231 @@
+// Row-wise and elementwise kernels of the model's hot path (fp32 in HBM, one wave per row where a
+// row reduction is needed, grid-stride elementwise otherwise).  Each kernel names the reference
+// op(s) it replaces.
+#include "common.h"
+
+namespace asrx {
+
+constexpr int RW = 4;  // waves per workgroup for row kernels
+
+__device__ __forceinline__ int64_t row_begin() { return (int64_t)blockIdx.x * RW + (threadIdx.x >> 6); }
+__device__ __forceinline__ int64_t row_step() { return (int64_t)gridDim.x * RW; }
+
+static unsigned row_grid(int64_t rows, int64_t cap = 8192) {
+  int64_t g = (rows + RW - 1) / RW;
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  return (unsigned)g;
+}
+static unsigned ew_grid(int64_t n, int64_t cap = 16384) {
+  int64_t g = (n + 255) / 256;
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  return (unsigned)g;
+}
+
+// Workgroup reduction of per-wave partials `part[RW][n]` then atomicAdd into dst[n].
+__device__ __forceinline__ void flush_partials(float* part, int n, float* dst) {
+  __syncthreads();
+  for (int j = threadIdx.x; j < n; j += 64 * RW) {
+    float s = 0.f;
+    for (int w = 0; w < RW; ++w) s += part[w * n + j];
+    atomicAdd(dst + j, s);
+  }
+}
+
+// ============================================================================ LayerNorm
+// nn.LayerNorm over the last dim (MSheath layers[i].ln / mlp_ln, model.py:405, 427) and
+// essentials.LayerNorm over channels (essentials.py:110-113) on channels-last activations.
+__global__ __launch_bounds__(64 * RW) void ln_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                         const float* __restrict__ b, float* __restrict__ y,
+                                                         float* __restrict__ mean, float* __restrict__ rstd,
+                                                         int64_t rows, int d, float eps) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t r = row_begin(); r < rows; r += row_step()) {
+    const float* xr = x + r * d;
+    float s = 0.f;
+    for (int j = lane; j < d; j += 64) s += xr[j];
+    const float mu = wave_sum(s) / d;
+    float v = 0.f;
+    for (int j = lane; j < d; j += 64) {
+      const float t = xr[j] - mu;
+      v += t * t;
+    }
+    const float rs = rsqrtf(wave_sum(v) / d + eps);
+    float* yr = y + r * d;
+    for (int j = lane; j < d; j += 64) yr[j] = (xr[j] - mu) * rs * w[j] + b[j];
+    if (lane == 0) {
+      mean[r] = mu;
+      rstd[r] = rs;
+    }
+  }
+}
+
+__global__ __launch_bounds__(64 * RW) void ln_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x,
+                                                         const float* __restrict__ w, const float* __restrict__ mean,
+                                                         const float* __restrict__ rstd, float* __restrict__ dx,
+                                                         float* __restrict__ dw, float* __restrict__ db, int64_t rows,
+                                                         int d) {
+  extern __shared__ float part[];  // [RW][2*d]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float* pw = part + wid * 2 * d;
+  for (int j = lane; j < 2 * d; j += 64) pw[j] = 0.f;
+  for (int64_t r = row_begin(); r < rows; r += row_step()) {
+    const float* xr = x + r * d;
+    const float* gr = dy + r * d;
+    const float mu = mean[r], rs = rstd[r];
+    float s1 = 0.f, s2 = 0.f;
+    for (int j = lane; j < d; j += 64) {
+      const float xh = (xr[j] - mu) * rs;
+      const float g = gr[j] * w[j];
+      s1 += g;
+      s2 += g * xh;
+      pw[j] += gr[j] * xh;
+      pw[d + j] += gr[j];
+    }
+    s1 = wave_sum(s1) / d;
+    s2 = wave_sum(s2) / d;
+    float* dxr = dx + r * d;
+    for (int j = lane; j < d; j += 64) {
+      const float xh = (xr[j] - mu) * rs;
+      dxr[j] = rs * (gr[j] * w[j] - s1 - xh * s2);
+    }
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < d; j += 64 * RW) {
+    float a = 0.f, c = 0.f;
+    for (int ww = 0; ww < RW; ++ww) {
+      a += part[ww * 2 * d + j];
+      c += part[ww * 2 * d + d + j];
+    }
+    atomicAdd(dw + j, a);
+    atomicAdd(db + j, c);
+  }
+}
+
+// ============================================================================ small-N linear
+// y[r, n] = act(x[r] . W[n] + b[n]) for N <= 4 outputs: gate / mem_gate / mlp_gate Linear(D, 1)
+// (model.py:398, 406, 420), v_gate.mlp[2] Linear(D/2, 1) and concat (model.py:341, 344),
+// tgate.cs Linear(D, 3) (model.py:530), MPNet's Linear(128, 3) (model.py:381).
+template <int NS>
+__global__ __launch_bounds__(64 * RW) void small_linear_fwd_kernel(const float* __restrict__ x,
+                                                                   const float* __restrict__ W,
+                                                                   const float* __restrict__ b,
+                                                                   float* __restrict__ y, int64_t rows, int K,
+                                                                   int act) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t r = row_begin(); r < rows; r += row_step()) {
+    const float* xr = x + r * K;
+    float acc[NS];
+#pragma unroll
+    for (int n = 0; n < NS; ++n) acc[n] = 0.f;
+    for (int k = lane; k < K; k += 64) {
+      const float xv = xr[k];
+#pragma unroll
+      for (int n = 0; n < NS; ++n) acc[n] += xv * W[n * K + k];
+    }
+#pragma unroll
+    for (int n = 0; n < NS; ++n) {
+      const float v = wave_sum(acc[n]) + (b ? b[n] : 0.f);
+      if (lane == n) y[r * NS + n] = apply_act(act, v);
+    }
+  }
+}
+
+// dy is the gradient of the post-activation output; y the saved output (for sigmoid').
+template <int NS>
+__global__ __launch_bounds__(64 * RW) void small_linear_bwd_kernel(
+    const float* __restrict__ dy, const float* __restrict__ y, const float* __restrict__ x,
+    const float* __restrict__ W, float* __restrict__ dx, float* __restrict__ dW, float* __restrict__ db,
+    int64_t rows, int K, int act, float beta) {
+  extern __shared__ float part[];  // [RW][NS*K + NS]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int PN = NS * K + NS;
+  float* pw = part + wid * PN;
+  for (int j = lane; j < PN; j += 64) pw[j] = 0.f;
+  for (int64_t r = row_begin(); r < rows; r += row_step()) {
+    float dz[NS];
+#pragma unroll
+    for (int n = 0; n < NS; ++n) {
+      float g = dy[r * NS + n];
+      if (act == ACT_SIGMOID) {
+        const float s = y[r * NS + n];
+        g *= s * (1.f - s);
+      }
+      dz[n] = g;
+    }
+    const float* xr = x + r * K;
+    float* dxr = dx ? dx + r * K : nullptr;
+    for (int k = lane; k < K; k += 64) {
+      const float xv = xr[k];
+      float s = 0.f;
+#pragma unroll
+      for (int n = 0; n < NS; ++n) {
+        s += dz[n] * W[n * K + k];
+        pw[n * K + k] += dz[n] * xv;
+      }
+      if (dxr) dxr[k] = (beta != 0.f ? beta * dxr[k] : 0.f) + s;
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int n = 0; n < NS; ++n) pw[NS * K + n] += dz[n];
+    }
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < PN; j += 64 * RW) {
+    float s = 0.f;
+    for (int ww = 0; ww < RW; ++ww) s += part[ww * PN + j];
+    if (j < NS * K) atomicAdd(dW + j, s);
+    else if (db) atomicAdd(db + (j - NS * K), s);
+  }
+}
+
+// ============================================================================ row L2 norm
+// torch.norm(xa, dim=-1) of rotary (model.py:201) and F.normalize in v_gate (model.py:347).
+__global__ __launch_bounds__(64 * RW) void rownorm_kernel(const float* __restrict__ x, float* __restrict__ n,
+                                                          int64_t rows, int d) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t r = row_begin(); r < rows; r += row_step()) {
+    float s = 0.f;
+    for (int j = lane; j < d; j += 64) s += x[r * d + j] * x[r * d + j];
+    s = wave_sum(s);
+    if (lane == 0) n[r] = sqrtf(s);
+  }
+}
+
+// dx[r] += dn[r] * x[r] / n[r]
+__global__ void rownorm_bwd_kernel(const float* __restrict__ dn, const float* __restrict__ x,
+                                   const float* __restrict__ n, float* __restrict__ dx, int64_t rows, int d) {
+  const int64_t total = rows * d;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / d;
+    const float nn = n[r];
+    if (nn > 0.f) dx[i] += dn[r] * x[i] / nn;
+  }
+}
+
+// ============================================================================ rotary
+// rotary.forward (model.py:198-214) fused with the hd^-0.25 pre-scale (model.py:303-304):
+// x (B, L, H, hd) viewed as rows of D = H*hd per position; pairs (2j, 2j+1) are complex numbers
+// multiplied by polar(m[b,l], fp32(l * f[j])) and by `scale`.
+__global__ __launch_bounds__(64 * RW) void rotary_fwd_kernel(const float* __restrict__ x, const float* __restrict__ m,
+                                                             const float* __restrict__ f, float* __restrict__ y,
+                                                             int64_t BL, int64_t L, int D, int hd, float scale) {
+  const int lane = threadIdx.x & 63;
+  const int half = hd / 2;
+  for (int64_t r = row_begin(); r < BL; r += row_step()) {
+    const float l = (float)(r % L);
+    const float mm = m[r] * scale;
+    const float2* xr = reinterpret_cast<const float2*>(x + r * D);
+    float2* yr = reinterpret_cast<float2*>(y + r * D);
+    for (int p = lane; p < D / 2; p += 64) {
+      const int j = p % half;
+      const float ang = l * f[j];
+      float sn, cs;
+      sincosf(ang, &sn, &cs);
+      const float2 v = xr[p];
+      yr[p] = make_float2(mm * (v.x * cs - v.y * sn), mm * (v.x * sn + v.y * cs));
+    }
+  }
+}
+
+// dx = scale*m*R(-ang) g ; dm[r] = sum over the row of g . (R(ang) x) * scale (i.e. g . y / m)
+__global__ __launch_bounds__(64 * RW) void rotary_bwd_kernel(const float* __restrict__ g, const float* __restrict__ x,
+                                                             const float* __restrict__ m, const float* __restrict__ f,
+                                                             float* __restrict__ dx, float* __restrict__ dm,
+                                                             int64_t BL, int64_t L, int D, int hd, float scale) {
+  const int lane = threadIdx.x & 63;
+  const int half = hd / 2;
+  for (int64_t r = row_begin(); r < BL; r += row_step()) {
+    const float l = (float)(r % L);
+    const float mm = m[r] * scale;
+    const float2* xr = reinterpret_cast<const float2*>(x + r * D);
+    const float2* gr = reinterpret_cast<const float2*>(g + r * D);
+    float2* dxr = reinterpret_cast<float2*>(dx + r * D);
+    float acc = 0.f;
+    for (int p = lane; p < D / 2; p += 64) {
+      const int j = p % half;
+      const float ang = l * f[j];
+      float sn, cs;
+      sincosf(ang, &sn, &cs);
+      const float2 v = xr[p], gg = gr[p];
+      dxr[p] = make_float2(mm * (gg.x * cs + gg.y * sn), mm * (-gg.x * sn + gg.y * cs));
+      acc += gg.x * (v.x * cs - v.y * sn) + gg.y * (v.x * sn + v.y * cs);
+    }
+    acc = wave_sum(acc) * scale;
+    if (lane == 0) dm[r] += acc;
+  }
+}
+
+// ============================================================================ v_gate
+// model.py:346-351: key = softmax(normalize(x) . mkey_n^T / sqrt(D)); x_val = concat([key . mval,
+// mlp(x)]); ion = x_val > tx (STE).  S = x . mkey_n^T (rows x M) and h = mlp[0](x) pre-activation
+// (rows x D/2) come from GEMMs; nx = ||x||.
+__global__ __launch_bounds__(64 * RW) void vgate_fwd_kernel(
+    const float* __restrict__ S, const float* __restrict__ nx, const float* __restrict__ mval,
+    const float* __restrict__ h, const float* __restrict__ w2, const float* __restrict__ b2,
+    const float* __restrict__ cw, const float* __restrict__ cb, const float* __restrict__ tx,
+    float* __restrict__ ion, float* __restrict__ xval, float* __restrict__ kv_out, float* __restrict__ m2_out,
+    int64_t rows, int M, int Dh, float inv_sqrt_d) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t r = row_begin(); r < rows; r += row_step()) {
+    const float inx = 1.0f / fmaxf(nx[r], 1e-12f);
+    // softmax over M (<= 64) logits, one per lane
+    const float z = lane < M ? S[r * M + lane] * inx * inv_sqrt_d : -INFINITY;
+    const float zm = wave_max(z);
+    const float e = lane < M ? expf(z - zm) : 0.f;
+    const float se = wave_sum(e);
+    const float kv = wave_sum(lane < M ? e / se * mval[lane] : 0.f);
+    float acc = 0.f;
+    for (int j = lane; j < Dh; j += 64) acc += silu_f(h[r * Dh + j]) * w2[j];
+    const float m2 = wave_sum(acc) + b2[0];
+    const float xv = cw[0] * kv + cw[1] * m2 + cb[0];
+    if (lane == 0) {
+      xval[r] = xv;
+      ion[r] = xv > tx[0] ? 1.f : 0.f;
+      kv_out[r] = kv;
+      m2_out[r] = m2;
+    }
+  }
+}
+
+// dion: gradient of ion (= of x_val through the STE).  Writes dS (rows x M, already divided by
+// nx*sqrt(D): the gradient w.r.t. normalize(x) . mkey_n^T before the scale, i.e. dS_raw), dnx[r]
+// (gradient of ||x|| through the normalisation), dh (rows x Dh) and accumulates dmval[M],
+// dw2[Dh], db2, dcw[2], dcb.
+__global__ __launch_bounds__(64 * RW) void vgate_bwd_kernel(
+    const float* __restrict__ dion, const float* __restrict__ S, const float* __restrict__ nx,
+    const float* __restrict__ mval, const float* __restrict__ h, const float* __restrict__ w2,
+    const float* __restrict__ cw, const float* __restrict__ kvv, const float* __restrict__ m2v,
+    float* __restrict__ dS, float* __restrict__ dnx, float* __restrict__ dh, float* __restrict__ dmval,
+    float* __restrict__ dw2, float* __restrict__ db2, float* __restrict__ dcw, float* __restrict__ dcb,
+    int64_t rows, int M, int Dh, float inv_sqrt_d) {
+  extern __shared__ float part[];  // [RW][M + Dh + 4]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int PN = M + Dh + 4;
+  float* pw = part + wid * PN;
+  for (int j = lane; j < PN; j += 64) pw[j] = 0.f;
+  for (int64_t r = row_begin(); r < rows; r += row_step()) {
+    const float g = dion[r];
+    const float nxr = fmaxf(nx[r], 1e-12f);
+    const float inx = 1.0f / nxr;
+    const float z = lane < M ? S[r * M + lane] * inx * inv_sqrt_d : -INFINITY;
+    const float zm = wave_max(z);
+    const float e = lane < M ? expf(z - zm) : 0.f;
+    const float key = e / wave_sum(e);
+    const float dkv = g * cw[0];
+    const float dm2 = g * cw[1];
+    const float dkey = lane < M ? dkv * mval[lane] : 0.f;
+    const float dot = wave_sum(key * dkey);
+    const float dz = lane < M ? key * (dkey - dot) : 0.f;
+    // z = S * inx * c  ->  dS = dz * inx * c ; d(inx) = sum dz * S * c
+    if (lane < M) {
+      dS[r * M + lane] = dz * inx * inv_sqrt_d;
+      pw[lane] += dkv * key;
+    }
+    const float dinx = wave_sum(lane < M ? dz * S[r * M + lane] * inv_sqrt_d : 0.f);
+    if (lane == 0) {
+      // inx = 1/max(nx, eps): d nx = -dinx / nx^2 (zero when clamped)
+      dnx[r] = nx[r] > 1e-12f ? -dinx * inx * inx : 0.f;
+      pw[M + Dh + 0] += dm2;            // db2
+      pw[M + Dh + 1] += g * kvv[r];     // dcw0
+      pw[M + Dh + 2] += g * m2v[r];     // dcw1
+      pw[M + Dh + 3] += g;              // dcb
+    }
+    for (int j = lane; j < Dh; j += 64) {
+      const float hv = h[r * Dh + j];
+      dh[r * Dh + j] = dm2 * w2[j] * silu_grad(hv);
+      pw[M + j] += dm2 * silu_f(hv);
+    }
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < PN; j += 64 * RW) {
+    float s = 0.f;
+    for (int ww = 0; ww < RW; ++ww) s += part[ww * PN + j];
+    if (j < M) atomicAdd(dmval + j, s);
+    else if (j < M + Dh) atomicAdd(dw2 + (j - M), s);
+    else if (j == M + Dh) atomicAdd(db2, s);
+    else if (j == M + Dh + 1) atomicAdd(dcw, s);
+    else if (j == M + Dh + 2) atomicAdd(dcw + 1, s);
+    else atomicAdd(dcb, s);
+  }
+}
+
+// ============================================================================ tgate
+// model.py:532-535 (num_types=3): out[d] = sum_k G[k*D + d] * softmax(c)[k], G = sigmoid(...)
+__global__ __launch_bounds__(64 * RW) void tgate_fwd_kernel(const float* __restrict__ G, const float* __restrict__ c,
+                                                            float* __restrict__ out, int64_t rows, int D) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t r = row_begin(); r < rows; r += row_step()) {
+    const float c0 = c[r * 3], c1 = c[r * 3 + 1], c2 = c[r * 3 + 2];
+    const float cm = fmaxf(c0, fmaxf(c1, c2));
+    const float e0 = expf(c0 - cm), e1 = expf(c1 - cm), e2 = expf(c2 - cm);
+    const float inv = 1.f / (e0 + e1 + e2);
+    const float t0 = e0 * inv, t1 = e1 * inv, t2 = e2 * inv;
+    const float* gr = G + r * 3 * D;
+    for (int j = lane; j < D; j += 64) out[r * D + j] = gr[j] * t0 + gr[D + j] * t1 + gr[2 * D + j] * t2;
+  }
+}
+
+// dG = dout * t_k * G(1-G) (gradient of the pre-sigmoid GEMM output); dc = softmax backward.
+__global__ __launch_bounds__(64 * RW) void tgate_bwd_kernel(const float* __restrict__ dout, const float* __restrict__ G,
+                                                            const float* __restrict__ c, float* __restrict__ dGz,
+                                                            float* __restrict__ dc, int64_t rows, int D) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t r = row_begin(); r < rows; r += row_step()) {
+    const float c0 = c[r * 3], c1 = c[r * 3 + 1], c2 = c[r * 3 + 2];
+    const float cm = fmaxf(c0, fmaxf(c1, c2));
+    const float e0 = expf(c0 - cm), e1 = expf(c1 - cm), e2 = expf(c2 - cm);
+    const float inv = 1.f / (e0 + e1 + e2);
+    const float t0 = e0 * inv, t1 = e1 * inv, t2 = e2 * inv;
+    const float* gr = G + r * 3 * D;
+    float* dg = dGz + r * 3 * D;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+    for (int j = lane; j < D; j += 64) {
+      const float go = dout[r * D + j];
+      const float g0 = gr[j], g1 = gr[D + j], g2 = gr[2 * D + j];
+      a0 += go * g0;
+      a1 += go * g1;
+      a2 += go * g2;
+      dg[j] = go * t0 * g0 * (1.f - g0);
+      dg[D + j] = go * t1 * g1 * (1.f - g1);
+      dg[2 * D + j] = go * t2 * g2 * (1.f - g2);
+    }
+    a0 = wave_sum(a0);
+    a1 = wave_sum(a1);
+    a2 = wave_sum(a2);
+    const float dot = t0 * a0 + t1 * a1 + t2 * a2;
+    if (lane == 0) {
+      dc[r * 3] = t0 * (a0 - dot);
+      dc[r * 3 + 1] = t1 * (a1 - dot);
+      dc[r * 3 + 2] = t2 * (a2 - dot);
+    }
+  }
+}
+
+// ============================================================================ elementwise
+// out = x + s[r] * y   (MSheath layer update x + g*(out*ion) with s = g*ion, model.py:461, and the
+// final x + gate*output, model.py:505).  s may be null (s = 1).
+__global__ void axpy_row_kernel(const float* __restrict__ x, const float* __restrict__ s, const float* __restrict__ y,
+                                float* __restrict__ out, int64_t rows, int d) {
+  const int64_t total = rows * d;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const float sc = s ? s[i / d] : 1.f;
+    out[i] = x[i] + sc * y[i];
+  }
+}
+
+// ds[r] = sum_j g[r,j] * y[r,j] ;  dy = s[r] * g  (dy may alias nothing)
+__global__ __launch_bounds__(64 * RW) void axpy_row_bwd_kernel(const float* __restrict__ g, const float* __restrict__ s,
+                                                               const float* __restrict__ y, float* __restrict__ dy,
+                                                               float* __restrict__ ds, int64_t rows, int d) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t r = row_begin(); r < rows; r += row_step()) {
+    const float sc = s[r];
+    float acc = 0.f;
+    for (int j = lane; j < d; j += 64) {
+      const float gv = g[r * d + j];
+      acc += gv * y[r * d + j];
+      dy[r * d + j] = sc * gv;
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) ds[r] = acc;
+  }
+}
+
+// MSheath jump / keep step (model.py:489-501) with per-sample masking (batch-1 semantics):
+// out[b,l,:] = act[b] ? alpha[b]*xn + beta[b]*orig + gam[b,:] : xold
+__global__ void jump_select_kernel(const float* __restrict__ xn, const float* __restrict__ orig,
+                                   const float* __restrict__ xold, const float* __restrict__ act,
+                                   const float* __restrict__ alpha, const float* __restrict__ beta,
+                                   const float* __restrict__ gam, float* __restrict__ out, int64_t B, int64_t L,
+                                   int d) {
+  const int64_t total = B * L * d;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = i / (L * d);
+    const int c = (int)(i % d);
+    out[i] = act[b] != 0.f ? alpha[b] * xn[i] + beta[b] * orig[i] + gam[b * d + c] : xold[i];
+  }
+}
+
+// Backward: per-sample reductions dalpha[b] = act*sum g*xn, dbeta[b] = act*sum g*orig,
+// dgam[b,:] = act*sum_l g; elementwise dxn = act*alpha*g, dorig = act*beta*g, dxold = (1-act)*g.
+// One workgroup per (sample, 256-column chunk)... implemented as: grid (ceil(d/64), B), 4 waves
+// split L; column reductions through LDS.
+__global__ __launch_bounds__(256) void jump_select_bwd_kernel(
+    const float* __restrict__ g, const float* __restrict__ xn, const float* __restrict__ orig,
+    const float* __restrict__ act, const float* __restrict__ alpha, const float* __restrict__ beta,
+    float* __restrict__ dxn, float* __restrict__ dorig, float* __restrict__ dxold, float* __restrict__ dalpha,
+    float* __restrict__ dbeta, float* __restrict__ dgam, int64_t L, int d) {
+  __shared__ float red[3][4][64];
+  const int b = blockIdx.y;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int part = threadIdx.x >> 6;
+  const float a = act[b], al = alpha[b], be = beta[b];
+  float sa = 0.f, sb = 0.f, sg = 0.f;
+  if (c < d) {
+    for (int64_t l = part; l < L; l += 4) {
+      const int64_t i = ((int64_t)b * L + l) * d + c;
+      const float gv = g[i];
+      if (a != 0.f) {
+        sa += gv * xn[i];
+        sb += gv * orig[i];
+        sg += gv;
+        dxn[i] = al * gv;
+        dorig[i] = be * gv;
+        dxold[i] = 0.f;
+      } else {
+        dxn[i] = 0.f;
+        dorig[i] = 0.f;
+        dxold[i] = gv;
+      }
+    }
+  }
+  red[0][part][threadIdx.x & 63] = sa;
+  red[1][part][threadIdx.x & 63] = sb;
+  red[2][part][threadIdx.x & 63] = sg;
+  __syncthreads();
+  if (part == 0 && c < d) {
+    const int t = threadIdx.x;
+    float A = 0.f, Bv = 0.f, G = 0.f;
+    for (int p = 0; p < 4; ++p) {
+      A += red[0][p][t];
+      Bv += red[1][p][t];
+      G += red[2][p][t];
+    }
+    dgam[(int64_t)b * d + c] = G;
+    atomicAdd(dalpha + b, A);
+    atomicAdd(dbeta + b, Bv);
+  }
+}
+
+// Per-sample column sums: out[b, c] = scale * sum_l x[b, l, c]  (x.mean(dim=1), model.py:435, 463;
+// BatchNorm / bias reductions).  grid (ceil(d/64), B), 4 waves split L.
+__global__ __launch_bounds__(256) void seg_colsum_kernel(const float* __restrict__ x, float* __restrict__ out,
+                                                         int64_t L, int d, float scale, int accumulate) {
+  __shared__ float red[4][64];
+  const int b = blockIdx.y;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int part = threadIdx.x >> 6;
+  float s = 0.f;
+  if (c < d)
+    for (int64_t l = part; l < L; l += 4) s += x[((int64_t)b * L + l) * d + c];
+  red[part][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (part == 0 && c < d) {
+    const int t = threadIdx.x;
+    const float v = (red[0][t] + red[1][t] + red[2][t] + red[3][t]) * scale;
+    if (accumulate) out[(int64_t)b * d + c] += v;
+    else out[(int64_t)b * d + c] = v;
+  }
+}
+
+// Column sums over many rows (bias gradients): out[c] += sum_r x[r, c].  grid (ceil(d/64), chunks).
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ x, float* __restrict__ out,
+                                                     int64_t rows, int d, int64_t chunk) {
+  __shared__ float red[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int part = threadIdx.x >> 6;
+  const int64_t r0 = (int64_t)blockIdx.y * chunk;
+  const int64_t r1 = min(rows, r0 + chunk);
+  float s = 0.f;
+  if (c < d)
+    for (int64_t r = r0 + part; r < r1; r += 4) s += x[r * d + c];
+  red[part][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (part == 0 && c < d) {
+    const int t = threadIdx.x;
+    atomicAdd(out + c, red[0][t] + red[1][t] + red[2][t] + red[3][t]);
+  }
+}
+
+// out[b, l, :] = x[b, l, :] + t[l, :] (+ u[b, :]).  Sinusoid PE add (model.py:161, 580),
+// position add (model.py:615) and the broadcast of per-sample vectors.
+__global__ void add_rows_kernel(const float* __restrict__ x, const float* __restrict__ t, const float* __restrict__ u,
+                                float* __restrict__ out, int64_t B, int64_t L, int d) {
+  const int64_t total = B * L * d;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = i % d;
+    const int64_t l = (i / d) % L;
+    const int64_t b = i / (L * d);
+    float v = x ? x[i] : 0.f;
+    if (t) v += t[l * d + c];
+    if (u) v += u[b * d + c];
+    out[i] = v;
+  }
+}
+
+// out = a*x + b*y (+ c*z): residual sums, e = a+b+c, blend (model.py:578-583, 624, 628)
+__global__ void lincomb_kernel(const float* __restrict__ x, const float* __restrict__ y, const float* __restrict__ z,
+                               float a, float b, float c, float* __restrict__ out, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float v = a * x[i];
+    if (y) v += b * y[i];
+    if (z) v += c * z[i];
+    out[i] = v;
+  }
+}
+
+// activation forward / backward (GELU / SiLU / sigmoid, model.py:104, 143-147)
+__global__ void act_fwd_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n, int act) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    y[i] = apply_act(act, x[i]);
+}
+__global__ void act_bwd_kernel(const float* __restrict__ g, const float* __restrict__ x, float* __restrict__ dx,
+                               int64_t n, int act) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float v = x[i];
+    float d;
+    switch (act) {
+      case ACT_GELU: d = gelu_grad(v); break;
+      case ACT_SILU: d = silu_grad(v); break;
+      case ACT_SIGMOID: {
+        const float s = sigmoid_f(v);
+        d = s * (1.f - s);
+        break;
+      }
+      default: d = 1.f;
+    }
+    dx[i] = g[i] * d;
+  }
+}
+
+// GLU over channels (nn.GLU(dim=1), model.py:97) on channels-last rows of 2C: out = a * sigmoid(b)
+__global__ void glu_fwd_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t rows, int C) {
+  const int64_t total = rows * C;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / C, c = i % C;
+    y[i] = x[r * 2 * C + c] * sigmoid_f(x[r * 2 * C + C + c]);
+  }
+}
+__global__ void glu_bwd_kernel(const float* __restrict__ g, const float* __restrict__ x, float* __restrict__ dx,
+                               int64_t rows, int C) {
+  const int64_t total = rows * C;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / C, c = i % C;
+    const float a = x[r * 2 * C + c], s = sigmoid_f(x[r * 2 * C + C + c]);
+    dx[r * 2 * C + c] = g[i] * s;
+    dx[r * 2 * C + C + c] = g[i] * a * s * (1.f - s);
+  }
+}
+
+// nn.Dropout(0.1) in train mode (model.py:107, 147) with keyed masks on channels-last (B, T, C):
+// keep iff noise_uniform(key, (sid*C + c)*4096 + t) >= p, scaled by 1/(1-p).  Same kernel for
+// backward (the mask is recomputed).
+__global__ void dropout_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t B, int64_t T, int C,
+                               int64_t sid_base, uint32_t key, float p) {
+  const int64_t total = B * T * C;
+  const float sc = 1.0f / (1.0f - p);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = i % C;
+    const int64_t t = (i / C) % T;
+    const int64_t b = i / ((int64_t)T * C);
+    const uint32_t idx = (uint32_t)(((sid_base + b) * C + c) * 4096 + t);
+    y[i] = noise_uniform(key, idx) >= p ? x[i] * sc : 0.f;
+  }
+}
+
+// ============================================================================ depthwise conv
+// groups=D Conv1d with kernel K, padding K/2 (ConvLite.depth k15, model.py:99-102; encoder k3,
+// model.py:147) on channels-last (B, T, C).
+__global__ void dwconv_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ b,
+                                  float* __restrict__ y, int64_t B, int64_t T, int C, int K) {
+  const int64_t total = B * T * C;
+  const int pad = K / 2;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = i % C;
+    const int64_t t = (i / C) % T;
+    const int64_t base = i - t * C;  // (b, 0, c)
+    float s = b ? b[c] : 0.f;
+    for (int k = 0; k < K; ++k) {
+      const int64_t tt = t + k - pad;
+      if (tt >= 0 && tt < T) s += w[c * K + k] * x[base + tt * C];
+    }
+    y[i] = s;
+  }
+}
+
+__global__ void dwconv_bwd_data_kernel(const float* __restrict__ g, const float* __restrict__ w, float* __restrict__ dx,
+                                       int64_t B, int64_t T, int C, int K) {
+  const int64_t total = B * T * C;
+  const int pad = K / 2;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = i % C;
+    const int64_t t = (i / C) % T;
+    const int64_t base = i - t * C;
+    float s = 0.f;
+    for (int k = 0; k < K; ++k) {
+      const int64_t tt = t - k + pad;
+      if (tt >= 0 && tt < T) s += w[c * K + k] * g[base + tt * C];
+    }
+    dx[i] = s;
+  }
+}
+
+// dw[c, k] += sum_{b,t} g[b,t,c] x[b,t+k-pad,c] ; db[c] += sum g.  grid (ceil(C/64), B*chunks)
+__global__ __launch_bounds__(256) void dwconv_bwd_w_kernel(const float* __restrict__ g, const float* __restrict__ x,
+                                                           float* __restrict__ dw, float* __restrict__ db, int64_t B,
+                                                           int64_t T, int C, int K, int64_t chunk) {
+  __shared__ float red[4][64][17];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int part = threadIdx.x >> 6;
+  const int64_t nch = (T + chunk - 1) / chunk;
+  const int64_t b = blockIdx.y / nch;
+  const int64_t t0 = (blockIdx.y % nch) * chunk;
+  const int64_t t1 = min(T, t0 + chunk);
+  const int pad = K / 2;
+  float acc[16];
+  float ab = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) acc[k] = 0.f;
+  if (c < C) {
+    for (int64_t t = t0 + part; t < t1; t += 4) {
+      const float gv = g[(b * T + t) * C + c];
+      ab += gv;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        if (k < K) {
+          const int64_t tt = t + k - pad;
+          if (tt >= 0 && tt < T) acc[k] += gv * x[(b * T + tt) * C + c];
+        }
+      }
+    }
+  }
+  const int tl = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) red[part][tl][k] = acc[k];
+  red[part][tl][16] = ab;
+  __syncthreads();
+  if (part == 0 && c < C) {
+    for (int k = 0; k < K; ++k) {
+      const float s = red[0][tl][k] + red[1][tl][k] + red[2][tl][k] + red[3][tl][k];
+      atomicAdd(dw + c * K + k, s);
+    }
+    if (db) atomicAdd(db + c, red[0][tl][16] + red[1][tl][16] + red[2][tl][16] + red[3][tl][16]);
+  }
+}
+
+// ============================================================================ BatchNorm (per sample)
+// nn.BatchNorm1d in train mode at batch 1 (ConvLite.bn, model.py:103, 114): statistics over T for
+// each (sample, channel).  Stats kernel: grid (ceil(C/64), B).
+__global__ __launch_bounds__(256) void bn_stats_kernel(const float* __restrict__ x, float* __restrict__ mean,
+                                                       float* __restrict__ rstd, int64_t T, int C, float eps) {
+  __shared__ float red[4][64];
+  __shared__ float mu_s[64];
+  const int b = blockIdx.y;
+  const int tl = threadIdx.x & 63;
+  const int c = blockIdx.x * 64 + tl;
+  const int part = threadIdx.x >> 6;
+  float s = 0.f;
+  if (c < C)
+    for (int64_t t = part; t < T; t += 4) s += x[((int64_t)b * T + t) * C + c];
+  red[part][tl] = s;
+  __syncthreads();
+  if (part == 0) mu_s[tl] = (red[0][tl] + red[1][tl] + red[2][tl] + red[3][tl]) / T;
+  __syncthreads();
+  const float mu = mu_s[tl];
+  float v = 0.f;
+  if (c < C)
+    for (int64_t t = part; t < T; t += 4) {
+      const float d = x[((int64_t)b * T + t) * C + c] - mu;
+      v += d * d;
+    }
+  __syncthreads();
+  red[part][tl] = v;
+  __syncthreads();
+  if (part == 0 && c < C) {
+    const float var = (red[0][tl] + red[1][tl] + red[2][tl] + red[3][tl]) / T;
+    mean[(int64_t)b * C + c] = mu;
+    rstd[(int64_t)b * C + c] = rsqrtf(var + eps);
+  }
+}
+
+// y = (x - mean[b,c]) * rstd[b,c] * w[c] + bb[c]   (mean/rstd per sample, or shared when B_stats == 1)
+__global__ void bn_apply_kernel(const float* __restrict__ x, const float* __restrict__ mean,
+                                const float* __restrict__ rstd, const float* __restrict__ w, const float* __restrict__ bb,
+                                float* __restrict__ y, int64_t B, int64_t T, int C, int per_sample) {
+  const int64_t total = B * T * C;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = i % C;
+    const int64_t b = i / (T * C);
+    const int64_t s = per_sample ? b * C + c : c;
+    y[i] = (x[i] - mean[s]) * rstd[s] * w[c] + bb[c];
+  }
+}
+
+// per-(b,c) sums for backward: sg[b,c] = sum_t g*w, sgx[b,c] = sum_t g*w*xhat ; dw += sum g*xhat,
+// db += sum g.  grid (ceil(C/64), B)
+__global__ __launch_bounds__(256) void bn_bwd_stats_kernel(const float* __restrict__ g, const float* __restrict__ x,
+                                                           const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                           const float* __restrict__ w, float* __restrict__ sg,
+                                                           float* __restrict__ sgx, float* __restrict__ dw,
+                                                           float* __restrict__ db, int64_t T, int C) {
+  __shared__ float red[2][4][64];
+  const int b = blockIdx.y;
+  const int tl = threadIdx.x & 63;
+  const int c = blockIdx.x * 64 + tl;
+  const int part = threadIdx.x >> 6;
+  float a = 0.f, ax = 0.f;
+  if (c < C) {
+    const float mu = mean[(int64_t)b * C + c], rs = rstd[(int64_t)b * C + c];
+    for (int64_t t = part; t < T; t += 4) {
+      const int64_t i = ((int64_t)b * T + t) * C + c;
+      const float gv = g[i];
+      a += gv;
+      ax += gv * (x[i] - mu) * rs;
+    }
+  }
+  red[0][part][tl] = a;
+  red[1][part][tl] = ax;
+  __syncthreads();
+  if (part == 0 && c < C) {
+    const float A = red[0][0][tl] + red[0][1][tl] + red[0][2][tl] + red[0][3][tl];
+    const float AX = red[1][0][tl] + red[1][1][tl] + red[1][2][tl] + red[1][3][tl];
+    sg[(int64_t)b * C + c] = A * w[c];
+    sgx[(int64_t)b * C + c] = AX * w[c];
+    atomicAdd(dw + c, AX);
+    atomicAdd(db + c, A);
+  }
+}
+
+__global__ void bn_bwd_apply_kernel(const float* __restrict__ g, const float* __restrict__ x,
+                                    const float* __restrict__ mean, const float* __restrict__ rstd,
+                                    const float* __restrict__ w, const float* __restrict__ sg,
+                                    const float* __restrict__ sgx, float* __restrict__ dx, int64_t B, int64_t T, int C) {
+  const int64_t total = B * T * C;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = i % C;
+    const int64_t b = i / (T * C);
+    const int64_t s = b * C + c;
+    const float rs = rstd[s];
+    const float xh = (x[i] - mean[s]) * rs;
+    dx[i] = rs * (g[i] * w[c] - sg[s] / T - xh * sgx[s] / T);
+  }
+}
+
+// ============================================================================ Conv1d(1, D, 3) stem
+// AudioEncoder.conv2 (model.py:132-135) for single-channel streams: y[b,t,o] = bias[o] +
+// sum_k W[o,k] x[b, t+k-1].  Output channels-last.
+__global__ void stem1_fwd_kernel(const float* __restrict__ x, const float* __restrict__ W, const float* __restrict__ bias,
+                                 float* __restrict__ y, int64_t B, int64_t T, int D) {
+  const int64_t total = B * T * D;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t o = i % D;
+    const int64_t t = (i / D) % T;
+    const int64_t b = i / (T * D);
+    const float* xr = x + b * T;
+    float s = bias[o];
+    if (t > 0) s += W[o * 3 + 0] * xr[t - 1];
+    s += W[o * 3 + 1] * xr[t];
+    if (t + 1 < T) s += W[o * 3 + 2] * xr[t + 1];
+    y[i] = s;
+  }
+}
+// dW[o,k] += sum_{b,t} g[b,t,o] x[b,t+k-1]; db[o] += sum g.  grid (ceil(D/64), B*chunks)
+__global__ __launch_bounds__(256) void stem1_bwd_w_kernel(const float* __restrict__ g, const float* __restrict__ x,
+                                                          float* __restrict__ dW, float* __restrict__ db, int64_t B,
+                                                          int64_t T, int D, int64_t chunk) {
+  __shared__ float red[4][64][4];
+  const int tl = threadIdx.x & 63;
+  const int o = blockIdx.x * 64 + tl;
+  const int part = threadIdx.x >> 6;
+  const int64_t nch = (T + chunk - 1) / chunk;
+  const int64_t b = blockIdx.y / nch;
+  const int64_t t0 = (blockIdx.y % nch) * chunk, t1 = min(T, t0 + chunk);
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, ab = 0.f;
+  if (o < D) {
+    const float* xr = x + b * T;
+    for (int64_t t = t0 + part; t < t1; t += 4) {
+      const float gv = g[(b * T + t) * D + o];
+      ab += gv;
+      if (t > 0) a0 += gv * xr[t - 1];
+      a1 += gv * xr[t];
+      if (t + 1 < T) a2 += gv * xr[t + 1];
+    }
+  }
+  red[part][tl][0] = a0;
+  red[part][tl][1] = a1;
+  red[part][tl][2] = a2;
+  red[part][tl][3] = ab;
+  __syncthreads();
+  if (part == 0 && o < D) {
+    for (int k = 0; k < 4; ++k) {
+      const float s = red[0][tl][k] + red[1][tl][k] + red[2][tl][k] + red[3][tl][k];
+      if (k < 3) atomicAdd(dW + o * 3 + k, s);
+      else atomicAdd(db + o, s);
+    }
+  }
+}
+
+// ============================================================================ embedding
+// processor.token (model.py:592, 606): y[r] = E[ids[r]]; backward scatter-adds rows.
+__global__ void embed_fwd_kernel(const int64_t* __restrict__ ids, const float* __restrict__ E, float* __restrict__ y,
+                                 int64_t rows, int d) {
+  const int64_t total = rows * d;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / d, c = i % d;
+    y[i] = E[ids[r] * d + c];
+  }
+}
+__global__ void embed_bwd_kernel(const int64_t* __restrict__ ids, const float* __restrict__ g, float* __restrict__ dE,
+                                 int64_t rows, int d) {
+  const int64_t total = rows * d;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / d, c = i % d;
+    atomicAdd(dE + ids[r] * d + c, g[i]);
+  }
+}
+
+// ============================================================================ cross entropy
+// F.cross_entropy(logits, labels, ignore_index=0) (model.py:670) over fp32 logits rows of V:
+// loss[r] = logsumexp(z_r) - z_r[label] (0 for ignored rows), lse[r] saved.
+__global__ __launch_bounds__(256) void ce_fwd_kernel(const float* __restrict__ z, const int64_t* __restrict__ labels,
+                                                     float* __restrict__ loss, float* __restrict__ lse, int64_t V) {
+  __shared__ float red[4];
+  const int64_t r = blockIdx.x;
+  const float* zr = z + r * V;
+  float m = -INFINITY;
+  for (int64_t j = threadIdx.x; j < V; j += 256) m = fmaxf(m, zr[j]);
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float s = 0.f;
+  for (int64_t j = threadIdx.x; j < V; j += 256) s += expf(zr[j] - m);
+  s = block_sum<256>(s, red);
+  if (threadIdx.x == 0) {
+    const float l = m + logf(s);
+    lse[r] = l;
+    const int64_t y = labels[r];
+    loss[r] = (y == 0) ? 0.f : l - zr[y];
+  }
+}
+// dz = scale * (softmax - onehot) for non-ignored rows, 0 otherwise (in place allowed)
+__global__ __launch_bounds__(256) void ce_bwd_kernel(const float* __restrict__ z, const int64_t* __restrict__ labels,
+                                                     const float* __restrict__ lse, const float* __restrict__ scale,
+                                                     float* __restrict__ dz, int64_t V) {
+  const int64_t r = blockIdx.x;
+  const int64_t y = labels[r];
+  const float sc = (y == 0) ? 0.f : scale[0];
+  const float l = lse[r];
+  for (int64_t j = threadIdx.x; j < V; j += 256) {
+    const float p = expf(z[r * V + j] - l);
+    dz[r * V + j] = sc * (p - (j == y ? 1.f : 0.f));
+  }
+}
+
+}  // namespace asrx
+
+using namespace asrx;
+
+#define LAUNCH_ROWS(kernel, rows, shm, ...) \
+  kernel<<<row_grid(rows), 64 * RW, shm, stream>>>(__VA_ARGS__)
+#define LAUNCH_EW(kernel, n, ...) kernel<<<ew_grid(n), 256, 0, stream>>>(__VA_ARGS__)
+
+extern "C" {
+
+int asrx_layernorm_fwd(const float* x, const float* w, const float* b, float* y, float* mean, float* rstd,
+                       int64_t rows, int64_t d, float eps, hipStream_t stream) {
+  if (rows == 0) return 0;
+  LAUNCH_ROWS(ln_fwd_kernel, rows, 0, x, w, b, y, mean, rstd, rows, (int)d, eps);
+  ASRX_LAUNCHED("asrx_layernorm_fwd");
+}
+
+int asrx_layernorm_bwd(const float* dy, const float* x, const float* w, const float* mean, const float* rstd,
+                       float* dx, float* dw, float* db, int64_t rows, int64_t d, hipStream_t stream) {
+  ASRX_REQUIRE(d <= 2048, "layernorm_bwd: d too large");
+  if (rows == 0) return 0;
+  const size_t shm = (size_t)RW * 2 * d * sizeof(float);
+  ln_bwd_kernel<<<row_grid(rows, 1024), 64 * RW, shm, stream>>>(dy, x, w, mean, rstd, dx, dw, db, rows, (int)d);
+  ASRX_LAUNCHED("asrx_layernorm_bwd");
+}
+
+int asrx_small_linear_fwd(const float* x, const float* W, const float* b, float* y, int64_t rows, int64_t K,
+                          int64_t N, int act, hipStream_t stream) {
+  if (rows == 0) return 0;
+  switch (N) {
+    case 1: LAUNCH_ROWS(small_linear_fwd_kernel<1>, rows, 0, x, W, b, y, rows, (int)K, act); break;
+    case 2: LAUNCH_ROWS(small_linear_fwd_kernel<2>, rows, 0, x, W, b, y, rows, (int)K, act); break;
+    case 3: LAUNCH_ROWS(small_linear_fwd_kernel<3>, rows, 0, x, W, b, y, rows, (int)K, act); break;
+    case 4: LAUNCH_ROWS(small_linear_fwd_kernel<4>, rows, 0, x, W, b, y, rows, (int)K, act); break;
+    default: ASRX_REQUIRE(false, "small_linear: N=%ld not in 1..4", (long)N);
+  }
+  ASRX_LAUNCHED("asrx_small_linear_fwd");
+}
+
+int asrx_small_linear_bwd(const float* dy, const float* y, const float* x, const float* W, float* dx, float* dW,
+                          float* db, int64_t rows, int64_t K, int64_t N, int act, float beta, hipStream_t stream) {
+  if (rows == 0) return 0;
+  const size_t shm = (size_t)RW * (N * K + N) * sizeof(float);
+  ASRX_REQUIRE(shm <= 64 * 1024, "small_linear_bwd: K too large");
+  const unsigned g = row_grid(rows, 1024);
+  switch (N) {
+    case 1: small_linear_bwd_kernel<1><<<g, 64 * RW, shm, stream>>>(dy, y, x, W, dx, dW, db, rows, (int)K, act, beta); break;
+    case 2: small_linear_bwd_kernel<2><<<g, 64 * RW, shm, stream>>>(dy, y, x, W, dx, dW, db, rows, (int)K, act, beta); break;
+    case 3: small_linear_bwd_kernel<3><<<g, 64 * RW, shm, stream>>>(dy, y, x, W, dx, dW, db, rows, (int)K, act, beta); break;
+    case 4: small_linear_bwd_kernel<4><<<g, 64 * RW, shm, stream>>>(dy, y, x, W, dx, dW, db, rows, (int)K, act, beta); break;
+    default: ASRX_REQUIRE(false, "small_linear: N=%ld not in 1..4", (long)N);
+  }
+  ASRX_LAUNCHED("asrx_small_linear_bwd");
+}
+
+int asrx_rownorm(const float* x, float* n, int64_t rows, int64_t d, hipStream_t stream) {
+  if (rows == 0) return 0;
+  LAUNCH_ROWS(rownorm_kernel, rows, 0, x, n, rows, (int)d);
+  ASRX_LAUNCHED("asrx_rownorm");
+}
+
+int asrx_rownorm_bwd(const float* dn, const float* x, const float* n, float* dx, int64_t rows, int64_t d,
+                     hipStream_t stream) {
+  if (rows == 0) return 0;
+  LAUNCH_EW(rownorm_bwd_kernel, rows * d, dn, x, n, dx, rows, (int)d);
+  ASRX_LAUNCHED("asrx_rownorm_bwd");
+}
+
+int asrx_rotary_fwd(const float* x, const float* m, const float* f, float* y, int64_t BL, int64_t L, int64_t D,
+                    int64_t hd, float scale, hipStream_t stream) {
+  ASRX_REQUIRE(hd % 2 == 0 && D % hd == 0, "rotary: bad head dim");
+  if (BL == 0) return 0;
+  LAUNCH_ROWS(rotary_fwd_kernel, BL, 0, x, m, f, y, BL, L, (int)D, (int)hd, scale);
+  ASRX_LAUNCHED("asrx_rotary_fwd");
+}
+
+int asrx_rotary_bwd(const float* g, const float* x, const float* m, const float* f, float* dx, float* dm, int64_t BL,
+                    int64_t L, int64_t D, int64_t hd, float scale, hipStream_t stream) {
+  if (BL == 0) return 0;
+  LAUNCH_ROWS(rotary_bwd_kernel, BL, 0, g, x, m, f, dx, dm, BL, L, (int)D, (int)hd, scale);
+  ASRX_LAUNCHED("asrx_rotary_bwd");
+}
+
+int asrx_vgate_fwd(const float* S, const float* nx, const float* mval, const float* h, const float* w2,
+                   const float* b2, const float* cw, const float* cb, const float* tx, float* ion, float* xval,
+                   float* kv, float* m2, int64_t rows, int64_t M, int64_t Dh, float inv_sqrt_d, hipStream_t stream) {
+  ASRX_REQUIRE(M <= 64, "vgate: memory size must be <= 64");
+  if (rows == 0) return 0;
+  LAUNCH_ROWS(vgate_fwd_kernel, rows, 0, S, nx, mval, h, w2, b2, cw, cb, tx, ion, xval, kv, m2, rows, (int)M,
+              (int)Dh, inv_sqrt_d);
+  ASRX_LAUNCHED("asrx_vgate_fwd");
+}
+
+int asrx_vgate_bwd(const float* dion, const float* S, const float* nx, const float* mval, const float* h,
+                   const float* w2, const float* cw, const float* kv, const float* m2, float* dS, float* dnx,
+                   float* dh, float* dmval, float* dw2, float* db2, float* dcw, float* dcb, int64_t rows, int64_t M,
+                   int64_t Dh, float inv_sqrt_d, hipStream_t stream) {
+  if (rows == 0) return 0;
+  const size_t shm = (size_t)RW * (M + Dh + 4) * sizeof(float);
+  vgate_bwd_kernel<<<row_grid(rows, 1024), 64 * RW, shm, stream>>>(dion, S, nx, mval, h, w2, cw, kv, m2, dS, dnx, dh,
+                                                                    dmval, dw2, db2, dcw, dcb, rows, (int)M, (int)Dh,
+                                                                    inv_sqrt_d);
+  ASRX_LAUNCHED("asrx_vgate_bwd");
+}
+
+int asrx_tgate_fwd(const float* G, const float* c, float* out, int64_t rows, int64_t D, hipStream_t stream) {
+  if (rows == 0) return 0;
+  LAUNCH_ROWS(tgate_fwd_kernel, rows, 0, G, c, out, rows, (int)D);
+  ASRX_LAUNCHED("asrx_tgate_fwd");
+}
+
+int asrx_tgate_bwd(const float* dout, const float* G, const float* c, float* dGz, float* dc, int64_t rows, int64_t D,
+                   hipStream_t stream) {
+  if (rows == 0) return 0;
+  LAUNCH_ROWS(tgate_bwd_kernel, rows, 0, dout, G, c, dGz, dc, rows, (int)D);
+  ASRX_LAUNCHED("asrx_tgate_bwd");
+}
+
+int asrx_axpy_row(const float* x, const float* s, const float* y, float* out, int64_t rows, int64_t d,
+                  hipStream_t stream) {
+  if (rows == 0) return 0;
+  LAUNCH_EW(axpy_row_kernel, rows * d, x, s, y, out, rows, (int)d);
+  ASRX_LAUNCHED("asrx_axpy_row");
+}
+
+int asrx_axpy_row_bwd(const float* g, const float* s, const float* y, float* dy, float* ds, int64_t rows, int64_t d,
+                      hipStream_t stream) {
+  if (rows == 0) return 0;
+  LAUNCH_ROWS(axpy_row_bwd_kernel, rows, 0, g, s, y, dy, ds, rows, (int)d);
+  ASRX_LAUNCHED("asrx_axpy_row_bwd");
+}
+
+int asrx_jump_select(const float* xn, const float* orig, const float* xold, const float* act, const float* alpha,
+                     const float* beta, const float* gam, float* out, int64_t B, int64_t L, int64_t d,
+                     hipStream_t stream) {
+  if (B * L == 0) return 0;
+  LAUNCH_EW(jump_select_kernel, B * L * d, xn, orig, xold, act, alpha, beta, gam, out, B, L, (int)d);
+  ASRX_LAUNCHED("asrx_jump_select");
+}
+
+int asrx_jump_select_bwd(const float* g, const float* xn, const float* orig, const float* act, const float* alpha,
+                         const float* beta, float* dxn, float* dorig, float* dxold, float* dalpha, float* dbeta,
+                         float* dgam, int64_t B, int64_t L, int64_t d, hipStream_t stream) {
+  if (B * L == 0) return 0;
+  dim3 grid((unsigned)((d + 63) / 64), (unsigned)B);
+  jump_select_bwd_kernel<<<grid, 256, 0, stream>>>(g, xn, orig, act, alpha, beta, dxn, dorig, dxold, dalpha, dbeta,
+                                                   dgam, L, (int)d);
+  ASRX_LAUNCHED("asrx_jump_select_bwd");
+}
+
+int asrx_seg_colsum(const float* x, float* out, int64_t B, int64_t L, int64_t d, float scale, int accumulate,
+                    hipStream_t stream) {
+  if (B == 0) return 0;
+  dim3 grid((unsigned)((d + 63) / 64), (unsigned)B);
+  seg_colsum_kernel<<<grid, 256, 0, stream>>>(x, out, L, (int)d, scale, accumulate);
+  ASRX_LAUNCHED("asrx_seg_colsum");
+}
+
+int asrx_colsum(const float* x, float* out, int64_t rows, int64_t d, hipStream_t stream) {
+  if (rows == 0) return 0;
+  int64_t chunks = std::min<int64_t>(std::max<int64_t>(rows / 512, 1), 1024);
+  const int64_t chunk = (rows + chunks - 1) / chunks;
+  chunks = (rows + chunk - 1) / chunk;
+  dim3 grid((unsigned)((d + 63) / 64), (unsigned)chunks);
+  colsum_kernel<<<grid, 256, 0, stream>>>(x, out, rows, (int)d, chunk);
+  ASRX_LAUNCHED("asrx_colsum");
+}
+
+int asrx_add_rows(const float* x, const float* t, const float* u, float* out, int64_t B, int64_t L, int64_t d,
+                  hipStream_t stream) {
+  if (B * L * d == 0) return 0;
+  LAUNCH_EW(add_rows_kernel, B * L * d, x, t, u, out, B, L, (int)d);
+  ASRX_LAUNCHED("asrx_add_rows");
+}
+
+int asrx_lincomb(const float* x, const float* y, const float* z, float a, float b, float c, float* out, int64_t n,
+                 hipStream_t stream) {
+  if (n == 0) return 0;
+  LAUNCH_EW(lincomb_kernel, n, x, y, z, a, b, c, out, n);
+  ASRX_LAUNCHED("asrx_lincomb");
+}
+
+int asrx_act_fwd(const float* x, float* y, int64_t n, int act, hipStream_t stream) {
+  if (n == 0) return 0;
+  LAUNCH_EW(act_fwd_kernel, n, x, y, n, act);
+  ASRX_LAUNCHED("asrx_act_fwd");
+}
+
+int asrx_act_bwd(const float* g, const float* x, float* dx, int64_t n, int act, hipStream_t stream) {
+  if (n == 0) return 0;
+  LAUNCH_EW(act_bwd_kernel, n, g, x, dx, n, act);
+  ASRX_LAUNCHED("asrx_act_bwd");
+}
+
+int asrx_glu_fwd(const float* x, float* y, int64_t rows, int64_t C, hipStream_t stream) {
+  if (rows == 0) return 0;
+  LAUNCH_EW(glu_fwd_kernel, rows * C, x, y, rows, (int)C);
+  ASRX_LAUNCHED("asrx_glu_fwd");
+}
+
+int asrx_glu_bwd(const float* g, const float* x, float* dx, int64_t rows, int64_t C, hipStream_t stream) {
+  if (rows == 0) return 0;
+  LAUNCH_EW(glu_bwd_kernel, rows * C, g, x, dx, rows, (int)C);
+  ASRX_LAUNCHED("asrx_glu_bwd");
+}
+
+int asrx_dropout(const float* x, float* y, int64_t B, int64_t T, int64_t C, int64_t sid_base, uint32_t key, float p,
+                 hipStream_t stream) {
+  if (B * T * C == 0) return 0;
+  LAUNCH_EW(dropout_kernel, B * T * C, x, y, B, T, (int)C, sid_base, key, p);
+  ASRX_LAUNCHED("asrx_dropout");
+}
+
+int asrx_dwconv_fwd(const float* x, const float* w, const float* b, float* y, int64_t B, int64_t T, int64_t C,
+                    int64_t K, hipStream_t stream) {
+  ASRX_REQUIRE(K % 2 == 1 && K <= 16, "dwconv: K must be odd and <= 15");
+  if (B * T == 0) return 0;
+  LAUNCH_EW(dwconv_fwd_kernel, B * T * C, x, w, b, y, B, T, (int)C, (int)K);
+  ASRX_LAUNCHED("asrx_dwconv_fwd");
+}
+
+int asrx_dwconv_bwd(const float* g, const float* x, const float* w, float* dx, float* dw, float* db, int64_t B,
+                    int64_t T, int64_t C, int64_t K, hipStream_t stream) {
+  if (B * T == 0) return 0;
+  if (dx) LAUNCH_EW(dwconv_bwd_data_kernel, B * T * C, g, w, dx, B, T, (int)C, (int)K);
+  const int64_t chunk = 256;
+  const int64_t nch = (T + chunk - 1) / chunk;
+  dim3 grid((unsigned)((C + 63) / 64), (unsigned)(B * nch));
+  dwconv_bwd_w_kernel<<<grid, 256, 0, stream>>>(g, x, dw, db, B, T, (int)C, (int)K, chunk);
+  ASRX_LAUNCHED("asrx_dwconv_bwd");
+}
+
+int asrx_bn_fwd(const float* x, const float* w, const float* b, float* y, float* mean, float* rstd, int64_t B,
+                int64_t T, int64_t C, float eps, int use_batch_stats, hipStream_t stream) {
+  if (B * T == 0) return 0;
+  if (use_batch_stats) {
+    dim3 grid((unsigned)((C + 63) / 64), (unsigned)B);
+    bn_stats_kernel<<<grid, 256, 0, stream>>>(x, mean, rstd, T, (int)C, eps);
+  }
+  LAUNCH_EW(bn_apply_kernel, B * T * C, x, mean, rstd, w, b, y, B, T, (int)C, use_batch_stats);
+  ASRX_LAUNCHED("asrx_bn_fwd");
+}
+
+int asrx_bn_bwd(const float* g, const float* x, const float* mean, const float* rstd, const float* w, float* sg_ws,
+                float* sgx_ws, float* dx, float* dw, float* db, int64_t B, int64_t T, int64_t C, hipStream_t stream) {
+  if (B * T == 0) return 0;
+  dim3 grid((unsigned)((C + 63) / 64), (unsigned)B);
+  bn_bwd_stats_kernel<<<grid, 256, 0, stream>>>(g, x, mean, rstd, w, sg_ws, sgx_ws, dw, db, T, (int)C);
+  LAUNCH_EW(bn_bwd_apply_kernel, B * T * C, g, x, mean, rstd, w, sg_ws, sgx_ws, dx, B, T, (int)C);
+  ASRX_LAUNCHED("asrx_bn_bwd");
+}
+
+int asrx_stem1_fwd(const float* x, const float* W, const float* bias, float* y, int64_t B, int64_t T, int64_t D,
+                   hipStream_t stream) {
+  if (B * T == 0) return 0;
+  LAUNCH_EW(stem1_fwd_kernel, B * T * D, x, W, bias, y, B, T, (int)D);
+  ASRX_LAUNCHED("asrx_stem1_fwd");
+}
+
+int asrx_stem1_bwd(const float* g, const float* x, float* dW, float* db, int64_t B, int64_t T, int64_t D,
+                   hipStream_t stream) {
+  if (B * T == 0) return 0;
+  const int64_t chunk = 256, nch = (T + chunk - 1) / chunk;
+  dim3 grid((unsigned)((D + 63) / 64), (unsigned)(B * nch));
+  stem1_bwd_w_kernel<<<grid, 256, 0, stream>>>(g, x, dW, db, B, T, (int)D, chunk);
+  ASRX_LAUNCHED("asrx_stem1_bwd");
+}
+
+int asrx_embed_fwd(const int64_t* ids, const float* E, float* y, int64_t rows, int64_t d, hipStream_t stream) {
+  if (rows == 0) return 0;
+  LAUNCH_EW(embed_fwd_kernel, rows * d, ids, E, y, rows, (int)d);
+  ASRX_LAUNCHED("asrx_embed_fwd");
+}
+
+int asrx_embed_bwd(const int64_t* ids, const float* g, float* dE, int64_t rows, int64_t d, hipStream_t stream) {
+  if (rows == 0) return 0;
+  LAUNCH_EW(embed_bwd_kernel, rows * d, ids, g, dE, rows, (int)d);
+  ASRX_LAUNCHED("asrx_embed_bwd");
+}
+
+int asrx_ce_fwd(const float* z, const int64_t* labels, float* loss, float* lse, int64_t rows, int64_t V,
+                hipStream_t stream) {
+  if (rows == 0) return 0;
+  ASRX_REQUIRE(rows < (1LL << 31), "ce: too many rows");
+  ce_fwd_kernel<<<(unsigned)rows, 256, 0, stream>>>(z, labels, loss, lse, V);
+  ASRX_LAUNCHED("asrx_ce_fwd");
+}
+
+int asrx_ce_bwd(const float* z, const int64_t* labels, const float* lse, const float* scale, float* dz, int64_t rows,
+                int64_t V, hipStream_t stream) {
+  if (rows == 0) return 0;
+  ce_bwd_kernel<<<(unsigned)rows, 256, 0, stream>>>(z, labels, lse, scale, dz, V);
+  ASRX_LAUNCHED("asrx_ce_bwd");
+}
+
+}  // extern "C"
+
+// MSheath policy gumbel noise (model.py:476): out[b, i, k] = gumbel(key, ((sid_base + b)*64 + i)*3 + k)
+namespace asrx {
+__global__ void policy_noise_kernel(float* out, int64_t B, int64_t layers, int64_t sid_base, uint32_t key) {
+  const int64_t n = B * layers * 3;
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = j % 3, i = (j / 3) % layers, b = j / (3 * layers);
+    out[j] = noise_gumbel(key, (uint32_t)(((sid_base + b) * 64 + i) * 3 + k));
+  }
+}
+}  // namespace asrx
+extern "C" int asrx_policy_noise(float* out, int64_t B, int64_t layers, int64_t sid_base, uint32_t key,
+                                 hipStream_t stream) {
+  ASRX_REQUIRE(layers <= 64, "policy noise: at most 64 layers");
+  if (B * layers == 0) return 0;
+  asrx::policy_noise_kernel<<<(unsigned)((B * layers * 3 + 255) / 256), 256, 0, stream>>>(out, B, layers, sid_base, key);
+  ASRX_LAUNCHED("asrx_policy_noise");
+}

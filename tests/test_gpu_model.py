@@ -1,0 +1,75 @@
+"""Whole-model parity: the HIP Model (fp32 parity mode) against the oracle forward (float64 CPU) on
+identical parameters, inputs and keyed noise — logits, argmax ids, loss and parameter gradients."""
+import pytest
+import torch
+
+from oracle import model as om
+
+pytestmark = pytest.mark.gpu
+
+
+def _toy_inputs(B=2, T=8, S=101, V=1000, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    spec = torch.randn(B, 128, S, generator=g)
+    pitch = torch.rand(B, 1, S, generator=g) * 200
+    wav = torch.randn(B, 1, S - 1, generator=g) * 0.1
+    ids = torch.randint(3, V, (B, T), generator=g)
+    ids[:, 0] = 1
+    labels = torch.cat([ids[:, 1:], torch.full((B, 1), 2)], 1)
+    labels[1, -2:] = 0  # some ignored positions
+    return spec, pitch, wav, ids, labels
+
+
+def _rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-12))
+
+
+@pytest.mark.parametrize("train", [True, False])
+def test_model_parity_fp32(cuda, train):
+    from asrx import prec
+    from asrx.config import Dimensions
+    from asrx.model import Model
+
+    torch.manual_seed(0)
+    cfg = Dimensions(tokens=1000, mels=128, dims=128, head=2, layer=4, act="gelu", n_type="AbbyNormal")
+    model = Model(cfg).cuda()
+    model.train(train)
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    spec, pitch, wav, ids, labels = _toy_inputs()
+    seed, step = 7, 3
+    model.set_noise(seed, step)
+    with prec.precision("fp32"):
+        out = model(labels=labels.cuda(), text_ids=ids.cuda(), spectrogram=spec.cuda(), pitch=pitch.cuda(),
+                    waveform=wav.cuda())
+        out["loss"].backward()
+    P = {k: (v.double().requires_grad_(True) if v.is_floating_point() else v) for k, v in sd.items()}
+    ref = om.forward(P, {"dims": 128, "head": 2, "layer": 4}, ids, labels, spectrogram=spec, pitch=pitch,
+                     waveform=wav, seed=seed, step=step, training=train)
+    ref["loss"].backward()
+    lg, lr = out["logits"].detach().cpu().double(), ref["logits"].detach()
+    err = float(((lg - lr).abs() / lr.abs().max()).max())
+    print("logits rel err", err, "loss", float(out["loss"]), float(ref["loss"]))
+    assert err < 1e-3
+    assert torch.equal(lg.argmax(-1), lr.argmax(-1))
+    assert abs(float(out["loss"]) - float(ref["loss"])) / abs(float(ref["loss"])) < 1e-3
+    if not train:
+        return
+    names = dict(model.named_parameters())
+    checked = 0
+    for name in ["processor.token.weight", "processor.position", "processor.ln.mode_router.0.weight",
+                 "processor.block.3.attn.q.1.weight", "processor.block.3.attn.kv.1.weight",
+                 "processor.block.3.jump.layers.0.v_gate.mkey", "processor.block.3.mlp.2.weight",
+                 "processor.block.3.jump.pnet.net.0.weight", "processor.block.3.jump.jump_s",
+                 "enc.conv1.0.weight", "enc.conv2.0.weight", "enc.encoder.0.3.depth.weight",
+                 "enc.encoder.1.1.parametrizations.weight.original1", "enc.encoder.0.3.bn.weight"]:
+        pg = names[name].grad
+        rg = P[name].grad
+        assert pg is not None and rg is not None, name
+        e = _rel(pg, rg)
+        print(name, e)
+        assert e < 5e-3, (name, e)
+        checked += 1
+    assert checked == 14
+    # dead blocks get no gradient in either implementation (model.py:617-628)
+    assert names["processor.block.0.attn.q.1.weight"].grad is None
