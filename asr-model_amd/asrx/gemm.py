@@ -6,7 +6,7 @@ from __future__ import annotations
 
 import torch
 
-from . import lib, prec
+from . import lib, prec, probe
 
 ACT = {"none": 0, "gelu": 1, "silu": 2, "sigmoid": 3, "relu": 4}
 
@@ -16,9 +16,11 @@ def gemm(A, B, C, *, M, N, K, lda, ldb, ldc, a_kc=True, b_kc=True, batch=1, sA=0
          conv_F=0, conv_C=0, splitk=1, precision=None):
     lib.require_gpu(A, B, C)
     p = prec.get() if precision is None else precision
+    e0 = probe.begin("gemm")
     lib.call("asrx_gemm", p, lib.ptr(A), lda, sA, int(a_kc), int(conv_a), lib.ptr(B), ldb, sB,
              int(b_kc), int(conv_b), lib.ptr(C), ldc, sC, lib.ptr(bias), lib.ptr(Z), M, N, K, batch,
              float(alpha), float(beta), ACT[act], conv_F, conv_C, int(splitk), lib.stream())
+    probe.end("gemm", e0, 2.0 * M * N * K * batch)
     return C
 
 

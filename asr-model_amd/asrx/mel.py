@@ -14,7 +14,7 @@ import math
 
 import torch
 
-from . import lib
+from . import lib, probe
 
 N_FFT = 1024
 HOP = 160
@@ -88,6 +88,12 @@ def n_frames(n_samples: int) -> int:
     return 1 + n_samples // HOP
 
 
+def algorithmic_bytes(B: int, N: int, pool: bool) -> float:
+    """read N*4 + write 128*F*4 per clip (+ the pooled waveform feature)."""
+    F = n_frames(N)
+    return float(B * (N * 4 + N_MELS * F * 4 + ((N // HOP) * 4 if pool else 0)))
+
+
 def logmel(wav: torch.Tensor, layout: str = "BFM", pool: bool = False):
     """Batched log-mel of (B, N) float32 device audio.
 
@@ -119,6 +125,8 @@ def logmel(wav: torch.Tensor, layout: str = "BFM", pool: bool = False):
         if T * HOP != N:
             raise ValueError("fused waveform pool needs N to be a multiple of 160")
         pooled = torch.empty(B, T, device=wav.device, dtype=torch.float32)
+    e0 = probe.begin("logmel")
     lib.call("asrx_logmel", lib.ptr(wav), B, N, wav.stride(0), lib.ptr(consts), lib.ptr(fbw),
              lib.ptr(fbs), lib.ptr(out), lay, F * N_MELS, lib.ptr(ws), lib.ptr(pooled), T, lib.stream())
+    probe.end("logmel", e0, algorithmic_bytes(B, N, pool))
     return (out, pooled) if pool else out

@@ -1,0 +1,45 @@
+"""Live per-kernel timing for bench.py: HIP events recorded around selected launches on the stream
+they run on (torch.cuda.Event on torch's current stream, which is the stream every asrx launch
+uses).  Off unless a bench enables it."""
+from __future__ import annotations
+
+import torch
+
+_active: dict | None = None
+
+
+def enable(kinds=("gemm", "logmel", "attn")):
+    global _active
+    _active = {k: [] for k in kinds}
+
+
+def disable():
+    global _active
+    out, _active = _active, None
+    return out
+
+
+def begin(kind):
+    if _active is None or kind not in _active:
+        return None
+    e = torch.cuda.Event(enable_timing=True)
+    e.record()
+    return e
+
+
+def end(kind, e0, work):
+    if e0 is None:
+        return
+    e1 = torch.cuda.Event(enable_timing=True)
+    e1.record()
+    _active[kind].append((work, e0, e1))
+
+
+def summarize(records):
+    """-> (launches, total work, total seconds); call after a device synchronize."""
+    n, work, sec = 0, 0.0, 0.0
+    for w, e0, e1 in records:
+        n += 1
+        work += w
+        sec += e0.elapsed_time(e1) * 1e-3
+    return n, work, sec

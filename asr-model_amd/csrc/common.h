@@ -103,7 +103,8 @@ __host__ __device__ __forceinline__ float ordered_to_float(int i) {
 // ------------------------------------------------------------ counter-based noise
 // The reference draws torch Exp(1) noise inside F.gumbel_softmax (essentials.py:170,
 // model.py:476) and Bernoulli masks inside nn.Dropout (model.py:107,147). Here noise is a pure
-// function of (site key, logical element index): u = (mix(mix(idx ^ k0) + k1) >> 8 + 0.5)/2^24,
+// function of (site key, logical element index): u = ((mix(mix(idx ^ k0) + k1) >> 9) + 0.5) / 2^23,
+// so 2^-24 <= u <= 1 - 2^-24 exactly in fp32 (u never rounds to 0 or 1, gumbel noise stays finite),
 // restated bit-for-bit in oracle/noise.py so the oracle sees the same draws.
 __host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
   x ^= x >> 16;
@@ -115,7 +116,7 @@ __host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
 }
 __device__ __forceinline__ float noise_uniform(uint32_t key, uint32_t idx) {
   uint32_t h = mix32(mix32(idx ^ key) + (key * 0x9E3779B9U + 0x632BE5ABU));
-  return ((float)(h >> 8) + 0.5f) * (1.0f / 16777216.0f);
+  return ((float)(h >> 9) + 0.5f) * (1.0f / 8388608.0f);
 }
 // Gumbel(0,1) sample g = -log(E), E = -log(u) ~ Exp(1).
 __device__ __forceinline__ float noise_gumbel(uint32_t key, uint32_t idx) {

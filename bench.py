@@ -1,0 +1,197 @@
+#!/usr/bin/env python
+"""Headline benchmark: audio-sec/sec fwd+bwd on 30 s / 16 kHz clips (BASELINE.json `metric`).
+
+One step = the hot path over one batch of synthetic clips already resident in HBM:
+  log-mel + waveform pool (HIP) on the raw 30 s waveforms -> Model.forward (tiny config,
+  BASELINE configs[1]: 4 enc / 4 dec, d=384, 6 heads, bf16 MFMA) -> cross entropy -> backward ->
+  (N > 1) RCCL bucketed gradient all-reduce overlapped with backward, joined before the step ends.
+Weak scaling: every rank processes its own B clips; `value` is the whole-job aggregate.
+
+python bench.py --gpus N --steps K --warmup W         (N > 1: launched by torch.distributed.run)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "asr-model_amd")]
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+CLIP_SECONDS = 30.0
+HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md chip table (spec)
+BF16_PEAK_TFS = 2500.0   # dense bf16 MFMA (spec, no sparsity)
+F32_PEAK_TFS = 157.3     # fp32 MFMA == fp32 vector peak
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="tiny")
+    ap.add_argument("--batch", type=int, default=32, help="clips per GPU")
+    ap.add_argument("--text-len", type=int, default=256)
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-probe", action="store_true", help="skip the live per-kernel event probe")
+    return ap.parse_args()
+
+
+def cpu_baseline(model, cfg_name, budget_s=10.0, max_clips=3):
+    """The oracle (op-for-op CPU restatement of the reference forward, fp32) timed on the host cores
+    on a bounded sample of the same workload: whole 30 s clips through mel + forward + backward at
+    the same config, repeated until `budget_s` of CPU work has been done."""
+    import numpy as np
+
+    from asrx import synth
+    from asrx.config import CONFIGS
+    from oracle import mel as omel
+    from oracle import model as om
+
+    cfg = CONFIGS[cfg_name]
+    P = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+    for k, v in P.items():
+        if v.is_floating_point() and not k.endswith(("running_mean", "running_var")):
+            v.requires_grad_(True)
+    wav = synth.waveform(1, CLIP_SECONDS)
+    pitch = synth.pitch(1)
+    ids, labels = synth.text(1)
+    clips, t_total = 0, 0.0
+    while clips < max_clips and (t_total < budget_s or clips == 0):
+        t0 = time.perf_counter()
+        spec = torch.from_numpy(omel.log_mel(wav[0].numpy().astype(np.float64))).float().unsqueeze(0)
+        wf = torch.from_numpy(omel.waveform_feature(wav[0].numpy())).float().unsqueeze(0)
+        out = om.forward(P, {"dims": cfg.dims, "head": cfg.head, "layer": cfg.layer}, ids, labels,
+                         spectrogram=spec, pitch=pitch, waveform=wf, seed=0, step=clips, dtype=torch.float32)
+        out["loss"].backward()
+        t_total += time.perf_counter() - t0
+        clips += 1
+    return {"value": clips * CLIP_SECONDS / t_total, "unit": "audio-sec/sec", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"{clips} x 30 s clip, {cfg_name} config, T=256, oracle mel + fwd + bwd, fp32, "
+                      f"batch 1, {t_total:.1f} s of CPU time"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from asrx import prec, probe, synth
+    from asrx.config import CONFIGS
+    from asrx.dist import GradSync, broadcast_parameters
+    from asrx.mel import algorithmic_bytes, logmel
+    from asrx.model import Model
+
+    prec.set_precision(args.precision)
+    cfg = CONFIGS[args.config]
+    torch.manual_seed(0)
+    model = Model(cfg).to(dev).train()
+    if world > 1:
+        broadcast_parameters(model)
+    gsync = GradSync(model)
+    model.set_noise(seed=0, step=rank * 1_000_000)
+
+    B = args.batch
+    wav = synth.waveform(B, CLIP_SECONDS, first_seed=1000 + rank * B).to(dev)
+    pitch = synth.pitch(B, first_seed=1000 + rank * B, mask_seed=2000 + rank * B).to(dev)
+    ids, labels = synth.text(B, args.text_len, cfg.tokens, seed=7 + rank)
+    ids, labels = ids.to(dev), labels.to(dev)
+
+    def step():
+        gsync.zero_grad()
+        spec, wfeat = logmel(wav, layout="BMF", pool=True)
+        out = model(labels=labels, text_ids=ids, spectrogram=spec, pitch=pitch, waveform=wfeat.unsqueeze(1))
+        out["loss"].backward()
+        gsync.finish()
+        return out["loss"]
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if not args.no_probe:
+        probe.enable(("gemm", "logmel", "attn"))
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    recs = probe.disable()
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    loss_v = float(loss.item())
+
+    audio_s = world * B * CLIP_SECONDS * args.steps
+    value = audio_s / elapsed
+    result = {
+        "metric": "audio-sec/sec fwd+bwd on 30s@16kHz LibriSpeech-shaped clips (whole job, all GPUs)",
+        "value": round(value, 3),
+        "unit": "audio-sec/sec",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.precision,
+        "data": "synthetic (SURVEY.md §8(d) seeded clips, random-init weights)",
+        "config": {"workload": f"{args.config} (BASELINE configs[1]): log-mel + 4 enc/4 dec d={cfg.dims} "
+                               f"h={cfg.head} fwd+bwd, {B} x 30 s clips per GPU, T={args.text_len}",
+                   "model": args.config, "global_batch": world * B, "seq_len": 3001, "text_len": args.text_len,
+                   "parallelism": f"dp{world}"},
+        "per_gpu": round(value / world, 3),
+        "loss": loss_v,
+    }
+    if recs is not None:
+        n, flops, sec = probe.summarize(recs["gemm"])
+        peak = BF16_PEAK_TFS if args.precision == "bf16" else F32_PEAK_TFS
+        achieved = flops / sec / 1e12 if sec > 0 else 0.0
+        result["roofline"] = {"kernel": "asrx gemm_kernel (MFMA GEMM, all Linear/conv fwd+dgrad+wgrad)",
+                              "bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                              "frac": round(achieved / peak, 4), "traffic": None,
+                              "launches_per_step": n // args.steps,
+                              "share_of_step": round(sec / elapsed, 3)}
+        n2, byts, sec2 = probe.summarize(recs["logmel"])
+        if sec2 > 0:
+            gbs = byts / sec2 / 1e9
+            result["mel_roofline"] = {"kernel": "asrx_logmel (frames + finalize)", "bound": "hbm",
+                                      "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                      "frac": round(gbs / HBM_PEAK_GBS, 4),
+                                      "algorithmic_bytes": algorithmic_bytes(B, wav.shape[1], True),
+                                      "avg_us": round(sec2 / n2 * 1e6, 1)}
+        n3, af, sec3 = probe.summarize(recs["attn"])
+        if sec3 > 0:
+            result["attn_fwd"] = {"achieved": round(af / sec3 / 1e12, 2), "unit": "TFLOP/s",
+                                  "frac": round(af / sec3 / 1e12 / peak, 4), "share_of_step": round(sec3 / elapsed, 3)}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(model, args.config)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -49,6 +49,125 @@ int asrx_gemm(int prec, const float* A, int64_t lda, int64_t sA, int a_kc, int c
               int64_t batch, float alpha, float beta, int act, int64_t conv_F, int64_t conv_C,
               int splitk, asrx_stream_t stream);
 
+
+/* ---- AbbyNormal: essentials.py:140-191 (router SiLU-MLP, cv, gumbel hard decision, avg/max pool of
+ *      x^2 along the feature axis, x / (1 + 1e-4 div)^0.75).  hpre = x @ W1^T + b1 from asrx_gemm.
+ *      Rows are (sample, position, head)-major; noise index ((sid*H+h)*4096+l)*3+k, sid = sid_base + b.
+ *      ys (rows,3) / idx (rows) int32 are saved for backward. ----------------------------------- */
+int asrx_abby_fwd(const float* x, const float* hpre, const float* W2, const float* b2, float* out, float* ys,
+                  int* idx, int64_t rows, int64_t d, int64_t L, int64_t H, int64_t sid_base, uint32_t key,
+                  int use_noise, asrx_stream_t stream);
+/* dx, dhpre overwritten; dW2 (3,d) / db2 (3) accumulated. */
+int asrx_abby_bwd(const float* dout, const float* x, const float* hpre, const float* W2, const float* ys,
+                  const int* idx, float* dx, float* dhpre, float* dW2, float* db2, int64_t rows, int64_t d,
+                  asrx_stream_t stream);
+
+/* ---- attention: F.scaled_dot_product_attention(q,k,v,is_causal) at model.py:307, head dim 64.
+ *      q/k/v/o are (B,L,H,64) with strides sX = int64[3] {batch, seq, head}; lse (B,H,Lq). -------- */
+int asrx_attn_fwd(int prec, const float* q, const int64_t* sq, const float* k, const int64_t* sk, const float* v,
+                  const int64_t* sv, float* o, const int64_t* so, float* lse, int64_t B, int64_t H, int64_t Lq,
+                  int64_t Lk, int64_t hd, int causal, float scale, asrx_stream_t stream);
+/* delta_ws: B*H*Lq floats of workspace. */
+int asrx_attn_bwd(int prec, const float* q, const int64_t* sq, const float* k, const int64_t* sk, const float* v,
+                  const int64_t* sv, const float* o, const int64_t* so, const float* dO, const int64_t* sd,
+                  const float* lse, float* delta_ws, float* dq, const int64_t* sdq, float* dk, const int64_t* sdk,
+                  float* dv, const int64_t* sdv, int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t hd,
+                  int causal, float scale, asrx_stream_t stream);
+
+/* ---- LayerNorm over the last dim: nn.LayerNorm in MSheath (model.py:405, 427) and the channel
+ *      LayerNorm of the encoder (essentials.py:110-113) on channels-last rows. ------------------ */
+int asrx_layernorm_fwd(const float* x, const float* w, const float* b, float* y, float* mean, float* rstd,
+                       int64_t rows, int64_t d, float eps, asrx_stream_t stream);
+int asrx_layernorm_bwd(const float* dy, const float* x, const float* w, const float* mean, const float* rstd,
+                       float* dx, float* dw, float* db, int64_t rows, int64_t d, asrx_stream_t stream);
+
+/* ---- small-N linear (N <= 4): gate / mem_gate / mlp_gate Linear(D,1) (model.py:398, 406, 420),
+ *      v_gate.mlp[2] (341), tgate.cs Linear(D,3) (530), MPNet's Linear(128,3) (381).
+ *      act: 0 none, 3 sigmoid.  Backward: dx = beta*dx + dz W; dW/db accumulated. ------------------ */
+int asrx_small_linear_fwd(const float* x, const float* W, const float* b, float* y, int64_t rows, int64_t K,
+                          int64_t N, int act, asrx_stream_t stream);
+int asrx_small_linear_bwd(const float* dy, const float* y, const float* x, const float* W, float* dx, float* dW,
+                          float* db, int64_t rows, int64_t K, int64_t N, int act, float beta,
+                          asrx_stream_t stream);
+
+/* ---- row L2 norms: torch.norm in rotary (model.py:201), F.normalize in v_gate (347). ---------- */
+int asrx_rownorm(const float* x, float* n, int64_t rows, int64_t d, asrx_stream_t stream);
+int asrx_rownorm_bwd(const float* dn, const float* x, const float* n, float* dx, int64_t rows, int64_t d,
+                     asrx_stream_t stream);
+
+/* ---- rotary (model.py:198-214) fused with the hd^-0.25 pre-scale (303-304); x (B,L,H*hd),
+ *      m[B*L] = |src| rows, f[hd/2] float32 frequencies; dm accumulated in backward. ------------- */
+int asrx_rotary_fwd(const float* x, const float* m, const float* f, float* y, int64_t BL, int64_t L, int64_t D,
+                    int64_t hd, float scale, asrx_stream_t stream);
+int asrx_rotary_bwd(const float* g, const float* x, const float* m, const float* f, float* dx, float* dm,
+                    int64_t BL, int64_t L, int64_t D, int64_t hd, float scale, asrx_stream_t stream);
+
+/* ---- v_gate (model.py:346-351): S = x mkey_n^T, h = mlp[0](x) pre-activation from asrx_gemm. ---- */
+int asrx_vgate_fwd(const float* S, const float* nx, const float* mval, const float* h, const float* w2,
+                   const float* b2, const float* cw, const float* cb, const float* tx, float* ion, float* xval,
+                   float* kv, float* m2, int64_t rows, int64_t M, int64_t Dh, float inv_sqrt_d,
+                   asrx_stream_t stream);
+int asrx_vgate_bwd(const float* dion, const float* S, const float* nx, const float* mval, const float* h,
+                   const float* w2, const float* cw, const float* kv, const float* m2, float* dS, float* dnx,
+                   float* dh, float* dmval, float* dw2, float* db2, float* dcw, float* dcb, int64_t rows, int64_t M,
+                   int64_t Dh, float inv_sqrt_d, asrx_stream_t stream);
+
+/* ---- tgate (model.py:532-535): G = sigmoid(x Wcat^T + b) (rows,3D) from asrx_gemm, c (rows,3). */
+int asrx_tgate_fwd(const float* G, const float* c, float* out, int64_t rows, int64_t D, asrx_stream_t stream);
+int asrx_tgate_bwd(const float* dout, const float* G, const float* c, float* dGz, float* dc, int64_t rows,
+                   int64_t D, asrx_stream_t stream);
+
+/* ---- MSheath updates (model.py:461, 489-505) and reductions ---------------------------------- */
+int asrx_axpy_row(const float* x, const float* s, const float* y, float* out, int64_t rows, int64_t d,
+                  asrx_stream_t stream);
+int asrx_axpy_row_bwd(const float* g, const float* s, const float* y, float* dy, float* ds, int64_t rows,
+                      int64_t d, asrx_stream_t stream);
+int asrx_jump_select(const float* xn, const float* orig, const float* xold, const float* act, const float* alpha,
+                     const float* beta, const float* gam, float* out, int64_t B, int64_t L, int64_t d,
+                     asrx_stream_t stream);
+int asrx_jump_select_bwd(const float* g, const float* xn, const float* orig, const float* act, const float* alpha,
+                         const float* beta, float* dxn, float* dorig, float* dxold, float* dalpha, float* dbeta,
+                         float* dgam, int64_t B, int64_t L, int64_t d, asrx_stream_t stream);
+int asrx_seg_colsum(const float* x, float* out, int64_t B, int64_t L, int64_t d, float scale, int accumulate,
+                    asrx_stream_t stream);
+int asrx_colsum(const float* x, float* out, int64_t rows, int64_t d, asrx_stream_t stream);
+int asrx_add_rows(const float* x, const float* t, const float* u, float* out, int64_t B, int64_t L, int64_t d,
+                  asrx_stream_t stream);
+int asrx_lincomb(const float* x, const float* y, const float* z, float a, float b, float c, float* out, int64_t n,
+                 asrx_stream_t stream);
+/* MSheath policy gumbel noise (model.py:476): out (B, layers, 3). */
+int asrx_policy_noise(float* out, int64_t B, int64_t layers, int64_t sid_base, uint32_t key,
+                      asrx_stream_t stream);
+
+/* ---- encoder elementwise / conv pieces (model.py:93-147), channels-last (B, T, C) ------------- */
+int asrx_act_fwd(const float* x, float* y, int64_t n, int act, asrx_stream_t stream);
+int asrx_act_bwd(const float* g, const float* x, float* dx, int64_t n, int act, asrx_stream_t stream);
+int asrx_glu_fwd(const float* x, float* y, int64_t rows, int64_t C, asrx_stream_t stream);
+int asrx_glu_bwd(const float* g, const float* x, float* dx, int64_t rows, int64_t C, asrx_stream_t stream);
+int asrx_dropout(const float* x, float* y, int64_t B, int64_t T, int64_t C, int64_t sid_base, uint32_t key,
+                 float p, asrx_stream_t stream);
+int asrx_dwconv_fwd(const float* x, const float* w, const float* b, float* y, int64_t B, int64_t T, int64_t C,
+                    int64_t K, asrx_stream_t stream);
+int asrx_dwconv_bwd(const float* g, const float* x, const float* w, float* dx, float* dw, float* db, int64_t B,
+                    int64_t T, int64_t C, int64_t K, asrx_stream_t stream);
+int asrx_bn_fwd(const float* x, const float* w, const float* b, float* y, float* mean, float* rstd, int64_t B,
+                int64_t T, int64_t C, float eps, int use_batch_stats, asrx_stream_t stream);
+int asrx_bn_bwd(const float* g, const float* x, const float* mean, const float* rstd, const float* w, float* sg_ws,
+                float* sgx_ws, float* dx, float* dw, float* db, int64_t B, int64_t T, int64_t C,
+                asrx_stream_t stream);
+int asrx_stem1_fwd(const float* x, const float* W, const float* bias, float* y, int64_t B, int64_t T, int64_t D,
+                   asrx_stream_t stream);
+int asrx_stem1_bwd(const float* g, const float* x, float* dW, float* db, int64_t B, int64_t T, int64_t D,
+                   asrx_stream_t stream);
+
+/* ---- token embedding (model.py:592, 606) and tied-logits cross entropy (model.py:629, 670) ---- */
+int asrx_embed_fwd(const int64_t* ids, const float* E, float* y, int64_t rows, int64_t d, asrx_stream_t stream);
+int asrx_embed_bwd(const int64_t* ids, const float* g, float* dE, int64_t rows, int64_t d, asrx_stream_t stream);
+int asrx_ce_fwd(const float* z, const int64_t* labels, float* loss, float* lse, int64_t rows, int64_t V,
+                asrx_stream_t stream);
+int asrx_ce_bwd(const float* z, const int64_t* labels, const float* lse, const float* scale, float* dz,
+                int64_t rows, int64_t V, asrx_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

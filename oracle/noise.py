@@ -31,9 +31,9 @@ def hash32(key: int, idx):
 
 
 def uniform(key: int, idx):
-    """u in (0, 1): ((h >> 8) + 0.5) / 2^24, computed in float32 like the device."""
+    """u in [2^-24, 1 - 2^-24]: ((h >> 9) + 0.5) / 2^23, computed in float32 like the device."""
     h = hash32(key, idx)
-    return ((h >> np.uint32(8)).astype(np.float32) + np.float32(0.5)) * np.float32(1.0 / 16777216.0)
+    return ((h >> np.uint32(9)).astype(np.float32) + np.float32(0.5)) * np.float32(1.0 / 8388608.0)
 
 
 def gumbel(key: int, idx):

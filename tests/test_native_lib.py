@@ -52,3 +52,16 @@ def test_mel_frames():
     L = lib.load()
     assert L.asrx_mel_frames(480000) == 3001
     assert L.asrx_mel_frames(16000) == 101
+
+
+def test_noise_uniform_never_hits_0_or_1():
+    import numpy as np
+
+    from oracle import noise
+
+    # the extreme hash values map strictly inside (0, 1) in float32, so gumbel noise stays finite
+    h = np.array([0, 0xFFFFFFFF], dtype=np.uint32)
+    u = ((h >> np.uint32(9)).astype(np.float32) + np.float32(0.5)) * np.float32(1.0 / 8388608.0)
+    assert u[0] > 0 and u[1] < 1
+    g = noise.gumbel(12345, np.arange(1 << 20, dtype=np.uint64))
+    assert np.all(np.isfinite(g))
