@@ -14,10 +14,13 @@
 //            v_mfma_f32_16x16x32_bf16 (fp32 accumulate)          — the perf mode;
 // PREC_F32:  exact fp32 v_mfma_f32_16x16x4_f32                    — the parity mode.
 //
-// Tiling: 128x128 block tile, 256 threads = 4 waves (2x2), 64x64 per wave = 4x4 MFMA 16x16 tiles.
-// Register-staged double buffering: the next K-tile's global loads are issued before the MFMAs
-// of the current one and written to the other LDS buffer after them.
+// Tiling: 128x128 block tile, 256 threads = 4 waves (2x2), 64x64 per wave = 4x4 MFMA 16x16 tiles,
+// BK = 32.  fp32 tiles stream HBM -> LDS by LDS-DMA (global_load_lds_dwordx4, 8 x 1 KB per wave per
+// stage) into a 3-stage ring; a counted s_waitcnt vmcnt + raw s_barrier per K-step keeps the next
+// stage's DMA in flight under the current stage's MFMAs.  Fragments are read from the swizzled fp32
+// images and rounded to bf16 in registers.  Tail / conv-padding lanes read a zero page.
 #include "common.h"
+#include <cstdlib>
 
 namespace asrx {
 
@@ -42,136 +45,150 @@ struct GemmParams {
   int64_t kchunk;
 };
 
-constexpr int BM = 128, BN = 128, NTHR = 256;
+constexpr int BM = 128, BN = 128, NTHR = 256, BK = 32;
+constexpr int TILE_BYTES = 128 * BK * 4;                 // one fp32 operand tile per stage (16 KB)
+constexpr int STAGE_BYTES = 2 * TILE_BYTES;              // A + B
+constexpr int GLDS_PER_WAVE = 2 * TILE_BYTES / 1024 / 4; // 1-KB LDS-DMA pieces per wave per stage (8)
 
-template <int PREC>
-struct GemmCfg;
-template <>
-struct GemmCfg<PREC_BF16> {
-  static constexpr int BK = 64;
-  static constexpr int LDS_STRIDE = BK + 8;  // bf16 elements per LDS row (144 B)
-  typedef unsigned short T;
-};
-template <>
-struct GemmCfg<PREC_F32> {
-  static constexpr int BK = 32;
-  static constexpr int LDS_STRIDE = BK + 2;  // floats per LDS row (conflict-free b32 reads)
-  typedef float T;
+__device__ __attribute__((aligned(16))) float g_zero_page[4];  // source of zero-filled tile lanes
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef const __attribute__((address_space(1))) void gbl_void;
+
+// ---------------------------------------------------------------------------------------------
+// LDS images (fp32, unpadded, written lane-linearly by global_load_lds_dwordx4; the swizzles are
+// applied to the per-lane SOURCE address and undone on the read, see cdna_hip_programming.md
+// rule 21):
+//   K-contiguous operand: [128 rows][32 k]   row = 128 B = 8 chunks of 16 B; chunk c of row r is
+//     stored at position c ^ ((r >> 1) & 7)  -> the 16 lanes of a fragment read hit 16 slots.
+//   MN-contiguous operand: [32 k][128 rows]  k-row = 512 B = 32 chunks; chunk c of k-row kr is
+//     stored at c ^ (((kr >> 3) & 1) << 2)   -> the two 16-lane halves of a b32 read differ.
+// ---------------------------------------------------------------------------------------------
+// Per-lane LDS-DMA issue state for one operand: everything that does not change along K is
+// computed once.  Element offsets are 32-bit (the host checks every operand spans < 2^31 elements).
+template <bool KC, bool CONV>
+struct Stager {
+  const float* base;
+  int ld;
+  uint32_t off[4];  // KC: row * ld + 4c ; !KC: row0 + 4c   (k contribution added per stage)
+  int kk[4];        // KC: 4c (k within the tile) ; !KC: k-row within the tile
+  int cpos[4];      // CONV: KC: row % F ; !KC: column / C (tap)
+  bool rok[4];
+
+  __device__ __forceinline__ void init(const GemmOperand& op, int r0, int R, int convF, int convC) {
+    base = op.p;
+    ld = (int)op.ld;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = wid * 4 + i;  // 1-KB piece index within the 16-KB tile
+      if (KC) {
+        const int row = 8 * q + (lane >> 3);
+        const int c = (lane & 7) ^ ((row >> 1) & 7);
+        const int r = r0 + row;
+        rok[i] = r < R;
+        off[i] = (uint32_t)r * (uint32_t)ld + 4 * c;
+        kk[i] = 4 * c;
+        cpos[i] = CONV ? r % convF : 0;
+      } else {
+        const int kr = 2 * q + (lane >> 5);
+        const int c = (lane & 31) ^ (((kr >> 3) & 1) << 2);
+        const int r = r0 + 4 * c;
+        rok[i] = r < R;
+        off[i] = (uint32_t)r;
+        kk[i] = kr;
+        cpos[i] = CONV ? r / convC : 0;
+      }
+    }
+  }
+
+  __device__ __forceinline__ void issue(char* lds_tile, int k0, int K, int convF, int convC) const {
+    const int wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = k0 + kk[i];
+      bool ok = rok[i] && k < K;
+      uint32_t o = KC ? off[i] + (uint32_t)k0 : off[i] + (uint32_t)k * (uint32_t)ld;
+      if (CONV) {
+        const int pos = KC ? cpos[i] + (k0 + kk[i]) / convC - 1 : (k % convF) + cpos[i] - 1;
+        ok = ok && pos >= 0 && pos < convF;
+        o -= (uint32_t)convC;
+      }
+      const float* src = ok ? base + o : g_zero_page;
+      __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(lds_tile + (wid * 4 + i) * 1024), 16, 0, 0);
+    }
+  }
 };
 
-__device__ __forceinline__ unsigned short f2bf(float f) {
-  __bf16 h = (__bf16)f;
-  return __builtin_bit_cast(unsigned short, h);
+// 8 consecutive k (k = kb .. kb+7) of tile row r, as fp32.
+template <bool KC>
+__device__ __forceinline__ void read8(const char* tile, int r, int kb, float (&o)[8]) {
+  if (KC) {
+    const int sw = (r >> 1) & 7;
+    const char* row = tile + r * 128;
+    const float4 x = *reinterpret_cast<const float4*>(row + 16 * ((kb >> 2) ^ sw));
+    const float4 y = *reinterpret_cast<const float4*>(row + 16 * (((kb >> 2) + 1) ^ sw));
+    o[0] = x.x; o[1] = x.y; o[2] = x.z; o[3] = x.w;
+    o[4] = y.x; o[5] = y.y; o[6] = y.z; o[7] = y.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = kb + j;
+      const int c = (r >> 2) ^ (((k >> 3) & 1) << 2);
+      o[j] = *reinterpret_cast<const float*>(tile + k * 512 + 16 * c + 4 * (r & 3));
+    }
+  }
 }
 
-// Tile loader for one operand (ROWS x BK tile, ROWS = BM or BN).
-//   KC: element (r, k) at p[r*ld + k]     (float4 along k)
-//   !KC: element (r, k) at p[k*ld + r]    (float4 along r)
-template <int PREC, bool KC, int ROWS>
-struct TileLoader {
-  static constexpr int BK = GemmCfg<PREC>::BK;
-  static constexpr int NV = ROWS * BK / 4 / NTHR;  // float4 per thread
-  float4 v[NV];
-
-  __device__ __forceinline__ void load(const GemmOperand& op, int64_t r0, int64_t k0, int64_t R,
-                                       int64_t K, int64_t convF, int64_t convC) {
-    const int t = threadIdx.x;
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int q = t + NTHR * i;
-      int64_t r, k;
-      if (KC) {
-        r = r0 + q / (BK / 4);
-        k = k0 + 4 * (q % (BK / 4));
-      } else {
-        k = k0 + q / (ROWS / 4);
-        r = r0 + 4 * (q % (ROWS / 4));
-      }
-      bool ok = (r < R) && (k < K);
-      int64_t off = KC ? (r * op.ld + k) : (k * op.ld + r);
-      if (op.conv) {
-        // spatial index s: the row for KC (A of a conv fwd), the k index for !KC (B of a wgrad);
-        // channel index c: the other one.
-        const int64_t s = KC ? r : k;
-        const int64_t c = KC ? k : r;
-        const int64_t pos = (s % convF) + c / convC - 1;
-        ok = ok && pos >= 0 && pos < convF;
-        off -= convC;
-      }
-      if (ok) {
-        v[i] = *reinterpret_cast<const float4*>(op.p + off);
-      } else {
-        v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-    }
+template <bool KC>
+__device__ __forceinline__ float read1(const char* tile, int r, int k) {
+  if (KC) {
+    return *reinterpret_cast<const float*>(tile + r * 128 + 16 * ((k >> 2) ^ ((r >> 1) & 7)) + 4 * (k & 3));
+  } else {
+    const int c = (r >> 2) ^ (((k >> 3) & 1) << 2);
+    return *reinterpret_cast<const float*>(tile + k * 512 + 16 * c + 4 * (r & 3));
   }
+}
 
-  __device__ __forceinline__ void store(typename GemmCfg<PREC>::T* lds) const {
-    constexpr int S = GemmCfg<PREC>::LDS_STRIDE;
-    const int t = threadIdx.x;
+__device__ __forceinline__ bf16x8 to_bf16x8(const float (&f)[8]) {
+  bf16x8 r;
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int q = t + NTHR * i;
-      if (KC) {
-        const int r = q / (BK / 4), k = 4 * (q % (BK / 4));
-        if constexpr (PREC == PREC_BF16) {
-          ushort4 h = make_ushort4(f2bf(v[i].x), f2bf(v[i].y), f2bf(v[i].z), f2bf(v[i].w));
-          *reinterpret_cast<ushort4*>(lds + r * S + k) = h;
-        } else {
-          float* d = lds + r * S + k;
-          *reinterpret_cast<float2*>(d) = make_float2(v[i].x, v[i].y);
-          *reinterpret_cast<float2*>(d + 2) = make_float2(v[i].z, v[i].w);
-        }
-      } else {
-        const int k = q / (ROWS / 4), r = 4 * (q % (ROWS / 4));
-        if constexpr (PREC == PREC_BF16) {
-          lds[(r + 0) * S + k] = f2bf(v[i].x);
-          lds[(r + 1) * S + k] = f2bf(v[i].y);
-          lds[(r + 2) * S + k] = f2bf(v[i].z);
-          lds[(r + 3) * S + k] = f2bf(v[i].w);
-        } else {
-          lds[(r + 0) * S + k] = v[i].x;
-          lds[(r + 1) * S + k] = v[i].y;
-          lds[(r + 2) * S + k] = v[i].z;
-          lds[(r + 3) * S + k] = v[i].w;
-        }
-      }
-    }
-  }
-};
+  for (int j = 0; j < 8; ++j) r[j] = (__bf16)f[j];
+  return r;
+}
 
-// acc[mt][nt] += As[wave rows][BK] * Bs[wave cols][BK]^T for one K-tile.
-template <int PREC>
-__device__ __forceinline__ void mma_tile(f32x4 (&acc)[4][4], const typename GemmCfg<PREC>::T* As,
-                                         const typename GemmCfg<PREC>::T* Bs, int wm, int wn) {
-  constexpr int S = GemmCfg<PREC>::LDS_STRIDE;
-  constexpr int BK = GemmCfg<PREC>::BK;
+// acc[mt][nt] += A(wave rows, 32 k) * B(wave cols, 32 k)^T from one stage.
+template <int PREC, bool A_KC, bool B_KC>
+__device__ __forceinline__ void mma_stage(f32x4 (&acc)[4][4], const char* At, const char* Bt, int wm, int wn) {
   const int lane = threadIdx.x & 63;
   const int lr = lane & 15, lk = lane >> 4;
   if constexpr (PREC == PREC_BF16) {
+    bf16x8 a[4], b[4];
 #pragma unroll
-    for (int ks = 0; ks < BK / 32; ++ks) {
-      bf16x8 a[4], b[4];
+    for (int mt = 0; mt < 4; ++mt) {
+      float f[8];
+      read8<A_KC>(At, wm * 64 + mt * 16 + lr, 8 * lk, f);
+      a[mt] = to_bf16x8(f);
+    }
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-        a[mt] = *reinterpret_cast<const bf16x8*>(As + (wm * 64 + mt * 16 + lr) * S + ks * 32 + 8 * lk);
+    for (int nt = 0; nt < 4; ++nt) {
+      float f[8];
+      read8<B_KC>(Bt, wn * 64 + nt * 16 + lr, 8 * lk, f);
+      b[nt] = to_bf16x8(f);
+    }
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt)
-        b[nt] = *reinterpret_cast<const bf16x8*>(Bs + (wn * 64 + nt * 16 + lr) * S + ks * 32 + 8 * lk);
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt)
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt], b[nt], acc[mt][nt], 0, 0, 0);
-    }
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt], b[nt], acc[mt][nt], 0, 0, 0);
   } else {
 #pragma unroll
     for (int ks = 0; ks < BK / 4; ++ks) {
       float a[4], b[4];
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) a[mt] = As[(wm * 64 + mt * 16 + lr) * S + ks * 4 + lk];
+      for (int mt = 0; mt < 4; ++mt) a[mt] = read1<A_KC>(At, wm * 64 + mt * 16 + lr, ks * 4 + lk);
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) b[nt] = Bs[(wn * 64 + nt * 16 + lr) * S + ks * 4 + lk];
+      for (int nt = 0; nt < 4; ++nt) b[nt] = read1<B_KC>(Bt, wn * 64 + nt * 16 + lr, ks * 4 + lk);
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
@@ -181,16 +198,33 @@ __device__ __forceinline__ void mma_tile(f32x4 (&acc)[4][4], const typename Gemm
   }
 }
 
-template <int PREC, bool A_KC, bool B_KC>
-__global__ __launch_bounds__(NTHR) void gemm_kernel(GemmParams p) {
-  typedef typename GemmCfg<PREC>::T T;
-  constexpr int BK = GemmCfg<PREC>::BK;
-  constexpr int S = GemmCfg<PREC>::LDS_STRIDE;
-  __shared__ __attribute__((aligned(16))) T lds[2][(BM + BN) * S];
+// Workgroup -> output tile.  Blocks b and b+8 share an XCD (round-robin dispatch), so the remap
+// hands each XCD a contiguous run of tiles; tiles are ordered N-fastest, so the N-tiles that re-read
+// one A row panel run on the same XCD at about the same time and hit its L2.  (Speed only.)
+__device__ __forceinline__ void tile_of(int bid, int nblk, int nN, int& tm, int& tn) {
+  const int xcd = bid & 7, q = nblk >> 3, r = nblk & 7;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  tn = wg % nN;
+  tm = wg / nN;
+}
 
-  const int64_t n0 = (int64_t)blockIdx.x * BN;
-  const int64_t m0 = (int64_t)blockIdx.y * BM;
-  const int z = blockIdx.z;
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+}
+
+template <int PREC, bool A_KC, bool B_KC, bool CA, bool CB, int NSTAGE>
+__global__ __launch_bounds__(NTHR, 1) void gemm_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // NSTAGE x [A tile | B tile]
+
+  const int nN = (int)((p.N + BN - 1) / BN);
+  int tm, tn;
+  tile_of(blockIdx.x, gridDim.x, nN, tm, tn);
+  const int n0 = tn * BN;
+  const int m0 = tm * BM;
+  const int z = blockIdx.y;
   const int batch = z / p.splitk, split = z % p.splitk;
   const int64_t kbeg = (int64_t)split * p.kchunk;
   const int64_t kend = min(p.K, kbeg + p.kchunk);
@@ -200,6 +234,8 @@ __global__ __launch_bounds__(NTHR) void gemm_kernel(GemmParams p) {
   b.p += batch * b.bstride;
   float* C = p.c + batch * p.sC;
   float* Z = p.z ? p.z + batch * p.sC : nullptr;
+  const int M = (int)p.M, N = (int)p.N;
+  const int convF = (int)p.convF, convC = (int)p.convC;
 
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wm = wid >> 1, wn = wid & 1;
@@ -210,31 +246,38 @@ __global__ __launch_bounds__(NTHR) void gemm_kernel(GemmParams p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  TileLoader<PREC, A_KC, BM> la;
-  TileLoader<PREC, B_KC, BN> lb;
-  const int64_t nk = (kend - kbeg + BK - 1) / BK;
-  if (nk > 0) {
-    la.load(a, m0, kbeg, p.M, kend, p.convF, p.convC);
-    lb.load(b, n0, kbeg, p.N, kend, p.convF, p.convC);
-    la.store(lds[0]);
-    lb.store(lds[0] + BM * S);
-    __syncthreads();
-  }
-  int cur = 0;
-  for (int64_t kt = 0; kt < nk; ++kt) {
-    const bool more = kt + 1 < nk;
-    if (more) {
-      la.load(a, m0, kbeg + (kt + 1) * BK, p.M, kend, p.convF, p.convC);
-      lb.load(b, n0, kbeg + (kt + 1) * BK, p.N, kend, p.convF, p.convC);
+  const int nk = (int)((kend - kbeg + BK - 1) / BK);
+  const int kb0 = (int)kbeg, kE = (int)kend;
+  Stager<A_KC, CA> sa;
+  Stager<B_KC, CB> sb;
+  sa.init(a, m0, M, convF, convC);
+  sb.init(b, n0, N, convF, convC);
+  // prologue: stages 0 .. NSTAGE-2
+#pragma unroll
+  for (int s = 0; s < NSTAGE - 1; ++s) {
+    if (s < nk) {
+      char* st = smem + s * STAGE_BYTES;
+      sa.issue(st, kb0 + s * BK, kE, convF, convC);
+      sb.issue(st + TILE_BYTES, kb0 + s * BK, kE, convF, convC);
     }
-    mma_tile<PREC>(acc, lds[cur], lds[cur] + BM * S, wm, wn);
-    if (more) {
-      la.store(lds[cur ^ 1]);
-      lb.store(lds[cur ^ 1] + BM * S);
-    }
-    __syncthreads();
-    cur ^= 1;
   }
+  for (int kt = 0; kt < nk; ++kt) {
+    // stage kt must have landed: leave the younger stages (issued after it) in flight
+    const int younger = min(kt + NSTAGE - 1, nk) - kt - 1;
+    if (younger >= 1) wait_vm<GLDS_PER_WAVE>();
+    else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int nxt = kt + NSTAGE - 1;
+    if (nxt < nk) {  // refill the slot every wave finished reading before this barrier
+      char* st = smem + (nxt % NSTAGE) * STAGE_BYTES;
+      sa.issue(st, kb0 + nxt * BK, kE, convF, convC);
+      sb.issue(st + TILE_BYTES, kb0 + nxt * BK, kE, convF, convC);
+    }
+    const char* st = smem + (kt % NSTAGE) * STAGE_BYTES;
+    mma_stage<PREC, A_KC, B_KC>(acc, st, st + TILE_BYTES, wm, wn);
+  }
+  wait_vm<0>();
 
   // epilogue: C/D map of 16x16 MFMA: col = lane & 15, row = (lane >> 4) * 4 + r
   const int lc = lane & 15, lr4 = (lane >> 4) * 4;
@@ -242,20 +285,20 @@ __global__ __launch_bounds__(NTHR) void gemm_kernel(GemmParams p) {
   for (int mt = 0; mt < 4; ++mt) {
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
-      const int64_t col = n0 + wn * 64 + nt * 16 + lc;
-      if (col >= p.N) continue;
+      const int col = n0 + wn * 64 + nt * 16 + lc;
+      if (col >= N) continue;
       const float bv = (p.bias && split == 0) ? p.bias[col] : 0.f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int64_t row = m0 + wm * 64 + mt * 16 + lr4 + r;
-        if (row >= p.M) continue;
-        float* dst = C + row * p.ldc + col;
+        const int row = m0 + wm * 64 + mt * 16 + lr4 + r;
+        if (row >= M) continue;
+        float* dst = C + (int64_t)row * p.ldc + col;
         float v = p.alpha * acc[mt][nt][r] + bv;
         if (p.splitk > 1) {
           atomicAdd(dst, v);
         } else {
           if (p.beta != 0.f) v += p.beta * *dst;
-          if (Z) Z[row * p.ldc + col] = v;
+          if (Z) Z[(int64_t)row * p.ldc + col] = v;
           *dst = apply_act(p.act, v);
         }
       }
@@ -263,12 +306,38 @@ __global__ __launch_bounds__(NTHR) void gemm_kernel(GemmParams p) {
   }
 }
 
+static int g_stages = 0;  // 2 or 3 (ASRX_GEMM_STAGES, default 2)
+
+template <int PREC, bool AK, bool BKC, bool CA, bool CB, int NS>
+static void launch_ns(const GemmParams& p, dim3 g, hipStream_t s) {
+  static bool attr_set = false;  // benign race: idempotent attribute
+  const int shm = NS * STAGE_BYTES;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)gemm_kernel<PREC, AK, BKC, CA, CB, NS>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, shm);
+    attr_set = true;
+  }
+  gemm_kernel<PREC, AK, BKC, CA, CB, NS><<<g, NTHR, shm, s>>>(p);
+}
+
+template <int PREC, bool AK, bool BKC, bool CA, bool CB>
+static void launch_one(const GemmParams& p, dim3 g, hipStream_t s) {
+  if (g_stages == 0) {
+    const char* e = getenv("ASRX_GEMM_STAGES");
+    g_stages = (e && atoi(e) == 3) ? 3 : 2;
+  }
+  if (g_stages == 3) launch_ns<PREC, AK, BKC, CA, CB, 3>(p, g, s);
+  else launch_ns<PREC, AK, BKC, CA, CB, 2>(p, g, s);
+}
+
 template <int PREC>
-static void launch_prec(const GemmParams& p, bool akc, bool bkc, dim3 g, hipStream_t s) {
-  if (akc && bkc) gemm_kernel<PREC, true, true><<<g, NTHR, 0, s>>>(p);
-  else if (akc && !bkc) gemm_kernel<PREC, true, false><<<g, NTHR, 0, s>>>(p);
-  else if (!akc && bkc) gemm_kernel<PREC, false, true><<<g, NTHR, 0, s>>>(p);
-  else gemm_kernel<PREC, false, false><<<g, NTHR, 0, s>>>(p);
+static void launch_prec(const GemmParams& p, bool akc, bool bkc, bool ca, bool cb, dim3 g, hipStream_t s) {
+  if (ca) launch_one<PREC, true, true, true, false>(p, g, s);        // k3 conv fwd / dgrad
+  else if (cb) launch_one<PREC, false, false, false, true>(p, g, s); // k3 conv wgrad
+  else if (akc && bkc) launch_one<PREC, true, true, false, false>(p, g, s);
+  else if (akc && !bkc) launch_one<PREC, true, false, false, false>(p, g, s);
+  else if (!akc && bkc) launch_one<PREC, false, true, false, false>(p, g, s);
+  else launch_one<PREC, false, false, false, false>(p, g, s);
 }
 
 }  // namespace asrx
@@ -286,6 +355,7 @@ extern "C" int asrx_gemm(int prec, const float* A, int64_t lda, int64_t sA, int 
   ASRX_REQUIRE(M > 0 && N > 0 && K > 0 && batch > 0, "asrx_gemm: empty problem M=%ld N=%ld K=%ld",
                (long)M, (long)N, (long)K);
   ASRX_REQUIRE(aligned16(A) && aligned16(B), "asrx_gemm: A/B must be 16-byte aligned");
+  ASRX_REQUIRE(!conv_a || (conv_F < (1LL << 30)), "asrx_gemm: conv segment too long");
   ASRX_REQUIRE(lda % 4 == 0 && ldb % 4 == 0, "asrx_gemm: lda/ldb must be multiples of 4");
   ASRX_REQUIRE(a_kc ? (K % 4 == 0) : (M % 4 == 0), "asrx_gemm: A vector dim must be a multiple of 4");
   ASRX_REQUIRE(b_kc ? (K % 4 == 0) : (N % 4 == 0), "asrx_gemm: B vector dim must be a multiple of 4");
@@ -313,16 +383,24 @@ extern "C" int asrx_gemm(int prec, const float* A, int64_t lda, int64_t sA, int 
   p.alpha = alpha;
   p.beta = beta;
   p.act = act;
-  const int BK = prec == PREC_BF16 ? GemmCfg<PREC_BF16>::BK : GemmCfg<PREC_F32>::BK;
   int64_t kchunk = (K + splitk - 1) / splitk;
   kchunk = (kchunk + BK - 1) / BK * BK;
   splitk = (int)((K + kchunk - 1) / kchunk);
   p.splitk = splitk;
   p.kchunk = kchunk;
   ASRX_REQUIRE(batch * splitk < 65536, "asrx_gemm: batch*splitk too large");
-  dim3 g((unsigned)((N + BN - 1) / BN), (unsigned)((M + BM - 1) / BM), (unsigned)(batch * splitk));
-  ASRX_REQUIRE(g.y < 65536u, "asrx_gemm: M too large for grid.y");
-  if (prec == PREC_BF16) launch_prec<PREC_BF16>(p, a_kc, b_kc, g, stream);
-  else launch_prec<PREC_F32>(p, a_kc, b_kc, g, stream);
+  ASRX_REQUIRE(M < (1LL << 31) && N < (1LL << 31), "asrx_gemm: M/N must fit int32");
+  const int64_t tiles = ((N + BN - 1) / BN) * ((M + BM - 1) / BM);
+  ASRX_REQUIRE(tiles < (1LL << 31), "asrx_gemm: too many tiles");
+  dim3 g((unsigned)tiles, (unsigned)(batch * splitk));
+  ASRX_REQUIRE(!conv_a || b_kc, "asrx_gemm: conv fwd needs a K-contiguous B");
+  ASRX_REQUIRE(!conv_b || !a_kc, "asrx_gemm: conv wgrad needs an M-contiguous A");
+  ASRX_REQUIRE(!(conv_a && conv_b), "asrx_gemm: one implicit im2col operand at most");
+  // 32-bit element offsets inside each operand
+  const int64_t spanA = a_kc ? M * lda : K * lda, spanB = b_kc ? N * ldb : K * ldb;
+  ASRX_REQUIRE(spanA < (1LL << 31) && spanB < (1LL << 31) && K < (1LL << 31),
+               "asrx_gemm: operand spans >= 2^31 elements");
+  if (prec == PREC_BF16) launch_prec<PREC_BF16>(p, a_kc, b_kc, conv_a, conv_b, g, stream);
+  else launch_prec<PREC_F32>(p, a_kc, b_kc, conv_a, conv_b, g, stream);
   ASRX_LAUNCHED("asrx_gemm");
 }
