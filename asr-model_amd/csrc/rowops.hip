@@ -499,24 +499,24 @@ __global__ __launch_bounds__(256) void jump_select_bwd_kernel(
   }
 }
 
-// Per-sample column sums: out[b, c] = scale * sum_l x[b, l, c]  (x.mean(dim=1), model.py:435, 463;
-// BatchNorm / bias reductions).  grid (ceil(d/64), B), 4 waves split L.
+// Per-sample column sums: out[b, c] (+)= scale * sum_l x[b, l, c]  (x.mean(dim=1), model.py:435, 463).
+// grid (ceil(d/64), B, chunks of L); each workgroup reduces a 64-column x chunk slab with float
+// atomics into `out` (zeroed by the launcher unless accumulating).
 __global__ __launch_bounds__(256) void seg_colsum_kernel(const float* __restrict__ x, float* __restrict__ out,
-                                                         int64_t L, int d, float scale, int accumulate) {
+                                                         int64_t L, int d, float scale, int64_t chunk) {
   __shared__ float red[4][64];
   const int b = blockIdx.y;
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int part = threadIdx.x >> 6;
+  const int64_t l0 = (int64_t)blockIdx.z * chunk, l1 = min(L, l0 + chunk);
   float s = 0.f;
   if (c < d)
-    for (int64_t l = part; l < L; l += 4) s += x[((int64_t)b * L + l) * d + c];
+    for (int64_t l = l0 + part; l < l1; l += 4) s += x[((int64_t)b * L + l) * d + c];
   red[part][threadIdx.x & 63] = s;
   __syncthreads();
   if (part == 0 && c < d) {
     const int t = threadIdx.x;
-    const float v = (red[0][t] + red[1][t] + red[2][t] + red[3][t]) * scale;
-    if (accumulate) out[(int64_t)b * d + c] += v;
-    else out[(int64_t)b * d + c] = v;
+    atomicAdd(out + (int64_t)b * d + c, (red[0][t] + red[1][t] + red[2][t] + red[3][t]) * scale);
   }
 }
 
@@ -1068,8 +1068,10 @@ int asrx_jump_select_bwd(const float* g, const float* xn, const float* orig, con
 int asrx_seg_colsum(const float* x, float* out, int64_t B, int64_t L, int64_t d, float scale, int accumulate,
                     hipStream_t stream) {
   if (B == 0) return 0;
-  dim3 grid((unsigned)((d + 63) / 64), (unsigned)B);
-  seg_colsum_kernel<<<grid, 256, 0, stream>>>(x, out, L, (int)d, scale, accumulate);
+  if (!accumulate) hipMemsetAsync(out, 0, (size_t)B * d * sizeof(float), stream);
+  const int64_t chunk = 64;
+  dim3 grid((unsigned)((d + 63) / 64), (unsigned)B, (unsigned)((L + chunk - 1) / chunk));
+  seg_colsum_kernel<<<grid, 256, 0, stream>>>(x, out, L, (int)d, scale, chunk);
   ASRX_LAUNCHED("asrx_seg_colsum");
 }
 

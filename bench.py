@@ -40,6 +40,8 @@ def parse():
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true", help="skip the live per-kernel event probe")
+    ap.add_argument("--eager", action="store_true", help="launch every kernel from Python instead of replaying "
+                    "the captured HIP graph of the step")
     return ap.parse_args()
 
 
@@ -119,22 +121,44 @@ def main():
         gsync.finish()
         return out["loss"]
 
-    for _ in range(args.warmup):
-        step()
+    use_graph = not args.eager and world == 1
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):  # warmup off the default stream (graph-capture requirement)
+        for _ in range(max(args.warmup, 1 if use_graph else 0)):
+            step()
+    torch.cuda.current_stream().wait_stream(side)
     torch.cuda.synchronize()
-    if not args.no_probe:
+    graph = None
+    if use_graph:
+        # One training step -> one HIP graph: every launch (kernels, memsets, events of the probe) is
+        # recorded once and replayed, so the host cost per step is one graphLaunch.  All control
+        # flow of the step is on device (masked MSheath, no host syncs), so the replay is the step.
+        if not args.no_probe:
+            probe.enable(("gemm", "logmel", "attn"))
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            loss = step()
+        recs = probe.disable()
+        torch.cuda.synchronize()
+    elif not args.no_probe:
         probe.enable(("gemm", "logmel", "attn"))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss = step()
+        if graph is not None:
+            graph.replay()
+        else:
+            loss = step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    recs = probe.disable()
+    if graph is None:
+        recs = probe.disable()
+    probe_steps = 1 if graph is not None else args.steps  # captured events hold the last replay
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -170,8 +194,9 @@ def main():
         result["roofline"] = {"kernel": "asrx gemm_kernel (MFMA GEMM, all Linear/conv fwd+dgrad+wgrad)",
                               "bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                               "frac": round(achieved / peak, 4), "traffic": None,
-                              "launches_per_step": n // args.steps,
-                              "share_of_step": round(sec / elapsed, 3)}
+                              "launches_per_step": n // probe_steps,
+                              "avg_us": round(sec / max(n, 1) * 1e6, 2),
+                              "share_of_step": round(sec / probe_steps / (elapsed / args.steps), 3)}
         n2, byts, sec2 = probe.summarize(recs["logmel"])
         if sec2 > 0:
             gbs = byts / sec2 / 1e9
@@ -183,7 +208,9 @@ def main():
         n3, af, sec3 = probe.summarize(recs["attn"])
         if sec3 > 0:
             result["attn_fwd"] = {"achieved": round(af / sec3 / 1e12, 2), "unit": "TFLOP/s",
-                                  "frac": round(af / sec3 / 1e12 / peak, 4), "share_of_step": round(sec3 / elapsed, 3)}
+                                  "frac": round(af / sec3 / 1e12 / peak, 4),
+                                  "share_of_step": round(sec3 / probe_steps / (elapsed / args.steps), 3)}
+    result["launch"] = "hip-graph replay" if graph is not None else "eager"
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(model, args.config)
     if world > 1:
