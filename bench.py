@@ -134,12 +134,9 @@ def main():
         # One training step -> one HIP graph: every launch (kernels, memsets, events of the probe) is
         # recorded once and replayed, so the host cost per step is one graphLaunch.  All control
         # flow of the step is on device (masked MSheath, no host syncs), so the replay is the step.
-        if not args.no_probe:
-            probe.enable(("gemm", "logmel", "attn"))
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             loss = step()
-        recs = probe.disable()
         torch.cuda.synchronize()
     elif not args.no_probe:
         probe.enable(("gemm", "logmel", "attn"))
@@ -158,7 +155,17 @@ def main():
     elapsed = time.perf_counter() - t0
     if graph is None:
         recs = probe.disable()
-    probe_steps = 1 if graph is not None else args.steps  # captured events hold the last replay
+        probe_steps = args.steps
+    elif not args.no_probe:
+        # timing events cannot be read back from inside a captured graph: time the identical step
+        # (same kernels, shapes and inputs) once more eagerly, right after the timed replays
+        probe.enable(("gemm", "logmel", "attn"))
+        step()
+        torch.cuda.synchronize()
+        recs = probe.disable()
+        probe_steps = 1
+    else:
+        recs = None
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -211,6 +218,8 @@ def main():
                                   "frac": round(af / sec3 / 1e12 / peak, 4),
                                   "share_of_step": round(sec3 / probe_steps / (elapsed / args.steps), 3)}
     result["launch"] = "hip-graph replay" if graph is not None else "eager"
+    if graph is not None and recs is not None:
+        result["probe"] = "per-kernel HIP events on one eager pass of the same step after the timed replays"
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(model, args.config)
     if world > 1:
