@@ -28,6 +28,62 @@ def _rows(x):
     return x.reshape(-1, x.shape[-1])
 
 
+# ------------------------------------------------------------------ wide-N activation x weight GEMM
+# bf16 copies of the weights used in this step (asrx_weight_to_bf16), keyed by storage, layout and
+# version; cleared at the start of every Model.forward so that updated weights are re-converted and
+# the conversions of a step stay inside that step (and inside its captured graph).
+_WCACHE: dict = {}
+
+
+def clear_weight_cache():
+    _WCACHE.clear()
+
+
+def weight_bf16(W, trans=False, cache=True):
+    """bf16 N x K copy of a weight: W is (N, K) (trans=False) or (K, N) (trans=True)."""
+    key = (W.data_ptr(), tuple(W.shape), tuple(W.stride()), bool(trans), W._version) if cache else None
+    if key is not None and key in _WCACHE:
+        return _WCACHE[key]
+    rows, cols = W.shape
+    if W.stride(1) != 1:
+        W = W.contiguous()
+    out = torch.empty((cols, rows) if trans else (rows, cols), dtype=torch.int16, device=W.device)
+    lib.call("asrx_weight_to_bf16", lib.ptr(W), lib.ptr(out), rows, cols, W.stride(0), int(trans), lib.stream())
+    if key is not None:
+        _WCACHE[key] = out
+    return out
+
+
+_nj_override = None
+
+
+def _nj(M, N):
+    """Tile width 128*nj: the widest that still gives >= 1.5 waves of workgroups on 256 CUs."""
+    if _nj_override:
+        return _nj_override
+    tm = (M + 127) // 128
+    for nj in (3, 2):
+        if 128 * nj <= ((N + 127) // 128) * 128 and tm * ((N + 128 * nj - 1) // (128 * nj)) >= 384:
+            return nj
+    return 1
+
+
+def gemm_wn(A, Wb, C, *, M, N, K, lda, ldc, bias=None, Z=None, alpha=1.0, beta=0.0, act="none",
+            conv=False, conv_F=0, conv_C=0):
+    """C = act(alpha A Wb^T + beta C + bias); Wb bf16 (N, K) from weight_bf16."""
+    lib.require_gpu(A, Wb, C)
+    e0 = probe.begin("gemm")
+    lib.call("asrx_gemm_wn", lib.ptr(A), lda, int(conv), conv_F, conv_C, lib.ptr(Wb), Wb.stride(0), lib.ptr(C),
+             ldc, lib.ptr(bias), lib.ptr(Z), M, N, K, float(alpha), float(beta), ACT[act], _nj(M, N),
+             lib.stream())
+    probe.end("gemm", e0, 2.0 * M * N * K)
+    return C
+
+
+def use_wide(K) -> bool:
+    return prec.get() == prec.PREC_BF16 and K % 8 == 0
+
+
 def linear_fwd(x, W, b=None, act="none", out=None, preact=None):
     """y = act(x @ W^T + b) for x (..., K), W (N, K)."""
     x2 = _rows(x)
@@ -36,8 +92,11 @@ def linear_fwd(x, W, b=None, act="none", out=None, preact=None):
     M, K = x2.shape
     N = W.shape[0]
     y = out if out is not None else torch.empty(*x.shape[:-1], N, device=x.device, dtype=torch.float32)
-    gemm(x2, W, y, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, a_kc=True, b_kc=True, bias=b, act=act,
-         Z=preact)
+    if use_wide(K):
+        gemm_wn(x2, weight_bf16(W), y, M=M, N=N, K=K, lda=K, ldc=N, bias=b, act=act, Z=preact)
+    else:
+        gemm(x2, W, y, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, a_kc=True, b_kc=True, bias=b, act=act,
+             Z=preact)
     return y
 
 
@@ -49,7 +108,10 @@ def linear_dgrad(dy, W, out=None, beta=0.0):
     M, N = d2.shape
     K = W.shape[1]
     dx = out if out is not None else torch.empty(*dy.shape[:-1], K, device=dy.device, dtype=torch.float32)
-    gemm(d2, W, dx, M=M, N=K, K=N, lda=N, ldb=K, ldc=K, a_kc=True, b_kc=False, beta=beta)
+    if use_wide(N):
+        gemm_wn(d2, weight_bf16(W, trans=True), dx, M=M, N=K, K=N, lda=N, ldc=K, beta=beta)
+    else:
+        gemm(d2, W, dx, M=M, N=K, K=N, lda=N, ldb=K, ldc=K, a_kc=True, b_kc=False, beta=beta)
     return dx
 
 

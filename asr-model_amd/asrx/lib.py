@@ -76,6 +76,9 @@ SIGNATURES = {
     "asrx_ce_fwd": (_i32, [_p, _p, _p, _p, _i64, _i64, _p]),
     "asrx_ce_bwd": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _p]),
     "asrx_policy_noise": (_i32, [_p, _i64, _i64, _i64, _u32, _p]),
+    "asrx_weight_to_bf16": (_i32, [_p, _p, _i64, _i64, _i64, _i32, _p]),
+    "asrx_gemm_wn": (_i32, [_p, _i64, _i32, _i64, _i64, _p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _f32, _f32,
+                            _i32, _i32, _p]),
 }
 
 _lib = None

@@ -18,6 +18,7 @@ import torch
 from torch import nn
 from torch.nn.utils.parametrizations import weight_norm
 
+from . import gemm as gemm_mod
 from . import ops
 from .config import Dimensions
 from .noise import NoiseCtx
@@ -533,6 +534,7 @@ class Model(nn.Module):
                    aborc(waveform, pitch, spectrogram)]
         streams = [s.to(torch.float32).contiguous() for s in streams]
         B = first.shape[0]
+        gemm_mod.clear_weight_cache()
         noise = NoiseCtx(self.noise_seed, self.noise_step, self.training)
         if self.training:
             self.noise_step += 1

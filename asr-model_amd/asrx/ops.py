@@ -666,8 +666,12 @@ class Conv3(torch.autograd.Function):
         Co = W.shape[0]
         Wt = W.permute(0, 2, 1).reshape(Co, 3 * Ci).contiguous()
         y = _E(B, T, Co, device=x.device)
-        G.gemm(x, Wt, y, M=B * T, N=Co, K=3 * Ci, lda=Ci, ldb=3 * Ci, ldc=Co, bias=b, conv_a=True, conv_F=T,
-               conv_C=Ci)
+        if G.use_wide(3 * Ci):
+            G.gemm_wn(x, G.weight_bf16(Wt, cache=False), y, M=B * T, N=Co, K=3 * Ci, lda=Ci, ldc=Co, bias=b,
+                      conv=True, conv_F=T, conv_C=Ci)
+        else:
+            G.gemm(x, Wt, y, M=B * T, N=Co, K=3 * Ci, lda=Ci, ldb=3 * Ci, ldc=Co, bias=b, conv_a=True, conv_F=T,
+                   conv_C=Ci)
         ctx.save_for_backward(x, W)
         return y
 
@@ -681,7 +685,12 @@ class Conv3(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             Wf = W.flip(2).permute(1, 2, 0).reshape(Ci, 3 * Co).contiguous()
             dx = _E(x.shape, device=x.device)
-            G.gemm(g, Wf, dx, M=B * T, N=Ci, K=3 * Co, lda=Co, ldb=3 * Co, ldc=Ci, conv_a=True, conv_F=T, conv_C=Co)
+            if G.use_wide(3 * Co):
+                G.gemm_wn(g, G.weight_bf16(Wf, cache=False), dx, M=B * T, N=Ci, K=3 * Co, lda=Co, ldc=Ci, conv=True,
+                          conv_F=T, conv_C=Co)
+            else:
+                G.gemm(g, Wf, dx, M=B * T, N=Ci, K=3 * Co, lda=Co, ldb=3 * Co, ldc=Ci, conv_a=True, conv_F=T,
+                       conv_C=Co)
         dWt = torch.zeros(Co, 3 * Ci, device=x.device)
         tiles = ((Co + 127) // 128) * ((3 * Ci + 127) // 128)
         G.gemm(g, x, dWt, M=Co, N=3 * Ci, K=B * T, lda=Co, ldb=Ci, ldc=3 * Ci, a_kc=False, b_kc=False, conv_b=True,

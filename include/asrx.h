@@ -50,6 +50,16 @@ int asrx_gemm(int prec, const float* A, int64_t lda, int64_t sA, int a_kc, int c
               int splitk, asrx_stream_t stream);
 
 
+/* ---- wide-N GEMM for activation x weight products in perf mode (same call sites as asrx_gemm):
+ * C (M x N) = act(alpha * A W^T + beta * C + bias); A fp32 (M x K, lda) or its implicit k3 im2col
+ * (conv: lda = channels, convF segment length, convC channels); W bf16 N x K (ldw) prepared by
+ * asrx_weight_to_bf16; nj in 1..3 selects the 128*nj-wide output tile. ------------------------- */
+int asrx_weight_to_bf16(const float* src, unsigned short* dst, int64_t rows, int64_t cols, int64_t ld, int trans,
+                        asrx_stream_t stream);
+int asrx_gemm_wn(const float* A, int64_t lda, int conv, int64_t convF, int64_t convC, const unsigned short* W,
+                 int64_t ldw, float* C, int64_t ldc, const float* bias, float* Z, int64_t M, int64_t N, int64_t K,
+                 float alpha, float beta, int act, int nj, asrx_stream_t stream);
+
 /* ---- AbbyNormal: essentials.py:140-191 (router SiLU-MLP, cv, gumbel hard decision, avg/max pool of
  *      x^2 along the feature axis, x / (1 + 1e-4 div)^0.75).  hpre = x @ W1^T + b1 from asrx_gemm.
  *      Rows are (sample, position, head)-major; noise index ((sid*H+h)*4096+l)*3+k, sid = sid_base + b.

@@ -145,3 +145,39 @@ def test_logmel_pool_and_silence(cuda):
     ref = omel.waveform_feature(clips[0].astype(np.float64))[0]
     assert np.abs(pooled[0] - ref).max() < 1e-6
     assert np.all(pooled[1] == 0)
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 384, 384), (300, 1152, 384), (4200, 384, 1536), (129, 64, 384),
+                                   (777, 200, 96)])
+def test_wide_gemm_bf16(cuda, M, N, K):
+    """asrx_gemm_wn (bf16 weights, fp32 activations) for fwd, dgrad and the k3 conv path."""
+    from asrx import gemm as G
+    from asrx import prec
+
+    g = torch.Generator().manual_seed(M + N)
+    x = torch.randn(M, K, generator=g)
+    W = torch.randn(N, K, generator=g) / K ** 0.5
+    b = torch.randn(N, generator=g)
+    dy = torch.randn(M, N, generator=g)
+    with prec.precision("bf16"):
+        G.clear_weight_cache()
+        y = G.linear_fwd(x.to(cuda), W.to(cuda), b.to(cuda), act="gelu").cpu()
+        dx = G.linear_dgrad(dy.to(cuda), W.to(cuda)).cpu()
+    ref_y = torch.nn.functional.gelu(x.double() @ W.double().t() + b.double())
+    ref_dx = dy.double() @ W.double()
+    assert float((y.double() - ref_y).abs().max() / ref_y.abs().max()) < 2e-2
+    assert float((dx.double() - ref_dx).abs().max() / ref_dx.abs().max()) < 2e-2
+
+
+def test_wide_conv3_bf16(cuda):
+    from asrx import ops, prec
+
+    g = torch.Generator().manual_seed(5)
+    Bn, T, C, O = 3, 101, 64, 136
+    x = torch.randn(Bn, C, T, generator=g)
+    W = torch.randn(O, C, 3, generator=g) / (3 * C) ** 0.5
+    bias = torch.randn(O, generator=g)
+    with prec.precision("bf16"):
+        y = ops.Conv3.apply(x.transpose(1, 2).contiguous().to(cuda), W.to(cuda), bias.to(cuda)).cpu()
+    ref = torch.nn.functional.conv1d(x.double(), W.double(), bias.double(), padding=1).transpose(1, 2)
+    assert float((y.double() - ref).abs().max() / ref.abs().max()) < 2e-2

@@ -26,14 +26,21 @@ def gemm_bench():
     from asrx import gemm as G
 
     dev = torch.device("cuda:0")
-    for (M, N, K) in [(96032, 384, 384), (96032, 1152, 384), (96032, 384, 1152), (8192, 40000, 384),
+    for (M, N, K) in [(192064, 384, 384), (96032, 384, 384), (8192, 384, 384), (96032, 1536, 384), (96032, 384, 1536), (96032, 1152, 384), (96032, 384, 1152), (8192, 40000, 384),
                       (4096, 4096, 4096)]:
         x = torch.randn(M, K, device=dev)
         W = torch.randn(N, K, device=dev)
-        for p in (1, 0):
+        for p in (1,):
             y = torch.empty(M, N, device=dev)
             t = timeit(lambda: G.gemm(x, W, y, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, precision=p))
             print(f"gemm prec={p} M={M} N={N} K={K}: {t*1e6:.1f} us  {2*M*N*K/t/1e12:.1f} TF/s", flush=True)
+        Wb = G.weight_bf16(W)
+        for nj in (1, 2, 3):
+            y = torch.empty(M, N, device=dev)
+            G._nj_override = nj
+            t = timeit(lambda: G.gemm_wn(x, Wb, y, M=M, N=N, K=K, lda=K, ldc=N))
+            print(f"  wide nj={nj}: {t*1e6:.1f} us  {2*M*N*K/t/1e12:.1f} TF/s", flush=True)
+        G._nj_override = None
         dy = torch.randn(M, N, device=dev)
         t = timeit(lambda: G.linear_wgrad(dy, x))
         print(f"  wgrad bf16: {t*1e6:.1f} us {2*M*N*K/t/1e12:.1f} TF/s", flush=True)
