@@ -1,0 +1,103 @@
+"""Data-parallel gradient sync (asrx/dist.py) on the gloo backend, world_size 2, CPU: bucketing,
+hook-driven launch during backward, unused parameters, averaging and multi-step reuse."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+class Toy(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.a = torch.nn.Linear(16, 32)
+        self.b = torch.nn.Linear(32, 8)
+        self.unused = torch.nn.Linear(8, 8)  # never receives a gradient (like the dead blocks)
+        self.c = torch.nn.Linear(8, 4)
+
+    def forward(self, x):
+        return self.c(torch.tanh(self.b(torch.relu(self.a(x)))))
+
+
+def _worker(rank, world, port, bucket_mb, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "asr-model_amd")]
+    from asrx.dist import GradSync, broadcast_parameters
+
+    torch.manual_seed(rank)  # different init per rank: broadcast must make them equal
+    model = Toy()
+    broadcast_parameters(model)
+    sync = GradSync(model, bucket_mb=bucket_mb)
+    results = []
+    for step in range(3):
+        sync.zero_grad()
+        g = torch.Generator().manual_seed(100 * step + rank)
+        x = torch.randn(5, 16, generator=g)
+        loss = model(x).pow(2).sum() * (rank + 1)
+        loss.backward()
+        launched_in_backward = sum(int(b.launched) for b in (sync.buckets or []))
+        sync.finish()
+        results.append(({n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None},
+                        launched_in_backward, len(sync.buckets)))
+    # each rank's own local gradient for the last step, for the reference average
+    model.zero_grad(set_to_none=True)
+    sync.remove()
+    g = torch.Generator().manual_seed(100 * 2 + rank)
+    x = torch.randn(5, 16, generator=g)
+    (model(x).pow(2).sum() * (rank + 1)).backward()
+    local = {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None}
+    np_ = lambda d: {k: v.numpy().copy() for k, v in d.items()}  # noqa: E731  (no shared-memory fds)
+    q.put((rank, [(np_(g), l_, nb) for g, l_, nb in results], np_(local),
+           np_({n: p.detach() for n, p in model.named_parameters()})))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("bucket_mb", [64.0, 0.0005])
+def test_gradsync_gloo_world2(bucket_mb):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, bucket_mb, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(2):
+        r, results, local, params = q.get(timeout=120)
+        t = lambda d: {k: torch.from_numpy(v) for k, v in d.items()}  # noqa: E731
+        out[r] = ([(t(g), l_, nb) for g, l_, nb in results], t(local), t(params))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # replicas identical after broadcast
+    for n in out[0][2]:
+        assert torch.equal(out[0][2][n], out[1][2][n])
+    # synced grads are identical on both ranks and equal the average of the local grads
+    g0, g1 = out[0][0][-1][0], out[1][0][-1][0]
+    ref = {n: (out[0][1][n] + out[1][1][n]) / 2 for n in out[0][1]}
+    assert set(g0) == set(ref)
+    for n in ref:
+        assert torch.allclose(g0[n], ref[n], atol=1e-6), n
+        assert torch.equal(g0[n], g1[n])
+    assert "unused.weight" not in g0
+    # from the second step on, buckets are launched from the backward hooks (overlap), not at finish
+    for step in (1, 2):
+        launched, nb = out[0][0][step][1], out[0][0][step][2]
+        assert launched == nb, (step, launched, nb)
+    if bucket_mb < 0.01:
+        assert out[0][0][-1][2] > 1  # tiny buckets -> several all-reduces
