@@ -705,6 +705,171 @@ __global__ __launch_bounds__(256) void dwconv_bwd_w_kernel(const float* __restri
   }
 }
 
+// Tiled depthwise conv for C % 4 == 0 (every call site of the model): one thread owns 4 channels
+// (one float4 column) and R = 16 consecutive outputs; the R + K - 1 input rows stream through one
+// register each and are scattered into the R accumulators with compile-time taps, so each input
+// float4 is loaded once per tile and every x / y access is a coalesced 16-byte lane access.
+// FLIP = 1 runs the transposed conv (backward data: dx[t] = sum_k w[k] g[t - k + P]).
+constexpr int DW_R = 16;
+
+template <int K, bool FLIP>
+__global__ __launch_bounds__(256) void dwconv_tile_kernel(const float4* __restrict__ x, const float* __restrict__ w,
+                                                          const float* __restrict__ b, float4* __restrict__ y,
+                                                          int B, int T, int C4, int ntile) {
+  constexpr int P = K / 2, W = DW_R + K - 1;
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= (int64_t)B * ntile * C4) return;
+  const int c4 = (int)(gid % C4);
+  const int64_t rest = gid / C4;
+  const int t0 = (int)(rest % ntile) * DW_R;
+  const int64_t bb = rest / ntile;
+  const float4* xs = x + bb * T * C4 + c4;
+  float4 wk[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int kk = FLIP ? K - 1 - k : k;
+    const float* wc = w + (int64_t)(4 * c4) * K + kk;
+    wk[k] = make_float4(wc[0], wc[K], wc[2 * K], wc[3 * K]);
+  }
+  float4 bias = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (b) bias = *reinterpret_cast<const float4*>(b + 4 * c4);
+  float4 acc[DW_R];
+#pragma unroll
+  for (int r = 0; r < DW_R; ++r) acc[r] = bias;
+#pragma unroll
+  for (int j = 0; j < W; ++j) {
+    const int row = t0 - P + j;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (row >= 0 && row < T) v = xs[(int64_t)row * C4];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int r = j - k;
+      if (r >= 0 && r < DW_R) {
+        acc[r].x += wk[k].x * v.x;
+        acc[r].y += wk[k].y * v.y;
+        acc[r].z += wk[k].z * v.z;
+        acc[r].w += wk[k].w * v.w;
+      }
+    }
+  }
+  float4* ys = y + bb * T * C4 + c4;
+#pragma unroll
+  for (int r = 0; r < DW_R; ++r)
+    if (t0 + r < T) ys[(int64_t)(t0 + r) * C4] = acc[r];
+}
+
+// Weight/bias gradient: dw[c, k] += sum_{b,t} g[b,t,c] x[b,t+k-P,c], db[c] += sum g.  A workgroup
+// owns 32 float4 columns (128 channels) x 8 row groups (two per wave: lanes 0-31 / 32-63) of
+// DW_S tiles of R rows each; partials are combined lane l + l^32 by a shuffle, then across the 4
+// waves in LDS, and the workgroup's 128 x (K + 1) sums -- a contiguous slice of the (C, K) weight
+// -- leave as coalesced atomics.
+constexpr int DW_S = 4;
+
+template <int K>
+__global__ __launch_bounds__(256) void dwconv_wgrad_kernel(const float4* __restrict__ g, const float4* __restrict__ x,
+                                                           float* __restrict__ dw, float* __restrict__ db, int T,
+                                                           int C4, int nchunk) {
+  constexpr int P = K / 2, W = DW_R + K - 1;
+  __shared__ float4 red[4][32][K + 1];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int cl = lane & 31, grp = wid * 2 + (lane >> 5);
+  const int cchunks = (C4 + 31) / 32;
+  const int cc = blockIdx.x % cchunks;
+  const int chunk = (blockIdx.x / cchunks) % nchunk;
+  const int64_t bb = blockIdx.x / ((int64_t)cchunks * nchunk);
+  const int c4 = cc * 32 + cl;
+  float4 acc[K + 1];
+#pragma unroll
+  for (int k = 0; k <= K; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c4 < C4) {
+    const float4* gs = g + bb * T * C4 + c4;
+    const float4* xs = x + bb * T * C4 + c4;
+    for (int s = 0; s < DW_S; ++s) {
+      const int t0 = ((chunk * 8 + grp) * DW_S + s) * DW_R;
+      if (t0 >= T) break;
+      float4 gv[DW_R];
+#pragma unroll
+      for (int r = 0; r < DW_R; ++r) {
+        gv[r] = (t0 + r < T) ? gs[(int64_t)(t0 + r) * C4] : make_float4(0.f, 0.f, 0.f, 0.f);
+        acc[K].x += gv[r].x; acc[K].y += gv[r].y; acc[K].z += gv[r].z; acc[K].w += gv[r].w;
+      }
+#pragma unroll
+      for (int j = 0; j < W; ++j) {
+        const int row = t0 - P + j;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (row >= 0 && row < T) v = xs[(int64_t)row * C4];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const int r = j - k;
+          if (r >= 0 && r < DW_R) {
+            acc[k].x += gv[r].x * v.x;
+            acc[k].y += gv[r].y * v.y;
+            acc[k].z += gv[r].z * v.z;
+            acc[k].w += gv[r].w * v.w;
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k <= K; ++k) {
+    acc[k].x += __shfl_xor(acc[k].x, 32);
+    acc[k].y += __shfl_xor(acc[k].y, 32);
+    acc[k].z += __shfl_xor(acc[k].z, 32);
+    acc[k].w += __shfl_xor(acc[k].w, 32);
+    if (lane < 32) red[wid][cl][k] = acc[k];
+  }
+  __syncthreads();
+  // the workgroup's slice: channels [128 cc, 128 cc + 128) x taps, contiguous in dw
+  const int c_base = cc * 128;
+  const int nch = min(128, 4 * C4 - c_base);
+  const float* rf = reinterpret_cast<const float*>(&red[0][0][0]);
+  constexpr int WS = 32 * (K + 1) * 4;  // floats per wave slice
+  for (int i = threadIdx.x; i < nch * K; i += 256) {
+    const int c = i / K, k = i % K;  // channel within slice, tap
+    const int off = ((c >> 2) * (K + 1) + k) * 4 + (c & 3);
+    atomicAdd(dw + (int64_t)(c_base + c) * K + k, rf[off] + rf[WS + off] + rf[2 * WS + off] + rf[3 * WS + off]);
+  }
+  if (db)
+    for (int c = threadIdx.x; c < nch; c += 256) {
+      const int off = ((c >> 2) * (K + 1) + K) * 4 + (c & 3);
+      atomicAdd(db + c_base + c, rf[off] + rf[WS + off] + rf[2 * WS + off] + rf[3 * WS + off]);
+    }
+}
+
+template <int K>
+static void dwconv_tiled(const float* x, const float* w, const float* b, float* y, const float* g, float* dx,
+                         float* dw, float* db, int64_t B, int64_t T, int64_t C, hipStream_t stream) {
+  const int C4 = (int)(C / 4);
+  const int ntile = (int)((T + DW_R - 1) / DW_R);
+  const int64_t threads = B * ntile * C4;
+  const unsigned grid = (unsigned)((threads + 255) / 256);
+  if (y) dwconv_tile_kernel<K, false><<<grid, 256, 0, stream>>>((const float4*)x, w, b, (float4*)y, (int)B, (int)T, C4,
+                                                                 ntile);
+  if (dx) dwconv_tile_kernel<K, true><<<grid, 256, 0, stream>>>((const float4*)g, w, nullptr, (float4*)dx, (int)B,
+                                                                 (int)T, C4, ntile);
+  if (dw) {
+    const int nchunk = (int)((T + 8 * DW_S * DW_R - 1) / (8 * DW_S * DW_R));
+    const int64_t blocks = B * nchunk * ((C4 + 31) / 32);
+    dwconv_wgrad_kernel<K><<<(unsigned)blocks, 256, 0, stream>>>((const float4*)g, (const float4*)x, dw, db, (int)T,
+                                                                   C4, nchunk);
+  }
+}
+
+static bool dwconv_dispatch(const float* x, const float* w, const float* b, float* y, const float* g, float* dx,
+                            float* dw, float* db, int64_t B, int64_t T, int64_t C, int64_t K, hipStream_t stream) {
+  if (C % 4 != 0 || ((uintptr_t)(x ? x : g) & 15) || (y && ((uintptr_t)y & 15)) || (dx && ((uintptr_t)dx & 15)) ||
+      (b && ((uintptr_t)b & 15)) || B * T * C >= (1LL << 31))
+    return false;
+  switch (K) {
+    case 3: dwconv_tiled<3>(x, w, b, y, g, dx, dw, db, B, T, C, stream); return true;
+    case 5: dwconv_tiled<5>(x, w, b, y, g, dx, dw, db, B, T, C, stream); return true;
+    case 7: dwconv_tiled<7>(x, w, b, y, g, dx, dw, db, B, T, C, stream); return true;
+    case 15: dwconv_tiled<15>(x, w, b, y, g, dx, dw, db, B, T, C, stream); return true;
+    default: return false;
+  }
+}
+
 // ============================================================================ BatchNorm (per sample)
 // nn.BatchNorm1d in train mode at batch 1 (ConvLite.bn, model.py:103, 114): statistics over T for
 // each (sample, channel).  Stats kernel: grid (ceil(C/64), B).
@@ -737,6 +902,116 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const float* __restrict__
     const float var = (red[0][tl] + red[1][tl] + red[2][tl] + red[3][tl]) / T;
     mean[(int64_t)b * C + c] = mu;
     rstd[(int64_t)b * C + c] = rsqrtf(var + eps);
+  }
+}
+
+// float4 variant (C % 4 == 0): a 1024-thread workgroup per (sample, 128 channels); 32 row groups
+// of 32 lanes stride over T, each lane keeping a Welford (mean, M2) for its 4 channels, combined
+// across row groups with Chan's formula -- one HBM pass, numerically as stable as two passes.
+__device__ __forceinline__ void chan_combine(float& na, float& ma, float& m2a, float nb, float mb, float m2b) {
+  const float n = na + nb;
+  if (n == 0.f) return;
+  const float d = mb - ma;
+  const float f = nb / n;
+  ma += d * f;
+  m2a += m2b + d * d * na * f;
+  na = n;
+}
+
+__global__ __launch_bounds__(1024) void bn_stats4_kernel(const float4* __restrict__ x, float* __restrict__ mean,
+                                                         float* __restrict__ rstd, int T, int C4, float eps) {
+  __shared__ float4 sm[32][32], sq[32][32];
+  const int lane = threadIdx.x & 31, grp = threadIdx.x >> 5;
+  const int cchunks = (C4 + 31) / 32;
+  const int cc = blockIdx.x % cchunks;
+  const int64_t b = blockIdx.x / cchunks;
+  const int c4 = cc * 32 + lane;
+  float4 mu = make_float4(0.f, 0.f, 0.f, 0.f), m2 = mu;
+  float n = 0.f;
+  if (c4 < C4) {
+    const float4* xs = x + b * T * C4 + c4;
+    for (int t = grp; t < T; t += 32) {
+      const float4 v = xs[(int64_t)t * C4];
+      n += 1.f;
+      const float r = 1.f / n;
+      float d;
+      d = v.x - mu.x; mu.x += d * r; m2.x += d * (v.x - mu.x);
+      d = v.y - mu.y; mu.y += d * r; m2.y += d * (v.y - mu.y);
+      d = v.z - mu.z; mu.z += d * r; m2.z += d * (v.z - mu.z);
+      d = v.w - mu.w; mu.w += d * r; m2.w += d * (v.w - mu.w);
+    }
+  }
+  sm[grp][lane] = mu;
+  sq[grp][lane] = m2;
+  __syncthreads();
+  if (grp == 0 && c4 < C4) {
+    // row group g saw rows g, g + 32, ...: count_g = ceil((T - g) / 32)
+    float na = (float)((T + 31) / 32);
+    float4 ma = sm[0][lane], qa = sq[0][lane];
+    for (int g2 = 1; g2 < 32; ++g2) {
+      const float nb = (float)((T - g2 + 31) / 32 > 0 ? (T - g2 + 31) / 32 : 0);
+      const float4 mb = sm[g2][lane], qb = sq[g2][lane];
+      float nx = na, ny = na, nz = na, nw = na;
+      chan_combine(nx, ma.x, qa.x, nb, mb.x, qb.x);
+      chan_combine(ny, ma.y, qa.y, nb, mb.y, qb.y);
+      chan_combine(nz, ma.z, qa.z, nb, mb.z, qb.z);
+      chan_combine(nw, ma.w, qa.w, nb, mb.w, qb.w);
+      na = nx;
+    }
+    float* mo = mean + b * 4 * C4 + 4 * c4;
+    float* ro = rstd + b * 4 * C4 + 4 * c4;
+    mo[0] = ma.x; mo[1] = ma.y; mo[2] = ma.z; mo[3] = ma.w;
+    ro[0] = rsqrtf(qa.x / T + eps); ro[1] = rsqrtf(qa.y / T + eps);
+    ro[2] = rsqrtf(qa.z / T + eps); ro[3] = rsqrtf(qa.w / T + eps);
+  }
+}
+
+// float4 variant of the backward sums (same workgroup shape as bn_stats4_kernel).
+__global__ __launch_bounds__(1024) void bn_bwd_stats4_kernel(const float4* __restrict__ g, const float4* __restrict__ x,
+                                                             const float* __restrict__ mean,
+                                                             const float* __restrict__ rstd,
+                                                             const float* __restrict__ w, float* __restrict__ sg,
+                                                             float* __restrict__ sgx, float* __restrict__ dw,
+                                                             float* __restrict__ db, int T, int C4) {
+  __shared__ float4 sa[32][32], sx[32][32];
+  const int lane = threadIdx.x & 31, grp = threadIdx.x >> 5;
+  const int cchunks = (C4 + 31) / 32;
+  const int cc = blockIdx.x % cchunks;
+  const int64_t b = blockIdx.x / cchunks;
+  const int c4 = cc * 32 + lane;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f), ax = a;
+  if (c4 < C4) {
+    const float4 mu = *reinterpret_cast<const float4*>(mean + b * 4 * C4 + 4 * c4);
+    const float4 rs = *reinterpret_cast<const float4*>(rstd + b * 4 * C4 + 4 * c4);
+    const float4* gs = g + b * T * C4 + c4;
+    const float4* xs = x + b * T * C4 + c4;
+    for (int t = grp; t < T; t += 32) {
+      const float4 gv = gs[(int64_t)t * C4], xv = xs[(int64_t)t * C4];
+      a.x += gv.x; a.y += gv.y; a.z += gv.z; a.w += gv.w;
+      ax.x += gv.x * (xv.x - mu.x) * rs.x;
+      ax.y += gv.y * (xv.y - mu.y) * rs.y;
+      ax.z += gv.z * (xv.z - mu.z) * rs.z;
+      ax.w += gv.w * (xv.w - mu.w) * rs.w;
+    }
+  }
+  sa[grp][lane] = a;
+  sx[grp][lane] = ax;
+  __syncthreads();
+  if (grp < 8 && c4 < C4) {  // 8 x 32 lanes: one (channel, sum) each
+    const int q = grp & 3, which = grp >> 2;
+    float s = 0.f;
+    for (int g2 = 0; g2 < 32; ++g2) {
+      const float4 v = which ? sx[g2][lane] : sa[g2][lane];
+      s += q == 0 ? v.x : q == 1 ? v.y : q == 2 ? v.z : v.w;
+    }
+    const int c = 4 * c4 + q;
+    if (which) {
+      sgx[b * 4 * C4 + c] = s * w[c];
+      atomicAdd(dw + c, s);
+    } else {
+      sg[b * 4 * C4 + c] = s * w[c];
+      atomicAdd(db + c, s);
+    }
   }
 }
 
@@ -1068,7 +1343,7 @@ int asrx_jump_select_bwd(const float* g, const float* xn, const float* orig, con
 int asrx_seg_colsum(const float* x, float* out, int64_t B, int64_t L, int64_t d, float scale, int accumulate,
                     hipStream_t stream) {
   if (B == 0) return 0;
-  if (!accumulate) hipMemsetAsync(out, 0, (size_t)B * d * sizeof(float), stream);
+  if (!accumulate) (void)hipMemsetAsync(out, 0, (size_t)B * d * sizeof(float), stream);
   const int64_t chunk = 64;
   dim3 grid((unsigned)((d + 63) / 64), (unsigned)B, (unsigned)((L + chunk - 1) / chunk));
   seg_colsum_kernel<<<grid, 256, 0, stream>>>(x, out, L, (int)d, scale, chunk);
@@ -1134,13 +1409,15 @@ int asrx_dwconv_fwd(const float* x, const float* w, const float* b, float* y, in
                     int64_t K, hipStream_t stream) {
   ASRX_REQUIRE(K % 2 == 1 && K <= 16, "dwconv: K must be odd and <= 15");
   if (B * T == 0) return 0;
-  LAUNCH_EW(dwconv_fwd_kernel, B * T * C, x, w, b, y, B, T, (int)C, (int)K);
+  if (!dwconv_dispatch(x, w, b, y, nullptr, nullptr, nullptr, nullptr, B, T, C, K, stream))
+    LAUNCH_EW(dwconv_fwd_kernel, B * T * C, x, w, b, y, B, T, (int)C, (int)K);
   ASRX_LAUNCHED("asrx_dwconv_fwd");
 }
 
 int asrx_dwconv_bwd(const float* g, const float* x, const float* w, float* dx, float* dw, float* db, int64_t B,
                     int64_t T, int64_t C, int64_t K, hipStream_t stream) {
   if (B * T == 0) return 0;
+  if (dwconv_dispatch(x, w, nullptr, nullptr, g, dx, dw, db, B, T, C, K, stream)) ASRX_LAUNCHED("asrx_dwconv_bwd");
   if (dx) LAUNCH_EW(dwconv_bwd_data_kernel, B * T * C, g, w, dx, B, T, (int)C, (int)K);
   const int64_t chunk = 256;
   const int64_t nch = (T + chunk - 1) / chunk;
@@ -1153,8 +1430,14 @@ int asrx_bn_fwd(const float* x, const float* w, const float* b, float* y, float*
                 int64_t T, int64_t C, float eps, int use_batch_stats, hipStream_t stream) {
   if (B * T == 0) return 0;
   if (use_batch_stats) {
-    dim3 grid((unsigned)((C + 63) / 64), (unsigned)B);
-    bn_stats_kernel<<<grid, 256, 0, stream>>>(x, mean, rstd, T, (int)C, eps);
+    if (C % 4 == 0 && ((uintptr_t)x & 15) == 0) {
+      const int C4 = (int)(C / 4);
+      bn_stats4_kernel<<<(unsigned)(B * ((C4 + 31) / 32)), 1024, 0, stream>>>((const float4*)x, mean, rstd, (int)T,
+                                                                             C4, eps);
+    } else {
+      dim3 grid((unsigned)((C + 63) / 64), (unsigned)B);
+      bn_stats_kernel<<<grid, 256, 0, stream>>>(x, mean, rstd, T, (int)C, eps);
+    }
   }
   LAUNCH_EW(bn_apply_kernel, B * T * C, x, mean, rstd, w, b, y, B, T, (int)C, use_batch_stats);
   ASRX_LAUNCHED("asrx_bn_fwd");
@@ -1163,8 +1446,15 @@ int asrx_bn_fwd(const float* x, const float* w, const float* b, float* y, float*
 int asrx_bn_bwd(const float* g, const float* x, const float* mean, const float* rstd, const float* w, float* sg_ws,
                 float* sgx_ws, float* dx, float* dw, float* db, int64_t B, int64_t T, int64_t C, hipStream_t stream) {
   if (B * T == 0) return 0;
-  dim3 grid((unsigned)((C + 63) / 64), (unsigned)B);
-  bn_bwd_stats_kernel<<<grid, 256, 0, stream>>>(g, x, mean, rstd, w, sg_ws, sgx_ws, dw, db, T, (int)C);
+  if (C % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)g & 15) == 0 && ((uintptr_t)mean & 15) == 0 &&
+      ((uintptr_t)rstd & 15) == 0) {
+    const int C4 = (int)(C / 4);
+    bn_bwd_stats4_kernel<<<(unsigned)(B * ((C4 + 31) / 32)), 1024, 0, stream>>>(
+        (const float4*)g, (const float4*)x, mean, rstd, w, sg_ws, sgx_ws, dw, db, (int)T, C4);
+  } else {
+    dim3 grid((unsigned)((C + 63) / 64), (unsigned)B);
+    bn_bwd_stats_kernel<<<grid, 256, 0, stream>>>(g, x, mean, rstd, w, sg_ws, sgx_ws, dw, db, T, (int)C);
+  }
   LAUNCH_EW(bn_bwd_apply_kernel, B * T * C, g, x, mean, rstd, w, sg_ws, sgx_ws, dx, B, T, (int)C);
   ASRX_LAUNCHED("asrx_bn_bwd");
 }

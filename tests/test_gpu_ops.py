@@ -239,3 +239,48 @@ def test_encoder_stream(cuda):
     for s, src in enumerate([pitch, spec, wav]):
         ref = om.encode_stream(P, src.double(), layers, onoise, [s * B + b for b in range(B)], True)
         assert _rel(outs[s], ref) < 1e-5, s
+
+
+@pytest.mark.parametrize("K,C,T", [(3, 384, 101), (15, 128, 517), (15, 384, 16), (7, 6, 33), (5, 64, 1)])
+def test_dwconv(cuda, K, C, T):
+    """Depthwise conv (ConvLite.depth model.py:101, encoder k3 model.py:147) on channels-last input:
+    forward, input and weight/bias gradients vs torch float64 conv1d(groups=C) -- the tiled float4
+    kernels for C % 4 == 0 and the generic kernels otherwise (C = 6)."""
+    from asrx import ops
+
+    torch.manual_seed(K * 1000 + C + T)
+    B = 3
+    x = torch.randn(B, T, C)
+    w = torch.randn(C, 1, K) * 0.3
+    b = torch.randn(C)
+
+    def ref(x, w, b):
+        return F.conv1d(x.transpose(1, 2), w, b, padding=K // 2, groups=C).transpose(1, 2)
+
+    yg, yr, gg, gr = _grads(ops.DWConv.apply, ref, [x, w, b])
+    assert _rel(yg, yr) < 1e-5
+    for a, r in zip(gg, gr):
+        assert _rel(a, r) < 1e-5
+
+
+@pytest.mark.parametrize("C,T", [(384, 301), (128, 3001), (6, 40)])
+def test_batchnorm_per_sample(cuda, C, T):
+    """ConvLite.bn (model.py:103, 114) in train mode at the reference's batch 1, applied per clip:
+    forward and gradients vs torch float64 batch_norm on each clip separately."""
+    from asrx import ops
+
+    torch.manual_seed(C + T)
+    B = 3
+    x = torch.randn(B, T, C) * 2 + 5  # offset mean: exercises the one-pass (Welford) statistics
+    w = torch.rand(C) + 0.5
+    b = torch.randn(C)
+
+    def ref(x, w, b):
+        outs = [F.batch_norm(x[i:i + 1].transpose(1, 2), None, None, w, b, training=True, eps=1e-5).transpose(1, 2)
+                for i in range(B)]
+        return torch.cat(outs)
+
+    yg, yr, gg, gr = _grads(lambda x, w, b: ops.BatchNormPS.apply(x, w, b, 1e-5, None), ref, [x, w, b])
+    assert _rel(yg, yr) < 1e-5
+    for a, r in zip(gg, gr):
+        assert _rel(a, r) < 2e-5

@@ -65,9 +65,38 @@ def mel_bench():
         print(f"logmel {lay} B={B}: {t*1e6:.1f} us  {byts/t/1e9:.0f} GB/s (algorithmic)", flush=True)
 
 
+def rowops_bench():
+    from asrx import ops
+
+    dev = torch.device("cuda:0")
+    B, T, C = 64, 3001, 384
+    x = torch.randn(B, T, C, device=dev)
+    g = torch.randn(B, T, C, device=dev)
+    nb = B * T * C * 4
+    for K in (3, 15):
+        w = torch.randn(C, 1, K, device=dev, requires_grad=True)
+        b = torch.randn(C, device=dev, requires_grad=True)
+        xr = x.clone().requires_grad_(True)
+        t = timeit(lambda: ops.DWConv.apply(x, w, b))
+        print(f"dwconv fwd K={K}: {t*1e6:.1f} us {2*nb/t/1e9:.0f} GB/s", flush=True)
+        y = ops.DWConv.apply(xr, w, b)
+        t = timeit(lambda: torch.autograd.grad(y, (xr, w, b), g, retain_graph=True))
+        print(f"dwconv bwd K={K}: {t*1e6:.1f} us {3*nb/t/1e9:.0f} GB/s (dx+dw)", flush=True)
+    w = torch.rand(C, device=dev, requires_grad=True)
+    b = torch.randn(C, device=dev, requires_grad=True)
+    xr = x.clone().requires_grad_(True)
+    t = timeit(lambda: ops.BatchNormPS.apply(x, w, b, 1e-5, None))
+    print(f"bn fwd: {t*1e6:.1f} us {3*nb/t/1e9:.0f} GB/s (stats + apply)", flush=True)
+    y = ops.BatchNormPS.apply(xr, w, b, 1e-5, None)
+    t = timeit(lambda: torch.autograd.grad(y, (xr, w, b), g, retain_graph=True))
+    print(f"bn bwd: {t*1e6:.1f} us {5*nb/t/1e9:.0f} GB/s", flush=True)
+
+
 if __name__ == "__main__":
     what = sys.argv[1:] or ["gemm", "mel"]
     if "mel" in what:
         mel_bench()
     if "gemm" in what:
         gemm_bench()
+    if "rowops" in what:
+        rowops_bench()
