@@ -57,6 +57,15 @@ SIGNATURES = {
     "asrx_jump_select": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p]),
     "asrx_jump_select_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p]),
     "asrx_seg_colsum": (_i32, [_p, _p, _i64, _i64, _i64, _f32, _i32, _p]),
+    "asrx_msheath_ctrl_fwd": (_i32, [_p, _p, _i64, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64,
+                                     _p, _p, _p, _p, _p, _p, _p, _p]),
+    "asrx_msheath_ctrl_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p, _p, _p, _p, _p,
+                                     _p]),
+    "asrx_msheath_rec_bytes": (_i64, []),
+    "asrx_axpy_row2": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _p]),
+    "asrx_axpy_row2_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _p]),
+    "asrx_jump_select4": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p]),
+    "asrx_jump_select4_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p]),
     "asrx_colsum": (_i32, [_p, _p, _i64, _i64, _p]),
     "asrx_add_rows": (_i32, [_p, _p, _p, _p, _i64, _i64, _i64, _p]),
     "asrx_lincomb": (_i32, [_p, _p, _p, _f32, _f32, _f32, _p, _i64, _p]),

@@ -331,7 +331,7 @@ class MSheath(nn.Module):
         B, L, D = x.shape
         dev = x.device
         orig = x
-        mem_w = self.mem_w.reshape(1, D).expand(B, D)
+        mem_w = self.mem_w.reshape(1, D).expand(B, D).contiguous()
         pooled = ops.seg_mean(x)
         h = ops.linear(pooled, self.pnet.net[0].weight, self.pnet.net[0].bias, act="silu")
         policy = torch.softmax(ops.small_linear(h, self.pnet.net[2].weight, self.pnet.net[2].bias), dim=-1)
@@ -339,36 +339,16 @@ class MSheath(nn.Module):
         next_i = torch.zeros(B, device=dev)
         for i in range(self.layer):
             lay = self.layers[i]
-            active = (next_i == i).to(torch.float32)
             ion = ops.v_gate(lay["v_gate"], x)  # (B, L)
             px = ops.layer_norm(x, lay["ln"].weight, lay["ln"].bias, lay["ln"].eps)
             out = ops.linear(px, lay["adapter"].weight, lay["adapter"].bias) if lay["adapter"] is not None else px
             g_val = ops.small_linear(px, lay["gate"][0].weight, lay["gate"][0].bias, act="sigmoid")  # (B, L, 1)
-            x_new = ops.axpy_row(x, (g_val.reshape(B, L) * ion).contiguous(), out)
+            x_new = ops.AxpyRow2.apply(x, g_val.reshape(B, L), ion, out)
             mem = ops.seg_mean(x_new)
             mem_v = ops.small_linear(mem, self.mem_gate[0].weight, self.mem_gate[0].bias, act="sigmoid")  # (B, 1)
-            mem_w_new = mem_v * mem_w + (1 - mem_v) * mem
-            potential = ion.mean(dim=1)
-            if i < self.layer - 1:
-                ys = torch.softmax(policy + gpol[:, i], dim=-1)
-                a_g = ys.argmax(dim=-1)
-                hard = torch.zeros_like(ys).scatter_(-1, a_g.unsqueeze(-1), 1.0) - ys.detach() + ys
-                jg_g = hard.gather(-1, a_g.unsqueeze(-1)).squeeze(-1)
-                low = potential < 0.1
-                action = torch.where(low, torch.ones_like(a_g), a_g)
-                jump_g = torch.where(low, torch.ones_like(jg_g), jg_g)
-            else:
-                action = torch.zeros(B, dtype=torch.long, device=dev)
-                jump_g = torch.ones(B, device=dev)
-            jumped = action > 0
-            jw = self.jump_s[(action - 1).clamp(0, 2)]
-            alpha = torch.where(jumped, torch.ones_like(jump_g), jump_g)
-            beta = torch.where(jumped, jw * jump_g, torch.zeros_like(jump_g))
-            gam = torch.where(jumped, (1 - jw) * jump_g, torch.zeros_like(jump_g)).unsqueeze(-1) * mem_w_new
+            alpha, beta, gam, mem_w, active, next_i = ops.MSheathCtrl.apply(
+                policy, gpol[:, i], ion, mem_v.reshape(B), mem_w, mem, self.jump_s, next_i, i, self.layer)
             x = ops.JumpSelect.apply(x_new, orig, x, active, alpha, beta, gam)
-            mem_w = torch.where(active.bool().unsqueeze(-1), mem_w_new, mem_w)
-            step = torch.where(jumped, torch.clamp(i + action + 1, max=self.layer), torch.full_like(action, i + 1))
-            next_i = torch.where(active.bool(), step.to(torch.float32), next_i)
         gate = ops.small_linear(x, self.mlp_gate[0].weight, self.mlp_gate[0].bias, act="sigmoid")
         hh = ops.layer_norm(x, self.mlp_ln.weight, self.mlp_ln.bias, self.mlp_ln.eps)
         hh = ops.linear(hh, self.mlp[0].weight, self.mlp[0].bias, act="silu")

@@ -419,8 +419,9 @@ class JumpSelect(torch.autograd.Function):
         act, alpha, beta, gam = _c(act), _c(alpha), _c(beta), _c(gam)
         B, L, d = xn.shape
         out = _E(xn.shape, device=xn.device)
-        lib.call("asrx_jump_select", _P(xn), _P(orig), _P(xold), _P(act), _P(alpha), _P(beta), _P(gam), _P(out), B,
-                 L, d, _S())
+        ctx.v4 = d % 4 == 0
+        lib.call("asrx_jump_select4" if ctx.v4 else "asrx_jump_select", _P(xn), _P(orig), _P(xold), _P(act),
+                 _P(alpha), _P(beta), _P(gam), _P(out), B, L, d, _S())
         ctx.save_for_backward(xn, orig, act, alpha, beta)
         return out
 
@@ -430,12 +431,87 @@ class JumpSelect(torch.autograd.Function):
         g = _c(g)
         B, L, d = xn.shape
         dxn, dorig, dxold = _E(xn.shape, device=g.device), _E(xn.shape, device=g.device), _E(xn.shape, device=g.device)
-        dalpha = torch.zeros(B, device=g.device)
-        dbeta = torch.zeros(B, device=g.device)
-        dgam = _E(B, d, device=g.device)
-        lib.call("asrx_jump_select_bwd", _P(g), _P(xn), _P(orig), _P(act), _P(alpha), _P(beta), _P(dxn), _P(dorig),
-                 _P(dxold), _P(dalpha), _P(dbeta), _P(dgam), B, L, d, _S())
+        if ctx.v4:  # zeroes its own accumulators
+            dalpha, dbeta, dgam = _E(B, device=g.device), _E(B, device=g.device), _E(B, d, device=g.device)
+        else:
+            dalpha, dbeta = torch.zeros(B, device=g.device), torch.zeros(B, device=g.device)
+            dgam = _E(B, d, device=g.device)
+        lib.call("asrx_jump_select4_bwd" if ctx.v4 else "asrx_jump_select_bwd", _P(g), _P(xn), _P(orig), _P(act),
+                 _P(alpha), _P(beta), _P(dxn), _P(dorig), _P(dxold), _P(dalpha), _P(dbeta), _P(dgam), B, L, d, _S())
         return dxn, dorig, dxold, None, dalpha, dbeta, dgam
+
+
+class AxpyRow2(torch.autograd.Function):
+    """out = x + s1[row] * s2[row] * y   (MSheath layer update x + g * (out * ion), model.py:461)."""
+
+    @staticmethod
+    def forward(ctx, x, s1, s2, y):
+        x, s1, s2, y = _c(x), _c(s1), _c(s2), _c(y)
+        d = x.shape[-1]
+        out = _E(x.shape, device=x.device)
+        lib.call("asrx_axpy_row2", _P(x), _P(s1), _P(s2), _P(y), _P(out), _rows(x), d, _S())
+        ctx.save_for_backward(s1, s2, y)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        s1, s2, y = ctx.saved_tensors
+        g = _c(g)
+        d = y.shape[-1]
+        dy = _E(y.shape, device=y.device)
+        ds1 = _E(s1.shape, device=y.device)
+        ds2 = _E(s2.shape, device=y.device)
+        lib.call("asrx_axpy_row2_bwd", _P(g), _P(s1), _P(s2), _P(y), _P(dy), _P(ds1), _P(ds2), _rows(y), d, _S())
+        return g, ds1, ds2, dy
+
+
+_REC_BYTES = None
+
+
+class MSheathCtrl(torch.autograd.Function):
+    """One MSheath layer's per-sample control (model.py:461-501) as one kernel each way: potential =
+    mean(ion), gumbel-hard policy -> action (forced 1 when potential < 0.1), jump weights
+    alpha/beta/gam, mem_w update, next layer index.  Returns (alpha, beta, gam, mem_w_out, active,
+    next_i_out); the last two carry no gradient."""
+
+    @staticmethod
+    def forward(ctx, policy, gpol_i, ion, mem_v, mem_w, mem, jump_s, next_i, layer_i, layers):
+        global _REC_BYTES
+        if _REC_BYTES is None:
+            _REC_BYTES = int(lib.load().asrx_msheath_rec_bytes())
+        policy, ion, mem_v, mem_w, mem, next_i = _c(policy), _c(ion), _c(mem_v), _c(mem_w), _c(mem), _c(next_i)
+        B, L = ion.shape
+        D = mem.shape[-1]
+        dev = ion.device
+        alpha, beta, active, next_out = (_E(B, device=dev) for _ in range(4))
+        gam, mwo = _E(B, D, device=dev), _E(B, D, device=dev)
+        rec = _E(B * _REC_BYTES, dtype=torch.uint8, device=dev)
+        lib.call("asrx_msheath_ctrl_fwd", _P(policy), _P(gpol_i), gpol_i.stride(0), _P(ion), _P(mem_v), _P(mem_w),
+                 _P(mem), _P(jump_s), _P(next_i), layer_i, layers, B, L, D, _P(alpha), _P(beta), _P(gam), _P(mwo),
+                 _P(active), _P(next_out), _P(rec), _S())
+        ctx.mark_non_differentiable(active, next_out)
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(mem_v, mem_w, mem, jump_s, rec)
+        ctx.layer_i, ctx.layers = layer_i, layers
+        return alpha, beta, gam, mwo, active, next_out
+
+    @staticmethod
+    def backward(ctx, g_alpha, g_beta, g_gam, g_mwo, _ga, _gn):
+        mem_v, mem_w, mem, jump_s, rec = ctx.saved_tensors
+        B, D = mem.shape
+        dev = mem.device
+        g_alpha = torch.zeros(B, device=dev) if g_alpha is None else _c(g_alpha)
+        g_beta = torch.zeros(B, device=dev) if g_beta is None else _c(g_beta)
+        g_gam = torch.zeros(B, D, device=dev) if g_gam is None else _c(g_gam)
+        g_mwo = None if g_mwo is None else _c(g_mwo)
+        g_policy = _E(B, 3, device=dev)
+        g_mem_v = _E(mem_v.shape, device=dev)
+        g_mem_w, g_mem = _E(B, D, device=dev), _E(B, D, device=dev)
+        g_jump_s = torch.zeros(3, device=dev)
+        lib.call("asrx_msheath_ctrl_bwd", _P(g_alpha), _P(g_beta), _P(g_gam), _P(g_mwo), _P(mem_v), _P(mem_w),
+                 _P(mem), _P(jump_s), _P(rec), ctx.layer_i, ctx.layers, B, D, _P(g_policy), _P(g_mem_v), _P(g_mem_w),
+                 _P(g_mem), _P(g_jump_s), _S())
+        return g_policy, None, None, g_mem_v, g_mem_w, g_mem, g_jump_s, None, None, None
 
 
 class SegMean(torch.autograd.Function):

@@ -313,7 +313,7 @@ static void launch_ns(const GemmParams& p, dim3 g, hipStream_t s) {
   static bool attr_set = false;  // benign race: idempotent attribute
   const int shm = NS * STAGE_BYTES;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)gemm_kernel<PREC, AK, BKC, CA, CB, NS>,
+    (void)hipFuncSetAttribute((const void*)gemm_kernel<PREC, AK, BKC, CA, CB, NS>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, shm);
     attr_set = true;
   }

@@ -235,7 +235,7 @@ static void launch(const Params& p, hipStream_t s) {
   static bool attr = false;
   const int shm = NSTAGE * CF::STAGE;
   if (!attr) {
-    hipFuncSetAttribute((const void*)gemm_wn_kernel<NJ, CONV>, hipFuncAttributeMaxDynamicSharedMemorySize, shm);
+    (void)hipFuncSetAttribute((const void*)gemm_wn_kernel<NJ, CONV>, hipFuncAttributeMaxDynamicSharedMemorySize, shm);
     attr = true;
   }
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + CF::BN - 1) / CF::BN);

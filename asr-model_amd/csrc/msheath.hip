@@ -1,0 +1,348 @@
+// MSheath (model.py:387-507) per-sample control flow and its row updates, batched with batch-1
+// semantics per sample.  The reference runs a Python while-loop with `.item()` branches per layer;
+// here every sample's trajectory is device state and each layer step is three launches:
+//   x_new = x + g * ion * out               axpy_row2 (model.py:461)
+//   control: potential, gumbel policy, action, alpha/beta/gam, mem_w, next layer  msheath_ctrl
+//   x = act ? alpha*x_new + beta*orig + gam : x                                     jump_select
+// instead of ~25 small tensor ops forward and ~40 backward.
+#include "common.h"
+
+namespace asrx {
+
+// Per-sample record saved by the control forward for its backward.
+struct CtrlRec {
+  float ys[3];    // softmax(policy + gumbel) of this layer
+  float action;   // 0, 1, 2 (model.py:478-482)
+  float low;      // potential < 0.1 forced action 1 (model.py:480)
+  float jump_g;   // the STE-gathered jump weight (1 when low or last layer)
+  float cg;       // gam coefficient (1 - jw) * jump_g when jumped, else 0
+  float act;      // sample was at this layer
+};
+
+// Forward.  grid B, 256 threads.  policy (B,3), gpol (B,3) with row stride ld_gpol (the noise of
+// this layer), ion (B,L) the v_gate output, mem_v (B) sigmoid(mem_gate(mem)), mem_w / mem (B,D),
+// jump_s (3), next_i (B) float layer index.  Outputs alpha, beta (B), gam (B,D), mem_w_out (B,D),
+// active (B), next_out (B), rec (B).
+__global__ __launch_bounds__(256) void msheath_ctrl_fwd_kernel(
+    const float* __restrict__ policy, const float* __restrict__ gpol, int64_t ld_gpol, const float* __restrict__ ion,
+    const float* __restrict__ mem_v, const float* __restrict__ mem_w, const float* __restrict__ mem,
+    const float* __restrict__ jump_s, const float* __restrict__ next_i, int layer_i, int layers, int64_t L, int D,
+    float* __restrict__ alpha, float* __restrict__ beta, float* __restrict__ gam, float* __restrict__ mem_w_out,
+    float* __restrict__ active, float* __restrict__ next_out, CtrlRec* __restrict__ rec) {
+  __shared__ float red[4];
+  const int64_t b = blockIdx.x;
+  float s = 0.f;
+  for (int64_t l = threadIdx.x; l < L; l += 256) s += ion[b * L + l];
+  const float potential = block_sum<256>(s, red) / (float)L;  // ion.mean(dim=1), model.py:466
+  const float act = next_i[b] == (float)layer_i ? 1.f : 0.f;
+  float ys[3] = {0.f, 0.f, 0.f};
+  int action;
+  float jump_g, low = 0.f;
+  if (layer_i < layers - 1) {
+    // F.gumbel_softmax(policy, tau=1, hard=True) (model.py:475-477) with keyed gumbel noise
+    float z[3], m = -INFINITY;
+    for (int k = 0; k < 3; ++k) {
+      z[k] = policy[b * 3 + k] + gpol[b * ld_gpol + k];
+      m = fmaxf(m, z[k]);
+    }
+    float den = 0.f;
+    for (int k = 0; k < 3; ++k) {
+      ys[k] = expf(z[k] - m);
+      den += ys[k];
+    }
+    int a = 0;
+    for (int k = 0; k < 3; ++k) {
+      ys[k] /= den;
+      if (ys[k] > ys[a]) a = k;
+    }
+    const float jg = (1.f - ys[a]) + ys[a];  // (y_hard - y.detach() + y)[a]
+    low = potential < 0.1f ? 1.f : 0.f;
+    action = low != 0.f ? 1 : a;
+    jump_g = low != 0.f ? 1.f : jg;
+  } else {
+    action = 0;
+    jump_g = 1.f;
+  }
+  const bool jumped = action > 0;
+  const float jw = jump_s[min(max(action - 1, 0), 2)];
+  const float al = jumped ? 1.f : jump_g;
+  const float be = jumped ? jw * jump_g : 0.f;
+  const float cg = jumped ? (1.f - jw) * jump_g : 0.f;
+  const float mv = mem_v[b];
+  for (int c = threadIdx.x; c < D; c += 256) {
+    const float mw = mem_w[b * D + c];
+    const float mwn = mv * mw + (1.f - mv) * mem[b * D + c];  // model.py:464
+    gam[b * D + c] = cg * mwn;
+    mem_w_out[b * D + c] = act != 0.f ? mwn : mw;
+  }
+  if (threadIdx.x == 0) {
+    alpha[b] = al;
+    beta[b] = be;
+    active[b] = act;
+    const float step = jumped ? (float)min(layer_i + action + 1, layers) : (float)(layer_i + 1);
+    next_out[b] = act != 0.f ? step : next_i[b];
+    CtrlRec r;
+    r.ys[0] = ys[0];
+    r.ys[1] = ys[1];
+    r.ys[2] = ys[2];
+    r.action = (float)action;
+    r.low = low;
+    r.jump_g = jump_g;
+    r.cg = cg;
+    r.act = act;
+    rec[b] = r;
+  }
+}
+
+// Backward.  g_mwo may be null (mem_w of the last layer is not used).  Writes g_policy (B,3),
+// g_mem_v (B), g_mem_w (B,D), g_mem (B,D); accumulates g_jump_s (3) with atomics.
+__global__ __launch_bounds__(256) void msheath_ctrl_bwd_kernel(
+    const float* __restrict__ g_alpha, const float* __restrict__ g_beta, const float* __restrict__ g_gam,
+    const float* __restrict__ g_mwo, const float* __restrict__ mem_v, const float* __restrict__ mem_w,
+    const float* __restrict__ mem, const float* __restrict__ jump_s, const CtrlRec* __restrict__ rec, int layer_i,
+    int layers, int D, float* __restrict__ g_policy, float* __restrict__ g_mem_v, float* __restrict__ g_mem_w,
+    float* __restrict__ g_mem, float* __restrict__ g_jump_s) {
+  __shared__ float red[4];
+  const int64_t b = blockIdx.x;
+  const CtrlRec r = rec[b];
+  const float mv = mem_v[b];
+  const bool act = r.act != 0.f;
+  float s_cg = 0.f, s_mv = 0.f;
+  for (int c = threadIdx.x; c < D; c += 256) {
+    const float mw = mem_w[b * D + c], me = mem[b * D + c];
+    const float mwn = mv * mw + (1.f - mv) * me;
+    const float gg = g_gam[b * D + c];
+    const float go = g_mwo ? g_mwo[b * D + c] : 0.f;
+    const float gmwn = gg * r.cg + (act ? go : 0.f);
+    s_cg += gg * mwn;
+    s_mv += gmwn * (mw - me);
+    g_mem_w[b * D + c] = gmwn * mv + (act ? 0.f : go);
+    g_mem[b * D + c] = gmwn * (1.f - mv);
+  }
+  s_cg = block_sum<256>(s_cg, red);
+  s_mv = block_sum<256>(s_mv, red);
+  if (threadIdx.x == 0) {
+    g_mem_v[b] = s_mv;
+    const int action = (int)r.action;
+    const bool jumped = action > 0;
+    const float ga = g_alpha[b], gb = g_beta[b];
+    const int widx = min(max(action - 1, 0), 2);
+    const float jw = jump_s[widx];
+    const float g_jump = jumped ? jw * gb + (1.f - jw) * s_cg : ga;
+    if (jumped) atomicAdd(g_jump_s + widx, r.jump_g * (gb - s_cg));
+    float gp[3] = {0.f, 0.f, 0.f};
+    if (layer_i < layers - 1 && r.low == 0.f) {
+      // d jump_g / d ys[a] = 1 (straight-through), then softmax backward to the policy logits
+      int a = 0;
+      for (int k = 1; k < 3; ++k)
+        if (r.ys[k] > r.ys[a]) a = k;
+      for (int k = 0; k < 3; ++k) gp[k] = r.ys[k] * ((k == a ? 1.f : 0.f) - r.ys[a]) * g_jump;
+    }
+    for (int k = 0; k < 3; ++k) g_policy[b * 3 + k] = gp[k];
+  }
+}
+
+// out = x + s1[r] * s2[r] * y  (s2 may be null) -- model.py:461 with s1 = gate, s2 = ion.
+__global__ void axpy_row2_kernel(const float4* __restrict__ x, const float* __restrict__ s1,
+                                 const float* __restrict__ s2, const float4* __restrict__ y, float4* __restrict__ out,
+                                 int64_t rows, int d4) {
+  const int64_t total = rows * d4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / d4;
+    const float sc = s1[r] * (s2 ? s2[r] : 1.f);
+    const float4 a = x[i], v = y[i];
+    out[i] = make_float4(a.x + sc * v.x, a.y + sc * v.y, a.z + sc * v.z, a.w + sc * v.w);
+  }
+}
+
+// dy = s1 s2 g ; t = sum_j g y ; ds1 = s2 t ; ds2 = s1 t.  One wave per row.
+__global__ __launch_bounds__(256) void axpy_row2_bwd_kernel(const float4* __restrict__ g, const float* __restrict__ s1,
+                                                            const float* __restrict__ s2, const float4* __restrict__ y,
+                                                            float4* __restrict__ dy, float* __restrict__ ds1,
+                                                            float* __restrict__ ds2, int64_t rows, int d4) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += (int64_t)gridDim.x * 4) {
+    const float a = s1[r], c = s2 ? s2[r] : 1.f;
+    const float sc = a * c;
+    float t = 0.f;
+    for (int j = lane; j < d4; j += 64) {
+      const float4 gv = g[r * d4 + j], yv = y[r * d4 + j];
+      t += gv.x * yv.x + gv.y * yv.y + gv.z * yv.z + gv.w * yv.w;
+      dy[r * d4 + j] = make_float4(sc * gv.x, sc * gv.y, sc * gv.z, sc * gv.w);
+    }
+    t = wave_sum(t);
+    if (lane == 0) {
+      ds1[r] = c * t;
+      if (ds2) ds2[r] = a * t;
+    }
+  }
+}
+
+// jump_select forward, float4: out = act ? alpha*xn + beta*orig + gam : xold.  grid (chunks, B).
+__global__ void jump_select4_kernel(const float4* __restrict__ xn, const float4* __restrict__ orig,
+                                    const float4* __restrict__ xold, const float* __restrict__ act,
+                                    const float* __restrict__ alpha, const float* __restrict__ beta,
+                                    const float4* __restrict__ gam, float4* __restrict__ out, int64_t L, int d4) {
+  const int64_t b = blockIdx.y;
+  const int64_t n = L * d4;
+  const int64_t base = b * n;
+  const bool a = act[b] != 0.f;
+  const float al = alpha[b], be = beta[b];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (a) {
+      const float4 u = xn[base + i], v = orig[base + i], w = gam[b * d4 + i % d4];
+      out[base + i] = make_float4(al * u.x + be * v.x + w.x, al * u.y + be * v.y + w.y, al * u.z + be * v.z + w.z,
+                                  al * u.w + be * v.w + w.w);
+    } else {
+      out[base + i] = xold[base + i];
+    }
+  }
+}
+
+// jump_select backward, float4: a 256-thread workgroup per (sample, 32 float4 columns, L chunk):
+// 8 row groups of 32 lanes; per-sample sums leave as atomics (dalpha, dbeta, dgam zeroed by the
+// launcher).  Inactive samples only copy g to dxold.
+__global__ __launch_bounds__(256) void jump_select4_bwd_kernel(
+    const float4* __restrict__ g, const float4* __restrict__ xn, const float4* __restrict__ orig,
+    const float* __restrict__ act, const float* __restrict__ alpha, const float* __restrict__ beta,
+    float4* __restrict__ dxn, float4* __restrict__ dorig, float4* __restrict__ dxold, float* __restrict__ dalpha,
+    float* __restrict__ dbeta, float* __restrict__ dgam, int64_t L, int d4, int lchunk) {
+  __shared__ float4 sg_s[8][32];
+  __shared__ float red[2][4];
+  const int lane = threadIdx.x & 31, grp = threadIdx.x >> 5;
+  const int cchunks = (d4 + 31) / 32;
+  const int cc = blockIdx.x % cchunks;
+  const int64_t b = blockIdx.y;
+  const int64_t l0 = (int64_t)(blockIdx.x / cchunks) * lchunk;
+  const int64_t l1 = min(L, l0 + lchunk);
+  const int c4 = cc * 32 + lane;
+  const bool a = act[b] != 0.f;
+  const float al = alpha[b], be = beta[b];
+  float sa = 0.f, sb = 0.f;
+  float4 sgv = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c4 < d4) {
+    for (int64_t l = l0 + grp; l < l1; l += 8) {
+      const int64_t i = (b * L + l) * d4 + c4;
+      const float4 gv = g[i];
+      if (a) {
+        const float4 u = xn[i], v = orig[i];
+        sa += gv.x * u.x + gv.y * u.y + gv.z * u.z + gv.w * u.w;
+        sb += gv.x * v.x + gv.y * v.y + gv.z * v.z + gv.w * v.w;
+        sgv.x += gv.x; sgv.y += gv.y; sgv.z += gv.z; sgv.w += gv.w;
+        dxn[i] = make_float4(al * gv.x, al * gv.y, al * gv.z, al * gv.w);
+        dorig[i] = make_float4(be * gv.x, be * gv.y, be * gv.z, be * gv.w);
+        dxold[i] = z4;
+      } else {
+        dxn[i] = z4;
+        dorig[i] = z4;
+        dxold[i] = gv;
+      }
+    }
+  }
+  if (!a) return;  // uniform per workgroup
+  sg_s[grp][lane] = sgv;
+  sa = wave_sum(sa);
+  sb = wave_sum(sb);
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = sa;
+    red[1][threadIdx.x >> 6] = sb;
+  }
+  __syncthreads();
+  if (threadIdx.x < 128) {  // 32 float4 columns x 4 components
+    const int cl = threadIdx.x >> 2, q = threadIdx.x & 3;
+    const int c4b = cc * 32 + cl;
+    if (c4b < d4) {
+      float t = 0.f;
+      for (int g2 = 0; g2 < 8; ++g2) {
+        const float4 v = sg_s[g2][cl];
+        t += q == 0 ? v.x : q == 1 ? v.y : q == 2 ? v.z : v.w;
+      }
+      atomicAdd(dgam + b * 4 * d4 + 4 * c4b + q, t);
+    }
+  } else if (threadIdx.x == 128) {
+    atomicAdd(dalpha + b, red[0][0] + red[0][1] + red[0][2] + red[0][3]);
+    atomicAdd(dbeta + b, red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+  }
+}
+
+}  // namespace asrx
+
+using namespace asrx;
+
+extern "C" {
+
+int asrx_msheath_ctrl_fwd(const float* policy, const float* gpol, int64_t ld_gpol, const float* ion,
+                          const float* mem_v, const float* mem_w, const float* mem, const float* jump_s,
+                          const float* next_i, int64_t layer_i, int64_t layers, int64_t B, int64_t L, int64_t D,
+                          float* alpha, float* beta, float* gam, float* mem_w_out, float* active, float* next_out,
+                          void* rec, hipStream_t stream) {
+  if (B == 0) return 0;
+  msheath_ctrl_fwd_kernel<<<(unsigned)B, 256, 0, stream>>>(policy, gpol, ld_gpol, ion, mem_v, mem_w, mem, jump_s,
+                                                           next_i, (int)layer_i, (int)layers, L, (int)D, alpha, beta,
+                                                           gam, mem_w_out, active, next_out, (CtrlRec*)rec);
+  ASRX_LAUNCHED("asrx_msheath_ctrl_fwd");
+}
+
+int asrx_msheath_ctrl_bwd(const float* g_alpha, const float* g_beta, const float* g_gam, const float* g_mwo,
+                          const float* mem_v, const float* mem_w, const float* mem, const float* jump_s,
+                          const void* rec, int64_t layer_i, int64_t layers, int64_t B, int64_t D, float* g_policy,
+                          float* g_mem_v, float* g_mem_w, float* g_mem, float* g_jump_s, hipStream_t stream) {
+  if (B == 0) return 0;
+  msheath_ctrl_bwd_kernel<<<(unsigned)B, 256, 0, stream>>>(g_alpha, g_beta, g_gam, g_mwo, mem_v, mem_w, mem, jump_s,
+                                                           (const CtrlRec*)rec, (int)layer_i, (int)layers, (int)D,
+                                                           g_policy, g_mem_v, g_mem_w, g_mem, g_jump_s);
+  ASRX_LAUNCHED("asrx_msheath_ctrl_bwd");
+}
+
+int64_t asrx_msheath_rec_bytes(void) { return (int64_t)sizeof(CtrlRec); }
+
+int asrx_axpy_row2(const float* x, const float* s1, const float* s2, const float* y, float* out, int64_t rows,
+                   int64_t d, hipStream_t stream) {
+  ASRX_REQUIRE(d % 4 == 0, "asrx_axpy_row2: d % 4 != 0");
+  if (rows == 0) return 0;
+  const int64_t n = rows * d / 4;
+  axpy_row2_kernel<<<(unsigned)std::min<int64_t>((n + 255) / 256, 16384), 256, 0, stream>>>(
+      (const float4*)x, s1, s2, (const float4*)y, (float4*)out, rows, (int)(d / 4));
+  ASRX_LAUNCHED("asrx_axpy_row2");
+}
+
+int asrx_axpy_row2_bwd(const float* g, const float* s1, const float* s2, const float* y, float* dy, float* ds1,
+                       float* ds2, int64_t rows, int64_t d, hipStream_t stream) {
+  ASRX_REQUIRE(d % 4 == 0, "asrx_axpy_row2_bwd: d % 4 != 0");
+  if (rows == 0) return 0;
+  axpy_row2_bwd_kernel<<<(unsigned)std::min<int64_t>((rows + 3) / 4, 8192), 256, 0, stream>>>(
+      (const float4*)g, s1, s2, (const float4*)y, (float4*)dy, ds1, ds2, rows, (int)(d / 4));
+  ASRX_LAUNCHED("asrx_axpy_row2_bwd");
+}
+
+int asrx_jump_select4(const float* xn, const float* orig, const float* xold, const float* act, const float* alpha,
+                      const float* beta, const float* gam, float* out, int64_t B, int64_t L, int64_t d,
+                      hipStream_t stream) {
+  ASRX_REQUIRE(d % 4 == 0, "asrx_jump_select4: d % 4 != 0");
+  if (B * L == 0) return 0;
+  const int64_t n = L * d / 4;
+  dim3 grid((unsigned)std::min<int64_t>((n + 255) / 256, 512), (unsigned)B);
+  jump_select4_kernel<<<grid, 256, 0, stream>>>((const float4*)xn, (const float4*)orig, (const float4*)xold, act,
+                                                alpha, beta, (const float4*)gam, (float4*)out, L, (int)(d / 4));
+  ASRX_LAUNCHED("asrx_jump_select4");
+}
+
+int asrx_jump_select4_bwd(const float* g, const float* xn, const float* orig, const float* act, const float* alpha,
+                          const float* beta, float* dxn, float* dorig, float* dxold, float* dalpha, float* dbeta,
+                          float* dgam, int64_t B, int64_t L, int64_t d, hipStream_t stream) {
+  ASRX_REQUIRE(d % 4 == 0, "asrx_jump_select4_bwd: d % 4 != 0");
+  if (B * L == 0) return 0;
+  (void)hipMemsetAsync(dalpha, 0, B * sizeof(float), stream);
+  (void)hipMemsetAsync(dbeta, 0, B * sizeof(float), stream);
+  (void)hipMemsetAsync(dgam, 0, B * d * sizeof(float), stream);
+  const int d4 = (int)(d / 4);
+  const int lchunk = 128;
+  dim3 grid((unsigned)(((d4 + 31) / 32) * ((L + lchunk - 1) / lchunk)), (unsigned)B);
+  jump_select4_bwd_kernel<<<grid, 256, 0, stream>>>((const float4*)g, (const float4*)xn, (const float4*)orig, act,
+                                                    alpha, beta, (float4*)dxn, (float4*)dorig, (float4*)dxold, dalpha,
+                                                    dbeta, dgam, L, d4, lchunk);
+  ASRX_LAUNCHED("asrx_jump_select4_bwd");
+}
+
+}  // extern "C"

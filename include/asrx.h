@@ -138,6 +138,31 @@ int asrx_jump_select(const float* xn, const float* orig, const float* xold, cons
 int asrx_jump_select_bwd(const float* g, const float* xn, const float* orig, const float* act, const float* alpha,
                          const float* beta, float* dxn, float* dorig, float* dxold, float* dalpha, float* dbeta,
                          float* dgam, int64_t B, int64_t L, int64_t d, asrx_stream_t stream);
+/* MSheath per-layer control (model.py:461-501), batched with per-sample trajectories: potential,
+ * gumbel-hard policy, action, alpha/beta/gam, mem_w update, next layer.  rec: B records of
+ * asrx_msheath_rec_bytes() bytes saved for the backward.  g_mwo may be NULL. */
+int asrx_msheath_ctrl_fwd(const float* policy, const float* gpol, int64_t ld_gpol, const float* ion,
+                          const float* mem_v, const float* mem_w, const float* mem, const float* jump_s,
+                          const float* next_i, int64_t layer_i, int64_t layers, int64_t B, int64_t L, int64_t D,
+                          float* alpha, float* beta, float* gam, float* mem_w_out, float* active, float* next_out,
+                          void* rec, asrx_stream_t stream);
+int asrx_msheath_ctrl_bwd(const float* g_alpha, const float* g_beta, const float* g_gam, const float* g_mwo,
+                          const float* mem_v, const float* mem_w, const float* mem, const float* jump_s,
+                          const void* rec, int64_t layer_i, int64_t layers, int64_t B, int64_t D, float* g_policy,
+                          float* g_mem_v, float* g_mem_w, float* g_mem, float* g_jump_s, asrx_stream_t stream);
+int64_t asrx_msheath_rec_bytes(void);
+/* out = x + s1[r] * s2[r] * y (s2 may be NULL), d % 4 == 0 (model.py:461: x + gate * ion * out). */
+int asrx_axpy_row2(const float* x, const float* s1, const float* s2, const float* y, float* out, int64_t rows,
+                   int64_t d, asrx_stream_t stream);
+int asrx_axpy_row2_bwd(const float* g, const float* s1, const float* s2, const float* y, float* dy, float* ds1,
+                       float* ds2, int64_t rows, int64_t d, asrx_stream_t stream);
+/* float4 forms of asrx_jump_select(_bwd) for d % 4 == 0 (the backward zeroes dalpha/dbeta/dgam). */
+int asrx_jump_select4(const float* xn, const float* orig, const float* xold, const float* act, const float* alpha,
+                      const float* beta, const float* gam, float* out, int64_t B, int64_t L, int64_t d,
+                      asrx_stream_t stream);
+int asrx_jump_select4_bwd(const float* g, const float* xn, const float* orig, const float* act, const float* alpha,
+                          const float* beta, float* dxn, float* dorig, float* dxold, float* dalpha, float* dbeta,
+                          float* dgam, int64_t B, int64_t L, int64_t d, asrx_stream_t stream);
 int asrx_seg_colsum(const float* x, float* out, int64_t B, int64_t L, int64_t d, float scale, int accumulate,
                     asrx_stream_t stream);
 int asrx_colsum(const float* x, float* out, int64_t rows, int64_t d, asrx_stream_t stream);
