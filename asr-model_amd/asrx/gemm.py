@@ -58,12 +58,13 @@ _nj_override = None
 
 
 def _nj(M, N):
-    """Tile width 128*nj: the widest that still gives >= 1.5 waves of workgroups on 256 CUs."""
+    """Tile width 128*nj of the persistent wide GEMM: the widest that still gives >= 200 tiles
+    (most of the 256 CUs busy); narrow tiles run two workgroups per CU."""
     if _nj_override:
         return _nj_override
     tm = (M + 127) // 128
     for nj in (3, 2):
-        if 128 * nj <= ((N + 127) // 128) * 128 and tm * ((N + 128 * nj - 1) // (128 * nj)) >= 384:
+        if 128 * nj <= ((N + 127) // 128) * 128 and tm * ((N + 128 * nj - 1) // (128 * nj)) >= 200:
             return nj
     return 1
 

@@ -91,6 +91,47 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return t;
 }
 
+// ------------------------------------------------------------ LDS-DMA from inline asm
+// global -> LDS copies (global_load_lds_dword{,x4}) issued from inline asm.  The compiler's waitcnt
+// model does not see them, so it neither drains them (vmcnt(0)) before every ds_read -- which is what
+// it does for __builtin_amdgcn_global_load_lds, defeating any prefetch ring -- nor counts them:
+// completion is tracked by hand with s_waitcnt vmcnt(N) + s_barrier.  M0 is written and restored
+// inside the statement (MI355X guide, "LDS-DMA recipe").
+typedef __attribute__((address_space(3))) char lds_char_t;
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)(const lds_char_t*)p);
+}
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}
+__device__ __forceinline__ void glds4(const void* gsrc, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}
+// s_waitcnt vmcnt(k) for the largest listed k <= n (waiting for more than needed is always safe).
+__device__ __forceinline__ void wait_vm_le(int n) {
+  if (n >= 48) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+  else if (n >= 40) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
+  else if (n >= 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+  else if (n >= 28) asm volatile("s_waitcnt vmcnt(28)" ::: "memory");
+  else if (n >= 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  else if (n >= 20) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+  else if (n >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if (n >= 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if (n >= 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if (n >= 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else if (n >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if (n >= 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // Ordered-int encoding so that atomicMax on int works for any float.
 __host__ __device__ __forceinline__ int float_to_ordered(float f) {
   int i = __builtin_bit_cast(int, f);

@@ -115,7 +115,7 @@ struct Stager {
         o -= (uint32_t)convC;
       }
       const float* src = ok ? base + o : g_zero_page;
-      __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(lds_tile + (wid * 4 + i) * 1024), 16, 0, 0);
+      glds16(src, lds_addr(lds_tile + (wid * 4 + i) * 1024));
     }
   }
 };

@@ -4,26 +4,30 @@
 //   A  fp32 activations (M x K, row-major, or the implicit k3 im2col of a channels-last sequence),
 //   W  the weight pre-converted to bf16, stored N x K (K contiguous) -- asrx_weight_to_bf16.
 //
-// Why a second GEMM: at the model's shapes (M = 8k..192k rows, N, K = 64..1536) the kernel is bound
-// by bytes moved HBM/L2 -> LDS, not by MFMA.  A 128 x BN tile with BN = 128 * NJ up to 384 reads
-// each activation row panel once (instead of once per 128-column tile) and the bf16 weight panel
-// costs half the fp32 bytes.  512 threads = 8 waves (2 x 4), each wave 64 x 32*NJ of the output
-// (4 x 2*NJ MFMA 16x16x32 bf16 tiles).  A (fp32, 16 KB) and W (bf16, 8*NJ KB) tiles of 32 k stream
-// HBM -> LDS by LDS-DMA into a 3-stage ring with counted vmcnt; A fragments are rounded to bf16 in
-// registers.  Images are XOR-swizzled through the per-lane source address (rule 21).
+// At the model's shapes (M = 8k..192k rows, N, K = 64..1536) the kernel is bound by bytes moved
+// (A from HBM, W from L2, C back to HBM), not by MFMA.  Design:
+//  * 128 x BN tiles, BN = 128 * NJ up to 384, so an activation row panel is read once per 384
+//    output columns; 512 threads = 8 waves (2 x 4), each 64 x 32*NJ of the output.
+//  * Persistent workgroups (grid = resident capacity) walk their tiles in an XCD-grouped order;
+//    the LDS-DMA ring (A fp32 16 KB + W bf16 8*NJ KB per 32-deep k-step) runs across tile
+//    boundaries, so the next tile's first k-steps are in flight while this tile's epilogue stores
+//    drain.  The bias slice of each tile rides the ring as one extra dword DMA per lane.
+//  * LDS-DMA from inline asm (common.h glds16): the compiler's own waitcnt logic would otherwise
+//    drain the ring (vmcnt(0)) before every ds_read.  Completion is counted by hand.
+//  * Images are XOR-swizzled through the per-lane source address so the ds_read_b128 fragment
+//    reads are bank-conflict-free under gfx950's 64-bank, 16-lane-group rule.
+//  * MFMA 16x16x32 bf16 with the W fragment as the row operand: each lane ends up owning 4
+//    consecutive output columns of one row, so the epilogue stores float4.
 #include "common.h"
 
 namespace asrx {
 
 namespace wn {
 
-constexpr int BM = 128, BK = 32, NTHR = 512, NSTAGE = 3;
+constexpr int BM = 128, BK = 32, NTHR = 512;
 constexpr int A_BYTES = BM * BK * 4;  // 16 KB fp32
 
 __device__ __attribute__((aligned(16))) float zero_page[4];
-
-typedef __attribute__((address_space(3))) void lds_void;
-typedef const __attribute__((address_space(1))) void gbl_void;
 
 struct Params {
   const float* A;
@@ -45,10 +49,15 @@ struct Cfg {
   static constexpr int BN = 128 * NJ;
   static constexpr int B_BYTES = BN * BK * 2;  // bf16
   static constexpr int STAGE = A_BYTES + B_BYTES;
-  static constexpr int A_PIECES = A_BYTES / 1024 / 8;  // per wave: 2
-  static constexpr int B_PIECES = B_BYTES / 1024 / 8;  // per wave: NJ
-  static constexpr int PIECES = A_PIECES + B_PIECES;
+  static constexpr int PIECES = 2 + NJ;  // 1 KB DMAs per wave per k-step: A 2, W NJ
+  static constexpr int BNR = (BN + NTHR - 1) / NTHR * NTHR;  // bias slice in whole DMA rounds
+  static constexpr int BIAS_OPS = BNR / NTHR;
 };
+
+// conflict-free swizzles (chunk XOR by row) for the A image (rows of 8 x 16 B) and the W image
+// (rows of 4 x 16 B) under ds_read_b128 lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31}, ...
+__device__ __forceinline__ int swa(int row) { return ((row >> 1) & 1) | (((row >> 3) & 1) << 2); }
+__device__ __forceinline__ int swb(int n) { return ((n >> 3) & 1) << 1; }
 
 template <int NJ, bool CONV>
 struct Loader {
@@ -56,6 +65,7 @@ struct Loader {
   int akk[2], apos[2];
   bool aok[2];
   uint32_t boff[NJ];
+  int bkc[NJ];
   bool bok[NJ];
 
   __device__ __forceinline__ void init(const Params& p, int m0, int n0) {
@@ -64,7 +74,7 @@ struct Loader {
     for (int i = 0; i < 2; ++i) {  // A: [128 rows][8 chunks of 4 fp32]; piece q = 8 rows
       const int q = wid * 2 + i;
       const int row = 8 * q + (lane >> 3);
-      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      const int c = (lane & 7) ^ swa(row);
       const int r = m0 + row;
       aok[i] = r < p.M;
       aoff[i] = (uint32_t)r * (uint32_t)p.lda + 4 * c;
@@ -75,10 +85,11 @@ struct Loader {
     for (int i = 0; i < NJ; ++i) {  // W: [BN rows][4 chunks of 8 bf16]; piece q = 16 rows
       const int q = wid * NJ + i;
       const int row = 16 * q + (lane >> 2);
-      const int c = (lane & 3) ^ ((row >> 2) & 3);
+      const int c = (lane & 3) ^ swb(row);
       const int n = n0 + row;
       bok[i] = n < p.N;
       boff[i] = (uint32_t)n * (uint32_t)p.ldw + 8 * c;
+      bkc[i] = 8 * c;
     }
   }
 
@@ -94,50 +105,123 @@ struct Loader {
         ok = ok && pos >= 0 && pos < p.convF;
         o -= (uint32_t)p.convC;
       }
-      const float* src = ok ? p.A + o : zero_page;
-      __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(st + (wid * 2 + i) * 1024), 16, 0, 0);
+      glds16(ok ? (const void*)(p.A + o) : (const void*)zero_page, lds_addr(st + (wid * 2 + i) * 1024));
     }
     char* bt = st + A_BYTES;
 #pragma unroll
     for (int i = 0; i < NJ; ++i) {
-      const int lane = threadIdx.x & 63;
-      const int kc = k0 + 8 * ((lane & 3) ^ (((16 * (wid * NJ + i) + (lane >> 2)) >> 2) & 3));
-      const bool ok = bok[i] && kc < p.K;
-      const void* src = ok ? (const void*)(p.W + boff[i] + k0) : (const void*)zero_page;
-      __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(bt + (wid * NJ + i) * 1024), 16, 0, 0);
+      const bool ok = bok[i] && k0 + bkc[i] < p.K;
+      glds16(ok ? (const void*)(p.W + boff[i] + k0) : (const void*)zero_page, lds_addr(bt + (wid * NJ + i) * 1024));
     }
   }
 };
 
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+__device__ __forceinline__ bool vec_ok(const Params& p) {
+  return ((p.N | p.ldc) & 3) == 0 && ((uintptr_t)p.C & 15) == 0 && ((uintptr_t)p.Z & 15) == 0;
 }
 
-__device__ __forceinline__ void tile_of(int bid, int nblk, int nN, int& tm, int& tn) {
-  const int xcd = bid & 7, q = nblk >> 3, r = nblk & 7;
-  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  tn = wg % nN;
-  tm = wg / nN;
+template <int ACT>
+__device__ __forceinline__ float act_t(float x) {
+  if constexpr (ACT == ACT_GELU) return gelu_f(x);
+  else if constexpr (ACT == ACT_SILU) return silu_f(x);
+  else if constexpr (ACT == ACT_SIGMOID) return sigmoid_f(x);
+  else if constexpr (ACT == ACT_RELU) return x > 0.f ? x : 0.f;
+  else return x;
 }
 
-template <int NJ, bool CONV>
-__global__ __launch_bounds__(NTHR, 1) void gemm_wn_kernel(Params p) {
+// Tile epilogue: v = alpha * acc + bias (+ beta * C); Z <- v (pre-activation); C <- act(v).
+template <int NJ, int ACT>
+__device__ __forceinline__ void epilogue(const Params& p, f32x4 (&acc)[4][2 * NJ], const float* bsl, int m0, int n0,
+                                         int wm, int wn, int lr, int lk) {
+  constexpr int NT = 2 * NJ;
+  const bool vec = vec_ok(p);
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int nl = wn * (32 * NJ) + nt * 16 + 4 * lk;
+    const int col = n0 + nl;
+    if (col >= p.N) continue;
+    float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (p.bias) bv = *reinterpret_cast<const float4*>(bsl + nl);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const int row = m0 + wm * 64 + mt * 16 + lr;
+      if (row >= p.M) continue;
+      float v[4] = {p.alpha * acc[mt][nt][0] + bv.x, p.alpha * acc[mt][nt][1] + bv.y,
+                    p.alpha * acc[mt][nt][2] + bv.z, p.alpha * acc[mt][nt][3] + bv.w};
+      float* dst = p.C + (int64_t)row * p.ldc + col;
+      float* zdst = p.Z ? p.Z + (int64_t)row * p.ldc + col : nullptr;
+      if (vec) {
+        if (p.beta != 0.f) {
+          const float4 o = *reinterpret_cast<const float4*>(dst);
+          v[0] += p.beta * o.x; v[1] += p.beta * o.y; v[2] += p.beta * o.z; v[3] += p.beta * o.w;
+        }
+        if (zdst) *reinterpret_cast<float4*>(zdst) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4*>(dst) = make_float4(act_t<ACT>(v[0]), act_t<ACT>(v[1]), act_t<ACT>(v[2]),
+                                                      act_t<ACT>(v[3]));
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (col + r >= p.N) break;
+          float x = v[r];
+          if (p.beta != 0.f) x += p.beta * dst[r];
+          if (zdst) zdst[r] = x;
+          dst[r] = act_t<ACT>(x);
+        }
+      }
+    }
+  }
+}
+
+template <int NJ, bool CONV, int NS>
+__global__ __launch_bounds__(NTHR, 1) void gemm_wn_kernel(Params p, int ntiles) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   typedef Cfg<NJ> CF;
-  constexpr int BN = CF::BN;
-  constexpr int NT = 2 * NJ;  // 16-wide n tiles per wave
+  constexpr int BN = CF::BN, NT = 2 * NJ, BNR = CF::BNR;
+  float* bias_s = reinterpret_cast<float*>(smem + NS * CF::STAGE);  // [2][BNR]
 
   const int nN = (p.N + BN - 1) / BN;
-  int tm, tn;
-  tile_of(blockIdx.x, gridDim.x, nN, tm, tn);
-  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk = (p.K + BK - 1) / BK;
+  const int G = gridDim.x, bid = blockIdx.x;
+  const int r = (G % 8 == 0) ? (bid & 7) * (G >> 3) + (bid >> 3) : bid;  // XCD-grouped tile ranks
+  const int my = r < ntiles ? (ntiles - r + G - 1) / G : 0;
+  const int S = my * nk;  // this workgroup's k-steps over all its tiles
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wm = wid >> 2, wn = wid & 3;
   const int lr = lane & 15, lk = lane >> 4;
+  const bool has_bias = p.bias != nullptr;
+  // store instructions per wave in one full-tile float4 epilogue (partial or scalar epilogues
+  // drain with vmcnt(0) instead, so this count never over-states what is in flight)
+  const int E = 4 * NT * (p.Z ? 2 : 1);
+  const bool vec = vec_ok(p);
+
+  auto coords = [&](int j, int& m0, int& n0) {
+    const int t = j * G + r;
+    m0 = (t / nN) * BM;
+    n0 = (t % nN) * BN;
+  };
+
+  Loader<NJ, CONV> ld;
+  int ld_tile = -1;
+  auto issue = [&](int s) {
+    const int j = s / nk, kt = s - j * nk;
+    int m0, n0;
+    coords(j, m0, n0);
+    if (j != ld_tile) {
+      ld.init(p, m0, n0);
+      ld_tile = j;
+    }
+    ld.issue(p, smem + (s % NS) * CF::STAGE, kt * BK);
+    if (kt == 0 && has_bias) {  // every lane of every wave issues: uniform op count per wave
+      float* dst = bias_s + (j & 1) * BNR;
+#pragma unroll
+      for (int c0 = 0; c0 < BNR; c0 += NTHR) {
+        const int c = c0 + threadIdx.x;
+        glds4((c < BN && n0 + c < p.N) ? (const void*)(p.bias + n0 + c) : (const void*)zero_page,
+              lds_addr(dst + c0 + wid * 64));
+      }
+    }
+  };
+  auto ops_of = [&](int s) { return CF::PIECES + ((s % nk == 0 && has_bias) ? CF::BIAS_OPS : 0); };
 
   f32x4 acc[4][NT];
 #pragma unroll
@@ -145,28 +229,29 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wn_kernel(Params p) {
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  Loader<NJ, CONV> ld;
-  ld.init(p, m0, n0);
-  const int nk = (p.K + BK - 1) / BK;
 #pragma unroll
-  for (int s = 0; s < NSTAGE - 1; ++s)
-    if (s < nk) ld.issue(p, smem + s * CF::STAGE, s * BK);
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < S) issue(s);
 
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) wait_vm<CF::PIECES>();
-    else wait_vm<0>();
+  for (int s = 0; s < S; ++s) {
+    // this wave's vector-memory ops younger than step s: later k-steps already issued and the
+    // epilogue stores of tiles that ended after step s was issued
+    int younger = 0;
+    for (int q = s + 1; q <= min(s + NS - 2, S - 1); ++q) younger += ops_of(q);
+    for (int it = max(s - NS + 1, 0); it < s; ++it)
+      if (it % nk == nk - 1) younger += E;
+    wait_vm_le(younger);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    const int nxt = kt + NSTAGE - 1;
-    if (nxt < nk) ld.issue(p, smem + (nxt % NSTAGE) * CF::STAGE, nxt * BK);
-    const char* At = smem + (kt % NSTAGE) * CF::STAGE;
+    if (s + NS - 1 < S) issue(s + NS - 1);  // refills the slot every wave finished reading
+    const char* At = smem + (s % NS) * CF::STAGE;
     const char* Bt = At + A_BYTES;
     bf16x8 a[4], b[NT];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
-      const int r = wm * 64 + mt * 16 + lr;
-      const int sw = (r >> 1) & 7;
-      const char* row = At + r * 128;
+      const int rr = wm * 64 + mt * 16 + lr;
+      const int sw = swa(rr);
+      const char* row = At + rr * 128;
       const float4 x = *reinterpret_cast<const float4*>(row + 16 * ((2 * lk) ^ sw));
       const float4 y = *reinterpret_cast<const float4*>(row + 16 * ((2 * lk + 1) ^ sw));
       bf16x8 v;
@@ -177,35 +262,34 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wn_kernel(Params p) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       const int n = wn * (32 * NJ) + nt * 16 + lr;
-      b[nt] = *reinterpret_cast<const bf16x8*>(Bt + n * 64 + 16 * (lk ^ ((n >> 2) & 3)));
+      b[nt] = *reinterpret_cast<const bf16x8*>(Bt + n * 64 + 16 * (lk ^ swb(n)));
     }
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt)
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt], b[nt], acc[mt][nt], 0, 0, 0);
-  }
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nt], a[mt], acc[mt][nt], 0, 0, 0);
 
-  const int lc = lane & 15, lr4 = (lane >> 4) * 4;
-#pragma unroll
-  for (int nt = 0; nt < NT; ++nt) {
-    const int col = n0 + wn * (32 * NJ) + nt * 16 + lc;
-    if (col >= p.N) continue;
-    const float bv = p.bias ? p.bias[col] : 0.f;
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * 64 + mt * 16 + lr4 + r;
-        if (row >= p.M) continue;
-        float* dst = p.C + (int64_t)row * p.ldc + col;
-        float v = p.alpha * acc[mt][nt][r] + bv;
-        if (p.beta != 0.f) v += p.beta * *dst;
-        if (p.Z) p.Z[(int64_t)row * p.ldc + col] = v;
-        *dst = apply_act(p.act, v);
+    if (s % nk == nk - 1) {  // tile done: D[n][m] layout -> lane owns C[m = lr][n = 4 lk .. 4 lk + 3]
+      const int j = s / nk;
+      int m0, n0;
+      coords(j, m0, n0);
+      const float* bsl = bias_s + (j & 1) * BNR;
+      switch (p.act) {
+        case ACT_GELU: epilogue<NJ, ACT_GELU>(p, acc, bsl, m0, n0, wm, wn, lr, lk); break;
+        case ACT_SILU: epilogue<NJ, ACT_SILU>(p, acc, bsl, m0, n0, wm, wn, lr, lk); break;
+        case ACT_SIGMOID: epilogue<NJ, ACT_SIGMOID>(p, acc, bsl, m0, n0, wm, wn, lr, lk); break;
+        case ACT_RELU: epilogue<NJ, ACT_RELU>(p, acc, bsl, m0, n0, wm, wn, lr, lk); break;
+        default: epilogue<NJ, ACT_NONE>(p, acc, bsl, m0, n0, wm, wn, lr, lk); break;
       }
+      if (!vec || m0 + BM > p.M || n0 + BN > p.N) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int q = 0; q < NT; ++q) acc[i][q] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // fp32 (rows x cols, row stride ld) -> bf16 N x K contiguous.  trans == 0: N = rows, K = cols;
@@ -229,17 +313,23 @@ __global__ void weight_to_bf16_kernel(const float* __restrict__ src, unsigned sh
   }
 }
 
-template <int NJ, bool CONV>
+template <int NJ, bool CONV, int NS>
 static void launch(const Params& p, hipStream_t s) {
   typedef Cfg<NJ> CF;
-  static bool attr = false;
-  const int shm = NSTAGE * CF::STAGE;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_wn_kernel<NJ, CONV>, hipFuncAttributeMaxDynamicSharedMemorySize, shm);
-    attr = true;
+  static int resident = 0;
+  const int shm = NS * CF::STAGE + 2 * CF::BNR * 4;
+  if (!resident) {
+    (void)hipFuncSetAttribute((const void*)gemm_wn_kernel<NJ, CONV, NS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              shm);
+    int per_cu = 0, dev = 0, cus = 0;
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)gemm_wn_kernel<NJ, CONV, NS>, NTHR, shm);
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    resident = std::max(1, per_cu) * std::max(1, cus);
   }
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + CF::BN - 1) / CF::BN);
-  gemm_wn_kernel<NJ, CONV><<<tiles, NTHR, shm, s>>>(p);
+  const int grid = std::min(tiles, resident);
+  gemm_wn_kernel<NJ, CONV, NS><<<grid, NTHR, shm, s>>>(p, tiles);
 }
 
 }  // namespace wn
@@ -270,8 +360,14 @@ extern "C" int asrx_gemm_wn(const float* A, int64_t lda, int conv, int64_t convF
   ASRX_REQUIRE(!conv || (convF > 0 && convC % 4 == 0), "asrx_gemm_wn: conv needs F > 0 and C %% 4 == 0");
   wn::Params p{A, (int)lda, W, (int)ldw, C, (int)ldc, bias, Z, (int)M, (int)N, (int)K,
                (int)(convF > 0 ? convF : 1), (int)(convC > 0 ? convC : 1), alpha, beta, act};
-  if (nj == 3) conv ? wn::launch<3, true>(p, stream) : wn::launch<3, false>(p, stream);
-  else if (nj == 2) conv ? wn::launch<2, true>(p, stream) : wn::launch<2, false>(p, stream);
-  else conv ? wn::launch<1, true>(p, stream) : wn::launch<1, false>(p, stream);
+  // ring depth: 3 stages for short K (more tile switches to hide), 2 for long K (measured)
+  if (nj == 3) {
+    if (K <= 512) conv ? wn::launch<3, true, 3>(p, stream) : wn::launch<3, false, 3>(p, stream);
+    else conv ? wn::launch<3, true, 2>(p, stream) : wn::launch<3, false, 2>(p, stream);
+  } else if (nj == 2) {
+    conv ? wn::launch<2, true, 2>(p, stream) : wn::launch<2, false, 2>(p, stream);
+  } else {
+    conv ? wn::launch<1, true, 3>(p, stream) : wn::launch<1, false, 3>(p, stream);
+  }
   ASRX_LAUNCHED("asrx_gemm_wn");
 }

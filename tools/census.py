@@ -1,0 +1,48 @@
+"""Launch census of one training step without a GPU: asrx.lib.call is replaced by a recorder and
+the model runs on CPU tensors (kernels are not executed, values are garbage).  Lists every C-ABI
+call with its problem sizes, so launch counts and GEMM shapes can be read off per step."""
+import collections
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "asr-model_amd")]
+import torch  # noqa: E402
+
+from asrx import lib  # noqa: E402
+
+calls = []
+lib.call = lambda name, *a: calls.append((name, a))
+lib.require_gpu = lambda *t: None
+lib.load = lambda: type("L", (), {"asrx_msheath_rec_bytes": staticmethod(lambda: 36)})()
+
+from asrx import prec, synth  # noqa: E402
+from asrx.config import CONFIGS  # noqa: E402
+from asrx.model import Model  # noqa: E402
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+prec.set_precision("bf16")
+torch.cuda.current_stream = lambda: type("S", (), {"cuda_stream": 0})()
+cfg = CONFIGS["tiny"]
+model = Model(cfg).train()
+model.set_noise(seed=0, step=0)
+wav = synth.waveform(B, 30.0)
+pitch = synth.pitch(B)
+ids, labels = synth.text(B, 256, cfg.tokens)
+spec = torch.zeros(B, 128, 3001)
+wf = torch.zeros(B, 1, 3000)
+out = model(labels=labels, text_ids=ids, spectrogram=spec, pitch=pitch, waveform=wf)
+nf = len(calls)
+out["loss"].backward()
+c = collections.Counter(n for n, _ in calls)
+print(f"calls fwd {nf} bwd {len(calls)-nf}")
+for n, v in c.most_common():
+    print(f"{v:6d} {n}")
+g = collections.Counter()
+for n, a in calls:
+    if n == "asrx_gemm_wn":
+        g[("wn", a[11], a[12], a[13], a[17], a[2])] += 1  # M N K nj conv
+    elif n == "asrx_gemm":
+        g[("gemm", a[16], a[17], a[18], a[19], a[4], a[9])] += 1  # M N K batch a_kc b_kc
+for k, v in sorted(g.items(), key=lambda kv: -kv[1] * kv[0][1] * kv[0][2] * kv[0][3]):
+    print(v, k)
