@@ -43,14 +43,17 @@ def weight_bf16(W, trans=False, cache=True):
     """bf16 N x K copy of a weight: W is (N, K) (trans=False) or (K, N) (trans=True)."""
     key = (W.data_ptr(), tuple(W.shape), tuple(W.stride()), bool(trans), W._version) if cache else None
     if key is not None and key in _WCACHE:
-        return _WCACHE[key]
+        return _WCACHE[key][1]
+    src = W
     rows, cols = W.shape
     if W.stride(1) != 1:
         W = W.contiguous()
     out = torch.empty((cols, rows) if trans else (rows, cols), dtype=torch.int16, device=W.device)
     lib.call("asrx_weight_to_bf16", lib.ptr(W), lib.ptr(out), rows, cols, W.stride(0), int(trans), lib.stream())
     if key is not None:
-        _WCACHE[key] = out
+        # the entry holds the source tensor too, so its address cannot be recycled for another
+        # tensor (which would alias the key) while the entry lives
+        _WCACHE[key] = (src, out)
     return out
 
 
@@ -79,6 +82,21 @@ def gemm_wn(A, Wb, C, *, M, N, K, lda, ldc, bias=None, Z=None, alpha=1.0, beta=0
              lib.stream())
     probe.end("gemm", e0, 2.0 * M * N * K)
     return C
+
+
+def router_fwd(x2, W1, b1, W2, keep_hpre):
+    """AbbyNormal router in one GEMM pass: (hpre or None, logits (M, 3) without b2)."""
+    M, K = x2.shape
+    N = W1.shape[0]
+    Wb = weight_bf16(W1)
+    hpre = torch.empty(M, N, device=x2.device) if keep_hpre else None
+    logits = torch.empty(M, 3, device=x2.device)
+    lib.require_gpu(x2, Wb, logits)
+    e0 = probe.begin("gemm")
+    lib.call("asrx_gemm_wn_router", lib.ptr(x2), K, lib.ptr(Wb), Wb.stride(0), lib.ptr(b1), lib.ptr(W2),
+             lib.ptr(hpre), N, lib.ptr(logits), M, N, K, lib.stream())
+    probe.end("gemm", e0, 2.0 * M * N * K)
+    return hpre, logits
 
 
 def use_wide(K) -> bool:

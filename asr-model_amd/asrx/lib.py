@@ -35,6 +35,7 @@ SIGNATURES = {
          _i64, _i64, _i64, _i64, _f32, _f32, _i32, _i64, _i64, _i32, _p],
     ),
     "asrx_abby_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _u32, _i32, _p]),
+    "asrx_abby_fwd_logits": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _u32, _i32, _p]),
     "asrx_abby_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _p]),
     "asrx_attn_fwd": (_i32, [_i32, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i32, _f32, _p]),
     "asrx_attn_bwd": (_i32, [_i32, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p,
@@ -86,6 +87,7 @@ SIGNATURES = {
     "asrx_ce_bwd": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _p]),
     "asrx_policy_noise": (_i32, [_p, _i64, _i64, _i64, _u32, _p]),
     "asrx_weight_to_bf16": (_i32, [_p, _p, _i64, _i64, _i64, _i32, _p]),
+    "asrx_gemm_wn_router": (_i32, [_p, _i64, _p, _i64, _p, _p, _p, _i64, _p, _i64, _i64, _i64, _p]),
     "asrx_gemm_wn": (_i32, [_p, _i64, _i32, _i64, _i64, _p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _f32, _f32,
                             _i32, _i32, _p]),
 }

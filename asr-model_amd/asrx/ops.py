@@ -112,16 +112,23 @@ class AbbyNormalFn(torch.autograd.Function):
     """essentials.AbbyNormal (essentials.py:155-191): router GEMM on MFMA + fused row kernel."""
 
     @staticmethod
-    def forward(ctx, x, W1, b1, W2, b2, L, H, sid_base, key, use_noise):
+    def forward(ctx, x, W1, b1, W2, b2, L, H, sid_base, key, use_noise, keep):
         x = _c(x)
         d = x.shape[-1]
         rows = _rows(x)
-        hpre = G.linear_fwd(x, W1, b1)
         out = _E(x.shape, device=x.device)
         ys = _E(rows, 3, device=x.device)
         idx = _E(rows, dtype=torch.int32, device=x.device)
-        lib.call("asrx_abby_fwd", _P(x), _P(hpre), _P(W2), _P(b2), _P(out), _P(ys), _P(idx), rows, d, L, H,
-                 sid_base, key & 0xFFFFFFFF, int(use_noise), _S())
+        if G.use_wide(d) and d <= 384:
+            # perf mode: the router's d x d GEMM also applies SiLU and Linear(d, 3) in its epilogue,
+            # so h_pre never makes the HBM round trip unless the backward needs it
+            hpre, logits = G.router_fwd(x.view(rows, d), W1, b1, W2, keep)
+            lib.call("asrx_abby_fwd_logits", _P(x), _P(logits), _P(b2), _P(out), _P(ys), _P(idx), rows, d, L, H,
+                     sid_base, key & 0xFFFFFFFF, int(use_noise), _S())
+        else:
+            hpre = G.linear_fwd(x, W1, b1)
+            lib.call("asrx_abby_fwd", _P(x), _P(hpre), _P(W2), _P(b2), _P(out), _P(ys), _P(idx), rows, d, L, H,
+                     sid_base, key & 0xFFFFFFFF, int(use_noise), _S())
         ctx.save_for_backward(x, hpre, W1, W2, ys, idx)
         return out
 
@@ -140,12 +147,14 @@ class AbbyNormalFn(torch.autograd.Function):
         G.linear_dgrad(dh, W1, out=dx, beta=1.0)
         dW1 = G.linear_wgrad(dh, x)
         db1 = colsum(dh.view(-1, d))
-        return dx, dW1, db1, dW2, db2, None, None, None, None, None
+        return dx, dW1, db1, dW2, db2, None, None, None, None, None, None
 
 
 def abby_normal(mod, x, L, H, sid_base, key, use_noise=True):
     r = mod.mode_router
-    return AbbyNormalFn.apply(x, r[0].weight, r[0].bias, r[2].weight, r[2].bias, L, H, sid_base, key, use_noise)
+    keep = torch.is_grad_enabled() and (x.requires_grad or r[0].weight.requires_grad)
+    return AbbyNormalFn.apply(x, r[0].weight, r[0].bias, r[2].weight, r[2].bias, L, H, sid_base, key, use_noise,
+                              keep)
 
 
 # =============================================================================== LayerNorm

@@ -97,7 +97,8 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_fwd_kernel(const float* 
                                                                   const float* __restrict__ W2,
                                                                   const float* __restrict__ b2,
                                                                   float* __restrict__ out, float* __restrict__ ys,
-                                                                  int* __restrict__ idx_out, AbbyGeom g) {
+                                                                  int* __restrict__ idx_out, AbbyGeom g,
+                                                                  const float* __restrict__ logits) {
   __shared__ float sq_all[ABBY_WAVES][64 * ABBY_MAXE];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   float* sq = sq_all[wid];
@@ -105,22 +106,34 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_fwd_kernel(const float* 
   const int w = abby_window(d);
   for (int64_t r = (int64_t)blockIdx.x * ABBY_WAVES + wid; r < g.rows; r += (int64_t)gridDim.x * ABBY_WAVES) {
     const float* xr = x + r * d;
-    const float* hr = hpre + r * d;
     float xv[ABBY_MAXE];
     float l0 = 0.f, l1 = 0.f, l2 = 0.f;
+    if (logits) {  // router logits from the GEMM epilogue (asrx_gemm_wn_router)
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const int j = e * 64 + lane;
-      xv[e] = xr[j];
-      const float hs = silu_f(hr[j]);
-      l0 += hs * W2[j];
-      l1 += hs * W2[d + j];
-      l2 += hs * W2[2 * d + j];
-      sq[j] = xv[e] * xv[e];
+      for (int e = 0; e < E; ++e) {
+        const int j = e * 64 + lane;
+        xv[e] = xr[j];
+        sq[j] = xv[e] * xv[e];
+      }
+      l0 = logits[r * 3 + 0];
+      l1 = logits[r * 3 + 1];
+      l2 = logits[r * 3 + 2];
+    } else {
+      const float* hr = hpre + r * d;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int j = e * 64 + lane;
+        xv[e] = xr[j];
+        const float hs = silu_f(hr[j]);
+        l0 += hs * W2[j];
+        l1 += hs * W2[d + j];
+        l2 += hs * W2[2 * d + j];
+        sq[j] = xv[e] * xv[e];
+      }
+      l0 = wave_sum(l0);
+      l1 = wave_sum(l1);
+      l2 = wave_sum(l2);
     }
-    l0 = wave_sum(l0);
-    l1 = wave_sum(l1);
-    l2 = wave_sum(l2);
     float mu, sd, mabs;
     abby_row_stats<E>(xv, d, mu, sd, mabs);
     const float cv = sd / (mabs + 1e-6f);
@@ -367,8 +380,22 @@ extern "C" int asrx_abby_fwd(const float* x, const float* hpre, const float* W2,
   const int E = (int)(d / 64);
   AbbyGeom g = make_geom(rows, d, L, H, sid_base, key, use_noise);
   const unsigned grid = (unsigned)std::min<int64_t>((rows + ABBY_WAVES - 1) / ABBY_WAVES, 4096);
-  ABBY_DISPATCH(abby_fwd_kernel, x, hpre, W2, b2, out, ys, idx, g);
+  ABBY_DISPATCH(abby_fwd_kernel, x, hpre, W2, b2, out, ys, idx, g, nullptr);
   ASRX_LAUNCHED("asrx_abby_fwd");
+}
+
+// Same, with the router logits (rows x 3, without b2) precomputed by asrx_gemm_wn_router.
+extern "C" int asrx_abby_fwd_logits(const float* x, const float* logits, const float* b2, float* out, float* ys,
+                                    int* idx, int64_t rows, int64_t d, int64_t L, int64_t H, int64_t sid_base,
+                                    uint32_t key, int use_noise, hipStream_t stream) {
+  ASRX_REQUIRE(d % 64 == 0 && d >= 64 && d <= 1024, "AbbyNormal: d=%ld must be a multiple of 64 in [64,1024]",
+               (long)d);
+  if (rows == 0) return 0;
+  const int E = (int)(d / 64);
+  AbbyGeom g = make_geom(rows, d, L, H, sid_base, key, use_noise);
+  const unsigned grid = (unsigned)std::min<int64_t>((rows + ABBY_WAVES - 1) / ABBY_WAVES, 4096);
+  ABBY_DISPATCH(abby_fwd_kernel, x, nullptr, nullptr, b2, out, ys, idx, g, logits);
+  ASRX_LAUNCHED("asrx_abby_fwd_logits");
 }
 
 // dW2 / db2 are accumulated (caller zeroes them).  dx, dhpre are overwritten.

@@ -14,6 +14,7 @@
 // PREC_BF16 rounds MFMA operands (Q, K, V, P, dO, dS) to bf16 with fp32 accumulation;
 // PREC_F32 uses exact fp32 MFMA (parity mode).
 #include "common.h"
+#include <cstdlib>
 
 namespace asrx {
 
@@ -407,6 +408,12 @@ using namespace asrx;
 static bool attn_ok(const int64_t* st) { return st[0] % 4 == 0 && st[1] % 4 == 0 && st[2] % 4 == 0; }
 
 // Strides are passed as int64[3] = {batch, seq, head} in elements; the head-dim stride must be 1.
+namespace asrx {
+int attn_fwd_mf(const float* q, const int64_t* sq, const float* k, const int64_t* sk, const float* v,
+                const int64_t* sv, float* o, const int64_t* so, float* lse, int64_t B, int64_t H, int64_t Lq,
+                int64_t Lk, int causal, float scale, hipStream_t stream);
+}
+
 extern "C" int asrx_attn_fwd(int prec, const float* q, const int64_t* sq, const float* k, const int64_t* sk,
                              const float* v, const int64_t* sv, float* o, const int64_t* so, float* lse, int64_t B,
                              int64_t H, int64_t Lq, int64_t Lk, int64_t hd, int causal, float scale,
@@ -418,7 +425,10 @@ extern "C" int asrx_attn_fwd(int prec, const float* q, const int64_t* sq, const 
   ASRX_REQUIRE(Lk > 0, "attention: empty key sequence");
   dim3 g((unsigned)((Lq + ATILE - 1) / ATILE), (unsigned)H, (unsigned)B);
   AttnStrides Sq{sq[0], sq[1], sq[2]}, Sk{sk[0], sk[1], sk[2]}, Sv{sv[0], sv[1], sv[2]}, So{so[0], so[1], so[2]};
-  if (prec == PREC_BF16)
+  const bool al16 = (((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)o) & 15) == 0;
+  if (prec == PREC_BF16 && al16 && getenv("ASRX_ATTN_OLD") == nullptr)
+    attn_fwd_mf(q, sq, k, sk, v, sv, o, so, lse, B, H, Lq, Lk, causal, scale, stream);
+  else if (prec == PREC_BF16)
     attn_fwd_kernel<PREC_BF16><<<g, 256, 0, stream>>>(q, k, v, o, lse, Sq, Sk, Sv, So, H, Lq, Lk, causal, scale);
   else
     attn_fwd_kernel<PREC_F32><<<g, 256, 0, stream>>>(q, k, v, o, lse, Sq, Sk, Sv, So, H, Lq, Lk, causal, scale);

@@ -1,0 +1,247 @@
+// Flash-attention forward for the perf (bf16 MFMA) mode: F.scaled_dot_product_attention at
+// model.py:307, head dim 64, non-causal or causal (top-left), Lq != Lk, ragged tails; q/k/v/o fp32
+// (B, L, H, 64) with arbitrary strides, lse (B, H, Lq) natural log (consumed by the backward).
+//
+// Workgroup = 8 waves = 256 query rows of one (b, h); wave = 32 rows.  Per 64-key tile:
+//   S^T = K Q^T     8 x v_mfma_f32_32x32x16_bf16 (K rows from LDS, Q^T fragments held in registers)
+//                   -> each lane owns ONE query row (lane & 31) and 32 of the tile's 64 keys, so the
+//                   row max is 31 in-lane fmax + one xor-32 exchange, and l is a per-lane partial sum
+//   P^T = exp2(S^T * scale * log2e - m)   in registers, packed to bf16: the packed registers ARE the
+//                   B operand of the next product (no LDS round trip, no lane permutes)
+//   O^T += V^T P^T  8 x 32x32x16 MFMA, V^T fragments by ds_read_b64_tr_b16 (hardware transpose read
+//                   of the row-major V tile), so O^T keeps the query on the lane too: the online-
+//                   softmax rescale and the final 1/l are lane-local
+// K/V tiles are register-staged (issue the next tile's global loads before the MFMAs, convert to
+// bf16 and write LDS after them), double-buffered, one barrier per tile.  LDS images are XOR-
+// swizzled at 16-byte granularity: K for the ds_read_b128 row reads, V for the transposed reads
+// (both bank-conflict-free under the gfx950 lane-group rules).
+#include "common.h"
+
+namespace asrx {
+
+struct AttnStridesMF {
+  int64_t b, l, h;
+};
+
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+
+namespace amf {
+
+constexpr int QB = 256;  // query rows per workgroup
+constexpr int KT = 64;   // keys per tile
+constexpr int NTHR = 512;
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+
+__device__ __forceinline__ int kswz(int key) { return (key >> 1) & 7; }
+__device__ __forceinline__ int vswz(int key) { return ((key >> 1) & 1) << 2; }
+
+__device__ __forceinline__ unsigned pack2(float a, float b) {
+  const unsigned lo = __builtin_bit_cast(unsigned short, (__bf16)a);
+  const unsigned hi = __builtin_bit_cast(unsigned short, (__bf16)b);
+  return lo | (hi << 16);
+}
+
+__device__ __forceinline__ bf16x8 pack8(const float (&v)[8]) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 u = {pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7])};
+  return __builtin_bit_cast(bf16x8, u);
+}
+
+// one 16-byte chunk (8 consecutive d) of one key row of a K or V tile: fp32 -> bf16 -> LDS.
+// Rows past Lk load the last row (always in bounds) and are zeroed, so there is no branch.
+__device__ __forceinline__ void stage_load(const float* base, AttnStridesMF st, int64_t key, int64_t Lk, int c,
+                                           float4& a, float4& b) {
+  const int64_t kc = key < Lk ? key : Lk - 1;
+  const float* p = base + kc * st.l + 8 * c;
+  a = *reinterpret_cast<const float4*>(p);
+  b = *reinterpret_cast<const float4*>(p + 4);
+  if (key >= Lk) {
+    a = make_float4(0.f, 0.f, 0.f, 0.f);
+    b = a;
+  }
+}
+__device__ __forceinline__ void stage_store(unsigned short* tile, int key, int pc, const float4& a, const float4& b) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 u = {pack2(a.x, a.y), pack2(a.z, a.w), pack2(b.x, b.y), pack2(b.z, b.w)};
+  *reinterpret_cast<u32x4*>(tile + key * 64 + 8 * pc) = u;
+}
+
+__global__ __launch_bounds__(NTHR, 1) void attn_fwd_mf_kernel(const float* __restrict__ q, const float* __restrict__ k,
+                                                              const float* __restrict__ v, float* __restrict__ o,
+                                                              float* __restrict__ lse, AttnStridesMF sq,
+                                                              AttnStridesMF sk, AttnStridesMF sv, AttnStridesMF so,
+                                                              int64_t H, int64_t Lq, int64_t Lk, int causal,
+                                                              float scale) {
+  __shared__ __attribute__((aligned(16))) unsigned short Ks[2][KT * 64];
+  __shared__ __attribute__((aligned(16))) unsigned short Vs[2][KT * 64];
+
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int64_t q0 = (int64_t)blockIdx.x * QB;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int j = lane & 31, hi = lane >> 5;
+  const int64_t qi = q0 + wid * 32 + j;  // this lane's query row
+  const float* qb = q + b * sq.b + h * sq.h;
+  const float* kb = k + b * sk.b + h * sk.h;
+  const float* vb = v + b * sv.b + h * sv.h;
+  const float c = scale * LOG2E;
+
+  // Q^T fragments (B operand): lane (q = j, hi) holds Q[q][16 s + 8 hi .. +7], s = 0..3
+  bf16x8 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    float t[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (qi < Lq) {
+      const float* p = qb + qi * sq.l + 16 * s + 8 * hi;
+      const float4 x = *reinterpret_cast<const float4*>(p), y = *reinterpret_cast<const float4*>(p + 4);
+      t[0] = x.x; t[1] = x.y; t[2] = x.z; t[3] = x.w; t[4] = y.x; t[5] = y.y; t[6] = y.z; t[7] = y.w;
+    }
+    qf[s] = pack8(t);
+  }
+
+  int64_t kend = Lk;
+  if (causal) kend = min(Lk, q0 + QB);
+  const int ntiles = (int)((kend + KT - 1) / KT);
+  const int skey = tid >> 3, sc = tid & 7;  // staging: one 16-B chunk of one key row per thread
+
+  float4 ka, kb4, va, vb4;
+  stage_load(kb, sk, skey, Lk, sc, ka, kb4);
+  stage_load(vb, sv, skey, Lk, sc, va, vb4);
+  stage_store(Ks[0], skey, sc ^ kswz(skey), ka, kb4);
+  stage_store(Vs[0], skey, sc ^ vswz(skey), va, vb4);
+  __syncthreads();
+
+  f32x16 oacc[2];
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) oacc[d][r] = 0.f;
+  float m = -INFINITY;  // running max of raw scores (log2 domain after * c)
+  float l = 0.f;        // partial (this half's keys) running denominator
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    const int64_t k0 = (int64_t)t * KT;
+    if (t + 1 < ntiles) {  // next tile's loads fly under this tile's MFMAs
+      stage_load(kb, sk, k0 + KT + skey, Lk, sc, ka, kb4);
+      stage_load(vb, sv, k0 + KT + skey, Lk, sc, va, vb4);
+    }
+    const unsigned short* Kt = Ks[buf];
+    const unsigned short* Vt = Vs[buf];
+
+    // ---- S^T = K Q^T : two 32-key blocks
+    f32x16 sacc[2];
+#pragma unroll
+    for (int kb2 = 0; kb2 < 2; ++kb2) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sacc[kb2][r] = 0.f;
+      const int key = 32 * kb2 + j;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(Kt + key * 64 + 8 * ((2 * s + hi) ^ kswz(key)));
+        sacc[kb2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s], sacc[kb2], 0, 0, 0);
+      }
+    }
+
+    // ---- mask + online softmax (lane = query j, keys crow(r, hi) of each block)
+    const bool need_mask = (k0 + KT > Lk) || (causal && k0 + KT - 1 > q0 + wid * 32);
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int kb2 = 0; kb2 < 2; ++kb2)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float x = sacc[kb2][r];
+        if (need_mask) {
+          const int64_t key = k0 + 32 * kb2 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+          if (key >= Lk || (causal && key > qi)) x = -INFINITY;
+          sacc[kb2][r] = x;
+        }
+        tmax = fmaxf(tmax, x);
+      }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+    const float mnew = fmaxf(m, tmax);
+    const float mc = mnew == -INFINITY ? 0.f : mnew * c;       // a row with no valid key yet: p = 0
+    const float alpha = __builtin_amdgcn_exp2f(m * c - mc);   // m = -inf on the first tile -> 0
+    m = mnew;
+    bf16x8 pb[2][2];
+    float lsum = 0.f;
+#pragma unroll
+    for (int kb2 = 0; kb2 < 2; ++kb2)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        float pv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          pv[e] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[kb2][8 * s2 + e], c, -mc));
+          lsum += pv[e];
+        }
+        pb[kb2][s2] = pack8(pv);
+      }
+    l = l * alpha + lsum;
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) oacc[d][r] *= alpha;
+
+    // ---- O^T += V^T P^T
+    const int g = lane >> 4, gi = lane & 15;
+    const int trow = gi >> 2, tcol = 4 * (gi & 3);
+#pragma unroll
+    for (int kb2 = 0; kb2 < 2; ++kb2)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int kbase = 32 * kb2 + 16 * s2 + 4 * (g >> 1);
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          const int col = 32 * d + 16 * (g & 1) + tcol;
+          const int key1 = kbase + trow, key2 = kbase + 8 + trow;
+          const v4i16 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_v4i16*)(Vt + key1 * 64 + 8 * ((col >> 3) ^ vswz(key1)) + (col & 7)));
+          const v4i16 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_v4i16*)(Vt + key2 * 64 + 8 * ((col >> 3) ^ vswz(key2)) + (col & 7)));
+          typedef short v8i16 __attribute__((ext_vector_type(8)));
+          const v8i16 a8 = {t1[0], t1[1], t1[2], t1[3], t2[0], t2[1], t2[2], t2[3]};
+          oacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a8), pb[kb2][s2], oacc[d],
+                                                              0, 0, 0);
+        }
+      }
+
+    if (t + 1 < ntiles) {  // every wave finished reading buf^1 (tile t-1) before the last barrier
+      stage_store(Ks[buf ^ 1], skey, sc ^ kswz(skey), ka, kb4);
+      stage_store(Vs[buf ^ 1], skey, sc ^ vswz(skey), va, vb4);
+    }
+    __syncthreads();
+  }
+
+  // ---- finalize: l over both halves, O = O^T / l, lse in natural log
+  const float lt = l + __shfl_xor(l, 32);
+  if (qi < Lq) {
+    const float inv = 1.0f / lt;
+    float* orow = o + b * so.b + h * so.h + qi * so.l;
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int dd = 32 * d + 8 * g4 + 4 * hi;
+        *reinterpret_cast<float4*>(orow + dd) =
+            make_float4(oacc[d][4 * g4] * inv, oacc[d][4 * g4 + 1] * inv, oacc[d][4 * g4 + 2] * inv,
+                        oacc[d][4 * g4 + 3] * inv);
+      }
+    if (hi == 0) lse[((int64_t)b * H + h) * Lq + qi] = (m * c + __builtin_amdgcn_logf(lt)) * LN2;
+  }
+}
+
+}  // namespace amf
+
+// bf16 flash-attention forward (see header); called by asrx_attn_fwd for prec == PREC_BF16.
+int attn_fwd_mf(const float* q, const int64_t* sq, const float* k, const int64_t* sk, const float* v,
+                const int64_t* sv, float* o, const int64_t* so, float* lse, int64_t B, int64_t H, int64_t Lq,
+                int64_t Lk, int causal, float scale, hipStream_t stream) {
+  dim3 g((unsigned)((Lq + amf::QB - 1) / amf::QB), (unsigned)H, (unsigned)B);
+  AttnStridesMF Sq{sq[0], sq[1], sq[2]}, Sk{sk[0], sk[1], sk[2]}, Sv{sv[0], sv[1], sv[2]}, So{so[0], so[1], so[2]};
+  amf::attn_fwd_mf_kernel<<<g, amf::NTHR, 0, stream>>>(q, k, v, o, lse, Sq, Sk, Sv, So, H, Lq, Lk, causal, scale);
+  return 0;
+}
+
+}  // namespace asrx

@@ -42,6 +42,8 @@ struct Params {
   int convF, convC;
   float alpha, beta;
   int act;
+  const float* W2;  // router: Linear(d, 3) weight (3 x N) applied to SiLU(C) in the epilogue
+  float* R;         // router: logits without bias (M x 3); C may be null (h_pre not kept)
 };
 
 template <int NJ>
@@ -172,12 +174,85 @@ __device__ __forceinline__ void epilogue(const Params& p, f32x4 (&acc)[4][2 * NJ
   }
 }
 
-template <int NJ, bool CONV, int NS>
+// AbbyNormal router epilogue (essentials.py:155-161): h = alpha*acc + bias is h_pre; the tile holds
+// whole rows (N <= BN), so logits[row][k] = sum_n SiLU(h[row][n]) W2[k][n] reduce in-tile: over
+// each lane's 4 columns and NT sub-tiles, across the 4 lanes of a row (shuffles) and across the 4
+// column waves (LDS).  h_pre is stored only when C != null (it is needed by the backward).
+template <int NJ>
+__device__ __forceinline__ void epilogue_router(const Params& p, f32x4 (&acc)[4][2 * NJ], const float* bsl,
+                                                const float* w2s, float* red, int m0, int wm, int wn, int lr,
+                                                int lk) {
+  constexpr int NT = 2 * NJ, BNL = 128 * NJ;
+  const bool vec = vec_ok(p);
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    const int row = m0 + wm * 64 + mt * 16 + lr;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int nl = wn * (32 * NJ) + nt * 16 + 4 * lk;
+      if (nl >= p.N) continue;
+      float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (p.bias) bv = *reinterpret_cast<const float4*>(bsl + nl);
+      const float v[4] = {p.alpha * acc[mt][nt][0] + bv.x, p.alpha * acc[mt][nt][1] + bv.y,
+                          p.alpha * acc[mt][nt][2] + bv.z, p.alpha * acc[mt][nt][3] + bv.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (nl + q < p.N) {
+          const float h = silu_f(v[q]);
+          s0 += h * w2s[nl + q];
+          s1 += h * w2s[BNL + nl + q];
+          s2 += h * w2s[2 * BNL + nl + q];
+        }
+      }
+      if (p.C && row < p.M) {
+        float* dst = p.C + (int64_t)row * p.ldc + nl;
+        if (vec) {
+          *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (nl + q < p.N) dst[q] = v[q];
+        }
+      }
+    }
+    s0 += __shfl_xor(s0, 16); s1 += __shfl_xor(s1, 16); s2 += __shfl_xor(s2, 16);
+    s0 += __shfl_xor(s0, 32); s1 += __shfl_xor(s1, 32); s2 += __shfl_xor(s2, 32);
+    if (lk == 0) {
+      float* rr = red + ((wm * 64 + mt * 16 + lr) * 4 + wn) * 3;
+      rr[0] = s0; rr[1] = s1; rr[2] = s2;
+    }
+  }
+  // LDS writes visible, then barrier -- not __syncthreads(), whose fence would emit vmcnt(0) and
+  // drain the next tile's LDS-DMA prefetch
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  for (int i = threadIdx.x; i < BM * 3; i += NTHR) {
+    const int rl = i / 3, k = i % 3;
+    const int row = m0 + rl;
+    if (row < p.M) {
+      const float* rr = red + rl * 12 + k;
+      p.R[(int64_t)row * 3 + k] = rr[0] + rr[3] + rr[6] + rr[9];
+    }
+  }
+}
+
+template <int NJ, bool CONV, int NS, bool RT>
 __global__ __launch_bounds__(NTHR, 1) void gemm_wn_kernel(Params p, int ntiles) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   typedef Cfg<NJ> CF;
   constexpr int BN = CF::BN, NT = 2 * NJ, BNR = CF::BNR;
   float* bias_s = reinterpret_cast<float*>(smem + NS * CF::STAGE);  // [2][BNR]
+  float* w2s = bias_s + 2 * BNR;   // RT: W2 (3 x BN), staged once
+  float* red = w2s + 3 * BN;       // RT: [BM][4][3] cross-wave logit partials
+  if constexpr (RT) {  // before any LDS-DMA is in flight, so the compiler's own waits cost nothing
+    for (int i = threadIdx.x; i < 3 * BN; i += NTHR) {
+      const int k = i / BN, n = i % BN;
+      w2s[i] = n < p.N ? p.W2[k * p.N + n] : 0.f;
+    }
+    __syncthreads();
+  }
 
   const int nN = (p.N + BN - 1) / BN;
   const int nk = (p.K + BK - 1) / BK;
@@ -191,7 +266,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wn_kernel(Params p, int ntiles) 
   const bool has_bias = p.bias != nullptr;
   // store instructions per wave in one full-tile float4 epilogue (partial or scalar epilogues
   // drain with vmcnt(0) instead, so this count never over-states what is in flight)
-  const int E = 4 * NT * (p.Z ? 2 : 1);
+  const int E = RT ? (p.C ? 4 * NT : 0) : 4 * NT * (p.Z ? 2 : 1);
   const bool vec = vec_ok(p);
 
   auto coords = [&](int j, int& m0, int& n0) {
@@ -275,7 +350,9 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wn_kernel(Params p, int ntiles) 
       int m0, n0;
       coords(j, m0, n0);
       const float* bsl = bias_s + (j & 1) * BNR;
-      switch (p.act) {
+      if constexpr (RT) {
+        epilogue_router<NJ>(p, acc, bsl, w2s, red, m0, wm, wn, lr, lk);
+      } else switch (p.act) {
         case ACT_GELU: epilogue<NJ, ACT_GELU>(p, acc, bsl, m0, n0, wm, wn, lr, lk); break;
         case ACT_SILU: epilogue<NJ, ACT_SILU>(p, acc, bsl, m0, n0, wm, wn, lr, lk); break;
         case ACT_SIGMOID: epilogue<NJ, ACT_SIGMOID>(p, acc, bsl, m0, n0, wm, wn, lr, lk); break;
@@ -313,23 +390,23 @@ __global__ void weight_to_bf16_kernel(const float* __restrict__ src, unsigned sh
   }
 }
 
-template <int NJ, bool CONV, int NS>
+template <int NJ, bool CONV, int NS, bool RT = false>
 static void launch(const Params& p, hipStream_t s) {
   typedef Cfg<NJ> CF;
   static int resident = 0;
-  const int shm = NS * CF::STAGE + 2 * CF::BNR * 4;
+  const int shm = NS * CF::STAGE + 2 * CF::BNR * 4 + (RT ? (3 * CF::BN + BM * 12) * 4 : 0);
   if (!resident) {
-    (void)hipFuncSetAttribute((const void*)gemm_wn_kernel<NJ, CONV, NS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)gemm_wn_kernel<NJ, CONV, NS, RT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               shm);
     int per_cu = 0, dev = 0, cus = 0;
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)gemm_wn_kernel<NJ, CONV, NS>, NTHR, shm);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)gemm_wn_kernel<NJ, CONV, NS, RT>, NTHR, shm);
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     resident = std::max(1, per_cu) * std::max(1, cus);
   }
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + CF::BN - 1) / CF::BN);
   const int grid = std::min(tiles, resident);
-  gemm_wn_kernel<NJ, CONV, NS><<<grid, NTHR, shm, s>>>(p, tiles);
+  gemm_wn_kernel<NJ, CONV, NS, RT><<<grid, NTHR, shm, s>>>(p, tiles);
 }
 
 }  // namespace wn
@@ -359,7 +436,7 @@ extern "C" int asrx_gemm_wn(const float* A, int64_t lda, int conv, int64_t convF
   ASRX_REQUIRE(M * lda < (1LL << 31) && N * ldw < (1LL << 31), "asrx_gemm_wn: operand spans >= 2^31 elements");
   ASRX_REQUIRE(!conv || (convF > 0 && convC % 4 == 0), "asrx_gemm_wn: conv needs F > 0 and C %% 4 == 0");
   wn::Params p{A, (int)lda, W, (int)ldw, C, (int)ldc, bias, Z, (int)M, (int)N, (int)K,
-               (int)(convF > 0 ? convF : 1), (int)(convC > 0 ? convC : 1), alpha, beta, act};
+               (int)(convF > 0 ? convF : 1), (int)(convC > 0 ? convC : 1), alpha, beta, act, nullptr, nullptr};
   // ring depth: 3 stages for short K (more tile switches to hide), 2 for long K (measured)
   if (nj == 3) {
     if (K <= 512) conv ? wn::launch<3, true, 3>(p, stream) : wn::launch<3, false, 3>(p, stream);
@@ -370,4 +447,23 @@ extern "C" int asrx_gemm_wn(const float* A, int64_t lda, int conv, int64_t convF
     conv ? wn::launch<1, true, 3>(p, stream) : wn::launch<1, false, 3>(p, stream);
   }
   ASRX_LAUNCHED("asrx_gemm_wn");
+}
+
+// AbbyNormal router (essentials.py:155-161) in one pass: h_pre = A W1^T + b1 (kept in hpre when
+// non-null, for the backward) and logits = SiLU(h_pre) W2^T (M x 3, without b2), for d <= 384.
+extern "C" int asrx_gemm_wn_router(const float* A, int64_t lda, const unsigned short* W1, int64_t ldw,
+                                   const float* b1, const float* W2, float* hpre, int64_t ldc, float* logits,
+                                   int64_t M, int64_t N, int64_t K, hipStream_t stream) {
+  ASRX_REQUIRE(M > 0 && N > 0 && K > 0, "asrx_gemm_wn_router: empty problem");
+  ASRX_REQUIRE(N <= 384, "asrx_gemm_wn_router: N must be <= 384 (one tile column)");
+  ASRX_REQUIRE(((uintptr_t)A & 15) == 0 && ((uintptr_t)W1 & 15) == 0, "asrx_gemm_wn_router: A/W must be 16-byte aligned");
+  ASRX_REQUIRE(K % 8 == 0 && lda % 4 == 0 && ldw % 8 == 0, "asrx_gemm_wn_router: K%%8, lda%%4, ldw%%8 required");
+  ASRX_REQUIRE(M * lda < (1LL << 31), "asrx_gemm_wn_router: operand spans >= 2^31 elements");
+  wn::Params p{A, (int)lda, W1, (int)ldw, hpre, (int)ldc, b1, nullptr, (int)M, (int)N, (int)K, 1, 1, 1.f, 0.f,
+               ACT_NONE, W2, logits};
+  if (N <= 128) wn::launch<1, false, 3, true>(p, stream);
+  else if (N <= 256) wn::launch<2, false, 2, true>(p, stream);
+  else if (K <= 512) wn::launch<3, false, 3, true>(p, stream);
+  else wn::launch<3, false, 2, true>(p, stream);
+  ASRX_LAUNCHED("asrx_gemm_wn_router");
 }

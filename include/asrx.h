@@ -56,6 +56,11 @@ int asrx_gemm(int prec, const float* A, int64_t lda, int64_t sA, int a_kc, int c
  * asrx_weight_to_bf16; nj in 1..3 selects the 128*nj-wide output tile. ------------------------- */
 int asrx_weight_to_bf16(const float* src, unsigned short* dst, int64_t rows, int64_t cols, int64_t ld, int trans,
                         asrx_stream_t stream);
+/* AbbyNormal router in one GEMM pass (essentials.py:155-161): hpre = A W1^T + b1 (stored when
+ * hpre != NULL) and logits = SiLU(hpre) W2^T (M x 3, without b2); W1 bf16 (N x K), N <= 384. */
+int asrx_gemm_wn_router(const float* A, int64_t lda, const unsigned short* W1, int64_t ldw, const float* b1,
+                        const float* W2, float* hpre, int64_t ldc, float* logits, int64_t M, int64_t N, int64_t K,
+                        asrx_stream_t stream);
 int asrx_gemm_wn(const float* A, int64_t lda, int conv, int64_t convF, int64_t convC, const unsigned short* W,
                  int64_t ldw, float* C, int64_t ldc, const float* bias, float* Z, int64_t M, int64_t N, int64_t K,
                  float alpha, float beta, int act, int nj, asrx_stream_t stream);
@@ -68,6 +73,10 @@ int asrx_abby_fwd(const float* x, const float* hpre, const float* W2, const floa
                   int* idx, int64_t rows, int64_t d, int64_t L, int64_t H, int64_t sid_base, uint32_t key,
                   int use_noise, asrx_stream_t stream);
 /* dx, dhpre overwritten; dW2 (3,d) / db2 (3) accumulated. */
+/* AbbyNormal forward from precomputed router logits (rows x 3, no b2) -- asrx_gemm_wn_router. */
+int asrx_abby_fwd_logits(const float* x, const float* logits, const float* b2, float* out, float* ys, int* idx,
+                         int64_t rows, int64_t d, int64_t L, int64_t H, int64_t sid_base, uint32_t key,
+                         int use_noise, asrx_stream_t stream);
 int asrx_abby_bwd(const float* dout, const float* x, const float* hpre, const float* W2, const float* ys,
                   const int* idx, float* dx, float* dhpre, float* dW2, float* db2, int64_t rows, int64_t d,
                   asrx_stream_t stream);

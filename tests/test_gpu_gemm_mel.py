@@ -181,3 +181,85 @@ def test_wide_conv3_bf16(cuda):
         y = ops.Conv3.apply(x.transpose(1, 2).contiguous().to(cuda), W.to(cuda), bias.to(cuda)).cpu()
     ref = torch.nn.functional.conv1d(x.double(), W.double(), bias.double(), padding=1).transpose(1, 2)
     assert float((y.double() - ref).abs().max() / ref.abs().max()) < 2e-2
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).double()
+
+
+@pytest.mark.parametrize("nj", [1, 2, 3])
+@pytest.mark.parametrize("M,N,K", [(5000, 384, 384), (1000, 1152, 64), (257, 200, 96), (70000, 64, 384)])
+def test_wide_gemm_exact_bf16_inputs(cuda, nj, M, N, K):
+    """Persistent wide GEMM against float64 on the same bf16-rounded operands: only the fp32
+    accumulation order differs, so the tolerance is tight.  Covers every tile width, partial tiles
+    in M and N, bias + GELU with the pre-activation Z, and the beta (accumulate) epilogue."""
+    from asrx import gemm as G
+    from asrx import lib
+
+    g = torch.Generator().manual_seed(M * 7 + N + K + nj)
+    x = torch.randn(M, K, generator=g)
+    W = torch.randn(N, K, generator=g) / K ** 0.5
+    b = torch.randn(N, generator=g)
+    c0 = torch.randn(M, N, generator=g)
+    xg, Wg, bg = x.to(cuda), W.to(cuda), b.to(cuda)
+    Wb = G.weight_bf16(Wg, cache=False)
+    y = torch.empty(M, N, device=cuda)
+    z = torch.empty(M, N, device=cuda)
+    G._nj_override = nj
+    try:
+        G.gemm_wn(xg, Wb, y, M=M, N=N, K=K, lda=K, ldc=N, bias=bg, act="gelu", Z=z)
+        acc = c0.to(cuda)
+        G.gemm_wn(xg, Wb, acc, M=M, N=N, K=K, lda=K, ldc=N, alpha=0.5, beta=2.0)
+    finally:
+        G._nj_override = None
+    ref_z = _bf(x) @ _bf(W).t() + b.double()
+    ref_y = torch.nn.functional.gelu(ref_z)
+    ref_acc = 0.5 * (_bf(x) @ _bf(W).t()) + 2.0 * c0.double()
+    for got, ref in ((z, ref_z), (y, ref_y), (acc, ref_acc)):
+        assert float((got.cpu().double() - ref).abs().max() / ref.abs().max()) < 2e-6
+
+
+@pytest.mark.parametrize("M,N,keep", [(3001, 384, True), (12000, 384, False), (777, 64, True), (129, 256, False)])
+def test_router_gemm(cuda, M, N, keep):
+    """asrx_gemm_wn_router: h_pre = x W1^T + b1 and logits = SiLU(h_pre) W2^T fused in the GEMM
+    epilogue (AbbyNormal mode_router, essentials.py:155-161), on bf16-rounded operands."""
+    from asrx import gemm as G
+
+    g = torch.Generator().manual_seed(M + N)
+    x = torch.randn(M, N, generator=g)
+    W1 = torch.randn(N, N, generator=g) / N ** 0.5
+    b1 = torch.randn(N, generator=g)
+    W2 = torch.randn(3, N, generator=g) / N ** 0.5
+    hpre, logits = G.router_fwd(x.to(cuda), W1.to(cuda), b1.to(cuda), W2.to(cuda), keep)
+    ref_h = _bf(x) @ _bf(W1).t() + b1.double()
+    ref_l = torch.nn.functional.silu(ref_h) @ W2.double().t()
+    assert float((logits.cpu().double() - ref_l).abs().max() / ref_l.abs().max()) < 1e-5
+    if keep:
+        assert float((hpre.cpu().double() - ref_h).abs().max() / ref_h.abs().max()) < 2e-6
+    else:
+        assert hpre is None
+
+
+def test_abby_fused_router_matches_unfused(cuda):
+    """Perf-mode AbbyNormal: the fused router path (logits from the GEMM epilogue) selects the same
+    normalisation per row as the two-kernel path and gives the same output."""
+    from asrx import gemm as G
+    from asrx import lib, ops, prec
+
+    g = torch.Generator().manual_seed(3)
+    rows, d = 6000, 384
+    x = torch.randn(rows, d, generator=g).to(cuda) * 3
+    W1 = (torch.randn(d, d, generator=g) / d ** 0.5).to(cuda)
+    b1 = torch.randn(d, generator=g).to(cuda)
+    W2 = (torch.randn(3, d, generator=g) / d ** 0.5).to(cuda)
+    b2 = torch.randn(3, generator=g).to(cuda)
+    with prec.precision("bf16"):
+        fused = ops.AbbyNormalFn.apply(x, W1, b1, W2, b2, 3000, 1, 0, 1234, True, False)
+        hpre = G.linear_fwd(x, W1, b1)
+    out = torch.empty_like(x)
+    ys = torch.empty(rows, 3, device=cuda)
+    idx = torch.empty(rows, dtype=torch.int32, device=cuda)
+    lib.call("asrx_abby_fwd", lib.ptr(x), lib.ptr(hpre), lib.ptr(W2), lib.ptr(b2), lib.ptr(out), lib.ptr(ys),
+             lib.ptr(idx), rows, d, 3000, 1, 0, 1234, 1, lib.stream())
+    same = (fused - out).abs().max(dim=1).values <= 1e-5 * out.abs().max()
+    assert float(same.float().mean()) > 0.999  # only near-tie gumbel picks may differ

@@ -63,7 +63,7 @@ def test_abby_normal(cuda, d, H):
         return om.abby_normal(PP, "n", xr, g)
 
     def gpu(xg, w0, b0, w2, b2):
-        return ops.AbbyNormalFn.apply(xg, w0, b0, w2, b2, L, H, sid_base, key, True)
+        return ops.AbbyNormalFn.apply(xg, w0, b0, w2, b2, L, H, sid_base, key, True, True)
 
     r = mod.mode_router
     ins = [x, r[0].weight.detach().cpu(), r[0].bias.detach().cpu(), r[2].weight.detach().cpu(),
@@ -112,15 +112,36 @@ def test_attention(cuda, Lq, Lk, causal):
         assert _rel(a, b) < 1e-4
 
 
-def test_attention_bf16_tolerance(cuda):
-    from asrx import ops, prec
+@pytest.mark.parametrize("B,H,Lq,Lk,causal", [(1, 2, 300, 300, False), (2, 3, 600, 517, False),
+                                                (1, 2, 256, 256, True), (2, 1, 70, 70, True), (1, 2, 33, 3001, False),
+                                                (1, 1, 513, 64, False)])
+def test_attention_bf16(cuda, B, H, Lq, Lk, causal):
+    """Perf-mode flash attention (32x32x16 bf16 MFMA, transposed-read V) against float64 softmax
+    attention on the same bf16-rounded q, k, v: output and log-sum-exp."""
+    from asrx import lib, prec
 
-    B, H, hd, L = 1, 2, 64, 300
-    q, k, v = (torch.randn(B, L, H, hd) for _ in range(3))
-    with prec.precision("bf16"):
-        o = ops.attention(q.cuda(), k.cuda(), v.cuda(), False).cpu()
-    ref = F.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)).transpose(1, 2)
-    assert _rel(o, ref) < 3e-2
+    hd = 64
+    g = torch.Generator().manual_seed(Lq * 3 + Lk + causal)
+    q, k, v = (torch.randn(B, L, H, hd, generator=g) for L in (Lq, Lk, Lk))
+    o = torch.empty(B, Lq, H, hd, device=cuda)
+    lse = torch.empty(B, H, Lq, device=cuda)
+    qg, kg, vg = q.to(cuda), k.to(cuda), v.to(cuda)
+    st = lambda t: (ctypes_arr(t.stride(0), t.stride(1), t.stride(2)))  # noqa: E731
+    import ctypes
+
+    def ctypes_arr(*s):
+        return (ctypes.c_int64 * 3)(*s)
+
+    lib.call("asrx_attn_fwd", 1, lib.ptr(qg), st(qg), lib.ptr(kg), st(kg), lib.ptr(vg), st(vg), lib.ptr(o), st(o),
+             lib.ptr(lse), B, H, Lq, Lk, hd, int(causal), 1.0 / 8.0, lib.stream())
+    bq, bk, bv = (t.to(torch.bfloat16).double().transpose(1, 2) for t in (q, k, v))
+    s = bq @ bk.transpose(-1, -2) / 8.0
+    if causal:
+        s = s.masked_fill(torch.ones(Lq, Lk, dtype=torch.bool).triu(1), float("-inf"))
+    ref_lse = torch.logsumexp(s, -1)
+    ref = (torch.softmax(s, -1) @ bv).transpose(1, 2)
+    assert _rel(o, ref) < 1e-2
+    assert float((lse.cpu().double() - ref_lse).abs().max()) < 1e-3
 
 
 @pytest.mark.parametrize("masked", [False, True])

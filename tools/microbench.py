@@ -92,6 +92,33 @@ def rowops_bench():
     print(f"bn bwd: {t*1e6:.1f} us {5*nb/t/1e9:.0f} GB/s", flush=True)
 
 
+def attn_bench():
+    from asrx import ops, prec
+
+    dev = torch.device("cuda:0")
+    for (B, H, Lq, Lk, causal) in [(64, 6, 3001, 3001, False), (32, 6, 256, 3001, False), (32, 6, 256, 256, True)]:
+        q = torch.randn(B, Lq, H, 64, device=dev)
+        k = torch.randn(B, Lk, H, 64, device=dev)
+        v = torch.randn(B, Lk, H, 64, device=dev)
+        fl = 4.0 * B * H * Lq * Lk * 64 * (0.5 if causal else 1.0)
+        with prec.precision("bf16"):
+            for old in (False, True):
+                if old:
+                    os.environ["ASRX_ATTN_OLD"] = "1"
+                else:
+                    os.environ.pop("ASRX_ATTN_OLD", None)
+                t = timeit(lambda: ops.attention(q, k, v, causal), iters=5)
+                print(f"attn fwd {'old' if old else 'mf '} B={B} H={H} Lq={Lq} Lk={Lk} causal={causal}: "
+                      f"{t*1e6:.1f} us {fl/t/1e12:.1f} TF/s", flush=True)
+            os.environ.pop("ASRX_ATTN_OLD", None)
+            qr, kr, vr = (t_.clone().requires_grad_(True) for t_ in (q, k, v))
+            y = ops.attention(qr, kr, vr, causal)
+            gy = torch.randn_like(y)
+            t = timeit(lambda: torch.autograd.grad(y, (qr, kr, vr), gy, retain_graph=True), iters=3)
+            print(f"attn bwd B={B} Lq={Lq} Lk={Lk}: {t*1e6:.1f} us {2.5*fl/t/1e12:.1f} TF/s", flush=True)
+        del q, k, v
+
+
 if __name__ == "__main__":
     what = sys.argv[1:] or ["gemm", "mel"]
     if "mel" in what:
@@ -100,3 +127,5 @@ if __name__ == "__main__":
         gemm_bench()
     if "rowops" in what:
         rowops_bench()
+    if "attn" in what:
+        attn_bench()
