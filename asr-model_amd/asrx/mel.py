@@ -60,6 +60,48 @@ def sparse_filterbank(fb: torch.Tensor, width: int = FB_WIDTH):
     return starts, w
 
 
+FB_A, FB_B = 8, 24  # taps of a lane's two bands in the kernel (csrc/logmel.hip)
+
+
+def lane_filterbank(fb: torch.Tensor):
+    """Pack the filterbank for the log-mel kernel's lanes.
+
+    Lane m of a wave owns two bands: band_a (the 64 lowest, <= FB_A taps) and band_b (<= FB_B
+    taps), each read as even-aligned pairs of power bins starting at an even bin.  The two 32-lane
+    halves of a wave read the power buffer in separate LDS cycles, so the bands are split between
+    them such that few lanes of a half hit the same bank (bank = (start/2) mod 32 for 8-byte reads).
+    Returns (ints[256] = band_a | band_b | start_a | start_b, weights[8, 64, 4] float32 holding
+    w/4 — the kernel forms 4|X|^2)."""
+    starts, w = sparse_filterbank(fb)
+    n_mels = fb.shape[1]
+    assert n_mels == 128
+    width = (w > 0).sum(1)
+    sp = [int(s) & ~1 for s in starts]
+
+    def split(bands):
+        groups, seen = [[], []], [{}, {}]
+        for b in sorted(bands, key=lambda b: ((sp[b] // 2) % 32, sp[b])):
+            r = (sp[b] // 2) % 32
+            opts = [i for i in (0, 1) if len(groups[i]) < 32]
+            i = min(opts, key=lambda i: (len(seen[i].get(r, set()) | {sp[b]}), len(groups[i])))
+            groups[i].append(b)
+            seen[i].setdefault(r, set()).add(sp[b])
+        return groups[0] + groups[1]
+
+    lanes_a, lanes_b = split(list(range(64))), split(list(range(64, 128)))
+    ints = torch.zeros(256, dtype=torch.int32)
+    wts = torch.zeros(FB_A + FB_B, 64, dtype=torch.float32)
+    for lane in range(64):
+        for slot, (band, taps, off) in enumerate(((lanes_a[lane], FB_A, 0), (lanes_b[lane], FB_B, FB_A))):
+            s0, sh = sp[band], int(starts[band]) - sp[band]
+            if int(width[band]) + sh > taps:
+                raise ValueError(f"band {band} needs {int(width[band]) + sh} taps > {taps}")
+            ints[slot * 64 + lane] = band
+            ints[128 + slot * 64 + lane] = s0
+            wts[off + sh: off + sh + int(width[band]), lane] = 0.25 * w[band, : int(width[band])]
+    return ints, wts.view(8, 4, 64).permute(0, 2, 1).contiguous()
+
+
 def fft_consts(dtype=torch.float32) -> torch.Tensor:
     """window[1024] | tw512 (re,im)[512] | tw1024 (re,im)[513], float32."""
     win = torch.hann_window(N_FFT, periodic=True, dtype=torch.float32)
@@ -78,9 +120,8 @@ _DEV_CACHE: dict = {}
 def device_consts(device):
     key = str(device)
     if key not in _DEV_CACHE:
-        starts, w = sparse_filterbank(mel_filterbank())
-        _DEV_CACHE[key] = (fft_consts().to(device), w.contiguous().to(device),
-                           starts.contiguous().to(device))
+        ints, wts = lane_filterbank(mel_filterbank())
+        _DEV_CACHE[key] = (fft_consts().to(device), wts.to(device), ints.to(device))
     return _DEV_CACHE[key]
 
 

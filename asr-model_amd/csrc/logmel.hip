@@ -6,15 +6,27 @@
 //   -> maximum(x, max(x) - 8)  (max over the whole clip)  ->  (x + 4) / 4
 //   adaptive_avg_pool1d(audio, N/160)  (exact 160-sample block means when 160 | N)
 //
-// Kernel 1 (logmel_frames): one workgroup = 4 waves = FPB consecutive frames of one clip.  The
-// (FPB-1)*160 + 1024 samples those frames touch are staged once in LDS (each sample is re-used
-// 6.4x by overlapping windows), so HBM sees every input byte once.  Each wave turns one frame at a
-// time into a 512-point complex FFT (even/odd packing of the 1024 real samples), runs three radix-8
-// Stockham passes through a per-wave LDS ping-pong, untangles the real spectrum, forms |X|^2 on the
-// 513 bins and applies the sparse filterbank (<= 32 bins per band).  log10 values are staged in LDS
-// and written with coalesced stores in either (B, F, 128) or (B, 128, F) layout; the per-clip max
-// goes to an ordered-int atomicMax.  The fused waveform pool reads the same LDS samples.
-// Kernel 2 (logmel_finalize): x -> (max(x, clipmax - 8) + 4) / 4 in place.
+// Kernel 1 (logmel_tiles): a tile is MEL_FPT consecutive frames of one clip; the (FPT-1)*160+1024
+// samples a tile touches are staged once in LDS (each sample re-used 6.4x by the overlapping
+// windows), so HBM sees every input byte about once.  Workgroups are persistent over a contiguous
+// run of tiles (XCD-aware block order, so neighbouring tiles — which share 864 samples — stay in
+// one XCD's L2) and prefetch the next tile's samples into registers while the current one is
+// transformed.  Each wave owns one frame at a time and never synchronises with the other waves
+// inside a frame: per frame it
+//   * packs the windowed real frame as z[n] = x[2n] w[2n] + i x[2n+1] w[2n+1] (lane j holds
+//     n = j + 64 r, r = 0..7; the window values are lane constants kept in VGPRs),
+//   * runs a 512-point complex FFT as three radix-8 Stockham passes whose twiddles are lane
+//     constants in VGPRs; the two inter-pass transposes go through a per-wave LDS buffer padded
+//     with one slot every 8 (p(i) = i + i/8) so the stride-8 writes are bank-conflict free,
+//   * untangles the real spectrum (lane j already holds Z[j + 64 r]; only the mirrored Z[512-k]
+//     is read back) and forms 4|X_k|^2 (the factor 4 is folded into the filterbank weights),
+//   * applies the sparse filterbank: lane m owns bands m (<= FB_LO taps) and m + 64 (<= FB_HI
+//     taps) with the weights in VGPRs, reading the power bins by immediate LDS offsets,
+//   * takes log10 as log2 * log10(2) (v_log_f32).
+// Per tile the block stages the 128 x FPT log values in LDS, writes them with coalesced stores in
+// (B, F, 128) or (B, 128, F) layout and folds its maximum into the clip's ordered-int atomicMax.
+// The fused waveform pool reads the same LDS samples.
+// Kernel 2 (logmel_finalize): x -> (max(x, clipmax - 8) + 4) / 4 in place, float4.
 #include "common.h"
 #include "fft.h"
 
@@ -23,149 +35,268 @@ using asrx_fft::cpx;
 namespace asrx {
 
 constexpr int MEL_NFFT = 1024, MEL_HOP = 160, MEL_NBINS = 513, MEL_BANDS = 128, MEL_FBW = 32;
-constexpr int MEL_FPB = 32;  // frames per workgroup
-constexpr int MEL_SAMP = (MEL_FPB - 1) * MEL_HOP + MEL_NFFT;
+constexpr int FB_A = 8, FB_B = 24;  // taps of a lane's two bands (see lane_filterbank in mel.py)
+constexpr int FB_QUADS = (FB_A + FB_B) / 4;
+constexpr int MEL_WAVES = 4;
+constexpr int MEL_FPT = 16;  // frames per tile
+constexpr int MEL_TSAMP = (MEL_FPT - 1) * MEL_HOP + MEL_NFFT;  // 3424 samples per tile
+constexpr int MEL_TSAMP4 = MEL_TSAMP / 4;                      // 856 float4
+constexpr int MEL_PF = (MEL_TSAMP4 + 255) / 256;               // prefetch float4 per thread
+constexpr int FFT_SLOTS = 512 + 64 + 8;                        // padded cpx slots per wave
+static_assert(MEL_TSAMP % 4 == 0, "tile samples must be float4 aligned");
 
-// consts layout (floats): window[1024] | tw512[512] (re,im) | tw1024[513] (re,im)
-struct MelConsts {
-  const float* win;
-  const cpx* tw512;
-  const cpx* tw1024;
-};
+__constant__ float kRot[8][2] = {
+    {1.0f, 0.0f},
+    {0.92387953251128674f, -0.38268343236508978f},
+    {0.70710678118654757f, -0.70710678118654757f},
+    {0.38268343236508984f, -0.92387953251128674f},
+    {0.0f, -1.0f},
+    {-0.38268343236508973f, -0.92387953251128674f},
+    {-0.70710678118654746f, -0.70710678118654768f},
+    {-0.92387953251128674f, -0.38268343236508989f}};
 
-__global__ __launch_bounds__(256) void logmel_frames_kernel(
-    const float* __restrict__ wav, int64_t N, int64_t ld_wav, int64_t F, const float* __restrict__ consts,
-    const float* __restrict__ fbw, const int* __restrict__ fbs, float* __restrict__ out, int layout,
-    int64_t ld_out, int* __restrict__ clip_max, float* __restrict__ pool, int64_t T_pool) {
-  __shared__ __attribute__((aligned(16))) float samp[MEL_SAMP];
-  __shared__ __attribute__((aligned(16))) cpx fbuf[4][2][512];
-  __shared__ float melst[MEL_FPB][MEL_BANDS + 1];
-  __shared__ float red[4];
+__device__ __forceinline__ int pidx(int i) { return i + (i >> 3); }
 
-  const int b = blockIdx.y;
-  const int64_t f0 = (int64_t)blockIdx.x * MEL_FPB;
+// Orders this wave's LDS accesses (the LDS unit executes one wave's DS instructions in order;
+// this only stops the compiler from moving them across the exchange point).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ void dft8_tw(cpx (&v)[8], const cpx (&tw)[7]) {
+#pragma unroll
+  for (int r = 1; r < 8; ++r) v[r] = asrx_fft::cmul(v[r], tw[r - 1]);
+  asrx_fft::dft8(v);
+}
+
+// contiguous run of tiles per workgroup; consecutive runs on one XCD (blocks are dealt to the 8
+// XCDs round-robin by blockIdx)
+__device__ __forceinline__ int xcd_block(int bid, int G) {
+  const int per = G / 8, rem = G % 8, x = bid % 8, q = bid / 8;
+  return (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + q;
+}
+
+__global__ __launch_bounds__(256) void logmel_tiles_kernel(
+    const float* __restrict__ wav, int64_t N, int64_t ld_wav, int vec_ok, int64_t F, int tiles_per_clip,
+    int64_t n_tiles, int tiles_per_block, const float* __restrict__ consts, const float* __restrict__ fbw,
+    const int* __restrict__ fbs, float* __restrict__ out, int layout, int64_t ld_out,
+    int* __restrict__ clip_max, float* __restrict__ pool, int64_t T_pool) {
+  __shared__ __attribute__((aligned(16))) float samp[MEL_TSAMP];
+  __shared__ __attribute__((aligned(16))) cpx fbuf[MEL_WAVES][FFT_SLOTS];
+  __shared__ float melst[MEL_FPT][MEL_BANDS + 1];
+  __shared__ float red[MEL_WAVES];
+  __shared__ float4 fbw_s[FB_QUADS * 64];
+
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const float* x = wav + b * ld_wav;
-  MelConsts C{consts, reinterpret_cast<const cpx*>(consts + MEL_NFFT),
-              reinterpret_cast<const cpx*>(consts + MEL_NFFT + 1024)};
+  const int64_t t_begin = (int64_t)xcd_block(blockIdx.x, gridDim.x) * tiles_per_block;
+  if (t_begin >= n_tiles) return;
+  const int64_t t_end = t_begin + tiles_per_block < n_tiles ? t_begin + tiles_per_block : n_tiles;
 
-  // 1. stage samples [f0*160 - 512, f0*160 - 512 + MEL_SAMP) (zero outside the clip)
-  const int64_t g0 = f0 * MEL_HOP - MEL_NFFT / 2;
-  for (int i = tid; i < MEL_SAMP; i += 256) {
-    const int64_t g = g0 + i;
-    samp[i] = (g >= 0 && g < N) ? x[g] : 0.f;
+  // ---- lane constants: window, pass-2/3 twiddles, untangle twiddles, filterbank rows
+  const float* win = consts;
+  const cpx* tw512 = reinterpret_cast<const cpx*>(consts + MEL_NFFT);
+  const cpx* tw1024 = reinterpret_cast<const cpx*>(consts + MEL_NFFT + 1024);
+  float2 wv[8];
+  cpx t2[7], t3[7];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) wv[r] = *reinterpret_cast<const float2*>(win + 2 * (lane + 64 * r));
+  const cpx tu0 = tw1024[lane];
+#pragma unroll
+  for (int r = 1; r < 8; ++r) {
+    t2[r - 1] = tw512[(r * (lane & 7) * 8) & 511];
+    t3[r - 1] = tw512[(r * lane) & 511];
   }
-  __syncthreads();
+  // lane-packed filterbank (asrx/mel.py lane_filterbank): lane m owns band_a (<= 8 taps from the
+  // even bin sa) and band_b (<= 24 taps from the even bin sb); weights [tap/4][lane][4] in LDS
+  const int band_a = fbs[lane], band_b = fbs[64 + lane];
+  const int sa2 = fbs[128 + lane] >> 1, sb2 = fbs[192 + lane] >> 1;
+  for (int i = tid; i < FB_QUADS * 64; i += 256) fbw_s[i] = reinterpret_cast<const float4*>(fbw)[i];
 
-  // 2. fused waveform feature: exact 160-sample block means (pool index == frame index)
-  if (pool) {
-    for (int fi = wid; fi < MEL_FPB; fi += 4) {
-      const int64_t f = f0 + fi;
-      if (f >= T_pool) break;
-      const int base = MEL_NFFT / 2 + fi * MEL_HOP;
-      float s = samp[base + lane] + samp[base + lane + 64] + (lane < 32 ? samp[base + lane + 128] : 0.f);
-      s = wave_sum(s);
-      if (lane == 0) pool[b * T_pool + f] = s * (1.0f / MEL_HOP);
-    }
-  }
+  cpx* S = fbuf[wid];
+  float* P = reinterpret_cast<float*>(S);
 
-  float lmax = -3.0e38f;
-  cpx* b0 = fbuf[wid][0];
-  cpx* b1 = fbuf[wid][1];
-  for (int fi = wid; fi < MEL_FPB; fi += 4) {
-    const int64_t f = f0 + fi;  // wave-uniform
-    const bool live = f < F;
-    const int base = fi * MEL_HOP;
-    // 3. pack windowed real frame as z[n] = x[2n] w[2n] + i x[2n+1] w[2n+1], lane j holds n = j + 64 r
-    cpx v[8];
+  // ---- sample prefetch (registers) for tile t; the bounds test is per tile (wave-uniform)
+  float4 pf[MEL_PF];
+  auto prefetch = [&](int64_t t) {
+    const int64_t b = t / tiles_per_clip;
+    const int64_t f0 = (t - b * tiles_per_clip) * MEL_FPT;
+    const int64_t g0 = f0 * MEL_HOP - MEL_NFFT / 2;
+    const float* x = wav + b * ld_wav + g0;
+    if (vec_ok && g0 >= 0 && g0 + MEL_TSAMP <= N) {
+      const float4* x4 = reinterpret_cast<const float4*>(x);
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const int n = lane + 64 * r;
-      const float2 s2 = *reinterpret_cast<const float2*>(&samp[base + 2 * n]);
-      const float2 w2 = *reinterpret_cast<const float2*>(&C.win[2 * n]);
-      v[r] = cpx{s2.x * w2.x, s2.y * w2.y};
-    }
-    // 4. three radix-8 Stockham passes
-    asrx_fft::stockham_pass(lane, 1, v, b0, C.tw512);
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 8; ++r) v[r] = b0[lane + 64 * r];
-    asrx_fft::stockham_pass(lane, 8, v, b1, C.tw512);
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 8; ++r) v[r] = b1[lane + 64 * r];
-    asrx_fft::stockham_pass(lane, 64, v, b0, C.tw512);
-    __syncthreads();
-    // 5. real-FFT untangle + power spectrum into b1 (reused as float[513])
-    float* pw = reinterpret_cast<float*>(b1);
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const int k = lane + 64 * r;
-      const cpx zk = b0[k];
-      const cpx zn = b0[(512 - k) & 511];
-      // E = (Zk + conj(Zn)) / 2 ; O = (Zk - conj(Zn)) / (2i)
-      const cpx e{0.5f * (zk.x + zn.x), 0.5f * (zk.y - zn.y)};
-      const cpx o{0.5f * (zk.y + zn.y), -0.5f * (zk.x - zn.x)};
-      const cpx t = asrx_fft::cmul(C.tw1024[k], o);
-      const float re = e.x + t.x, im = e.y + t.y;
-      pw[k] = re * re + im * im;
-    }
-    if (lane == 0) {
-      const cpx z0 = b0[0];
-      const float nyq = z0.x - z0.y;
-      pw[512] = nyq * nyq;
-    }
-    __syncthreads();
-    // 6. sparse filterbank (two bands per lane) + log10(clamp(., 1e-10))
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int m = lane + 64 * h;
-      const int s = fbs[m];
-      const float* w = fbw + m * MEL_FBW;
-      float acc = 0.f;
-#pragma unroll 8
-      for (int i = 0; i < MEL_FBW; ++i) {
-        const int bin = s + i;
-        acc += w[i] * pw[bin < MEL_NBINS ? bin : MEL_NBINS - 1];
+      for (int q = 0; q < MEL_PF; ++q) {
+        const int i4 = tid + 256 * q;
+        pf[q] = i4 < MEL_TSAMP4 ? x4[i4] : make_float4(0.f, 0.f, 0.f, 0.f);
       }
-      const float lv = (float)log10((double)fmaxf(acc, 1e-10f));  // correctly rounded like libm
-      melst[fi][m] = lv;
-      if (live) lmax = fmaxf(lmax, lv);
+    } else {
+#pragma unroll
+      for (int q = 0; q < MEL_PF; ++q) {
+        const int i4 = tid + 256 * q;
+        float e[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int64_t g = g0 + 4 * i4 + c;
+          e[c] = (i4 < MEL_TSAMP4 && g >= 0 && g < N) ? x[4 * i4 + c] : 0.f;
+        }
+        pf[q] = make_float4(e[0], e[1], e[2], e[3]);
+      }
+    }
+  };
+  prefetch(t_begin);
+
+#pragma unroll 1
+  for (int64_t t = t_begin; t < t_end; ++t) {
+    const int64_t b = t / tiles_per_clip;
+    const int64_t f0 = (t - b * tiles_per_clip) * MEL_FPT;
+    __syncthreads();  // the previous tile's readers are done with samp / melst
+#pragma unroll
+    for (int q = 0; q < MEL_PF; ++q) {
+      const int i4 = tid + 256 * q;
+      if (i4 < MEL_TSAMP4) reinterpret_cast<float4*>(samp)[i4] = pf[q];
     }
     __syncthreads();
-  }
+    if (t + 1 < t_end) prefetch(t + 1);
 
-  // 7. coalesced output of the staged log10 block
-  if (layout == 0) {  // (B, F, 128): row f contiguous
-    for (int i = tid; i < MEL_FPB * MEL_BANDS; i += 256) {
-      const int fi = i / MEL_BANDS, m = i % MEL_BANDS;
-      const int64_t f = f0 + fi;
-      if (f < F) out[b * ld_out + f * MEL_BANDS + m] = melst[fi][m];
+    // fused waveform feature: exact 160-sample block means (pool index == frame index)
+    if (pool) {
+      for (int fi = wid; fi < MEL_FPT; fi += MEL_WAVES) {
+        const int64_t f = f0 + fi;
+        if (f >= T_pool) break;
+        const int base = MEL_NFFT / 2 + fi * MEL_HOP;
+        float s = samp[base + lane] + samp[base + lane + 64] + (lane < 32 ? samp[base + lane + 128] : 0.f);
+        s = wave_sum(s);
+        if (lane == 0) pool[b * T_pool + f] = s * (1.0f / MEL_HOP);
+      }
     }
-  } else {  // (B, 128, F): each band's FPB frames contiguous
-    for (int i = tid; i < MEL_FPB * MEL_BANDS; i += 256) {
-      const int m = i / MEL_FPB, fi = i % MEL_FPB;
-      const int64_t f = f0 + fi;
-      if (f < F) out[b * ld_out + m * F + f] = melst[fi][m];
+
+    float lmax = -3.0e38f;
+#pragma unroll 1
+    for (int fi = wid; fi < MEL_FPT; fi += MEL_WAVES) {
+      const bool live = f0 + fi < F;  // wave-uniform
+      const float2* s2 = reinterpret_cast<const float2*>(samp + fi * MEL_HOP);
+      cpx v[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const float2 s = s2[lane + 64 * r];
+        v[r] = cpx{s.x * wv[r].x, s.y * wv[r].y};
+      }
+      // pass 1 (Ns = 1): out[8j + r]
+      asrx_fft::dft8(v);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) S[9 * lane + r] = v[r];
+      wave_lds_sync();
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] = S[pidx(lane) + 72 * r];
+      wave_lds_sync();
+      // pass 2 (Ns = 8): out[(j/8)*64 + j%8 + 8r]
+      dft8_tw(v, t2);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) S[72 * (lane >> 3) + (lane & 7) + 9 * r] = v[r];
+      wave_lds_sync();
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] = S[pidx(lane) + 72 * r];
+      wave_lds_sync();
+      // pass 3 (Ns = 64): out[j + 64 r] = Z[j + 64 r], kept in v
+      dft8_tw(v, t3);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) S[pidx(lane) + 72 * r] = v[r];
+      wave_lds_sync();
+      // real-FFT untangle: 2 X_k = (Z_k + conj Z_{512-k}) + W1024^k (-i)(Z_k - conj Z_{512-k})
+      float pw[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int k = lane + 64 * r;
+        const cpx zn = S[pidx((512 - k) & 511)];
+        const cpx zk = v[r];
+        const cpx e{zk.x + zn.x, zk.y - zn.y};
+        const cpx o{zk.y + zn.y, zn.x - zk.x};
+        // W1024^(j + 64 r) = W1024^j * exp(-i pi r / 8)
+        const cpx tt = asrx_fft::cmul(asrx_fft::cmul(tu0, cpx{kRot[r][0], kRot[r][1]}), o);
+        const float re = e.x + tt.x, im = e.y + tt.y;
+        pw[r] = re * re + im * im;  // 4 |X_k|^2
+      }
+      wave_lds_sync();
+#pragma unroll
+      for (int r = 0; r < 8; ++r) P[lane + 64 * r] = pw[r];
+      if (lane < 16) {
+        const float nyq = 2.0f * (v[0].x - v[0].y);  // lane 0: 2 X_512 = 2 (Re Z0 - Im Z0)
+        P[512 + lane] = lane == 0 ? nyq * nyq : 0.f;  // bins past 512 are zero pads for the taps
+      }
+      wave_lds_sync();
+      // sparse filterbank (weights carry the 1/4; bins read in even-aligned pairs)
+      const float2* P2 = reinterpret_cast<const float2*>(P);
+      float acc_a = 0.f, acc_b = 0.f;
+#pragma unroll
+      for (int q = 0; q < FB_A / 4; ++q) {
+        const float4 wq = fbw_s[q * 64 + lane];
+        const float2 p0 = P2[sa2 + 2 * q], p1 = P2[sa2 + 2 * q + 1];
+        acc_a = fmaf(wq.x, p0.x, fmaf(wq.y, p0.y, fmaf(wq.z, p1.x, fmaf(wq.w, p1.y, acc_a))));
+      }
+#pragma unroll
+      for (int q = 0; q < FB_B / 4; ++q) {
+        const float4 wq = fbw_s[(FB_A / 4 + q) * 64 + lane];
+        const float2 p0 = P2[sb2 + 2 * q], p1 = P2[sb2 + 2 * q + 1];
+        acc_b = fmaf(wq.x, p0.x, fmaf(wq.y, p0.y, fmaf(wq.z, p1.x, fmaf(wq.w, p1.y, acc_b))));
+      }
+      wave_lds_sync();
+      // clamp(1e-10).log10(): the clamped value maps to exactly -10 like the correctly rounded
+      // library log10; elsewhere log2 * log10(2) is within a few ulp
+      const float l_a = acc_a <= 1e-10f ? -10.0f : __builtin_amdgcn_logf(acc_a) * 0.30102999566398120f;
+      const float l_b = acc_b <= 1e-10f ? -10.0f : __builtin_amdgcn_logf(acc_b) * 0.30102999566398120f;
+      melst[fi][band_a] = l_a;
+      melst[fi][band_b] = l_b;
+      if (live) lmax = fmaxf(lmax, fmaxf(l_a, l_b));
     }
-  }
-  lmax = wave_max(lmax);
-  if (lane == 0) red[wid] = lmax;
-  __syncthreads();
-  if (tid == 0) {
-    const float bm = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    atomicMax(clip_max + b, float_to_ordered(bm));
+    lmax = wave_max(lmax);
+    if (lane == 0) red[wid] = lmax;
+    __syncthreads();
+
+    // coalesced output of the staged block
+    float* o = out + b * ld_out;
+    if (layout == 0) {  // (B, F, 128): the tile is FPT contiguous rows of 128
+      for (int i = tid; i < MEL_FPT * MEL_BANDS / 4; i += 256) {
+        const int fi = i / (MEL_BANDS / 4), m4 = (i % (MEL_BANDS / 4)) * 4;
+        if (f0 + fi < F) {
+          const float* src = &melst[fi][m4];
+          *reinterpret_cast<float4*>(o + (f0 + fi) * MEL_BANDS + m4) = make_float4(src[0], src[1], src[2], src[3]);
+        }
+      }
+    } else {  // (B, 128, F): each band's FPT frames contiguous
+      for (int i = tid; i < MEL_FPT * MEL_BANDS; i += 256) {
+        const int m = i / MEL_FPT, fi = i % MEL_FPT;
+        if (f0 + fi < F) o[m * F + f0 + fi] = melst[fi][m];
+      }
+    }
+    if (tid == 0) {
+      float bm = red[0];
+#pragma unroll
+      for (int w = 1; w < MEL_WAVES; ++w) bm = fmaxf(bm, red[w]);
+      atomicMax(clip_max + b, float_to_ordered(bm));
+    }
   }
 }
 
 __global__ void logmel_finalize_kernel(float* __restrict__ out, int64_t per_clip, int64_t ld_out,
-                                       const int* __restrict__ clip_max) {
+                                       const int* __restrict__ clip_max, int vec) {
   const int b = blockIdx.y;
   const float floor_v = ordered_to_float(clip_max[b]) - 8.0f;
   float* o = out + b * ld_out;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < per_clip;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    o[i] = (fmaxf(o[i], floor_v) + 4.0f) * 0.25f;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  if (vec) {
+    float4* o4 = reinterpret_cast<float4*>(o);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < per_clip / 4; i += stride) {
+      float4 v = o4[i];
+      v.x = (fmaxf(v.x, floor_v) + 4.0f) * 0.25f;
+      v.y = (fmaxf(v.y, floor_v) + 4.0f) * 0.25f;
+      v.z = (fmaxf(v.z, floor_v) + 4.0f) * 0.25f;
+      v.w = (fmaxf(v.w, floor_v) + 4.0f) * 0.25f;
+      o4[i] = v;
+    }
+  } else {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < per_clip; i += stride)
+      o[i] = (fmaxf(o[i], floor_v) + 4.0f) * 0.25f;
   }
 }
 
@@ -180,24 +311,36 @@ using namespace asrx;
 
 // wav: (B, N) rows at stride ld_wav.  out: (B, F, 128) if layout == 0 else (B, 128, F), clip stride
 // ld_out (>= 128*F).  clip_max_ws: int workspace of B entries (overwritten).  pool: (B, T_pool) or
-// null; the fused pool requires N == 160 * T_pool.
+// null; the fused pool requires N == 160 * T_pool.  fbw/fbs: the lane-packed filterbank of
+// asrx/mel.py lane_filterbank: fbs = band_a[64] | band_b[64] | start_a[64] | start_b[64] (even
+// starts), fbw = weights [8 tap quads][64 lanes][4] (taps 0-7 band_a, 8-31 band_b, x 1/4).
 extern "C" int asrx_logmel(const float* wav, int64_t B, int64_t N, int64_t ld_wav, const float* consts,
                            const float* fbw, const int* fbs, float* out, int layout, int64_t ld_out,
                            int* clip_max_ws, float* pool, int64_t T_pool, hipStream_t stream) {
   ASRX_REQUIRE(B > 0 && N > 0, "asrx_logmel: empty input");
-  ASRX_REQUIRE(B < 65536, "asrx_logmel: too many clips");
+  ASRX_REQUIRE(B < (1 << 24), "asrx_logmel: too many clips");
   const int64_t F = 1 + N / MEL_HOP;
   ASRX_REQUIRE(ld_out >= F * MEL_BANDS, "asrx_logmel: ld_out too small");
+  ASRX_REQUIRE(layout != 0 || (ld_out % 4 == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0),
+               "asrx_logmel: (B, F, 128) layout needs 16-byte aligned rows");
   ASRX_REQUIRE(!pool || N == (int64_t)MEL_HOP * T_pool,
                "asrx_logmel: fused pool needs N == 160*T_pool (N=%ld T=%ld)", (long)N, (long)T_pool);
   fill_int_kernel<<<(unsigned)((B + 255) / 256), 256, 0, stream>>>(clip_max_ws, (int)B,
                                                                    float_to_ordered(-3.0e38f));
-  dim3 g((unsigned)((F + MEL_FPB - 1) / MEL_FPB), (unsigned)B);
-  logmel_frames_kernel<<<g, 256, 0, stream>>>(wav, N, ld_wav, F, consts, fbw, fbs, out, layout, ld_out,
-                                              clip_max_ws, pool, T_pool);
-  int64_t per_clip = F * MEL_BANDS;
-  unsigned gx = (unsigned)std::min<int64_t>((per_clip + 255) / 256, 64);
-  logmel_finalize_kernel<<<dim3(gx, (unsigned)B), 256, 0, stream>>>(out, per_clip, ld_out, clip_max_ws);
+  const int tiles_per_clip = (int)((F + MEL_FPT - 1) / MEL_FPT);
+  const int64_t n_tiles = B * tiles_per_clip;
+  // 3 resident workgroups per CU (168 VGPRs, 48.8 KB LDS) on 256 CUs; each takes a contiguous run
+  const int64_t slots = 256 * 3;
+  const int tiles_per_block = (int)std::max<int64_t>(1, (n_tiles + slots - 1) / slots);
+  const int64_t grid = (n_tiles + tiles_per_block - 1) / tiles_per_block;
+  const int vec_ok = (ld_wav % 4 == 0) && ((reinterpret_cast<uintptr_t>(wav) & 15) == 0);
+  logmel_tiles_kernel<<<(unsigned)grid, 256, 0, stream>>>(wav, N, ld_wav, vec_ok, F, tiles_per_clip, n_tiles,
+                                                          tiles_per_block, consts, fbw, fbs, out, layout, ld_out,
+                                                          clip_max_ws, pool, T_pool);
+  const int64_t per_clip = F * MEL_BANDS;
+  const int vec = (ld_out % 4 == 0) && ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
+  const unsigned gx = (unsigned)std::min<int64_t>((per_clip / (vec ? 4 : 1) + 255) / 256, 96);
+  logmel_finalize_kernel<<<dim3(gx, (unsigned)B), 256, 0, stream>>>(out, per_clip, ld_out, clip_max_ws, vec);
   ASRX_LAUNCHED("asrx_logmel");
 }
 

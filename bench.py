@@ -115,8 +115,11 @@ def main():
 
     def step():
         gsync.zero_grad()
-        spec, wfeat = logmel(wav, layout="BMF", pool=True)
-        out = model(labels=labels, text_ids=ids, spectrogram=spec, pitch=pitch, waveform=wfeat.unsqueeze(1))
+        # the kernel writes (B, F, 128) (what the encoder's k3 conv consumes); the model receives the
+        # reference's (B, 128, F) spectrogram as a transposed view of it, so no copy is made
+        spec, wfeat = logmel(wav, layout="BFM", pool=True)
+        out = model(labels=labels, text_ids=ids, spectrogram=spec.transpose(1, 2), pitch=pitch,
+                    waveform=wfeat.unsqueeze(1))
         out["loss"].backward()
         gsync.finish()
         return out["loss"]
