@@ -20,7 +20,8 @@ def gemm(A, B, C, *, M, N, K, lda, ldb, ldc, a_kc=True, b_kc=True, batch=1, sA=0
     lib.call("asrx_gemm", p, lib.ptr(A), lda, sA, int(a_kc), int(conv_a), lib.ptr(B), ldb, sB,
              int(b_kc), int(conv_b), lib.ptr(C), ldc, sC, lib.ptr(bias), lib.ptr(Z), M, N, K, batch,
              float(alpha), float(beta), ACT[act], conv_F, conv_C, int(splitk), lib.stream())
-    probe.end("gemm", e0, 2.0 * M * N * K * batch)
+    probe.end("gemm", e0, 2.0 * M * N * K * batch,
+              ("gemm", p, M, N, K, batch, int(a_kc), int(b_kc), int(conv_a), splitk, act))
     return C
 
 
@@ -80,7 +81,7 @@ def gemm_wn(A, Wb, C, *, M, N, K, lda, ldc, bias=None, Z=None, alpha=1.0, beta=0
     lib.call("asrx_gemm_wn", lib.ptr(A), lda, int(conv), conv_F, conv_C, lib.ptr(Wb), Wb.stride(0), lib.ptr(C),
              ldc, lib.ptr(bias), lib.ptr(Z), M, N, K, float(alpha), float(beta), ACT[act], _nj(M, N),
              lib.stream())
-    probe.end("gemm", e0, 2.0 * M * N * K)
+    probe.end("gemm", e0, 2.0 * M * N * K, ("wn", M, N, K, _nj(M, N), int(conv), act, Z is not None, beta != 0))
     return C
 
 
@@ -95,7 +96,7 @@ def router_fwd(x2, W1, b1, W2, keep_hpre):
     e0 = probe.begin("gemm")
     lib.call("asrx_gemm_wn_router", lib.ptr(x2), K, lib.ptr(Wb), Wb.stride(0), lib.ptr(b1), lib.ptr(W2),
              lib.ptr(hpre), N, lib.ptr(logits), M, N, K, lib.stream())
-    probe.end("gemm", e0, 2.0 * M * N * K)
+    probe.end("gemm", e0, 2.0 * M * N * K, ("router", M, N, K, keep_hpre))
     return hpre, logits
 
 

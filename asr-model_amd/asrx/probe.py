@@ -27,19 +27,28 @@ def begin(kind):
     return e
 
 
-def end(kind, e0, work):
+def end(kind, e0, work, tag=None):
     if e0 is None:
         return
     e1 = torch.cuda.Event(enable_timing=True)
     e1.record()
-    _active[kind].append((work, e0, e1))
+    _active[kind].append((work, e0, e1, tag))
 
 
 def summarize(records):
     """-> (launches, total work, total seconds); call after a device synchronize."""
     n, work, sec = 0, 0.0, 0.0
-    for w, e0, e1 in records:
+    for w, e0, e1, _ in records:
         n += 1
         work += w
         sec += e0.elapsed_time(e1) * 1e-3
     return n, work, sec
+
+
+def by_tag(records):
+    """-> {tag: (launches, total work, total seconds)}; call after a device synchronize."""
+    out: dict = {}
+    for w, e0, e1, tag in records:
+        n, wk, sec = out.get(tag, (0, 0.0, 0.0))
+        out[tag] = (n + 1, wk + w, sec + e0.elapsed_time(e1) * 1e-3)
+    return out

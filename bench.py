@@ -40,6 +40,9 @@ def parse():
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true", help="skip the live per-kernel event probe")
+    ap.add_argument("--dist-backend", default="nccl", help="process-group backend for N > 1 (nccl = RCCL); "
+                    "gloo + --same-device is a one-GPU rehearsal of the multi-rank path")
+    ap.add_argument("--same-device", action="store_true", help="every rank on cuda:0 (rehearsal only)")
     ap.add_argument("--eager", action="store_true", help="launch every kernel from Python instead of replaying "
                     "the captured HIP graph of the step")
     return ap.parse_args()
@@ -87,10 +90,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    if args.same_device:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
 
     from asrx import prec, probe, synth
     from asrx.config import CONFIGS
@@ -141,8 +149,6 @@ def main():
         with torch.cuda.graph(graph):
             loss = step()
         torch.cuda.synchronize()
-    elif not args.no_probe:
-        probe.enable(("gemm", "logmel", "attn"))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -156,12 +162,10 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if graph is None:
-        recs = probe.disable()
-        probe_steps = args.steps
-    elif not args.no_probe:
-        # timing events cannot be read back from inside a captured graph: time the identical step
-        # (same kernels, shapes and inputs) once more eagerly, right after the timed replays
+    if not args.no_probe:
+        # per-kernel HIP events stay out of the timed region (and cannot be read back from inside a
+        # captured graph): every rank runs the identical step (same kernels, shapes and inputs)
+        # once more eagerly with the probe on, right after the timed steps
         probe.enable(("gemm", "logmel", "attn"))
         step()
         torch.cuda.synchronize()
@@ -170,6 +174,12 @@ def main():
     else:
         recs = None
     if world > 1:
+        # replicas must hold identical averaged gradients after the all-reduce
+        gsum = torch.stack([p.grad.double().norm() for p in model.parameters() if p.grad is not None]).sum()
+        lo, hi = gsum.clone(), gsum.clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        grad_spread = float((hi - lo) / hi.clamp_min(1e-30))
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -195,18 +205,47 @@ def main():
                    "model": args.config, "global_batch": world * B, "seq_len": 3001, "text_len": args.text_len,
                    "parallelism": f"dp{world}"},
         "per_gpu": round(value / world, 3),
+        **({"grad_sync_rel_spread": grad_spread} if world > 1 else {}),
         "loss": loss_v,
     }
     if recs is not None:
         n, flops, sec = probe.summarize(recs["gemm"])
         peak = BF16_PEAK_TFS if args.precision == "bf16" else F32_PEAK_TFS
         achieved = flops / sec / 1e12 if sec > 0 else 0.0
-        result["roofline"] = {"kernel": "asrx gemm_kernel (MFMA GEMM, all Linear/conv fwd+dgrad+wgrad)",
+        step_s = elapsed / args.steps
+        # dominant kernel: the wide bf16-weight GEMM (asrx_gemm_wn, every activation x weight product
+        # of the forward and of the input gradients; the top kernel of the rocprof summary).  With
+        # fp32 activations at K, N <= 1536 its arithmetic intensity (<= ~190 flop/B) is below the
+        # MI355X ridge point (2500 TF/s / 8 TB/s = 312 flop/B), so its roofline is HBM bandwidth:
+        # algorithmic bytes per launch = A (4 M K) + W (2 N K) + C (4 M N) [+ 4 M N if beta, + 4 M N if
+        # the pre-activation is saved].
+        wn_n, wn_bytes, wn_flops, wn_sec = 0, 0.0, 0.0, 0.0
+        for tag, (cnt, fl, sc) in probe.by_tag(recs["gemm"]).items():
+            if not tag or tag[0] != "wn":
+                continue
+            _, M, N, K, _nj, _conv, _act, has_z, has_beta = tag
+            per = 4 * M * K + 2 * N * K + 4 * M * N * (1 + int(has_z) + int(has_beta))
+            wn_n += cnt
+            wn_bytes += cnt * per
+            wn_flops += fl
+            wn_sec += sc
+        if wn_sec > 0:
+            gbs = wn_bytes / wn_sec / 1e9
+            result["roofline"] = {"kernel": "asrx::wn::gemm_wn_kernel (wide bf16-weight MFMA GEMM, fp32 activations)",
+                                  "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                  "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                                  "algorithmic_bytes_per_launch": round(wn_bytes / wn_n),
+                                  "launches_per_step": wn_n // probe_steps,
+                                  "avg_us": round(wn_sec / wn_n * 1e6, 2),
+                                  "share_of_step": round(wn_sec / probe_steps / step_s, 3),
+                                  "mfma_achieved_tflops": round(wn_flops / wn_sec / 1e12, 2),
+                                  "mfma_frac": round(wn_flops / wn_sec / 1e12 / peak, 4)}
+        result["gemm_all"] = {"kernel": "every asrx GEMM launch (wide, generic fp32/bf16 incl. wgrad, router)",
                               "bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                              "frac": round(achieved / peak, 4), "traffic": None,
+                              "frac": round(achieved / peak, 4),
                               "launches_per_step": n // probe_steps,
                               "avg_us": round(sec / max(n, 1) * 1e6, 2),
-                              "share_of_step": round(sec / probe_steps / (elapsed / args.steps), 3)}
+                              "share_of_step": round(sec / probe_steps / step_s, 3)}
         n2, byts, sec2 = probe.summarize(recs["logmel"])
         if sec2 > 0:
             gbs = byts / sec2 / 1e9
@@ -219,10 +258,10 @@ def main():
         if sec3 > 0:
             result["attn_fwd"] = {"achieved": round(af / sec3 / 1e12, 2), "unit": "TFLOP/s",
                                   "frac": round(af / sec3 / 1e12 / peak, 4),
-                                  "share_of_step": round(sec3 / probe_steps / (elapsed / args.steps), 3)}
+                                  "share_of_step": round(sec3 / probe_steps / step_s, 3)}
     result["launch"] = "hip-graph replay" if graph is not None else "eager"
-    if graph is not None and recs is not None:
-        result["probe"] = "per-kernel HIP events on one eager pass of the same step after the timed replays"
+    if recs is not None:
+        result["probe"] = "per-kernel HIP events on one eager pass of the same step after the timed steps"
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(model, args.config)
     if world > 1:

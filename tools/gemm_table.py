@@ -1,0 +1,61 @@
+"""Per-shape GEMM / attention timing of one eager training step (GPU box; not part of the product).
+Runs the bench workload once eagerly with the HIP-event probe on and prints one row per GEMM shape:
+launches, avg us, TF/s, and the fp32-activation byte rate (A + C read/write, bf16 weights)."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "asr-model_amd")]
+import torch  # noqa: E402
+
+from asrx import prec, probe, synth  # noqa: E402
+from asrx.config import CONFIGS  # noqa: E402
+from asrx.mel import logmel  # noqa: E402
+from asrx.model import Model  # noqa: E402
+
+cfg_name = sys.argv[1] if len(sys.argv) > 1 else "tiny"
+B = int(sys.argv[2]) if len(sys.argv) > 2 else 32
+dev = torch.device("cuda:0")
+prec.set_precision("bf16")
+cfg = CONFIGS[cfg_name]
+torch.manual_seed(0)
+model = Model(cfg).to(dev).train()
+model.set_noise(seed=0, step=0)
+wav = synth.waveform(B, 30.0).to(dev)
+pitch = synth.pitch(B).to(dev)
+ids, labels = synth.text(B, 256, cfg.tokens)
+ids, labels = ids.to(dev), labels.to(dev)
+
+
+def step():
+    for p in model.parameters():
+        p.grad = None
+    spec, wf = logmel(wav, layout="BFM", pool=True)
+    out = model(labels=labels, text_ids=ids, spectrogram=spec.transpose(1, 2), pitch=pitch, waveform=wf.unsqueeze(1))
+    out["loss"].backward()
+
+
+step()
+torch.cuda.synchronize()
+probe.enable(("gemm", "attn", "logmel"))
+t0 = torch.cuda.Event(enable_timing=True)
+t1 = torch.cuda.Event(enable_timing=True)
+t0.record()
+step()
+t1.record()
+torch.cuda.synchronize()
+recs = probe.disable()
+total = t0.elapsed_time(t1) * 1e-3
+print(f"eager step {total*1e3:.1f} ms")
+for kind in ("gemm", "attn", "logmel"):
+    tab = probe.by_tag(recs[kind])
+    tsum = sum(v[2] for v in tab.values())
+    print(f"== {kind}: {sum(v[0] for v in tab.values())} launches, {tsum*1e3:.1f} ms "
+          f"({100*tsum/total:.1f}% of step), {sum(v[1] for v in tab.values())/max(tsum,1e-12)/1e12:.1f} TF/s")
+    for tag, (n, w, sec) in sorted(tab.items(), key=lambda kv: -kv[1][2]):
+        extra = ""
+        if kind == "gemm" and tag and tag[0] in ("wn", "router"):
+            M, N, K = tag[1], tag[2], tag[3]
+            byts = 4 * M * K + 4 * M * N + 2 * N * K
+            extra = f" {byts*n/sec/1e9:7.0f} GB/s(fp32 A+C)"
+        print(f"{n:5d} x {sec/n*1e6:8.1f} us = {sec*1e3:7.2f} ms  {w/sec/1e12:7.1f} TF/s{extra}  {tag}")
