@@ -14,7 +14,8 @@ import os
 import torch  # noqa: F401  (loads the HIP runtime first so libasrx binds to the same instance)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libasrx.so")
+# ASRX_LIB: an alternative build of the same library (tools/exp A/B experiments only)
+LIB_PATH = os.environ.get("ASRX_LIB") or os.path.join(_HERE, "libasrx.so")
 
 _i64 = ctypes.c_int64
 _i32 = ctypes.c_int

@@ -18,6 +18,10 @@
 //    reads are bank-conflict-free under gfx950's 64-bank, 16-lane-group rule.
 //  * MFMA 16x16x32 bf16 with the W fragment as the row operand: each lane ends up owning 4
 //    consecutive output columns of one row, so the epilogue stores float4.
+// Two pipelines share the tiles, swizzles and epilogues: gemm_wr_kernel (production: operands
+// global -> VGPR -> LDS, A converted to bf16 on the way in, 3 k-steps of register prefetch) and
+// gemm_wn_kernel (LDS-DMA ring; ASRX_WN_IMPL=dma selects it for A/B timing).  Measured on MI355X
+// at M = 192064, N = 384: K = 384 195 us vs 219 us, K = 1536 454 us vs 560 us (tools/exp).
 #include "common.h"
 
 namespace asrx {
@@ -269,7 +273,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wn_kernel(Params p, int ntiles) 
   const int E = RT ? (p.C ? 4 * NT : 0) : 4 * NT * (p.Z ? 2 : 1);
   const bool vec = vec_ok(p);
 
-  auto coords = [&](int j, int& m0, int& n0) {
+  auto coords = [&](int j, int& m0, int& n0) __attribute__((always_inline)) {
     const int t = j * G + r;
     m0 = (t / nN) * BM;
     n0 = (t % nN) * BN;
@@ -369,6 +373,207 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wn_kernel(Params p, int ntiles) 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// ---------------------------------------------------------------------------------------------
+// Register-staged variant (gemm_wr_kernel): the same tiles, waves, MFMA and epilogues, but both
+// operands travel global -> VGPR -> LDS with plain dwordx4 loads issued DEPTH k-steps ahead (the
+// compiler counts their vmcnt), A is converted to bf16 once on the way into LDS (the four waves
+// that share an A fragment no longer convert it four times, and the A image halves to 8 KB), and
+// the LDS images are double-buffered with one barrier per k-step.  An LDS-DMA piece costs ~100+
+// issue cycles per KB on gfx950 (MI355X_MICROARCH.md constants table); a dwordx4 load + ds_write
+// moves the same KB for a fraction of that, which is what bounded gemm_wn_kernel's pipeline.
+constexpr int WR_DEPTH = 3;  // register stages in flight (k-steps of prefetch)
+
+template <int NJ>
+struct WrStage {
+  float4 a[2];     // 2 x 4 fp32 of the A tile (row q/8, k chunk q%8), q = tid + 512 i
+  uint4 b[NJ];     // NJ x 8 bf16 of the W tile (row q/4, k chunk q%4), q = tid + 512 i
+};
+
+template <int NJ, bool CONV>
+__device__ __forceinline__ void wr_load(const Params& p, WrStage<NJ>& st, int m0, int n0, int k0) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int q = t + NTHR * i;
+    const int row = q >> 3, c = q & 7;
+    const int r = m0 + row, k = k0 + 4 * c;
+    bool ok = r < p.M && k < p.K;
+    int64_t o = (int64_t)r * p.lda + k;
+    if (CONV) {
+      const int pos = r % p.convF + k / p.convC - 1;
+      ok = ok && pos >= 0 && pos < p.convF;
+      o -= p.convC;
+    }
+    // unconditional load from a clamped address (a branch around the load would make the
+    // compiler drain vmcnt at the join, serialising the prefetch)
+    st.a[i] = *reinterpret_cast<const float4*>(ok ? (const void*)(p.A + o) : (const void*)zero_page);
+  }
+#pragma unroll
+  for (int i = 0; i < NJ; ++i) {
+    const int q = t + NTHR * i;
+    const int n = n0 + (q >> 2), k = k0 + 8 * (q & 3);
+    st.b[i] = *reinterpret_cast<const uint4*>((n < p.N && k < p.K) ? (const void*)(p.W + (int64_t)n * p.ldw + k)
+                                                                  : (const void*)zero_page);
+  }
+}
+
+// A image: [128 rows][4 chunks of 8 bf16] (64 B rows), W image: [BN rows][4 chunks], both with the
+// chunk XOR swizzle swb(row) (conflict-free ds_read_b128 fragment reads).
+template <int NJ>
+__device__ __forceinline__ void wr_store(const WrStage<NJ>& st, char* At, char* Bt) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int q = t + NTHR * i;
+    const int row = q >> 3, c = q & 7;
+    const float4 v = st.a[i];
+    typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+    bf16x4 h;
+    h[0] = (__bf16)v.x; h[1] = (__bf16)v.y; h[2] = (__bf16)v.z; h[3] = (__bf16)v.w;
+    *reinterpret_cast<bf16x4*>(At + row * 64 + 16 * ((c >> 1) ^ swb(row)) + 8 * (c & 1)) = h;
+  }
+#pragma unroll
+  for (int i = 0; i < NJ; ++i) {
+    const int q = t + NTHR * i;
+    const int n = q >> 2, c = q & 3;
+    *reinterpret_cast<uint4*>(Bt + n * 64 + 16 * (c ^ swb(n))) = st.b[i];
+  }
+}
+
+template <int NJ, bool CONV, bool RT>
+__global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) {
+  typedef Cfg<NJ> CF;
+  constexpr int BN = CF::BN, NT = 2 * NJ, BNR = CF::BNR;
+  constexpr int AB = BM * BK * 2, BB = BN * BK * 2;  // bf16 images
+  __shared__ __attribute__((aligned(16))) char a_img[2][AB];
+  __shared__ __attribute__((aligned(16))) char b_img[2][BB];
+  __shared__ __attribute__((aligned(16))) float bias_s[2][BNR];
+  __shared__ float w2s[RT ? 3 * BN : 1];
+  __shared__ float red[RT ? BM * 12 : 1];
+  if constexpr (RT) {
+    for (int i = threadIdx.x; i < 3 * BN; i += NTHR) {
+      const int k = i / BN, n = i % BN;
+      w2s[i] = n < p.N ? p.W2[k * p.N + n] : 0.f;
+    }
+  }
+
+  const int nN = (p.N + BN - 1) / BN;
+  const int nk = (p.K + BK - 1) / BK;
+  const int G = gridDim.x, bid = blockIdx.x;
+  const int r = (G % 8 == 0) ? (bid & 7) * (G >> 3) + (bid >> 3) : bid;  // XCD-grouped tile ranks
+  const int my = r < ntiles ? (ntiles - r + G - 1) / G : 0;
+  const int S = my * nk;
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wm = wid >> 2, wn = wid & 3;
+  const int lr = lane & 15, lk = lane >> 4;
+  const bool vec = vec_ok(p);
+
+  auto coords = [&](int s, int& m0, int& n0, int& k0) __attribute__((always_inline)) {
+    const int j = s / nk;
+    const int t = j * G + r;
+    m0 = (t / nN) * BM;
+    n0 = (t % nN) * BN;
+    k0 = (s - j * nk) * BK;
+  };
+  auto load = [&](int s, WrStage<NJ>& st) __attribute__((always_inline)) {
+    int m0, n0, k0;
+    coords(s, m0, n0, k0);
+    wr_load<NJ, CONV>(p, st, m0, n0, k0);
+  };
+  auto store = [&](int s, const WrStage<NJ>& st) __attribute__((always_inline)) {
+    wr_store<NJ>(st, a_img[s & 1], b_img[s & 1]);
+    if (s % nk == 0) {  // first k-step of a tile: its bias slice (read by the tile's epilogue)
+      int m0, n0, k0;
+      coords(s, m0, n0, k0);
+      float* dst = bias_s[(s / nk) & 1];
+      for (int c = threadIdx.x; c < BN; c += NTHR) dst[c] = (p.bias && n0 + c < p.N) ? p.bias[n0 + c] : 0.f;
+    }
+  };
+
+  f32x4 acc[4][NT];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  static_assert(WR_DEPTH == 3, "the k-loop below is written out for three stage register sets");
+  WrStage<NJ> st0, st1, st2;  // named (not an array) so they stay in VGPRs
+  if (S > 0) load(0, st0);
+  if (S > 1) load(1, st1);
+  if (S > 2) load(2, st2);
+  if (S > 0) store(0, st0);
+  __syncthreads();
+
+  // one k-step: `cur` held step s (already in LDS) and is refilled with step s + 3; `nxt` holds
+  // step s + 1, which goes into the other LDS image after this step's MFMAs
+  auto kstep = [&](int s, WrStage<NJ>& cur, const WrStage<NJ>& nxt) __attribute__((always_inline)) {
+    // unconditional: past the last step the A rows fall beyond M and read the zero page, so the
+    // number of loads in flight is the same on every path and the compiler's vmcnt waits stay
+    // counted (a conditional load here would force vmcnt(0) at every later wait)
+    load(s + WR_DEPTH, cur);
+    const char* At = a_img[s & 1];
+    const char* Bt = b_img[s & 1];
+    bf16x8 a[4], b[NT];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const int rr = wm * 64 + mt * 16 + lr;
+      a[mt] = *reinterpret_cast<const bf16x8*>(At + rr * 64 + 16 * (lk ^ swb(rr)));
+    }
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int n = wn * (32 * NJ) + nt * 16 + lr;
+      b[nt] = *reinterpret_cast<const bf16x8*>(Bt + n * 64 + 16 * (lk ^ swb(n)));
+    }
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nt], a[mt], acc[mt][nt], 0, 0, 0);
+    if (s + 1 < S) store(s + 1, nxt);
+    if (s % nk == nk - 1) {
+      int m0, n0, k0;
+      coords(s, m0, n0, k0);
+      const float* bsl = bias_s[(s / nk) & 1];
+      if constexpr (RT) {
+        epilogue_router<NJ>(p, acc, bsl, w2s, red, m0, wm, wn, lr, lk);
+      } else switch (p.act) {
+        case ACT_GELU: epilogue<NJ, ACT_GELU>(p, acc, bsl, m0, n0, wm, wn, lr, lk); break;
+        case ACT_SILU: epilogue<NJ, ACT_SILU>(p, acc, bsl, m0, n0, wm, wn, lr, lk); break;
+        case ACT_SIGMOID: epilogue<NJ, ACT_SIGMOID>(p, acc, bsl, m0, n0, wm, wn, lr, lk); break;
+        case ACT_RELU: epilogue<NJ, ACT_RELU>(p, acc, bsl, m0, n0, wm, wn, lr, lk); break;
+        default: epilogue<NJ, ACT_NONE>(p, acc, bsl, m0, n0, wm, wn, lr, lk); break;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int q = 0; q < NT; ++q) acc[i][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    __syncthreads();
+  };
+
+  for (int s = 0; s < S; s += WR_DEPTH) {
+    kstep(s, st0, st1);
+    if (s + 1 < S) kstep(s + 1, st1, st2);
+    if (s + 2 < S) kstep(s + 2, st2, st0);
+  }
+}
+
+template <int NJ, bool CONV, bool RT = false>
+static void launch_wr(const Params& p, hipStream_t s) {
+  static int resident = 0;
+  const void* fn = (const void*)gemm_wr_kernel<NJ, CONV, RT>;
+  if (!resident) {
+    int per_cu = 0, dev = 0, cus = 0;
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, NTHR, 0);
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    resident = std::max(1, per_cu) * std::max(1, cus);
+  }
+  const int tiles = ((p.M + BM - 1) / BM) * ((p.N + Cfg<NJ>::BN - 1) / Cfg<NJ>::BN);
+  const int grid = std::min(tiles, resident);
+  gemm_wr_kernel<NJ, CONV, RT><<<grid, NTHR, 0, s>>>(p, tiles);
+}
+
 // fp32 (rows x cols, row stride ld) -> bf16 N x K contiguous.  trans == 0: N = rows, K = cols;
 // trans == 1: N = cols, K = rows (the weight is used transposed, e.g. dgrad's dY W).
 __global__ void weight_to_bf16_kernel(const float* __restrict__ src, unsigned short* __restrict__ dst, int rows,
@@ -437,6 +642,13 @@ extern "C" int asrx_gemm_wn(const float* A, int64_t lda, int conv, int64_t convF
   ASRX_REQUIRE(!conv || (convF > 0 && convC % 4 == 0), "asrx_gemm_wn: conv needs F > 0 and C %% 4 == 0");
   wn::Params p{A, (int)lda, W, (int)ldw, C, (int)ldc, bias, Z, (int)M, (int)N, (int)K,
                (int)(convF > 0 ? convF : 1), (int)(convC > 0 ? convC : 1), alpha, beta, act, nullptr, nullptr};
+  static const bool use_dma = getenv("ASRX_WN_IMPL") && std::string(getenv("ASRX_WN_IMPL")) == "dma";
+  if (!use_dma) {
+    if (nj == 3) conv ? wn::launch_wr<3, true>(p, stream) : wn::launch_wr<3, false>(p, stream);
+    else if (nj == 2) conv ? wn::launch_wr<2, true>(p, stream) : wn::launch_wr<2, false>(p, stream);
+    else conv ? wn::launch_wr<1, true>(p, stream) : wn::launch_wr<1, false>(p, stream);
+    ASRX_LAUNCHED("asrx_gemm_wn");
+  }
   // ring depth: 3 stages for short K (more tile switches to hide), 2 for long K (measured)
   if (nj == 3) {
     if (K <= 512) conv ? wn::launch<3, true, 3>(p, stream) : wn::launch<3, false, 3>(p, stream);
@@ -461,6 +673,13 @@ extern "C" int asrx_gemm_wn_router(const float* A, int64_t lda, const unsigned s
   ASRX_REQUIRE(M * lda < (1LL << 31), "asrx_gemm_wn_router: operand spans >= 2^31 elements");
   wn::Params p{A, (int)lda, W1, (int)ldw, hpre, (int)ldc, b1, nullptr, (int)M, (int)N, (int)K, 1, 1, 1.f, 0.f,
                ACT_NONE, W2, logits};
+  static const bool use_dma = getenv("ASRX_WN_IMPL") && std::string(getenv("ASRX_WN_IMPL")) == "dma";
+  if (!use_dma) {
+    if (N <= 128) wn::launch_wr<1, false, true>(p, stream);
+    else if (N <= 256) wn::launch_wr<2, false, true>(p, stream);
+    else wn::launch_wr<3, false, true>(p, stream);
+    ASRX_LAUNCHED("asrx_gemm_wn_router");
+  }
   if (N <= 128) wn::launch<1, false, 3, true>(p, stream);
   else if (N <= 256) wn::launch<2, false, 2, true>(p, stream);
   else if (K <= 512) wn::launch<3, false, 3, true>(p, stream);
