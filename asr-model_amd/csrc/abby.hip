@@ -8,7 +8,8 @@
 //   div    = dec0*avg + dec1*(max > 2 avg ? max : avg) + dec2*avg
 //   out    = x / (1 + 1e-4 div)^0.75
 //
-// One wave per row (d % 64 == 0, d <= 1024); x^2 is staged in LDS for the windowed pools.
+// One wave per row (d % 64 == 0, d <= 1024); each lane owns d/64 consecutive features and reads
+// its window halo of x^2 from a padded per-wave LDS row (see AbbyShape).
 // Noise: gumbel g_k = -log(-log(u)) with u = noise_uniform(key, ((sid*H + h)*4096 + l)*3 + k); the
 // row r (kernel order: sample-major, then position, then head) maps to sid = sid_base + r/(L*H),
 // l = (r % (L*H)) / H, h = r % H.
@@ -21,7 +22,6 @@
 namespace asrx {
 
 constexpr int ABBY_WAVES = 4;
-constexpr int ABBY_MAXE = 16;  // d <= 1024
 
 struct AbbyGeom {
   int64_t rows, d;
@@ -31,12 +31,20 @@ struct AbbyGeom {
   int use_noise;
 };
 
-__device__ __forceinline__ int abby_window(int d) {
-  int w = (int)(d * 0.05f);
-  if (w < 3) w = 3;
-  if ((w & 1) == 0) w += 1;
-  return w;
-}
+// Per-row layout (MI355X design): lane l owns the E = d/64 CONSECUTIVE features [l E, l E + E), read
+// and written as float2; a wave reads the 2 PAD neighbours its windows need (the halo) from a
+// per-wave LDS row of x^2 padded with PAD entries of -1 on both sides (-inf for the max pool, 0
+// for the zero-padded avg pool after fmax(.,0)).  Window sums are running sums and window maxima
+// a register scan, so the pools cost O(E + W) per lane instead of W LDS reads per feature.
+template <int E>
+struct AbbyShape {
+  static constexpr int D = 64 * E;
+  static constexpr int W0 = (int)(D * 0.05f);
+  static constexpr int W = ((W0 < 3 ? 3 : W0) % 2 == 0) ? (W0 < 3 ? 3 : W0) + 1 : (W0 < 3 ? 3 : W0);
+  static constexpr int PAD = W / 2;
+  static constexpr int HL = E + 2 * PAD;      // halo length per lane
+  static constexpr int ROW = D + 2 * PAD + 2;  // padded LDS row (even, so lane bases stay 8-byte aligned)
+};
 
 __device__ __forceinline__ uint32_t abby_noise_idx(const AbbyGeom& g, int64_t r, int k) {
   const int64_t per = g.L * g.H;
@@ -46,49 +54,111 @@ __device__ __forceinline__ uint32_t abby_noise_idx(const AbbyGeom& g, int64_t r,
   return (uint32_t)(((sid * g.H + h) * 4096 + l) * 3 + k);
 }
 
-// Row statistics shared by fwd and bwd.
 template <int E>
-__device__ __forceinline__ void abby_row_stats(const float (&xv)[ABBY_MAXE], int d, float& mu, float& sd,
-                                               float& mabs) {
+__device__ __forceinline__ void ld_row(const float* __restrict__ src, int lane, float (&v)[E]) {
+  if constexpr (E % 2 == 0) {
+    const float2* s2 = reinterpret_cast<const float2*>(src + lane * E);
+#pragma unroll
+    for (int e = 0; e < E / 2; ++e) {
+      const float2 t = s2[e];
+      v[2 * e] = t.x;
+      v[2 * e + 1] = t.y;
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < E; ++e) v[e] = src[lane * E + e];
+  }
+}
+
+template <int E>
+__device__ __forceinline__ void st_row(float* __restrict__ dst, int lane, const float (&v)[E]) {
+  if constexpr (E % 2 == 0) {
+    float2* d2 = reinterpret_cast<float2*>(dst + lane * E);
+#pragma unroll
+    for (int e = 0; e < E / 2; ++e) d2[e] = make_float2(v[2 * e], v[2 * e + 1]);
+  } else {
+#pragma unroll
+    for (int e = 0; e < E; ++e) dst[lane * E + e] = v[e];
+  }
+}
+
+// row statistics (cv = std(x, unbiased) / (mean|x| + 1e-6)) from the lane-contiguous values
+template <int E>
+__device__ __forceinline__ void abby_row_stats(const float (&xv)[E], float& mu, float& sd, float& mabs) {
+  constexpr int D = 64 * E;
   float s = 0.f, sa = 0.f;
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     s += xv[e];
     sa += fabsf(xv[e]);
   }
-  s = wave_sum(s);
-  sa = wave_sum(sa);
-  mu = s / d;
-  mabs = sa / d;
+  s = wave_sum_dpp(s);
+  sa = wave_sum_dpp(sa);
+  mu = s / D;
+  mabs = sa / D;
   float v = 0.f;
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const float t = xv[e] - mu;
     v += t * t;
   }
-  v = wave_sum(v);
-  sd = sqrtf(v / (d - 1));
+  v = wave_sum_dpp(v);
+  sd = sqrtf(v / (D - 1));
 }
 
-// avg / max pool of sq (LDS row) at element j.  Returns avg, max and the argmax index (first max).
-__device__ __forceinline__ void abby_pool(const float* sq, int d, int w, int j, float& avg, float& mx,
-                                          int& amax) {
-  const int pad = w >> 1;
-  float s = 0.f, m = -INFINITY;
-  int am = j;
-  const int lo = j - pad, hi = j + pad;
-  for (int i = lo; i <= hi; ++i) {
-    if (i < 0 || i >= d) continue;
-    const float v = sq[i];
-    s += v;
-    if (v > m) {
-      m = v;
-      am = i;
-    }
+// stage x^2 of this lane's features in the wave's padded LDS row and read back the halo
+template <int E>
+__device__ __forceinline__ void abby_halo(float* row, int lane, const float (&xv)[E], float (&h)[AbbyShape<E>::HL]) {
+  typedef AbbyShape<E> S;
+#pragma unroll
+  for (int e = 0; e < E; ++e) row[S::PAD + lane * E + e] = xv[e] * xv[e];
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#pragma unroll
+  for (int i = 0; i < S::HL; ++i) h[i] = row[lane * E + i];
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+}
+
+// window sums (zero padding) of the halo for the lane's E outputs
+template <int E>
+__device__ __forceinline__ void abby_wsum(const float (&h)[AbbyShape<E>::HL], float (&avg)[E]) {
+  typedef AbbyShape<E> S;
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < S::W; ++i) s += fmaxf(h[i], 0.f);
+  avg[0] = s * (1.0f / S::W);
+#pragma unroll
+  for (int e = 1; e < E; ++e) {
+    s += fmaxf(h[e + S::W - 1], 0.f) - fmaxf(h[e - 1], 0.f);
+    avg[e] = s * (1.0f / S::W);
   }
-  avg = s / (float)w;
-  mx = m;
-  amax = am;
+}
+
+// window max and first argmax (as an offset into the halo) for the lane's E outputs
+template <int E, bool ARG>
+__device__ __forceinline__ void abby_wmax(const float (&h)[AbbyShape<E>::HL], float (&mx)[E], int (&am)[E]) {
+  typedef AbbyShape<E> S;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    float m = h[e];
+    int a = e;
+#pragma unroll
+    for (int i = 1; i < S::W; ++i) {
+      const float v = h[e + i];
+      if (ARG) {
+        a = v > m ? e + i : a;
+      }
+      m = fmaxf(m, v);
+    }
+    mx[e] = m;
+    if (ARG) am[e] = a;
+  }
+}
+
+__device__ __forceinline__ float abby_denom(float div, float& base) {
+  base = div * 1e-4f + 1.0f;
+  return __builtin_amdgcn_exp2f(0.75f * __builtin_amdgcn_logf(base));  // base^0.75, base >= 1
 }
 
 template <int E>
@@ -99,43 +169,46 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_fwd_kernel(const float* 
                                                                   float* __restrict__ out, float* __restrict__ ys,
                                                                   int* __restrict__ idx_out, AbbyGeom g,
                                                                   const float* __restrict__ logits) {
-  __shared__ float sq_all[ABBY_WAVES][64 * ABBY_MAXE];
+  typedef AbbyShape<E> S;
+  __shared__ __attribute__((aligned(16))) float rows_all[ABBY_WAVES][S::ROW];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  float* sq = sq_all[wid];
-  const int d = (int)g.d;
-  const int w = abby_window(d);
-  for (int64_t r = (int64_t)blockIdx.x * ABBY_WAVES + wid; r < g.rows; r += (int64_t)gridDim.x * ABBY_WAVES) {
-    const float* xr = x + r * d;
-    float xv[ABBY_MAXE];
-    float l0 = 0.f, l1 = 0.f, l2 = 0.f;
-    if (logits) {  // router logits from the GEMM epilogue (asrx_gemm_wn_router)
+  float* row = rows_all[wid];
+  for (int i = lane; i < S::PAD; i += 64) {  // pads: -1 (below every x^2)
+    row[i] = -1.f;
+    row[S::PAD + S::D + i] = -1.f;
+  }
+  const int64_t stride = (int64_t)gridDim.x * ABBY_WAVES;
+  int64_t r = (int64_t)blockIdx.x * ABBY_WAVES + wid;
+  float xn[E];  // next row's x, loaded while this row is processed
+  if (r < g.rows) ld_row<E>(x + r * S::D, lane, xn);
+  for (; r < g.rows; r += stride) {
+    float xv[E];
 #pragma unroll
-      for (int e = 0; e < E; ++e) {
-        const int j = e * 64 + lane;
-        xv[e] = xr[j];
-        sq[j] = xv[e] * xv[e];
-      }
+    for (int e = 0; e < E; ++e) xv[e] = xn[e];
+    if (r + stride < g.rows) ld_row<E>(x + (r + stride) * S::D, lane, xn);
+    float l0, l1, l2;
+    if (logits) {  // router logits from the GEMM epilogue (asrx_gemm_wn_router)
       l0 = logits[r * 3 + 0];
       l1 = logits[r * 3 + 1];
       l2 = logits[r * 3 + 2];
     } else {
-      const float* hr = hpre + r * d;
+      float hv[E];
+      ld_row<E>(hpre + r * S::D, lane, hv);
+      l0 = l1 = l2 = 0.f;
 #pragma unroll
       for (int e = 0; e < E; ++e) {
-        const int j = e * 64 + lane;
-        xv[e] = xr[j];
-        const float hs = silu_f(hr[j]);
+        const int j = lane * E + e;
+        const float hs = silu_f(hv[e]);
         l0 += hs * W2[j];
-        l1 += hs * W2[d + j];
-        l2 += hs * W2[2 * d + j];
-        sq[j] = xv[e] * xv[e];
+        l1 += hs * W2[S::D + j];
+        l2 += hs * W2[2 * S::D + j];
       }
-      l0 = wave_sum(l0);
-      l1 = wave_sum(l1);
-      l2 = wave_sum(l2);
+      l0 = wave_sum_dpp(l0);
+      l1 = wave_sum_dpp(l1);
+      l2 = wave_sum_dpp(l2);
     }
     float mu, sd, mabs;
-    abby_row_stats<E>(xv, d, mu, sd, mabs);
+    abby_row_stats<E>(xv, mu, sd, mabs);
     const float cv = sd / (mabs + 1e-6f);
     float z0 = l0 + b2[0] + cv, z1 = l1 + b2[1] + cv, z2 = l2 + b2[2] + cv;
     if (g.use_noise) {
@@ -160,21 +233,23 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_fwd_kernel(const float* 
       ys[r * 3 + 2] = y2;
       idx_out[r] = sel;
     }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    float* o = out + r * d;
+    float h[S::HL];
+    abby_halo<E>(row, lane, xv, h);
+    float avg[E], ov[E];
+    abby_wsum<E>(h, avg);
+    if (sel == 1) {  // wave-uniform: mode 2 (max pool where max > 2 avg)
+      float mx[E];
+      int am[E];
+      abby_wmax<E, false>(h, mx, am);
+#pragma unroll
+      for (int e = 0; e < E; ++e) avg[e] = mx[e] > 2.0f * avg[e] ? mx[e] : avg[e];
+    }
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      const int j = e * 64 + lane;
-      float avg, mx;
-      int am;
-      abby_pool(sq, d, w, j, avg, mx, am);
-      const float div = (sel == 1 && mx > 2.0f * avg) ? mx : avg;
-      const float denom = powf(div * 1e-4f + 1.0f, 0.75f);
-      o[j] = xv[e] / denom;
+      float base;
+      ov[e] = xv[e] / abby_denom(avg[e], base);
     }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    st_row<E>(out + r * S::D, lane, ov);
   }
 }
 
@@ -184,150 +259,189 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_bwd_kernel(
     const float* __restrict__ W2, const float* __restrict__ ys, const int* __restrict__ idx_in,
     float* __restrict__ dx, float* __restrict__ dhpre, float* __restrict__ dW2, float* __restrict__ db2,
     AbbyGeom g) {
-  __shared__ float sq_all[ABBY_WAVES][64 * ABBY_MAXE];
-  __shared__ float cA_all[ABBY_WAVES][64 * ABBY_MAXE];  // q_j * coefA_j / w
-  __shared__ float cM_all[ABBY_WAVES][64 * ABBY_MAXE];  // q_j * coefM_j
-  __shared__ int am_all[ABBY_WAVES][64 * ABBY_MAXE];
-  __shared__ float red[ABBY_WAVES][4];
+  typedef AbbyShape<E> S;
+  __shared__ __attribute__((aligned(16))) float rows_all[ABBY_WAVES][S::ROW];   // x^2, then q coefA / w
+  __shared__ __attribute__((aligned(16))) float cm_all[ABBY_WAVES][S::ROW];     // q coefM (sel == 1)
+  __shared__ __attribute__((aligned(16))) int am_all[ABBY_WAVES][S::ROW];       // argmax (halo offset + base)
+  __shared__ float red[ABBY_WAVES][3];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  float* sq = sq_all[wid];
-  float* cA = cA_all[wid];
-  float* cM = cM_all[wid];
-  int* amx = am_all[wid];
-  const int d = (int)g.d;
-  const int w = abby_window(d);
-  float accW[3][ABBY_MAXE];
+  float* row = rows_all[wid];
+  float* cmr = cm_all[wid];
+  int* amr = am_all[wid];
+  float accW[3][E];
   float accb[3] = {0.f, 0.f, 0.f};
 #pragma unroll
   for (int k = 0; k < 3; ++k)
 #pragma unroll
-    for (int e = 0; e < ABBY_MAXE; ++e) accW[k][e] = 0.f;
+    for (int e = 0; e < E; ++e) accW[k][e] = 0.f;
 
-  for (int64_t r = (int64_t)blockIdx.x * ABBY_WAVES + wid; r < g.rows; r += (int64_t)gridDim.x * ABBY_WAVES) {
-    const float* xr = x + r * d;
-    const float* gr = dout + r * d;
-    float xv[ABBY_MAXE], gv[ABBY_MAXE], qv[ABBY_MAXE], avgv[ABBY_MAXE], m2v[ABBY_MAXE];
+  const int64_t stride = (int64_t)gridDim.x * ABBY_WAVES;
+  int64_t r = (int64_t)blockIdx.x * ABBY_WAVES + wid;
+  float xn[E], gn[E];  // next row's x and dout, loaded while this row is processed
+  if (r < g.rows) {
+    ld_row<E>(x + r * S::D, lane, xn);
+    ld_row<E>(dout + r * S::D, lane, gn);
+  }
+  for (; r < g.rows; r += stride) {
+    float xv[E], gv[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      const int j = e * 64 + lane;
-      xv[e] = xr[j];
-      gv[e] = gr[j];
-      sq[j] = xv[e] * xv[e];
+      xv[e] = xn[e];
+      gv[e] = gn[e];
+    }
+    if (r + stride < g.rows) {
+      ld_row<E>(x + (r + stride) * S::D, lane, xn);
+      ld_row<E>(dout + (r + stride) * S::D, lane, gn);
     }
     const int sel = idx_in[r];
     const float y0 = ys[r * 3 + 0], y1 = ys[r * 3 + 1], y2 = ys[r * 3 + 2];
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    // the pad entries of `row` hold -1 for the x^2 halo; the coefficient pass below re-pads with 0
+    for (int i = lane; i < S::PAD; i += 64) {
+      row[i] = -1.f;
+      row[S::PAD + S::D + i] = -1.f;
+    }
+    float h[S::HL];
+    abby_halo<E>(row, lane, xv, h);
+    // mode 2 enters dd1 (the straight-through gradient of the mode choice) on every row; its
+    // argmax is needed only where mode 2 was chosen (sel == 1, wave-uniform)
+    float avg[E], m2[E], mx[E];
+    int am[E];
+    abby_wsum<E>(h, avg);
+    if (sel == 1) {
+      abby_wmax<E, true>(h, mx, am);
+    } else {
+      abby_wmax<E, false>(h, mx, am);
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) m2[e] = mx[e] > 2.0f * avg[e] ? mx[e] : avg[e];
+    float dxv[E], qa[E], qm[E];
     float dd0 = 0.f, dd1 = 0.f;  // dd2 == dd0 (mode3 == mode1 == avg)
-    float dxv[ABBY_MAXE];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      const int j = e * 64 + lane;
-      float avg, mx;
-      int am;
-      abby_pool(sq, d, w, j, avg, mx, am);
-      const bool cnd = mx > 2.0f * avg;
-      const float mode2 = cnd ? mx : avg;
-      const float div = (sel == 1) ? mode2 : avg;
-      const float base = div * 1e-4f + 1.0f;
-      const float denom = powf(base, 0.75f);
+      const float div = sel == 1 ? m2[e] : avg[e];
+      float base;
+      const float denom = abby_denom(div, base);
       dxv[e] = gv[e] / denom;
       const float q = -gv[e] * xv[e] * (1e-4f * 0.75f) / (denom * base);
-      qv[e] = q;
-      avgv[e] = avg;
-      m2v[e] = mode2;
-      dd0 += q * avg;
-      dd1 += q * mode2;
-      float coefA, coefM;
-      if (sel == 1) {
-        coefA = cnd ? 0.f : 1.f;
-        coefM = cnd ? 1.f : 0.f;
-      } else {
-        coefA = 1.f;
-        coefM = 0.f;
-      }
-      cA[j] = q * coefA / (float)w;
-      cM[j] = q * coefM;
-      amx[j] = am;
+      dd0 += q * avg[e];
+      dd1 += q * m2[e];
+      const bool maxsel = sel == 1 && m2[e] != avg[e];
+      qa[e] = maxsel ? 0.f : q * (1.0f / S::W);
+      qm[e] = maxsel ? q : 0.f;
     }
-    dd0 = wave_sum(dd0);
-    dd1 = wave_sum(dd1);
+    dd0 = wave_sum_dpp(dd0);
+    dd1 = wave_sum_dpp(dd1);
     const float dd2 = dd0;
+    // pool backward in gather form: dsq_i = sum_{j in win(i)} qa_j + sum_{j in win(i), am_j == i} qm_j
+    for (int i = lane; i < S::PAD; i += 64) {
+      row[i] = 0.f;
+      row[S::PAD + S::D + i] = 0.f;
+      if (sel == 1) {
+        cmr[i] = 0.f;
+        cmr[S::PAD + S::D + i] = 0.f;
+        amr[i] = -1;
+        amr[S::PAD + S::D + i] = -1;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) row[S::PAD + lane * E + e] = qa[e];
+    if (sel == 1) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        cmr[S::PAD + lane * E + e] = qm[e];
+        amr[S::PAD + lane * E + e] = lane * E + am[e] - S::PAD;  // feature index of the argmax
+      }
+    }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    // pool backward (gather form): dsq_i = sum_{j in win(i)} cA_j + sum_{j in win(i), amax_j == i} cM_j
-    const int pad = w >> 1;
+    {
+      float ha[S::HL];
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const int i = e * 64 + lane;
+      for (int i = 0; i < S::HL; ++i) ha[i] = row[lane * E + i];
       float s = 0.f;
-      for (int j = i - pad; j <= i + pad; ++j) {
-        if (j < 0 || j >= d) continue;
-        s += cA[j];
-        if (amx[j] == i) s += cM[j];
+#pragma unroll
+      for (int i = 0; i < S::W; ++i) s += ha[i];
+      dxv[0] += 2.0f * xv[0] * s;
+#pragma unroll
+      for (int e = 1; e < E; ++e) {
+        s += ha[e + S::W - 1] - ha[e - 1];
+        dxv[e] += 2.0f * xv[e] * s;
       }
-      dxv[e] += 2.0f * xv[e] * s;
     }
+    if (sel == 1) {
+      float hc[S::HL];
+      int hm[S::HL];
+#pragma unroll
+      for (int i = 0; i < S::HL; ++i) {  // halo position i holds feature lane E - PAD + i
+        hc[i] = cmr[lane * E + i];
+        hm[i] = amr[lane * E + i];
+      }
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int fi = lane * E + e;
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < S::W; ++i) s += hm[e + i] == fi ? hc[e + i] : 0.f;
+        dxv[e] += 2.0f * xv[e] * s;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     // straight-through softmax backward
     const float dot = y0 * dd0 + y1 * dd1 + y2 * dd2;
     const float dz0 = y0 * (dd0 - dot), dz1 = y1 * (dd1 - dot), dz2 = y2 * (dd2 - dot);
     const float dcv = dz0 + dz1 + dz2;
     // cv = sd / (mabs + 1e-6)
     float mu, sd, mabs;
-    abby_row_stats<E>(xv, d, mu, sd, mabs);
+    abby_row_stats<E>(xv, mu, sd, mabs);
     const float den = mabs + 1e-6f;
     const float dsd = dcv / den;
     const float dmabs = -dcv * sd / (den * den);
-    const float csd = sd > 0.f ? dsd / ((d - 1) * sd) : 0.f;
-    const float cma = dmabs / d;
-    const float* hr = hpre + r * d;
-    float* dxo = dx + r * d;
-    float* dho = dhpre + r * d;
+    const float csd = sd > 0.f ? dsd / ((S::D - 1) * sd) : 0.f;
+    const float cma = dmabs / S::D;
+    float hv[E], dh[E], w2v[3][E];
+    ld_row<E>(hpre + r * S::D, lane, hv);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) ld_row<E>(W2 + k * S::D, lane, w2v[k]);  // L1-resident
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      const int j = e * 64 + lane;
       const float sgn = xv[e] > 0.f ? 1.f : (xv[e] < 0.f ? -1.f : 0.f);
-      dxo[j] = dxv[e] + csd * (xv[e] - mu) + cma * sgn;
-      const float h = hr[j];
-      const float wsum = dz0 * W2[j] + dz1 * W2[d + j] + dz2 * W2[2 * d + j];
-      dho[j] = silu_grad(h) * wsum;
-      const float hs = silu_f(h);
+      dxv[e] += csd * (xv[e] - mu) + cma * sgn;
+      const float wsum = dz0 * w2v[0][e] + dz1 * w2v[1][e] + dz2 * w2v[2][e];
+      dh[e] = silu_grad(hv[e]) * wsum;
+      const float hs = silu_f(hv[e]);
       accW[0][e] += dz0 * hs;
       accW[1][e] += dz1 * hs;
       accW[2][e] += dz2 * hs;
     }
+    st_row<E>(dx + r * S::D, lane, dxv);
+    st_row<E>(dhpre + r * S::D, lane, dh);
     accb[0] += dz0;
     accb[1] += dz1;
     accb[2] += dz2;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   }
-  // workgroup reduction of dW2 / db2, then one atomic per element
+  // workgroup reduction of dW2 / db2 through LDS, then one atomic per element
   __syncthreads();
-  float* buf = sq_all[0];  // reuse: 3 * d floats <= 3072 < 4 * 1024
-#pragma unroll
-  for (int e = 0; e < E; ++e) {
-    const int j = e * 64 + lane;
-    if (wid == 0) {
-      buf[j] = accW[0][e];
-      buf[d + j] = accW[1][e];
-      buf[2 * d + j] = accW[2][e];
-    }
-  }
-  __syncthreads();
-  for (int ww = 1; ww < ABBY_WAVES; ++ww) {
+  float* buf = &rows_all[0][0];  // 3 D floats fit in the 4 x ROW x-rows plus the cm rows
+  float* buf2 = &cm_all[0][0];
+  static_assert(3 * S::D <= 2 * ABBY_WAVES * S::ROW, "dW2 staging must fit");
+  auto slot = [&](int k, int j) -> float* {
+    const int i = k * S::D + j;
+    return i < ABBY_WAVES * S::ROW ? buf + i : buf2 + (i - ABBY_WAVES * S::ROW);
+  };
+  for (int ww = 0; ww < ABBY_WAVES; ++ww) {
     if (wid == ww) {
 #pragma unroll
-      for (int e = 0; e < E; ++e) {
-        const int j = e * 64 + lane;
-        buf[j] += accW[0][e];
-        buf[d + j] += accW[1][e];
-        buf[2 * d + j] += accW[2][e];
-      }
+      for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          float* sl = slot(k, lane * E + e);
+          *sl = (ww == 0 ? 0.f : *sl) + accW[k][e];
+        }
     }
     __syncthreads();
   }
-  for (int j = threadIdx.x; j < 3 * d; j += 64 * ABBY_WAVES) atomicAdd(dW2 + j, buf[j]);
+  for (int j = threadIdx.x; j < 3 * S::D; j += 64 * ABBY_WAVES) atomicAdd(dW2 + j, *slot(j / S::D, j % S::D));
   if (lane == 0) {
     red[wid][0] = accb[0];
     red[wid][1] = accb[1];
@@ -338,6 +452,257 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_bwd_kernel(
     float s = 0.f;
     for (int ww = 0; ww < ABBY_WAVES; ++ww) s += red[ww][threadIdx.x];
     atomicAdd(db2 + threadIdx.x, s);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// d = 64 (the per-head AbbyNormal on q and k, model.py:302-306): a 64-feature row is one DPP row of
+// 16 lanes holding 4 consecutive features each (float4 in, float4 out), 4 rows per wave.  Every
+// reduction is 4 in-row DPP steps and the w = 3 window halo is one row_shr / row_shl (the source
+// lane outside the 16-lane row leaves the pad value), so the kernel never touches LDS.
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));
+  return v;
+}
+// value of lane - 1 (row_shr:1) / lane + 1 (row_shl:1) in the same 16-lane row, `pad` at the row ends
+__device__ __forceinline__ float from_prev(float v, float pad) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, pad), __builtin_bit_cast(int, v),
+                                                               0x111, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float from_next(float v, float pad) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, pad), __builtin_bit_cast(int, v),
+                                                               0x101, 0xF, 0xF, false));
+}
+__device__ __forceinline__ int from_prev_i(int v, int pad) { return __builtin_amdgcn_update_dpp(pad, v, 0x111, 0xF, 0xF, false); }
+__device__ __forceinline__ int from_next_i(int v, int pad) { return __builtin_amdgcn_update_dpp(pad, v, 0x101, 0xF, 0xF, false); }
+
+struct Row64 {
+  float v[4];
+};
+__device__ __forceinline__ Row64 ld64(const float* p) {
+  const float4 t = *reinterpret_cast<const float4*>(p);
+  return Row64{{t.x, t.y, t.z, t.w}};
+}
+__device__ __forceinline__ void st64(float* p, const float (&v)[4]) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+}
+
+// x^2 halo of the lane's 4 features: h[0] = feature 4l - 1, h[1..4] own, h[5] = feature 4l + 4
+__device__ __forceinline__ void halo64(const float (&sq)[4], float (&h)[6]) {
+  h[0] = from_prev(sq[3], -1.f);
+  h[1] = sq[0]; h[2] = sq[1]; h[3] = sq[2]; h[4] = sq[3];
+  h[5] = from_next(sq[0], -1.f);
+}
+
+__device__ __forceinline__ void stats64(const float (&xv)[4], float& mu, float& sd, float& mabs) {
+  float s = xv[0] + xv[1] + xv[2] + xv[3];
+  float sa = fabsf(xv[0]) + fabsf(xv[1]) + fabsf(xv[2]) + fabsf(xv[3]);
+  s = row16_sum(s);
+  sa = row16_sum(sa);
+  mu = s / 64.f;
+  mabs = sa / 64.f;
+  float v = 0.f;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) v += (xv[e] - mu) * (xv[e] - mu);
+  sd = sqrtf(row16_sum(v) / 63.f);
+}
+
+__global__ __launch_bounds__(64 * ABBY_WAVES) void abby_fwd64_kernel(const float* __restrict__ x,
+                                                                    const float* __restrict__ hpre,
+                                                                    const float* __restrict__ W2,
+                                                                    const float* __restrict__ b2,
+                                                                    float* __restrict__ out, float* __restrict__ ys,
+                                                                    int* __restrict__ idx_out, AbbyGeom g,
+                                                                    const float* __restrict__ logits) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, l16 = lane & 15;
+  const int64_t stride = (int64_t)gridDim.x * ABBY_WAVES * 4;
+  for (int64_t r = ((int64_t)blockIdx.x * ABBY_WAVES + wid) * 4 + (lane >> 4); r < g.rows; r += stride) {
+    // (rows is a multiple of nothing in particular: a 16-lane row past the end simply idles; the
+    // DPP reductions never cross rows, so the live rows are unaffected)
+    const Row64 xr = ld64(x + r * 64 + 4 * l16);
+    const float(&xv)[4] = xr.v;
+    float l0, l1, l2;
+    if (logits) {
+      l0 = logits[r * 3 + 0];
+      l1 = logits[r * 3 + 1];
+      l2 = logits[r * 3 + 2];
+    } else {
+      const Row64 hr = ld64(hpre + r * 64 + 4 * l16);
+      l0 = l1 = l2 = 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int j = 4 * l16 + e;
+        const float hs = silu_f(hr.v[e]);
+        l0 += hs * W2[j];
+        l1 += hs * W2[64 + j];
+        l2 += hs * W2[128 + j];
+      }
+      l0 = row16_sum(l0);
+      l1 = row16_sum(l1);
+      l2 = row16_sum(l2);
+    }
+    float mu, sd, mabs;
+    stats64(xv, mu, sd, mabs);
+    const float cv = sd / (mabs + 1e-6f);
+    float z0 = l0 + b2[0] + cv, z1 = l1 + b2[1] + cv, z2 = l2 + b2[2] + cv;
+    if (g.use_noise) {
+      z0 += noise_gumbel(g.key, abby_noise_idx(g, r, 0));
+      z1 += noise_gumbel(g.key, abby_noise_idx(g, r, 1));
+      z2 += noise_gumbel(g.key, abby_noise_idx(g, r, 2));
+    }
+    const float zm = fmaxf(z0, fmaxf(z1, z2));
+    const float e0 = expf(z0 - zm), e1 = expf(z1 - zm), e2 = expf(z2 - zm);
+    const float inv = 1.0f / (e0 + e1 + e2);
+    const float y0 = e0 * inv, y1 = e1 * inv, y2 = e2 * inv;
+    int sel = 0;
+    float ym = y0;
+    if (y1 > ym) {
+      sel = 1;
+      ym = y1;
+    }
+    if (y2 > ym) sel = 2;
+    if (l16 == 0) {
+      ys[r * 3 + 0] = y0;
+      ys[r * 3 + 1] = y1;
+      ys[r * 3 + 2] = y2;
+      idx_out[r] = sel;
+    }
+    float sq[4] = {xv[0] * xv[0], xv[1] * xv[1], xv[2] * xv[2], xv[3] * xv[3]};
+    float h[6];
+    halo64(sq, h);
+    float ov[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float avg = (fmaxf(h[e], 0.f) + h[e + 1] + fmaxf(h[e + 2], 0.f)) * (1.0f / 3.0f);
+      const float mx = fmaxf(h[e], fmaxf(h[e + 1], h[e + 2]));
+      const float div = (sel == 1 && mx > 2.0f * avg) ? mx : avg;
+      float base;
+      ov[e] = xv[e] / abby_denom(div, base);
+    }
+    st64(out + r * 64 + 4 * l16, ov);
+  }
+}
+
+__global__ __launch_bounds__(64 * ABBY_WAVES) void abby_bwd64_kernel(
+    const float* __restrict__ dout, const float* __restrict__ x, const float* __restrict__ hpre,
+    const float* __restrict__ W2, const float* __restrict__ ys, const int* __restrict__ idx_in,
+    float* __restrict__ dx, float* __restrict__ dhpre, float* __restrict__ dW2, float* __restrict__ db2,
+    AbbyGeom g) {
+  __shared__ float wred[ABBY_WAVES * 4][3 * 64 + 3];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, l16 = lane & 15;
+  float accW[3][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  float accb[3] = {0.f, 0.f, 0.f};
+  float w2v[3][4];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const Row64 t = ld64(W2 + k * 64 + 4 * l16);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) w2v[k][e] = t.v[e];
+  }
+  const int64_t stride = (int64_t)gridDim.x * ABBY_WAVES * 4;
+  for (int64_t r = ((int64_t)blockIdx.x * ABBY_WAVES + wid) * 4 + (lane >> 4); r < g.rows; r += stride) {
+    const Row64 xr = ld64(x + r * 64 + 4 * l16);
+    const Row64 gr = ld64(dout + r * 64 + 4 * l16);
+    const Row64 hr = ld64(hpre + r * 64 + 4 * l16);
+    const float(&xv)[4] = xr.v;
+    const float(&gv)[4] = gr.v;
+    const int sel = idx_in[r];
+    const float y0 = ys[r * 3 + 0], y1 = ys[r * 3 + 1], y2 = ys[r * 3 + 2];
+    float sq[4] = {xv[0] * xv[0], xv[1] * xv[1], xv[2] * xv[2], xv[3] * xv[3]};
+    float h[6];
+    halo64(sq, h);
+    float dxv[4], qa[4], qm[4];
+    int am[4];
+    float dd0 = 0.f, dd1 = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float avg = (fmaxf(h[e], 0.f) + h[e + 1] + fmaxf(h[e + 2], 0.f)) * (1.0f / 3.0f);
+      // max and first argmax over features 4l+e-1 .. 4l+e+1
+      float mx = h[e];
+      int a = 4 * l16 + e - 1;
+      if (h[e + 1] > mx) { mx = h[e + 1]; a = 4 * l16 + e; }
+      if (h[e + 2] > mx) { mx = h[e + 2]; a = 4 * l16 + e + 1; }
+      am[e] = a;
+      const bool cnd = mx > 2.0f * avg;
+      const float m2 = cnd ? mx : avg;
+      const float div = sel == 1 ? m2 : avg;
+      float base;
+      const float denom = abby_denom(div, base);
+      dxv[e] = gv[e] / denom;
+      const float q = -gv[e] * xv[e] * (1e-4f * 0.75f) / (denom * base);
+      dd0 += q * avg;
+      dd1 += q * m2;
+      const bool maxsel = sel == 1 && cnd;
+      qa[e] = maxsel ? 0.f : q * (1.0f / 3.0f);
+      qm[e] = maxsel ? q : 0.f;
+    }
+    dd0 = row16_sum(dd0);
+    dd1 = row16_sum(dd1);
+    const float dd2 = dd0;
+    // pool backward: dsq_i = qa_{i-1} + qa_i + qa_{i+1} + sum_{j in i-1..i+1, am_j == i} qm_j
+    {
+      const float qa_p = from_prev(qa[3], 0.f), qa_n = from_next(qa[0], 0.f);
+      const float qm_p = from_prev(qm[3], 0.f), qm_n = from_next(qm[0], 0.f);
+      const int am_p = from_prev_i(am[3], -2), am_n = from_next_i(am[0], -2);
+      const float qa6[6] = {qa_p, qa[0], qa[1], qa[2], qa[3], qa_n};
+      const float qm6[6] = {qm_p, qm[0], qm[1], qm[2], qm[3], qm_n};
+      const int am6[6] = {am_p, am[0], am[1], am[2], am[3], am_n};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int fi = 4 * l16 + e;
+        float s = qa6[e] + qa6[e + 1] + qa6[e + 2];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) s += am6[e + i] == fi ? qm6[e + i] : 0.f;
+        dxv[e] += 2.0f * xv[e] * s;
+      }
+    }
+    const float dot = y0 * dd0 + y1 * dd1 + y2 * dd2;
+    const float dz0 = y0 * (dd0 - dot), dz1 = y1 * (dd1 - dot), dz2 = y2 * (dd2 - dot);
+    const float dcv = dz0 + dz1 + dz2;
+    float mu, sd, mabs;
+    stats64(xv, mu, sd, mabs);
+    const float den = mabs + 1e-6f;
+    const float dsd = dcv / den;
+    const float dmabs = -dcv * sd / (den * den);
+    const float csd = sd > 0.f ? dsd / (63.f * sd) : 0.f;
+    const float cma = dmabs / 64.f;
+    float dh[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float sgn = xv[e] > 0.f ? 1.f : (xv[e] < 0.f ? -1.f : 0.f);
+      dxv[e] += csd * (xv[e] - mu) + cma * sgn;
+      const float hv = hr.v[e];
+      dh[e] = silu_grad(hv) * (dz0 * w2v[0][e] + dz1 * w2v[1][e] + dz2 * w2v[2][e]);
+      const float hs = silu_f(hv);
+      accW[0][e] += dz0 * hs;
+      accW[1][e] += dz1 * hs;
+      accW[2][e] += dz2 * hs;
+    }
+    st64(dx + r * 64 + 4 * l16, dxv);
+    st64(dhpre + r * 64 + 4 * l16, dh);
+    accb[0] += dz0;
+    accb[1] += dz1;
+    accb[2] += dz2;
+  }
+  // reduce the 16 row-groups of the workgroup (4 per wave), then one atomic per element
+  const int grp = wid * 4 + (lane >> 4);
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) wred[grp][k * 64 + 4 * l16 + e] = accW[k][e];
+  if (l16 == 0) {
+    wred[grp][192] = accb[0];
+    wred[grp][193] = accb[1];
+    wred[grp][194] = accb[2];
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < 195; j += 64 * ABBY_WAVES) {
+    float sacc = 0.f;
+    for (int q = 0; q < ABBY_WAVES * 4; ++q) sacc += wred[q][j];
+    atomicAdd(j < 192 ? dW2 + j : db2 + (j - 192), sacc);
   }
 }
 
@@ -380,6 +745,11 @@ extern "C" int asrx_abby_fwd(const float* x, const float* hpre, const float* W2,
   const int E = (int)(d / 64);
   AbbyGeom g = make_geom(rows, d, L, H, sid_base, key, use_noise);
   const unsigned grid = (unsigned)std::min<int64_t>((rows + ABBY_WAVES - 1) / ABBY_WAVES, 4096);
+  if (d == 64) {
+    const unsigned g64 = (unsigned)std::min<int64_t>((rows + 4 * ABBY_WAVES - 1) / (4 * ABBY_WAVES), 4096);
+    abby_fwd64_kernel<<<g64, 64 * ABBY_WAVES, 0, stream>>>(x, hpre, W2, b2, out, ys, idx, g, nullptr);
+    ASRX_LAUNCHED("asrx_abby_fwd");
+  }
   ABBY_DISPATCH(abby_fwd_kernel, x, hpre, W2, b2, out, ys, idx, g, nullptr);
   ASRX_LAUNCHED("asrx_abby_fwd");
 }
@@ -394,6 +764,11 @@ extern "C" int asrx_abby_fwd_logits(const float* x, const float* logits, const f
   const int E = (int)(d / 64);
   AbbyGeom g = make_geom(rows, d, L, H, sid_base, key, use_noise);
   const unsigned grid = (unsigned)std::min<int64_t>((rows + ABBY_WAVES - 1) / ABBY_WAVES, 4096);
+  if (d == 64) {
+    const unsigned g64 = (unsigned)std::min<int64_t>((rows + 4 * ABBY_WAVES - 1) / (4 * ABBY_WAVES), 4096);
+    abby_fwd64_kernel<<<g64, 64 * ABBY_WAVES, 0, stream>>>(x, nullptr, nullptr, b2, out, ys, idx, g, logits);
+    ASRX_LAUNCHED("asrx_abby_fwd_logits");
+  }
   ABBY_DISPATCH(abby_fwd_kernel, x, nullptr, nullptr, b2, out, ys, idx, g, logits);
   ASRX_LAUNCHED("asrx_abby_fwd_logits");
 }
@@ -408,6 +783,11 @@ extern "C" int asrx_abby_bwd(const float* dout, const float* x, const float* hpr
   const int E = (int)(d / 64);
   AbbyGeom g = make_geom(rows, d, 1, 1, 0, 0, 0);
   const unsigned grid = (unsigned)std::min<int64_t>((rows + ABBY_WAVES - 1) / ABBY_WAVES, 1024);
+  if (d == 64) {
+    const unsigned g64 = (unsigned)std::min<int64_t>((rows + 4 * ABBY_WAVES - 1) / (4 * ABBY_WAVES), 1024);
+    abby_bwd64_kernel<<<g64, 64 * ABBY_WAVES, 0, stream>>>(dout, x, hpre, W2, ys, idx, dx, dhpre, dW2, db2, g);
+    ASRX_LAUNCHED("asrx_abby_bwd");
+  }
   ABBY_DISPATCH(abby_bwd_kernel, dout, x, hpre, W2, ys, idx, dx, dhpre, dW2, db2, g);
   ASRX_LAUNCHED("asrx_abby_bwd");
 }

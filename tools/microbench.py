@@ -92,6 +92,33 @@ def rowops_bench():
     print(f"bn bwd: {t*1e6:.1f} us {5*nb/t/1e9:.0f} GB/s", flush=True)
 
 
+def abby_bench():
+    from asrx import lib
+
+    dev = torch.device("cuda:0")
+    P = lib.ptr
+    for rows, d in ((192064, 384), (1152384, 64), (48016, 768)):
+        x = torch.randn(rows, d, device=dev) * 3
+        lg = torch.randn(rows, 3, device=dev)
+        b2 = torch.randn(3, device=dev)
+        out = torch.empty_like(x)
+        ys = torch.empty(rows, 3, device=dev)
+        idx = torch.empty(rows, dtype=torch.int32, device=dev)
+        t = timeit(lambda: lib.call("asrx_abby_fwd_logits", P(x), P(lg), P(b2), P(out), P(ys), P(idx), rows, d, 1, 1,
+                                    0, 7, 1, lib.stream()))
+        print(f"abby fwd rows={rows} d={d}: {t*1e6:.1f} us {2*rows*d*4/t/1e9:.0f} GB/s (x in, out)", flush=True)
+        h = torch.randn(rows, d, device=dev)
+        w2 = torch.randn(3, d, device=dev)
+        g = torch.randn(rows, d, device=dev)
+        dx, dh = torch.empty_like(x), torch.empty_like(x)
+        dW2, db2 = torch.zeros(3, d, device=dev), torch.zeros(3, device=dev)
+        t = timeit(lambda: lib.call("asrx_abby_bwd", P(g), P(x), P(h), P(w2), P(ys), P(idx), P(dx), P(dh), P(dW2),
+                                    P(db2), rows, d, lib.stream()))
+        print(f"abby bwd rows={rows} d={d}: {t*1e6:.1f} us {5*rows*d*4/t/1e9:.0f} GB/s (g,x,h in; dx,dh out)",
+              flush=True)
+        del x, h, g, dx, dh, out
+
+
 def attn_bench():
     from asrx import ops, prec
 
@@ -129,3 +156,5 @@ if __name__ == "__main__":
         rowops_bench()
     if "attn" in what:
         attn_bench()
+    if "abby" in what:
+        abby_bench()
