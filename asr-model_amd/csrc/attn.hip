@@ -412,6 +412,10 @@ namespace asrx {
 int attn_fwd_mf(const float* q, const int64_t* sq, const float* k, const int64_t* sk, const float* v,
                 const int64_t* sv, float* o, const int64_t* so, float* lse, int64_t B, int64_t H, int64_t Lq,
                 int64_t Lk, int causal, float scale, hipStream_t stream);
+int attn_bwd_mf(const float* q, const int64_t* sq, const float* k, const int64_t* sk, const float* v,
+                const int64_t* sv, const float* dO, const int64_t* sd, const float* lse, const float* delta,
+                float* dq, const int64_t* sdq, float* dk, const int64_t* sdk, float* dv, const int64_t* sdv,
+                int64_t B, int64_t H, int64_t Lq, int64_t Lk, int causal, float scale, hipStream_t stream);
 }
 
 extern "C" int asrx_attn_fwd(int prec, const float* q, const int64_t* sq, const float* k, const int64_t* sk,
@@ -454,7 +458,12 @@ extern "C" int asrx_attn_bwd(int prec, const float* q, const int64_t* sq, const 
                                                                                           H, Lq);
   dim3 gk((unsigned)((Lk + ATILE - 1) / ATILE), (unsigned)H, (unsigned)B);
   dim3 gq((unsigned)((Lq + ATILE - 1) / ATILE), (unsigned)H, (unsigned)B);
-  if (prec == PREC_BF16) {
+  const bool al16 = (((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)dO | (uintptr_t)dq | (uintptr_t)dk |
+                       (uintptr_t)dv) & 15) == 0;
+  if (prec == PREC_BF16 && al16 && getenv("ASRX_ATTN_OLD") == nullptr) {
+    attn_bwd_mf(q, sq, k, sk, v, sv, dO, sd, lse, delta_ws, dq, sdq, dk, sdk, dv, sdv, B, H, Lq, Lk, causal, scale,
+                stream);
+  } else if (prec == PREC_BF16) {
     attn_bwd_dkdv_kernel<PREC_BF16><<<gk, 256, 0, stream>>>(q, k, v, dO, lse, delta_ws, dk, dv, Sq, Sk, Sv, Sd, Sdk,
                                                             Sdv, H, Lq, Lk, causal, scale);
     attn_bwd_dq_kernel<PREC_BF16><<<gq, 256, 0, stream>>>(q, k, v, dO, lse, delta_ws, dq, Sq, Sk, Sv, Sd, Sdq, H, Lq,

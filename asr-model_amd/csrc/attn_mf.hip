@@ -232,6 +232,309 @@ __global__ __launch_bounds__(NTHR, 1) void attn_fwd_mf_kernel(const float* __res
   }
 }
 
+// ============================================================================================
+// Backward (perf mode), the same operand tricks as the forward:
+//   Delta_i = rowsum(dO_i * O_i) (attn_delta_kernel), P = exp(S * scale - lse), dS = P (dP - Delta)
+//   dkdv kernel (key-major, lane = key): S = Q K^T and dP = dO V^T with K^T / V^T fragments held in
+//     registers for the wave's 32 keys, Q / dO rows read from LDS; P and dS are MFMA outputs with
+//     the query on the row, so they pack straight into the B operand of dV^T += dO^T P and
+//     dK^T += Q^T dS (dO^T / Q^T by transposed LDS reads) and both accumulators keep the key on
+//     the lane.  Q and dO tiles are staged twice: row-read and transpose-read swizzles.
+//   dq kernel (query-major, lane = query, the forward's layout): S^T = K Q^T, dP^T = V dO^T with
+//     Q^T / dO^T fragments in registers, dS^T packed into the B operand of dQ^T += K^T dS^T.
+// No atomics; every accumulator is written once.
+
+// one 16-byte chunk of a [row][64] bf16 tile, stored under both swizzles (row reads / tr reads)
+__device__ __forceinline__ void stage_store2(unsigned short* tr_rows, unsigned short* tr_t, int row, int c,
+                                             const float4& a, const float4& b) {
+  stage_store(tr_rows, row, c ^ kswz(row), a, b);
+  stage_store(tr_t, row, c ^ vswz(row), a, b);
+}
+
+// A operand of X^T (d rows 32 dd.., k = 16 rows of X in the MFMA-output order of block kb2, half
+// s2) from a transpose-swizzled [row][64] bf16 tile: the forward's V^T read, generalised
+__device__ __forceinline__ bf16x8 tr_frag(const unsigned short* X, int lane, int kb2, int s2, int dd) {
+  const int g = lane >> 4, gi = lane & 15;
+  const int trow = gi >> 2, tcol = 4 * (gi & 3);
+  const int kbase = 32 * kb2 + 16 * s2 + 4 * (g >> 1);
+  const int col = 32 * dd + 16 * (g & 1) + tcol;
+  const int r1 = kbase + trow, r2 = kbase + 8 + trow;
+  const v4i16 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(X + r1 * 64 + 8 * ((col >> 3) ^ vswz(r1)) + (col & 7)));
+  const v4i16 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(X + r2 * 64 + 8 * ((col >> 3) ^ vswz(r2)) + (col & 7)));
+  typedef short v8i16 __attribute__((ext_vector_type(8)));
+  const v8i16 a8 = {t1[0], t1[1], t1[2], t1[3], t2[0], t2[1], t2[2], t2[3]};
+  return __builtin_bit_cast(bf16x8, a8);
+}
+
+// register fragment (B operand of a d-contraction): row `row` of X, d = 16 s + 8 hi .. +7, as bf16
+__device__ __forceinline__ void row_frags(const float* base, int64_t stride_l, int64_t row, int64_t rows, int hi,
+                                          bf16x8 (&f)[4]) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    float t[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (row < rows) {
+      const float* p = base + row * stride_l + 16 * s + 8 * hi;
+      const float4 x = *reinterpret_cast<const float4*>(p), y = *reinterpret_cast<const float4*>(p + 4);
+      t[0] = x.x; t[1] = x.y; t[2] = x.z; t[3] = x.w; t[4] = y.x; t[5] = y.y; t[6] = y.z; t[7] = y.w;
+    }
+    f[s] = pack8(t);
+  }
+}
+
+constexpr int BQT = 64;   // queries per tile of the dkdv loop
+constexpr int BKB = 256;  // keys per dkdv workgroup (8 waves x 32)
+
+__global__ __launch_bounds__(NTHR, 1) void attn_bwd_dkdv_mf_kernel(
+    const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v,
+    const float* __restrict__ dO, const float* __restrict__ lse, const float* __restrict__ delta,
+    float* __restrict__ dk, float* __restrict__ dv, AttnStridesMF sq, AttnStridesMF sk, AttnStridesMF sv,
+    AttnStridesMF sd, AttnStridesMF sdk, AttnStridesMF sdv, int64_t H, int64_t Lq, int64_t Lk, int causal,
+    float scale) {
+  __shared__ __attribute__((aligned(16))) unsigned short Qr[2][BQT * 64], Qt[2][BQT * 64];
+  __shared__ __attribute__((aligned(16))) unsigned short Dr[2][BQT * 64], Dt[2][BQT * 64];
+  __shared__ __attribute__((aligned(16))) float2 LD[2][BQT];  // (lse * log2e or +inf past Lq, Delta)
+
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int64_t k0 = (int64_t)blockIdx.x * BKB;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int j = lane & 31, hi = lane >> 5;
+  const int64_t key = k0 + wid * 32 + j;  // this lane's key
+  const float* qb = q + b * sq.b + h * sq.h;
+  const float* kbp = k + b * sk.b + h * sk.h;
+  const float* vbp = v + b * sv.b + h * sv.h;
+  const float* gb = dO + b * sd.b + h * sd.h;
+  const float* lb = lse + ((int64_t)b * H + h) * Lq;
+  const float* db = delta + ((int64_t)b * H + h) * Lq;
+  const float c = scale * LOG2E;
+
+  bf16x8 kf[4], vf[4];
+  row_frags(kbp, sk.l, key, Lk, hi, kf);
+  row_frags(vbp, sv.l, key, Lk, hi, vf);
+
+  const int64_t qt0 = causal ? k0 / BQT : 0;  // causal: tiles entirely before the block's keys are masked
+  const int ntiles = (int)((Lq + BQT - 1) / BQT - qt0);
+  const int srow = tid >> 3, sc = tid & 7;
+  auto stage_ld = [&](int t, float4& qa, float4& qb4, float4& ga, float4& gb4, float2& ld) {
+    const int64_t q0 = (qt0 + t) * BQT;
+    stage_load(qb, sq, q0 + srow, Lq, sc, qa, qb4);
+    stage_load(gb, sd, q0 + srow, Lq, sc, ga, gb4);
+    if (tid < BQT) {
+      const int64_t qi = q0 + tid;
+      ld = qi < Lq ? make_float2(lb[qi] * LOG2E, db[qi]) : make_float2(INFINITY, 0.f);
+    }
+  };
+  auto stage_st = [&](int buf, const float4& qa, const float4& qb4, const float4& ga, const float4& gb4,
+                      const float2& ld) {
+    stage_store2(Qr[buf], Qt[buf], srow, sc, qa, qb4);
+    stage_store2(Dr[buf], Dt[buf], srow, sc, ga, gb4);
+    if (tid < BQT) LD[buf][tid] = ld;
+  };
+
+  f32x16 dvacc[2], dkacc[2];
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      dvacc[d][r] = 0.f;
+      dkacc[d][r] = 0.f;
+    }
+  float4 qa, qb4, ga, gb4;
+  float2 ld = make_float2(0.f, 0.f);
+  if (ntiles > 0) {
+    stage_ld(0, qa, qb4, ga, gb4, ld);
+    stage_st(0, qa, qb4, ga, gb4, ld);
+  }
+  __syncthreads();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    const int64_t q0 = (qt0 + t) * BQT;
+    if (t + 1 < ntiles) stage_ld(t + 1, qa, qb4, ga, gb4, ld);
+    const unsigned short* Qrt = Qr[buf];
+    const unsigned short* Drt = Dr[buf];
+    const unsigned short* Dtt = Dt[buf];
+    const unsigned short* Qtt = Qt[buf];
+    const bool need_mask = causal && q0 < k0 + wid * 32 + 32;
+    // one 32-query half at a time (keeps S / dP / P / dS of a single half live)
+#pragma unroll
+    for (int qb2 = 0; qb2 < 2; ++qb2) {
+      // ---- S = Q K^T, dP = dO V^T (rows = queries, lane = key)
+      f32x16 sacc, pacc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        sacc[r] = 0.f;
+        pacc[r] = 0.f;
+      }
+      const int qr = 32 * qb2 + j;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(Qrt + qr * 64 + 8 * ((2 * s + hi) ^ kswz(qr)));
+        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, kf[s], sacc, 0, 0, 0);
+        const bf16x8 g = *reinterpret_cast<const bf16x8*>(Drt + qr * 64 + 8 * ((2 * s + hi) ^ kswz(qr)));
+        pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(g, vf[s], pacc, 0, 0, 0);
+      }
+      // ---- P, dS (query row of register r: 32 qb2 + (r & 3) + 8 (r >> 2) + 4 hi)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        float pv[8], dsv[8];
+#pragma unroll
+        for (int e4 = 0; e4 < 2; ++e4) {
+          const int ql = 32 * qb2 + 8 * (2 * s2 + e4) + 4 * hi;  // 4 consecutive queries
+          const float4 lo = *reinterpret_cast<const float4*>(&LD[buf][ql]);
+          const float4 hi4 = *reinterpret_cast<const float4*>(&LD[buf][ql + 2]);
+          const float l2v[4] = {lo.x, lo.z, hi4.x, hi4.z}, dlv[4] = {lo.y, lo.w, hi4.y, hi4.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 8 * s2 + 4 * e4 + e;
+            float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[r], c, -l2v[e]));
+            if (need_mask && key > q0 + ql + e) p = 0.f;
+            pv[4 * e4 + e] = p;
+            dsv[4 * e4 + e] = p * (pacc[r] - dlv[e]);
+          }
+        }
+        const bf16x8 pb = pack8(pv), sb = pack8(dsv);
+        // ---- dV^T += dO^T P, dK^T += Q^T dS  (lane = key)
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          dvacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Dtt, lane, qb2, s2, d), pb, dvacc[d], 0, 0, 0);
+          dkacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Qtt, lane, qb2, s2, d), sb, dkacc[d], 0, 0, 0);
+        }
+      }
+    }
+    if (t + 1 < ntiles) stage_st(buf ^ 1, qa, qb4, ga, gb4, ld);
+    __syncthreads();
+  }
+
+  if (key < Lk) {
+    float* dkr = dk + b * sdk.b + h * sdk.h + key * sdk.l;
+    float* dvr = dv + b * sdv.b + h * sdv.h + key * sdv.l;
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int dd = 32 * d + 8 * g4 + 4 * hi;
+        *reinterpret_cast<float4*>(dkr + dd) = make_float4(dkacc[d][4 * g4] * scale, dkacc[d][4 * g4 + 1] * scale,
+                                                           dkacc[d][4 * g4 + 2] * scale, dkacc[d][4 * g4 + 3] * scale);
+        *reinterpret_cast<float4*>(dvr + dd) =
+            make_float4(dvacc[d][4 * g4], dvacc[d][4 * g4 + 1], dvacc[d][4 * g4 + 2], dvacc[d][4 * g4 + 3]);
+      }
+  }
+}
+
+__global__ __launch_bounds__(NTHR, 1) void attn_bwd_dq_mf_kernel(
+    const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v,
+    const float* __restrict__ dO, const float* __restrict__ lse, const float* __restrict__ delta,
+    float* __restrict__ dq, AttnStridesMF sq, AttnStridesMF sk, AttnStridesMF sv, AttnStridesMF sd,
+    AttnStridesMF sdq, int64_t H, int64_t Lq, int64_t Lk, int causal, float scale) {
+  __shared__ __attribute__((aligned(16))) unsigned short Kr[2][KT * 64], Kt2[2][KT * 64], Vr[2][KT * 64];
+
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int64_t q0 = (int64_t)blockIdx.x * QB;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int j = lane & 31, hi = lane >> 5;
+  const int64_t qi = q0 + wid * 32 + j;  // this lane's query row
+  const float* kbp = k + b * sk.b + h * sk.h;
+  const float* vbp = v + b * sv.b + h * sv.h;
+  const float c = scale * LOG2E;
+
+  bf16x8 qf[4], gf[4];
+  row_frags(q + b * sq.b + h * sq.h, sq.l, qi, Lq, hi, qf);
+  row_frags(dO + b * sd.b + h * sd.h, sd.l, qi, Lq, hi, gf);
+  const float l2 = qi < Lq ? lse[((int64_t)b * H + h) * Lq + qi] * LOG2E : 0.f;
+  const float dl = qi < Lq ? delta[((int64_t)b * H + h) * Lq + qi] : 0.f;
+
+  int64_t kend = Lk;
+  if (causal) kend = min(Lk, q0 + QB);
+  const int ntiles = (int)((kend + KT - 1) / KT);
+  const int skey = tid >> 3, sc = tid & 7;
+
+  float4 ka, kb4, va, vb4;
+  stage_load(kbp, sk, skey, Lk, sc, ka, kb4);
+  stage_load(vbp, sv, skey, Lk, sc, va, vb4);
+  stage_store2(Kr[0], Kt2[0], skey, sc, ka, kb4);
+  stage_store(Vr[0], skey, sc ^ kswz(skey), va, vb4);
+  __syncthreads();
+
+  f32x16 dqacc[2];
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dqacc[d][r] = 0.f;
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    const int64_t k0 = (int64_t)t * KT;
+    if (t + 1 < ntiles) {
+      stage_load(kbp, sk, k0 + KT + skey, Lk, sc, ka, kb4);
+      stage_load(vbp, sv, k0 + KT + skey, Lk, sc, va, vb4);
+    }
+    const unsigned short* Krt = Kr[buf];
+    const unsigned short* Vrt = Vr[buf];
+    f32x16 sacc[2], pacc[2];
+#pragma unroll
+    for (int kb2 = 0; kb2 < 2; ++kb2) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        sacc[kb2][r] = 0.f;
+        pacc[kb2][r] = 0.f;
+      }
+      const int kr = 32 * kb2 + j;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(Krt + kr * 64 + 8 * ((2 * s + hi) ^ kswz(kr)));
+        sacc[kb2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s], sacc[kb2], 0, 0, 0);
+        const bf16x8 vv = *reinterpret_cast<const bf16x8*>(Vrt + kr * 64 + 8 * ((2 * s + hi) ^ kswz(kr)));
+        pacc[kb2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vv, gf[s], pacc[kb2], 0, 0, 0);
+      }
+    }
+    const bool need_mask = (k0 + KT > Lk) || (causal && k0 + KT - 1 > q0 + wid * 32);
+    bf16x8 sb[2][2];
+#pragma unroll
+    for (int kb2 = 0; kb2 < 2; ++kb2)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        float dsv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int r = 8 * s2 + e;
+          float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[kb2][r], c, -l2));
+          if (need_mask) {
+            const int64_t kk = k0 + 32 * kb2 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+            if (kk >= Lk || (causal && kk > qi)) p = 0.f;
+          }
+          dsv[e] = p * (pacc[kb2][r] - dl);
+        }
+        sb[kb2][s2] = pack8(dsv);
+      }
+    const unsigned short* Ktt = Kt2[buf];
+#pragma unroll
+    for (int kb2 = 0; kb2 < 2; ++kb2)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int d = 0; d < 2; ++d)
+          dqacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Ktt, lane, kb2, s2, d), sb[kb2][s2], dqacc[d],
+                                                             0, 0, 0);
+    if (t + 1 < ntiles) {
+      stage_store2(Kr[buf ^ 1], Kt2[buf ^ 1], skey, sc, ka, kb4);
+      stage_store(Vr[buf ^ 1], skey, sc ^ kswz(skey), va, vb4);
+    }
+    __syncthreads();
+  }
+
+  if (qi < Lq) {
+    float* dqr = dq + b * sdq.b + h * sdq.h + qi * sdq.l;
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int dd = 32 * d + 8 * g4 + 4 * hi;
+        *reinterpret_cast<float4*>(dqr + dd) = make_float4(dqacc[d][4 * g4] * scale, dqacc[d][4 * g4 + 1] * scale,
+                                                           dqacc[d][4 * g4 + 2] * scale, dqacc[d][4 * g4 + 3] * scale);
+      }
+  }
+}
+
 }  // namespace amf
 
 // bf16 flash-attention forward (see header); called by asrx_attn_fwd for prec == PREC_BF16.
@@ -241,6 +544,22 @@ int attn_fwd_mf(const float* q, const int64_t* sq, const float* k, const int64_t
   dim3 g((unsigned)((Lq + amf::QB - 1) / amf::QB), (unsigned)H, (unsigned)B);
   AttnStridesMF Sq{sq[0], sq[1], sq[2]}, Sk{sk[0], sk[1], sk[2]}, Sv{sv[0], sv[1], sv[2]}, So{so[0], so[1], so[2]};
   amf::attn_fwd_mf_kernel<<<g, amf::NTHR, 0, stream>>>(q, k, v, o, lse, Sq, Sk, Sv, So, H, Lq, Lk, causal, scale);
+  return 0;
+}
+
+// bf16 flash-attention backward (dkdv + dq kernels above); delta = rowsum(dO * O) already computed.
+int attn_bwd_mf(const float* q, const int64_t* sq, const float* k, const int64_t* sk, const float* v,
+                const int64_t* sv, const float* dO, const int64_t* sd, const float* lse, const float* delta,
+                float* dq, const int64_t* sdq, float* dk, const int64_t* sdk, float* dv, const int64_t* sdv,
+                int64_t B, int64_t H, int64_t Lq, int64_t Lk, int causal, float scale, hipStream_t stream) {
+  AttnStridesMF Sq{sq[0], sq[1], sq[2]}, Sk{sk[0], sk[1], sk[2]}, Sv{sv[0], sv[1], sv[2]}, Sd{sd[0], sd[1], sd[2]};
+  AttnStridesMF Sdq{sdq[0], sdq[1], sdq[2]}, Sdk{sdk[0], sdk[1], sdk[2]}, Sdv{sdv[0], sdv[1], sdv[2]};
+  dim3 gk((unsigned)((Lk + amf::BKB - 1) / amf::BKB), (unsigned)H, (unsigned)B);
+  amf::attn_bwd_dkdv_mf_kernel<<<gk, amf::NTHR, 0, stream>>>(q, k, v, dO, lse, delta, dk, dv, Sq, Sk, Sv, Sd, Sdk, Sdv,
+                                                            H, Lq, Lk, causal, scale);
+  dim3 gq((unsigned)((Lq + amf::QB - 1) / amf::QB), (unsigned)H, (unsigned)B);
+  amf::attn_bwd_dq_mf_kernel<<<gq, amf::NTHR, 0, stream>>>(q, k, v, dO, lse, delta, dq, Sq, Sk, Sv, Sd, Sdq, H, Lq, Lk,
+                                                          causal, scale);
   return 0;
 }
 

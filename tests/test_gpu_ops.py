@@ -144,6 +144,37 @@ def test_attention_bf16(cuda, B, H, Lq, Lk, causal):
     assert float((lse.cpu().double() - ref_lse).abs().max()) < 1e-3
 
 
+@pytest.mark.parametrize("B,H,Lq,Lk,causal", [(1, 2, 300, 300, False), (2, 3, 600, 517, False),
+                                                (1, 2, 256, 256, True), (2, 1, 70, 70, True), (1, 2, 33, 3001, False),
+                                                (1, 1, 513, 64, False), (1, 2, 700, 700, True)])
+def test_attention_bf16_backward(cuda, B, H, Lq, Lk, causal):
+    """Perf-mode flash-attention backward (dkdv kernel with the key on the lane, dq kernel with the
+    query on the lane, 32x32x16 bf16 MFMA) against float64 autograd of softmax attention on the
+    same bf16-rounded q, k, v, dO.  P and dS are rounded to bf16 before their products, so the
+    tolerance is the bf16 one (3e-2 of max |grad|)."""
+    from asrx import ops, prec
+
+    hd = 64
+    g = torch.Generator().manual_seed(Lq * 5 + Lk + causal)
+    q, k, v = (torch.randn(B, L, H, hd, generator=g) for L in (Lq, Lk, Lk))
+    dO = torch.randn(B, Lq, H, hd, generator=g)
+    rnd = lambda t: t.to(torch.bfloat16).float()  # noqa: E731
+    q, k, v, dO = rnd(q), rnd(k), rnd(v), rnd(dO)
+    qg, kg, vg = (t.to(cuda).requires_grad_(True) for t in (q, k, v))
+    with prec.precision("bf16"):
+        o = ops.attention(qg, kg, vg, causal)
+        o.backward(dO.to(cuda))
+    qr, kr, vr = (t.double().requires_grad_(True) for t in (q, k, v))
+    s = (qr.transpose(1, 2) @ kr.transpose(1, 2).transpose(-1, -2)) / math.sqrt(hd)
+    if causal:
+        s = s.masked_fill(torch.ones(Lq, Lk, dtype=torch.bool).triu(1), float("-inf"))
+    ref = (torch.softmax(s, -1) @ vr.transpose(1, 2)).transpose(1, 2)
+    ref.backward(dO.double())
+    assert _rel(o.detach(), ref.detach()) < 1e-2
+    for a, b in ((qg.grad, qr.grad), (kg.grad, kr.grad), (vg.grad, vr.grad)):
+        assert _rel(a, b) < 3e-2, _rel(a, b)
+
+
 @pytest.mark.parametrize("masked", [False, True])
 def test_rotary(cuda, masked):
     from asrx import ops

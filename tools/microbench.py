@@ -137,12 +137,18 @@ def attn_bench():
                 t = timeit(lambda: ops.attention(q, k, v, causal), iters=5)
                 print(f"attn fwd {'old' if old else 'mf '} B={B} H={H} Lq={Lq} Lk={Lk} causal={causal}: "
                       f"{t*1e6:.1f} us {fl/t/1e12:.1f} TF/s", flush=True)
+            for old in (False, True):
+                if old:
+                    os.environ["ASRX_ATTN_OLD"] = "1"
+                else:
+                    os.environ.pop("ASRX_ATTN_OLD", None)
+                qr, kr, vr = (t_.clone().requires_grad_(True) for t_ in (q, k, v))
+                y = ops.attention(qr, kr, vr, causal)
+                gy = torch.randn_like(y)
+                t = timeit(lambda: torch.autograd.grad(y, (qr, kr, vr), gy, retain_graph=True), iters=3)
+                print(f"attn bwd {'old' if old else 'mf '} B={B} Lq={Lq} Lk={Lk}: {t*1e6:.1f} us "
+                      f"{2.5*fl/t/1e12:.1f} TF/s", flush=True)
             os.environ.pop("ASRX_ATTN_OLD", None)
-            qr, kr, vr = (t_.clone().requires_grad_(True) for t_ in (q, k, v))
-            y = ops.attention(qr, kr, vr, causal)
-            gy = torch.randn_like(y)
-            t = timeit(lambda: torch.autograd.grad(y, (qr, kr, vr), gy, retain_graph=True), iters=3)
-            print(f"attn bwd B={B} Lq={Lq} Lk={Lk}: {t*1e6:.1f} us {2.5*fl/t/1e12:.1f} TF/s", flush=True)
         del q, k, v
 
 
