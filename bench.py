@@ -40,6 +40,7 @@ def parse():
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true", help="skip the live per-kernel event probe")
+    ap.add_argument("--no-optimizer", action="store_true", help="skip timing the fused MaxFactor step")
     ap.add_argument("--dist-backend", default="nccl", help="process-group backend for N > 1 (nccl = RCCL); "
                     "gloo + --same-device is a one-GPU rehearsal of the multi-rank path")
     ap.add_argument("--same-device", action="store_true", help="every rank on cuda:0 (rehearsal only)")
@@ -173,6 +174,23 @@ def main():
         probe_steps = 1
     else:
         recs = None
+    opt_ms = None
+    if not args.no_optimizer:
+        # the reference's MaxFactor step (model.py:772-787 groups and
+        # hyper-parameters) as one fused native call over every parameter with a gradient; timed
+        # after the measured steps, not part of `value` (the metric is fwd + bwd)
+        from asrx.optim import MaxFactor, reference_param_groups
+        opt = MaxFactor(reference_param_groups(model), lr=2.5e-3, b_decay=-0.8, eps=(1e-8, 1e-8), d=1.0,
+                        decay=1e-2, gamma=0.99, max=False, bias=1, min_lr=1e-9, clip=False, cap=0.0)
+        opt.step()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(5):
+            opt.step()
+        e1.record()
+        torch.cuda.synchronize()
+        opt_ms = e0.elapsed_time(e1) / 5
     if world > 1:
         # replicas must hold identical averaged gradients after the all-reduce
         gsum = torch.stack([p.grad.double().norm() for p in model.parameters() if p.grad is not None]).sum()
@@ -259,6 +277,8 @@ def main():
             result["attn_fwd"] = {"achieved": round(af / sec3 / 1e12, 2), "unit": "TFLOP/s",
                                   "frac": round(af / sec3 / 1e12 / peak, 4),
                                   "share_of_step": round(sec3 / probe_steps / step_s, 3)}
+    if opt_ms is not None:
+        result["maxfactor_step_ms"] = round(opt_ms, 3)
     result["launch"] = "hip-graph replay" if graph is not None else "eager"
     if recs is not None:
         result["probe"] = "per-kernel HIP events on one eager pass of the same step after the timed steps"

@@ -28,10 +28,11 @@ uint32_t asrx_noise_hash(uint32_t key, uint32_t idx);
 /* ---- log-mel front end: replaces torchaudio MelSpectrogram + log10 + clip-max floor,
  *      essentials.py:469-491, and the waveform adaptive_avg_pool1d, essentials.py:493-510 -------- */
 int asrx_mel_frames(int64_t n_samples); /* 1 + N/160 (host) */
-/* wav (B,N) at row stride ld_wav; consts = window|tw512|tw1024 (see asrx/mel.py); fbw (128,32)
- * band weights and fbs[128] int32 start bins of the sparse HTK filterbank; out (B,F,128) when
- * layout==0 or (B,128,F) when layout==1, clip stride ld_out; clip_max_ws int32[B] workspace;
- * pool (B,T_pool) or NULL (needs N == 160*T_pool). */
+/* wav (B,N) at row stride ld_wav; consts = window|tw512|tw1024 (see asrx/mel.py); fbw/fbs the
+ * lane-packed HTK filterbank of asrx/mel.py lane_filterbank (fbs int32[256] = band_a | band_b |
+ * even start bins a | b, fbw float[8][64][4] = weights/4); out (B,F,128) when layout==0 or
+ * (B,128,F) when layout==1, clip stride ld_out; clip_max_ws int32[B] workspace; pool (B,T_pool)
+ * or NULL (needs N == 160*T_pool). */
 int asrx_logmel(const float* wav, int64_t B, int64_t N, int64_t ld_wav, const float* consts,
                 const float* fbw, const int* fbs, float* out, int layout, int64_t ld_out,
                 int* clip_max_ws, float* pool, int64_t T_pool, asrx_stream_t stream);
@@ -211,6 +212,16 @@ int asrx_ce_fwd(const float* z, const int64_t* labels, float* loss, float* lse, 
                 asrx_stream_t stream);
 int asrx_ce_bwd(const float* z, const int64_t* labels, const float* lse, const float* scale, float* dz,
                 int64_t rows, int64_t V, asrx_stream_t stream);
+
+/* ---- MaxFactor optimizer step: replaces MaxFactor.step, optimizerc.py:6-147 (the optimizer
+ *      model.py:783-787 builds), for every parameter of the model in one call.  table: device array
+ *      of np parameter records (layout and packing: asrx/optim.py; record size from
+ *      asrx_maxfactor_param_bytes()); nrows / ncols / ncc / nmats: sizes of the flat row, (mat,
+ *      col), (mat, col, 256-row chunk) and mat spaces; ws: float workspace of 4 np + 4 nrows +
+ *      ncols + nmats.  Updates parameters and optimizer state in place. ----------------------------- */
+int asrx_maxfactor_param_bytes(void);
+int asrx_maxfactor_step(const void* table, int np, int64_t nrows, int64_t ncols, int64_t ncc, int64_t nmats,
+                        float* ws, asrx_stream_t stream);
 
 #ifdef __cplusplus
 }
