@@ -231,7 +231,7 @@ def main():
         peak = BF16_PEAK_TFS if args.precision == "bf16" else F32_PEAK_TFS
         achieved = flops / sec / 1e12 if sec > 0 else 0.0
         step_s = elapsed / args.steps
-        # dominant kernel: the wide bf16-weight GEMM (asrx_gemm_wn, every activation x weight product
+        # dominant kernel: the wide bf16-weight GEMM (asrx_gemm_wn -> gemm_wr_kernel, every activation x weight product
         # of the forward and of the input gradients; the top kernel of the rocprof summary).  With
         # fp32 activations at K, N <= 1536 its arithmetic intensity (<= ~190 flop/B) is below the
         # MI355X ridge point (2500 TF/s / 8 TB/s = 312 flop/B), so its roofline is HBM bandwidth:
@@ -249,7 +249,7 @@ def main():
             wn_sec += sc
         if wn_sec > 0:
             gbs = wn_bytes / wn_sec / 1e9
-            result["roofline"] = {"kernel": "asrx::wn::gemm_wn_kernel (wide bf16-weight MFMA GEMM, fp32 activations)",
+            result["roofline"] = {"kernel": "asrx::wn::gemm_wr_kernel (wide bf16-weight MFMA GEMM, fp32 activations)",
                                   "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                   "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
                                   "algorithmic_bytes_per_launch": round(wn_bytes / wn_n),
