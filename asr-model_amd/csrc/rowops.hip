@@ -36,6 +36,119 @@ __device__ __forceinline__ void flush_partials(float* part, int n, float* dst) {
 // ============================================================================ LayerNorm
 // nn.LayerNorm over the last dim (MSheath layers[i].ln / mlp_ln, model.py:405, 427) and
 // essentials.LayerNorm over channels (essentials.py:110-113) on channels-last activations.
+// Register-resident variants for d = 64 E (E even): a lane owns E consecutive features (float2
+// I/O), the row is read once, statistics by DPP wave sums, the next row is prefetched; the backward
+// keeps its dw / db partials in registers.  The generic kernels below remain for other d.
+template <int E>
+__device__ __forceinline__ void ld_lane(const float* __restrict__ src, int lane, float (&v)[E]) {
+  const float2* s2 = reinterpret_cast<const float2*>(src + lane * E);
+#pragma unroll
+  for (int e = 0; e < E / 2; ++e) {
+    const float2 t = s2[e];
+    v[2 * e] = t.x;
+    v[2 * e + 1] = t.y;
+  }
+}
+template <int E>
+__device__ __forceinline__ void st_lane(float* __restrict__ dst, int lane, const float (&v)[E]) {
+  float2* d2 = reinterpret_cast<float2*>(dst + lane * E);
+#pragma unroll
+  for (int e = 0; e < E / 2; ++e) d2[e] = make_float2(v[2 * e], v[2 * e + 1]);
+}
+
+template <int E>
+__global__ __launch_bounds__(64 * RW) void ln_fwd_t_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                           const float* __restrict__ b, float* __restrict__ y,
+                                                           float* __restrict__ mean, float* __restrict__ rstd,
+                                                           int64_t rows, float eps) {
+  constexpr int D = 64 * E;
+  const int lane = threadIdx.x & 63;
+  float wv[E], bv[E], xn[E];
+  ld_lane<E>(w, lane, wv);
+  ld_lane<E>(b, lane, bv);
+  int64_t r = row_begin();
+  if (r < rows) ld_lane<E>(x + r * D, lane, xn);
+  for (; r < rows; r += row_step()) {
+    float xv[E];
+    float s = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      xv[e] = xn[e];
+      s += xv[e];
+    }
+    if (r + row_step() < rows) ld_lane<E>(x + (r + row_step()) * D, lane, xn);
+    const float mu = wave_sum_dpp(s) * (1.0f / D);
+    float v = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const float t = xv[e] - mu;
+      v += t * t;
+    }
+    const float rs = rsqrtf(wave_sum_dpp(v) * (1.0f / D) + eps);
+    float yv[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) yv[e] = (xv[e] - mu) * rs * wv[e] + bv[e];
+    st_lane<E>(y + r * D, lane, yv);
+    if (lane == 0) {
+      mean[r] = mu;
+      rstd[r] = rs;
+    }
+  }
+}
+
+template <int E>
+__global__ __launch_bounds__(64 * RW) void ln_bwd_t_kernel(const float* __restrict__ dy, const float* __restrict__ x,
+                                                           const float* __restrict__ w, const float* __restrict__ mean,
+                                                           const float* __restrict__ rstd, float* __restrict__ dx,
+                                                           float* __restrict__ dw, float* __restrict__ db,
+                                                           int64_t rows) {
+  constexpr int D = 64 * E;
+  __shared__ float part[RW][2 * D];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float wv[E], aw[E], ab[E];
+  ld_lane<E>(w, lane, wv);
+#pragma unroll
+  for (int e = 0; e < E; ++e) aw[e] = ab[e] = 0.f;
+  for (int64_t r = row_begin(); r < rows; r += row_step()) {
+    float xv[E], gv[E];
+    ld_lane<E>(x + r * D, lane, xv);
+    ld_lane<E>(dy + r * D, lane, gv);
+    const float mu = mean[r], rs = rstd[r];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      xv[e] = (xv[e] - mu) * rs;  // x-hat
+      const float g = gv[e] * wv[e];
+      s1 += g;
+      s2 += g * xv[e];
+      aw[e] += gv[e] * xv[e];
+      ab[e] += gv[e];
+    }
+    s1 = wave_sum_dpp(s1) * (1.0f / D);
+    s2 = wave_sum_dpp(s2) * (1.0f / D);
+    float dv[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) dv[e] = rs * (gv[e] * wv[e] - s1 - xv[e] * s2);
+    st_lane<E>(dx + r * D, lane, dv);
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    part[wid][lane * E + e] = aw[e];
+    part[wid][D + lane * E + e] = ab[e];
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < D; j += 64 * RW) {
+    float a = 0.f, c = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < RW; ++ww) {
+      a += part[ww][j];
+      c += part[ww][D + j];
+    }
+    atomicAdd(dw + j, a);
+    atomicAdd(db + j, c);
+  }
+}
+
 __global__ __launch_bounds__(64 * RW) void ln_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                          const float* __restrict__ b, float* __restrict__ y,
                                                          float* __restrict__ mean, float* __restrict__ rstd,
@@ -528,9 +641,17 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ x
   const int part = threadIdx.x >> 6;
   const int64_t r0 = (int64_t)blockIdx.y * chunk;
   const int64_t r1 = min(rows, r0 + chunk);
-  float s = 0.f;
-  if (c < d)
-    for (int64_t r = r0 + part; r < r1; r += 4) s += x[r * d + c];
+  float s = 0.f, s2 = 0.f;
+  if (c < d) {  // two independent chains, unrolled: keeps ~16 row loads in flight per wave
+    int64_t r = r0 + part;
+#pragma unroll 4
+    for (; r + 4 < r1; r += 8) {
+      s += x[r * d + c];
+      s2 += x[(r + 4) * d + c];
+    }
+    if (r < r1) s += x[r * d + c];
+  }
+  s += s2;
   red[part][threadIdx.x & 63] = s;
   __syncthreads();
   if (part == 0 && c < d) {
@@ -1203,7 +1324,16 @@ extern "C" {
 int asrx_layernorm_fwd(const float* x, const float* w, const float* b, float* y, float* mean, float* rstd,
                        int64_t rows, int64_t d, float eps, hipStream_t stream) {
   if (rows == 0) return 0;
-  LAUNCH_ROWS(ln_fwd_kernel, rows, 0, x, w, b, y, mean, rstd, rows, (int)d, eps);
+  const bool al = ((((uintptr_t)x | (uintptr_t)w | (uintptr_t)b | (uintptr_t)y) & 7) == 0);
+  switch (al ? d : 0) {
+    case 128: LAUNCH_ROWS(ln_fwd_t_kernel<2>, rows, 0, x, w, b, y, mean, rstd, rows, eps); break;
+    case 256: LAUNCH_ROWS(ln_fwd_t_kernel<4>, rows, 0, x, w, b, y, mean, rstd, rows, eps); break;
+    case 384: LAUNCH_ROWS(ln_fwd_t_kernel<6>, rows, 0, x, w, b, y, mean, rstd, rows, eps); break;
+    case 512: LAUNCH_ROWS(ln_fwd_t_kernel<8>, rows, 0, x, w, b, y, mean, rstd, rows, eps); break;
+    case 768: LAUNCH_ROWS(ln_fwd_t_kernel<12>, rows, 0, x, w, b, y, mean, rstd, rows, eps); break;
+    case 1024: LAUNCH_ROWS(ln_fwd_t_kernel<16>, rows, 0, x, w, b, y, mean, rstd, rows, eps); break;
+    default: LAUNCH_ROWS(ln_fwd_kernel, rows, 0, x, w, b, y, mean, rstd, rows, (int)d, eps);
+  }
   ASRX_LAUNCHED("asrx_layernorm_fwd");
 }
 
@@ -1211,8 +1341,20 @@ int asrx_layernorm_bwd(const float* dy, const float* x, const float* w, const fl
                        float* dx, float* dw, float* db, int64_t rows, int64_t d, hipStream_t stream) {
   ASRX_REQUIRE(d <= 2048, "layernorm_bwd: d too large");
   if (rows == 0) return 0;
-  const size_t shm = (size_t)RW * 2 * d * sizeof(float);
-  ln_bwd_kernel<<<row_grid(rows, 1024), 64 * RW, shm, stream>>>(dy, x, w, mean, rstd, dx, dw, db, rows, (int)d);
+  const bool al = ((((uintptr_t)dy | (uintptr_t)x | (uintptr_t)w | (uintptr_t)dx) & 7) == 0);
+  const unsigned g = row_grid(rows, 1024);
+  switch (al ? d : 0) {
+    case 128: ln_bwd_t_kernel<2><<<g, 64 * RW, 0, stream>>>(dy, x, w, mean, rstd, dx, dw, db, rows); break;
+    case 256: ln_bwd_t_kernel<4><<<g, 64 * RW, 0, stream>>>(dy, x, w, mean, rstd, dx, dw, db, rows); break;
+    case 384: ln_bwd_t_kernel<6><<<g, 64 * RW, 0, stream>>>(dy, x, w, mean, rstd, dx, dw, db, rows); break;
+    case 512: ln_bwd_t_kernel<8><<<g, 64 * RW, 0, stream>>>(dy, x, w, mean, rstd, dx, dw, db, rows); break;
+    case 768: ln_bwd_t_kernel<12><<<g, 64 * RW, 0, stream>>>(dy, x, w, mean, rstd, dx, dw, db, rows); break;
+    case 1024: ln_bwd_t_kernel<16><<<g, 64 * RW, 0, stream>>>(dy, x, w, mean, rstd, dx, dw, db, rows); break;
+    default: {
+      const size_t shm = (size_t)RW * 2 * d * sizeof(float);
+      ln_bwd_kernel<<<g, 64 * RW, shm, stream>>>(dy, x, w, mean, rstd, dx, dw, db, rows, (int)d);
+    }
+  }
   ASRX_LAUNCHED("asrx_layernorm_bwd");
 }
 

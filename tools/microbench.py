@@ -92,6 +92,30 @@ def rowops_bench():
     print(f"bn bwd: {t*1e6:.1f} us {5*nb/t/1e9:.0f} GB/s", flush=True)
 
 
+def norm_bench():
+    from asrx import lib
+
+    dev = torch.device("cuda:0")
+    P = lib.ptr
+    for rows, d in ((192064, 384), (8192, 384), (48016, 768)):
+        x = torch.randn(rows, d, device=dev)
+        w, b = torch.randn(d, device=dev), torch.randn(d, device=dev)
+        y = torch.empty_like(x)
+        mean, rstd = torch.empty(rows, device=dev), torch.empty(rows, device=dev)
+        t = timeit(lambda: lib.call("asrx_layernorm_fwd", P(x), P(w), P(b), P(y), P(mean), P(rstd), rows, d, 1e-5,
+                                    lib.stream()))
+        print(f"ln fwd rows={rows} d={d}: {t*1e6:.1f} us {2*rows*d*4/t/1e9:.0f} GB/s", flush=True)
+        g = torch.randn_like(x)
+        dx = torch.empty_like(x)
+        dw, db = torch.zeros(d, device=dev), torch.zeros(d, device=dev)
+        t = timeit(lambda: lib.call("asrx_layernorm_bwd", P(g), P(x), P(w), P(mean), P(rstd), P(dx), P(dw), P(db),
+                                    rows, d, lib.stream()))
+        print(f"ln bwd rows={rows} d={d}: {t*1e6:.1f} us {3*rows*d*4/t/1e9:.0f} GB/s", flush=True)
+        out = torch.zeros(d, device=dev)
+        t = timeit(lambda: lib.call("asrx_colsum", P(x), P(out), rows, d, lib.stream()))
+        print(f"colsum rows={rows} d={d}: {t*1e6:.1f} us {rows*d*4/t/1e9:.0f} GB/s", flush=True)
+
+
 def abby_bench():
     from asrx import lib
 
@@ -164,3 +188,5 @@ if __name__ == "__main__":
         attn_bench()
     if "abby" in what:
         abby_bench()
+    if "norm" in what:
+        norm_bench()
