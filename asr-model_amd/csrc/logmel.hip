@@ -64,6 +64,46 @@ __device__ __forceinline__ void wave_lds_sync() {
   asm volatile("" ::: "memory");
 }
 
+// Explicit ds_read_b64 (2 LDS cycles per wave, 256 B/clk): left to itself the compiler merges pairs
+// of these reads into ds_read2_b64 / ds_read2st64_b64, which the LDS services at half the rate
+// (MI355X_MICROARCH.md LDS table).  The loads are issued back to back and completed by one
+// lgkmcnt(0) wait that also names every destination, so no use can be scheduled before it.
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t lds_off(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+template <int OFF>
+__device__ __forceinline__ f2v ds_rd64(uint32_t a) {
+  f2v r;
+  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF) : "memory");
+  return r;
+}
+// eight b64 reads at base + OFF0 + r * STRIDE bytes, r = 0..7
+template <int OFF0, int STRIDE>
+__device__ __forceinline__ void ds_rd64x8(uint32_t a, f2v (&o)[8]) {
+  o[0] = ds_rd64<OFF0>(a);
+  o[1] = ds_rd64<OFF0 + STRIDE>(a);
+  o[2] = ds_rd64<OFF0 + 2 * STRIDE>(a);
+  o[3] = ds_rd64<OFF0 + 3 * STRIDE>(a);
+  o[4] = ds_rd64<OFF0 + 4 * STRIDE>(a);
+  o[5] = ds_rd64<OFF0 + 5 * STRIDE>(a);
+  o[6] = ds_rd64<OFF0 + 6 * STRIDE>(a);
+  o[7] = ds_rd64<OFF0 + 7 * STRIDE>(a);
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(o[0]), "+v"(o[1]), "+v"(o[2]), "+v"(o[3]), "+v"(o[4]), "+v"(o[5]), "+v"(o[6]), "+v"(o[7])
+               :
+               : "memory");
+}
+
+template <int OFF0, int STRIDE>
+__device__ __forceinline__ void ds_rd64x4(uint32_t a, f2v (&o)[4]) {
+  o[0] = ds_rd64<OFF0>(a);
+  o[1] = ds_rd64<OFF0 + STRIDE>(a);
+  o[2] = ds_rd64<OFF0 + 2 * STRIDE>(a);
+  o[3] = ds_rd64<OFF0 + 3 * STRIDE>(a);
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(o[0]), "+v"(o[1]), "+v"(o[2]), "+v"(o[3]) : : "memory");
+}
+
 __device__ __forceinline__ void dft8_tw(cpx (&v)[8], const cpx (&tw)[7]) {
 #pragma unroll
   for (int r = 1; r < 8; ++r) v[r] = asrx_fft::cmul(v[r], tw[r - 1]);
@@ -77,7 +117,7 @@ __device__ __forceinline__ int xcd_block(int bid, int G) {
   return (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + q;
 }
 
-__global__ __launch_bounds__(256) void logmel_tiles_kernel(
+__global__ __launch_bounds__(256, 3) void logmel_tiles_kernel(
     const float* __restrict__ wav, int64_t N, int64_t ld_wav, int vec_ok, int64_t F, int tiles_per_clip,
     int64_t n_tiles, int tiles_per_block, const float* __restrict__ consts, const float* __restrict__ fbw,
     const int* __restrict__ fbs, float* __restrict__ out, int layout, int64_t ld_out,
@@ -175,40 +215,52 @@ __global__ __launch_bounds__(256) void logmel_tiles_kernel(
 #pragma unroll 1
     for (int fi = wid; fi < MEL_FPT; fi += MEL_WAVES) {
       const bool live = f0 + fi < F;  // wave-uniform
-      const float2* s2 = reinterpret_cast<const float2*>(samp + fi * MEL_HOP);
       cpx v[8];
+      {
+        f2v sv[8];
+        ds_rd64x8<0, 512>(lds_off(samp + fi * MEL_HOP + 2 * lane), sv);
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const float2 s = s2[lane + 64 * r];
-        v[r] = cpx{s.x * wv[r].x, s.y * wv[r].y};
+        for (int r = 0; r < 8; ++r) v[r] = cpx{sv[r].x * wv[r].x, sv[r].y * wv[r].y};
       }
       // pass 1 (Ns = 1): out[8j + r]
       asrx_fft::dft8(v);
 #pragma unroll
       for (int r = 0; r < 8; ++r) S[9 * lane + r] = v[r];
       wave_lds_sync();
+      {
+        f2v t[8];
+        ds_rd64x8<0, 576>(lds_off(S + pidx(lane)), t);
 #pragma unroll
-      for (int r = 0; r < 8; ++r) v[r] = S[pidx(lane) + 72 * r];
+        for (int r = 0; r < 8; ++r) v[r] = cpx{t[r].x, t[r].y};
+      }
       wave_lds_sync();
       // pass 2 (Ns = 8): out[(j/8)*64 + j%8 + 8r]
       dft8_tw(v, t2);
 #pragma unroll
       for (int r = 0; r < 8; ++r) S[72 * (lane >> 3) + (lane & 7) + 9 * r] = v[r];
       wave_lds_sync();
+      {
+        f2v t[8];
+        ds_rd64x8<0, 576>(lds_off(S + pidx(lane)), t);
 #pragma unroll
-      for (int r = 0; r < 8; ++r) v[r] = S[pidx(lane) + 72 * r];
+        for (int r = 0; r < 8; ++r) v[r] = cpx{t[r].x, t[r].y};
+      }
       wave_lds_sync();
       // pass 3 (Ns = 64): out[j + 64 r] = Z[j + 64 r], kept in v
       dft8_tw(v, t3);
+      // third exchange unpadded: the R-pattern writes and the mirrored reads are conflict-free
+      // without padding (lane 0 also stores Z_0 at 512, the mirror of its r = 0 slot)
 #pragma unroll
-      for (int r = 0; r < 8; ++r) S[pidx(lane) + 72 * r] = v[r];
+      for (int r = 0; r < 8; ++r) S[lane + 64 * r] = v[r];
+      if (lane == 0) S[512] = v[0];
       wave_lds_sync();
+      f2v zm[8];  // zm[r] = Z[(512 - lane - 64 r) & 511] = S[64 - lane + 64 (7 - r)]
+      ds_rd64x8<0, 512>(lds_off(S + 64 - lane), zm);
       // real-FFT untangle: 2 X_k = (Z_k + conj Z_{512-k}) + W1024^k (-i)(Z_k - conj Z_{512-k})
       float pw[8];
 #pragma unroll
       for (int r = 0; r < 8; ++r) {
-        const int k = lane + 64 * r;
-        const cpx zn = S[pidx((512 - k) & 511)];
+        const cpx zn{zm[7 - r].x, zm[7 - r].y};
         const cpx zk = v[r];
         const cpx e{zk.x + zn.x, zk.y - zn.y};
         const cpx o{zk.y + zn.y, zn.x - zk.x};
@@ -226,18 +278,22 @@ __global__ __launch_bounds__(256) void logmel_tiles_kernel(
       }
       wave_lds_sync();
       // sparse filterbank (weights carry the 1/4; bins read in even-aligned pairs)
-      const float2* P2 = reinterpret_cast<const float2*>(P);
+      static_assert(FB_A == 8 && FB_B == 24, "the filterbank reads below are written out for 8 + 24 taps");
+      f2v pa[4], pb[8], pc[4];  // bins sa .. sa+7 | sb .. sb+15 | sb+16 .. sb+23
+      ds_rd64x4<0, 8>(lds_off(P + 2 * sa2), pa);
+      ds_rd64x8<0, 8>(lds_off(P + 2 * sb2), pb);
+      ds_rd64x4<64, 8>(lds_off(P + 2 * sb2), pc);
       float acc_a = 0.f, acc_b = 0.f;
 #pragma unroll
       for (int q = 0; q < FB_A / 4; ++q) {
         const float4 wq = fbw_s[q * 64 + lane];
-        const float2 p0 = P2[sa2 + 2 * q], p1 = P2[sa2 + 2 * q + 1];
+        const f2v p0 = pa[2 * q], p1 = pa[2 * q + 1];
         acc_a = fmaf(wq.x, p0.x, fmaf(wq.y, p0.y, fmaf(wq.z, p1.x, fmaf(wq.w, p1.y, acc_a))));
       }
 #pragma unroll
       for (int q = 0; q < FB_B / 4; ++q) {
         const float4 wq = fbw_s[(FB_A / 4 + q) * 64 + lane];
-        const float2 p0 = P2[sb2 + 2 * q], p1 = P2[sb2 + 2 * q + 1];
+        const f2v p0 = q < 4 ? pb[2 * q] : pc[2 * (q - 4)], p1 = q < 4 ? pb[2 * q + 1] : pc[2 * (q - 4) + 1];
         acc_b = fmaf(wq.x, p0.x, fmaf(wq.y, p0.y, fmaf(wq.z, p1.x, fmaf(wq.w, p1.y, acc_b))));
       }
       wave_lds_sync();

@@ -218,8 +218,9 @@ def main():
         "vs_baseline": None,
         "dtype": args.precision,
         "data": "synthetic (SURVEY.md §8(d) seeded clips, random-init weights)",
-        "config": {"workload": f"{args.config} (BASELINE configs[1]): log-mel + 4 enc/4 dec d={cfg.dims} "
-                               f"h={cfg.head} fwd+bwd, {B} x 30 s clips per GPU, T={args.text_len}",
+        "config": {"workload": f"{args.config}{' (BASELINE configs[1])' if args.config == 'tiny' else ''}: log-mel + "
+                               f"{cfg.layer} enc/{cfg.layer} dec d={cfg.dims} h={cfg.head} fwd+bwd, {B} x 30 s clips "
+                               f"per GPU, T={args.text_len}",
                    "model": args.config, "global_batch": world * B, "seq_len": 3001, "text_len": args.text_len,
                    "parallelism": f"dp{world}"},
         "per_gpu": round(value / world, 3),
