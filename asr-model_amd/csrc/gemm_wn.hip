@@ -136,6 +136,8 @@ __device__ __forceinline__ float act_t(float x) {
 }
 
 // Tile epilogue: v = alpha * acc + bias (+ beta * C); Z <- v (pre-activation); C <- act(v).
+// Full float4 rows go out as non-temporal stores (streaming writes that would otherwise sit dirty
+// in L2 ahead of the next tile's loads: -8 % at M = 192064, N = K = 384).
 template <int NJ, int ACT>
 __device__ __forceinline__ void epilogue(const Params& p, f32x4 (&acc)[4][2 * NJ], const float* bsl, int m0, int n0,
                                          int wm, int wn, int lr, int lk) {
@@ -161,9 +163,9 @@ __device__ __forceinline__ void epilogue(const Params& p, f32x4 (&acc)[4][2 * NJ
           const float4 o = *reinterpret_cast<const float4*>(dst);
           v[0] += p.beta * o.x; v[1] += p.beta * o.y; v[2] += p.beta * o.z; v[3] += p.beta * o.w;
         }
-        if (zdst) *reinterpret_cast<float4*>(zdst) = make_float4(v[0], v[1], v[2], v[3]);
-        *reinterpret_cast<float4*>(dst) = make_float4(act_t<ACT>(v[0]), act_t<ACT>(v[1]), act_t<ACT>(v[2]),
-                                                      act_t<ACT>(v[3]));
+        if (zdst) __builtin_nontemporal_store(f32x4{v[0], v[1], v[2], v[3]}, reinterpret_cast<f32x4*>(zdst));
+        __builtin_nontemporal_store(f32x4{act_t<ACT>(v[0]), act_t<ACT>(v[1]), act_t<ACT>(v[2]), act_t<ACT>(v[3])},
+                                    reinterpret_cast<f32x4*>(dst));
       } else {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
