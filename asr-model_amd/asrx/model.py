@@ -460,6 +460,33 @@ class processor(nn.Module):  # noqa: N801  (model.py:585-629)
         out = self.ln.run(out.contiguous(), noise, "final.ln", 0, T)
         return ops.linear(out, self.token.weight)
 
+    # ---- decoding (Model.generate): the y-independent audio side of the only live block, once
+    def audio_cache(self, xa, noise: NoiseCtx, B: int):
+        """The last block's audio self-calls i(xa['a'|'b'|'c']) and their cross-attention k/v
+        (model.py:619-622): they do not depend on the text, so generate computes them once.  Earlier
+        blocks are dead in processor.forward (each restarts from the embeddings and only the last
+        block's d / g reach the output), so they are not run at all when decoding."""
+        i = len(self.block) - 1
+        blk = self.block[i]
+        A = self._audio(blk, [xa["a"], xa["b"], xa["c"]], noise, f"b{i}.audio", B, "call")
+        return self._audio(blk, A, noise, f"b{i}.xa", B, "xa")
+
+    def decode_logits(self, x, kv, noise: NoiseCtx):
+        """processor.forward(x, xa, seq=True) (model.py:624-629) from an audio_cache: the last
+        block's text-side calls a, b, c, d, g and the tied logits."""
+        B, T = x.shape
+        i = len(self.block) - 1
+        blk = self.block[i]
+        h = ops.add_rows(ops.Embedding.apply(x, self.token.weight), self.position[:T])
+        a = blk.call(h, noise, f"b{i}.ta", 0, masked=True)
+        b_ = blk.call(a, noise, f"b{i}.tb", 0, kv=kv[0])
+        c_ = blk.call(b_, noise, f"b{i}.tc", 0, kv=kv[1])
+        d = blk.call(c_, noise, f"b{i}.td", 0, kv=kv[2])
+        e = ops.add(a, b_, c_)
+        g = blk.call(d, noise, f"b{i}.tg", 0, kv=blk.xa_side(e, noise, f"b{i}.tg.xa", 0))
+        out = self.ln.run(g.contiguous(), noise, "final.ln", 0, T)
+        return ops.linear(out, self.token.weight)
+
     @staticmethod
     def _audio(blk, streams, noise, site, B, kind):
         """Run blk.call / blk.xa_side on the 3 audio streams, batching streams of equal length."""
@@ -524,3 +551,43 @@ class Model(nn.Module):
         if labels is not None:
             loss = ops.CrossEntropy.apply(logits, labels)
         return {"logits": logits, "loss": loss}
+
+    @torch.no_grad()
+    def generate(self, spectrogram=None, pitch=None, waveform=None, pitch_tokens=None, max_new_tokens=150):
+        """Greedy decoding, model.py:674-701: the encoder once, then per new token the processor with
+        seq=True on the tokens so far (BOS = 1 first), argmax of the last position, stop when every
+        sequence emitted EOS = 2.  Returns LongTensor (B, <= 1 + max_new_tokens).
+
+        The text side is recomputed over the whole prefix each step, as in the reference: its
+        self-attention is causal only in call a (calls b, c, d, g attend over the whole text) and
+        MSheath pools over positions, so earlier positions change as the text grows and a
+        text-side KV cache would change the result.  What is y-independent is cached: the audio
+        self-calls and the cross-attention k/v of the live block (processor.audio_cache).  The
+        gumbel noise is the model's keyed noise at one (seed, step), the same for every decoding
+        step (the reference draws fresh noise per call: its decoding is not reproducible)."""
+        if pitch_tokens is not None:
+            raise NotImplementedError("pitch_tokens: see Model.forward")
+        self.eval()
+        first = next((t for t in (pitch, spectrogram, waveform) if t is not None), None)
+        if first is None:
+            raise ValueError("generate needs at least one of pitch/spectrogram/waveform")
+
+        def aborc(a, b, c):
+            return a if a is not None else (b if b is not None else c)
+
+        streams = [aborc(pitch, spectrogram, waveform), aborc(spectrogram, pitch, waveform),
+                   aborc(waveform, pitch, spectrogram)]
+        streams = [s.to(torch.float32).contiguous() for s in streams]
+        B = first.shape[0]
+        gemm_mod.clear_weight_cache()
+        noise = NoiseCtx(self.noise_seed, self.noise_step, False)
+        enc = self.enc.encode(streams, noise, B)
+        kv = self.processor.audio_cache({"a": enc[0], "b": enc[1], "c": enc[2]}, noise, B)
+        y = torch.ones(B, 1, dtype=torch.long, device=first.device)
+        for _ in range(max_new_tokens):
+            logits = self.processor.decode_logits(y, kv, noise)
+            nxt = torch.argmax(logits[:, -1, :], dim=-1, keepdim=True)
+            y = torch.cat((y, nxt), dim=1)
+            if bool((nxt == 2).all()):
+                break
+        return y
