@@ -3,8 +3,9 @@
 # The variant source replaces the production object of the same basename (csrc/<base>.hip);
 # every other object is the production one from asr-model_amd/build.
 set -e
+SRC_ABS=$(realpath "$2")
 cd "$(dirname "$0")/../../asr-model_amd"
-NAME=$1; SRC=$2; shift 2
+NAME=$1; SRC=$SRC_ABS; shift 2
 BASE=$(basename "$SRC" .hip); BASE=${BASE%_old}; BASE=${BASE%_v2}
 mkdir -p ../tools/exp/vbuild
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Icsrc "$@" -c "$SRC" -o ../tools/exp/vbuild/${BASE}_$NAME.o
