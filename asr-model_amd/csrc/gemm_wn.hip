@@ -180,6 +180,59 @@ __device__ __forceinline__ void epilogue(const Params& p, f32x4 (&acc)[4][2 * NJ
   }
 }
 
+// The same epilogue staged through a per-wave LDS slab, one 16-row slice (mt) at a time: the MFMA
+// layout gives each lane 4 columns of one row, so a direct store instruction writes 16 rows x 64 B;
+// re-read from LDS, every store instruction writes whole contiguous row segments (32*NJ floats per
+// row: 384 B at NJ = 3).  Requires vec_ok(p) (float4-aligned C/Z, N % 4 == 0).
+constexpr int EP_PAD = 4;
+template <int NJ>
+struct EpLds {
+  static constexpr int W = 32 * NJ;           // columns of a wave's sub-tile
+  static constexpr int LD = W + EP_PAD;       // slab row stride (floats)
+  static constexpr int FLOATS = 16 * LD;      // one 16-row slice
+};
+template <int NJ, int ACT>
+__device__ __forceinline__ void epilogue_lds(const Params& p, f32x4 (&acc)[4][2 * NJ], const float* bsl, int m0,
+                                             int n0, int wm, int wn, int lr, int lk, float* ep) {
+  constexpr int NT = 2 * NJ, W = EpLds<NJ>::W, LD = EpLds<NJ>::LD, W4 = W / 4;
+  constexpr int PER = 16 * W4 / 64;  // float4 per lane per slice
+  static_assert((16 * W4) % 64 == 0, "slice must split evenly over the wave");
+  const int lane = threadIdx.x & 63;
+  const int cbase = n0 + wn * W;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int nl = nt * 16 + 4 * lk;
+      float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (p.bias) bv = *reinterpret_cast<const float4*>(bsl + wn * W + nl);
+      *reinterpret_cast<float4*>(ep + lr * LD + nl) =
+          make_float4(p.alpha * acc[mt][nt][0] + bv.x, p.alpha * acc[mt][nt][1] + bv.y,
+                      p.alpha * acc[mt][nt][2] + bv.z, p.alpha * acc[mt][nt][3] + bv.w);
+    }
+    __builtin_amdgcn_wave_barrier();
+    const int rbase = m0 + wm * 64 + mt * 16;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int f = j * 64 + lane, r = f / W4, c = 4 * (f % W4);
+      float4 x = *reinterpret_cast<const float4*>(ep + r * LD + c);
+      const int row = rbase + r, col = cbase + c;
+      if (row >= p.M || col >= p.N) continue;
+      float* dst = p.C + (int64_t)row * p.ldc + col;
+      if (p.beta != 0.f) {
+        const float4 o = *reinterpret_cast<const float4*>(dst);
+        x.x += p.beta * o.x; x.y += p.beta * o.y; x.z += p.beta * o.z; x.w += p.beta * o.w;
+      }
+      if (p.Z)
+        __builtin_nontemporal_store(f32x4{x.x, x.y, x.z, x.w},
+                                    reinterpret_cast<f32x4*>(p.Z + (int64_t)row * p.ldc + col));
+      __builtin_nontemporal_store(f32x4{act_t<ACT>(x.x), act_t<ACT>(x.y), act_t<ACT>(x.z), act_t<ACT>(x.w)},
+                                  reinterpret_cast<f32x4*>(dst));
+    }
+    __builtin_amdgcn_wave_barrier();  // the next slice overwrites the slab
+  }
+}
+
 // AbbyNormal router epilogue (essentials.py:155-161): h = alpha*acc + bias is h_pre; the tile holds
 // whole rows (N <= BN), so logits[row][k] = sum_n SiLU(h[row][n]) W2[k][n] reduce in-tile: over
 // each lane's 4 columns and NT sub-tiles, across the 4 lanes of a row (shuffles) and across the 4
@@ -383,7 +436,12 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wn_kernel(Params p, int ntiles) 
 // the LDS images are double-buffered with one barrier per k-step.  An LDS-DMA piece costs ~100+
 // issue cycles per KB on gfx950 (MI355X_MICROARCH.md constants table); a dwordx4 load + ds_write
 // moves the same KB for a fraction of that, which is what bounded gemm_wn_kernel's pipeline.
-constexpr int WR_DEPTH = 3;  // register stages in flight (k-steps of prefetch)
+#ifndef WR_EPI_LDS
+#define WR_EPI_LDS 1  // LDS-staged epilogue (whole row segments per store instruction)
+#endif
+#ifndef WR_DEPTH
+#define WR_DEPTH 3  // register stages in flight (k-steps of prefetch)
+#endif
 
 template <int NJ>
 struct WrStage {
@@ -452,6 +510,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
   __shared__ __attribute__((aligned(16))) float bias_s[2][BNR];
   __shared__ float w2s[RT ? 3 * BN : 1];
   __shared__ float red[RT ? BM * 12 : 1];
+  __shared__ __attribute__((aligned(16))) float ep_s[RT ? 1 : 8 * EpLds<NJ>::FLOATS];
   if constexpr (RT) {
     for (int i = threadIdx.x; i < 3 * BN; i += NTHR) {
       const int k = i / BN, n = i % BN;
@@ -465,6 +524,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
   const int r = (G % 8 == 0) ? (bid & 7) * (G >> 3) + (bid >> 3) : bid;  // XCD-grouped tile ranks
   const int my = r < ntiles ? (ntiles - r + G - 1) / G : 0;
   const int S = my * nk;
+  float* ep = ep_s + (threadIdx.x >> 6) * EpLds<NJ>::FLOATS;
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wm = wid >> 2, wn = wid & 3;
   const int lr = lane & 15, lk = lane >> 4;
@@ -498,11 +558,24 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  static_assert(WR_DEPTH == 3, "the k-loop below is written out for three stage register sets");
-  WrStage<NJ> st0, st1, st2;  // named (not an array) so they stay in VGPRs
+  // stage register sets are named variables (an array, even constant-indexed after unrolling,
+  // ends up in scratch)
+  WrStage<NJ> st0, st1, st2;
+#if WR_DEPTH >= 4
+  WrStage<NJ> st3;
+#endif
+#if WR_DEPTH >= 5
+  WrStage<NJ> st4;
+#endif
   if (S > 0) load(0, st0);
   if (S > 1) load(1, st1);
   if (S > 2) load(2, st2);
+#if WR_DEPTH >= 4
+  if (S > 3) load(3, st3);
+#endif
+#if WR_DEPTH >= 5
+  if (S > 4) load(4, st4);
+#endif
   if (S > 0) store(0, st0);
   __syncthreads();
 
@@ -538,6 +611,12 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
       const float* bsl = bias_s[(s / nk) & 1];
       if constexpr (RT) {
         epilogue_router<NJ>(p, acc, bsl, w2s, red, m0, wm, wn, lr, lk);
+      } else if (WR_EPI_LDS && vec) switch (p.act) {
+        case ACT_GELU: epilogue_lds<NJ, ACT_GELU>(p, acc, bsl, m0, n0, wm, wn, lr, lk, ep); break;
+        case ACT_SILU: epilogue_lds<NJ, ACT_SILU>(p, acc, bsl, m0, n0, wm, wn, lr, lk, ep); break;
+        case ACT_SIGMOID: epilogue_lds<NJ, ACT_SIGMOID>(p, acc, bsl, m0, n0, wm, wn, lr, lk, ep); break;
+        case ACT_RELU: epilogue_lds<NJ, ACT_RELU>(p, acc, bsl, m0, n0, wm, wn, lr, lk, ep); break;
+        default: epilogue_lds<NJ, ACT_NONE>(p, acc, bsl, m0, n0, wm, wn, lr, lk, ep); break;
       } else switch (p.act) {
         case ACT_GELU: epilogue<NJ, ACT_GELU>(p, acc, bsl, m0, n0, wm, wn, lr, lk); break;
         case ACT_SILU: epilogue<NJ, ACT_SILU>(p, acc, bsl, m0, n0, wm, wn, lr, lk); break;
@@ -553,10 +632,24 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
     __syncthreads();
   };
 
+  static_assert(WR_DEPTH >= 3 && WR_DEPTH <= 5, "stage sets are written out for depths 3..5");
   for (int s = 0; s < S; s += WR_DEPTH) {
+#if WR_DEPTH == 3
     kstep(s, st0, st1);
     if (s + 1 < S) kstep(s + 1, st1, st2);
     if (s + 2 < S) kstep(s + 2, st2, st0);
+#elif WR_DEPTH == 4
+    kstep(s, st0, st1);
+    if (s + 1 < S) kstep(s + 1, st1, st2);
+    if (s + 2 < S) kstep(s + 2, st2, st3);
+    if (s + 3 < S) kstep(s + 3, st3, st0);
+#else
+    kstep(s, st0, st1);
+    if (s + 1 < S) kstep(s + 1, st1, st2);
+    if (s + 2 < S) kstep(s + 2, st2, st3);
+    if (s + 3 < S) kstep(s + 3, st3, st4);
+    if (s + 4 < S) kstep(s + 4, st4, st0);
+#endif
   }
 }
 
