@@ -6,9 +6,12 @@ Design (MI355X-first, not a translation of DDP's call pattern):
   * the bucket plan covers exactly the parameters that receive gradients in this model (found on
     the first step: dead blocks, the unused attn.c / rot.lin / router / span_scale / pitch_tokens
     never do), in reverse registration order = roughly the order backward produces them;
-  * gradients live in the flat bucket buffers (p.grad is a view), so no copy is needed; a
-    post-accumulate-grad hook counts readiness and, when a bucket is complete, a comm stream waits
-    on the compute stream and launches the all-reduce, which then runs under the rest of backward;
+  * gradients live in the flat bucket buffers (p.grad is a view), so no copy is needed;
+  * readiness is counted in gradient events: autograd's post-accumulate-grad hook, and each
+    contribution the asrx kernels accumulate straight into p.grad (asrx.ops.GRAD_LISTENERS).  The
+    first step learns how many events each parameter receives; afterwards, when a bucket has seen
+    all of its events, a comm stream waits on the compute stream and launches the all-reduce,
+    which then runs under the rest of backward;
   * finish() joins the comm stream; buckets a step left incomplete are reduced there with their
     missing slots zero (SURVEY §7: variable unused parameters);
   * bucket size defaults to 64 MB: one 8-GPU ring step over 7 xGMI links moves bucket/8 per link
@@ -17,12 +20,16 @@ Design (MI355X-first, not a translation of DDP's call pattern):
 """
 from __future__ import annotations
 
+import weakref
+
 import torch
 import torch.distributed as dist
 
+from . import ops
+
 
 class _Bucket:
-    __slots__ = ("params", "buf", "pending", "work", "launched", "offsets")
+    __slots__ = ("params", "buf", "pending", "expected", "work", "launched", "offsets")
 
     def __init__(self, params, device):
         self.params = params
@@ -33,7 +40,7 @@ class _Bucket:
         for p in params:
             self.offsets.append(off)
             off += p.numel()
-        self.pending = len(params)
+        self.expected = self.pending = len(params)
         self.work = None
         self.launched = False
 
@@ -50,6 +57,9 @@ class GradSync:
         self.cuda = dev.type == "cuda"
         self.comm = torch.cuda.Stream(device=dev) if self.cuda else None
         self.hooks = [p.register_post_accumulate_grad_hook(self._ready) for p in self.params]
+        self.events: dict[int, int] = {}  # gradient events per parameter, counted during the first step
+        self._listener = weakref.WeakMethod(self._ready)
+        ops.GRAD_LISTENERS.append(self._listener)
 
     # ------------------------------------------------------------------ plan
     def _build(self):
@@ -66,6 +76,7 @@ class GradSync:
         dev = live[0].device
         self.buckets = [_Bucket(ps, dev) for ps in buckets]
         for b in self.buckets:
+            b.expected = b.pending = sum(max(1, self.events.get(id(p), 0)) for p in b.params)
             for p, off in zip(b.params, b.offsets):
                 self.where[id(p)] = (b, off)
                 b.buf[off:off + p.numel()].copy_(p.grad.reshape(-1))
@@ -79,7 +90,7 @@ class GradSync:
             return
         for b in self.buckets:
             b.buf.zero_()
-            b.pending = len(b.params)
+            b.pending = b.expected
             b.work = None
             b.launched = False
             for p, off in zip(b.params, b.offsets):
@@ -88,7 +99,10 @@ class GradSync:
 
     # ------------------------------------------------------------------ overlap
     def _ready(self, p):
-        if self.buckets is None or self.world == 1:
+        if self.buckets is None:
+            self.events[id(p)] = self.events.get(id(p), 0) + 1
+            return
+        if self.world == 1:
             return
         entry = self.where.get(id(p))
         if entry is None:
@@ -133,6 +147,8 @@ class GradSync:
     def remove(self):
         for h in self.hooks:
             h.remove()
+        if self._listener in ops.GRAD_LISTENERS:
+            ops.GRAD_LISTENERS.remove(self._listener)
 
 
 def broadcast_parameters(model: torch.nn.Module, src: int = 0):

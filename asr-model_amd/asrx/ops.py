@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import weakref
 
 import torch
 
@@ -32,6 +33,47 @@ def _zeros_like(t):
 
 ACT = G.ACT
 
+# =============================================================================== parameter gradients
+# Kernels that produce a leaf parameter's gradient accumulate it straight into p.grad (GEMM beta = 1,
+# atomic reductions) instead of returning it to autograd.  A parameter of this model is used 10-50
+# times per step (every residual call re-uses its block's weights, AbbyNormal's router runs ~6 times
+# per call); returned gradients cost a zero-filled buffer per use plus one autograd sum launch per
+# extra use (~3000 small launches per tiny-config step).  `.backward()` semantics are unchanged (p.grad
+# holds the sum); torch.autograd.grad(..., inputs=params) needs DIRECT = False.  Every contribution
+# that lands is announced to GRAD_LISTENERS (asrx.dist.GradSync counts them to start a bucket's
+# all-reduce as soon as the bucket is complete).
+DIRECT = True
+GRAD_LISTENERS: list = []
+
+
+def _direct(ctx, i, p):
+    """Forward-time decision for input i: True when p's gradient goes straight into p.grad."""
+    return DIRECT and p is not None and ctx.needs_input_grad[i] and p.is_leaf
+
+
+def _gbuf(p, direct):
+    """Accumulation target for p's gradient: p.grad (created zeroed on first use) when direct."""
+    if not direct:
+        return torch.zeros_like(p)
+    g = p.grad
+    if g is None:
+        g = torch.zeros_like(p)
+        p.grad = g
+    return g
+
+
+def _gret(p, g, direct):
+    """What backward returns for p: None once g (== p.grad) holds the contribution."""
+    if not direct:
+        return g
+    for ref in list(GRAD_LISTENERS):
+        fn = ref() if isinstance(ref, weakref.WeakMethod) else ref
+        if fn is None:
+            GRAD_LISTENERS.remove(ref)
+        else:
+            fn(p)
+    return None
+
 # =============================================================================== Linear (GEMM)
 
 
@@ -45,12 +87,13 @@ class Linear(torch.autograd.Function):
         y = G.linear_fwd(x, W, b, act=act, preact=z)
         ctx.act = act
         ctx.has_b = b is not None
-        ctx.save_for_backward(x, W, z)
+        ctx.dW, ctx.db = _direct(ctx, 1, W), _direct(ctx, 2, b)
+        ctx.save_for_backward(x, W, z, b if ctx.db else None)
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        x, W, z = ctx.saved_tensors
+        x, W, z, b = ctx.saved_tensors
         gy = _c(gy)
         if ctx.act != "none":
             gz = _E(gy.shape, device=gy.device)
@@ -58,8 +101,11 @@ class Linear(torch.autograd.Function):
         else:
             gz = gy
         dx = G.linear_dgrad(gz, W) if ctx.needs_input_grad[0] else None
-        dW = G.linear_wgrad(gz, x) if ctx.needs_input_grad[1] else None
-        db = colsum(gz) if ctx.has_b and ctx.needs_input_grad[2] else None
+        dW = db = None
+        if ctx.needs_input_grad[1]:
+            dW = _gret(W, G.linear_wgrad(gz, x, out=_gbuf(W, ctx.dW), accumulate=True), ctx.dW)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = _gret(b, colsum(gz, out=_gbuf(b, True) if ctx.db else None), ctx.db)
         return dx, dW, db, None
 
 
@@ -67,9 +113,11 @@ def linear(x, W, b=None, act="none"):
     return Linear.apply(x, W, b, act)
 
 
-def colsum(x2):
+def colsum(x2, out=None):
+    """Column sums of (rows, d), accumulated into `out` when given."""
     d = x2.shape[-1]
-    out = torch.zeros(d, device=x2.device)
+    if out is None:
+        out = torch.zeros(d, device=x2.device)
     lib.call("asrx_colsum", _P(x2), _P(out), _rows(x2), d, _S())
     return out
 
@@ -85,20 +133,21 @@ class SmallLinear(torch.autograd.Function):
         lib.call("asrx_small_linear_fwd", _P(x), _P(W), _P(b), _P(y), _rows(x), K, N, ACT[act], _S())
         ctx.act = act
         ctx.has_b = b is not None
-        ctx.save_for_backward(x, W, y)
+        ctx.dW, ctx.db = _direct(ctx, 1, W), _direct(ctx, 2, b)
+        ctx.save_for_backward(x, W, y, b)
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        x, W, y = ctx.saved_tensors
+        x, W, y, b = ctx.saved_tensors
         gy = _c(gy)
         N, K = W.shape
         dx = _E(x.shape, device=x.device) if ctx.needs_input_grad[0] else None
-        dW = torch.zeros_like(W)
-        db = torch.zeros(N, device=W.device) if ctx.has_b else None
+        dW = _gbuf(W, ctx.dW)
+        db = (_gbuf(b, True) if ctx.db else torch.zeros(N, device=W.device)) if ctx.has_b else None
         lib.call("asrx_small_linear_bwd", _P(gy), _P(y), _P(x), _P(W), _P(dx), _P(dW), _P(db), _rows(x), K, N,
                  ACT[ctx.act], 0.0, _S())
-        return dx, dW, db, None
+        return dx, _gret(W, dW, ctx.dW), (_gret(b, db, ctx.db) if ctx.has_b else None), None
 
 
 def small_linear(x, W, b=None, act="none"):
@@ -129,25 +178,27 @@ class AbbyNormalFn(torch.autograd.Function):
             hpre = G.linear_fwd(x, W1, b1)
             lib.call("asrx_abby_fwd", _P(x), _P(hpre), _P(W2), _P(b2), _P(out), _P(ys), _P(idx), rows, d, L, H,
                      sid_base, key & 0xFFFFFFFF, int(use_noise), _S())
-        ctx.save_for_backward(x, hpre, W1, W2, ys, idx)
+        ctx.dp = [_direct(ctx, i, t) for i, t in ((1, W1), (2, b1), (3, W2), (4, b2))]
+        ctx.save_for_backward(x, hpre, W1, W2, ys, idx, b1, b2)
         return out
 
     @staticmethod
     def backward(ctx, gout):
-        x, hpre, W1, W2, ys, idx = ctx.saved_tensors
+        x, hpre, W1, W2, ys, idx, b1, b2 = ctx.saved_tensors
         gout = _c(gout)
         d = x.shape[-1]
         rows = _rows(x)
+        fW1, fb1, fW2, fb2 = ctx.dp
         dx = _E(x.shape, device=x.device)
         dh = _E(x.shape, device=x.device)
-        dW2 = torch.zeros_like(W2)
-        db2 = torch.zeros(3, device=x.device)
+        dW2, db2 = _gbuf(W2, fW2), _gbuf(b2, fb2)
         lib.call("asrx_abby_bwd", _P(gout), _P(x), _P(hpre), _P(W2), _P(ys), _P(idx), _P(dx), _P(dh), _P(dW2),
                  _P(db2), rows, d, _S())
         G.linear_dgrad(dh, W1, out=dx, beta=1.0)
-        dW1 = G.linear_wgrad(dh, x)
-        db1 = colsum(dh.view(-1, d))
-        return dx, dW1, db1, dW2, db2, None, None, None, None, None, None
+        dW1 = G.linear_wgrad(dh, x, out=_gbuf(W1, fW1), accumulate=True)
+        db1 = colsum(dh.view(-1, d), out=_gbuf(b1, fb1))
+        return (dx, _gret(W1, dW1, fW1), _gret(b1, db1, fb1), _gret(W2, dW2, fW2), _gret(b2, db2, fb2),
+                None, None, None, None, None, None)
 
 
 def abby_normal(mod, x, L, H, sid_base, key, use_noise=True):
@@ -170,20 +221,20 @@ class LayerNormFn(torch.autograd.Function):
         mean = _E(rows, device=x.device)
         rstd = _E(rows, device=x.device)
         lib.call("asrx_layernorm_fwd", _P(x), _P(w), _P(b), _P(y), _P(mean), _P(rstd), rows, d, float(eps), _S())
-        ctx.save_for_backward(x, w, mean, rstd)
+        ctx.dw, ctx.db = _direct(ctx, 1, w), _direct(ctx, 2, b)
+        ctx.save_for_backward(x, w, mean, rstd, b)
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        x, w, mean, rstd = ctx.saved_tensors
+        x, w, mean, rstd, b = ctx.saved_tensors
         gy = _c(gy)
         d = x.shape[-1]
         dx = _E(x.shape, device=x.device)
-        dw = torch.zeros_like(w)
-        db = torch.zeros_like(w)
+        dw, db = _gbuf(w, ctx.dw), _gbuf(b, ctx.db)
         lib.call("asrx_layernorm_bwd", _P(gy), _P(x), _P(w), _P(mean), _P(rstd), _P(dx), _P(dw), _P(db), _rows(x),
                  d, _S())
-        return dx, dw, db, None
+        return dx, _gret(w, dw, ctx.dw), _gret(b, db, ctx.db), None
 
 
 def layer_norm(x, w, b, eps=1e-5):
@@ -306,25 +357,24 @@ class VGateFn(torch.autograd.Function):
         c = 1.0 / math.sqrt(D)
         lib.call("asrx_vgate_fwd", _P(S), _P(nx), _P(mval), _P(h), _P(W2), _P(b2), _P(cw), _P(cb), _P(tx), _P(ion),
                  _P(xval), _P(kv), _P(m2), rows, M, Dh, c, _S())
-        ctx.save_for_backward(x, mkeyn, mval, W1, W2, cw, nx, S, h, kv, m2)
+        ctx.dp = [_direct(ctx, i, t) for i, t in ((2, mval), (3, W1), (4, b1), (5, W2), (6, b2), (7, cw), (8, cb))]
+        ctx.save_for_backward(x, mkeyn, mval, W1, W2, cw, nx, S, h, kv, m2, b1, b2, cb)
         return ion.view(*x.shape[:-1])
 
     @staticmethod
     def backward(ctx, gion):
-        x, mkeyn, mval, W1, W2, cw, nx, S, h, kv, m2 = ctx.saved_tensors
+        x, mkeyn, mval, W1, W2, cw, nx, S, h, kv, m2, b1, b2, cb = ctx.saved_tensors
         gion = _c(gion)
         D = x.shape[-1]
         rows = _rows(x)
         M = mkeyn.shape[0]
         Dh = W1.shape[0]
+        fmval, fW1, fb1, fW2, fb2, fcw, fcb = ctx.dp
         dS = _E(rows, M, device=x.device)
         dnx = _E(rows, device=x.device)
         dh = _E(rows, Dh, device=x.device)
-        dmval = torch.zeros(M, device=x.device)
-        dW2 = torch.zeros_like(W2)
-        db2 = torch.zeros(1, device=x.device)
-        dcw = torch.zeros(2, device=x.device)
-        dcb = torch.zeros(1, device=x.device)
+        dmval, dW2, db2 = _gbuf(mval, fmval), _gbuf(W2, fW2), _gbuf(b2, fb2)
+        dcw, dcb = _gbuf(cw, fcw), _gbuf(cb, fcb)
         lib.call("asrx_vgate_bwd", _P(gion), _P(S), _P(nx), _P(mval), _P(h), _P(W2), _P(cw), _P(kv), _P(m2), _P(dS),
                  _P(dnx), _P(dh), _P(dmval), _P(dW2), _P(db2), _P(dcw), _P(dcb), rows, M, Dh, 1.0 / math.sqrt(D),
                  _S())
@@ -333,10 +383,11 @@ class VGateFn(torch.autograd.Function):
         G.linear_dgrad(dh, W1, out=dx, beta=1.0)
         lib.call("asrx_rownorm_bwd", _P(dnx), _P(x2), _P(nx), _P(dx), rows, D, _S())
         dmkeyn = G.linear_wgrad(dS, x2)
-        dW1 = G.linear_wgrad(dh, x2)
-        db1 = colsum(dh)
-        return (dx.view(x.shape), dmkeyn, dmval.view(M, 1), dW1, db1, dW2.view(1, Dh), db2, dcw.view(1, 2), dcb,
-                None)
+        dW1 = G.linear_wgrad(dh, x2, out=_gbuf(W1, fW1), accumulate=True)
+        db1 = colsum(dh, out=_gbuf(b1, fb1))
+        return (dx.view(x.shape), dmkeyn, _gret(mval, dmval.view(M, 1), fmval), _gret(W1, dW1, fW1),
+                _gret(b1, db1, fb1), _gret(W2, dW2.view(1, Dh), fW2), _gret(b2, db2, fb2),
+                _gret(cw, dcw.view(1, 2), fcw), _gret(cb, dcb, fcb), None)
 
 
 def v_gate(mod, x):
@@ -361,12 +412,13 @@ class TGateFn(torch.autograd.Function):
         lib.call("asrx_small_linear_fwd", _P(x), _P(Wcs), _P(bcs), _P(c), rows, D, 3, 0, _S())
         out = _E(x.shape, device=x.device)
         lib.call("asrx_tgate_fwd", _P(Gs), _P(c), _P(out), rows, D, _S())
-        ctx.save_for_backward(x, Wcat, Wcs, Gs, c)
+        ctx.dWcs, ctx.dbcs = _direct(ctx, 3, Wcs), _direct(ctx, 4, bcs)
+        ctx.save_for_backward(x, Wcat, Wcs, Gs, c, bcs)
         return out
 
     @staticmethod
     def backward(ctx, gout):
-        x, Wcat, Wcs, Gs, c = ctx.saved_tensors
+        x, Wcat, Wcs, Gs, c, bcs = ctx.saved_tensors
         gout = _c(gout)
         D = x.shape[-1]
         rows = _rows(x)
@@ -374,13 +426,12 @@ class TGateFn(torch.autograd.Function):
         dc = _E(rows, 3, device=x.device)
         lib.call("asrx_tgate_bwd", _P(gout), _P(Gs), _P(c), _P(dGz), _P(dc), rows, D, _S())
         dx = G.linear_dgrad(dGz, Wcat)
-        dWcs = torch.zeros_like(Wcs)
-        dbcs = torch.zeros(3, device=x.device)
+        dWcs, dbcs = _gbuf(Wcs, ctx.dWcs), _gbuf(bcs, ctx.dbcs)
         lib.call("asrx_small_linear_bwd", _P(dc), None, _P(x), _P(Wcs), _P(dx), _P(dWcs), _P(dbcs), rows, D, 3, 0,
                  1.0, _S())
         dWcat = G.linear_wgrad(dGz, x)
         dbcat = colsum(dGz)
-        return dx.view(x.shape), dWcat, dbcat, dWcs, dbcs
+        return dx.view(x.shape), dWcat, dbcat, _gret(Wcs, dWcs, ctx.dWcs), _gret(bcs, dbcs, ctx.dbcs)
 
 
 def tgate(mod, x):
@@ -500,6 +551,7 @@ class MSheathCtrl(torch.autograd.Function):
                  _P(active), _P(next_out), _P(rec), _S())
         ctx.mark_non_differentiable(active, next_out)
         ctx.set_materialize_grads(False)
+        ctx.djs = _direct(ctx, 6, jump_s)
         ctx.save_for_backward(mem_v, mem_w, mem, jump_s, rec)
         ctx.layer_i, ctx.layers = layer_i, layers
         return alpha, beta, gam, mwo, active, next_out
@@ -516,11 +568,11 @@ class MSheathCtrl(torch.autograd.Function):
         g_policy = _E(B, 3, device=dev)
         g_mem_v = _E(mem_v.shape, device=dev)
         g_mem_w, g_mem = _E(B, D, device=dev), _E(B, D, device=dev)
-        g_jump_s = torch.zeros(3, device=dev)
+        g_jump_s = _gbuf(jump_s, ctx.djs)
         lib.call("asrx_msheath_ctrl_bwd", _P(g_alpha), _P(g_beta), _P(g_gam), _P(g_mwo), _P(mem_v), _P(mem_w),
                  _P(mem), _P(jump_s), _P(rec), ctx.layer_i, ctx.layers, B, D, _P(g_policy), _P(g_mem_v), _P(g_mem_w),
                  _P(g_mem), _P(g_jump_s), _S())
-        return g_policy, None, None, g_mem_v, g_mem_w, g_mem, g_jump_s, None, None, None
+        return g_policy, None, None, g_mem_v, g_mem_w, g_mem, _gret(jump_s, g_jump_s, ctx.djs), None, None, None
 
 
 class SegMean(torch.autograd.Function):
@@ -684,20 +736,20 @@ class DWConv(torch.autograd.Function):
         K = w.shape[-1]
         y = _E(x.shape, device=x.device)
         lib.call("asrx_dwconv_fwd", _P(x), _P(w), _P(b), _P(y), B, T, C, K, _S())
-        ctx.save_for_backward(x, w)
+        ctx.dw, ctx.db = _direct(ctx, 1, w), _direct(ctx, 2, b)
+        ctx.save_for_backward(x, w, b)
         return y
 
     @staticmethod
     def backward(ctx, g):
-        x, w = ctx.saved_tensors
+        x, w, b = ctx.saved_tensors
         g = _c(g)
         B, T, C = x.shape
         K = w.shape[-1]
         dx = _E(x.shape, device=x.device)
-        dw = torch.zeros_like(w)
-        db = torch.zeros(C, device=x.device)
+        dw, db = _gbuf(w, ctx.dw), _gbuf(b, ctx.db)
         lib.call("asrx_dwconv_bwd", _P(g), _P(x), _P(w), _P(dx), _P(dw), _P(db), B, T, C, K, _S())
-        return dx, dw, db
+        return dx, _gret(w, dw, ctx.dw), _gret(b, db, ctx.db)
 
 
 class BatchNormPS(torch.autograd.Function):
@@ -713,22 +765,22 @@ class BatchNormPS(torch.autograd.Function):
         lib.call("asrx_bn_fwd", _P(x), _P(w), _P(b), _P(y), _P(mean), _P(rstd), B, T, C, float(eps), 1, _S())
         if stats is not None:
             stats.append((mean, rstd))
-        ctx.save_for_backward(x, w, mean, rstd)
+        ctx.dw, ctx.db = _direct(ctx, 1, w), _direct(ctx, 2, b)
+        ctx.save_for_backward(x, w, mean, rstd, b)
         return y
 
     @staticmethod
     def backward(ctx, g):
-        x, w, mean, rstd = ctx.saved_tensors
+        x, w, mean, rstd, b = ctx.saved_tensors
         g = _c(g)
         B, T, C = x.shape
         sg = _E(B, C, device=x.device)
         sgx = _E(B, C, device=x.device)
         dx = _E(x.shape, device=x.device)
-        dw = torch.zeros_like(w)
-        db = torch.zeros_like(w)
+        dw, db = _gbuf(w, ctx.dw), _gbuf(b, ctx.db)
         lib.call("asrx_bn_bwd", _P(g), _P(x), _P(mean), _P(rstd), _P(w), _P(sg), _P(sgx), _P(dx), _P(dw), _P(db), B,
                  T, C, _S())
-        return dx, dw, db, None, None
+        return dx, _gret(w, dw, ctx.dw), _gret(b, db, ctx.db), None, None
 
 
 def batch_norm_eval(x, w, b, rm, rv, eps):
@@ -757,12 +809,13 @@ class Conv3(torch.autograd.Function):
         else:
             G.gemm(x, Wt, y, M=B * T, N=Co, K=3 * Ci, lda=Ci, ldb=3 * Ci, ldc=Co, bias=b, conv_a=True, conv_F=T,
                    conv_C=Ci)
-        ctx.save_for_backward(x, W)
+        ctx.db = _direct(ctx, 2, b)
+        ctx.save_for_backward(x, W, b)
         return y
 
     @staticmethod
     def backward(ctx, g):
-        x, W = ctx.saved_tensors
+        x, W, b = ctx.saved_tensors
         g = _c(g)
         B, T, Ci = x.shape
         Co = W.shape[0]
@@ -781,7 +834,7 @@ class Conv3(torch.autograd.Function):
         G.gemm(g, x, dWt, M=Co, N=3 * Ci, K=B * T, lda=Co, ldb=Ci, ldc=3 * Ci, a_kc=False, b_kc=False, conv_b=True,
                conv_F=T, conv_C=Ci, beta=1.0, splitk=G._splitk_for(B * T, tiles))
         dW = dWt.view(Co, 3, Ci).permute(0, 2, 1).contiguous()
-        db = colsum(g.view(-1, Co))
+        db = _gret(b, colsum(g.view(-1, Co), out=_gbuf(b, True) if ctx.db else None), ctx.db)
         return dx, dW, db
 
 
@@ -795,18 +848,18 @@ class Stem1(torch.autograd.Function):
         D = W.shape[0]
         y = _E(B, T, D, device=x.device)
         lib.call("asrx_stem1_fwd", _P(x), _P(W), _P(b), _P(y), B, T, D, _S())
-        ctx.save_for_backward(x, W)
+        ctx.dW, ctx.db = _direct(ctx, 1, W), _direct(ctx, 2, b)
+        ctx.save_for_backward(x, W, b)
         return y
 
     @staticmethod
     def backward(ctx, g):
-        x, W = ctx.saved_tensors
+        x, W, b = ctx.saved_tensors
         B, T = x.shape
         D = W.shape[0]
-        dW = torch.zeros_like(W)
-        db = torch.zeros(D, device=x.device)
+        dW, db = _gbuf(W, ctx.dW), _gbuf(b, ctx.db)
         lib.call("asrx_stem1_bwd", _P(_c(g)), _P(x), _P(dW), _P(db), B, T, D, _S())
-        return None, dW, db
+        return None, _gret(W, dW, ctx.dW), _gret(b, db, ctx.db)
 
 
 class Embedding(torch.autograd.Function):
@@ -816,16 +869,17 @@ class Embedding(torch.autograd.Function):
         d = E.shape[1]
         y = _E(*ids.shape, d, device=E.device)
         lib.call("asrx_embed_fwd", _P(ids), _P(E), _P(y), ids.numel(), d, _S())
-        ctx.save_for_backward(ids)
+        ctx.dE = _direct(ctx, 1, E)
+        ctx.save_for_backward(ids, E if ctx.dE else None)
         ctx.Eshape = E.shape
         return y
 
     @staticmethod
     def backward(ctx, g):
-        (ids,) = ctx.saved_tensors
-        dE = torch.zeros(ctx.Eshape, device=g.device)
+        ids, E = ctx.saved_tensors
+        dE = _gbuf(E, True) if ctx.dE else torch.zeros(ctx.Eshape, device=g.device)
         lib.call("asrx_embed_bwd", _P(ids), _P(_c(g)), _P(dE), ids.numel(), ctx.Eshape[1], _S())
-        return None, dE
+        return None, _gret(E, dE, ctx.dE)
 
 
 class CrossEntropy(torch.autograd.Function):

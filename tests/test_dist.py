@@ -29,7 +29,42 @@ class Toy(torch.nn.Module):
         return self.c(torch.tanh(self.b(torch.relu(self.a(x)))))
 
 
-def _worker(rank, world, port, bucket_mb, q):
+class _DirectLinear(torch.autograd.Function):
+    """CPU stand-in for an asrx op: y = x W^T + b with W's and b's gradients accumulated straight into
+    .grad through asrx.ops' direct-gradient helpers (events reach GradSync via GRAD_LISTENERS)."""
+
+    @staticmethod
+    def forward(ctx, x, W, b):
+        from asrx import ops
+
+        ctx.dW, ctx.db = ops._direct(ctx, 1, W), ops._direct(ctx, 2, b)
+        ctx.save_for_backward(x, W, b)
+        return x @ W.t() + b
+
+    @staticmethod
+    def backward(ctx, gy):
+        from asrx import ops
+
+        x, W, b = ctx.saved_tensors
+        dW, db = ops._gbuf(W, ctx.dW), ops._gbuf(b, ctx.db)
+        dW += gy.reshape(-1, gy.shape[-1]).t() @ x.reshape(-1, x.shape[-1])
+        db += gy.reshape(-1, gy.shape[-1]).sum(0)
+        return gy @ W, ops._gret(W, dW, ctx.dW), ops._gret(b, db, ctx.db)
+
+
+class ToyDirect(Toy):
+    """Shared weights used several times per step through direct-gradient ops, plus a parameter with
+    both direct and autograd contributions (b.bias)."""
+
+    def forward(self, x):
+        h = torch.relu(_DirectLinear.apply(x, self.a.weight, self.a.bias))
+        h = torch.tanh(_DirectLinear.apply(h, self.b.weight, self.b.bias) + self.b.bias)
+        h2 = _DirectLinear.apply(torch.relu(_DirectLinear.apply(x, self.a.weight, self.a.bias)), self.b.weight,
+                                 self.b.bias)
+        return self.c(h + h2)
+
+
+def _worker(rank, world, port, bucket_mb, q, kind="plain"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -40,7 +75,7 @@ def _worker(rank, world, port, bucket_mb, q):
     from asrx.dist import GradSync, broadcast_parameters
 
     torch.manual_seed(rank)  # different init per rank: broadcast must make them equal
-    model = Toy()
+    model = Toy() if kind == "plain" else ToyDirect()
     broadcast_parameters(model)
     sync = GradSync(model, bucket_mb=bucket_mb)
     results = []
@@ -68,12 +103,13 @@ def _worker(rank, world, port, bucket_mb, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("bucket_mb", [64.0, 0.0005])
-def test_gradsync_gloo_world2(bucket_mb):
+@pytest.mark.parametrize("bucket_mb,kind", [(64.0, "plain"), (0.0005, "plain"), (64.0, "direct"),
+                                            (0.0005, "direct")])
+def test_gradsync_gloo_world2(bucket_mb, kind):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, bucket_mb, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, bucket_mb, q, kind)) for r in range(2)]
     for p in procs:
         p.start()
     out = {}

@@ -68,6 +68,7 @@ def mel_bench():
 def rowops_bench():
     from asrx import ops
 
+    ops.DIRECT = False  # torch.autograd.grad over parameters below
     dev = torch.device("cuda:0")
     B, T, C = 64, 3001, 384
     x = torch.randn(B, T, C, device=dev)
