@@ -14,6 +14,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import re
 import sys
 import time
 
@@ -252,7 +253,7 @@ def main():
             gbs = wn_bytes / wn_sec / 1e9
             result["roofline"] = {"kernel": "asrx::wn::gemm_wr_kernel (wide bf16-weight MFMA GEMM, fp32 activations)",
                                   "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                  "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                                  "frac": round(gbs / HBM_PEAK_GBS, 4), **pmc_traffic("gemm_wr_kernel"),
                                   "algorithmic_bytes_per_launch": round(wn_bytes / wn_n),
                                   "launches_per_step": wn_n // probe_steps,
                                   "avg_us": round(wn_sec / wn_n * 1e6, 2),
@@ -290,6 +291,30 @@ def main():
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(result), flush=True)
+
+
+def pmc_traffic(kernel_substr):
+    """HBM bytes per launch of a kernel from the newest committed PMC table (profiles/
+    r01_pmc_traffic_v*.csv: separate rocprofv3 FETCH_SIZE and WRITE_SIZE passes over one eager step,
+    FETCH doubled per the gfx950 note, see tools/pmc_traffic.py), launch-weighted over every template
+    instance whose name contains kernel_substr.  PMC counters cannot be read inside the timed run,
+    so the figure comes from the profiling pass of the same step; null when no table is present."""
+    import csv
+    import glob
+    tabs = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
+                                         "r*_pmc_traffic_v*.csv")),
+                  key=lambda p: int(re.search(r"_v(\d+)\.csv$", p).group(1)))
+    if not tabs:
+        return {"traffic": None}
+    n, tot = 0, 0.0
+    for r in csv.DictReader(open(tabs[-1])):
+        if kernel_substr in r["kernel"]:
+            n += int(r["launches"])
+            tot += int(r["launches"]) * float(r["avg_hbm_bytes"])
+    if n == 0:
+        return {"traffic": None}
+    return {"traffic": round(tot / n), "traffic_unit": "B/launch",
+            "traffic_source": os.path.join("profiles", os.path.basename(tabs[-1]))}
 
 
 if __name__ == "__main__":
