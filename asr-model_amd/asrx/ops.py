@@ -266,7 +266,7 @@ class AttentionFn(torch.autograd.Function):
         sq, sk, sv, so = _st3(q), _st3(k), _st3(v), _st3(o)
         p = prec.get()
         e0 = probe.begin("attn")
-        lib.call("asrx_attn_fwd", p, _P(q), _addr(sq), _P(k), _addr(sk), _P(v), _addr(sv), _P(o), _addr(so),
+        lib.call("asrx_attn_fwd", prec.attention_prec(), _P(q), _addr(sq), _P(k), _addr(sk), _P(v), _addr(sv), _P(o), _addr(so),
                  _P(lse), B, H, Lq, Lk, hd, int(causal), 1.0 / math.sqrt(hd), _S())
         probe.end("attn", e0, 4.0 * B * H * Lq * Lk * hd * (0.5 if causal else 1.0))
         ctx.causal = causal

@@ -416,6 +416,10 @@ int attn_bwd_mf(const float* q, const int64_t* sq, const float* k, const int64_t
                 const int64_t* sv, const float* dO, const int64_t* sd, const float* lse, const float* delta,
                 float* dq, const int64_t* sdq, float* dk, const int64_t* sdk, float* dv, const int64_t* sdv,
                 int64_t B, int64_t H, int64_t Lq, int64_t Lk, int causal, float scale, hipStream_t stream);
+int attn_fwd_f8(const float* q, const int64_t* sq, const float* k, const int64_t* sk, const float* v,
+                const int64_t* sv, float* o, const int64_t* so, float* lse, int64_t B, int64_t H, int64_t Lq,
+                int64_t Lk, int causal, float scale, hipStream_t stream);
+constexpr int PREC_FP8ATT = 2;  // forward only: e4m3 QK^T (attn_f8.hip)
 }
 
 extern "C" int asrx_attn_fwd(int prec, const float* q, const int64_t* sq, const float* k, const int64_t* sk,
@@ -430,7 +434,11 @@ extern "C" int asrx_attn_fwd(int prec, const float* q, const int64_t* sq, const 
   dim3 g((unsigned)((Lq + ATILE - 1) / ATILE), (unsigned)H, (unsigned)B);
   AttnStrides Sq{sq[0], sq[1], sq[2]}, Sk{sk[0], sk[1], sk[2]}, Sv{sv[0], sv[1], sv[2]}, So{so[0], so[1], so[2]};
   const bool al16 = (((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)o) & 15) == 0;
-  if (prec == PREC_BF16 && al16 && getenv("ASRX_ATTN_OLD") == nullptr)
+  ASRX_REQUIRE(prec == PREC_F32 || prec == PREC_BF16 || prec == PREC_FP8ATT, "attention: bad precision %d", prec);
+  if (prec == PREC_FP8ATT) {
+    ASRX_REQUIRE(al16, "attention: fp8 mode needs 16-byte aligned q/k/v/o");
+    attn_fwd_f8(q, sq, k, sk, v, sv, o, so, lse, B, H, Lq, Lk, causal, scale, stream);
+  } else if (prec == PREC_BF16 && al16 && getenv("ASRX_ATTN_OLD") == nullptr)
     attn_fwd_mf(q, sq, k, sk, v, sv, o, so, lse, B, H, Lq, Lk, causal, scale, stream);
   else if (prec == PREC_BF16)
     attn_fwd_kernel<PREC_BF16><<<g, 256, 0, stream>>>(q, k, v, o, lse, Sq, Sk, Sv, So, H, Lq, Lk, causal, scale);
@@ -445,6 +453,7 @@ extern "C" int asrx_attn_bwd(int prec, const float* q, const int64_t* sq, const 
                              const int64_t* sd, const float* lse, float* delta_ws, float* dq, const int64_t* sdq,
                              float* dk, const int64_t* sdk, float* dv, const int64_t* sdv, int64_t B, int64_t H,
                              int64_t Lq, int64_t Lk, int64_t hd, int causal, float scale, hipStream_t stream) {
+  ASRX_REQUIRE(prec == PREC_F32 || prec == PREC_BF16, "attention backward: precision %d (fp8 is forward only)", prec);
   ASRX_REQUIRE(hd == AHD, "attention: head dim %ld unsupported (64 only)", (long)hd);
   ASRX_REQUIRE(attn_ok(sq) && attn_ok(sk) && attn_ok(sv) && attn_ok(sd) && attn_ok(sdq) && attn_ok(sdk) &&
                    attn_ok(sdv),

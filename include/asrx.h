@@ -83,7 +83,9 @@ int asrx_abby_bwd(const float* dout, const float* x, const float* hpre, const fl
                   asrx_stream_t stream);
 
 /* ---- attention: F.scaled_dot_product_attention(q,k,v,is_causal) at model.py:307, head dim 64.
- *      q/k/v/o are (B,L,H,64) with strides sX = int64[3] {batch, seq, head}; lse (B,H,Lq). -------- */
+ *      q/k/v/o are (B,L,H,64) with strides sX = int64[3] {batch, seq, head}; lse (B,H,Lq).
+ *      asrx_attn_fwd also takes prec 2 = fp8 attention: QK^T on e4m3 with
+ *      per-row scales (MX-rate MFMA), softmax and PV in bf16; the backward takes 0 or 1 only. ---- */
 int asrx_attn_fwd(int prec, const float* q, const int64_t* sq, const float* k, const int64_t* sk, const float* v,
                   const int64_t* sv, float* o, const int64_t* so, float* lse, int64_t B, int64_t H, int64_t Lq,
                   int64_t Lk, int64_t hd, int causal, float scale, asrx_stream_t stream);

@@ -336,3 +336,74 @@ def test_batchnorm_per_sample(cuda, C, T):
     assert _rel(yg, yr) < 1e-5
     for a, r in zip(gg, gr):
         assert _rel(a, r) < 2e-5
+
+
+def _e4m3_rows(t):
+    """Per-row e4m3 quantisation of the fp8 attention mode (attn_f8.hip): x / s rounded to OCP
+    e4m3 (RNE), s = max|x_row| / 448; returns the dequantised values s * e4m3(x / s)."""
+    s = t.abs().amax(-1, keepdim=True) / 448.0
+    s = torch.where(s > 0, s, torch.ones_like(s))
+    return (t / s).to(torch.float8_e4m3fn).to(torch.float32) * s
+
+
+@pytest.mark.parametrize("B,H,Lq,Lk,causal", [(1, 2, 300, 300, False), (2, 3, 600, 517, False),
+                                                (1, 2, 256, 256, True), (2, 1, 70, 70, True), (1, 2, 33, 3001, False),
+                                                (1, 1, 513, 64, False), (2, 2, 1, 77, False)])
+def test_attention_fp8(cuda, B, H, Lq, Lk, causal):
+    """fp8 attention mode (prec 2: e4m3 QK^T with per-row scales, bf16 P and V) against float64
+    softmax attention on the same per-row e4m3-quantised q, k and bf16 v (tight: the kernel computes
+    exactly that), and, on unit-variance inputs (scores of std ~1, as after the model's hd^-0.25 and
+    AbbyNormal), against the unquantised inputs: the accuracy cost of the mode, stated tolerance
+    5e-2 relative Frobenius error of o."""
+    import ctypes
+
+    from asrx import lib
+
+    hd = 64
+    g = torch.Generator().manual_seed(Lq * 7 + Lk + causal)
+
+    def st(t):
+        return (ctypes.c_int64 * 3)(t.stride(0), t.stride(1), t.stride(2))
+
+    def run(q, k, v):
+        o = torch.empty(B, Lq, H, hd, device=cuda)
+        lse = torch.empty(B, H, Lq, device=cuda)
+        qg, kg, vg = q.to(cuda), k.to(cuda), v.to(cuda)
+        lib.call("asrx_attn_fwd", 2, lib.ptr(qg), st(qg), lib.ptr(kg), st(kg), lib.ptr(vg), st(vg), lib.ptr(o),
+                 st(o), lib.ptr(lse), B, H, Lq, Lk, hd, int(causal), 1.0 / 8.0, lib.stream())
+        torch.cuda.synchronize()
+        return o, lse
+
+    def ref(qq, kk, vv):
+        s = qq.double().transpose(1, 2) @ kk.double().transpose(1, 2).transpose(-1, -2) / 8.0
+        if causal:
+            s = s.masked_fill(torch.ones(Lq, Lk, dtype=torch.bool).triu(1), float("-inf"))
+        return (torch.softmax(s, -1) @ vv.double().transpose(1, 2)).transpose(1, 2), torch.logsumexp(s, -1)
+
+    q, k, v = (torch.randn(B, L, H, hd, generator=g) * 3.0 for L in (Lq, Lk, Lk))
+    o, lse = run(q, k, v)
+    r8, l8 = ref(_e4m3_rows(q), _e4m3_rows(k), v.to(torch.bfloat16).float())
+    assert _rel(o, r8) < 1e-2
+    assert float((lse.cpu().double() - l8).abs().max()) < 2e-3
+    q, k, v = (torch.randn(B, L, H, hd, generator=g) for L in (Lq, Lk, Lk))
+    o, _ = run(q, k, v)
+    r32, _ = ref(q, k, v)
+    o = o.cpu().double()
+    assert float((o - r32).norm() / r32.norm()) < 5e-2
+
+
+def test_attention_fp8_mode_forward_only(cuda):
+    """prec.attention('fp8') routes ops.attention's forward to the fp8 kernel; its backward runs the
+    bf16 kernels (asrx_attn_bwd rejects prec 2)."""
+    from asrx import ops, prec
+
+    g = torch.Generator().manual_seed(5)
+    q, k, v = (torch.randn(1, 130, 2, 64, generator=g).to(cuda).requires_grad_() for _ in range(3))
+    with prec.precision("bf16"):
+        ob = ops.attention(q, k, v, False)
+        with prec.attention("fp8"):
+            assert prec.attention_prec() == prec.PREC_FP8ATT
+            of = ops.attention(q, k, v, False)
+        of.sum().backward()
+    assert 0 < _rel(of, ob) < 5e-2
+    assert all(torch.isfinite(t.grad).all() for t in (q, k, v))

@@ -162,6 +162,11 @@ def attn_bench():
                 t = timeit(lambda: ops.attention(q, k, v, causal), iters=5)
                 print(f"attn fwd {'old' if old else 'mf '} B={B} H={H} Lq={Lq} Lk={Lk} causal={causal}: "
                       f"{t*1e6:.1f} us {fl/t/1e12:.1f} TF/s", flush=True)
+            os.environ.pop("ASRX_ATTN_OLD", None)
+            with prec.attention("fp8"):
+                t = timeit(lambda: ops.attention(q, k, v, causal), iters=5)
+            print(f"attn fwd fp8 B={B} H={H} Lq={Lq} Lk={Lk} causal={causal}: {t*1e6:.1f} us {fl/t/1e12:.1f} TF/s",
+                  flush=True)
             for old in (False, True):
                 if old:
                     os.environ["ASRX_ATTN_OLD"] = "1"
