@@ -92,7 +92,7 @@ SIGNATURES = {
     "asrx_gemm_wn": (_i32, [_p, _i64, _i32, _i64, _i64, _p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _f32, _f32,
                             _i32, _i32, _p]),
     "asrx_maxfactor_param_bytes": (_i32, []),
-    "asrx_maxfactor_step": (_i32, [_p, _i32, _i64, _i64, _i64, _i64, _p, _p]),
+    "asrx_maxfactor_step": (_i32, [_p, _i32, _i64, _i64, _i64, _i64, _i64, _p, _p]),
 }
 
 _lib = None

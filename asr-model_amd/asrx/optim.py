@@ -20,14 +20,23 @@ import torch
 from . import lib
 
 
-# one parameter record, byte-compatible with MFParam in csrc/maxfactor.hip (128 bytes)
+# one parameter record, byte-compatible with MFParam in csrc/maxfactor.hip (144 bytes)
 _REC = np.dtype([("p", "u8"), ("g", "u8"), ("rv", "u8"), ("cv", "u8"), ("v", "u8"), ("n", "i8"), ("mats", "i4"),
                  ("rows", "i4"), ("cols", "i4"), ("mode", "i4"), ("beta", "f4"), ("rho", "f4"), ("lr", "f4"),
                  ("decay", "f4"), ("gamma", "f4"), ("d", "f4"), ("eps1", "f4"), ("eps2", "f4"), ("row0", "i8"),
-                 ("cc0", "i8"), ("col0", "i8"), ("mat0", "i8")])
+                 ("cc0", "i8"), ("col0", "i8"), ("mat0", "i8"), ("item0", "i8"), ("gsz", "i4"),
+                 ("pad_", "i4")])
 
 
 _CHUNK = 256  # rows per column-sum work item (MF_CHUNK)
+
+
+def _group(length: int) -> int:
+    """Lanes per row in the row kernels: the power of two >= the row length, at most a wave (64)."""
+    g = 1
+    while g < min(length, 64):
+        g *= 2
+    return g
 
 
 def _geometry(p: torch.Tensor):
@@ -91,7 +100,7 @@ class MaxFactor(torch.optim.Optimizer):
         c["dev_tab"][k].copy_(c["pinned"][k], non_blocking=True)
         c["done"][k].record()
         lib.call("asrx_maxfactor_step", c["dev_tab"][k].data_ptr(), len(live), c["nrows"], c["ncols"], c["ncc"],
-                 c["nmats"], c["ws"].data_ptr(), lib.stream())
+                 c["nmats"], c["nitems"], c["ws"].data_ptr(), lib.stream())
         self._keep = [gr for _, _, gr in live]  # asynchronous call: keep converted gradients alive
         return loss
 
@@ -100,7 +109,7 @@ class MaxFactor(torch.optim.Optimizer):
         if _REC.itemsize != lib_.asrx_maxfactor_param_bytes():
             raise RuntimeError("MaxFactor record layout does not match libasrx")
         tab = np.zeros(len(live), dtype=_REC)
-        nrows = ncols = ncc = nmats = 0
+        nrows = ncols = ncc = nmats = nitems = 0
         steps, b_decay, min_lr, step_tensors = [], [], [], []
         for i, (group, p, grad) in enumerate(live):
             eps1, eps2 = group["eps"]
@@ -116,10 +125,12 @@ class MaxFactor(torch.optim.Optimizer):
                 state["v"] = torch.zeros_like(p)
             mats, rows, cols = _geometry(p)
             mode = 0 if p.dim() <= 1 else (1 if (p.dim() < 3 or group["bias"] == 1) else 2)
+            gsz = _group(p.numel() if mode == 0 else cols)
             tab[i] = (p.data_ptr(), grad.data_ptr(), lib.ptr(state.get("row_var")) or 0,
                       lib.ptr(state.get("col_var")) or 0, state["v"].data_ptr(), p.numel(), mats, rows, cols, mode,
                       0.0, 0.0, group["lr"], group["decay"], group["gamma"], group["d"], eps1, eps2, nrows, ncc, ncols,
-                      nmats)
+                      nmats, nitems, gsz, 0)
+            nitems += -(-(1 if mode == 0 else mats * rows) // (64 // gsz))
             if mode == 0:
                 nrows += 1
             else:
@@ -132,7 +143,7 @@ class MaxFactor(torch.optim.Optimizer):
             min_lr.append(group["min_lr"])
             step_tensors.append(state["step"])
         device = live[0][1].device
-        self._cache = dict(tab=tab, nrows=nrows, ncols=ncols, ncc=ncc, nmats=nmats, device=device,
+        self._cache = dict(tab=tab, nrows=nrows, ncols=ncols, ncc=ncc, nmats=nmats, nitems=nitems, device=device,
                            steps=np.array(steps, dtype=np.float64), b_decay=np.array(b_decay, dtype=np.float64),
                            min_lr=np.array(min_lr, dtype=np.float64), step_tensors=step_tensors,
                            ws=torch.empty(4 * len(live) + 4 * nrows + ncols + nmats, device=device,

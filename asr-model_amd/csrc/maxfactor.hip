@@ -15,8 +15,11 @@
 //   dir = sign(u) * max_c |u|  (dim < 3 or group bias == 1)   |   sign(u) * median_c |u|  (otherwise)
 //   p -= alpha / denom * dir
 // Layout: every parameter is a list of rows (matrix rows, or one row for a vector); the row kernels
-// run one wave per row over the flat row space of all parameters (a binary search over the table's
-// row offsets finds the parameter), so one launch covers the whole model.
+// walk a flat space of wave work items over all parameters (a binary search over the table's item
+// offsets finds the parameter), so one launch covers the whole model.  A work item is one wave
+// split into 64 / gsz lane groups of gsz = pow2 >= row length (<= 64) lanes, one row per group:
+// the k3 conv weights are 2*D*D rows of 3 (a row per wave ran 3 of 64 lanes and made the step ~30x
+// slower than its HBM bytes; now 16 rows share a wave).
 #include "common.h"
 
 namespace asrx {
@@ -35,6 +38,9 @@ struct MFParam {
   int64_t cc0;   // offset in the flat (mat, col, row-chunk) space of the column kernel
   int64_t col0;  // offset in the flat (mat, col) space
   int64_t mat0;  // offset in the flat mat space
+  int64_t item0; // offset in the flat wave-work-item space of the row kernels
+  int gsz;       // lanes per row (power of two <= 64); 64 / gsz rows per work item
+  int pad_;
 };
 
 constexpr int MF_CHUNK = 256;  // rows per column-sum work item
@@ -52,23 +58,39 @@ __device__ __forceinline__ int find_param(const MFParam* t, int n, int64_t idx, 
 
 constexpr int MF_MAXP = 2048;  // parameters per call (the row-offset table is staged in LDS)
 
-// Grid-stride loop of one wave per row over the flat row space; the parameter of a row is found by
-// a binary search over the row offsets staged in LDS (a global-memory search per row was the
-// latency bottleneck).
+// Grid-stride loop over wave work items; the parameter of an item is found by a binary search over
+// the item offsets staged in LDS (a global-memory search per row was the latency bottleneck).  The
+// body gets the flat row, the parameter, whether the lane group holds a real row, the lane's index
+// in its group and the group size; whole groups are valid or invalid together, so group-local
+// shuffles stay well defined.
 template <class F>
-__device__ __forceinline__ void mf_for_rows(const MFParam* __restrict__ tab, int np, int64_t nrows, F&& body) {
+__device__ __forceinline__ void mf_for_rows(const MFParam* __restrict__ tab, int np, int64_t nitems, F&& body) {
   __shared__ int64_t offs[MF_MAXP];
-  for (int k = threadIdx.x; k < np; k += blockDim.x) offs[k] = tab[k].row0;
+  for (int k = threadIdx.x; k < np; k += blockDim.x) offs[k] = tab[k].item0;
   __syncthreads();
-  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < nrows; row += (int64_t)gridDim.x * 4) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t it = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); it < nitems; it += (int64_t)gridDim.x * 4) {
     int lo = 0, hi = np - 1;
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
-      if (offs[mid] <= row) lo = mid;
+      if (offs[mid] <= it) lo = mid;
       else hi = mid - 1;
     }
-    body(row, lo);
+    const int G = tab[lo].gsz;
+    const int64_t nr = tab[lo].mode == 0 ? 1 : (int64_t)tab[lo].mats * tab[lo].rows;
+    const int64_t lr_ = (it - offs[lo]) * (64 / G) + lane / G;
+    body(tab[lo].row0 + lr_, lo, lr_ < nr, lane & (G - 1), G);
   }
+}
+
+// sums / maxima over the aligned group of G lanes (G a power of two)
+__device__ __forceinline__ float grp_sum(float x, int G) {
+  for (int o = G >> 1; o > 0; o >>= 1) x += __shfl_xor(x, o);
+  return x;
+}
+__device__ __forceinline__ float grp_max(float x, int G) {
+  for (int o = G >> 1; o > 0; o >>= 1) x = fmaxf(x, __shfl_xor(x, o));
+  return x;
 }
 
 // stats per parameter: [0] sum p^2, [1] sum u^2, [2] max|u|, [3] unused
@@ -76,25 +98,24 @@ __device__ __forceinline__ float* pstats(float* stats, int i) { return stats + 4
 
 // ---- K1: row sums of g^2 -> row_var (matrices) or v (vectors); per-row sum of p^2 (reduced per
 // parameter by K1b -- same-address atomics from thousands of rows would serialise)
-__global__ __launch_bounds__(256) void mf_rows_kernel(const MFParam* __restrict__ tab, int np, int64_t nrows,
+__global__ __launch_bounds__(256) void mf_rows_kernel(const MFParam* __restrict__ tab, int np, int64_t nitems,
                                                       float* __restrict__ row_p2) {
-  const int lane = threadIdx.x & 63;
-  mf_for_rows(tab, np, nrows, [&](int64_t row, int i) {
+  mf_for_rows(tab, np, nitems, [&](int64_t row, int i, bool ok, int sub, int G) {
     const MFParam P = tab[i];
     const int64_t lr_ = row - P.row0;
     const int64_t base = P.mode == 0 ? 0 : lr_ * P.cols;
-    const int len = P.mode == 0 ? (int)P.n : P.cols;
+    const int len = ok ? (P.mode == 0 ? (int)P.n : P.cols) : 0;
     float sg = 0.f, sp = 0.f;
 #pragma unroll 8
-    for (int c = lane; c < len; c += 64) {
+    for (int c = sub; c < len; c += G) {
       const float g = P.g[base + c], w = P.p[base + c];
       sg += g * g;
       sp += w * w;
       if (P.mode == 0) P.v[c] = P.gamma * P.v[c] + (1.f - P.gamma) * g * g;
     }
-    sg = wave_sum(sg);
-    sp = wave_sum(sp);
-    if (lane == 0) {
+    sg = grp_sum(sg, G);
+    sp = grp_sum(sp, G);
+    if (ok && sub == 0) {
       row_p2[row] = sp;
       if (P.mode != 0) {
         const float mean = sg / ((float)P.cols + 1e-8f);
@@ -188,14 +209,13 @@ __device__ __forceinline__ float mf_u(const MFParam& P, float g, float rvi, floa
 }
 
 // ---- K4: per row: u, row max |u| (or median |u|), and the parameter's sum u^2 / max |u|
-__global__ __launch_bounds__(256) void mf_ustats_kernel(const MFParam* __restrict__ tab, int np, int64_t nrows,
+__global__ __launch_bounds__(256) void mf_ustats_kernel(const MFParam* __restrict__ tab, int np, int64_t nitems,
                                                         const float* __restrict__ mrv, float* __restrict__ rowred,
                                                         float* __restrict__ row_u2, float* __restrict__ row_umax) {
-  const int lane = threadIdx.x & 63;
-  mf_for_rows(tab, np, nrows, [&](int64_t row, int i) {
+  mf_for_rows(tab, np, nitems, [&](int64_t row, int i, bool ok, int sub, int G) {
     const MFParam P = tab[i];
-    const int64_t lr_ = row - P.row0;
-    const int len = P.mode == 0 ? (int)P.n : P.cols;
+    const int64_t lr_ = ok ? row - P.row0 : 0;
+    const int len = ok ? (P.mode == 0 ? (int)P.n : P.cols) : 0;
     const int64_t base = P.mode == 0 ? 0 : lr_ * P.cols;
     const int m = P.mode == 0 ? 0 : (int)(lr_ / P.rows);
     const float rvi = P.mode == 0 ? 0.f : P.rv[lr_];
@@ -204,26 +224,26 @@ __global__ __launch_bounds__(256) void mf_ustats_kernel(const MFParam* __restric
     auto u_at = [&](int c) { return mf_u(P, P.g[base + c], P.mode == 0 ? cvr[c] : rvi, cvr[c], mr); };
     float su = 0.f, mx = 0.f;
 #pragma unroll 8
-    for (int c = lane; c < len; c += 64) {
+    for (int c = sub; c < len; c += G) {
       const float u = u_at(c);
       su += u * u;
       mx = fmaxf(mx, fabsf(u));
     }
-    su = wave_sum(su);
-    mx = wave_max(mx);
+    su = grp_sum(su, G);
+    mx = grp_max(mx, G);
     float red = mx;
     if (P.mode == 2) {
       // lower median of |u| over the row (torch.median): MSB-first radix select on the float bits
-      // (|u| >= 0 orders as uint), |u| recomputed per pass -- median rows are rare and short
+      // (|u| >= 0 orders as uint), |u| recomputed per pass -- median rows are short (conv taps)
       const int k = (len - 1) / 2;
       uint32_t prefix = 0, mask = 0;
       int below = 0;
       for (int bit = 31; bit >= 0; --bit) {
         const uint32_t m2 = mask | (1u << bit);
         float cnt = 0.f;
-        for (int c = lane; c < len; c += 64)
+        for (int c = sub; c < len; c += G)
           cnt += ((__builtin_bit_cast(uint32_t, fabsf(u_at(c))) & m2) == prefix) ? 1.f : 0.f;
-        const int total = (int)wave_sum(cnt);
+        const int total = (int)grp_sum(cnt, G);
         if (below + total <= k) {
           below += total;
           prefix |= 1u << bit;
@@ -232,7 +252,7 @@ __global__ __launch_bounds__(256) void mf_ustats_kernel(const MFParam* __restric
       }
       red = __builtin_bit_cast(float, prefix);
     }
-    if (lane == 0) {
+    if (ok && sub == 0) {
       rowred[row] = red;
       row_u2[row] = su;
       row_umax[row] = mx;
@@ -241,11 +261,11 @@ __global__ __launch_bounds__(256) void mf_ustats_kernel(const MFParam* __restric
 }
 
 // ---- K5: apply
-__global__ __launch_bounds__(256) void mf_apply_kernel(const MFParam* __restrict__ tab, int np, int64_t nrows,
+__global__ __launch_bounds__(256) void mf_apply_kernel(const MFParam* __restrict__ tab, int np, int64_t nitems,
                                                        const float* __restrict__ mrv, const float* __restrict__ rowred,
                                                        const float* __restrict__ stats) {
-  const int lane = threadIdx.x & 63;
-  mf_for_rows(tab, np, nrows, [&](int64_t row, int i) {
+  mf_for_rows(tab, np, nitems, [&](int64_t row, int i, bool ok, int sub, int G) {
+    if (!ok) return;  // no group-wide shuffles below
     const MFParam P = tab[i];
     const int64_t lr_ = row - P.row0;
     const int len = P.mode == 0 ? (int)P.n : P.cols;
@@ -264,7 +284,7 @@ __global__ __launch_bounds__(256) void mf_apply_kernel(const MFParam* __restrict
     const float keep = 1.f - P.lr * P.decay;
     const float* cvr = P.mode == 0 ? P.v : P.cv + (int64_t)m * P.cols;
 #pragma unroll 8
-    for (int c = lane; c < len; c += 64) {
+    for (int c = sub; c < len; c += G) {
       const float u = mf_u(P, P.g[base + c], P.mode == 0 ? cvr[c] : rvi, cvr[c], mr);
       const float sgn = u > 0.f ? 1.f : (u < 0.f ? -1.f : 0.f);
       P.p[base + c] = P.p[base + c] * keep - step * sgn * scale;
@@ -284,7 +304,7 @@ extern "C" int asrx_maxfactor_param_bytes(void) { return (int)sizeof(MFParam); }
 // table: device array of np MFParam (asrx/optim.py packs it); ws: float workspace of
 // 4 np + 4 nrows + ncols + nmats floats; ncc = size of the (mat, col, row-chunk) space.
 extern "C" int asrx_maxfactor_step(const void* table, int np, int64_t nrows, int64_t ncols, int64_t ncc,
-                                   int64_t nmats, float* ws, hipStream_t stream) {
+                                   int64_t nmats, int64_t nitems, float* ws, hipStream_t stream) {
   ASRX_REQUIRE(np > 0, "asrx_maxfactor_step: no parameters");
   const MFParam* tab = reinterpret_cast<const MFParam*>(table);
   float* stats = ws;
@@ -295,15 +315,16 @@ extern "C" int asrx_maxfactor_step(const void* table, int np, int64_t nrows, int
   float* mrv = colacc + ncols;
   if (ncols > 0) (void)hipMemsetAsync(colacc, 0, sizeof(float) * ncols, stream);
   ASRX_REQUIRE(np <= MF_MAXP, "asrx_maxfactor_step: at most %d parameters per call", MF_MAXP);
-  const unsigned gr = (unsigned)std::min<int64_t>((nrows + 3) / 4, 4096);
-  mf_rows_kernel<<<gr, 256, 0, stream>>>(tab, np, nrows, row_a);
+  ASRX_REQUIRE(nitems > 0 && nitems <= nrows, "asrx_maxfactor_step: bad work-item count %ld", (long)nitems);
+  const unsigned gr = (unsigned)std::min<int64_t>((nitems + 3) / 4, 4096);
+  mf_rows_kernel<<<gr, 256, 0, stream>>>(tab, np, nitems, row_a);
   mf_param_reduce_kernel<<<np, 256, 0, stream>>>(tab, np, 0, row_a, nullptr, stats, mrv);
   if (ncc > 0) {
     mf_cols_kernel<<<(unsigned)((ncc + 255) / 256), 256, 0, stream>>>(tab, np, ncc, colacc);
     mf_colfin_kernel<<<(unsigned)((ncols + 255) / 256), 256, 0, stream>>>(tab, np, ncols, colacc);
   }
-  mf_ustats_kernel<<<gr, 256, 0, stream>>>(tab, np, nrows, mrv, rowred, row_a, row_b);
+  mf_ustats_kernel<<<gr, 256, 0, stream>>>(tab, np, nitems, mrv, rowred, row_a, row_b);
   mf_param_reduce_kernel<<<np, 256, 0, stream>>>(tab, np, 1, row_a, row_b, stats, mrv);
-  mf_apply_kernel<<<gr, 256, 0, stream>>>(tab, np, nrows, mrv, rowred, stats);
+  mf_apply_kernel<<<gr, 256, 0, stream>>>(tab, np, nitems, mrv, rowred, stats);
   ASRX_LAUNCHED("asrx_maxfactor_step");
 }

@@ -219,11 +219,12 @@ int asrx_ce_bwd(const float* z, const int64_t* labels, const float* lse, const f
  *      model.py:783-787 builds), for every parameter of the model in one call.  table: device array
  *      of np parameter records (layout and packing: asrx/optim.py; record size from
  *      asrx_maxfactor_param_bytes()); nrows / ncols / ncc / nmats: sizes of the flat row, (mat,
- *      col), (mat, col, 256-row chunk) and mat spaces; ws: float workspace of 4 np + 4 nrows +
+ *      col), (mat, col, 256-row chunk) and mat spaces; nitems: size of the wave-work-item space
+ *      (each record's rows packed 64 / gsz to a wave); ws: float workspace of 4 np + 4 nrows +
  *      ncols + nmats.  Updates parameters and optimizer state in place. ----------------------------- */
 int asrx_maxfactor_param_bytes(void);
 int asrx_maxfactor_step(const void* table, int np, int64_t nrows, int64_t ncols, int64_t ncc, int64_t nmats,
-                        float* ws, asrx_stream_t stream);
+                        int64_t nitems, float* ws, asrx_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -10,7 +10,9 @@ from oracle import maxfactor as omf
 pytestmark = pytest.mark.gpu
 
 SHAPES = [((37, 53), 0), ((16, 4, 3), 0), ((29,), 0), ((), 0), ((384, 1, 1), 0), ((300, 40), 0),
-          ((1, 1, 384), 1), ((8, 20), 1), ((5,), 1), ((6, 2, 10), 1)]
+          ((1, 1, 384), 1), ((8, 20), 1), ((5,), 1), ((6, 2, 10), 1),
+          # short rows packed several to a wave (lane groups of 4 / 16 / 32), ragged last work item
+          ((48, 40, 3), 1), ((7, 5, 15), 0), ((33, 17), 0), ((9, 7, 2), 1)]
 
 
 def _rel(a, b):
