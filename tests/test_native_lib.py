@@ -65,3 +65,28 @@ def test_noise_uniform_never_hits_0_or_1():
     assert u[0] > 0 and u[1] < 1
     g = noise.gumbel(12345, np.arange(1 << 20, dtype=np.uint64))
     assert np.all(np.isfinite(g))
+
+
+def test_maxfactor_record_layout_and_grouping():
+    """The numpy record the optimizer packs matches MFParam; rows pack 64 / gsz to a wave."""
+    from asrx import lib, optim
+
+    assert optim._REC.itemsize == lib.load().asrx_maxfactor_param_bytes() == 144
+    assert [optim._group(n) for n in (1, 2, 3, 5, 15, 16, 17, 64, 65, 40000)] == [1, 2, 4, 8, 16, 16, 32, 64, 64, 64]
+
+
+def test_attention_mode_switch():
+    """fp8 attention is a forward-only mode layered on the bf16 perf mode."""
+    import pytest
+
+    from asrx import prec
+
+    with prec.precision("bf16"):
+        assert prec.attention_prec() == prec.PREC_BF16
+        with prec.attention("fp8"):
+            assert prec.attention_prec() == prec.PREC_FP8ATT
+            with prec.precision("fp32"):  # parity mode ignores the attention mode
+                assert prec.attention_prec() == prec.PREC_F32
+        assert prec.attention_prec() == prec.PREC_BF16
+    with pytest.raises(ValueError):
+        prec.set_attention("fp16")
