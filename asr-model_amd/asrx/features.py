@@ -9,6 +9,7 @@ from __future__ import annotations
 from dataclasses import dataclass
 from typing import Any, Dict, List
 
+import numpy as np
 import torch
 
 from . import mel as _mel
@@ -16,13 +17,68 @@ from . import mel as _mel
 _DEVICE = torch.device("cuda:0")
 
 
+def read_wav(path):
+    """RIFF/WAVE decode to float32 (frames, channels) the way soundfile.read(path, dtype='float32')
+    returns it: integer PCM scaled by 2^-(bits-1) (8-bit PCM is unsigned, offset 128), IEEE float
+    passed through; WAVE_FORMAT_EXTENSIBLE resolved through its sub-format.  Returns (array, rate);
+    the array is 1-D for mono, as soundfile returns it."""
+    raw = open(path, "rb").read()
+    if len(raw) < 12 or raw[:4] != b"RIFF" or raw[8:12] != b"WAVE":
+        raise NotImplementedError(f"load_wave({path!r}): only RIFF/WAVE files are decoded here "
+                                  "(soundfile, which the reference uses for FLAC, is not installed)")
+    fmt = data = None
+    pos = 12
+    while pos + 8 <= len(raw):
+        cid, size = raw[pos:pos + 4], int.from_bytes(raw[pos + 4:pos + 8], "little")
+        body = raw[pos + 8:pos + 8 + size]
+        if cid == b"fmt ":
+            fmt = body
+        elif cid == b"data":
+            data = body
+        pos += 8 + size + (size & 1)
+    if fmt is None or data is None:
+        raise ValueError(f"{path!r}: WAVE file without fmt/data chunks")
+    tag, ch, rate = int.from_bytes(fmt[0:2], "little"), int.from_bytes(fmt[2:4], "little"), int.from_bytes(fmt[4:8], "little")
+    bits = int.from_bytes(fmt[14:16], "little")
+    if tag == 0xFFFE and len(fmt) >= 26:
+        tag = int.from_bytes(fmt[24:26], "little")
+    width = bits // 8
+    n = len(data) // (width * ch)
+    buf = data[:n * width * ch]
+    if tag == 3 and bits in (32, 64):
+        x = np.frombuffer(buf, dtype="<f4" if bits == 32 else "<f8").astype(np.float32)
+    elif tag == 1 and bits == 8:
+        x = (np.frombuffer(buf, dtype=np.uint8).astype(np.float32) - 128.0) / 128.0
+    elif tag == 1 and bits in (16, 32):
+        x = np.frombuffer(buf, dtype="<i2" if bits == 16 else "<i4").astype(np.float64) / float(1 << (bits - 1))
+        x = x.astype(np.float32)
+    elif tag == 1 and bits == 24:
+        b = np.frombuffer(buf, dtype=np.uint8).reshape(-1, 3).astype(np.int32)
+        v = b[:, 0] | (b[:, 1] << 8) | (b[:, 2] << 16)
+        v = np.where(v >= 1 << 23, v - (1 << 24), v)
+        x = (v.astype(np.float64) / float(1 << 23)).astype(np.float32)
+    else:
+        raise NotImplementedError(f"{path!r}: WAVE format tag {tag} with {bits}-bit samples is not supported")
+    x = x.reshape(n, ch)
+    return (x[:, 0].copy() if ch == 1 else x), rate
+
+
 def load_wave(audio, sample_rate=16000):
-    """essentials.load_wave (essentials.py:301-319) for the in-memory dict branch.  The file-path
-    branch needs soundfile, which is absent here: decode the file to a dict first."""
+    """essentials.load_wave (essentials.py:301-319).  File path: decoded by read_wav (WAV only;
+    soundfile, which the reference calls, is absent here), then peak-normalised as the reference
+    does -- mono by max|x|, multi-channel by the per-channel max of x (not of |x|, essentials.py:306)
+    and returned channels-first.  Dict: the array as float32 with its own rate, not normalised."""
+    if isinstance(audio, str):
+        wp, sample_rate = read_wav(audio)
+        if wp.ndim > 1:
+            abs_max = wp.max(axis=0)
+            wp = wp / abs_max if any(abs_max > 0) else wp
+            return torch.from_numpy(np.ascontiguousarray(wp.T)), sample_rate
+        abs_max = float(np.abs(wp).max()) if wp.size else 0.0
+        wp = wp / abs_max if abs_max > 0 else wp
+        return torch.from_numpy(wp), sample_rate
     if isinstance(audio, dict):
         return torch.as_tensor(audio["array"]).float(), audio["sampling_rate"]
-    if isinstance(audio, str):
-        raise NotImplementedError("load_wave(path): soundfile is not installed; pass {'array', 'sampling_rate'}")
     raise TypeError("Invalid wave_data format.")
 
 
