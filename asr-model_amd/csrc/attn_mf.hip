@@ -160,10 +160,20 @@ __global__ __launch_bounds__(NTHR, 1) void attn_fwd_mf_kernel(const float* __res
         tmax = fmaxf(tmax, x);
       }
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
-    const float mnew = fmaxf(m, tmax);
-    const float mc = mnew == -INFINITY ? 0.f : mnew * c;       // a row with no valid key yet: p = 0
-    const float alpha = __builtin_amdgcn_exp2f(m * c - mc);   // m = -inf on the first tile -> 0
-    m = mnew;
+    // lazy rescale: the running max moves only when a score passes it by more than 2^8 in the exp2
+    // domain (p <= 256 otherwise, exact in the fp32 sums and fine in bf16), so most tiles skip the
+    // O / l rescale; m = -inf (nothing seen yet) moves on the first finite score
+    const bool up = tmax * c > m * c + 8.f;
+    if (__any(up)) {  // wave-uniform
+      const float alpha = up ? __builtin_amdgcn_exp2f(m * c - tmax * c) : 1.f;  // m = -inf -> 0
+      if (up) m = tmax;
+      l *= alpha;
+#pragma unroll
+      for (int d = 0; d < 2; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oacc[d][r] *= alpha;
+    }
+    const float mc = m == -INFINITY ? 0.f : m * c;
     bf16x8 pb[2][2];
     float lsum = 0.f;
 #pragma unroll
@@ -178,11 +188,7 @@ __global__ __launch_bounds__(NTHR, 1) void attn_fwd_mf_kernel(const float* __res
         }
         pb[kb2][s2] = pack8(pv);
       }
-    l = l * alpha + lsum;
-#pragma unroll
-    for (int d = 0; d < 2; ++d)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) oacc[d][r] *= alpha;
+    l += lsum;
 
     // ---- O^T += V^T P^T
     const int g = lane >> 4, gi = lane & 15;
