@@ -182,9 +182,10 @@ class AudioEncoder(nn.Module):
             x = layer[3].run(x, noise, f"enc.L{l}", sid_base)
             x = ops.act(x, "gelu")
             x = ops.DWConv.apply(x, layer[5].weight, layer[5].bias)
-            x = ops.act(x, "gelu")
-            if self.training:
-                x = ops.Dropout.apply(x, sid_base, noise.key(f"enc.L{l}.dr"), 0.1)
+            if self.training:  # GELU -> Dropout(0.1) in one kernel each way
+                x = ops.ActDropout.apply(x, "gelu", sid_base, noise.key(f"enc.L{l}.dr"), 0.1)
+            else:
+                x = ops.act(x, "gelu")
         return ops.add_rows(x, sinusoids(x.shape[1], x.shape[2], x.device))
 
     def encode(self, streams, noise: NoiseCtx, B: int):

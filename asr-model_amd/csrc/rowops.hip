@@ -746,6 +746,50 @@ __global__ void dropout_kernel(const float* __restrict__ x, float* __restrict__ 
   }
 }
 
+__device__ __forceinline__ float act_grad(int act, float v) {
+  switch (act) {
+    case ACT_GELU: return gelu_grad(v);
+    case ACT_SILU: return silu_grad(v);
+    case ACT_SIGMOID: {
+      const float s = sigmoid_f(v);
+      return s * (1.f - s);
+    }
+    default: return 1.f;
+  }
+}
+
+// act + nn.Dropout fused (the encoder layer's trailing GELU -> Dropout(0.1), model.py:147; act
+// NONE is plain dropout, ConvLite's model.py:107), float4 over channels with 32-bit index math:
+//   fwd: y = act(z) * keep / (1 - p)        bwd: dz = g * keep / (1 - p) * act'(z)
+// with the same keyed mask as dropout_kernel (identical products, so bit-identical to act then
+// dropout).  Saves the intermediate act(z) round trip (one write + one read of the tensor) and the
+// scalar kernel's 64-bit divisions.  Requires C % 4 == 0, 16-byte alignment and n / 4 < 2^32.
+template <bool BWD>
+__global__ void act_dropout4_kernel(const float4* __restrict__ g, const float4* __restrict__ z,
+                                    float4* __restrict__ out, uint32_t n4, uint32_t C4, uint32_t T, uint32_t C,
+                                    uint32_t sid_base, uint32_t key, float p, int act) {
+  const float sc = 1.0f / (1.0f - p);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
+    const uint32_t row = i / C4, c0 = (i - row * C4) * 4u;
+    const uint32_t t = row % T, b = row / T;
+    const uint32_t base = ((sid_base + b) * C + c0) * 4096u + t;
+    const float4 v = z[i];
+    float r[4] = {v.x, v.y, v.z, v.w};
+    float gg[4] = {0.f, 0.f, 0.f, 0.f};
+    if (BWD) {
+      const float4 gv = g[i];
+      gg[0] = gv.x; gg[1] = gv.y; gg[2] = gv.z; gg[3] = gv.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool keep = noise_uniform(key, base + (uint32_t)j * 4096u) >= p;
+      if (BWD) r[j] = (keep ? gg[j] * sc : 0.f) * act_grad(act, r[j]);
+      else r[j] = keep ? apply_act(act, r[j]) * sc : 0.f;
+    }
+    out[i] = make_float4(r[0], r[1], r[2], r[3]);
+  }
+}
+
 // ============================================================================ depthwise conv
 // groups=D Conv1d with kernel K, padding K/2 (ConvLite.depth k15, model.py:99-102; encoder k3,
 // model.py:147) on channels-last (B, T, C).
@@ -1540,11 +1584,43 @@ int asrx_glu_bwd(const float* g, const float* x, float* dx, int64_t rows, int64_
   ASRX_LAUNCHED("asrx_glu_bwd");
 }
 
+static bool act_dropout_vec_ok(const void* a, const void* b, const void* c, int64_t n, int64_t C) {
+  return C % 4 == 0 && ((((uintptr_t)a | (uintptr_t)b | (uintptr_t)c) & 15) == 0) && n / 4 < (1LL << 32);
+}
+
 int asrx_dropout(const float* x, float* y, int64_t B, int64_t T, int64_t C, int64_t sid_base, uint32_t key, float p,
                  hipStream_t stream) {
-  if (B * T * C == 0) return 0;
-  LAUNCH_EW(dropout_kernel, B * T * C, x, y, B, T, (int)C, sid_base, key, p);
+  const int64_t n = B * T * C;
+  if (n == 0) return 0;
+  if (act_dropout_vec_ok(x, y, nullptr, n, C))
+    LAUNCH_EW(act_dropout4_kernel<false>, n / 4, nullptr, reinterpret_cast<const float4*>(x),
+              reinterpret_cast<float4*>(y), (uint32_t)(n / 4), (uint32_t)(C / 4), (uint32_t)T, (uint32_t)C,
+              (uint32_t)sid_base, key, p, (int)ACT_NONE);
+  else
+    LAUNCH_EW(dropout_kernel, n, x, y, B, T, (int)C, sid_base, key, p);
   ASRX_LAUNCHED("asrx_dropout");
+}
+
+int asrx_act_dropout_fwd(const float* z, float* y, int64_t B, int64_t T, int64_t C, int64_t sid_base, uint32_t key,
+                         float p, int act, hipStream_t stream) {
+  const int64_t n = B * T * C;
+  if (n == 0) return 0;
+  ASRX_REQUIRE(act_dropout_vec_ok(z, y, nullptr, n, C), "act_dropout: needs C %% 4 == 0 and 16-byte aligned tensors");
+  LAUNCH_EW(act_dropout4_kernel<false>, n / 4, nullptr, reinterpret_cast<const float4*>(z),
+            reinterpret_cast<float4*>(y), (uint32_t)(n / 4), (uint32_t)(C / 4), (uint32_t)T, (uint32_t)C,
+            (uint32_t)sid_base, key, p, act);
+  ASRX_LAUNCHED("asrx_act_dropout_fwd");
+}
+
+int asrx_act_dropout_bwd(const float* g, const float* z, float* dz, int64_t B, int64_t T, int64_t C,
+                         int64_t sid_base, uint32_t key, float p, int act, hipStream_t stream) {
+  const int64_t n = B * T * C;
+  if (n == 0) return 0;
+  ASRX_REQUIRE(act_dropout_vec_ok(g, z, dz, n, C), "act_dropout: needs C %% 4 == 0 and 16-byte aligned tensors");
+  LAUNCH_EW(act_dropout4_kernel<true>, n / 4, reinterpret_cast<const float4*>(g), reinterpret_cast<const float4*>(z),
+            reinterpret_cast<float4*>(dz), (uint32_t)(n / 4), (uint32_t)(C / 4), (uint32_t)T, (uint32_t)C,
+            (uint32_t)sid_base, key, p, act);
+  ASRX_LAUNCHED("asrx_act_dropout_bwd");
 }
 
 int asrx_dwconv_fwd(const float* x, const float* w, const float* b, float* y, int64_t B, int64_t T, int64_t C,
