@@ -175,15 +175,21 @@ class AudioEncoder(nn.Module):
         return ops.Stem1.apply(x.reshape(B, T), self.conv2[0].weight, self.conv2[0].bias)
 
     def layers(self, x, noise: NoiseCtx, sid_base: int):
+        n = len(self.encoder)
+        fused_lead = False  # the previous layer's fused tail already applied this layer's leading GELU
         for l, layer in enumerate(self.encoder):
-            x = ops.act(x, "gelu")
+            if not fused_lead:
+                x = ops.act(x, "gelu")
+            fused_lead = False
             x = ops.Conv3.apply(x, layer[1].weight, layer[1].bias)
             x = ops.layer_norm(x, layer[2].gamma, layer[2].beta, layer[2].eps)
             x = layer[3].run(x, noise, f"enc.L{l}", sid_base)
             x = ops.act(x, "gelu")
             x = ops.DWConv.apply(x, layer[5].weight, layer[5].bias)
-            if self.training:  # GELU -> Dropout(0.1) in one kernel each way
-                x = ops.ActDropout.apply(x, "gelu", sid_base, noise.key(f"enc.L{l}.dr"), 0.1)
+            if self.training:  # GELU -> Dropout(0.1) [-> next layer's GELU] in one kernel each way
+                fused_lead = l + 1 < n
+                x = ops.ActDropout.apply(x, "gelu", sid_base, noise.key(f"enc.L{l}.dr"), 0.1,
+                                         "gelu" if fused_lead else "none")
             else:
                 x = ops.act(x, "gelu")
         return ops.add_rows(x, sinusoids(x.shape[1], x.shape[2], x.device))

@@ -727,29 +727,30 @@ class Dropout(torch.autograd.Function):
 
 
 class ActDropout(torch.autograd.Function):
-    """act then nn.Dropout(p) in train mode on channels-last (B, T, C), one kernel each way
-    (bit-identical to Act followed by Dropout with the same key)."""
+    """act, then nn.Dropout(p) in train mode, then act2 ("none" to skip) on channels-last (B, T, C),
+    one kernel each way (bit-identical to Act, Dropout, Act with the same key)."""
 
     @staticmethod
-    def forward(ctx, z, act, sid_base, key, p):
+    def forward(ctx, z, act, sid_base, key, p, act2="none"):
         z = _c(z)
         B, T, C = z.shape
         y = _E(z.shape, device=z.device)
-        lib.call("asrx_act_dropout_fwd", _P(z), _P(y), B, T, C, sid_base, key & 0xFFFFFFFF, float(p), ACT[act], _S())
-        ctx.args = (act, sid_base, key, p)
+        lib.call("asrx_act_dropout_fwd", _P(z), _P(y), B, T, C, sid_base, key & 0xFFFFFFFF, float(p), ACT[act],
+                 ACT[act2], _S())
+        ctx.args = (act, sid_base, key, p, act2)
         ctx.save_for_backward(z)
         return y
 
     @staticmethod
     def backward(ctx, g):
-        act, sid_base, key, p = ctx.args
+        act, sid_base, key, p, act2 = ctx.args
         (z,) = ctx.saved_tensors
         g = _c(g)
         B, T, C = z.shape
         dz = _E(z.shape, device=z.device)
         lib.call("asrx_act_dropout_bwd", _P(g), _P(z), _P(dz), B, T, C, sid_base, key & 0xFFFFFFFF, float(p),
-                 ACT[act], _S())
-        return dz, None, None, None, None
+                 ACT[act], ACT[act2], _S())
+        return dz, None, None, None, None, None
 
 
 class DWConv(torch.autograd.Function):

@@ -764,10 +764,12 @@ __device__ __forceinline__ float act_grad(int act, float v) {
 // with the same keyed mask as dropout_kernel (identical products, so bit-identical to act then
 // dropout).  Saves the intermediate act(z) round trip (one write + one read of the tensor) and the
 // scalar kernel's 64-bit divisions.  Requires C % 4 == 0, 16-byte alignment and n / 4 < 2^32.
+// act2 (applied after the dropout) is the NEXT encoder layer's leading GELU (model.py:143), fused in
+// when the layer output has no other consumer; the backward recomputes act(z) for act2'.
 template <bool BWD>
 __global__ void act_dropout4_kernel(const float4* __restrict__ g, const float4* __restrict__ z,
                                     float4* __restrict__ out, uint32_t n4, uint32_t C4, uint32_t T, uint32_t C,
-                                    uint32_t sid_base, uint32_t key, float p, int act) {
+                                    uint32_t sid_base, uint32_t key, float p, int act, int act2) {
   const float sc = 1.0f / (1.0f - p);
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
     const uint32_t row = i / C4, c0 = (i - row * C4) * 4u;
@@ -783,8 +785,14 @@ __global__ void act_dropout4_kernel(const float4* __restrict__ g, const float4* 
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const bool keep = noise_uniform(key, base + (uint32_t)j * 4096u) >= p;
-      if (BWD) r[j] = (keep ? gg[j] * sc : 0.f) * act_grad(act, r[j]);
-      else r[j] = keep ? apply_act(act, r[j]) * sc : 0.f;
+      if (BWD) {
+        float gj = gg[j];
+        if (act2 != ACT_NONE) gj = gj * act_grad(act2, keep ? apply_act(act, r[j]) * sc : 0.f);
+        r[j] = (keep ? gj * sc : 0.f) * act_grad(act, r[j]);
+      } else {
+        const float y = keep ? apply_act(act, r[j]) * sc : 0.f;
+        r[j] = act2 != ACT_NONE ? apply_act(act2, y) : y;
+      }
     }
     out[i] = make_float4(r[0], r[1], r[2], r[3]);
   }
@@ -1595,31 +1603,31 @@ int asrx_dropout(const float* x, float* y, int64_t B, int64_t T, int64_t C, int6
   if (act_dropout_vec_ok(x, y, nullptr, n, C))
     LAUNCH_EW(act_dropout4_kernel<false>, n / 4, nullptr, reinterpret_cast<const float4*>(x),
               reinterpret_cast<float4*>(y), (uint32_t)(n / 4), (uint32_t)(C / 4), (uint32_t)T, (uint32_t)C,
-              (uint32_t)sid_base, key, p, (int)ACT_NONE);
+              (uint32_t)sid_base, key, p, (int)ACT_NONE, (int)ACT_NONE);
   else
     LAUNCH_EW(dropout_kernel, n, x, y, B, T, (int)C, sid_base, key, p);
   ASRX_LAUNCHED("asrx_dropout");
 }
 
 int asrx_act_dropout_fwd(const float* z, float* y, int64_t B, int64_t T, int64_t C, int64_t sid_base, uint32_t key,
-                         float p, int act, hipStream_t stream) {
+                         float p, int act, int act2, hipStream_t stream) {
   const int64_t n = B * T * C;
   if (n == 0) return 0;
   ASRX_REQUIRE(act_dropout_vec_ok(z, y, nullptr, n, C), "act_dropout: needs C %% 4 == 0 and 16-byte aligned tensors");
   LAUNCH_EW(act_dropout4_kernel<false>, n / 4, nullptr, reinterpret_cast<const float4*>(z),
             reinterpret_cast<float4*>(y), (uint32_t)(n / 4), (uint32_t)(C / 4), (uint32_t)T, (uint32_t)C,
-            (uint32_t)sid_base, key, p, act);
+            (uint32_t)sid_base, key, p, act, act2);
   ASRX_LAUNCHED("asrx_act_dropout_fwd");
 }
 
 int asrx_act_dropout_bwd(const float* g, const float* z, float* dz, int64_t B, int64_t T, int64_t C,
-                         int64_t sid_base, uint32_t key, float p, int act, hipStream_t stream) {
+                         int64_t sid_base, uint32_t key, float p, int act, int act2, hipStream_t stream) {
   const int64_t n = B * T * C;
   if (n == 0) return 0;
   ASRX_REQUIRE(act_dropout_vec_ok(g, z, dz, n, C), "act_dropout: needs C %% 4 == 0 and 16-byte aligned tensors");
   LAUNCH_EW(act_dropout4_kernel<true>, n / 4, reinterpret_cast<const float4*>(g), reinterpret_cast<const float4*>(z),
             reinterpret_cast<float4*>(dz), (uint32_t)(n / 4), (uint32_t)(C / 4), (uint32_t)T, (uint32_t)C,
-            (uint32_t)sid_base, key, p, act);
+            (uint32_t)sid_base, key, p, act, act2);
   ASRX_LAUNCHED("asrx_act_dropout_bwd");
 }
 

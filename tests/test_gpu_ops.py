@@ -409,8 +409,9 @@ def test_attention_fp8_mode_forward_only(cuda):
     assert all(torch.isfinite(t.grad).all() for t in (q, k, v))
 
 
-@pytest.mark.parametrize("B,T,C,sid_base,act", [(2, 101, 384, 0, "gelu"), (3, 77, 64, 64, "gelu"), (1, 33, 8, 5, "none")])
-def test_act_dropout_fused(cuda, B, T, C, sid_base, act):
+@pytest.mark.parametrize("B,T,C,sid_base,act,act2", [(2, 101, 384, 0, "gelu", "none"), (3, 77, 64, 64, "gelu", "none"),
+                                                     (1, 33, 8, 5, "none", "none"), (2, 50, 384, 3, "gelu", "gelu")])
+def test_act_dropout_fused(cuda, B, T, C, sid_base, act, act2):
     """Fused act + dropout (encoder layer tail) and the float4 dropout: masks equal the oracle's keyed
     mask (keep iff uniform(key, (sid*C + c)*4096 + t) >= p, oracle/keys.py), forward/backward
     bit-identical to Act then Dropout."""
@@ -423,12 +424,16 @@ def test_act_dropout_fused(cuda, B, T, C, sid_base, act):
     g = torch.Generator().manual_seed(B * T + C)
     z = torch.randn(B, T, C, generator=g).to(cuda).requires_grad_()
     gout = torch.randn(B, T, C, generator=g).to(cuda)
-    y = ops.ActDropout.apply(z, act, sid_base, key, p)
+    y = ops.ActDropout.apply(z, act, sid_base, key, p, act2)
     (dz,) = torch.autograd.grad(y, z, gout)
     z2 = z.detach().clone().requires_grad_()
     y2 = ops.Dropout.apply(ops.act(z2, act) if act != "none" else z2 * 1.0, sid_base, key, p)
+    if act2 != "none":
+        y2 = ops.act(y2, act2)
     (dz2,) = torch.autograd.grad(y2, z2, gout)
     assert torch.equal(y, y2) and torch.equal(dz, dz2)
+    if act2 != "none":
+        return
     b, t, c = np.meshgrid(np.arange(B), np.arange(T), np.arange(C), indexing="ij")
     idx = (((sid_base + b) * C + c) * 4096 + t).astype(np.uint64) & 0xFFFFFFFF
     keep = torch.from_numpy(np.asarray(onoise.uniform(key, idx.ravel())).reshape(B, T, C) >= p)
