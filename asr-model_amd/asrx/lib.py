@@ -76,7 +76,7 @@ SIGNATURES = {
     "asrx_glu_fwd": (_i32, [_p, _p, _i64, _i64, _p]),
     "asrx_glu_bwd": (_i32, [_p, _p, _p, _i64, _i64, _p]),
     "asrx_dropout": (_i32, [_p, _p, _i64, _i64, _i64, _i64, _u32, _f32, _p]),
-    "asrx_act_dropout_fwd": (_i32, [_p, _p, _i64, _i64, _i64, _i64, _u32, _f32, _i32, _i32, _p]),
+    "asrx_act_dropout_fwd": (_i32, [_p, _p, _p, _i64, _i64, _i64, _i64, _u32, _f32, _i32, _i32, _p]),
     "asrx_act_dropout_bwd": (_i32, [_p, _p, _p, _i64, _i64, _i64, _i64, _u32, _f32, _i32, _i32, _p]),
     "asrx_dwconv_fwd": (_i32, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),
     "asrx_dwconv_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),

@@ -125,8 +125,8 @@ class ConvLite(nn.Module):
                                     self.bn.eps)
         y = ops.act(y, "silu")
         y = ops.linear(y, self.point2.weight.view(D, D), self.point2.bias)
-        if self.training:
-            y = ops.Dropout.apply(y, sid_base, noise.key(site + ".cl"), 0.1)
+        if self.training:  # res + dropout(y) in one pass
+            return ops.DropoutAdd.apply(res, y, sid_base, noise.key(site + ".cl"), 0.1)
         return ops.add(res, y)
 
     @torch.no_grad()

@@ -735,8 +735,8 @@ class ActDropout(torch.autograd.Function):
         z = _c(z)
         B, T, C = z.shape
         y = _E(z.shape, device=z.device)
-        lib.call("asrx_act_dropout_fwd", _P(z), _P(y), B, T, C, sid_base, key & 0xFFFFFFFF, float(p), ACT[act],
-                 ACT[act2], _S())
+        lib.call("asrx_act_dropout_fwd", _P(z), None, _P(y), B, T, C, sid_base, key & 0xFFFFFFFF, float(p),
+                 ACT[act], ACT[act2], _S())
         ctx.args = (act, sid_base, key, p, act2)
         ctx.save_for_backward(z)
         return y
@@ -751,6 +751,30 @@ class ActDropout(torch.autograd.Function):
         lib.call("asrx_act_dropout_bwd", _P(g), _P(z), _P(dz), B, T, C, sid_base, key & 0xFFFFFFFF, float(p),
                  ACT[act], ACT[act2], _S())
         return dz, None, None, None, None, None
+
+
+class DropoutAdd(torch.autograd.Function):
+    """res + nn.Dropout(p)(y) in train mode (ConvLite tail, model.py:107-118) in one pass; bit-identical
+    to add(res, Dropout(y)).  Backward: d res = g, d y = the dropout of g."""
+
+    @staticmethod
+    def forward(ctx, res, y, sid_base, key, p):
+        res, y = _c(res), _c(y)
+        B, T, C = y.shape
+        out = _E(y.shape, device=y.device)
+        lib.call("asrx_act_dropout_fwd", _P(y), _P(res), _P(out), B, T, C, sid_base, key & 0xFFFFFFFF, float(p),
+                 ACT["none"], ACT["none"], _S())
+        ctx.args = (sid_base, key, p)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        sid_base, key, p = ctx.args
+        g = _c(g)
+        B, T, C = g.shape
+        dy = _E(g.shape, device=g.device)
+        lib.call("asrx_dropout", _P(g), _P(dy), B, T, C, sid_base, key & 0xFFFFFFFF, float(p), _S())
+        return g, dy, None, None, None
 
 
 class DWConv(torch.autograd.Function):

@@ -766,10 +766,13 @@ __device__ __forceinline__ float act_grad(int act, float v) {
 // scalar kernel's 64-bit divisions.  Requires C % 4 == 0, 16-byte alignment and n / 4 < 2^32.
 // act2 (applied after the dropout) is the NEXT encoder layer's leading GELU (model.py:143), fused in
 // when the layer output has no other consumer; the backward recomputes act(z) for act2'.
+// res (forward only, nullable) adds a residual after everything: ConvLite's `res + dropout(point2(.))`
+// (model.py:107-118) in the same pass.
 template <bool BWD>
 __global__ void act_dropout4_kernel(const float4* __restrict__ g, const float4* __restrict__ z,
-                                    float4* __restrict__ out, uint32_t n4, uint32_t C4, uint32_t T, uint32_t C,
-                                    uint32_t sid_base, uint32_t key, float p, int act, int act2) {
+                                    const float4* __restrict__ res, float4* __restrict__ out, uint32_t n4,
+                                    uint32_t C4, uint32_t T, uint32_t C, uint32_t sid_base, uint32_t key, float p,
+                                    int act, int act2) {
   const float sc = 1.0f / (1.0f - p);
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
     const uint32_t row = i / C4, c0 = (i - row * C4) * 4u;
@@ -793,6 +796,10 @@ __global__ void act_dropout4_kernel(const float4* __restrict__ g, const float4* 
         const float y = keep ? apply_act(act, r[j]) * sc : 0.f;
         r[j] = act2 != ACT_NONE ? apply_act(act2, y) : y;
       }
+    }
+    if (!BWD && res) {
+      const float4 rv = res[i];
+      r[0] = rv.x + r[0]; r[1] = rv.y + r[1]; r[2] = rv.z + r[2]; r[3] = rv.w + r[3];
     }
     out[i] = make_float4(r[0], r[1], r[2], r[3]);
   }
@@ -1601,7 +1608,7 @@ int asrx_dropout(const float* x, float* y, int64_t B, int64_t T, int64_t C, int6
   const int64_t n = B * T * C;
   if (n == 0) return 0;
   if (act_dropout_vec_ok(x, y, nullptr, n, C))
-    LAUNCH_EW(act_dropout4_kernel<false>, n / 4, nullptr, reinterpret_cast<const float4*>(x),
+    LAUNCH_EW(act_dropout4_kernel<false>, n / 4, nullptr, reinterpret_cast<const float4*>(x), nullptr,
               reinterpret_cast<float4*>(y), (uint32_t)(n / 4), (uint32_t)(C / 4), (uint32_t)T, (uint32_t)C,
               (uint32_t)sid_base, key, p, (int)ACT_NONE, (int)ACT_NONE);
   else
@@ -1609,13 +1616,13 @@ int asrx_dropout(const float* x, float* y, int64_t B, int64_t T, int64_t C, int6
   ASRX_LAUNCHED("asrx_dropout");
 }
 
-int asrx_act_dropout_fwd(const float* z, float* y, int64_t B, int64_t T, int64_t C, int64_t sid_base, uint32_t key,
-                         float p, int act, int act2, hipStream_t stream) {
+int asrx_act_dropout_fwd(const float* z, const float* res, float* y, int64_t B, int64_t T, int64_t C,
+                         int64_t sid_base, uint32_t key, float p, int act, int act2, hipStream_t stream) {
   const int64_t n = B * T * C;
   if (n == 0) return 0;
-  ASRX_REQUIRE(act_dropout_vec_ok(z, y, nullptr, n, C), "act_dropout: needs C %% 4 == 0 and 16-byte aligned tensors");
+  ASRX_REQUIRE(act_dropout_vec_ok(z, y, res, n, C), "act_dropout: needs C %% 4 == 0 and 16-byte aligned tensors");
   LAUNCH_EW(act_dropout4_kernel<false>, n / 4, nullptr, reinterpret_cast<const float4*>(z),
-            reinterpret_cast<float4*>(y), (uint32_t)(n / 4), (uint32_t)(C / 4), (uint32_t)T, (uint32_t)C,
+            reinterpret_cast<const float4*>(res), reinterpret_cast<float4*>(y), (uint32_t)(n / 4), (uint32_t)(C / 4), (uint32_t)T, (uint32_t)C,
             (uint32_t)sid_base, key, p, act, act2);
   ASRX_LAUNCHED("asrx_act_dropout_fwd");
 }
@@ -1626,7 +1633,7 @@ int asrx_act_dropout_bwd(const float* g, const float* z, float* dz, int64_t B, i
   if (n == 0) return 0;
   ASRX_REQUIRE(act_dropout_vec_ok(g, z, dz, n, C), "act_dropout: needs C %% 4 == 0 and 16-byte aligned tensors");
   LAUNCH_EW(act_dropout4_kernel<true>, n / 4, reinterpret_cast<const float4*>(g), reinterpret_cast<const float4*>(z),
-            reinterpret_cast<float4*>(dz), (uint32_t)(n / 4), (uint32_t)(C / 4), (uint32_t)T, (uint32_t)C,
+            nullptr, reinterpret_cast<float4*>(dz), (uint32_t)(n / 4), (uint32_t)(C / 4), (uint32_t)T, (uint32_t)C,
             (uint32_t)sid_base, key, p, act, act2);
   ASRX_LAUNCHED("asrx_act_dropout_bwd");
 }

@@ -195,9 +195,10 @@ int asrx_dropout(const float* x, float* y, int64_t B, int64_t T, int64_t C, int6
                  float p, asrx_stream_t stream);
 /* act then nn.Dropout(p) then act2 fused (encoder layer tail GELU -> Dropout, model.py:147, and the
  * next layer's leading GELU, model.py:143; act2 = 0 for none): y = act2(act(z) masked and scaled with
- * asrx_dropout's keyed mask); bwd dz = g * act2'(.) * mask / (1 - p) * act'(z).  C % 4 == 0. */
-int asrx_act_dropout_fwd(const float* z, float* y, int64_t B, int64_t T, int64_t C, int64_t sid_base, uint32_t key,
-                         float p, int act, int act2, asrx_stream_t stream);
+ * asrx_dropout's keyed mask) [+ res when res != NULL: ConvLite's residual, model.py:118];
+ * bwd dz = g * act2'(.) * mask / (1 - p) * act'(z) (the residual's gradient is g itself).  C % 4 == 0. */
+int asrx_act_dropout_fwd(const float* z, const float* res, float* y, int64_t B, int64_t T, int64_t C,
+                         int64_t sid_base, uint32_t key, float p, int act, int act2, asrx_stream_t stream);
 int asrx_act_dropout_bwd(const float* g, const float* z, float* dz, int64_t B, int64_t T, int64_t C,
                          int64_t sid_base, uint32_t key, float p, int act, int act2, asrx_stream_t stream);
 int asrx_dwconv_fwd(const float* x, const float* w, const float* b, float* y, int64_t B, int64_t T, int64_t C,

@@ -438,3 +438,19 @@ def test_act_dropout_fused(cuda, B, T, C, sid_base, act, act2):
     idx = (((sid_base + b) * C + c) * 4096 + t).astype(np.uint64) & 0xFFFFFFFF
     keep = torch.from_numpy(np.asarray(onoise.uniform(key, idx.ravel())).reshape(B, T, C) >= p)
     assert torch.equal((y.detach().cpu() != 0), keep & (z.detach().cpu() != 0))
+
+
+def test_dropout_add_fused(cuda):
+    """ConvLite tail res + Dropout(y) in one pass: forward and both gradients bit-identical to
+    add(res, Dropout(y))."""
+    from asrx import ops
+
+    g = torch.Generator().manual_seed(11)
+    res, y = (torch.randn(2, 97, 384, generator=g).to(cuda).requires_grad_() for _ in range(2))
+    gout = torch.randn(2, 97, 384, generator=g).to(cuda)
+    out = ops.DropoutAdd.apply(res, y, 7, 0xBEEF, 0.1)
+    d1 = torch.autograd.grad(out, (res, y), gout)
+    out2 = ops.add(res, ops.Dropout.apply(y, 7, 0xBEEF, 0.1))
+    d2 = torch.autograd.grad(out2, (res, y), gout)
+    assert torch.equal(out, out2)
+    assert all(torch.equal(a, b) for a, b in zip(d1, d2))
