@@ -521,6 +521,10 @@ class Model(nn.Module):
 
     def __init__(self, param: Dimensions):
         super().__init__()
+        hd = param.dims // param.head if param.head > 0 else 0
+        if param.head <= 0 or param.dims % param.head or hd not in (64, 128) or param.dims % 64:
+            raise ValueError(f"Dimensions(dims={param.dims}, head={param.head}): head dim {hd} unsupported; the "
+                             "attention kernels take head dims 64 and 128 (dims a multiple of 64)")
         self.param = param
         self.processor = processor(tokens=param.tokens, mels=param.mels, dims=param.dims, head=param.head,
                                    layer=param.layer, act=param.act, n_type=param.n_type)
@@ -548,6 +552,9 @@ class Model(nn.Module):
                    aborc(waveform, pitch, spectrogram)]
         streams = [s.to(torch.float32).contiguous() for s in streams]
         B = first.shape[0]
+        # how this step is batched decides how many gradient contributions each shared weight gets
+        # (equal-length streams share one pass): asrx.dist.GradSync keys its event plans on it
+        self.grad_signature = (self.training, tuple(s.shape[-1] for s in streams))
         gemm_mod.clear_weight_cache()
         noise = NoiseCtx(self.noise_seed, self.noise_step, self.training)
         if self.training:

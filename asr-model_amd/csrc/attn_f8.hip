@@ -1,7 +1,8 @@
 // Flash-attention forward with an fp8 (OCP e4m3) QK^T: the "fp8 attention" precision mode of
 // SURVEY.md §8(b) (config 5: small model, fp8 attention, greedy decode).  Same SDPA contract as
-// attn_mf.hip (model.py:307: head dim 64, non-causal or top-left causal, Lq != Lk, ragged tails,
-// fp32 (B, L, H, 64) q/k/v/o with arbitrary strides, natural-log lse).
+// attn_mf.hip (model.py:307: head dim HD = 64 or 128, non-causal or top-left causal, Lq != Lk,
+// ragged tails, fp32 (B, L, H, HD) q/k/v/o with arbitrary strides, natural-log lse).  HD = 128 keeps
+// two 64-wide halves per tile (the attn_mf.hip layout) and issues one MX-rate MFMA per half.
 //
 // Workgroup = 8 waves = 256 query rows of one (b, h); wave = 32 rows; 64-key tiles, double-buffered.
 //   Q and K are quantised per ROW to e4m3: x' = x / s, s = max|x_row| / 448 (the scale of a row
@@ -76,20 +77,27 @@ __device__ __forceinline__ void load8(const float* base, int64_t ld, int64_t key
   }
 }
 
-// K chunk -> e4m3 in LDS with its row scale (the 8 threads of a key row are 8 consecutive lanes)
-__device__ __forceinline__ void store_k8(unsigned char* Kt, float* ksc, int key, int c, const float4& a,
-                                         const float4& b) {
-  float am = fmaxf(amax4(a), amax4(b));
+// K chunks (8 consecutive d of every half) -> e4m3 in LDS with the key row's scale (the 8 threads
+// of a key row are 8 consecutive lanes; each holds chunk c of every half)
+template <int NH>
+__device__ __forceinline__ void store_k8(unsigned char* Kt, float* ksc, int key, int c, const float4 (&a)[NH],
+                                         const float4 (&b)[NH]) {
+  float am = 0.f;
+#pragma unroll
+  for (int hf = 0; hf < NH; ++hf) am = fmaxf(am, fmaxf(amax4(a[hf]), amax4(b[hf])));
   am = fmaxf(am, __shfl_xor(am, 1));
   am = fmaxf(am, __shfl_xor(am, 2));
   am = fmaxf(am, __shfl_xor(am, 4));
   const float s = am > 0.f ? am / E4M3_MAX : 1.f;
   const float r = 1.f / s;
-  uint2 u;
-  u.x = f8x4(a.x * r, a.y * r, a.z * r, a.w * r);
-  u.y = f8x4(b.x * r, b.y * r, b.z * r, b.w * r);
   const int chunk = (c >> 1) ^ k8swz(key);
-  *reinterpret_cast<uint2*>(Kt + key * 64 + 16 * chunk + 8 * (c & 1)) = u;
+#pragma unroll
+  for (int hf = 0; hf < NH; ++hf) {
+    uint2 u;
+    u.x = f8x4(a[hf].x * r, a[hf].y * r, a[hf].z * r, a[hf].w * r);
+    u.y = f8x4(b[hf].x * r, b[hf].y * r, b[hf].z * r, b[hf].w * r);
+    *reinterpret_cast<uint2*>(Kt + hf * KT * 64 + key * 64 + 16 * chunk + 8 * (c & 1)) = u;
+  }
   if (c == 0) ksc[key] = s;
 }
 
@@ -99,15 +107,17 @@ __device__ __forceinline__ void store_v(unsigned short* tile, int key, int pc, c
   *reinterpret_cast<u32x4*>(tile + key * 64 + 8 * pc) = u;
 }
 
+template <int HD>
 __global__ __launch_bounds__(NTHR, 1) void attn_fwd_f8_kernel(const float* __restrict__ q, const float* __restrict__ k,
                                                               const float* __restrict__ v, float* __restrict__ o,
                                                               float* __restrict__ lse, AttnStridesMF sq,
                                                               AttnStridesMF sk, AttnStridesMF sv, AttnStridesMF so,
                                                               int64_t H, int64_t Lq, int64_t Lk, int causal,
                                                               float scale) {
-  __shared__ __attribute__((aligned(16))) unsigned char Ks[2][KT * 64];
+  constexpr int NH = HD / 64;
+  __shared__ __attribute__((aligned(16))) unsigned char Ks[2][NH * KT * 64];
   __shared__ __attribute__((aligned(16))) float Kscale[2][KT];
-  __shared__ __attribute__((aligned(16))) unsigned short Vs[2][KT * 64];
+  __shared__ __attribute__((aligned(16))) unsigned short Vs[2][NH * KT * 64];
 
   const int b = blockIdx.z, h = blockIdx.y;
   const int64_t q0 = (int64_t)blockIdx.x * QB;
@@ -118,26 +128,36 @@ __global__ __launch_bounds__(NTHR, 1) void attn_fwd_f8_kernel(const float* __res
   const float* kb = k + b * sk.b + h * sk.h;
   const float* vb = v + b * sv.b + h * sv.h;
 
-  // Q'^T (B operand): lane (q = j, hi) holds e4m3 Q[q][32 hi .. 32 hi + 31] / s_q
-  v8i32 qf;
+  // Q'^T (B operand): lane (q = j, hi) holds e4m3 Q[q][64 hf + 32 hi .. +31] / s_q, s_q over all HD
+  v8i32 qf[NH];
   float sq_row;
   {
-    float4 x[8];
+    float4 x[NH][8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) x[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int hf = 0; hf < NH; ++hf)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) x[hf][i] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (qi < Lq) {
-      const float* p = qb + qi * sq.l + 32 * hi;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) x[i] = *reinterpret_cast<const float4*>(p + 4 * i);
+      for (int hf = 0; hf < NH; ++hf) {
+        const float* p = qb + qi * sq.l + 64 * hf + 32 * hi;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[hf][i] = *reinterpret_cast<const float4*>(p + 4 * i);
+      }
     }
     float am = 0.f;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) am = fmaxf(am, amax4(x[i]));
+    for (int hf = 0; hf < NH; ++hf)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) am = fmaxf(am, amax4(x[hf][i]));
     am = fmaxf(am, __shfl_xor(am, 32));
     sq_row = am > 0.f ? am / E4M3_MAX : 1.f;
     const float r = 1.f / sq_row;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) qf[i] = (int)f8x4(x[i].x * r, x[i].y * r, x[i].z * r, x[i].w * r);
+    for (int hf = 0; hf < NH; ++hf)
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        qf[hf][i] = (int)f8x4(x[hf][i].x * r, x[hf][i].y * r, x[hf][i].z * r, x[hf][i].w * r);
   }
   const float c = scale * LOG2E;
   const float cq = c * sq_row;  // per-lane: score -> log2 domain, with the query's row scale folded in
@@ -147,16 +167,19 @@ __global__ __launch_bounds__(NTHR, 1) void attn_fwd_f8_kernel(const float* __res
   const int ntiles = (int)((kend + KT - 1) / KT);
   const int skey = tid >> 3, sc = tid & 7;
 
-  float4 ka, kb4, va, vb4;
-  load8(kb, sk.l, skey, Lk, sc, ka, kb4);
-  load8(vb, sv.l, skey, Lk, sc, va, vb4);
-  store_k8(Ks[0], Kscale[0], skey, sc, ka, kb4);
-  store_v(Vs[0], skey, sc ^ vswz(skey), va, vb4);
+  float4 ka[NH], kb4[NH], va[NH], vb4[NH];
+#pragma unroll
+  for (int hf = 0; hf < NH; ++hf) {
+    load8(kb + 64 * hf, sk.l, skey, Lk, sc, ka[hf], kb4[hf]);
+    load8(vb + 64 * hf, sv.l, skey, Lk, sc, va[hf], vb4[hf]);
+    store_v(Vs[0] + hf * KT * 64, skey, sc ^ vswz(skey), va[hf], vb4[hf]);
+  }
+  store_k8<NH>(Ks[0], Kscale[0], skey, sc, ka, kb4);
   __syncthreads();
 
-  f32x16 oacc[2];
+  f32x16 oacc[HD / 32];
 #pragma unroll
-  for (int d = 0; d < 2; ++d)
+  for (int d = 0; d < HD / 32; ++d)
 #pragma unroll
     for (int r = 0; r < 16; ++r) oacc[d][r] = 0.f;
   float m = -INFINITY;  // running max of (unscaled-by-c) scores
@@ -166,25 +189,31 @@ __global__ __launch_bounds__(NTHR, 1) void attn_fwd_f8_kernel(const float* __res
     const int buf = t & 1;
     const int64_t k0 = (int64_t)t * KT;
     if (t + 1 < ntiles) {
-      load8(kb, sk.l, k0 + KT + skey, Lk, sc, ka, kb4);
-      load8(vb, sv.l, k0 + KT + skey, Lk, sc, va, vb4);
+#pragma unroll
+      for (int hf = 0; hf < NH; ++hf) {
+        load8(kb + 64 * hf, sk.l, k0 + KT + skey, Lk, sc, ka[hf], kb4[hf]);
+        load8(vb + 64 * hf, sv.l, k0 + KT + skey, Lk, sc, va[hf], vb4[hf]);
+      }
     }
     const unsigned char* Kt = Ks[buf];
     const float* ksc = Kscale[buf];
     const unsigned short* Vt = Vs[buf];
 
-    // ---- S^T = K' Q'^T, one MX-rate MFMA per 32-key block, then the per-key scale
+    // ---- S^T = K' Q'^T, one MX-rate MFMA per 32-key block and half, then the per-key scale
     f32x16 sacc[2];
 #pragma unroll
     for (int kb2 = 0; kb2 < 2; ++kb2) {
       const int key = 32 * kb2 + j;
-      const uint4 a0 = *reinterpret_cast<const uint4*>(Kt + key * 64 + 16 * ((2 * hi) ^ k8swz(key)));
-      const uint4 a1 = *reinterpret_cast<const uint4*>(Kt + key * 64 + 16 * ((2 * hi + 1) ^ k8swz(key)));
-      const v8i32 a = {(int)a0.x, (int)a0.y, (int)a0.z, (int)a0.w, (int)a1.x, (int)a1.y, (int)a1.z, (int)a1.w};
-      f32x16 z;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) z[r] = 0.f;
-      sacc[kb2] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, qf, z, 0, 0, 0, 0, 0, 0);
+      for (int r = 0; r < 16; ++r) sacc[kb2][r] = 0.f;
+#pragma unroll
+      for (int hf = 0; hf < NH; ++hf) {
+        const unsigned char* row = Kt + hf * KT * 64 + key * 64;
+        const uint4 a0 = *reinterpret_cast<const uint4*>(row + 16 * ((2 * hi) ^ k8swz(key)));
+        const uint4 a1 = *reinterpret_cast<const uint4*>(row + 16 * ((2 * hi + 1) ^ k8swz(key)));
+        const v8i32 a = {(int)a0.x, (int)a0.y, (int)a0.z, (int)a0.w, (int)a1.x, (int)a1.y, (int)a1.z, (int)a1.w};
+        sacc[kb2] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, qf[hf], sacc[kb2], 0, 0, 0, 0, 0, 0);
+      }
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {  // keys 32 kb2 + 8 g4 + 4 hi + (0..3)
         const float4 s4 = *reinterpret_cast<const float4*>(ksc + 32 * kb2 + 8 * g4 + 4 * hi);
@@ -219,7 +248,7 @@ __global__ __launch_bounds__(NTHR, 1) void attn_fwd_f8_kernel(const float* __res
       if (up) m = tmax;
       l *= alpha;
 #pragma unroll
-      for (int d = 0; d < 2; ++d)
+      for (int d = 0; d < HD / 32; ++d)
 #pragma unroll
         for (int r = 0; r < 16; ++r) oacc[d][r] *= alpha;
     }
@@ -249,13 +278,14 @@ __global__ __launch_bounds__(NTHR, 1) void attn_fwd_f8_kernel(const float* __res
       for (int s2 = 0; s2 < 2; ++s2) {
         const int kbase = 32 * kb2 + 16 * s2 + 4 * (g >> 1);
 #pragma unroll
-        for (int d = 0; d < 2; ++d) {
-          const int col = 32 * d + 16 * (g & 1) + tcol;
+        for (int d = 0; d < HD / 32; ++d) {
+          const unsigned short* Vh = Vt + (d >> 1) * KT * 64;
+          const int col = 32 * (d & 1) + 16 * (g & 1) + tcol;
           const int key1 = kbase + trow, key2 = kbase + 8 + trow;
           const v4i16 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_v4i16*)(Vt + key1 * 64 + 8 * ((col >> 3) ^ vswz(key1)) + (col & 7)));
+              (lds_v4i16*)(Vh + key1 * 64 + 8 * ((col >> 3) ^ vswz(key1)) + (col & 7)));
           const v4i16 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_v4i16*)(Vt + key2 * 64 + 8 * ((col >> 3) ^ vswz(key2)) + (col & 7)));
+              (lds_v4i16*)(Vh + key2 * 64 + 8 * ((col >> 3) ^ vswz(key2)) + (col & 7)));
           typedef short v8i16 __attribute__((ext_vector_type(8)));
           const v8i16 a8 = {t1[0], t1[1], t1[2], t1[3], t2[0], t2[1], t2[2], t2[3]};
           oacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a8), pb[kb2][s2], oacc[d],
@@ -264,8 +294,9 @@ __global__ __launch_bounds__(NTHR, 1) void attn_fwd_f8_kernel(const float* __res
       }
 
     if (t + 1 < ntiles) {
-      store_k8(Ks[buf ^ 1], Kscale[buf ^ 1], skey, sc, ka, kb4);
-      store_v(Vs[buf ^ 1], skey, sc ^ vswz(skey), va, vb4);
+      store_k8<NH>(Ks[buf ^ 1], Kscale[buf ^ 1], skey, sc, ka, kb4);
+#pragma unroll
+      for (int hf = 0; hf < NH; ++hf) store_v(Vs[buf ^ 1] + hf * KT * 64, skey, sc ^ vswz(skey), va[hf], vb4[hf]);
     }
     __syncthreads();
   }
@@ -275,10 +306,10 @@ __global__ __launch_bounds__(NTHR, 1) void attn_fwd_f8_kernel(const float* __res
     const float inv = 1.0f / lt;
     float* orow = o + b * so.b + h * so.h + qi * so.l;
 #pragma unroll
-    for (int d = 0; d < 2; ++d)
+    for (int d = 0; d < HD / 32; ++d)
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
-        const int dd = 32 * d + 8 * g4 + 4 * hi;
+        const int dd = 64 * (d >> 1) + 32 * (d & 1) + 8 * g4 + 4 * hi;
         *reinterpret_cast<float4*>(orow + dd) =
             make_float4(oacc[d][4 * g4] * inv, oacc[d][4 * g4 + 1] * inv, oacc[d][4 * g4 + 2] * inv,
                         oacc[d][4 * g4 + 3] * inv);
@@ -292,10 +323,13 @@ __global__ __launch_bounds__(NTHR, 1) void attn_fwd_f8_kernel(const float* __res
 // fp8-QK^T flash-attention forward; called by asrx_attn_fwd for prec == PREC_FP8ATT.
 int attn_fwd_f8(const float* q, const int64_t* sq, const float* k, const int64_t* sk, const float* v,
                 const int64_t* sv, float* o, const int64_t* so, float* lse, int64_t B, int64_t H, int64_t Lq,
-                int64_t Lk, int causal, float scale, hipStream_t stream) {
+                int64_t Lk, int64_t hd, int causal, float scale, hipStream_t stream) {
   dim3 g((unsigned)((Lq + af8::QB - 1) / af8::QB), (unsigned)H, (unsigned)B);
   AttnStridesMF Sq{sq[0], sq[1], sq[2]}, Sk{sk[0], sk[1], sk[2]}, Sv{sv[0], sv[1], sv[2]}, So{so[0], so[1], so[2]};
-  af8::attn_fwd_f8_kernel<<<g, af8::NTHR, 0, stream>>>(q, k, v, o, lse, Sq, Sk, Sv, So, H, Lq, Lk, causal, scale);
+  if (hd == 64)
+    af8::attn_fwd_f8_kernel<64><<<g, af8::NTHR, 0, stream>>>(q, k, v, o, lse, Sq, Sk, Sv, So, H, Lq, Lk, causal, scale);
+  else
+    af8::attn_fwd_f8_kernel<128><<<g, af8::NTHR, 0, stream>>>(q, k, v, o, lse, Sq, Sk, Sv, So, H, Lq, Lk, causal, scale);
   return 0;
 }
 

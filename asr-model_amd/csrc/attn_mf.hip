@@ -1,20 +1,25 @@
-// Flash-attention forward for the perf (bf16 MFMA) mode: F.scaled_dot_product_attention at
-// model.py:307, head dim 64, non-causal or causal (top-left), Lq != Lk, ragged tails; q/k/v/o fp32
-// (B, L, H, 64) with arbitrary strides, lse (B, H, Lq) natural log (consumed by the backward).
+// Flash attention for the perf (bf16 MFMA) mode: F.scaled_dot_product_attention at model.py:307,
+// head dim HD = 64 (tiny/small/medium configs) or 128 (the reference's own Dimensions(dims=512,
+// head=4), model.py:746), non-causal or causal (top-left), Lq != Lk, ragged tails; q/k/v/o fp32
+// (B, L, H, HD) with arbitrary strides, lse (B, H, Lq) natural log (consumed by the backward).
 //
-// Workgroup = 8 waves = 256 query rows of one (b, h); wave = 32 rows.  Per 64-key tile:
-//   S^T = K Q^T     8 x v_mfma_f32_32x32x16_bf16 (K rows from LDS, Q^T fragments held in registers)
+// Forward: workgroup = 8 waves = 256 query rows of one (b, h); wave = 32 rows.  Per 64-key tile:
+//   S^T = K Q^T     v_mfma_f32_32x32x16_bf16 (K rows from LDS, Q^T fragments held in registers)
 //                   -> each lane owns ONE query row (lane & 31) and 32 of the tile's 64 keys, so the
 //                   row max is 31 in-lane fmax + one xor-32 exchange, and l is a per-lane partial sum
 //   P^T = exp2(S^T * scale * log2e - m)   in registers, packed to bf16: the packed registers ARE the
 //                   B operand of the next product (no LDS round trip, no lane permutes)
-//   O^T += V^T P^T  8 x 32x32x16 MFMA, V^T fragments by ds_read_b64_tr_b16 (hardware transpose read
+//   O^T += V^T P^T  32x32x16 MFMA, V^T fragments by ds_read_b64_tr_b16 (hardware transpose read
 //                   of the row-major V tile), so O^T keeps the query on the lane too: the online-
 //                   softmax rescale and the final 1/l are lane-local
 // K/V tiles are register-staged (issue the next tile's global loads before the MFMAs, convert to
 // bf16 and write LDS after them), double-buffered, one barrier per tile.  LDS images are XOR-
 // swizzled at 16-byte granularity: K for the ds_read_b128 row reads, V for the transposed reads
 // (both bank-conflict-free under the gfx950 lane-group rules).
+//
+// HD = 128 keeps every tile as NH = HD/64 separate 64-wide "halves" with exactly the HD = 64 image
+// layout and swizzle, so one tile read pattern serves both head dims: the d-contractions run over
+// both halves, and O^T / dK^T / dV^T / dQ^T hold HD/32 accumulator blocks (block dd -> half dd/2).
 #include "common.h"
 
 namespace asrx {
@@ -28,9 +33,10 @@ typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
 
 namespace amf {
 
-constexpr int QB = 256;  // query rows per workgroup
+constexpr int QB = 256;  // query rows per forward workgroup
 constexpr int KT = 64;   // keys per tile
 constexpr int NTHR = 512;
+constexpr int HALF = KT * 64;  // elements of one 64-wide half tile
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
 
@@ -49,12 +55,12 @@ __device__ __forceinline__ bf16x8 pack8(const float (&v)[8]) {
   return __builtin_bit_cast(bf16x8, u);
 }
 
-// one 16-byte chunk (8 consecutive d) of one key row of a K or V tile: fp32 -> bf16 -> LDS.
-// Rows past Lk load the last row (always in bounds) and are zeroed, so there is no branch.
-__device__ __forceinline__ void stage_load(const float* base, AttnStridesMF st, int64_t key, int64_t Lk, int c,
-                                           float4& a, float4& b) {
+// one 16-byte chunk (8 consecutive d of half `hf`) of one key row of a K or V tile: fp32 -> bf16
+// -> LDS.  Rows past Lk load the last row (always in bounds) and are zeroed, so there is no branch.
+__device__ __forceinline__ void stage_load(const float* base, AttnStridesMF st, int64_t key, int64_t Lk, int hf,
+                                           int c, float4& a, float4& b) {
   const int64_t kc = key < Lk ? key : Lk - 1;
-  const float* p = base + kc * st.l + 8 * c;
+  const float* p = base + kc * st.l + 64 * hf + 8 * c;
   a = *reinterpret_cast<const float4*>(p);
   b = *reinterpret_cast<const float4*>(p + 4);
   if (key >= Lk) {
@@ -68,53 +74,106 @@ __device__ __forceinline__ void stage_store(unsigned short* tile, int key, int p
   *reinterpret_cast<u32x4*>(tile + key * 64 + 8 * pc) = u;
 }
 
+// A operand of X^T (d rows 32 dd.. of one 64-wide half, k = 16 rows of X in the MFMA-output order
+// of block kb2, half s2) from a transpose-swizzled [row][64] bf16 half tile (the V^T read)
+__device__ __forceinline__ bf16x8 tr_frag(const unsigned short* X, int lane, int kb2, int s2, int dd) {
+  const int g = lane >> 4, gi = lane & 15;
+  const int trow = gi >> 2, tcol = 4 * (gi & 3);
+  const int kbase = 32 * kb2 + 16 * s2 + 4 * (g >> 1);
+  const int col = 32 * dd + 16 * (g & 1) + tcol;
+  const int r1 = kbase + trow, r2 = kbase + 8 + trow;
+  const v4i16 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(X + r1 * 64 + 8 * ((col >> 3) ^ vswz(r1)) + (col & 7)));
+  const v4i16 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(X + r2 * 64 + 8 * ((col >> 3) ^ vswz(r2)) + (col & 7)));
+  typedef short v8i16 __attribute__((ext_vector_type(8)));
+  const v8i16 a8 = {t1[0], t1[1], t1[2], t1[3], t2[0], t2[1], t2[2], t2[3]};
+  return __builtin_bit_cast(bf16x8, a8);
+}
+
+// register fragments (B operand of a d-contraction): row `row` of X, f[s] = d 64 (s/4) + 16 (s%4)
+// + 8 hi .. +7, as bf16; rows past `rows` are zero
+template <int HD>
+__device__ __forceinline__ void row_frags(const float* base, int64_t stride_l, int64_t row, int64_t rows, int hi,
+                                          bf16x8 (&f)[HD / 16]) {
+#pragma unroll
+  for (int s = 0; s < HD / 16; ++s) {
+    float t[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (row < rows) {
+      const float* p = base + row * stride_l + 64 * (s >> 2) + 16 * (s & 3) + 8 * hi;
+      const float4 x = *reinterpret_cast<const float4*>(p), y = *reinterpret_cast<const float4*>(p + 4);
+      t[0] = x.x; t[1] = x.y; t[2] = x.z; t[3] = x.w; t[4] = y.x; t[5] = y.y; t[6] = y.z; t[7] = y.w;
+    }
+    f[s] = pack8(t);
+  }
+}
+
+// acc (32 rows of X from LDS x 32 register rows) += X[row 32 kb + j] . F over all HD dims
+template <int HD>
+__device__ __forceinline__ void dot_rows(f32x16& acc, const unsigned short* X, int row, int hi,
+                                         const bf16x8 (&f)[HD / 16]) {
+#pragma unroll
+  for (int hf = 0; hf < HD / 64; ++hf)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(X + hf * HALF + row * 64 + 8 * ((2 * s + hi) ^ kswz(row)));
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, f[4 * hf + s], acc, 0, 0, 0);
+    }
+}
+
+// store a (32 rows on the lane) x HD accumulator set scaled by `sc` to row `r` of Y
+template <int HD>
+__device__ __forceinline__ void store_rowT(float* yr, const f32x16 (&acc)[HD / 32], float sc, int hi) {
+#pragma unroll
+  for (int dd = 0; dd < HD / 32; ++dd)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int c = 64 * (dd >> 1) + 32 * (dd & 1) + 8 * g4 + 4 * hi;
+      *reinterpret_cast<float4*>(yr + c) =
+          make_float4(acc[dd][4 * g4] * sc, acc[dd][4 * g4 + 1] * sc, acc[dd][4 * g4 + 2] * sc, acc[dd][4 * g4 + 3] * sc);
+    }
+}
+
+template <int HD>
 __global__ __launch_bounds__(NTHR, 1) void attn_fwd_mf_kernel(const float* __restrict__ q, const float* __restrict__ k,
                                                               const float* __restrict__ v, float* __restrict__ o,
                                                               float* __restrict__ lse, AttnStridesMF sq,
                                                               AttnStridesMF sk, AttnStridesMF sv, AttnStridesMF so,
                                                               int64_t H, int64_t Lq, int64_t Lk, int causal,
                                                               float scale) {
-  __shared__ __attribute__((aligned(16))) unsigned short Ks[2][KT * 64];
-  __shared__ __attribute__((aligned(16))) unsigned short Vs[2][KT * 64];
+  constexpr int NH = HD / 64;
+  __shared__ __attribute__((aligned(16))) unsigned short Ks[2][NH * HALF];
+  __shared__ __attribute__((aligned(16))) unsigned short Vs[2][NH * HALF];
 
   const int b = blockIdx.z, h = blockIdx.y;
   const int64_t q0 = (int64_t)blockIdx.x * QB;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int j = lane & 31, hi = lane >> 5;
   const int64_t qi = q0 + wid * 32 + j;  // this lane's query row
-  const float* qb = q + b * sq.b + h * sq.h;
   const float* kb = k + b * sk.b + h * sk.h;
   const float* vb = v + b * sv.b + h * sv.h;
   const float c = scale * LOG2E;
 
-  // Q^T fragments (B operand): lane (q = j, hi) holds Q[q][16 s + 8 hi .. +7], s = 0..3
-  bf16x8 qf[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    float t[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (qi < Lq) {
-      const float* p = qb + qi * sq.l + 16 * s + 8 * hi;
-      const float4 x = *reinterpret_cast<const float4*>(p), y = *reinterpret_cast<const float4*>(p + 4);
-      t[0] = x.x; t[1] = x.y; t[2] = x.z; t[3] = x.w; t[4] = y.x; t[5] = y.y; t[6] = y.z; t[7] = y.w;
-    }
-    qf[s] = pack8(t);
-  }
+  // Q^T fragments (B operand): lane (q = j, hi) holds Q[q][64 hf + 16 s + 8 hi .. +7]
+  bf16x8 qf[HD / 16];
+  row_frags<HD>(q + b * sq.b + h * sq.h, sq.l, qi, Lq, hi, qf);
 
   int64_t kend = Lk;
   if (causal) kend = min(Lk, q0 + QB);
   const int ntiles = (int)((kend + KT - 1) / KT);
-  const int skey = tid >> 3, sc = tid & 7;  // staging: one 16-B chunk of one key row per thread
+  const int skey = tid >> 3, sc = tid & 7;  // staging: one 16-B chunk of each half of one key row
 
-  float4 ka, kb4, va, vb4;
-  stage_load(kb, sk, skey, Lk, sc, ka, kb4);
-  stage_load(vb, sv, skey, Lk, sc, va, vb4);
-  stage_store(Ks[0], skey, sc ^ kswz(skey), ka, kb4);
-  stage_store(Vs[0], skey, sc ^ vswz(skey), va, vb4);
+  float4 ka[NH], kb4[NH], va[NH], vb4[NH];
+#pragma unroll
+  for (int hf = 0; hf < NH; ++hf) {
+    stage_load(kb, sk, skey, Lk, hf, sc, ka[hf], kb4[hf]);
+    stage_load(vb, sv, skey, Lk, hf, sc, va[hf], vb4[hf]);
+    stage_store(Ks[0] + hf * HALF, skey, sc ^ kswz(skey), ka[hf], kb4[hf]);
+    stage_store(Vs[0] + hf * HALF, skey, sc ^ vswz(skey), va[hf], vb4[hf]);
+  }
   __syncthreads();
 
-  f32x16 oacc[2];
+  f32x16 oacc[HD / 32];
 #pragma unroll
-  for (int d = 0; d < 2; ++d)
+  for (int d = 0; d < HD / 32; ++d)
 #pragma unroll
     for (int r = 0; r < 16; ++r) oacc[d][r] = 0.f;
   float m = -INFINITY;  // running max of raw scores (log2 domain after * c)
@@ -124,8 +183,11 @@ __global__ __launch_bounds__(NTHR, 1) void attn_fwd_mf_kernel(const float* __res
     const int buf = t & 1;
     const int64_t k0 = (int64_t)t * KT;
     if (t + 1 < ntiles) {  // next tile's loads fly under this tile's MFMAs
-      stage_load(kb, sk, k0 + KT + skey, Lk, sc, ka, kb4);
-      stage_load(vb, sv, k0 + KT + skey, Lk, sc, va, vb4);
+#pragma unroll
+      for (int hf = 0; hf < NH; ++hf) {
+        stage_load(kb, sk, k0 + KT + skey, Lk, hf, sc, ka[hf], kb4[hf]);
+        stage_load(vb, sv, k0 + KT + skey, Lk, hf, sc, va[hf], vb4[hf]);
+      }
     }
     const unsigned short* Kt = Ks[buf];
     const unsigned short* Vt = Vs[buf];
@@ -136,12 +198,7 @@ __global__ __launch_bounds__(NTHR, 1) void attn_fwd_mf_kernel(const float* __res
     for (int kb2 = 0; kb2 < 2; ++kb2) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) sacc[kb2][r] = 0.f;
-      const int key = 32 * kb2 + j;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(Kt + key * 64 + 8 * ((2 * s + hi) ^ kswz(key)));
-        sacc[kb2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s], sacc[kb2], 0, 0, 0);
-      }
+      dot_rows<HD>(sacc[kb2], Kt, 32 * kb2 + j, hi, qf);
     }
 
     // ---- mask + online softmax (lane = query j, keys crow(r, hi) of each block)
@@ -169,7 +226,7 @@ __global__ __launch_bounds__(NTHR, 1) void attn_fwd_mf_kernel(const float* __res
       if (up) m = tmax;
       l *= alpha;
 #pragma unroll
-      for (int d = 0; d < 2; ++d)
+      for (int d = 0; d < HD / 32; ++d)
 #pragma unroll
         for (int r = 0; r < 16; ++r) oacc[d][r] *= alpha;
     }
@@ -191,31 +248,21 @@ __global__ __launch_bounds__(NTHR, 1) void attn_fwd_mf_kernel(const float* __res
     l += lsum;
 
     // ---- O^T += V^T P^T
-    const int g = lane >> 4, gi = lane & 15;
-    const int trow = gi >> 2, tcol = 4 * (gi & 3);
 #pragma unroll
     for (int kb2 = 0; kb2 < 2; ++kb2)
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const int kbase = 32 * kb2 + 16 * s2 + 4 * (g >> 1);
+      for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-        for (int d = 0; d < 2; ++d) {
-          const int col = 32 * d + 16 * (g & 1) + tcol;
-          const int key1 = kbase + trow, key2 = kbase + 8 + trow;
-          const v4i16 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_v4i16*)(Vt + key1 * 64 + 8 * ((col >> 3) ^ vswz(key1)) + (col & 7)));
-          const v4i16 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_v4i16*)(Vt + key2 * 64 + 8 * ((col >> 3) ^ vswz(key2)) + (col & 7)));
-          typedef short v8i16 __attribute__((ext_vector_type(8)));
-          const v8i16 a8 = {t1[0], t1[1], t1[2], t1[3], t2[0], t2[1], t2[2], t2[3]};
-          oacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a8), pb[kb2][s2], oacc[d],
-                                                              0, 0, 0);
-        }
-      }
+        for (int d = 0; d < HD / 32; ++d)
+          oacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Vt + (d >> 1) * HALF, lane, kb2, s2, d & 1),
+                                                            pb[kb2][s2], oacc[d], 0, 0, 0);
 
     if (t + 1 < ntiles) {  // every wave finished reading buf^1 (tile t-1) before the last barrier
-      stage_store(Ks[buf ^ 1], skey, sc ^ kswz(skey), ka, kb4);
-      stage_store(Vs[buf ^ 1], skey, sc ^ vswz(skey), va, vb4);
+#pragma unroll
+      for (int hf = 0; hf < NH; ++hf) {
+        stage_store(Ks[buf ^ 1] + hf * HALF, skey, sc ^ kswz(skey), ka[hf], kb4[hf]);
+        stage_store(Vs[buf ^ 1] + hf * HALF, skey, sc ^ vswz(skey), va[hf], vb4[hf]);
+      }
     }
     __syncthreads();
   }
@@ -223,17 +270,7 @@ __global__ __launch_bounds__(NTHR, 1) void attn_fwd_mf_kernel(const float* __res
   // ---- finalize: l over both halves, O = O^T / l, lse in natural log
   const float lt = l + __shfl_xor(l, 32);
   if (qi < Lq) {
-    const float inv = 1.0f / lt;
-    float* orow = o + b * so.b + h * so.h + qi * so.l;
-#pragma unroll
-    for (int d = 0; d < 2; ++d)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int dd = 32 * d + 8 * g4 + 4 * hi;
-        *reinterpret_cast<float4*>(orow + dd) =
-            make_float4(oacc[d][4 * g4] * inv, oacc[d][4 * g4 + 1] * inv, oacc[d][4 * g4 + 2] * inv,
-                        oacc[d][4 * g4 + 3] * inv);
-      }
+    store_rowT<HD>(o + b * so.b + h * so.h + qi * so.l, oacc, 1.0f / lt, hi);
     if (hi == 0) lse[((int64_t)b * H + h) * Lq + qi] = (m * c + __builtin_amdgcn_logf(lt)) * LN2;
   }
 }
@@ -248,118 +285,98 @@ __global__ __launch_bounds__(NTHR, 1) void attn_fwd_mf_kernel(const float* __res
 //     the lane.  Q and dO tiles are staged twice: row-read and transpose-read swizzles.
 //   dq kernel (query-major, lane = query, the forward's layout): S^T = K Q^T, dP^T = V dO^T with
 //     Q^T / dO^T fragments in registers, dS^T packed into the B operand of dQ^T += K^T dS^T.
-// No atomics; every accumulator is written once.
+// No atomics; every accumulator is written once.  HD = 128 runs 4 waves per workgroup (one wave
+// per SIMD: its K/V fragments and four accumulator blocks need more than the 256 registers a
+// wave gets at two waves per SIMD); HD = 64 runs 8.
 
-// one 16-byte chunk of a [row][64] bf16 tile, stored under both swizzles (row reads / tr reads)
-__device__ __forceinline__ void stage_store2(unsigned short* tr_rows, unsigned short* tr_t, int row, int c,
-                                             const float4& a, const float4& b) {
-  stage_store(tr_rows, row, c ^ kswz(row), a, b);
-  stage_store(tr_t, row, c ^ vswz(row), a, b);
-}
+template <int HD>
+struct BwdCfg {
+  static constexpr int NW = HD == 64 ? 8 : 4;
+  static constexpr int NT = 64 * NW;
+  static constexpr int RI = KT * 8 / NT;  // staging row iterations (a thread stages chunk tid&7 of rows tid/8 + i NT/8)
+};
 
-// A operand of X^T (d rows 32 dd.., k = 16 rows of X in the MFMA-output order of block kb2, half
-// s2) from a transpose-swizzled [row][64] bf16 tile: the forward's V^T read, generalised
-__device__ __forceinline__ bf16x8 tr_frag(const unsigned short* X, int lane, int kb2, int s2, int dd) {
-  const int g = lane >> 4, gi = lane & 15;
-  const int trow = gi >> 2, tcol = 4 * (gi & 3);
-  const int kbase = 32 * kb2 + 16 * s2 + 4 * (g >> 1);
-  const int col = 32 * dd + 16 * (g & 1) + tcol;
-  const int r1 = kbase + trow, r2 = kbase + 8 + trow;
-  const v4i16 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(X + r1 * 64 + 8 * ((col >> 3) ^ vswz(r1)) + (col & 7)));
-  const v4i16 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(X + r2 * 64 + 8 * ((col >> 3) ^ vswz(r2)) + (col & 7)));
-  typedef short v8i16 __attribute__((ext_vector_type(8)));
-  const v8i16 a8 = {t1[0], t1[1], t1[2], t1[3], t2[0], t2[1], t2[2], t2[3]};
-  return __builtin_bit_cast(bf16x8, a8);
-}
+constexpr int BQT = 64;  // queries per tile of the dkdv loop
 
-// register fragment (B operand of a d-contraction): row `row` of X, d = 16 s + 8 hi .. +7, as bf16
-__device__ __forceinline__ void row_frags(const float* base, int64_t stride_l, int64_t row, int64_t rows, int hi,
-                                          bf16x8 (&f)[4]) {
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    float t[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (row < rows) {
-      const float* p = base + row * stride_l + 16 * s + 8 * hi;
-      const float4 x = *reinterpret_cast<const float4*>(p), y = *reinterpret_cast<const float4*>(p + 4);
-      t[0] = x.x; t[1] = x.y; t[2] = x.z; t[3] = x.w; t[4] = y.x; t[5] = y.y; t[6] = y.z; t[7] = y.w;
-    }
-    f[s] = pack8(t);
-  }
-}
-
-constexpr int BQT = 64;   // queries per tile of the dkdv loop
-constexpr int BKB = 256;  // keys per dkdv workgroup (8 waves x 32)
-
-__global__ __launch_bounds__(NTHR, 1) void attn_bwd_dkdv_mf_kernel(
+template <int HD>
+__global__ __launch_bounds__(BwdCfg<HD>::NT, 1) void attn_bwd_dkdv_mf_kernel(
     const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v,
     const float* __restrict__ dO, const float* __restrict__ lse, const float* __restrict__ delta,
     float* __restrict__ dk, float* __restrict__ dv, AttnStridesMF sq, AttnStridesMF sk, AttnStridesMF sv,
     AttnStridesMF sd, AttnStridesMF sdk, AttnStridesMF sdv, int64_t H, int64_t Lq, int64_t Lk, int causal,
     float scale) {
-  __shared__ __attribute__((aligned(16))) unsigned short Qr[2][BQT * 64], Qt[2][BQT * 64];
-  __shared__ __attribute__((aligned(16))) unsigned short Dr[2][BQT * 64], Dt[2][BQT * 64];
+  typedef BwdCfg<HD> C;
+  constexpr int NH = HD / 64;
+  __shared__ __attribute__((aligned(16))) unsigned short Qr[2][NH * HALF], Qt[2][NH * HALF];
+  __shared__ __attribute__((aligned(16))) unsigned short Dr[2][NH * HALF], Dt[2][NH * HALF];
   __shared__ __attribute__((aligned(16))) float2 LD[2][BQT];  // (lse * log2e or +inf past Lq, Delta)
 
   const int b = blockIdx.z, h = blockIdx.y;
-  const int64_t k0 = (int64_t)blockIdx.x * BKB;
+  const int64_t k0 = (int64_t)blockIdx.x * (32 * C::NW);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int j = lane & 31, hi = lane >> 5;
   const int64_t key = k0 + wid * 32 + j;  // this lane's key
   const float* qb = q + b * sq.b + h * sq.h;
-  const float* kbp = k + b * sk.b + h * sk.h;
-  const float* vbp = v + b * sv.b + h * sv.h;
   const float* gb = dO + b * sd.b + h * sd.h;
   const float* lb = lse + ((int64_t)b * H + h) * Lq;
   const float* db = delta + ((int64_t)b * H + h) * Lq;
   const float c = scale * LOG2E;
 
-  bf16x8 kf[4], vf[4];
-  row_frags(kbp, sk.l, key, Lk, hi, kf);
-  row_frags(vbp, sv.l, key, Lk, hi, vf);
+  bf16x8 kf[HD / 16], vf[HD / 16];
+  row_frags<HD>(k + b * sk.b + h * sk.h, sk.l, key, Lk, hi, kf);
+  row_frags<HD>(v + b * sv.b + h * sv.h, sv.l, key, Lk, hi, vf);
 
   const int64_t qt0 = causal ? k0 / BQT : 0;  // causal: tiles entirely before the block's keys are masked
   const int ntiles = (int)((Lq + BQT - 1) / BQT - qt0);
   const int srow = tid >> 3, sc = tid & 7;
-  auto stage_ld = [&](int t, float4& qa, float4& qb4, float4& ga, float4& gb4, float2& ld) {
+  float4 qa[C::RI][NH], qb4[C::RI][NH], ga[C::RI][NH], gb4[C::RI][NH];
+  float2 ld = make_float2(0.f, 0.f);
+  auto stage_ld = [&](int t) {
     const int64_t q0 = (qt0 + t) * BQT;
-    stage_load(qb, sq, q0 + srow, Lq, sc, qa, qb4);
-    stage_load(gb, sd, q0 + srow, Lq, sc, ga, gb4);
+#pragma unroll
+    for (int i = 0; i < C::RI; ++i)
+#pragma unroll
+      for (int hf = 0; hf < NH; ++hf) {
+        stage_load(qb, sq, q0 + srow + i * (C::NT / 8), Lq, hf, sc, qa[i][hf], qb4[i][hf]);
+        stage_load(gb, sd, q0 + srow + i * (C::NT / 8), Lq, hf, sc, ga[i][hf], gb4[i][hf]);
+      }
     if (tid < BQT) {
       const int64_t qi = q0 + tid;
       ld = qi < Lq ? make_float2(lb[qi] * LOG2E, db[qi]) : make_float2(INFINITY, 0.f);
     }
   };
-  auto stage_st = [&](int buf, const float4& qa, const float4& qb4, const float4& ga, const float4& gb4,
-                      const float2& ld) {
-    stage_store2(Qr[buf], Qt[buf], srow, sc, qa, qb4);
-    stage_store2(Dr[buf], Dt[buf], srow, sc, ga, gb4);
+  auto stage_st = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < C::RI; ++i)
+#pragma unroll
+      for (int hf = 0; hf < NH; ++hf) {
+        const int row = srow + i * (C::NT / 8);
+        stage_store(Qr[buf] + hf * HALF, row, sc ^ kswz(row), qa[i][hf], qb4[i][hf]);
+        stage_store(Qt[buf] + hf * HALF, row, sc ^ vswz(row), qa[i][hf], qb4[i][hf]);
+        stage_store(Dr[buf] + hf * HALF, row, sc ^ kswz(row), ga[i][hf], gb4[i][hf]);
+        stage_store(Dt[buf] + hf * HALF, row, sc ^ vswz(row), ga[i][hf], gb4[i][hf]);
+      }
     if (tid < BQT) LD[buf][tid] = ld;
   };
 
-  f32x16 dvacc[2], dkacc[2];
+  f32x16 dvacc[HD / 32], dkacc[HD / 32];
 #pragma unroll
-  for (int d = 0; d < 2; ++d)
+  for (int d = 0; d < HD / 32; ++d)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       dvacc[d][r] = 0.f;
       dkacc[d][r] = 0.f;
     }
-  float4 qa, qb4, ga, gb4;
-  float2 ld = make_float2(0.f, 0.f);
   if (ntiles > 0) {
-    stage_ld(0, qa, qb4, ga, gb4, ld);
-    stage_st(0, qa, qb4, ga, gb4, ld);
+    stage_ld(0);
+    stage_st(0);
   }
   __syncthreads();
 
   for (int t = 0; t < ntiles; ++t) {
     const int buf = t & 1;
     const int64_t q0 = (qt0 + t) * BQT;
-    if (t + 1 < ntiles) stage_ld(t + 1, qa, qb4, ga, gb4, ld);
-    const unsigned short* Qrt = Qr[buf];
-    const unsigned short* Drt = Dr[buf];
-    const unsigned short* Dtt = Dt[buf];
-    const unsigned short* Qtt = Qt[buf];
+    if (t + 1 < ntiles) stage_ld(t + 1);
     const bool need_mask = causal && q0 < k0 + wid * 32 + 32;
     // one 32-query half at a time (keeps S / dP / P / dS of a single half live)
 #pragma unroll
@@ -371,14 +388,8 @@ __global__ __launch_bounds__(NTHR, 1) void attn_bwd_dkdv_mf_kernel(
         sacc[r] = 0.f;
         pacc[r] = 0.f;
       }
-      const int qr = 32 * qb2 + j;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(Qrt + qr * 64 + 8 * ((2 * s + hi) ^ kswz(qr)));
-        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, kf[s], sacc, 0, 0, 0);
-        const bf16x8 g = *reinterpret_cast<const bf16x8*>(Drt + qr * 64 + 8 * ((2 * s + hi) ^ kswz(qr)));
-        pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(g, vf[s], pacc, 0, 0, 0);
-      }
+      dot_rows<HD>(sacc, Qr[buf], 32 * qb2 + j, hi, kf);
+      dot_rows<HD>(pacc, Dr[buf], 32 * qb2 + j, hi, vf);
       // ---- P, dS (query row of register r: 32 qb2 + (r & 3) + 8 (r >> 2) + 4 hi)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
@@ -401,41 +412,36 @@ __global__ __launch_bounds__(NTHR, 1) void attn_bwd_dkdv_mf_kernel(
         const bf16x8 pb = pack8(pv), sb = pack8(dsv);
         // ---- dV^T += dO^T P, dK^T += Q^T dS  (lane = key)
 #pragma unroll
-        for (int d = 0; d < 2; ++d) {
-          dvacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Dtt, lane, qb2, s2, d), pb, dvacc[d], 0, 0, 0);
-          dkacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Qtt, lane, qb2, s2, d), sb, dkacc[d], 0, 0, 0);
+        for (int d = 0; d < HD / 32; ++d) {
+          dvacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Dt[buf] + (d >> 1) * HALF, lane, qb2, s2, d & 1),
+                                                             pb, dvacc[d], 0, 0, 0);
+          dkacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Qt[buf] + (d >> 1) * HALF, lane, qb2, s2, d & 1),
+                                                             sb, dkacc[d], 0, 0, 0);
         }
       }
     }
-    if (t + 1 < ntiles) stage_st(buf ^ 1, qa, qb4, ga, gb4, ld);
+    if (t + 1 < ntiles) stage_st(buf ^ 1);
     __syncthreads();
   }
 
   if (key < Lk) {
-    float* dkr = dk + b * sdk.b + h * sdk.h + key * sdk.l;
-    float* dvr = dv + b * sdv.b + h * sdv.h + key * sdv.l;
-#pragma unroll
-    for (int d = 0; d < 2; ++d)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int dd = 32 * d + 8 * g4 + 4 * hi;
-        *reinterpret_cast<float4*>(dkr + dd) = make_float4(dkacc[d][4 * g4] * scale, dkacc[d][4 * g4 + 1] * scale,
-                                                           dkacc[d][4 * g4 + 2] * scale, dkacc[d][4 * g4 + 3] * scale);
-        *reinterpret_cast<float4*>(dvr + dd) =
-            make_float4(dvacc[d][4 * g4], dvacc[d][4 * g4 + 1], dvacc[d][4 * g4 + 2], dvacc[d][4 * g4 + 3]);
-      }
+    store_rowT<HD>(dk + b * sdk.b + h * sdk.h + key * sdk.l, dkacc, scale, hi);
+    store_rowT<HD>(dv + b * sdv.b + h * sdv.h + key * sdv.l, dvacc, 1.f, hi);
   }
 }
 
-__global__ __launch_bounds__(NTHR, 1) void attn_bwd_dq_mf_kernel(
+template <int HD>
+__global__ __launch_bounds__(BwdCfg<HD>::NT, 1) void attn_bwd_dq_mf_kernel(
     const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v,
     const float* __restrict__ dO, const float* __restrict__ lse, const float* __restrict__ delta,
     float* __restrict__ dq, AttnStridesMF sq, AttnStridesMF sk, AttnStridesMF sv, AttnStridesMF sd,
     AttnStridesMF sdq, int64_t H, int64_t Lq, int64_t Lk, int causal, float scale) {
-  __shared__ __attribute__((aligned(16))) unsigned short Kr[2][KT * 64], Kt2[2][KT * 64], Vr[2][KT * 64];
+  typedef BwdCfg<HD> C;
+  constexpr int NH = HD / 64;
+  __shared__ __attribute__((aligned(16))) unsigned short Kr[2][NH * HALF], Kt2[2][NH * HALF], Vr[2][NH * HALF];
 
   const int b = blockIdx.z, h = blockIdx.y;
-  const int64_t q0 = (int64_t)blockIdx.x * QB;
+  const int64_t q0 = (int64_t)blockIdx.x * (32 * C::NW);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int j = lane & 31, hi = lane >> 5;
   const int64_t qi = q0 + wid * 32 + j;  // this lane's query row
@@ -443,39 +449,52 @@ __global__ __launch_bounds__(NTHR, 1) void attn_bwd_dq_mf_kernel(
   const float* vbp = v + b * sv.b + h * sv.h;
   const float c = scale * LOG2E;
 
-  bf16x8 qf[4], gf[4];
-  row_frags(q + b * sq.b + h * sq.h, sq.l, qi, Lq, hi, qf);
-  row_frags(dO + b * sd.b + h * sd.h, sd.l, qi, Lq, hi, gf);
+  bf16x8 qf[HD / 16], gf[HD / 16];
+  row_frags<HD>(q + b * sq.b + h * sq.h, sq.l, qi, Lq, hi, qf);
+  row_frags<HD>(dO + b * sd.b + h * sd.h, sd.l, qi, Lq, hi, gf);
   const float l2 = qi < Lq ? lse[((int64_t)b * H + h) * Lq + qi] * LOG2E : 0.f;
   const float dl = qi < Lq ? delta[((int64_t)b * H + h) * Lq + qi] : 0.f;
 
   int64_t kend = Lk;
-  if (causal) kend = min(Lk, q0 + QB);
+  if (causal) kend = min(Lk, q0 + 32 * C::NW);
   const int ntiles = (int)((kend + KT - 1) / KT);
   const int skey = tid >> 3, sc = tid & 7;
 
-  float4 ka, kb4, va, vb4;
-  stage_load(kbp, sk, skey, Lk, sc, ka, kb4);
-  stage_load(vbp, sv, skey, Lk, sc, va, vb4);
-  stage_store2(Kr[0], Kt2[0], skey, sc, ka, kb4);
-  stage_store(Vr[0], skey, sc ^ kswz(skey), va, vb4);
+  float4 ka[C::RI][NH], kb4[C::RI][NH], va[C::RI][NH], vb4[C::RI][NH];
+  auto stage_ld = [&](int64_t k0) {
+#pragma unroll
+    for (int i = 0; i < C::RI; ++i)
+#pragma unroll
+      for (int hf = 0; hf < NH; ++hf) {
+        stage_load(kbp, sk, k0 + skey + i * (C::NT / 8), Lk, hf, sc, ka[i][hf], kb4[i][hf]);
+        stage_load(vbp, sv, k0 + skey + i * (C::NT / 8), Lk, hf, sc, va[i][hf], vb4[i][hf]);
+      }
+  };
+  auto stage_st = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < C::RI; ++i)
+#pragma unroll
+      for (int hf = 0; hf < NH; ++hf) {
+        const int row = skey + i * (C::NT / 8);
+        stage_store(Kr[buf] + hf * HALF, row, sc ^ kswz(row), ka[i][hf], kb4[i][hf]);
+        stage_store(Kt2[buf] + hf * HALF, row, sc ^ vswz(row), ka[i][hf], kb4[i][hf]);
+        stage_store(Vr[buf] + hf * HALF, row, sc ^ kswz(row), va[i][hf], vb4[i][hf]);
+      }
+  };
+  stage_ld(0);
+  stage_st(0);
   __syncthreads();
 
-  f32x16 dqacc[2];
+  f32x16 dqacc[HD / 32];
 #pragma unroll
-  for (int d = 0; d < 2; ++d)
+  for (int d = 0; d < HD / 32; ++d)
 #pragma unroll
     for (int r = 0; r < 16; ++r) dqacc[d][r] = 0.f;
 
   for (int t = 0; t < ntiles; ++t) {
     const int buf = t & 1;
     const int64_t k0 = (int64_t)t * KT;
-    if (t + 1 < ntiles) {
-      stage_load(kbp, sk, k0 + KT + skey, Lk, sc, ka, kb4);
-      stage_load(vbp, sv, k0 + KT + skey, Lk, sc, va, vb4);
-    }
-    const unsigned short* Krt = Kr[buf];
-    const unsigned short* Vrt = Vr[buf];
+    if (t + 1 < ntiles) stage_ld(k0 + KT);
     f32x16 sacc[2], pacc[2];
 #pragma unroll
     for (int kb2 = 0; kb2 < 2; ++kb2) {
@@ -484,14 +503,8 @@ __global__ __launch_bounds__(NTHR, 1) void attn_bwd_dq_mf_kernel(
         sacc[kb2][r] = 0.f;
         pacc[kb2][r] = 0.f;
       }
-      const int kr = 32 * kb2 + j;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(Krt + kr * 64 + 8 * ((2 * s + hi) ^ kswz(kr)));
-        sacc[kb2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s], sacc[kb2], 0, 0, 0);
-        const bf16x8 vv = *reinterpret_cast<const bf16x8*>(Vrt + kr * 64 + 8 * ((2 * s + hi) ^ kswz(kr)));
-        pacc[kb2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vv, gf[s], pacc[kb2], 0, 0, 0);
-      }
+      dot_rows<HD>(sacc[kb2], Kr[buf], 32 * kb2 + j, hi, qf);
+      dot_rows<HD>(pacc[kb2], Vr[buf], 32 * kb2 + j, hi, gf);
     }
     const bool need_mask = (k0 + KT > Lk) || (causal && k0 + KT - 1 > q0 + wid * 32);
     bf16x8 sb[2][2];
@@ -512,33 +525,19 @@ __global__ __launch_bounds__(NTHR, 1) void attn_bwd_dq_mf_kernel(
         }
         sb[kb2][s2] = pack8(dsv);
       }
-    const unsigned short* Ktt = Kt2[buf];
 #pragma unroll
     for (int kb2 = 0; kb2 < 2; ++kb2)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-        for (int d = 0; d < 2; ++d)
-          dqacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Ktt, lane, kb2, s2, d), sb[kb2][s2], dqacc[d],
-                                                             0, 0, 0);
-    if (t + 1 < ntiles) {
-      stage_store2(Kr[buf ^ 1], Kt2[buf ^ 1], skey, sc, ka, kb4);
-      stage_store(Vr[buf ^ 1], skey, sc ^ kswz(skey), va, vb4);
-    }
+        for (int d = 0; d < HD / 32; ++d)
+          dqacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Kt2[buf] + (d >> 1) * HALF, lane, kb2, s2, d & 1),
+                                                             sb[kb2][s2], dqacc[d], 0, 0, 0);
+    if (t + 1 < ntiles) stage_st(buf ^ 1);
     __syncthreads();
   }
 
-  if (qi < Lq) {
-    float* dqr = dq + b * sdq.b + h * sdq.h + qi * sdq.l;
-#pragma unroll
-    for (int d = 0; d < 2; ++d)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int dd = 32 * d + 8 * g4 + 4 * hi;
-        *reinterpret_cast<float4*>(dqr + dd) = make_float4(dqacc[d][4 * g4] * scale, dqacc[d][4 * g4 + 1] * scale,
-                                                           dqacc[d][4 * g4 + 2] * scale, dqacc[d][4 * g4 + 3] * scale);
-      }
-  }
+  if (qi < Lq) store_rowT<HD>(dq + b * sdq.b + h * sdq.h + qi * sdq.l, dqacc, scale, hi);
 }
 
 }  // namespace amf
@@ -546,26 +545,45 @@ __global__ __launch_bounds__(NTHR, 1) void attn_bwd_dq_mf_kernel(
 // bf16 flash-attention forward (see header); called by asrx_attn_fwd for prec == PREC_BF16.
 int attn_fwd_mf(const float* q, const int64_t* sq, const float* k, const int64_t* sk, const float* v,
                 const int64_t* sv, float* o, const int64_t* so, float* lse, int64_t B, int64_t H, int64_t Lq,
-                int64_t Lk, int causal, float scale, hipStream_t stream) {
+                int64_t Lk, int64_t hd, int causal, float scale, hipStream_t stream) {
   dim3 g((unsigned)((Lq + amf::QB - 1) / amf::QB), (unsigned)H, (unsigned)B);
   AttnStridesMF Sq{sq[0], sq[1], sq[2]}, Sk{sk[0], sk[1], sk[2]}, Sv{sv[0], sv[1], sv[2]}, So{so[0], so[1], so[2]};
-  amf::attn_fwd_mf_kernel<<<g, amf::NTHR, 0, stream>>>(q, k, v, o, lse, Sq, Sk, Sv, So, H, Lq, Lk, causal, scale);
+  if (hd == 64)
+    amf::attn_fwd_mf_kernel<64><<<g, amf::NTHR, 0, stream>>>(q, k, v, o, lse, Sq, Sk, Sv, So, H, Lq, Lk, causal, scale);
+  else
+    amf::attn_fwd_mf_kernel<128><<<g, amf::NTHR, 0, stream>>>(q, k, v, o, lse, Sq, Sk, Sv, So, H, Lq, Lk, causal, scale);
   return 0;
+}
+
+template <int HD>
+static void attn_bwd_mf_t(const float* q, AttnStridesMF Sq, const float* k, AttnStridesMF Sk, const float* v,
+                          AttnStridesMF Sv, const float* dO, AttnStridesMF Sd, const float* lse, const float* delta,
+                          float* dq, AttnStridesMF Sdq, float* dk, AttnStridesMF Sdk, float* dv, AttnStridesMF Sdv,
+                          int64_t B, int64_t H, int64_t Lq, int64_t Lk, int causal, float scale, hipStream_t stream) {
+  typedef amf::BwdCfg<HD> C;
+  const int64_t rows_per_wg = 32 * C::NW;
+  dim3 gk((unsigned)((Lk + rows_per_wg - 1) / rows_per_wg), (unsigned)H, (unsigned)B);
+  amf::attn_bwd_dkdv_mf_kernel<HD><<<gk, C::NT, 0, stream>>>(q, k, v, dO, lse, delta, dk, dv, Sq, Sk, Sv, Sd, Sdk, Sdv,
+                                                             H, Lq, Lk, causal, scale);
+  dim3 gq((unsigned)((Lq + rows_per_wg - 1) / rows_per_wg), (unsigned)H, (unsigned)B);
+  amf::attn_bwd_dq_mf_kernel<HD><<<gq, C::NT, 0, stream>>>(q, k, v, dO, lse, delta, dq, Sq, Sk, Sv, Sd, Sdq, H, Lq, Lk,
+                                                           causal, scale);
 }
 
 // bf16 flash-attention backward (dkdv + dq kernels above); delta = rowsum(dO * O) already computed.
 int attn_bwd_mf(const float* q, const int64_t* sq, const float* k, const int64_t* sk, const float* v,
                 const int64_t* sv, const float* dO, const int64_t* sd, const float* lse, const float* delta,
                 float* dq, const int64_t* sdq, float* dk, const int64_t* sdk, float* dv, const int64_t* sdv,
-                int64_t B, int64_t H, int64_t Lq, int64_t Lk, int causal, float scale, hipStream_t stream) {
+                int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t hd, int causal, float scale,
+                hipStream_t stream) {
   AttnStridesMF Sq{sq[0], sq[1], sq[2]}, Sk{sk[0], sk[1], sk[2]}, Sv{sv[0], sv[1], sv[2]}, Sd{sd[0], sd[1], sd[2]};
   AttnStridesMF Sdq{sdq[0], sdq[1], sdq[2]}, Sdk{sdk[0], sdk[1], sdk[2]}, Sdv{sdv[0], sdv[1], sdv[2]};
-  dim3 gk((unsigned)((Lk + amf::BKB - 1) / amf::BKB), (unsigned)H, (unsigned)B);
-  amf::attn_bwd_dkdv_mf_kernel<<<gk, amf::NTHR, 0, stream>>>(q, k, v, dO, lse, delta, dk, dv, Sq, Sk, Sv, Sd, Sdk, Sdv,
-                                                            H, Lq, Lk, causal, scale);
-  dim3 gq((unsigned)((Lq + amf::QB - 1) / amf::QB), (unsigned)H, (unsigned)B);
-  amf::attn_bwd_dq_mf_kernel<<<gq, amf::NTHR, 0, stream>>>(q, k, v, dO, lse, delta, dq, Sq, Sk, Sv, Sd, Sdq, H, Lq, Lk,
-                                                          causal, scale);
+  if (hd == 64)
+    attn_bwd_mf_t<64>(q, Sq, k, Sk, v, Sv, dO, Sd, lse, delta, dq, Sdq, dk, Sdk, dv, Sdv, B, H, Lq, Lk, causal, scale,
+                      stream);
+  else
+    attn_bwd_mf_t<128>(q, Sq, k, Sk, v, Sv, dO, Sd, lse, delta, dq, Sdq, dk, Sdk, dv, Sdv, B, H, Lq, Lk, causal, scale,
+                       stream);
   return 0;
 }
 

@@ -85,13 +85,31 @@ def cpu_baseline(model, cfg_name, budget_s=10.0, max_clips=3):
                       f"batch 1, {t_total:.1f} s of CPU time"}
 
 
+def self_launch(n):
+    """`bench.py --gpus N` without a launcher: start N ranks with torch.distributed.run (one process per
+    GPU, rendezvous on 127.0.0.1) as a child and exit with its status.  Runs before anything touches
+    the GPU (this process never initialises HIP), so no exec or fork happens after GPU init."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(self_launch(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     if args.same_device:
         local = 0
     torch.cuda.set_device(local)

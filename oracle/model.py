@@ -354,8 +354,14 @@ def residual(P, i, x, cfg, noise, site, sids, xa=None, xa_site=None, xa_sids=Non
 
 
 def forward(P, cfg, text_ids, labels=None, spectrogram=None, pitch=None, waveform=None,
-            seed=0, step=0, training=True, dtype=torch.float64):
-    """Model.forward (model.py:654-672) + processor.forward (model.py:602-629), seq=False."""
+            seed=0, step=0, training=True, dtype=torch.float64, live_only=False, seq=False):
+    """Model.forward (model.py:654-672) + processor.forward (model.py:602-629).
+
+    live_only: evaluate only the last block.  processor.forward restarts every block from the
+    embedding `x` and only the last block's d / g reach the output (model.py:617-628), and the
+    noise of a block is addressed by its own site keys, so skipping blocks 0..L-2 leaves logits,
+    loss and every gradient unchanged (they only cost the reference compute and RNG draws).
+    seq: processor(..., seq=True) (model.py:624-626, the generate path): out = g, no blend."""
     P = {k: v.to(dtype) if v.is_floating_point() else v for k, v in P.items()}
     noise = Noise(seed, step, dtype)
     L = cfg["layer"]
@@ -372,7 +378,7 @@ def forward(P, cfg, text_ids, labels=None, spectrogram=None, pitch=None, wavefor
     sids = {s: [si * B + b for b in range(B)] for si, s in enumerate("abc")}
     T = text_ids.shape[1]
     x = P["processor.token.weight"][text_ids] + P["processor.position"][:T]
-    for i in range(L):
+    for i in (range(L - 1, L) if live_only else range(L)):
         a = residual(P, i, x, cfg, noise, f"b{i}.ta", sid_t, masked=True)
         A1 = residual(P, i, xa["a"], cfg, noise, f"b{i}.audio", sids["a"])
         b_ = residual(P, i, a, cfg, noise, f"b{i}.tb", sid_t, xa=A1, xa_site=f"b{i}.xa", xa_sids=sids["a"])
@@ -382,8 +388,11 @@ def forward(P, cfg, text_ids, labels=None, spectrogram=None, pitch=None, wavefor
         d = residual(P, i, c_, cfg, noise, f"b{i}.td", sid_t, xa=A3, xa_site=f"b{i}.xa", xa_sids=sids["c"])
         e = a + b_ + c_
         g = residual(P, i, d, cfg, noise, f"b{i}.tg", sid_t, xa=e, xa_site=f"b{i}.tg.xa", xa_sids=sid_t)
-    blend = torch.sigmoid(P["processor.blend"])
-    x = blend * d + (1 - blend) * g
+    if seq:
+        x = g
+    else:
+        blend = torch.sigmoid(P["processor.blend"])
+        x = blend * d + (1 - blend) * g
     x = abby_rows(P, "processor.ln", x, noise, "final.ln", sid_t)
     logits = x @ P["processor.token.weight"].t()
     loss = None

@@ -137,3 +137,100 @@ def test_gradsync_gloo_world2(bucket_mb, kind):
         assert launched == nb, (step, launched, nb)
     if bucket_mb < 0.01:
         assert out[0][0][-1][2] > 1  # tiny buckets -> several all-reduces
+
+
+class ToyVarying(torch.nn.Module):
+    """A shared weight used `passes` times per step (like asrx's encoder weights when the pitch track's
+    length differs from the spectrogram's): the gradient-event count depends on the step signature."""
+
+    def __init__(self):
+        super().__init__()
+        self.a = torch.nn.Linear(16, 16)
+        self.c = torch.nn.Linear(16, 4)
+        self.passes = 1
+        self.grad_signature = None
+
+    def forward(self, x):
+        self.grad_signature = ("passes", self.passes)
+        h = x
+        for _ in range(self.passes):
+            h = torch.tanh(_DirectLinear.apply(h, self.a.weight, self.a.bias))
+        return self.c(h)
+
+
+def _worker_varying(rank, world, port, q, sig_override):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "asr-model_amd")]
+    from asrx.dist import GradSync, broadcast_parameters
+
+    torch.manual_seed(rank)
+    model = ToyVarying()
+    broadcast_parameters(model)
+    sig = (lambda: "fixed") if sig_override else None
+    sync = GradSync(model, bucket_mb=0.0005, signature=sig)
+    out = []
+    err = None
+    try:
+        for step, passes in enumerate([1, 1, 3, 3, 1, 2, 3]):
+            model.passes = passes
+            sync.zero_grad()
+            x = torch.randn(5, 16, generator=torch.Generator().manual_seed(100 * step + rank))
+            (model(x).pow(2).sum() * (rank + 1)).backward()
+            overlapped = sum(int(b.launched) for b in sync.buckets or [])
+            sync.finish()
+            synced = {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None}
+            # the reference: the average of both ranks' local gradients of this step
+            local = {}
+            for r in range(world):
+                model.zero_grad(set_to_none=True)
+                saved = sync.buckets
+                xr = torch.randn(5, 16, generator=torch.Generator().manual_seed(100 * step + r))
+                sync.buckets, sync._overlap = saved, False
+                (model(xr).pow(2).sum() * (r + 1)).backward()
+                for n, p in model.named_parameters():
+                    local[n] = local.get(n, 0) + p.grad.clone() / world
+            ok = all(torch.allclose(synced[n], local[n], atol=1e-5) for n in synced)
+            out.append((passes, overlapped, ok))
+            sync.zero_grad()
+    except RuntimeError as e:
+        err = str(e)
+    q.put((rank, out, err))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("sig_override", [False, True])
+def test_gradsync_event_plans_per_signature(sig_override):
+    """GradSync learns gradient-event counts per step signature (asrx Model sets it from its stream
+    lengths): steps whose signature was seen before overlap their all-reduces with backward, new
+    signatures are reduced in finish(), and every step's synced gradient equals the average of the
+    ranks' local gradients.  With the signature pinned to a constant, a step that delivers more
+    events than the plan must raise instead of reducing a partial bucket."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_varying, args=(r, 2, port, q, sig_override)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r, out, err = q.get(timeout=120)
+        res[r] = (out, err)
+    for p in procs:
+        p.join(timeout=60)
+    out, err = res[0]
+    if not sig_override:
+        assert err is None, err
+        assert [o[0] for o in out] == [1, 1, 3, 3, 1, 2, 3]
+        assert all(o[2] for o in out), out
+        overlapped = [o[1] > 0 for o in out]
+        # first sight of a signature: no overlap; repeats: launched from the backward hooks
+        assert overlapped == [False, True, False, True, True, False, True], out
+    else:
+        assert err is not None and "partial" in err, (out, err)
+        assert [o[0] for o in out] == [1, 1]  # the first 3-pass step raised
+        assert all(o[2] for o in out)

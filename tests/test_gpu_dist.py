@@ -1,0 +1,111 @@
+"""Data parallelism through the real asrx Model: two ranks on cuda:0 over gloo (the
+one-GPU box cannot host two RCCL ranks on one device), GradSync driven by the HIP kernels' direct
+gradient events and autograd hooks.  Three steps with different stream groupings (the pitch track as
+long as the spectrogram -> one batched encoder pass; shorter -> a separate pass, so shared weights
+get a different number of gradient contributions) must each give both ranks the average of the two
+ranks' local gradients, and repeated signatures must overlap their all-reduces with backward."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _inputs(step, rank, B=2, S=101, T=8, V=500):
+    g = torch.Generator().manual_seed(1000 * step + rank)
+    Sp = S if step != 1 else S - 20  # step 1: a shorter pitch track -> different stream grouping
+    spec = torch.randn(B, 128, S, generator=g)
+    pitch = torch.rand(B, 1, Sp, generator=g) * 200
+    wav = torch.randn(B, 1, S - 1, generator=g) * 0.1
+    ids = torch.randint(3, V, (B, T), generator=g)
+    ids[:, 0] = 1
+    labels = torch.cat([ids[:, 1:], torch.full((B, 1), 2)], 1)
+    return spec, pitch, wav, ids, labels
+
+
+def _worker(rank, world, port, q, root):
+    import sys
+
+    sys.path[:0] = [root, os.path.join(root, "asr-model_amd")]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from asrx import prec
+    from asrx.config import Dimensions
+    from asrx.dist import GradSync, broadcast_parameters
+    from asrx.model import Model
+
+    dev = torch.device("cuda:0")
+    cfg = Dimensions(tokens=500, mels=128, dims=128, head=2, layer=2, act="gelu", n_type="AbbyNormal")
+    torch.manual_seed(rank)  # different init per rank: the broadcast must equalise them
+    model = Model(cfg).to(dev).train()
+    broadcast_parameters(model)
+    ref = Model(cfg).to(dev).train()  # local-gradient twin (no GradSync hooks)
+    ref.load_state_dict(model.state_dict())
+    sync = GradSync(model, bucket_mb=1.0)
+    out = []
+    with prec.precision("fp32"):
+        for step in (0, 1, 0, 1):
+            spec, pitch, wav, ids, labels = (t.to(dev) for t in _inputs(step, rank))
+            model.set_noise(11, step)
+            sync.zero_grad()
+            loss = model(labels=labels, text_ids=ids, spectrogram=spec, pitch=pitch, waveform=wav)["loss"]
+            loss.backward()
+            overlapped = sum(int(b.launched) for b in sync.buckets or [])
+            sync.finish()
+            torch.cuda.synchronize()
+            synced = {n: p.grad.detach().cpu().clone() for n, p in model.named_parameters() if p.grad is not None}
+            ref.zero_grad(set_to_none=True)
+            ref.set_noise(11, step)
+            ref(labels=labels, text_ids=ids, spectrogram=spec, pitch=pitch, waveform=wav)["loss"].backward()
+            local = {n: p.grad.detach().cpu().clone() for n, p in ref.named_parameters() if p.grad is not None}
+            avg = {}
+            for n in sorted(local):
+                t = local[n].clone()
+                dist.all_reduce(t)
+                avg[n] = t / world
+            err = max(float((synced[n] - avg[n]).abs().max() / avg[n].abs().max().clamp_min(1e-20)) for n in avg)
+            same_set = set(synced) == set(avg)
+            out.append((step, overlapped, len(sync.buckets), err, same_set, model.grad_signature))
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gradsync_asrx_model_two_ranks(cuda):
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, root)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r, out = q.get(timeout=240)
+        res[r] = out
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in (0, 1):
+        out = res[r]
+        print(r, out)
+        sigs = [o[5] for o in out]
+        assert sigs[0] != sigs[1] and sigs[0] == sigs[2] and sigs[1] == sigs[3]
+        for step, overlapped, nb, err, same_set, _ in out:
+            assert same_set
+            assert err < 1e-5, (r, step, err)
+        # first sight of each signature reduces in finish(); the repeats launch from backward
+        assert [o[1] > 0 for o in out] == [False, False, True, True], out

@@ -38,7 +38,7 @@ def _grads(fn_gpu, fn_ref, inputs, gout_seed=0):
     return yg, yr, [t.grad for t in g_in], [t.grad for t in r_in]
 
 
-@pytest.mark.parametrize("d,H", [(128, 1), (384, 1), (64, 3)])
+@pytest.mark.parametrize("d,H", [(128, 1), (384, 1), (64, 3), (128, 4), (512, 1)])
 def test_abby_normal(cuda, d, H):
     from asrx import ops
     from asrx.model import AbbyNormal
@@ -89,12 +89,15 @@ def test_layer_norm(cuda):
         assert _rel(a, c) < 1e-4
 
 
-@pytest.mark.parametrize("Lq,Lk,causal", [(101, 101, False), (8, 101, False), (70, 70, True), (130, 3, False),
-                                          (64, 64, True)])
-def test_attention(cuda, Lq, Lk, causal):
+@pytest.mark.parametrize("Lq,Lk,causal,hd", [(101, 101, False, 64), (8, 101, False, 64), (70, 70, True, 64),
+                                             (130, 3, False, 64), (64, 64, True, 64), (101, 101, False, 128),
+                                             (70, 70, True, 128), (8, 130, False, 128)])
+def test_attention(cuda, Lq, Lk, causal, hd):
+    """Exact-fp32 parity-mode attention (hd 64 and the reference config's hd 128, model.py:746)
+    against float64 softmax attention: output and q/k/v gradients."""
     from asrx import ops
 
-    B, H, hd = 2, 3, 64
+    B, H = 2, 3
     g = torch.Generator().manual_seed(Lq + Lk)
     q = torch.randn(B, Lq, H, hd, generator=g)
     k = torch.randn(B, Lk, H, hd, generator=g)
@@ -112,15 +115,16 @@ def test_attention(cuda, Lq, Lk, causal):
         assert _rel(a, b) < 1e-4
 
 
-@pytest.mark.parametrize("B,H,Lq,Lk,causal", [(1, 2, 300, 300, False), (2, 3, 600, 517, False),
-                                                (1, 2, 256, 256, True), (2, 1, 70, 70, True), (1, 2, 33, 3001, False),
-                                                (1, 1, 513, 64, False)])
-def test_attention_bf16(cuda, B, H, Lq, Lk, causal):
+@pytest.mark.parametrize("B,H,Lq,Lk,causal,hd", [(1, 2, 300, 300, False, 64), (2, 3, 600, 517, False, 64),
+                                                   (1, 2, 256, 256, True, 64), (2, 1, 70, 70, True, 64),
+                                                   (1, 2, 33, 3001, False, 64), (1, 1, 513, 64, False, 64),
+                                                   (2, 2, 300, 517, False, 128), (1, 2, 256, 256, True, 128),
+                                                   (1, 1, 33, 3001, False, 128)])
+def test_attention_bf16(cuda, B, H, Lq, Lk, causal, hd):
     """Perf-mode flash attention (32x32x16 bf16 MFMA, transposed-read V) against float64 softmax
-    attention on the same bf16-rounded q, k, v: output and log-sum-exp."""
+    attention on the same bf16-rounded q, k, v: output and log-sum-exp (hd 64 and 128)."""
     from asrx import lib, prec
 
-    hd = 64
     g = torch.Generator().manual_seed(Lq * 3 + Lk + causal)
     q, k, v = (torch.randn(B, L, H, hd, generator=g) for L in (Lq, Lk, Lk))
     o = torch.empty(B, Lq, H, hd, device=cuda)
@@ -133,9 +137,9 @@ def test_attention_bf16(cuda, B, H, Lq, Lk, causal):
         return (ctypes.c_int64 * 3)(*s)
 
     lib.call("asrx_attn_fwd", 1, lib.ptr(qg), st(qg), lib.ptr(kg), st(kg), lib.ptr(vg), st(vg), lib.ptr(o), st(o),
-             lib.ptr(lse), B, H, Lq, Lk, hd, int(causal), 1.0 / 8.0, lib.stream())
+             lib.ptr(lse), B, H, Lq, Lk, hd, int(causal), 1.0 / math.sqrt(hd), lib.stream())
     bq, bk, bv = (t.to(torch.bfloat16).double().transpose(1, 2) for t in (q, k, v))
-    s = bq @ bk.transpose(-1, -2) / 8.0
+    s = bq @ bk.transpose(-1, -2) / math.sqrt(hd)
     if causal:
         s = s.masked_fill(torch.ones(Lq, Lk, dtype=torch.bool).triu(1), float("-inf"))
     ref_lse = torch.logsumexp(s, -1)
@@ -144,17 +148,18 @@ def test_attention_bf16(cuda, B, H, Lq, Lk, causal):
     assert float((lse.cpu().double() - ref_lse).abs().max()) < 1e-3
 
 
-@pytest.mark.parametrize("B,H,Lq,Lk,causal", [(1, 2, 300, 300, False), (2, 3, 600, 517, False),
-                                                (1, 2, 256, 256, True), (2, 1, 70, 70, True), (1, 2, 33, 3001, False),
-                                                (1, 1, 513, 64, False), (1, 2, 700, 700, True)])
-def test_attention_bf16_backward(cuda, B, H, Lq, Lk, causal):
+@pytest.mark.parametrize("B,H,Lq,Lk,causal,hd", [(1, 2, 300, 300, False, 64), (2, 3, 600, 517, False, 64),
+                                                   (1, 2, 256, 256, True, 64), (2, 1, 70, 70, True, 64),
+                                                   (1, 2, 33, 3001, False, 64), (1, 1, 513, 64, False, 64),
+                                                   (1, 2, 700, 700, True, 64), (2, 2, 300, 517, False, 128),
+                                                   (1, 2, 700, 700, True, 128), (1, 1, 33, 3001, False, 128)])
+def test_attention_bf16_backward(cuda, B, H, Lq, Lk, causal, hd):
     """Perf-mode flash-attention backward (dkdv kernel with the key on the lane, dq kernel with the
     query on the lane, 32x32x16 bf16 MFMA) against float64 autograd of softmax attention on the
     same bf16-rounded q, k, v, dO.  P and dS are rounded to bf16 before their products, so the
     tolerance is the bf16 one (3e-2 of max |grad|)."""
     from asrx import ops, prec
 
-    hd = 64
     g = torch.Generator().manual_seed(Lq * 5 + Lk + causal)
     q, k, v = (torch.randn(B, L, H, hd, generator=g) for L in (Lq, Lk, Lk))
     dO = torch.randn(B, Lq, H, hd, generator=g)
@@ -346,10 +351,12 @@ def _e4m3_rows(t):
     return (t / s).to(torch.float8_e4m3fn).to(torch.float32) * s
 
 
-@pytest.mark.parametrize("B,H,Lq,Lk,causal", [(1, 2, 300, 300, False), (2, 3, 600, 517, False),
-                                                (1, 2, 256, 256, True), (2, 1, 70, 70, True), (1, 2, 33, 3001, False),
-                                                (1, 1, 513, 64, False), (2, 2, 1, 77, False)])
-def test_attention_fp8(cuda, B, H, Lq, Lk, causal):
+@pytest.mark.parametrize("B,H,Lq,Lk,causal,hd", [(1, 2, 300, 300, False, 64), (2, 3, 600, 517, False, 64),
+                                                   (1, 2, 256, 256, True, 64), (2, 1, 70, 70, True, 64),
+                                                   (1, 2, 33, 3001, False, 64), (1, 1, 513, 64, False, 64),
+                                                   (2, 2, 1, 77, False, 64), (2, 2, 300, 517, False, 128),
+                                                   (1, 2, 256, 256, True, 128), (2, 1, 1, 77, False, 128)])
+def test_attention_fp8(cuda, B, H, Lq, Lk, causal, hd):
     """fp8 attention mode (prec 2: e4m3 QK^T with per-row scales, bf16 P and V) against float64
     softmax attention on the same per-row e4m3-quantised q, k and bf16 v (tight: the kernel computes
     exactly that), and, on unit-variance inputs (scores of std ~1, as after the model's hd^-0.25 and
@@ -359,7 +366,7 @@ def test_attention_fp8(cuda, B, H, Lq, Lk, causal):
 
     from asrx import lib
 
-    hd = 64
+    sc = 1.0 / math.sqrt(hd)
     g = torch.Generator().manual_seed(Lq * 7 + Lk + causal)
 
     def st(t):
@@ -370,12 +377,12 @@ def test_attention_fp8(cuda, B, H, Lq, Lk, causal):
         lse = torch.empty(B, H, Lq, device=cuda)
         qg, kg, vg = q.to(cuda), k.to(cuda), v.to(cuda)
         lib.call("asrx_attn_fwd", 2, lib.ptr(qg), st(qg), lib.ptr(kg), st(kg), lib.ptr(vg), st(vg), lib.ptr(o),
-                 st(o), lib.ptr(lse), B, H, Lq, Lk, hd, int(causal), 1.0 / 8.0, lib.stream())
+                 st(o), lib.ptr(lse), B, H, Lq, Lk, hd, int(causal), sc, lib.stream())
         torch.cuda.synchronize()
         return o, lse
 
     def ref(qq, kk, vv):
-        s = qq.double().transpose(1, 2) @ kk.double().transpose(1, 2).transpose(-1, -2) / 8.0
+        s = qq.double().transpose(1, 2) @ kk.double().transpose(1, 2).transpose(-1, -2) * sc
         if causal:
             s = s.masked_fill(torch.ones(Lq, Lk, dtype=torch.bool).triu(1), float("-inf"))
         return (torch.softmax(s, -1) @ vv.double().transpose(1, 2)).transpose(1, 2), torch.logsumexp(s, -1)

@@ -63,7 +63,7 @@ def test_maxfactor_reference_groups_on_model(cuda):
     from asrx.optim import FAMScheduler2, MaxFactor, reference_param_groups
 
     torch.manual_seed(0)
-    m = Model(Dimensions(tokens=300, mels=128, dims=64, head=2, layer=4, act="gelu", n_type="AbbyNormal")).to(cuda)
+    m = Model(Dimensions(tokens=300, mels=128, dims=128, head=2, layer=4, act="gelu", n_type="AbbyNormal")).to(cuda)
     groups = reference_param_groups(m)
     assert sum(len(g["params"]) for g in groups) == sum(1 for p in m.parameters() if p.requires_grad)
     opt = MaxFactor(groups, lr=2.5e-3, b_decay=-0.8, eps=(1e-8, 1e-8), d=1.0, decay=1e-2, gamma=0.99, max=False,
