@@ -41,8 +41,10 @@ def clear_weight_cache():
 
 
 def weight_bf16(W, trans=False, cache=True):
-    """bf16 N x K copy of a weight: W is (N, K) (trans=False) or (K, N) (trans=True)."""
-    key = (W.data_ptr(), tuple(W.shape), tuple(W.stride()), bool(trans), W._version) if cache else None
+    """bf16 N x K copy of a weight: W is (N, K) (trans=False) or (K, N) (trans=True).  Cached per
+    stream: a copy converted on one stream is never read by another before it is complete."""
+    key = (W.data_ptr(), tuple(W.shape), tuple(W.stride()), bool(trans), W._version,
+           torch.cuda.current_stream(W.device).cuda_stream if W.is_cuda else 0) if cache else None
     if key is not None and key in _WCACHE:
         return _WCACHE[key][1]
     src = W

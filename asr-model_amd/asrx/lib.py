@@ -28,6 +28,7 @@ SIGNATURES = {
     "asrx_last_error": (ctypes.c_char_p, []),
     "asrx_abi_version": (_i32, []),
     "asrx_noise_hash": (_u32, [_u32, _u32]),
+    "asrx_set_noise_epoch": (_i32, [_u32, _p]),
     "asrx_mel_frames": (_i32, [_i64]),
     "asrx_logmel": (_i32, [_p, _i64, _i64, _i64, _p, _p, _p, _p, _i32, _i64, _p, _p, _i64, _p]),
     "asrx_gemm": (

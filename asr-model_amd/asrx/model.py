@@ -37,8 +37,17 @@ def sinusoids(ctx: int, dims: int, device) -> torch.Tensor:
         tscales = torch.exp(-torch.log(torch.tensor(float(THETA))) / (dims // 2 - 1)
                             * torch.arange(dims // 2, dtype=torch.float32))
         scaled = torch.arange(ctx, dtype=torch.float32).unsqueeze(1) * tscales.unsqueeze(0)
-        _TABLES[key] = torch.cat([torch.sin(scaled), torch.cos(scaled)], dim=1).contiguous().to(device)
+        _TABLES[key] = _to_device(torch.cat([torch.sin(scaled), torch.cos(scaled)], dim=1).contiguous(), device)
     return _TABLES[key]
+
+
+def _to_device(t, device):
+    """A constant table, made once and then read from several streams: complete the copy before any
+    stream can use it."""
+    t = t.to(device)
+    if t.is_cuda:
+        torch.cuda.current_stream(t.device).synchronize()
+    return t
 
 
 def rotary_freqs(dims: int, head: int, masked: bool, device) -> torch.Tensor:
@@ -52,7 +61,7 @@ def rotary_freqs(dims: int, head: int, masked: bool, device) -> torch.Tensor:
             f = 200 * scale / 1000
         else:
             f = torch.arange(0, hd, 2, dtype=torch.float32) / hd * torch.log(torch.tensor(THETA))
-        _TABLES[key] = f.contiguous().to(device)
+        _TABLES[key] = _to_device(f.contiguous(), device)
     return _TABLES[key]
 
 
@@ -126,7 +135,7 @@ class ConvLite(nn.Module):
         y = ops.act(y, "silu")
         y = ops.linear(y, self.point2.weight.view(D, D), self.point2.bias)
         if self.training:  # res + dropout(y) in one pass
-            return ops.DropoutAdd.apply(res, y, sid_base, noise.key(site + ".cl"), 0.1)
+            return ops.dropout_add(res, y, sid_base, noise.key(site + ".cl"), 0.1)
         return ops.add(res, y)
 
     @torch.no_grad()
@@ -188,7 +197,7 @@ class AudioEncoder(nn.Module):
             x = ops.DWConv.apply(x, layer[5].weight, layer[5].bias)
             if self.training:  # GELU -> Dropout(0.1) [-> next layer's GELU] in one kernel each way
                 fused_lead = l + 1 < n
-                x = ops.ActDropout.apply(x, "gelu", sid_base, noise.key(f"enc.L{l}.dr"), 0.1,
+                x = ops.act_dropout(x, "gelu", sid_base, noise.key(f"enc.L{l}.dr"), 0.1,
                                          "gelu" if fused_lead else "none")
             else:
                 x = ops.act(x, "gelu")
@@ -440,6 +449,15 @@ class processor(nn.Module):  # noqa: N801  (model.py:585-629)
         self.position = nn.Parameter(torch.ones(ctx, dims), requires_grad=True)
         self.blend = nn.Parameter(torch.tensor(0.5), requires_grad=True)
         self.block = nn.ModuleList([residual(dims, head, layer, act, n_type) for _ in range(layer)])
+        # Blocks 0..L-2 restart from the embeddings and never reach the output (model.py:617-628).
+        # False (default): computed anyway, like the reference (faithful work).  True: skipped --
+        # output-identical (keyed noise: no RNG stream to keep in step), reported separately.
+        self.skip_dead_blocks = False
+        # Dead blocks carry no autograd state, so their text side (8192-row calls at the tiny config:
+        # launch-latency-bound kernels) runs on a second HIP stream under the next blocks' audio side
+        # (bandwidth-bound, 192k-row calls).  Scheduling only: same kernels, same results.
+        self.concurrent_dead_text = True
+        self._side = None
 
     def forward(self, x, xa, noise: NoiseCtx, seq=False):
         B, T = x.shape
@@ -447,18 +465,39 @@ class processor(nn.Module):  # noqa: N801  (model.py:585-629)
         x = ops.add_rows(xe, self.position[:T])
         A_in = [xa["a"], xa["b"], xa["c"]]
         nblk = len(self.block)
+        side = None
+        keep = []  # cross-stream inputs stay referenced until the side stream is joined
         for i, blk in enumerate(self.block):
-            dead = i < nblk - 1 and torch.is_grad_enabled()
-            with torch.no_grad() if dead else contextlib.nullcontext():
-                a = blk.call(x, noise, f"b{i}.ta", 0, masked=True)
+            if self.skip_dead_blocks and i < nblk - 1:
+                continue
+            dead = i < nblk - 1
+            conc = dead and self.concurrent_dead_text and x.is_cuda
+            with torch.no_grad() if dead and torch.is_grad_enabled() else contextlib.nullcontext():
+                if conc and side is None:
+                    if self._side is None or self._side.device != x.device:
+                        self._side = torch.cuda.Stream(device=x.device)
+                    side = self._side
+                    side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side) if conc else contextlib.nullcontext():
+                    a = blk.call(x, noise, f"b{i}.ta", 0, masked=True)
                 A = self._audio(blk, A_in, noise, f"b{i}.audio", B, "call")
                 KV = self._audio(blk, A, noise, f"b{i}.xa", B, "xa")
-                b_ = blk.call(a, noise, f"b{i}.tb", 0, kv=KV[0])
-                c_ = blk.call(b_, noise, f"b{i}.tc", 0, kv=KV[1])
-                d = blk.call(c_, noise, f"b{i}.td", 0, kv=KV[2])
-                e = ops.add(a, b_, c_)
-                kve = blk.xa_side(e, noise, f"b{i}.tg.xa", 0)
-                g = blk.call(d, noise, f"b{i}.tg", 0, kv=kve)
+                if conc:
+                    ev = torch.cuda.Event()
+                    ev.record(torch.cuda.current_stream())
+                    keep.append(KV)
+                with torch.cuda.stream(side) if conc else contextlib.nullcontext():
+                    if conc:
+                        side.wait_event(ev)
+                    b_ = blk.call(a, noise, f"b{i}.tb", 0, kv=KV[0])
+                    c_ = blk.call(b_, noise, f"b{i}.tc", 0, kv=KV[1])
+                    d = blk.call(c_, noise, f"b{i}.td", 0, kv=KV[2])
+                    e = ops.add(a, b_, c_)
+                    kve = blk.xa_side(e, noise, f"b{i}.tg.xa", 0)
+                    g = blk.call(d, noise, f"b{i}.tg", 0, kv=kve)
+        if side is not None:
+            torch.cuda.current_stream().wait_stream(side)
+        keep.clear()
         if seq:
             out = g
         else:

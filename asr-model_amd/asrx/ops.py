@@ -81,14 +81,17 @@ class Linear(torch.autograd.Function):
     """y = act(x W^T + b) on MFMA (nn.Linear / 1x1 Conv1d)."""
 
     @staticmethod
-    def forward(ctx, x, W, b, act="none"):
+    def forward(ctx, x, W, b, act="none", grad=True):
         x = _c(x)
-        z = _E(*x.shape[:-1], W.shape[0], device=x.device) if act != "none" else None
+        # the pre-activation is kept only for a backward that will run (none in the reference's dead
+        # blocks, eval or decoding: an N-wide fp32 write saved per call)
+        z = _E(*x.shape[:-1], W.shape[0], device=x.device) if act != "none" and grad else None
         y = G.linear_fwd(x, W, b, act=act, preact=z)
         ctx.act = act
         ctx.has_b = b is not None
-        ctx.dW, ctx.db = _direct(ctx, 1, W), _direct(ctx, 2, b)
-        ctx.save_for_backward(x, W, z, b if ctx.db else None)
+        if grad:
+            ctx.dW, ctx.db = _direct(ctx, 1, W), _direct(ctx, 2, b)
+            ctx.save_for_backward(x, W, z, b if ctx.db else None)
         return y
 
     @staticmethod
@@ -106,11 +109,15 @@ class Linear(torch.autograd.Function):
             dW = _gret(W, G.linear_wgrad(gz, x, out=_gbuf(W, ctx.dW), accumulate=True), ctx.dW)
         if ctx.has_b and ctx.needs_input_grad[2]:
             db = _gret(b, colsum(gz, out=_gbuf(b, True) if ctx.db else None), ctx.db)
-        return dx, dW, db, None
+        return dx, dW, db, None, None
+
+
+def _grad_needed(*ts):
+    return torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts)
 
 
 def linear(x, W, b=None, act="none"):
-    return Linear.apply(x, W, b, act)
+    return Linear.apply(x, W, b, act, _grad_needed(x, W, b))
 
 
 def colsum(x2, out=None):
@@ -202,6 +209,8 @@ class AbbyNormalFn(torch.autograd.Function):
 
 
 def abby_normal(mod, x, L, H, sid_base, key, use_noise=True):
+    if use_noise:
+        _noise_rows_ok(sid_base + _rows(x) // max(L * H, 1), H, L, 3)
     r = mod.mode_router
     keep = torch.is_grad_enabled() and (x.requires_grad or r[0].weight.requires_grad)
     return AbbyNormalFn.apply(x, r[0].weight, r[0].bias, r[2].weight, r[2].bias, L, H, sid_base, key, use_noise,
@@ -775,6 +784,43 @@ class DropoutAdd(torch.autograd.Function):
         dy = _E(g.shape, device=g.device)
         lib.call("asrx_dropout", _P(g), _P(dy), B, T, C, sid_base, key & 0xFFFFFFFF, float(p), _S())
         return g, dy, None, None, None
+
+
+def _noise_rows_ok(sid_end, C, T, k=1):
+    """Keyed-noise element indices ((sid * C + c) * 4096 + t for dropout, ((sid * H + h) * 4096 + l) * 3 + k
+    for the gumbel draws, oracle/keys.py) are uint32 and assume positions < 4096 (clips up to ~40.9 s
+    at hop 160): refuse shapes that would alias draws instead of silently reusing them."""
+    from .noise import LSTRIDE
+
+    if T > LSTRIDE:
+        raise ValueError(f"keyed noise: sequence length {T} > {LSTRIDE} positions (clips longer than ~40.9 s) "
+                         "would alias dropout/gumbel draws")
+    if sid_end * C * LSTRIDE * k >= 1 << 32:
+        raise ValueError(f"keyed noise: {sid_end} streams x {C} channels overflow the 32-bit noise index")
+
+
+def _vec4_ok(*ts):
+    return all(t is None or (t.data_ptr() % 16 == 0) for t in ts) and ts[0].shape[-1] % 4 == 0
+
+
+def act_dropout(z, act, sid_base, key, p, act2="none"):
+    """act -> Dropout(p) -> act2 on (B, T, C): one fused float4 kernel each way, or the separate ops
+    (bit-identical) when C % 4 != 0 or a tensor is not 16-byte aligned."""
+    z = _c(z)
+    _noise_rows_ok(sid_base + z.shape[0], z.shape[2], z.shape[1])
+    if _vec4_ok(z):
+        return ActDropout.apply(z, act, sid_base, key, p, act2)
+    y = Dropout.apply(Act.apply(z, act) if act != "none" else z, sid_base, key, p)
+    return Act.apply(y, act2) if act2 != "none" else y
+
+
+def dropout_add(res, y, sid_base, key, p):
+    """res + Dropout(p)(y) (ConvLite tail, model.py:107-118), fused when float4-able."""
+    res, y = _c(res), _c(y)
+    _noise_rows_ok(sid_base + y.shape[0], y.shape[2], y.shape[1])
+    if _vec4_ok(y, res):
+        return DropoutAdd.apply(res, y, sid_base, key, p)
+    return add(res, Dropout.apply(y, sid_base, key, p))
 
 
 class DWConv(torch.autograd.Function):

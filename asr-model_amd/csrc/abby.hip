@@ -791,3 +791,5 @@ extern "C" int asrx_abby_bwd(const float* dout, const float* x, const float* hpr
   ABBY_DISPATCH(abby_bwd_kernel, dout, x, hpre, W2, ys, idx, dx, dhpre, dW2, db2, g);
   ASRX_LAUNCHED("asrx_abby_bwd");
 }
+
+ASRX_NOISE_EPOCH_SETTER(asrx_set_noise_epoch_abby)

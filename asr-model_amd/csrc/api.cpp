@@ -31,6 +31,16 @@ const char* asrx_last_error(void) { return asrx::g_last_error.c_str(); }
 
 int asrx_abi_version(void) { return 1; }
 
+int asrx_set_noise_epoch_abby(uint32_t epoch, hipStream_t stream);
+int asrx_set_noise_epoch_rowops(uint32_t epoch, hipStream_t stream);
+
+// Noise epoch of every noise-drawing kernel (see common.h): stream-ordered, so a graph replayed on
+// `stream` after this call draws the epoch's noise.  0 = the oracle's keys.
+int asrx_set_noise_epoch(uint32_t epoch, hipStream_t stream) {
+  int e = asrx_set_noise_epoch_abby(epoch, stream);
+  return e ? e : asrx_set_noise_epoch_rowops(epoch, stream);
+}
+
 // Host-side restatement of the device noise hash (used by tests to cross-check oracle/noise.py).
 uint32_t asrx_noise_hash(uint32_t key, uint32_t idx) {
   return asrx::mix32(asrx::mix32(idx ^ key) + (key * 0x9E3779B9U + 0x632BE5ABU));

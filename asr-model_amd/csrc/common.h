@@ -28,6 +28,21 @@ int check_launch(const char* what);
 
 }  // namespace asrx
 
+#define ASRX_NOISE_EPOCH_SETTER(NAME)                                                                      \
+  extern "C" int NAME(uint32_t epoch, hipStream_t stream) {                                               \
+    static uint32_t host_epoch[64];                                                                       \
+    static unsigned slot = 0;                                                                             \
+    uint32_t* src = &host_epoch[(slot++) & 63]; /* stays valid while the copy may still be pending */    \
+    *src = epoch;                                                                                         \
+    hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(asrx::g_noise_epoch), src, sizeof(uint32_t), 0,      \
+                                          hipMemcpyHostToDevice, stream);                                 \
+    if (e != hipSuccess) {                                                                                \
+      asrx::set_error("%s: %s", #NAME, hipGetErrorString(e));                                             \
+      return (int)e;                                                                                      \
+    }                                                                                                     \
+    return 0;                                                                                             \
+  }
+
 #define ASRX_REQUIRE(cond, ...)            \
   do {                                     \
     if (!(cond)) {                         \
@@ -167,7 +182,16 @@ __host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
   x ^= x >> 16;
   return x;
 }
+// Noise epoch: a device-side word mixed into every site key when nonzero.  A captured HIP graph bakes
+// the host-computed site keys (seed, step, site) into its launches; bumping the epoch between replays
+// (asrx_set_noise_epoch, a stream-ordered copy outside the graph) gives every replayed step fresh
+// dropout masks and gumbel draws.  Epoch 0 (the default, and what every eager step uses) leaves the
+// keys exactly as oracle/keys.py computes them.  One copy per translation unit (no relocatable
+// device code); each noise-drawing TU exports its setter (ASRX_NOISE_EPOCH_SETTER).
+static __device__ uint32_t g_noise_epoch;
 __device__ __forceinline__ float noise_uniform(uint32_t key, uint32_t idx) {
+  const uint32_t ep = g_noise_epoch;
+  if (ep != 0u) key ^= mix32(ep * 0x9E3779B9U + 0x7F4A7C15U);
   uint32_t h = mix32(mix32(idx ^ key) + (key * 0x9E3779B9U + 0x632BE5ABU));
   return ((float)(h >> 9) + 0.5f) * (1.0f / 8388608.0f);
 }
@@ -178,3 +202,18 @@ __device__ __forceinline__ float noise_gumbel(uint32_t key, uint32_t idx) {
 }
 
 }  // namespace asrx
+
+#define ASRX_NOISE_EPOCH_SETTER(NAME)                                                                      \
+  extern "C" int NAME(uint32_t epoch, hipStream_t stream) {                                               \
+    static uint32_t host_epoch[64];                                                                       \
+    static unsigned slot = 0;                                                                             \
+    uint32_t* src = &host_epoch[(slot++) & 63]; /* stays valid while the copy may still be pending */    \
+    *src = epoch;                                                                                         \
+    hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(asrx::g_noise_epoch), src, sizeof(uint32_t), 0,      \
+                                          hipMemcpyHostToDevice, stream);                                 \
+    if (e != hipSuccess) {                                                                                \
+      asrx::set_error("%s: %s", #NAME, hipGetErrorString(e));                                             \
+      return (int)e;                                                                                      \
+    }                                                                                                     \
+    return 0;                                                                                             \
+  }

@@ -1754,3 +1754,5 @@ extern "C" int asrx_policy_noise(float* out, int64_t B, int64_t layers, int64_t 
   asrx::policy_noise_kernel<<<(unsigned)((B * layers * 3 + 255) / 256), 256, 0, stream>>>(out, B, layers, sid_base, key);
   ASRX_LAUNCHED("asrx_policy_noise");
 }
+
+ASRX_NOISE_EPOCH_SETTER(asrx_set_noise_epoch_rowops)

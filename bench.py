@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--same-device", action="store_true", help="every rank on cuda:0 (rehearsal only)")
     ap.add_argument("--eager", action="store_true", help="launch every kernel from Python instead of replaying "
                     "the captured HIP graph of the step")
+    ap.add_argument("--no-dead-block-line", action="store_true", help="skip the extra measurement with the "
+                    "reference's dead decoder blocks eliminated (reported beside, never as, the headline)")
     return ap.parse_args()
 
 
@@ -173,8 +175,12 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    from asrx import lib
+    for i in range(args.steps):
         if graph is not None:
+            # the captured launches carry the capture step's noise keys: a new epoch per replay gives
+            # every timed step its own dropout masks and gumbel draws (stream-ordered, outside the graph)
+            lib.call("asrx_set_noise_epoch", i + 1, lib.stream())
             graph.replay()
         else:
             loss = step()
@@ -182,12 +188,16 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if graph is not None:
+        lib.call("asrx_set_noise_epoch", 0, lib.stream())
     if not args.no_probe:
         # per-kernel HIP events stay out of the timed region (and cannot be read back from inside a
         # captured graph): every rank runs the identical step (same kernels, shapes and inputs)
         # once more eagerly with the probe on, right after the timed steps
         probe.enable(("gemm", "logmel", "attn"))
+        model.processor.concurrent_dead_text = False  # per-kernel event times without a concurrent stream
         step()
+        model.processor.concurrent_dead_text = True
         torch.cuda.synchronize()
         recs = probe.disable()
         probe_steps = 1
@@ -302,6 +312,38 @@ def main():
     result["launch"] = "hip-graph replay" if graph is not None else "eager"
     if recs is not None:
         result["probe"] = "per-kernel HIP events on one eager pass of the same step after the timed steps"
+    if not args.no_dead_block_line and world == 1:
+        # SURVEY.md §7 "Only the last block reaches the output": processor.forward computes blocks
+        # 0..L-2 and discards them.  The headline keeps that work (faithful); this line measures the
+        # same step with them skipped (output-identical under keyed noise), labelled as such.
+        model.processor.skip_dead_blocks = True
+        torch.cuda.synchronize()
+        with torch.cuda.stream(side):
+            step()
+        torch.cuda.current_stream().wait_stream(side)
+        g2 = None
+        if graph is not None:
+            g2 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g2):
+                step()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for i in range(args.steps):
+            if g2 is not None:
+                lib.call("asrx_set_noise_epoch", i + 1, lib.stream())
+                g2.replay()
+            else:
+                step()
+        torch.cuda.synchronize()
+        el2 = time.perf_counter() - t1
+        if g2 is not None:
+            lib.call("asrx_set_noise_epoch", 0, lib.stream())
+        model.processor.skip_dead_blocks = False
+        result["dead_block_eliminated"] = {
+            "value": round(B * CLIP_SECONDS * args.steps / el2, 3), "unit": "audio-sec/sec",
+            "ms_per_step": round(el2 / args.steps * 1e3, 3),
+            "note": "same step with processor blocks 0..L-2 skipped (they never reach the output, model.py:617-628); "
+                    "output-identical, NOT the headline"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(model, args.config)
     if world > 1:

@@ -24,6 +24,10 @@ int asrx_abi_version(void);
 /* Keyed noise hash shared by device kernels and oracle/noise.py (gumbel_softmax noise at
  * essentials.py:170 / model.py:476, dropout masks at model.py:107,147). Host function. */
 uint32_t asrx_noise_hash(uint32_t key, uint32_t idx);
+/* Noise epoch (stream-ordered): when nonzero it is mixed into every site key, so a captured HIP graph
+ * of a training step draws fresh dropout masks / gumbel noise per replay (the reference draws fresh
+ * noise every step, essentials.py:751-824); 0 (default) = the keys of oracle/keys.py. */
+int asrx_set_noise_epoch(uint32_t epoch, asrx_stream_t stream);
 
 /* ---- log-mel front end: replaces torchaudio MelSpectrogram + log10 + clip-max floor,
  *      essentials.py:469-491, and the waveform adaptive_avg_pool1d, essentials.py:493-510 -------- */
@@ -82,8 +86,9 @@ int asrx_abby_bwd(const float* dout, const float* x, const float* hpre, const fl
                   const int* idx, float* dx, float* dhpre, float* dW2, float* db2, int64_t rows, int64_t d,
                   asrx_stream_t stream);
 
-/* ---- attention: F.scaled_dot_product_attention(q,k,v,is_causal) at model.py:307, head dim 64.
- *      q/k/v/o are (B,L,H,64) with strides sX = int64[3] {batch, seq, head}; lse (B,H,Lq).
+/* ---- attention: F.scaled_dot_product_attention(q,k,v,is_causal) at model.py:307, head dim hd = 64
+ *      (tiny/small/medium) or 128 (the reference's Dimensions(dims=512, head=4), model.py:746).
+ *      q/k/v/o are (B,L,H,hd) with strides sX = int64[3] {batch, seq, head}; lse (B,H,Lq).
  *      asrx_attn_fwd also takes prec 2 = fp8 attention: QK^T on e4m3 with
  *      per-row scales (MX-rate MFMA), softmax and PV in bf16; the backward takes 0 or 1 only. ---- */
 int asrx_attn_fwd(int prec, const float* q, const int64_t* sq, const float* k, const int64_t* sk, const float* v,

@@ -399,3 +399,25 @@ def forward(P, cfg, text_ids, labels=None, spectrogram=None, pitch=None, wavefor
     if labels is not None:
         loss = F.cross_entropy(logits.reshape(-1, logits.shape[-1]), labels.reshape(-1), ignore_index=0)
     return {"logits": logits, "loss": loss}
+
+
+def generate(P, cfg, spectrogram=None, pitch=None, waveform=None, max_new_tokens=150, seed=0, step=0,
+             dtype=torch.float64):
+    """Model.generate (model.py:674-701): eval mode, the encoder on the audio streams, then per new
+    token the processor with seq=True over the tokens so far (starting from BOS = 1), argmax of the
+    last position, stop once every sequence emitted EOS = 2.  The whole forward is recomputed for every
+    token exactly as the reference does (blocks 0..L-2 are skipped: they never reach the output, see
+    forward(live_only)); the gumbel noise is the keyed noise of one (seed, step), the same for every
+    decoding step."""
+    first = next(t for t in (pitch, spectrogram, waveform) if t is not None)
+    B = first.shape[0]
+    y = torch.ones(B, 1, dtype=torch.long)
+    with torch.no_grad():
+        for _ in range(max_new_tokens):
+            logits = forward(P, cfg, y, spectrogram=spectrogram, pitch=pitch, waveform=waveform, seed=seed,
+                             step=step, training=False, dtype=dtype, live_only=True, seq=True)["logits"]
+            nxt = logits[:, -1, :].argmax(dim=-1, keepdim=True)
+            y = torch.cat((y, nxt), dim=1)
+            if bool((nxt == 2).all()):
+                break
+    return y

@@ -73,3 +73,37 @@ def test_model_parity_fp32(cuda, train):
     assert checked == 14
     # dead blocks get no gradient in either implementation (model.py:617-628)
     assert names["processor.block.0.attn.q.1.weight"].grad is None
+
+
+def test_skip_dead_blocks_is_output_identical(cuda):
+    """processor.skip_dead_blocks (the separately reported bench mode) skips blocks 0..L-2, which the
+    reference computes and discards (model.py:617-628): logits, loss and every gradient are
+    identical to the faithful run (keyed noise leaves no RNG stream to keep in step).  So is the
+    faithful run with the dead blocks' text side on the main stream instead of the side stream."""
+    from asrx import prec
+    from asrx.config import Dimensions
+    from asrx.model import Model
+
+    torch.manual_seed(0)
+    cfg = Dimensions(tokens=1000, mels=128, dims=128, head=2, layer=3, act="gelu", n_type="AbbyNormal")
+    model = Model(cfg).cuda().train()
+    spec, pitch, wav, ids, labels = _toy_inputs()
+    res = []
+    for skip, conc in ((False, True), (True, True), (False, False)):
+        model.processor.skip_dead_blocks = skip
+        model.processor.concurrent_dead_text = conc
+        model.zero_grad(set_to_none=True)
+        model.set_noise(3, 1)
+        with prec.precision("bf16"):
+            out = model(labels=labels.cuda(), text_ids=ids.cuda(), spectrogram=spec.cuda(), pitch=pitch.cuda(),
+                        waveform=wav.cuda())
+            out["loss"].backward()
+        res.append((out["logits"].detach().clone(), {n: p.grad.clone() for n, p in model.named_parameters()
+                                                     if p.grad is not None}))
+    model.processor.skip_dead_blocks = False
+    model.processor.concurrent_dead_text = True
+    for other in res[1:]:  # skipped dead blocks, and dead blocks run serially on one stream
+        assert torch.equal(res[0][0], other[0])
+        assert set(res[0][1]) == set(other[1])
+        # gradients: equal up to the float-atomic accumulation order of split-K / column-sum kernels
+        assert all(_rel(other[1][n], res[0][1][n]) < 1e-5 for n in res[0][1])

@@ -461,3 +461,47 @@ def test_dropout_add_fused(cuda):
     d2 = torch.autograd.grad(out2, (res, y), gout)
     assert torch.equal(out, out2)
     assert all(torch.equal(a, b) for a, b in zip(d1, d2))
+
+
+def test_noise_epoch(cuda):
+    """asrx_set_noise_epoch: a nonzero epoch changes every keyed draw (dropout masks and AbbyNormal's
+    gumbel decisions), epoch 0 restores the oracle's keys exactly; stream-ordered, so it also steers
+    launches replayed from a captured graph."""
+    from asrx import lib, ops
+
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(2, 301, 384, generator=g).to(cuda)
+    key = 0xC0FFEE
+    y0 = ops.Dropout.apply(x, 0, key, 0.1)
+    lib.call("asrx_set_noise_epoch", 7, lib.stream())
+    try:
+        y7 = ops.Dropout.apply(x, 0, key, 0.1)
+        y7b = ops.ActDropout.apply(x, "none", 0, key, 0.1, "none")
+        pol7 = ops.policy_noise(4, 3, 0, key, cuda)
+    finally:
+        lib.call("asrx_set_noise_epoch", 0, lib.stream())
+    y0b = ops.Dropout.apply(x, 0, key, 0.1)
+    pol0 = ops.policy_noise(4, 3, 0, key, cuda)
+    assert torch.equal(y0, y0b)
+    assert not torch.equal((y0 == 0), (y7 == 0))
+    assert torch.equal(y7, y7b)  # both kernels of the TU see the same epoch
+    assert not torch.equal(pol0, pol7)
+    keep7 = float((y7 != 0).double().mean())
+    assert 0.88 < keep7 < 0.92
+    # graph capture: the epoch set before a replay decides its draws
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        out = ops.Dropout.apply(x, 0, key, 0.1)
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        out = ops.Dropout.apply(x, 0, key, 0.1)
+    res = []
+    for ep in (0, 7, 0):
+        lib.call("asrx_set_noise_epoch", ep, lib.stream())
+        graph.replay()
+        res.append(out.clone())
+    lib.call("asrx_set_noise_epoch", 0, lib.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(res[0], y0) and torch.equal(res[1], y7) and torch.equal(res[2], y0)
