@@ -24,8 +24,8 @@ def read_wav(path):
     the array is 1-D for mono, as soundfile returns it."""
     raw = open(path, "rb").read()
     if len(raw) < 12 or raw[:4] != b"RIFF" or raw[8:12] != b"WAVE":
-        raise NotImplementedError(f"load_wave({path!r}): only RIFF/WAVE files are decoded here "
-                                  "(soundfile, which the reference uses for FLAC, is not installed)")
+        raise NotImplementedError(f"load_wave({path!r}): FLAC (asrx.data) and RIFF/WAVE files are decoded here "
+                                  "(soundfile's other formats are not installed)")
     fmt = data = None
     pos = 12
     while pos + 8 <= len(raw):
@@ -64,12 +64,15 @@ def read_wav(path):
 
 
 def load_wave(audio, sample_rate=16000):
-    """essentials.load_wave (essentials.py:301-319).  File path: decoded by read_wav (WAV only;
-    soundfile, which the reference calls, is absent here), then peak-normalised as the reference
-    does -- mono by max|x|, multi-channel by the per-channel max of x (not of |x|, essentials.py:306)
-    and returned channels-first.  Dict: the array as float32 with its own rate, not normalised."""
+    """essentials.load_wave (essentials.py:301-319).  File path: decoded like soundfile.read(path,
+    dtype='float32') (FLAC by the native decoder of asrx.data, WAV by read_wav), then peak-normalised
+    as the reference does -- mono by max|x|, multi-channel by the per-channel max of x (not of |x|,
+    essentials.py:306) and returned channels-first.  Dict: the array as float32 with its own rate, not
+    normalised.  asrx.data.load_batch is the batched device version of the file branch."""
     if isinstance(audio, str):
-        wp, sample_rate = read_wav(audio)
+        from .data import read_audio
+
+        wp, sample_rate = read_audio(audio)  # FLAC (native decoder) or WAV
         if wp.ndim > 1:
             abs_max = wp.max(axis=0)
             wp = wp / abs_max if any(abs_max > 0) else wp

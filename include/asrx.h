@@ -41,6 +41,20 @@ int asrx_logmel(const float* wav, int64_t B, int64_t N, int64_t ld_wav, const fl
                 const float* fbw, const int* fbs, float* out, int layout, int64_t ld_out,
                 int* clip_max_ws, float* pool, int64_t T_pool, asrx_stream_t stream);
 
+/* ---- audio IO: load_wave's soundfile.read + peak normalisation,
+ *      essentials.py:301-319, for the prepare_datasets path (998-1026). -------------------------
+ * FLAC (RFC 9639) decoding, host functions on an in-memory file: asrx_flac_info returns STREAMINFO
+ * (samples per channel, channels, rate, bits, MD5 of the audio); asrx_flac_decode writes planar int32
+ * (channels x cap), checking every frame's CRC-8 / CRC-16. */
+int asrx_flac_info(const uint8_t* buf, int64_t n, int64_t* frames, int* channels, int* rate, int* bits,
+                   uint8_t* md5);
+int asrx_flac_decode(const uint8_t* buf, int64_t n, int32_t* out, int64_t cap);
+/* Device: pcm (B,C,ld) int32 (is_float = 0) or fp32 (1) -> out (B,C,ld_out) fp32 = pcm * scale[b],
+ * then (normalize != 0) divided by max|x| (mono) or by each channel's max(x) (multi-channel, the
+ * reference's quirk); zero past lengths[b] (int64, device). */
+int asrx_pcm_normalize(const void* pcm, int is_float, int64_t B, int64_t C, int64_t ld, const int64_t* lengths,
+                       const float* scale, float* out, int64_t ld_out, int normalize, asrx_stream_t stream);
+
 /* ---- GEMM: replaces F.linear / 1x1 and k3 conv1d (fwd, dgrad, wgrad) at model.py:96-147,
  *      242-245, 341, 398-425, 529-574, essentials.py:149-153 ------------------------------------
  * C[b] = act(alpha*A[b]@B[b] + beta*C[b] + bias); A MxK (a_kc: row-major MxK, else KxM), B KxN

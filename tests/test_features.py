@@ -99,8 +99,12 @@ def test_load_wave_file_branch(tmp_path):
     np.testing.assert_allclose(x.numpy(), (st / st.max(axis=0)).T, rtol=1e-6)
 
     bad = str(tmp_path / "x.flac")
-    open(bad, "wb").write(b"fLaC" + bytes(40))
-    with pytest.raises(NotImplementedError):
+    open(bad, "wb").write(b"fLaC" + bytes(40))  # FLAC marker but no valid STREAMINFO (tests/test_flac.py)
+    with pytest.raises(RuntimeError, match="asrx_flac"):
         load_wave(bad)
+    other = str(tmp_path / "x.ogg")
+    open(other, "wb").write(b"OggS" + bytes(40))
+    with pytest.raises(NotImplementedError):
+        load_wave(other)
     with pytest.raises(TypeError):
         load_wave(3)
