@@ -47,10 +47,16 @@ SIGNATURES = {
                              _i64, _i64, _i64, _i64, _i64, _i32, _f32, _p]),
     "asrx_layernorm_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _i64, _f32, _p]),
     "asrx_layernorm_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _p]),
+    "asrx_layernorm_bwd_acc": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i32, _p]),
     "asrx_small_linear_fwd": (_i32, [_p, _p, _p, _p, _i64, _i64, _i64, _i32, _p]),
     "asrx_small_linear_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i32, _f32, _p]),
     "asrx_rownorm": (_i32, [_p, _p, _i64, _i64, _p]),
     "asrx_rownorm_bwd": (_i32, [_p, _p, _p, _p, _i64, _i64, _p]),
+    "asrx_row_normalize": (_i32, [_p, _p, _p, _i64, _i64, _p]),
+    "asrx_row_normalize_bwd": (_i32, [_p, _p, _p, _p, _i64, _i64, _i32, _p]),
+    "asrx_softmax_small": (_i32, [_p, _p, _i64, _i64, _p]),
+    "asrx_softmax_small_bwd": (_i32, [_p, _p, _p, _i64, _i64, _p]),
+    "asrx_zero": (_i32, [_p, _i64, _p]),
     "asrx_rotary_fwd": (_i32, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _f32, _p]),
     "asrx_rotary_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _f32, _p]),
     "asrx_vgate_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _f32, _p]),
@@ -60,6 +66,7 @@ SIGNATURES = {
     "asrx_tgate_bwd": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _p]),
     "asrx_axpy_row": (_i32, [_p, _p, _p, _p, _i64, _i64, _p]),
     "asrx_axpy_row_bwd": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _p]),
+    "asrx_axpy_row_bwd2": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _i64, _p]),
     "asrx_jump_select": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p]),
     "asrx_jump_select_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p]),
     "asrx_seg_colsum": (_i32, [_p, _p, _i64, _i64, _i64, _f32, _i32, _p]),
@@ -68,6 +75,13 @@ SIGNATURES = {
     "asrx_msheath_ctrl_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p, _p, _p, _p, _p,
                                      _p]),
     "asrx_msheath_rec_bytes": (_i64, []),
+    "asrx_msheath_ctrl_fwd2": (_i32, [_p, _p, _i64, _p, _p, _p, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _i64,
+                                      _p, _p, _p, _p, _p, _p, _p, _p]),
+    "asrx_msheath_ctrl_bwd2": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _p, _i32,
+                                      _p, _p, _p, _p, _p, _p]),
+    "asrx_jump_select4_bwd_acc": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p]),
+    "asrx_axpy_row2_bwd_acc": (_i32, [_p, _p, _f32, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p]),
+    "asrx_msheath_dx_final": (_i32, [_p, _p, _p, _p, _i64, _i64, _i64, _p]),
     "asrx_axpy_row2": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _p]),
     "asrx_axpy_row2_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _p]),
     "asrx_jump_select4": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p]),

@@ -341,9 +341,21 @@ class MSheath(nn.Module):
         self.mlp = nn.Sequential(nn.Linear(dims, dims * 4), nn.SiLU(), nn.Linear(dims * 4, dims))
         self.mlp_ln = nn.LayerNorm(dims)
 
+    # fused: one autograd node per call with a hand-written backward (asrx/msheath.py); False runs the
+    # per-op composition below (same kernels and results; kept as the reference implementation of it)
+    fused = True
+
     def run(self, x, noise: NoiseCtx, site: str, sid_base: int):
         """Batched MSheath.forward with batch-1 semantics per sample: every sample follows its own
         layer/jump trajectory, evaluated as masked compute on device (no host syncs)."""
+        if self.fused and ops.DIRECT:
+            from .msheath import msheath
+
+            gpol = ops.policy_noise(x.shape[0], self.layer, sid_base, noise.key(site), x.device)
+            return msheath(self, x, gpol)
+        return self.run_composed(x, noise, site, sid_base)
+
+    def run_composed(self, x, noise: NoiseCtx, site: str, sid_base: int):
         B, L, D = x.shape
         dev = x.device
         orig = x

@@ -1,0 +1,284 @@
+"""MSheath.forward (model.py:429-507) as ONE autograd node with a hand-written backward.
+
+Composed from per-op autograd Functions, a MSheath call leaves autograd to sum the gradient of every
+activation with several consumers -- each layer's input feeds v_gate, the LayerNorm, the x + g*ion*out
+update and the jump select, the original input feeds every layer's jump and the policy pooling -- which
+cost ~30 full-size add kernels per call in the backward (~14 ms of the tiny
+step).  MSheathFn runs the same forward kernels, then walks the layers backwards with every
+contribution to a layer input landing in one buffer: written by its first producer (the jump-select
+pass-through of inactive samples, the x_new backward of active ones), accumulated by the rest
+(LayerNorm backward in accumulate mode, v_gate's input GEMMs with beta = 1, row-norm backward), and
+the original input's jump gradient kept apart until one final pass.  Parameter gradients go straight
+into p.grad (asrx.ops direct-gradient convention).  Batch-1 semantics per sample exactly as
+asrx.model.MSheath.run_composed (masked per-sample trajectories, no host syncs).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import gemm as G
+from . import lib, ops
+
+_E = torch.empty
+_P = lib.ptr
+_S = lib.stream
+SIG = G.ACT["sigmoid"]
+SILU = G.ACT["silu"]
+
+_REC = None
+
+
+def _rec_bytes():
+    global _REC
+    if _REC is None:
+        _REC = int(lib.load().asrx_msheath_rec_bytes())
+    return _REC
+
+
+def _params(mod):
+    """Every parameter MSheathFn reads, in a fixed order (tx is a frozen buffer-like parameter)."""
+    ps = [mod.pnet.net[0].weight, mod.pnet.net[0].bias, mod.pnet.net[2].weight, mod.pnet.net[2].bias, mod.mem_w,
+          mod.mem_gate[0].weight, mod.mem_gate[0].bias, mod.jump_s, mod.mlp_gate[0].weight, mod.mlp_gate[0].bias,
+          mod.mlp_ln.weight, mod.mlp_ln.bias, mod.mlp[0].weight, mod.mlp[0].bias, mod.mlp[2].weight, mod.mlp[2].bias]
+    for i, lay in enumerate(mod.layers):
+        vg = lay["v_gate"]
+        ps += [lay["ln"].weight, lay["ln"].bias, lay["gate"][0].weight, lay["gate"][0].bias, vg.mkey, vg.mval,
+               vg.mlp[0].weight, vg.mlp[0].bias, vg.mlp[2].weight, vg.mlp[2].bias, vg.concat.weight, vg.concat.bias]
+        if lay["adapter"] is not None:
+            ps += [lay["adapter"].weight, lay["adapter"].bias]
+    return ps
+
+
+def forward(mod, x0, gpol, save):
+    """MSheath forward on (B, L, D) x0 with policy noise gpol (B, layers, 3).  Returns (out, saved)."""
+    B, L, D = x0.shape
+    rows = B * L
+    dev = x0.device
+    st = _S()
+    sv = {} if save else None
+    # policy = softmax(MPNet(mean_l x))            model.py:432-435, 375-385
+    pooled = _E(B, D, device=dev)
+    lib.call("asrx_seg_colsum", _P(x0), _P(pooled), B, L, D, 1.0 / L, 0, st)
+    net = mod.pnet.net
+    zp = _E(B, net[0].weight.shape[0], device=dev) if save else None
+    hp = G.linear_fwd(pooled, net[0].weight, net[0].bias, act="silu", preact=zp)
+    pl = _E(B, 3, device=dev)
+    lib.call("asrx_small_linear_fwd", _P(hp), _P(net[2].weight), _P(net[2].bias), _P(pl), B, hp.shape[1], 3, 0, st)
+    policy = _E(B, 3, device=dev)
+    lib.call("asrx_softmax_small", _P(pl), _P(policy), B, 3, st)
+    mem_w, ld_mw = mod.mem_w, 0
+    next_i = None
+    x = x0
+    rec_bytes = _rec_bytes()
+    layers = []
+    nl = len(mod.layers)
+    for i, lay in enumerate(mod.layers):
+        vg = lay["v_gate"]
+        Dh = vg.mlp[0].weight.shape[0]
+        M = vg.mkey.shape[0]
+        # v_gate: ion = STE(concat(softmax(n(x) n(mkey)^T / sqrt D) mval, mlp(x)) > tx)   model.py:346-351
+        nx = _E(rows, device=dev)
+        lib.call("asrx_rownorm", _P(x), _P(nx), rows, D, st)
+        mkeyn = _E(M, D, device=dev)
+        mkn = _E(M, device=dev)
+        lib.call("asrx_row_normalize", _P(vg.mkey), _P(mkeyn), _P(mkn), M, D, st)
+        Sm = G.linear_fwd(x, mkeyn)
+        h = G.linear_fwd(x, vg.mlp[0].weight, vg.mlp[0].bias)
+        ion, xval, kv, m2 = (_E(rows, device=dev) for _ in range(4))
+        lib.call("asrx_vgate_fwd", _P(Sm), _P(nx), _P(vg.mval), _P(h), _P(vg.mlp[2].weight), _P(vg.mlp[2].bias),
+                 _P(vg.concat.weight), _P(vg.concat.bias), _P(vg.tx), _P(ion), _P(xval), _P(kv), _P(m2), rows, M, Dh,
+                 1.0 / math.sqrt(D), st)
+        # px = LayerNorm(x); out = adapter(px) (even i); x_new = x + sigmoid(gate(px)) * out * ion   (452-461)
+        px, mean, rstd = _E(B, L, D, device=dev), _E(rows, device=dev), _E(rows, device=dev)
+        lib.call("asrx_layernorm_fwd", _P(x), _P(lay["ln"].weight), _P(lay["ln"].bias), _P(px), _P(mean), _P(rstd),
+                 rows, D, float(lay["ln"].eps), st)
+        out = G.linear_fwd(px, lay["adapter"].weight, lay["adapter"].bias) if lay["adapter"] is not None else px
+        gv = _E(rows, device=dev)
+        lib.call("asrx_small_linear_fwd", _P(px), _P(lay["gate"][0].weight), _P(lay["gate"][0].bias), _P(gv), rows, D,
+                 1, SIG, st)
+        x_new = _E(B, L, D, device=dev)
+        lib.call("asrx_axpy_row2", _P(x), _P(gv), _P(ion), _P(out), _P(x_new), rows, D, st)
+        # mem = mean_l x_new; mem_v = sigmoid(mem_gate(mem)); control; jump select   (463-501)
+        mem = _E(B, D, device=dev)
+        lib.call("asrx_seg_colsum", _P(x_new), _P(mem), B, L, D, 1.0 / L, 0, st)
+        mem_v = _E(B, device=dev)
+        lib.call("asrx_small_linear_fwd", _P(mem), _P(mod.mem_gate[0].weight), _P(mod.mem_gate[0].bias), _P(mem_v), B,
+                 D, 1, SIG, st)
+        alpha, beta, active, next_out = (_E(B, device=dev) for _ in range(4))
+        gam, mwo = _E(B, D, device=dev), _E(B, D, device=dev)
+        rec = _E(B * rec_bytes, dtype=torch.uint8, device=dev)
+        gp = gpol[:, i]
+        lib.call("asrx_msheath_ctrl_fwd2", _P(policy), _P(gp), gp.stride(0), _P(ion), _P(mem_v), _P(mem_w), ld_mw,
+                 _P(mem), _P(mod.jump_s), _P(next_i), i, nl, B, L, D, _P(alpha), _P(beta), _P(gam), _P(mwo),
+                 _P(active), _P(next_out), _P(rec), st)
+        x_out = _E(B, L, D, device=dev)
+        lib.call("asrx_jump_select4", _P(x_new), _P(x0), _P(x), _P(active), _P(alpha), _P(beta), _P(gam),
+                 _P(x_out), B, L, D, st)
+        if save:
+            layers.append(dict(x=x, nx=nx, mkeyn=mkeyn, mkn=mkn, S=Sm, h=h, kv=kv, m2=m2, px=px, mean=mean, rstd=rstd,
+                               out=out, g=gv, ion=ion, x_new=x_new, mem=mem, mem_v=mem_v, mem_w=mem_w, ld_mw=ld_mw,
+                               rec=rec, active=active, alpha=alpha, beta=beta))
+        mem_w, ld_mw, next_i = mwo, D, next_out
+        x = x_out
+    # x + sigmoid(mlp_gate(x)) * mlp(mlp_ln(x))   (503-506)
+    gate = _E(rows, device=dev)
+    lib.call("asrx_small_linear_fwd", _P(x), _P(mod.mlp_gate[0].weight), _P(mod.mlp_gate[0].bias), _P(gate), rows, D,
+             1, SIG, st)
+    hln, mean2, rstd2 = _E(B, L, D, device=dev), _E(rows, device=dev), _E(rows, device=dev)
+    lib.call("asrx_layernorm_fwd", _P(x), _P(mod.mlp_ln.weight), _P(mod.mlp_ln.bias), _P(hln), _P(mean2), _P(rstd2),
+             rows, D, float(mod.mlp_ln.eps), st)
+    z1 = _E(B, L, mod.mlp[0].weight.shape[0], device=dev) if save else None
+    a1 = G.linear_fwd(hln, mod.mlp[0].weight, mod.mlp[0].bias, act="silu", preact=z1)
+    hh = G.linear_fwd(a1, mod.mlp[2].weight, mod.mlp[2].bias)
+    y = _E(B, L, D, device=dev)
+    lib.call("asrx_axpy_row", _P(x), _P(gate), _P(hh), _P(y), rows, D, st)
+    if save:
+        sv.update(x0=x0, pooled=pooled, zp=zp, hp=hp, policy=policy, layers=layers, x=x, gate=gate, hln=hln,
+                  mean2=mean2, rstd2=rstd2, z1=z1, a1=a1, hh=hh)
+    return y, sv
+
+
+class MSheathFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x0, gpol, mod, *params):
+        x0 = x0 if x0.is_contiguous() else x0.contiguous()
+        y, sv = forward(mod, x0, gpol, save=True)
+        ctx.mod, ctx.sv = mod, sv
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        mod, sv = ctx.mod, ctx.sv
+        ctx.sv = None
+        gy = gy if gy.is_contiguous() else gy.contiguous()
+        x0 = sv["x0"]
+        B, L, D = x0.shape
+        rows = B * L
+        dev = x0.device
+        st = _S()
+        touched = []
+
+        def gb(p):  # accumulation target p.grad (created zeroed on first use)
+            touched.append(p)
+            return ops._gbuf(p, True)
+
+        # ---- tail: y = x + gate * hh, hh = mlp2(silu(mlp0(LN(x)))), gate = sigmoid(mlp_gate(x))
+        x = sv["x"]
+        dx = _E(B, L, D, device=dev)
+        dhh = _E(B, L, D, device=dev)
+        dgate = _E(rows, device=dev)
+        lib.call("asrx_axpy_row_bwd2", _P(gy), _P(sv["gate"]), _P(sv["hh"]), _P(dhh), _P(dgate), _P(dx), rows, D, st)
+        mg = mod.mlp_gate[0]
+        lib.call("asrx_small_linear_bwd", _P(dgate), _P(sv["gate"]), _P(x), _P(mg.weight), _P(dx), _P(gb(mg.weight)),
+                 _P(gb(mg.bias)), rows, D, 1, SIG, 1.0, st)
+        m0, m2l = mod.mlp[0], mod.mlp[2]
+        da1 = G.linear_dgrad(dhh, m2l.weight)
+        G.linear_wgrad(dhh, sv["a1"], out=gb(m2l.weight), accumulate=True)
+        ops.colsum(dhh.view(rows, D), out=gb(m2l.bias))
+        lib.call("asrx_act_bwd", _P(da1), _P(sv["z1"]), _P(da1), da1.numel(), SILU, st)
+        dhln = G.linear_dgrad(da1, m0.weight)
+        G.linear_wgrad(da1, sv["hln"], out=gb(m0.weight), accumulate=True)
+        ops.colsum(da1.view(rows, -1), out=gb(m0.bias))
+        lib.call("asrx_layernorm_bwd_acc", _P(dhln), _P(x), _P(mod.mlp_ln.weight), _P(sv["mean2"]), _P(sv["rstd2"]),
+                 _P(dx), _P(gb(mod.mlp_ln.weight)), _P(gb(mod.mlp_ln.bias)), rows, D, 1, st)
+        del dhh, da1, dhln
+        # ---- layers, last to first
+        nl = len(mod.layers)
+        g_policy = _E(B, 3, device=dev)
+        has_orig = _E(B, dtype=torch.int32, device=dev)
+        lib.call("asrx_zero", _P(has_orig), B * 4, st)
+        dorig = _E(B, L, D, device=dev)  # written by the first jumping layer of each sample (has_orig)
+        g_mwo = None
+        mg_w, mg_b = mod.mem_gate[0].weight, mod.mem_gate[0].bias
+        for i in range(nl - 1, -1, -1):
+            s = sv["layers"][i]
+            lay = mod.layers[i]
+            vg = lay["v_gate"]
+            M, Dh = vg.mkey.shape[0], vg.mlp[0].weight.shape[0]
+            xi = s["x"]
+            dxi = _E(B, L, D, device=dev)
+            dxn = _E(B, L, D, device=dev)
+            dalpha, dbeta, dgam = _E(B, device=dev), _E(B, device=dev), _E(B, D, device=dev)
+            lib.call("asrx_jump_select4_bwd_acc", _P(dx), _P(s["x_new"]), _P(x0), _P(s["active"]), _P(s["alpha"]),
+                     _P(s["beta"]), _P(has_orig), _P(dxn), _P(dorig), _P(dxi), _P(dalpha), _P(dbeta), _P(dgam), B, L,
+                     D, st)
+            g_mem_v, g_mem_w, g_mem = _E(B, device=dev), _E(B, D, device=dev), _E(B, D, device=dev)
+            lib.call("asrx_msheath_ctrl_bwd2", _P(dalpha), _P(dbeta), _P(dgam), _P(g_mwo), _P(s["mem_v"]),
+                     _P(s["mem_w"]), s["ld_mw"], _P(s["mem"]), _P(mod.jump_s), _P(s["rec"]), i, nl, B, D,
+                     _P(g_policy), int(i != nl - 1), _P(g_mem_v), _P(g_mem_w), _P(g_mem), _P(gb(mod.jump_s)),
+                     _P(has_orig), st)
+            lib.call("asrx_small_linear_bwd", _P(g_mem_v), _P(s["mem_v"]), _P(s["mem"]), _P(mg_w), _P(g_mem),
+                     _P(gb(mg_w)), _P(gb(mg_b)), B, D, 1, SIG, 1.0, st)
+            dout = _E(B, L, D, device=dev)
+            dgv, dion = _E(rows, device=dev), _E(rows, device=dev)
+            lib.call("asrx_axpy_row2_bwd_acc", _P(dxn), _P(g_mem), 1.0 / L, _P(s["active"]), _P(s["g"]), _P(s["ion"]),
+                     _P(s["out"]), _P(dout), _P(dgv), _P(dion), _P(dxi), B, L, D, st)
+            del dxn
+            gw = lay["gate"][0]
+            dpx = _E(B, L, D, device=dev)
+            lib.call("asrx_small_linear_bwd", _P(dgv), _P(s["g"]), _P(s["px"]), _P(gw.weight), _P(dpx),
+                     _P(gb(gw.weight)), _P(gb(gw.bias)), rows, D, 1, SIG, 0.0, st)
+            ad = lay["adapter"]
+            if ad is not None:
+                G.linear_dgrad(dout, ad.weight, out=dpx, beta=1.0)
+                G.linear_wgrad(dout, s["px"], out=gb(ad.weight), accumulate=True)
+                ops.colsum(dout.view(rows, D), out=gb(ad.bias))
+            else:
+                lib.call("asrx_lincomb", _P(dpx), _P(dout), None, 1.0, 1.0, 0.0, _P(dpx), dpx.numel(), st)
+            del dout
+            ln = lay["ln"]
+            lib.call("asrx_layernorm_bwd_acc", _P(dpx), _P(xi), _P(ln.weight), _P(s["mean"]), _P(s["rstd"]), _P(dxi),
+                     _P(gb(ln.weight)), _P(gb(ln.bias)), rows, D, 1, st)
+            del dpx
+            # v_gate backward: ion's straight-through gradient dion (STthreshold, model.py:319-334)
+            dS, dnx, dh = _E(rows, M, device=dev), _E(rows, device=dev), _E(rows, Dh, device=dev)
+            dmval = gb(vg.mval)
+            dw2, db2 = gb(vg.mlp[2].weight), gb(vg.mlp[2].bias)
+            dcw, dcb = gb(vg.concat.weight), gb(vg.concat.bias)
+            lib.call("asrx_vgate_bwd", _P(dion), _P(s["S"]), _P(s["nx"]), _P(vg.mval), _P(s["h"]), _P(vg.mlp[2].weight),
+                     _P(vg.concat.weight), _P(s["kv"]), _P(s["m2"]), _P(dS), _P(dnx), _P(dh), _P(dmval), _P(dw2),
+                     _P(db2), _P(dcw), _P(dcb), rows, M, Dh, 1.0 / math.sqrt(D), st)
+            G.linear_dgrad(dS, s["mkeyn"], out=dxi, beta=1.0)
+            G.linear_dgrad(dh, vg.mlp[0].weight, out=dxi, beta=1.0)
+            lib.call("asrx_rownorm_bwd", _P(dnx), _P(xi), _P(s["nx"]), _P(dxi), rows, D, st)
+            dmk = G.linear_wgrad(dS, xi)
+            lib.call("asrx_row_normalize_bwd", _P(dmk), _P(s["mkeyn"]), _P(s["mkn"]), _P(gb(vg.mkey)), M, D, 1, st)
+            G.linear_wgrad(dh, xi, out=gb(vg.mlp[0].weight), accumulate=True)
+            ops.colsum(dh, out=gb(vg.mlp[0].bias))
+            del dS, dh, dmk
+            g_mwo = g_mem_w
+            dx = dxi
+        # layer 0's mem_w is the (1, 1, D) parameter broadcast over the samples
+        lib.call("asrx_colsum", _P(g_mwo), _P(gb(mod.mem_w)), B, D, st)
+        # policy = softmax(MPNet(pooled)) backward, then the pooled-mean broadcast and orig's jump grads
+        net = mod.pnet.net
+        g_pl = _E(B, 3, device=dev)
+        lib.call("asrx_softmax_small_bwd", _P(g_policy), _P(sv["policy"]), _P(g_pl), B, 3, st)
+        dhp = _E(sv["hp"].shape, device=dev)
+        lib.call("asrx_small_linear_bwd", _P(g_pl), None, _P(sv["hp"]), _P(net[2].weight), _P(dhp),
+                 _P(gb(net[2].weight)), _P(gb(net[2].bias)), B, dhp.shape[1], 3, 0, 0.0, st)
+        lib.call("asrx_act_bwd", _P(dhp), _P(sv["zp"]), _P(dhp), dhp.numel(), SILU, st)
+        dpooled = G.linear_dgrad(dhp, net[0].weight)
+        G.linear_wgrad(dhp, sv["pooled"], out=gb(net[0].weight), accumulate=True)
+        ops.colsum(dhp, out=gb(net[0].bias))
+        u = _E(B, D, device=dev)
+        lib.call("asrx_lincomb", _P(dpooled), None, None, 1.0 / L, 0.0, 0.0, _P(u), B * D, st)
+        lib.call("asrx_msheath_dx_final", _P(dx), _P(dorig), _P(has_orig), _P(u), B, L, D, st)
+        # announce each parameter's accumulated gradient once (asrx.dist.GradSync counts events)
+        seen = set()
+        for p in touched:
+            if id(p) not in seen:
+                seen.add(id(p))
+                ops._gret(p, p.grad, True)
+        return (dx, None, None) + (None,) * len(ctx.needs_input_grad[3:])
+
+
+def msheath(mod, x, gpol):
+    """Fused MSheath call.  Without autograd (the reference's dead blocks, eval, decoding) the forward
+    runs without saving anything for a backward."""
+    params = _params(mod)
+    if not torch.is_grad_enabled() or not (x.requires_grad or any(p.requires_grad for p in params)):
+        return forward(mod, x if x.is_contiguous() else x.contiguous(), gpol, save=False)[0]
+    return MSheathFn.apply(x, gpol, mod, *params)

@@ -28,13 +28,14 @@ __global__ __launch_bounds__(256) void msheath_ctrl_fwd_kernel(
     const float* __restrict__ mem_v, const float* __restrict__ mem_w, const float* __restrict__ mem,
     const float* __restrict__ jump_s, const float* __restrict__ next_i, int layer_i, int layers, int64_t L, int D,
     float* __restrict__ alpha, float* __restrict__ beta, float* __restrict__ gam, float* __restrict__ mem_w_out,
-    float* __restrict__ active, float* __restrict__ next_out, CtrlRec* __restrict__ rec) {
+    float* __restrict__ active, float* __restrict__ next_out, CtrlRec* __restrict__ rec, int64_t ld_mem_w) {
   __shared__ float red[4];
   const int64_t b = blockIdx.x;
   float s = 0.f;
   for (int64_t l = threadIdx.x; l < L; l += 256) s += ion[b * L + l];
   const float potential = block_sum<256>(s, red) / (float)L;  // ion.mean(dim=1), model.py:466
-  const float act = next_i[b] == (float)layer_i ? 1.f : 0.f;
+  const float ni = next_i ? next_i[b] : 0.f;  // null: every sample starts at layer 0
+  const float act = ni == (float)layer_i ? 1.f : 0.f;
   float ys[3] = {0.f, 0.f, 0.f};
   int action;
   float jump_g, low = 0.f;
@@ -70,7 +71,7 @@ __global__ __launch_bounds__(256) void msheath_ctrl_fwd_kernel(
   const float cg = jumped ? (1.f - jw) * jump_g : 0.f;
   const float mv = mem_v[b];
   for (int c = threadIdx.x; c < D; c += 256) {
-    const float mw = mem_w[b * D + c];
+    const float mw = mem_w[b * ld_mem_w + c];                 // ld 0: the (1, 1, D) parameter broadcast
     const float mwn = mv * mw + (1.f - mv) * mem[b * D + c];  // model.py:464
     gam[b * D + c] = cg * mwn;
     mem_w_out[b * D + c] = act != 0.f ? mwn : mw;
@@ -80,7 +81,7 @@ __global__ __launch_bounds__(256) void msheath_ctrl_fwd_kernel(
     beta[b] = be;
     active[b] = act;
     const float step = jumped ? (float)min(layer_i + action + 1, layers) : (float)(layer_i + 1);
-    next_out[b] = act != 0.f ? step : next_i[b];
+    next_out[b] = act != 0.f ? step : ni;
     CtrlRec r;
     r.ys[0] = ys[0];
     r.ys[1] = ys[1];
@@ -101,7 +102,8 @@ __global__ __launch_bounds__(256) void msheath_ctrl_bwd_kernel(
     const float* __restrict__ g_mwo, const float* __restrict__ mem_v, const float* __restrict__ mem_w,
     const float* __restrict__ mem, const float* __restrict__ jump_s, const CtrlRec* __restrict__ rec, int layer_i,
     int layers, int D, float* __restrict__ g_policy, float* __restrict__ g_mem_v, float* __restrict__ g_mem_w,
-    float* __restrict__ g_mem, float* __restrict__ g_jump_s) {
+    float* __restrict__ g_mem, float* __restrict__ g_jump_s, int64_t ld_mem_w, int* __restrict__ has_orig,
+    int acc_policy) {
   __shared__ float red[4];
   const int64_t b = blockIdx.x;
   const CtrlRec r = rec[b];
@@ -109,7 +111,7 @@ __global__ __launch_bounds__(256) void msheath_ctrl_bwd_kernel(
   const bool act = r.act != 0.f;
   float s_cg = 0.f, s_mv = 0.f;
   for (int c = threadIdx.x; c < D; c += 256) {
-    const float mw = mem_w[b * D + c], me = mem[b * D + c];
+    const float mw = mem_w[b * ld_mem_w + c], me = mem[b * D + c];
     const float mwn = mv * mw + (1.f - mv) * me;
     const float gg = g_gam[b * D + c];
     const float go = g_mwo ? g_mwo[b * D + c] : 0.f;
@@ -138,7 +140,9 @@ __global__ __launch_bounds__(256) void msheath_ctrl_bwd_kernel(
         if (r.ys[k] > r.ys[a]) a = k;
       for (int k = 0; k < 3; ++k) gp[k] = r.ys[k] * ((k == a ? 1.f : 0.f) - r.ys[a]) * g_jump;
     }
-    for (int k = 0; k < 3; ++k) g_policy[b * 3 + k] = gp[k];
+    for (int k = 0; k < 3; ++k) g_policy[b * 3 + k] = (acc_policy ? g_policy[b * 3 + k] : 0.f) + gp[k];
+    // jump_select4_bwd_acc of this layer wrote orig's gradient for a jumping active sample
+    if (has_orig && act && jumped && jw * r.jump_g != 0.f) has_orig[b] = 1;
   }
 }
 
@@ -266,11 +270,195 @@ __global__ __launch_bounds__(256) void jump_select4_bwd_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Fused-backward variants (asrx/msheath.py MSheathFn): every gradient contribution to a layer's input
+// x_i lands in ONE buffer -- written by the first producer, accumulated by the rest -- instead of
+// separate tensors that autograd sums with extra add kernels.
+//
+// jump_select backward, accumulate form.  Active samples: dxn = alpha g; orig's gradient
+// dorig (+)= beta g only when beta != 0 (a jump), the first jumping layer of a sample writing
+// (has_orig[b] == 0, set afterwards by msheath_ctrl_bwd); x_i's gradient is left to
+// axpy_row2_bwd_acc.  Inactive samples: dx = g (the pass-through), nothing else.
+__global__ __launch_bounds__(256) void jump_select4_bwd_acc_kernel(
+    const float4* __restrict__ g, const float4* __restrict__ xn, const float4* __restrict__ orig,
+    const float* __restrict__ act, const float* __restrict__ alpha, const float* __restrict__ beta,
+    const int* __restrict__ has_orig, float4* __restrict__ dxn, float4* __restrict__ dorig, float4* __restrict__ dx,
+    float* __restrict__ dalpha, float* __restrict__ dbeta, float* __restrict__ dgam, int64_t L, int d4, int lchunk) {
+  __shared__ float4 sg_s[8][32];
+  __shared__ float red[2][4];
+  const int lane = threadIdx.x & 31, grp = threadIdx.x >> 5;
+  const int cchunks = (d4 + 31) / 32;
+  const int cc = blockIdx.x % cchunks;
+  const int64_t b = blockIdx.y;
+  const int64_t l0 = (int64_t)(blockIdx.x / cchunks) * lchunk;
+  const int64_t l1 = min(L, l0 + lchunk);
+  const int c4 = cc * 32 + lane;
+  const bool a = act[b] != 0.f;
+  const float al = alpha[b], be = beta[b];
+  const bool jo = be != 0.f, acc_o = has_orig[b] != 0;
+  float sa = 0.f, sb = 0.f;
+  float4 sgv = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c4 < d4) {
+    for (int64_t l = l0 + grp; l < l1; l += 8) {
+      const int64_t i = (b * L + l) * d4 + c4;
+      const float4 gv = g[i];
+      if (a) {
+        const float4 u = xn[i], v = orig[i];
+        sa += gv.x * u.x + gv.y * u.y + gv.z * u.z + gv.w * u.w;
+        sb += gv.x * v.x + gv.y * v.y + gv.z * v.z + gv.w * v.w;
+        sgv.x += gv.x; sgv.y += gv.y; sgv.z += gv.z; sgv.w += gv.w;
+        dxn[i] = make_float4(al * gv.x, al * gv.y, al * gv.z, al * gv.w);
+        if (jo) {
+          float4 o = make_float4(be * gv.x, be * gv.y, be * gv.z, be * gv.w);
+          if (acc_o) {
+            const float4 p = dorig[i];
+            o.x += p.x; o.y += p.y; o.z += p.z; o.w += p.w;
+          }
+          dorig[i] = o;
+        }
+      } else {
+        dx[i] = gv;
+      }
+    }
+  }
+  if (!a) return;  // uniform per workgroup
+  sg_s[grp][lane] = sgv;
+  sa = wave_sum(sa);
+  sb = wave_sum(sb);
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = sa;
+    red[1][threadIdx.x >> 6] = sb;
+  }
+  __syncthreads();
+  if (threadIdx.x < 128) {
+    const int cl = threadIdx.x >> 2, q = threadIdx.x & 3;
+    const int c4b = cc * 32 + cl;
+    if (c4b < d4) {
+      float t = 0.f;
+      for (int g2 = 0; g2 < 8; ++g2) {
+        const float4 v = sg_s[g2][cl];
+        t += q == 0 ? v.x : q == 1 ? v.y : q == 2 ? v.z : v.w;
+      }
+      atomicAdd(dgam + b * 4 * d4 + 4 * c4b + q, t);
+    }
+  } else if (threadIdx.x == 128) {
+    atomicAdd(dalpha + b, red[0][0] + red[0][1] + red[0][2] + red[0][3]);
+    atomicAdd(dbeta + b, red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+  }
+}
+
+// x_new = x + s1 s2 y (model.py:461) and mem = mean_l x_new (model.py:463) backward, for active
+// samples: g' = dxn + gm[b] / L (the seg-mean broadcast folded in), dy = s1 s2 g', ds1 = s2 g'.y,
+// ds2 = s1 g'.y, and dx = g' -- the first contribution to x_i of an active sample.  Inactive
+// samples: dy = 0, ds = 0, dx untouched (jump_select4_bwd_acc wrote the pass-through).
+__global__ __launch_bounds__(256) void axpy_row2_bwd_acc_kernel(const float4* __restrict__ dxn,
+                                                                const float* __restrict__ gm, float invL,
+                                                                const float* __restrict__ act,
+                                                                const float* __restrict__ s1, const float* __restrict__ s2,
+                                                                const float4* __restrict__ y, float4* __restrict__ dy,
+                                                                float* __restrict__ ds1, float* __restrict__ ds2,
+                                                                float4* __restrict__ dx, int64_t rows, int64_t L, int d4) {
+  const int lane = threadIdx.x & 63;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += (int64_t)gridDim.x * 4) {
+    const int64_t b = r / L;
+    if (act[b] == 0.f) {
+      for (int j = lane; j < d4; j += 64) dy[r * d4 + j] = z4;
+      if (lane == 0) {
+        ds1[r] = 0.f;
+        if (ds2) ds2[r] = 0.f;
+      }
+      continue;
+    }
+    const float a = s1[r], c = s2 ? s2[r] : 1.f;
+    const float sc = a * c;
+    const float4* gm4 = reinterpret_cast<const float4*>(gm + b * 4 * d4);
+    float t = 0.f;
+    for (int j = lane; j < d4; j += 64) {
+      float4 gv = dxn[r * d4 + j];
+      if (gm) {
+        const float4 m = gm4[j];
+        gv.x += m.x * invL; gv.y += m.y * invL; gv.z += m.z * invL; gv.w += m.w * invL;
+      }
+      const float4 yv = y[r * d4 + j];
+      t += gv.x * yv.x + gv.y * yv.y + gv.z * yv.z + gv.w * yv.w;
+      dy[r * d4 + j] = make_float4(sc * gv.x, sc * gv.y, sc * gv.z, sc * gv.w);
+      dx[r * d4 + j] = gv;
+    }
+    t = wave_sum(t);
+    if (lane == 0) {
+      ds1[r] = c * t;
+      if (ds2) ds2[r] = a * t;
+    }
+  }
+}
+
+// dx += (has_orig[b] ? dorig : 0) + u[b, :]   (orig's jump gradient and the pooled-mean broadcast of
+// the MSheath input, model.py:432-435, 497)
+__global__ void msheath_dx_final_kernel(float4* __restrict__ dx, const float4* __restrict__ dorig,
+                                        const int* __restrict__ has_orig, const float4* __restrict__ u, int64_t B,
+                                        int64_t L, int d4) {
+  const int64_t total = B * L * d4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = i / (L * d4);
+    float4 v = dx[i];
+    if (u) {
+      const float4 w = u[b * d4 + i % d4];
+      v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+    }
+    if (has_orig[b]) {
+      const float4 w = dorig[i];
+      v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+    }
+    dx[i] = v;
+  }
+}
+
 }  // namespace asrx
 
 using namespace asrx;
 
 extern "C" {
+
+int asrx_jump_select4_bwd_acc(const float* g, const float* xn, const float* orig, const float* act,
+                              const float* alpha, const float* beta, const int* has_orig, float* dxn, float* dorig,
+                              float* dx, float* dalpha, float* dbeta, float* dgam, int64_t B, int64_t L, int64_t d,
+                              hipStream_t stream) {
+  ASRX_REQUIRE(d % 4 == 0, "asrx_jump_select4_bwd_acc: d % 4 != 0");
+  if (B * L == 0) return 0;
+  (void)hipMemsetAsync(dalpha, 0, B * sizeof(float), stream);
+  (void)hipMemsetAsync(dbeta, 0, B * sizeof(float), stream);
+  (void)hipMemsetAsync(dgam, 0, B * d * sizeof(float), stream);
+  const int d4 = (int)(d / 4);
+  const int lchunk = 128;
+  dim3 grid((unsigned)(((d4 + 31) / 32) * ((L + lchunk - 1) / lchunk)), (unsigned)B);
+  jump_select4_bwd_acc_kernel<<<grid, 256, 0, stream>>>((const float4*)g, (const float4*)xn, (const float4*)orig, act,
+                                                        alpha, beta, has_orig, (float4*)dxn, (float4*)dorig,
+                                                        (float4*)dx, dalpha, dbeta, dgam, L, d4, lchunk);
+  ASRX_LAUNCHED("asrx_jump_select4_bwd_acc");
+}
+
+int asrx_axpy_row2_bwd_acc(const float* dxn, const float* gm, float invL, const float* act, const float* s1,
+                           const float* s2, const float* y, float* dy, float* ds1, float* ds2, float* dx, int64_t B,
+                           int64_t L, int64_t d, hipStream_t stream) {
+  ASRX_REQUIRE(d % 4 == 0, "asrx_axpy_row2_bwd_acc: d % 4 != 0");
+  const int64_t rows = B * L;
+  if (rows == 0) return 0;
+  axpy_row2_bwd_acc_kernel<<<(unsigned)std::min<int64_t>((rows + 3) / 4, 8192), 256, 0, stream>>>(
+      (const float4*)dxn, gm, invL, act, s1, s2, (const float4*)y, (float4*)dy, ds1, ds2, (float4*)dx, rows, L,
+      (int)(d / 4));
+  ASRX_LAUNCHED("asrx_axpy_row2_bwd_acc");
+}
+
+int asrx_msheath_dx_final(float* dx, const float* dorig, const int* has_orig, const float* u, int64_t B, int64_t L,
+                          int64_t d, hipStream_t stream) {
+  ASRX_REQUIRE(d % 4 == 0, "asrx_msheath_dx_final: d % 4 != 0");
+  if (B * L == 0) return 0;
+  const int64_t n = B * L * d / 4;
+  msheath_dx_final_kernel<<<(unsigned)std::min<int64_t>((n + 255) / 256, 16384), 256, 0, stream>>>(
+      (float4*)dx, (const float4*)dorig, has_orig, (const float4*)u, B, L, (int)(d / 4));
+  ASRX_LAUNCHED("asrx_msheath_dx_final");
+}
 
 int asrx_msheath_ctrl_fwd(const float* policy, const float* gpol, int64_t ld_gpol, const float* ion,
                           const float* mem_v, const float* mem_w, const float* mem, const float* jump_s,
@@ -280,8 +468,22 @@ int asrx_msheath_ctrl_fwd(const float* policy, const float* gpol, int64_t ld_gpo
   if (B == 0) return 0;
   msheath_ctrl_fwd_kernel<<<(unsigned)B, 256, 0, stream>>>(policy, gpol, ld_gpol, ion, mem_v, mem_w, mem, jump_s,
                                                            next_i, (int)layer_i, (int)layers, L, (int)D, alpha, beta,
-                                                           gam, mem_w_out, active, next_out, (CtrlRec*)rec);
+                                                           gam, mem_w_out, active, next_out, (CtrlRec*)rec, D);
   ASRX_LAUNCHED("asrx_msheath_ctrl_fwd");
+}
+
+// As asrx_msheath_ctrl_fwd with mem_w's row stride (0 = the parameter broadcast over samples) and a
+// nullable next_i (all samples at layer 0).
+int asrx_msheath_ctrl_fwd2(const float* policy, const float* gpol, int64_t ld_gpol, const float* ion,
+                           const float* mem_v, const float* mem_w, int64_t ld_mem_w, const float* mem,
+                           const float* jump_s, const float* next_i, int64_t layer_i, int64_t layers, int64_t B,
+                           int64_t L, int64_t D, float* alpha, float* beta, float* gam, float* mem_w_out, float* active,
+                           float* next_out, void* rec, hipStream_t stream) {
+  if (B == 0) return 0;
+  msheath_ctrl_fwd_kernel<<<(unsigned)B, 256, 0, stream>>>(policy, gpol, ld_gpol, ion, mem_v, mem_w, mem, jump_s,
+                                                           next_i, (int)layer_i, (int)layers, L, (int)D, alpha, beta,
+                                                           gam, mem_w_out, active, next_out, (CtrlRec*)rec, ld_mem_w);
+  ASRX_LAUNCHED("asrx_msheath_ctrl_fwd2");
 }
 
 int asrx_msheath_ctrl_bwd(const float* g_alpha, const float* g_beta, const float* g_gam, const float* g_mwo,
@@ -291,8 +493,23 @@ int asrx_msheath_ctrl_bwd(const float* g_alpha, const float* g_beta, const float
   if (B == 0) return 0;
   msheath_ctrl_bwd_kernel<<<(unsigned)B, 256, 0, stream>>>(g_alpha, g_beta, g_gam, g_mwo, mem_v, mem_w, mem, jump_s,
                                                            (const CtrlRec*)rec, (int)layer_i, (int)layers, (int)D,
-                                                           g_policy, g_mem_v, g_mem_w, g_mem, g_jump_s);
+                                                           g_policy, g_mem_v, g_mem_w, g_mem, g_jump_s, D, nullptr, 0);
   ASRX_LAUNCHED("asrx_msheath_ctrl_bwd");
+}
+
+// As asrx_msheath_ctrl_bwd with mem_w's row stride, g_policy accumulated when acc_policy != 0, and
+// has_orig[b] set when this layer's jump wrote orig's gradient (see jump_select4_bwd_acc).
+int asrx_msheath_ctrl_bwd2(const float* g_alpha, const float* g_beta, const float* g_gam, const float* g_mwo,
+                           const float* mem_v, const float* mem_w, int64_t ld_mem_w, const float* mem,
+                           const float* jump_s, const void* rec, int64_t layer_i, int64_t layers, int64_t B, int64_t D,
+                           float* g_policy, int acc_policy, float* g_mem_v, float* g_mem_w, float* g_mem,
+                           float* g_jump_s, int* has_orig, hipStream_t stream) {
+  if (B == 0) return 0;
+  msheath_ctrl_bwd_kernel<<<(unsigned)B, 256, 0, stream>>>(g_alpha, g_beta, g_gam, g_mwo, mem_v, mem_w, mem, jump_s,
+                                                           (const CtrlRec*)rec, (int)layer_i, (int)layers, (int)D,
+                                                           g_policy, g_mem_v, g_mem_w, g_mem, g_jump_s, ld_mem_w,
+                                                           has_orig, acc_policy);
+  ASRX_LAUNCHED("asrx_msheath_ctrl_bwd2");
 }
 
 int64_t asrx_msheath_rec_bytes(void) { return (int64_t)sizeof(CtrlRec); }

@@ -101,7 +101,7 @@ __global__ __launch_bounds__(64 * RW) void ln_bwd_t_kernel(const float* __restri
                                                            const float* __restrict__ w, const float* __restrict__ mean,
                                                            const float* __restrict__ rstd, float* __restrict__ dx,
                                                            float* __restrict__ dw, float* __restrict__ db,
-                                                           int64_t rows) {
+                                                           int64_t rows, int acc) {
   constexpr int D = 64 * E;
   __shared__ float part[RW][2 * D];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -127,8 +127,9 @@ __global__ __launch_bounds__(64 * RW) void ln_bwd_t_kernel(const float* __restri
     s1 = wave_sum_dpp(s1) * (1.0f / D);
     s2 = wave_sum_dpp(s2) * (1.0f / D);
     float dv[E];
+    if (acc) ld_lane<E>(dx + r * D, lane, dv);
 #pragma unroll
-    for (int e = 0; e < E; ++e) dv[e] = rs * (gv[e] * wv[e] - s1 - xv[e] * s2);
+    for (int e = 0; e < E; ++e) dv[e] = (acc ? dv[e] : 0.f) + rs * (gv[e] * wv[e] - s1 - xv[e] * s2);
     st_lane<E>(dx + r * D, lane, dv);
   }
 #pragma unroll
@@ -178,7 +179,7 @@ __global__ __launch_bounds__(64 * RW) void ln_bwd_kernel(const float* __restrict
                                                          const float* __restrict__ w, const float* __restrict__ mean,
                                                          const float* __restrict__ rstd, float* __restrict__ dx,
                                                          float* __restrict__ dw, float* __restrict__ db, int64_t rows,
-                                                         int d) {
+                                                         int d, int acc) {
   extern __shared__ float part[];  // [RW][2*d]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   float* pw = part + wid * 2 * d;
@@ -201,7 +202,7 @@ __global__ __launch_bounds__(64 * RW) void ln_bwd_kernel(const float* __restrict
     float* dxr = dx + r * d;
     for (int j = lane; j < d; j += 64) {
       const float xh = (xr[j] - mu) * rs;
-      dxr[j] = rs * (gr[j] * w[j] - s1 - xh * s2);
+      dxr[j] = (acc ? dxr[j] : 0.f) + rs * (gr[j] * w[j] - s1 - xh * s2);
     }
   }
   __syncthreads();
@@ -529,9 +530,11 @@ __global__ void axpy_row_kernel(const float* __restrict__ x, const float* __rest
 }
 
 // ds[r] = sum_j g[r,j] * y[r,j] ;  dy = s[r] * g  (dy may alias nothing)
+// (dxc, when non-null, receives a copy of g: x's pass-through gradient as a buffer the caller owns)
 __global__ __launch_bounds__(64 * RW) void axpy_row_bwd_kernel(const float* __restrict__ g, const float* __restrict__ s,
                                                                const float* __restrict__ y, float* __restrict__ dy,
-                                                               float* __restrict__ ds, int64_t rows, int d) {
+                                                               float* __restrict__ ds, int64_t rows, int d,
+                                                               float* __restrict__ dxc) {
   const int lane = threadIdx.x & 63;
   for (int64_t r = row_begin(); r < rows; r += row_step()) {
     const float sc = s[r];
@@ -540,6 +543,7 @@ __global__ __launch_bounds__(64 * RW) void axpy_row_bwd_kernel(const float* __re
       const float gv = g[r * d + j];
       acc += gv * y[r * d + j];
       dy[r * d + j] = sc * gv;
+      if (dxc) dxc[r * d + j] = gv;
     }
     acc = wave_sum(acc);
     if (lane == 0) ds[r] = acc;
@@ -1370,6 +1374,57 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(const float* __restrict__ z
   }
 }
 
+// F.normalize(x, p=2, dim=-1) rows (v_gate's memory keys, model.py:347): y = x / max(|x|, 1e-12),
+// n = max(|x|, 1e-12); backward dx (+)= (dy - y (y.dy)) / n (the clamp is never active at random
+// init, |mkey| ~ sqrt(D); a clamped row gets dy / n).
+__global__ __launch_bounds__(64 * RW) void row_normalize_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                                float* __restrict__ n, int64_t rows, int d) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t r = row_begin(); r < rows; r += row_step()) {
+    float s = 0.f;
+    for (int j = lane; j < d; j += 64) s += x[r * d + j] * x[r * d + j];
+    const float nn = fmaxf(sqrtf(wave_sum(s)), 1e-12f);
+    for (int j = lane; j < d; j += 64) y[r * d + j] = x[r * d + j] / nn;
+    if (lane == 0) n[r] = nn;
+  }
+}
+__global__ __launch_bounds__(64 * RW) void row_normalize_bwd_kernel(const float* __restrict__ dy,
+                                                                    const float* __restrict__ y,
+                                                                    const float* __restrict__ n, float* __restrict__ dx,
+                                                                    int64_t rows, int d, int acc) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t r = row_begin(); r < rows; r += row_step()) {
+    const float nn = n[r];
+    float s = 0.f;
+    for (int j = lane; j < d; j += 64) s += y[r * d + j] * dy[r * d + j];
+    s = wave_sum(s);
+    const bool clamped = nn <= 1e-12f;
+    for (int j = lane; j < d; j += 64) {
+      const float v = (dy[r * d + j] - (clamped ? 0.f : y[r * d + j] * s)) / nn;
+      dx[r * d + j] = (acc ? dx[r * d + j] : 0.f) + v;
+    }
+  }
+}
+
+// softmax over short rows (N <= 8): MPNet's policy, model.py:385
+__global__ void softmax_small_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t rows, int N) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += (int64_t)gridDim.x * blockDim.x) {
+    float m = -INFINITY;
+    for (int k = 0; k < N; ++k) m = fmaxf(m, x[r * N + k]);
+    float s = 0.f;
+    for (int k = 0; k < N; ++k) s += expf(x[r * N + k] - m);
+    for (int k = 0; k < N; ++k) y[r * N + k] = expf(x[r * N + k] - m) / s;
+  }
+}
+__global__ void softmax_small_bwd_kernel(const float* __restrict__ g, const float* __restrict__ y, float* __restrict__ dx,
+                                         int64_t rows, int N) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < N; ++k) s += g[r * N + k] * y[r * N + k];
+    for (int k = 0; k < N; ++k) dx[r * N + k] = y[r * N + k] * (g[r * N + k] - s);
+  }
+}
+
 }  // namespace asrx
 
 using namespace asrx;
@@ -1396,25 +1451,31 @@ int asrx_layernorm_fwd(const float* x, const float* w, const float* b, float* y,
   ASRX_LAUNCHED("asrx_layernorm_fwd");
 }
 
-int asrx_layernorm_bwd(const float* dy, const float* x, const float* w, const float* mean, const float* rstd,
-                       float* dx, float* dw, float* db, int64_t rows, int64_t d, hipStream_t stream) {
+int asrx_layernorm_bwd_acc(const float* dy, const float* x, const float* w, const float* mean, const float* rstd,
+                           float* dx, float* dw, float* db, int64_t rows, int64_t d, int acc, hipStream_t stream) {
   ASRX_REQUIRE(d <= 2048, "layernorm_bwd: d too large");
   if (rows == 0) return 0;
   const bool al = ((((uintptr_t)dy | (uintptr_t)x | (uintptr_t)w | (uintptr_t)dx) & 7) == 0);
   const unsigned g = row_grid(rows, 1024);
   switch (al ? d : 0) {
-    case 128: ln_bwd_t_kernel<2><<<g, 64 * RW, 0, stream>>>(dy, x, w, mean, rstd, dx, dw, db, rows); break;
-    case 256: ln_bwd_t_kernel<4><<<g, 64 * RW, 0, stream>>>(dy, x, w, mean, rstd, dx, dw, db, rows); break;
-    case 384: ln_bwd_t_kernel<6><<<g, 64 * RW, 0, stream>>>(dy, x, w, mean, rstd, dx, dw, db, rows); break;
-    case 512: ln_bwd_t_kernel<8><<<g, 64 * RW, 0, stream>>>(dy, x, w, mean, rstd, dx, dw, db, rows); break;
-    case 768: ln_bwd_t_kernel<12><<<g, 64 * RW, 0, stream>>>(dy, x, w, mean, rstd, dx, dw, db, rows); break;
-    case 1024: ln_bwd_t_kernel<16><<<g, 64 * RW, 0, stream>>>(dy, x, w, mean, rstd, dx, dw, db, rows); break;
+    case 128: ln_bwd_t_kernel<2><<<g, 64 * RW, 0, stream>>>(dy, x, w, mean, rstd, dx, dw, db, rows, acc); break;
+    case 256: ln_bwd_t_kernel<4><<<g, 64 * RW, 0, stream>>>(dy, x, w, mean, rstd, dx, dw, db, rows, acc); break;
+    case 384: ln_bwd_t_kernel<6><<<g, 64 * RW, 0, stream>>>(dy, x, w, mean, rstd, dx, dw, db, rows, acc); break;
+    case 512: ln_bwd_t_kernel<8><<<g, 64 * RW, 0, stream>>>(dy, x, w, mean, rstd, dx, dw, db, rows, acc); break;
+    case 768: ln_bwd_t_kernel<12><<<g, 64 * RW, 0, stream>>>(dy, x, w, mean, rstd, dx, dw, db, rows, acc); break;
+    case 1024: ln_bwd_t_kernel<16><<<g, 64 * RW, 0, stream>>>(dy, x, w, mean, rstd, dx, dw, db, rows, acc); break;
     default: {
       const size_t shm = (size_t)RW * 2 * d * sizeof(float);
-      ln_bwd_kernel<<<g, 64 * RW, shm, stream>>>(dy, x, w, mean, rstd, dx, dw, db, rows, (int)d);
+      ln_bwd_kernel<<<g, 64 * RW, shm, stream>>>(dy, x, w, mean, rstd, dx, dw, db, rows, (int)d, acc);
     }
   }
   ASRX_LAUNCHED("asrx_layernorm_bwd");
+}
+
+// dx = LN backward (overwritten); dw / db accumulated.
+int asrx_layernorm_bwd(const float* dy, const float* x, const float* w, const float* mean, const float* rstd,
+                       float* dx, float* dw, float* db, int64_t rows, int64_t d, hipStream_t stream) {
+  return asrx_layernorm_bwd_acc(dy, x, w, mean, rstd, dx, dw, db, rows, d, 0, stream);
 }
 
 int asrx_small_linear_fwd(const float* x, const float* W, const float* b, float* y, int64_t rows, int64_t K,
@@ -1444,6 +1505,44 @@ int asrx_small_linear_bwd(const float* dy, const float* y, const float* x, const
     default: ASRX_REQUIRE(false, "small_linear: N=%ld not in 1..4", (long)N);
   }
   ASRX_LAUNCHED("asrx_small_linear_bwd");
+}
+
+int asrx_row_normalize(const float* x, float* y, float* n, int64_t rows, int64_t d, hipStream_t stream) {
+  if (rows == 0) return 0;
+  LAUNCH_ROWS(row_normalize_kernel, rows, 0, x, y, n, rows, (int)d);
+  ASRX_LAUNCHED("asrx_row_normalize");
+}
+
+int asrx_row_normalize_bwd(const float* dy, const float* y, const float* n, float* dx, int64_t rows, int64_t d,
+                           int acc, hipStream_t stream) {
+  if (rows == 0) return 0;
+  LAUNCH_ROWS(row_normalize_bwd_kernel, rows, 0, dy, y, n, dx, rows, (int)d, acc);
+  ASRX_LAUNCHED("asrx_row_normalize_bwd");
+}
+
+int asrx_softmax_small(const float* x, float* y, int64_t rows, int64_t N, hipStream_t stream) {
+  ASRX_REQUIRE(N >= 1 && N <= 8, "softmax_small: N in 1..8");
+  if (rows == 0) return 0;
+  softmax_small_kernel<<<ew_grid(rows, 1024), 256, 0, stream>>>(x, y, rows, (int)N);
+  ASRX_LAUNCHED("asrx_softmax_small");
+}
+
+int asrx_softmax_small_bwd(const float* g, const float* y, float* dx, int64_t rows, int64_t N, hipStream_t stream) {
+  ASRX_REQUIRE(N >= 1 && N <= 8, "softmax_small: N in 1..8");
+  if (rows == 0) return 0;
+  softmax_small_bwd_kernel<<<ew_grid(rows, 1024), 256, 0, stream>>>(g, y, dx, rows, (int)N);
+  ASRX_LAUNCHED("asrx_softmax_small_bwd");
+}
+
+// zero `bytes` bytes of device memory (stream-ordered memset; no ATen fill kernel)
+int asrx_zero(void* p, int64_t bytes, hipStream_t stream) {
+  if (bytes == 0) return 0;
+  hipError_t e = hipMemsetAsync(p, 0, (size_t)bytes, stream);
+  if (e != hipSuccess) {
+    set_error("asrx_zero: %s", hipGetErrorString(e));
+    return (int)e;
+  }
+  return 0;
 }
 
 int asrx_rownorm(const float* x, float* n, int64_t rows, int64_t d, hipStream_t stream) {
@@ -1519,8 +1618,15 @@ int asrx_axpy_row(const float* x, const float* s, const float* y, float* out, in
 int asrx_axpy_row_bwd(const float* g, const float* s, const float* y, float* dy, float* ds, int64_t rows, int64_t d,
                       hipStream_t stream) {
   if (rows == 0) return 0;
-  LAUNCH_ROWS(axpy_row_bwd_kernel, rows, 0, g, s, y, dy, ds, rows, (int)d);
+  LAUNCH_ROWS(axpy_row_bwd_kernel, rows, 0, g, s, y, dy, ds, rows, (int)d, (float*)nullptr);
   ASRX_LAUNCHED("asrx_axpy_row_bwd");
+}
+
+int asrx_axpy_row_bwd2(const float* g, const float* s, const float* y, float* dy, float* ds, float* dxc, int64_t rows,
+                       int64_t d, hipStream_t stream) {
+  if (rows == 0) return 0;
+  LAUNCH_ROWS(axpy_row_bwd_kernel, rows, 0, g, s, y, dy, ds, rows, (int)d, dxc);
+  ASRX_LAUNCHED("asrx_axpy_row_bwd2");
 }
 
 int asrx_jump_select(const float* xn, const float* orig, const float* xold, const float* act, const float* alpha,

@@ -121,6 +121,9 @@ int asrx_layernorm_fwd(const float* x, const float* w, const float* b, float* y,
                        int64_t rows, int64_t d, float eps, asrx_stream_t stream);
 int asrx_layernorm_bwd(const float* dy, const float* x, const float* w, const float* mean, const float* rstd,
                        float* dx, float* dw, float* db, int64_t rows, int64_t d, asrx_stream_t stream);
+/* acc != 0: dx += the LayerNorm input gradient (one buffer collects every consumer's contribution). */
+int asrx_layernorm_bwd_acc(const float* dy, const float* x, const float* w, const float* mean, const float* rstd,
+                           float* dx, float* dw, float* db, int64_t rows, int64_t d, int acc, asrx_stream_t stream);
 
 /* ---- small-N linear (N <= 4): gate / mem_gate / mlp_gate Linear(D,1) (model.py:398, 406, 420),
  *      v_gate.mlp[2] (341), tgate.cs Linear(D,3) (530), MPNet's Linear(128,3) (381).
@@ -135,6 +138,16 @@ int asrx_small_linear_bwd(const float* dy, const float* y, const float* x, const
 int asrx_rownorm(const float* x, float* n, int64_t rows, int64_t d, asrx_stream_t stream);
 int asrx_rownorm_bwd(const float* dn, const float* x, const float* n, float* dx, int64_t rows, int64_t d,
                      asrx_stream_t stream);
+/* F.normalize(x, p=2, dim=-1) (v_gate's keys, model.py:347): y, n = max(|x|, 1e-12); backward
+ * dx (+)= (dy - y (y.dy)) / n. */
+int asrx_row_normalize(const float* x, float* y, float* n, int64_t rows, int64_t d, asrx_stream_t stream);
+int asrx_row_normalize_bwd(const float* dy, const float* y, const float* n, float* dx, int64_t rows, int64_t d,
+                           int acc, asrx_stream_t stream);
+/* softmax over rows of N <= 8 (MPNet policy, model.py:385) and its backward. */
+int asrx_softmax_small(const float* x, float* y, int64_t rows, int64_t N, asrx_stream_t stream);
+int asrx_softmax_small_bwd(const float* g, const float* y, float* dx, int64_t rows, int64_t N, asrx_stream_t stream);
+/* stream-ordered memset of device memory to zero */
+int asrx_zero(void* p, int64_t bytes, asrx_stream_t stream);
 
 /* ---- rotary (model.py:198-214) fused with the hd^-0.25 pre-scale (303-304); x (B,L,H*hd),
  *      m[B*L] = |src| rows, f[hd/2] float32 frequencies; dm accumulated in backward. ------------- */
@@ -163,6 +176,9 @@ int asrx_axpy_row(const float* x, const float* s, const float* y, float* out, in
                   asrx_stream_t stream);
 int asrx_axpy_row_bwd(const float* g, const float* s, const float* y, float* dy, float* ds, int64_t rows,
                       int64_t d, asrx_stream_t stream);
+/* as asrx_axpy_row_bwd, and dxc = g (x's pass-through gradient into a caller-owned buffer) */
+int asrx_axpy_row_bwd2(const float* g, const float* s, const float* y, float* dy, float* ds, float* dxc,
+                       int64_t rows, int64_t d, asrx_stream_t stream);
 int asrx_jump_select(const float* xn, const float* orig, const float* xold, const float* act, const float* alpha,
                      const float* beta, const float* gam, float* out, int64_t B, int64_t L, int64_t d,
                      asrx_stream_t stream);
@@ -182,6 +198,31 @@ int asrx_msheath_ctrl_bwd(const float* g_alpha, const float* g_beta, const float
                           const void* rec, int64_t layer_i, int64_t layers, int64_t B, int64_t D, float* g_policy,
                           float* g_mem_v, float* g_mem_w, float* g_mem, float* g_jump_s, asrx_stream_t stream);
 int64_t asrx_msheath_rec_bytes(void);
+/* ctrl with mem_w's row stride (0: the (1,1,D) parameter broadcast over samples) and a nullable
+ * next_i (every sample at layer 0); backward with g_policy accumulated (acc_policy) and has_orig[b]
+ * set when this layer's jump wrote orig's gradient (asrx_jump_select4_bwd_acc). */
+int asrx_msheath_ctrl_fwd2(const float* policy, const float* gpol, int64_t ld_gpol, const float* ion,
+                           const float* mem_v, const float* mem_w, int64_t ld_mem_w, const float* mem,
+                           const float* jump_s, const float* next_i, int64_t layer_i, int64_t layers, int64_t B,
+                           int64_t L, int64_t D, float* alpha, float* beta, float* gam, float* mem_w_out, float* active,
+                           float* next_out, void* rec, asrx_stream_t stream);
+int asrx_msheath_ctrl_bwd2(const float* g_alpha, const float* g_beta, const float* g_gam, const float* g_mwo,
+                           const float* mem_v, const float* mem_w, int64_t ld_mem_w, const float* mem,
+                           const float* jump_s, const void* rec, int64_t layer_i, int64_t layers, int64_t B, int64_t D,
+                           float* g_policy, int acc_policy, float* g_mem_v, float* g_mem_w, float* g_mem,
+                           float* g_jump_s, int* has_orig, asrx_stream_t stream);
+/* MSheath fused backward (asrx/msheath.py): jump_select backward in accumulate form (active: dxn =
+ * alpha g, orig's gradient (+)= beta g on a jump; inactive: dx = g), the x_new/mem backward writing
+ * x's gradient for active samples (g' = dxn + gm/L), and the final dx += orig grad + u broadcast. */
+int asrx_jump_select4_bwd_acc(const float* g, const float* xn, const float* orig, const float* act,
+                              const float* alpha, const float* beta, const int* has_orig, float* dxn, float* dorig,
+                              float* dx, float* dalpha, float* dbeta, float* dgam, int64_t B, int64_t L, int64_t d,
+                              asrx_stream_t stream);
+int asrx_axpy_row2_bwd_acc(const float* dxn, const float* gm, float invL, const float* act, const float* s1,
+                           const float* s2, const float* y, float* dy, float* ds1, float* ds2, float* dx, int64_t B,
+                           int64_t L, int64_t d, asrx_stream_t stream);
+int asrx_msheath_dx_final(float* dx, const float* dorig, const int* has_orig, const float* u, int64_t B, int64_t L,
+                          int64_t d, asrx_stream_t stream);
 /* out = x + s1[r] * s2[r] * y (s2 may be NULL), d % 4 == 0 (model.py:461: x + gate * ion * out). */
 int asrx_axpy_row2(const float* x, const float* s1, const float* s2, const float* y, float* out, int64_t rows,
                    int64_t d, asrx_stream_t stream);

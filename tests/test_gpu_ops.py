@@ -250,8 +250,12 @@ def test_tgate(cuda):
     assert _rel(gg[0], gr[0]) < 1e-4
 
 
-def test_msheath(cuda):
-    """Batched masked MSheath vs the per-sample while-loop restatement, with jumps exercised."""
+@pytest.mark.parametrize("fused", [True, False])
+def test_msheath(cuda, fused):
+    """MSheath (model.py:387-507), the fused single-node path (asrx/msheath.py, hand-written backward)
+    and the per-op composition, against the oracle's per-sample while-loop: output, input gradient and
+    every parameter's gradient, with potentials spread around the 0.1 threshold so samples take
+    different layer/jump trajectories."""
     from asrx import ops  # noqa: F401
     from asrx.model import MSheath
     from asrx.noise import NoiseCtx
@@ -259,13 +263,15 @@ def test_msheath(cuda):
     torch.manual_seed(3)
     D, layer = 128, 4
     mod = MSheath(D, 2, layer).cuda()
+    mod.fused = fused
     with torch.no_grad():
         for i in range(layer):  # spread x_val around the 0.3 threshold so potentials vary per sample
             mod.layers[i]["v_gate"].concat.bias.fill_(0.3 + 0.1 * (i - 1))
     B, L = 4, 30
     x = torch.randn(B, L, D)
     x[1] *= 0.1
-    P = {f"j.{k}": v.detach().cpu().double() for k, v in mod.state_dict().items()}
+    trainable = {n for n, p in mod.named_parameters() if p.requires_grad}  # v_gate.tx is frozen
+    P = {f"j.{k}": v.detach().cpu().double().requires_grad_(k in trainable) for k, v in mod.state_dict().items()}
     seed, step, site, sid_base = 9, 1, "t.jump", 5
     noise = NoiseCtx(seed, step, True)
     onoise = om.Noise(seed, step, torch.float64)
@@ -274,6 +280,16 @@ def test_msheath(cuda):
                             lambda a: om.msheath(P, "j", a, layer, gpol), [x])
     assert _rel(yg, yr) < 1e-5
     assert _rel(gg[0], gr[0]) < 1e-4
+    pn = dict(mod.named_parameters())
+    checked = 0
+    for n, p in pn.items():
+        ref = P[f"j.{n}"].grad
+        if not p.requires_grad or ref is None or n.startswith("shared_head"):
+            continue
+        assert p.grad is not None, n
+        assert _rel(p.grad, ref) < 2e-3, (n, _rel(p.grad, ref))
+        checked += 1
+    assert checked > 40
 
 
 def test_encoder_stream(cuda):
