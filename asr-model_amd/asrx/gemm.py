@@ -106,8 +106,8 @@ def use_wide(K) -> bool:
     return prec.get() == prec.PREC_BF16 and K % 8 == 0
 
 
-def linear_fwd(x, W, b=None, act="none", out=None, preact=None):
-    """y = act(x @ W^T + b) for x (..., K), W (N, K)."""
+def linear_fwd(x, W, b=None, act="none", out=None, preact=None, wbf=None):
+    """y = act(x @ W^T + b) for x (..., K), W (N, K); wbf: W's bf16 copy when the caller made it."""
     x2 = _rows(x)
     if not x2.is_contiguous():
         x2 = x2.contiguous()
@@ -115,7 +115,8 @@ def linear_fwd(x, W, b=None, act="none", out=None, preact=None):
     N = W.shape[0]
     y = out if out is not None else torch.empty(*x.shape[:-1], N, device=x.device, dtype=torch.float32)
     if use_wide(K):
-        gemm_wn(x2, weight_bf16(W), y, M=M, N=N, K=K, lda=K, ldc=N, bias=b, act=act, Z=preact)
+        gemm_wn(x2, weight_bf16(W) if wbf is None else wbf, y, M=M, N=N, K=K, lda=K, ldc=N, bias=b, act=act,
+                Z=preact)
     else:
         gemm(x2, W, y, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, a_kc=True, b_kc=True, bias=b, act=act,
              Z=preact)
@@ -142,6 +143,17 @@ def _splitk_for(m_rows: int, tiles: int) -> int:
     # slice keeps >= 256 rows (text-side 8192-row shapes: 32 slices ran 34 us vs 38 us at 16)
     want = max(1, 512 // max(tiles, 1))
     return int(max(1, min(want, m_rows // 256)))
+
+
+def wgrad_cols(dy, c0, n, x, out):
+    """out (n, K) += dy[:, c0:c0+n]^T @ x for row-major dy (rows, ld) and x (rows, K): the weight
+    gradient of one column block of a GEMM output, read in place (no copy of the block)."""
+    rows, ld = dy.shape
+    K = x.shape[1]
+    tiles = ((n + 127) // 128) * ((K + 127) // 128)
+    gemm(dy[:, c0:], x, out, M=n, N=K, K=rows, lda=ld, ldb=K, ldc=K, a_kc=False, b_kc=False, beta=1.0,
+         splitk=_splitk_for(rows, tiles))
+    return out
 
 
 def linear_wgrad(dy, x, out=None, accumulate=False):

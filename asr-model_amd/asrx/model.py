@@ -348,11 +348,11 @@ class MSheath(nn.Module):
     def run(self, x, noise: NoiseCtx, site: str, sid_base: int):
         """Batched MSheath.forward with batch-1 semantics per sample: every sample follows its own
         layer/jump trajectory, evaluated as masked compute on device (no host syncs)."""
-        if self.fused and ops.DIRECT:
-            from .msheath import msheath
+        from . import msheath as _ms
 
+        if self.fused and ops.DIRECT and _ms.supported(self, x.shape[-1]):
             gpol = ops.policy_noise(x.shape[0], self.layer, sid_base, noise.key(site), x.device)
-            return msheath(self, x, gpol)
+            return _ms.msheath(self, x, gpol)
         return self.run_composed(x, noise, site, sid_base)
 
     def run_composed(self, x, noise: NoiseCtx, site: str, sid_base: int):

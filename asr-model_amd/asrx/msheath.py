@@ -4,13 +4,20 @@ Composed from per-op autograd Functions, a MSheath call leaves autograd to sum t
 activation with several consumers -- each layer's input feeds v_gate, the LayerNorm, the x + g*ion*out
 update and the jump select, the original input feeds every layer's jump and the policy pooling -- which
 cost ~30 full-size add kernels per call in the backward (~14 ms of the tiny
-step).  MSheathFn runs the same forward kernels, then walks the layers backwards with every
-contribution to a layer input landing in one buffer: written by its first producer (the jump-select
-pass-through of inactive samples, the x_new backward of active ones), accumulated by the rest
-(LayerNorm backward in accumulate mode, v_gate's input GEMMs with beta = 1, row-norm backward), and
-the original input's jump gradient kept apart until one final pass.  Parameter gradients go straight
-into p.grad (asrx.ops direct-gradient convention).  Batch-1 semantics per sample exactly as
-asrx.model.MSheath.run_composed (masked per-sample trajectories, no host syncs).
+step).  MSheathFn runs the forward below, then walks the layers backwards with every contribution to a
+layer input landing in one buffer: written by its first producer (the jump-select pass-through of
+inactive samples, the x_new backward of active ones), accumulated by the rest (the fused row backward,
+v_gate's input GEMM with beta = 1), and the original input's jump gradient kept apart until one final
+pass.  Parameter gradients go straight into p.grad (asrx.ops direct-gradient convention).  Batch-1
+semantics per sample exactly as asrx.model.MSheath.run_composed (masked per-sample trajectories, no
+host syncs).
+
+Per layer the forward is 6-8 launches instead of the composed path's 17: v_gate's two projections as
+one GEMM against [normalize(mkey); mlp[0].weight] (asrx_vgate_weights builds it and its bf16 copy),
+one row pass for LayerNorm + |x| + gate + v_gate (asrx_msheath_row_fwd), the adapter GEMM (even
+layers), x_new with the per-sample mem mean in the same pass (asrx_axpy_row2_colsum), the control step
+with mem_gate inside it (asrx_msheath_ctrl_fwd3) and the jump select.  The backward mirrors it
+(asrx_msheath_row_bwd, asrx_msheath_ctrl_bwd3, one dgrad GEMM against the same combined weight).
 """
 from __future__ import annotations
 
@@ -29,12 +36,19 @@ SILU = G.ACT["silu"]
 
 _REC = None
 
+ROW_DIMS = (128, 256, 384, 512, 768, 1024)  # the fused row kernels' register-resident widths
+
 
 def _rec_bytes():
     global _REC
     if _REC is None:
         _REC = int(lib.load().asrx_msheath_rec_bytes())
     return _REC
+
+
+def supported(mod, D):
+    """The fused path covers these widths (msheath_row_* kernels); others run MSheath.run_composed."""
+    return D in ROW_DIMS and all(lay["v_gate"].mkey.shape[0] <= 64 for lay in mod.layers)
 
 
 def _params(mod):
@@ -68,67 +82,64 @@ def forward(mod, x0, gpol, save):
     lib.call("asrx_small_linear_fwd", _P(hp), _P(net[2].weight), _P(net[2].bias), _P(pl), B, hp.shape[1], 3, 0, st)
     policy = _E(B, 3, device=dev)
     lib.call("asrx_softmax_small", _P(pl), _P(policy), B, 3, st)
+    nl = len(mod.layers)
+    mem_all = _E(nl, B, D, device=dev)  # every layer's mem = mean_l x_new, accumulated by atomics
+    lib.call("asrx_zero", _P(mem_all), mem_all.numel() * 4, st)
+    wide = G.use_wide(D)
+    mg = mod.mem_gate[0]
     mem_w, ld_mw = mod.mem_w, 0
     next_i = None
     x = x0
     rec_bytes = _rec_bytes()
+    inv_sqrt_d = 1.0 / math.sqrt(D)
     layers = []
-    nl = len(mod.layers)
     for i, lay in enumerate(mod.layers):
         vg = lay["v_gate"]
         Dh = vg.mlp[0].weight.shape[0]
         M = vg.mkey.shape[0]
-        # v_gate: ion = STE(concat(softmax(n(x) n(mkey)^T / sqrt D) mval, mlp(x)) > tx)   model.py:346-351
-        nx = _E(rows, device=dev)
-        lib.call("asrx_rownorm", _P(x), _P(nx), rows, D, st)
-        mkeyn = _E(M, D, device=dev)
-        mkn = _E(M, device=dev)
-        lib.call("asrx_row_normalize", _P(vg.mkey), _P(mkeyn), _P(mkn), M, D, st)
-        Sm = G.linear_fwd(x, mkeyn)
-        h = G.linear_fwd(x, vg.mlp[0].weight, vg.mlp[0].bias)
-        ion, xval, kv, m2 = (_E(rows, device=dev) for _ in range(4))
-        lib.call("asrx_vgate_fwd", _P(Sm), _P(nx), _P(vg.mval), _P(h), _P(vg.mlp[2].weight), _P(vg.mlp[2].bias),
-                 _P(vg.concat.weight), _P(vg.concat.bias), _P(vg.tx), _P(ion), _P(xval), _P(kv), _P(m2), rows, M, Dh,
-                 1.0 / math.sqrt(D), st)
-        # px = LayerNorm(x); out = adapter(px) (even i); x_new = x + sigmoid(gate(px)) * out * ion   (452-461)
-        px, mean, rstd = _E(B, L, D, device=dev), _E(rows, device=dev), _E(rows, device=dev)
-        lib.call("asrx_layernorm_fwd", _P(x), _P(lay["ln"].weight), _P(lay["ln"].bias), _P(px), _P(mean), _P(rstd),
-                 rows, D, float(lay["ln"].eps), st)
+        N = M + Dh
+        # SH = [x normalize(mkey)^T | mlp[0](x)]     model.py:346-349
+        Wc, bc, mkn = _E(N, D, device=dev), _E(N, device=dev), _E(M, device=dev)
+        wb = _E(N, D, dtype=torch.int16, device=dev) if wide else None
+        lib.call("asrx_vgate_weights", _P(vg.mkey), _P(vg.mlp[0].weight), _P(vg.mlp[0].bias), _P(Wc), _P(bc),
+                 _P(mkn), _P(wb), M, Dh, D, st)
+        SH = G.linear_fwd(x, Wc, bc, wbf=wb)
+        # px = LayerNorm(x), |x|, g = sigmoid(gate(px)), ion = v_gate(x)   (346-351, 452-460)
+        ln, gt = lay["ln"], lay["gate"][0]
+        px = _E(B, L, D, device=dev)
+        mean, rstd, nx, gv, ion, kv, m2 = (_E(rows, device=dev) for _ in range(7))
+        lib.call("asrx_msheath_row_fwd", _P(x), _P(ln.weight), _P(ln.bias), _P(gt.weight), _P(gt.bias), _P(SH), N,
+                 _P(vg.mval), _P(vg.mlp[2].weight), _P(vg.mlp[2].bias), _P(vg.concat.weight), _P(vg.concat.bias),
+                 _P(vg.tx), _P(px), _P(mean), _P(rstd), _P(nx), _P(gv), _P(ion), _P(kv), _P(m2), rows, D, M, Dh,
+                 float(ln.eps), inv_sqrt_d, st)
         out = G.linear_fwd(px, lay["adapter"].weight, lay["adapter"].bias) if lay["adapter"] is not None else px
-        gv = _E(rows, device=dev)
-        lib.call("asrx_small_linear_fwd", _P(px), _P(lay["gate"][0].weight), _P(lay["gate"][0].bias), _P(gv), rows, D,
-                 1, SIG, st)
+        # x_new = x + g * ion * out; mem = mean_l x_new   (461-463)
         x_new = _E(B, L, D, device=dev)
-        lib.call("asrx_axpy_row2", _P(x), _P(gv), _P(ion), _P(out), _P(x_new), rows, D, st)
-        # mem = mean_l x_new; mem_v = sigmoid(mem_gate(mem)); control; jump select   (463-501)
-        mem = _E(B, D, device=dev)
-        lib.call("asrx_seg_colsum", _P(x_new), _P(mem), B, L, D, 1.0 / L, 0, st)
-        mem_v = _E(B, device=dev)
-        lib.call("asrx_small_linear_fwd", _P(mem), _P(mod.mem_gate[0].weight), _P(mod.mem_gate[0].bias), _P(mem_v), B,
-                 D, 1, SIG, st)
-        alpha, beta, active, next_out = (_E(B, device=dev) for _ in range(4))
+        mem = mem_all[i]
+        lib.call("asrx_axpy_row2_colsum", _P(x), _P(gv), _P(ion), _P(out), _P(x_new), _P(mem), B, L, D, st)
+        # mem_v = sigmoid(mem_gate(mem)); control; jump select   (464-501)
+        alpha, beta, active, next_out, mem_v = (_E(B, device=dev) for _ in range(5))
         gam, mwo = _E(B, D, device=dev), _E(B, D, device=dev)
         rec = _E(B * rec_bytes, dtype=torch.uint8, device=dev)
         gp = gpol[:, i]
-        lib.call("asrx_msheath_ctrl_fwd2", _P(policy), _P(gp), gp.stride(0), _P(ion), _P(mem_v), _P(mem_w), ld_mw,
-                 _P(mem), _P(mod.jump_s), _P(next_i), i, nl, B, L, D, _P(alpha), _P(beta), _P(gam), _P(mwo),
-                 _P(active), _P(next_out), _P(rec), st)
+        lib.call("asrx_msheath_ctrl_fwd3", _P(policy), _P(gp), gp.stride(0), _P(ion), _P(mg.weight), _P(mg.bias),
+                 _P(mem_v), _P(mem_w), ld_mw, _P(mem), _P(mod.jump_s), _P(next_i), i, nl, B, L, D, _P(alpha),
+                 _P(beta), _P(gam), _P(mwo), _P(active), _P(next_out), _P(rec), st)
         x_out = _E(B, L, D, device=dev)
         lib.call("asrx_jump_select4", _P(x_new), _P(x0), _P(x), _P(active), _P(alpha), _P(beta), _P(gam),
                  _P(x_out), B, L, D, st)
         if save:
-            layers.append(dict(x=x, nx=nx, mkeyn=mkeyn, mkn=mkn, S=Sm, h=h, kv=kv, m2=m2, px=px, mean=mean, rstd=rstd,
+            layers.append(dict(x=x, Wc=Wc, mkn=mkn, SH=SH, nx=nx, kv=kv, m2=m2, px=px, mean=mean, rstd=rstd,
                                out=out, g=gv, ion=ion, x_new=x_new, mem=mem, mem_v=mem_v, mem_w=mem_w, ld_mw=ld_mw,
                                rec=rec, active=active, alpha=alpha, beta=beta))
         mem_w, ld_mw, next_i = mwo, D, next_out
         x = x_out
-    # x + sigmoid(mlp_gate(x)) * mlp(mlp_ln(x))   (503-506)
+    # x + sigmoid(mlp_gate(x)) * mlp(mlp_ln(x))   (503-506): the gate from the LayerNorm's row pass
     gate = _E(rows, device=dev)
-    lib.call("asrx_small_linear_fwd", _P(x), _P(mod.mlp_gate[0].weight), _P(mod.mlp_gate[0].bias), _P(gate), rows, D,
-             1, SIG, st)
     hln, mean2, rstd2 = _E(B, L, D, device=dev), _E(rows, device=dev), _E(rows, device=dev)
-    lib.call("asrx_layernorm_fwd", _P(x), _P(mod.mlp_ln.weight), _P(mod.mlp_ln.bias), _P(hln), _P(mean2), _P(rstd2),
-             rows, D, float(mod.mlp_ln.eps), st)
+    lib.call("asrx_layernorm_fwd2", _P(x), _P(mod.mlp_ln.weight), _P(mod.mlp_ln.bias), _P(hln), _P(mean2),
+             _P(rstd2), None, _P(mod.mlp_gate[0].weight), _P(mod.mlp_gate[0].bias), _P(gate), 1, rows, D,
+             float(mod.mlp_ln.eps), st)
     z1 = _E(B, L, mod.mlp[0].weight.shape[0], device=dev) if save else None
     a1 = G.linear_fwd(hln, mod.mlp[0].weight, mod.mlp[0].bias, act="silu", preact=z1)
     hh = G.linear_fwd(a1, mod.mlp[2].weight, mod.mlp[2].bias)
@@ -192,62 +203,57 @@ class MSheathFn(torch.autograd.Function):
         dorig = _E(B, L, D, device=dev)  # written by the first jumping layer of each sample (has_orig)
         g_mwo = None
         mg_w, mg_b = mod.mem_gate[0].weight, mod.mem_gate[0].bias
+        inv_sqrt_d = 1.0 / math.sqrt(D)
         for i in range(nl - 1, -1, -1):
             s = sv["layers"][i]
             lay = mod.layers[i]
             vg = lay["v_gate"]
             M, Dh = vg.mkey.shape[0], vg.mlp[0].weight.shape[0]
+            N = M + Dh
             xi = s["x"]
             dxi = _E(B, L, D, device=dev)
             dxn = _E(B, L, D, device=dev)
-            dalpha, dbeta, dgam = _E(B, device=dev), _E(B, device=dev), _E(B, D, device=dev)
+            dctl = _E(B * (2 + D), device=dev)  # [dalpha | dbeta | dgam]: zeroed by one memset
+            dalpha, dbeta, dgam = dctl[:B], dctl[B:2 * B], dctl[2 * B:]
             lib.call("asrx_jump_select4_bwd_acc", _P(dx), _P(s["x_new"]), _P(x0), _P(s["active"]), _P(s["alpha"]),
                      _P(s["beta"]), _P(has_orig), _P(dxn), _P(dorig), _P(dxi), _P(dalpha), _P(dbeta), _P(dgam), B, L,
                      D, st)
-            g_mem_v, g_mem_w, g_mem = _E(B, device=dev), _E(B, D, device=dev), _E(B, D, device=dev)
-            lib.call("asrx_msheath_ctrl_bwd2", _P(dalpha), _P(dbeta), _P(dgam), _P(g_mwo), _P(s["mem_v"]),
+            g_mem_w, g_mem = _E(B, D, device=dev), _E(B, D, device=dev)
+            lib.call("asrx_msheath_ctrl_bwd3", _P(dalpha), _P(dbeta), _P(dgam), _P(g_mwo), _P(s["mem_v"]),
                      _P(s["mem_w"]), s["ld_mw"], _P(s["mem"]), _P(mod.jump_s), _P(s["rec"]), i, nl, B, D,
-                     _P(g_policy), int(i != nl - 1), _P(g_mem_v), _P(g_mem_w), _P(g_mem), _P(gb(mod.jump_s)),
-                     _P(has_orig), st)
-            lib.call("asrx_small_linear_bwd", _P(g_mem_v), _P(s["mem_v"]), _P(s["mem"]), _P(mg_w), _P(g_mem),
-                     _P(gb(mg_w)), _P(gb(mg_b)), B, D, 1, SIG, 1.0, st)
+                     _P(g_policy), int(i != nl - 1), _P(g_mem_w), _P(g_mem), _P(gb(mod.jump_s)), _P(has_orig),
+                     _P(mg_w), _P(gb(mg_w)), _P(gb(mg_b)), st)
             dout = _E(B, L, D, device=dev)
             dgv, dion = _E(rows, device=dev), _E(rows, device=dev)
             lib.call("asrx_axpy_row2_bwd_acc", _P(dxn), _P(g_mem), 1.0 / L, _P(s["active"]), _P(s["g"]), _P(s["ion"]),
                      _P(s["out"]), _P(dout), _P(dgv), _P(dion), _P(dxi), B, L, D, st)
             del dxn
-            gw = lay["gate"][0]
-            dpx = _E(B, L, D, device=dev)
-            lib.call("asrx_small_linear_bwd", _P(dgv), _P(s["g"]), _P(s["px"]), _P(gw.weight), _P(dpx),
-                     _P(gb(gw.weight)), _P(gb(gw.bias)), rows, D, 1, SIG, 0.0, st)
             ad = lay["adapter"]
             if ad is not None:
-                G.linear_dgrad(dout, ad.weight, out=dpx, beta=1.0)
+                dpx = G.linear_dgrad(dout, ad.weight)
                 G.linear_wgrad(dout, s["px"], out=gb(ad.weight), accumulate=True)
                 ops.colsum(dout.view(rows, D), out=gb(ad.bias))
             else:
-                lib.call("asrx_lincomb", _P(dpx), _P(dout), None, 1.0, 1.0, 0.0, _P(dpx), dpx.numel(), st)
-            del dout
-            ln = lay["ln"]
-            lib.call("asrx_layernorm_bwd_acc", _P(dpx), _P(xi), _P(ln.weight), _P(s["mean"]), _P(s["rstd"]), _P(dxi),
-                     _P(gb(ln.weight)), _P(gb(ln.bias)), rows, D, 1, st)
-            del dpx
-            # v_gate backward: ion's straight-through gradient dion (STthreshold, model.py:319-334)
-            dS, dnx, dh = _E(rows, M, device=dev), _E(rows, device=dev), _E(rows, Dh, device=dev)
-            dmval = gb(vg.mval)
-            dw2, db2 = gb(vg.mlp[2].weight), gb(vg.mlp[2].bias)
-            dcw, dcb = gb(vg.concat.weight), gb(vg.concat.bias)
-            lib.call("asrx_vgate_bwd", _P(dion), _P(s["S"]), _P(s["nx"]), _P(vg.mval), _P(s["h"]), _P(vg.mlp[2].weight),
-                     _P(vg.concat.weight), _P(s["kv"]), _P(s["m2"]), _P(dS), _P(dnx), _P(dh), _P(dmval), _P(dw2),
-                     _P(db2), _P(dcw), _P(dcb), rows, M, Dh, 1.0 / math.sqrt(D), st)
-            G.linear_dgrad(dS, s["mkeyn"], out=dxi, beta=1.0)
-            G.linear_dgrad(dh, vg.mlp[0].weight, out=dxi, beta=1.0)
-            lib.call("asrx_rownorm_bwd", _P(dnx), _P(xi), _P(s["nx"]), _P(dxi), rows, D, st)
-            dmk = G.linear_wgrad(dS, xi)
-            lib.call("asrx_row_normalize_bwd", _P(dmk), _P(s["mkeyn"]), _P(s["mkn"]), _P(gb(vg.mkey)), M, D, 1, st)
-            G.linear_wgrad(dh, xi, out=gb(vg.mlp[0].weight), accumulate=True)
-            ops.colsum(dh, out=gb(vg.mlp[0].bias))
-            del dS, dh, dmk
+                dpx = dout
+            # LayerNorm + gate + |x| + v_gate backward in one row pass; dSH = [dS | dh]
+            ln, gt = lay["ln"], lay["gate"][0]
+            dSH = _E(rows, N, device=dev)
+            lib.call("asrx_msheath_row_bwd", _P(dpx), _P(xi), _P(ln.weight), _P(ln.bias), _P(s["mean"]),
+                     _P(s["rstd"]), _P(dgv), _P(s["g"]), _P(gt.weight), _P(dion), _P(s["SH"]), N, _P(s["nx"]),
+                     _P(vg.mval), _P(vg.mlp[2].weight), _P(vg.concat.weight), _P(s["kv"]), _P(s["m2"]), _P(dxi),
+                     _P(gb(ln.weight)), _P(gb(ln.bias)), _P(gb(gt.weight)), _P(gb(gt.bias)), _P(dSH),
+                     _P(gb(vg.mval)), _P(gb(vg.mlp[2].weight)), _P(gb(vg.mlp[2].bias)), _P(gb(vg.concat.weight)),
+                     _P(gb(vg.concat.bias)), _P(gb(vg.mlp[0].bias)), rows, D, M, Dh, inv_sqrt_d, st)
+            del dout, dpx
+            # x's gradient through both projections: one GEMM against [normalize(mkey); mlp[0].weight]
+            G.linear_dgrad(dSH, s["Wc"], out=dxi, beta=1.0)
+            x2 = xi.view(rows, D)
+            dmk = _E(M, D, device=dev)
+            lib.call("asrx_zero", _P(dmk), dmk.numel() * 4, st)
+            G.wgrad_cols(dSH, 0, M, x2, dmk)
+            lib.call("asrx_row_normalize_bwd", _P(dmk), _P(s["Wc"]), _P(s["mkn"]), _P(gb(vg.mkey)), M, D, 1, st)
+            G.wgrad_cols(dSH, M, Dh, x2, gb(vg.mlp[0].weight))
+            del dSH, dmk
             g_mwo = g_mem_w
             dx = dxi
         # layer 0's mem_w is the (1, 1, D) parameter broadcast over the samples

@@ -28,12 +28,22 @@ __global__ __launch_bounds__(256) void msheath_ctrl_fwd_kernel(
     const float* __restrict__ mem_v, const float* __restrict__ mem_w, const float* __restrict__ mem,
     const float* __restrict__ jump_s, const float* __restrict__ next_i, int layer_i, int layers, int64_t L, int D,
     float* __restrict__ alpha, float* __restrict__ beta, float* __restrict__ gam, float* __restrict__ mem_w_out,
-    float* __restrict__ active, float* __restrict__ next_out, CtrlRec* __restrict__ rec, int64_t ld_mem_w) {
+    float* __restrict__ active, float* __restrict__ next_out, CtrlRec* __restrict__ rec, int64_t ld_mem_w,
+    const float* __restrict__ mg_w, const float* __restrict__ mg_b, float* __restrict__ mem_v_out) {
   __shared__ float red[4];
   const int64_t b = blockIdx.x;
   float s = 0.f;
   for (int64_t l = threadIdx.x; l < L; l += 256) s += ion[b * L + l];
   const float potential = block_sum<256>(s, red) / (float)L;  // ion.mean(dim=1), model.py:466
+  float mv;
+  if (mg_w) {  // mem_v = sigmoid(mem_gate(mem)) computed here (model.py:464)
+    float t = 0.f;
+    for (int c = threadIdx.x; c < D; c += 256) t += mem[b * D + c] * mg_w[c];
+    mv = sigmoid_f(block_sum<256>(t, red) + mg_b[0]);
+    if (threadIdx.x == 0) mem_v_out[b] = mv;
+  } else {
+    mv = mem_v[b];
+  }
   const float ni = next_i ? next_i[b] : 0.f;  // null: every sample starts at layer 0
   const float act = ni == (float)layer_i ? 1.f : 0.f;
   float ys[3] = {0.f, 0.f, 0.f};
@@ -69,7 +79,6 @@ __global__ __launch_bounds__(256) void msheath_ctrl_fwd_kernel(
   const float al = jumped ? 1.f : jump_g;
   const float be = jumped ? jw * jump_g : 0.f;
   const float cg = jumped ? (1.f - jw) * jump_g : 0.f;
-  const float mv = mem_v[b];
   for (int c = threadIdx.x; c < D; c += 256) {
     const float mw = mem_w[b * ld_mem_w + c];                 // ld 0: the (1, 1, D) parameter broadcast
     const float mwn = mv * mw + (1.f - mv) * mem[b * D + c];  // model.py:464
@@ -103,7 +112,7 @@ __global__ __launch_bounds__(256) void msheath_ctrl_bwd_kernel(
     const float* __restrict__ mem, const float* __restrict__ jump_s, const CtrlRec* __restrict__ rec, int layer_i,
     int layers, int D, float* __restrict__ g_policy, float* __restrict__ g_mem_v, float* __restrict__ g_mem_w,
     float* __restrict__ g_mem, float* __restrict__ g_jump_s, int64_t ld_mem_w, int* __restrict__ has_orig,
-    int acc_policy) {
+    int acc_policy, const float* __restrict__ mg_w, float* __restrict__ g_mg_w, float* __restrict__ g_mg_b) {
   __shared__ float red[4];
   const int64_t b = blockIdx.x;
   const CtrlRec r = rec[b];
@@ -123,8 +132,16 @@ __global__ __launch_bounds__(256) void msheath_ctrl_bwd_kernel(
   }
   s_cg = block_sum<256>(s_cg, red);
   s_mv = block_sum<256>(s_mv, red);
+  if (mg_w) {  // mem_v = sigmoid(mem . mg_w + mg_b): its backward onto mem and the gate parameters
+    const float gz = s_mv * mv * (1.f - mv);
+    for (int c = threadIdx.x; c < D; c += 256) {
+      g_mem[b * D + c] += gz * mg_w[c];
+      atomicAdd(g_mg_w + c, gz * mem[b * D + c]);
+    }
+    if (threadIdx.x == 0) atomicAdd(g_mg_b, gz);
+  }
   if (threadIdx.x == 0) {
-    g_mem_v[b] = s_mv;
+    if (g_mem_v) g_mem_v[b] = s_mv;
     const int action = (int)r.action;
     const bool jumped = action > 0;
     const float ga = g_alpha[b], gb = g_beta[b];
@@ -156,6 +173,45 @@ __global__ void axpy_row2_kernel(const float4* __restrict__ x, const float* __re
     const float sc = s1[r] * (s2 ? s2[r] : 1.f);
     const float4 a = x[i], v = y[i];
     out[i] = make_float4(a.x + sc * v.x, a.y + sc * v.y, a.z + sc * v.z, a.w + sc * v.w);
+  }
+}
+
+// x_new = x + s1 s2 y (model.py:461) and mem += invL sum_l x_new (model.py:463, accumulated into a
+// zeroed mem) in one pass.  grid (B, ceil(L / lch)); the 256 threads are nrl = 256 / d4 row lanes x d4
+// float4 columns (d4 <= 256), so each thread keeps its column's partial sum in registers.
+__global__ __launch_bounds__(256) void axpy_row2_colsum_kernel(const float4* __restrict__ x, const float* __restrict__ s1,
+                                                               const float* __restrict__ s2, const float4* __restrict__ y,
+                                                               float4* __restrict__ out, float* __restrict__ mem,
+                                                               int64_t L, int d4, float invL, int lch) {
+  __shared__ float4 red[256];
+  const int nrl = 256 / d4;
+  const int c = threadIdx.x % d4, rl = threadIdx.x / d4;
+  const int64_t b = blockIdx.x;
+  const int64_t l0 = (int64_t)blockIdx.y * lch, l1 = min<int64_t>(L, l0 + lch);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (rl < nrl) {
+    for (int64_t l = l0 + rl; l < l1; l += nrl) {
+      const int64_t r = b * L + l;
+      const float sc = s1[r] * s2[r];
+      const int64_t i = r * d4 + c;
+      const float4 a = x[i], v = y[i];
+      const float4 o = make_float4(a.x + sc * v.x, a.y + sc * v.y, a.z + sc * v.z, a.w + sc * v.w);
+      out[i] = o;
+      acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
+    }
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  if (rl == 0) {
+    for (int k = 1; k < nrl; ++k) {
+      const float4 t = red[k * d4 + c];
+      acc.x += t.x; acc.y += t.y; acc.z += t.z; acc.w += t.w;
+    }
+    float* m = mem + b * (int64_t)d4 * 4 + 4 * c;
+    atomicAdd(m + 0, acc.x * invL);
+    atomicAdd(m + 1, acc.y * invL);
+    atomicAdd(m + 2, acc.z * invL);
+    atomicAdd(m + 3, acc.w * invL);
   }
 }
 
@@ -426,9 +482,13 @@ int asrx_jump_select4_bwd_acc(const float* g, const float* xn, const float* orig
                               hipStream_t stream) {
   ASRX_REQUIRE(d % 4 == 0, "asrx_jump_select4_bwd_acc: d % 4 != 0");
   if (B * L == 0) return 0;
-  (void)hipMemsetAsync(dalpha, 0, B * sizeof(float), stream);
-  (void)hipMemsetAsync(dbeta, 0, B * sizeof(float), stream);
-  (void)hipMemsetAsync(dgam, 0, B * d * sizeof(float), stream);
+  if (dbeta == dalpha + B && dgam == dalpha + 2 * B) {  // one block [dalpha | dbeta | dgam]
+    (void)hipMemsetAsync(dalpha, 0, B * (2 + d) * sizeof(float), stream);
+  } else {
+    (void)hipMemsetAsync(dalpha, 0, B * sizeof(float), stream);
+    (void)hipMemsetAsync(dbeta, 0, B * sizeof(float), stream);
+    (void)hipMemsetAsync(dgam, 0, B * d * sizeof(float), stream);
+  }
   const int d4 = (int)(d / 4);
   const int lchunk = 128;
   dim3 grid((unsigned)(((d4 + 31) / 32) * ((L + lchunk - 1) / lchunk)), (unsigned)B);
@@ -468,7 +528,8 @@ int asrx_msheath_ctrl_fwd(const float* policy, const float* gpol, int64_t ld_gpo
   if (B == 0) return 0;
   msheath_ctrl_fwd_kernel<<<(unsigned)B, 256, 0, stream>>>(policy, gpol, ld_gpol, ion, mem_v, mem_w, mem, jump_s,
                                                            next_i, (int)layer_i, (int)layers, L, (int)D, alpha, beta,
-                                                           gam, mem_w_out, active, next_out, (CtrlRec*)rec, D);
+                                                           gam, mem_w_out, active, next_out, (CtrlRec*)rec, D, nullptr,
+                                                           nullptr, nullptr);
   ASRX_LAUNCHED("asrx_msheath_ctrl_fwd");
 }
 
@@ -482,8 +543,25 @@ int asrx_msheath_ctrl_fwd2(const float* policy, const float* gpol, int64_t ld_gp
   if (B == 0) return 0;
   msheath_ctrl_fwd_kernel<<<(unsigned)B, 256, 0, stream>>>(policy, gpol, ld_gpol, ion, mem_v, mem_w, mem, jump_s,
                                                            next_i, (int)layer_i, (int)layers, L, (int)D, alpha, beta,
-                                                           gam, mem_w_out, active, next_out, (CtrlRec*)rec, ld_mem_w);
+                                                           gam, mem_w_out, active, next_out, (CtrlRec*)rec, ld_mem_w,
+                                                           nullptr, nullptr, nullptr);
   ASRX_LAUNCHED("asrx_msheath_ctrl_fwd2");
+}
+
+// As asrx_msheath_ctrl_fwd2 with mem_v = sigmoid(mem . mg_w + mg_b) computed in the kernel (written
+// to mem_v_out for the backward) instead of read.
+int asrx_msheath_ctrl_fwd3(const float* policy, const float* gpol, int64_t ld_gpol, const float* ion,
+                           const float* mg_w, const float* mg_b, float* mem_v_out, const float* mem_w,
+                           int64_t ld_mem_w, const float* mem, const float* jump_s, const float* next_i,
+                           int64_t layer_i, int64_t layers, int64_t B, int64_t L, int64_t D, float* alpha, float* beta,
+                           float* gam, float* mem_w_out, float* active, float* next_out, void* rec,
+                           hipStream_t stream) {
+  if (B == 0) return 0;
+  msheath_ctrl_fwd_kernel<<<(unsigned)B, 256, 0, stream>>>(policy, gpol, ld_gpol, ion, nullptr, mem_w, mem, jump_s,
+                                                           next_i, (int)layer_i, (int)layers, L, (int)D, alpha, beta,
+                                                           gam, mem_w_out, active, next_out, (CtrlRec*)rec, ld_mem_w,
+                                                           mg_w, mg_b, mem_v_out);
+  ASRX_LAUNCHED("asrx_msheath_ctrl_fwd3");
 }
 
 int asrx_msheath_ctrl_bwd(const float* g_alpha, const float* g_beta, const float* g_gam, const float* g_mwo,
@@ -493,7 +571,8 @@ int asrx_msheath_ctrl_bwd(const float* g_alpha, const float* g_beta, const float
   if (B == 0) return 0;
   msheath_ctrl_bwd_kernel<<<(unsigned)B, 256, 0, stream>>>(g_alpha, g_beta, g_gam, g_mwo, mem_v, mem_w, mem, jump_s,
                                                            (const CtrlRec*)rec, (int)layer_i, (int)layers, (int)D,
-                                                           g_policy, g_mem_v, g_mem_w, g_mem, g_jump_s, D, nullptr, 0);
+                                                           g_policy, g_mem_v, g_mem_w, g_mem, g_jump_s, D, nullptr, 0,
+                                                           nullptr, nullptr, nullptr);
   ASRX_LAUNCHED("asrx_msheath_ctrl_bwd");
 }
 
@@ -508,8 +587,37 @@ int asrx_msheath_ctrl_bwd2(const float* g_alpha, const float* g_beta, const floa
   msheath_ctrl_bwd_kernel<<<(unsigned)B, 256, 0, stream>>>(g_alpha, g_beta, g_gam, g_mwo, mem_v, mem_w, mem, jump_s,
                                                            (const CtrlRec*)rec, (int)layer_i, (int)layers, (int)D,
                                                            g_policy, g_mem_v, g_mem_w, g_mem, g_jump_s, ld_mem_w,
-                                                           has_orig, acc_policy);
+                                                           has_orig, acc_policy, nullptr, nullptr, nullptr);
   ASRX_LAUNCHED("asrx_msheath_ctrl_bwd2");
+}
+
+// As asrx_msheath_ctrl_bwd2 with mem_v's gate backward fused: g_mem also receives
+// g_mem_v mv (1 - mv) mg_w, and g_mg_w / g_mg_b accumulate its parameter gradients (atomics).
+int asrx_msheath_ctrl_bwd3(const float* g_alpha, const float* g_beta, const float* g_gam, const float* g_mwo,
+                           const float* mem_v, const float* mem_w, int64_t ld_mem_w, const float* mem,
+                           const float* jump_s, const void* rec, int64_t layer_i, int64_t layers, int64_t B, int64_t D,
+                           float* g_policy, int acc_policy, float* g_mem_w, float* g_mem, float* g_jump_s,
+                           int* has_orig, const float* mg_w, float* g_mg_w, float* g_mg_b, hipStream_t stream) {
+  if (B == 0) return 0;
+  msheath_ctrl_bwd_kernel<<<(unsigned)B, 256, 0, stream>>>(g_alpha, g_beta, g_gam, g_mwo, mem_v, mem_w, mem, jump_s,
+                                                           (const CtrlRec*)rec, (int)layer_i, (int)layers, (int)D,
+                                                           g_policy, nullptr, g_mem_w, g_mem, g_jump_s, ld_mem_w,
+                                                           has_orig, acc_policy, mg_w, g_mg_w, g_mg_b);
+  ASRX_LAUNCHED("asrx_msheath_ctrl_bwd3");
+}
+
+int asrx_axpy_row2_colsum(const float* x, const float* s1, const float* s2, const float* y, float* out, float* mem,
+                          int64_t B, int64_t L, int64_t d, hipStream_t stream) {
+  ASRX_REQUIRE(d % 4 == 0 && d <= 1024, "asrx_axpy_row2_colsum: d %% 4 == 0 and d <= 1024 required");
+  ASRX_REQUIRE(s2 != nullptr, "asrx_axpy_row2_colsum: s2 required");
+  if (B * L == 0) return 0;
+  const int d4 = (int)(d / 4);
+  const int nrl = 256 / d4;
+  const int lch = std::max(nrl * 16, 32);
+  dim3 grid((unsigned)B, (unsigned)((L + lch - 1) / lch));
+  axpy_row2_colsum_kernel<<<grid, 256, 0, stream>>>((const float4*)x, s1, s2, (const float4*)y, (float4*)out, mem, L,
+                                                    d4, 1.0f / (float)L, lch);
+  ASRX_LAUNCHED("asrx_axpy_row2_colsum");
 }
 
 int64_t asrx_msheath_rec_bytes(void) { return (int64_t)sizeof(CtrlRec); }

@@ -56,16 +56,23 @@ __device__ __forceinline__ void st_lane(float* __restrict__ dst, int lane, const
   for (int e = 0; e < E / 2; ++e) d2[e] = make_float2(v[2 * e], v[2 * e + 1]);
 }
 
+// Optional fused row outputs (MSheath, asrx/msheath.py): nrm[r] = |x_r|_2 (v_gate's normalisation of
+// the same x, model.py:347) and gout[r] = sigmoid(y_r . gw + gb) (the Linear(D, 1) gate on the
+// normalised row: layers[i].gate at model.py:460, mlp_gate at 503 on x itself when gate_on_x).
 template <int E>
 __global__ __launch_bounds__(64 * RW) void ln_fwd_t_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                            const float* __restrict__ b, float* __restrict__ y,
                                                            float* __restrict__ mean, float* __restrict__ rstd,
-                                                           int64_t rows, float eps) {
+                                                           int64_t rows, float eps, float* __restrict__ nrm,
+                                                           const float* __restrict__ gw, const float* __restrict__ gb,
+                                                           float* __restrict__ gout, int gate_on_x) {
   constexpr int D = 64 * E;
   const int lane = threadIdx.x & 63;
-  float wv[E], bv[E], xn[E];
+  float wv[E], bv[E], xn[E], gwv[E];
   ld_lane<E>(w, lane, wv);
   ld_lane<E>(b, lane, bv);
+  if (gw) ld_lane<E>(gw, lane, gwv);
+  const float gbias = gw ? gb[0] : 0.f;
   int64_t r = row_begin();
   if (r < rows) ld_lane<E>(x + r * D, lane, xn);
   for (; r < rows; r += row_step()) {
@@ -89,6 +96,20 @@ __global__ __launch_bounds__(64 * RW) void ln_fwd_t_kernel(const float* __restri
 #pragma unroll
     for (int e = 0; e < E; ++e) yv[e] = (xv[e] - mu) * rs * wv[e] + bv[e];
     st_lane<E>(y + r * D, lane, yv);
+    if (nrm) {
+      float q = 0.f;
+#pragma unroll
+      for (int e = 0; e < E; ++e) q += xv[e] * xv[e];
+      q = wave_sum_dpp(q);
+      if (lane == 0) nrm[r] = sqrtf(q);
+    }
+    if (gw) {
+      float q = 0.f;
+#pragma unroll
+      for (int e = 0; e < E; ++e) q += (gate_on_x ? xv[e] : yv[e]) * gwv[e];
+      q = wave_sum_dpp(q) + gbias;
+      if (lane == 0) gout[r] = sigmoid_f(q);
+    }
     if (lane == 0) {
       mean[r] = mu;
       rstd[r] = rs;
@@ -462,6 +483,250 @@ __global__ __launch_bounds__(64 * RW) void vgate_bwd_kernel(
     else if (j == M + Dh + 1) atomicAdd(dcw, s);
     else if (j == M + Dh + 2) atomicAdd(dcw + 1, s);
     else atomicAdd(dcb, s);
+  }
+}
+
+// ============================================================================ MSheath layer rows
+// One MSheath layer (model.py:452-461) touches each row of its input x in several per-row ops: v_gate
+// (normalize(x), two projections, softmax, STE), the LayerNorm, the Linear(D, 1) gate on its output.
+// The fused path (asrx/msheath.py) runs v_gate's two projections as ONE GEMM against
+//   Wc = [normalize(mkey); mlp[0].weight]  ((M + Dh) x D),  bc = [0; mlp[0].bias],
+// whose output SH = [x mkey_n^T | mlp[0](x)] has row stride ldsh = M + Dh, and every per-row op in
+// one row pass forward (msheath_row_fwd) and one backward (msheath_row_bwd).
+
+// Wc / bc from mkey and mlp[0]; mkn = max(|mkey_j|, 1e-12) (row_normalize's norm, for the backward);
+// wb = bf16 Wc when non-null (asrx_weight_to_bf16's rounding), the wide GEMM's weight operand.
+__global__ __launch_bounds__(64 * RW) void vgate_weights_kernel(const float* __restrict__ mkey,
+                                                                const float* __restrict__ W1,
+                                                                const float* __restrict__ b1, float* __restrict__ Wc,
+                                                                float* __restrict__ bc, float* __restrict__ mkn,
+                                                                unsigned short* __restrict__ wb, int M, int Dh, int D) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t r = row_begin(); r < M + Dh; r += row_step()) {
+    const bool key = r < M;
+    const float* src = key ? mkey + r * D : W1 + (r - M) * D;
+    float nn = 1.f;
+    if (key) {
+      float s = 0.f;
+      for (int j = lane; j < D; j += 64) s += src[j] * src[j];
+      nn = fmaxf(sqrtf(wave_sum(s)), 1e-12f);
+    }
+    for (int j = lane; j < D; j += 64) {
+      const float v = key ? src[j] / nn : src[j];
+      Wc[r * D + j] = v;
+      if (wb) wb[r * D + j] = __builtin_bit_cast(unsigned short, (__bf16)v);
+    }
+    if (lane == 0) {
+      if (key) mkn[r] = nn;
+      bc[r] = key ? 0.f : b1[r - M];
+    }
+  }
+}
+
+struct MSRowFwd {
+  const float *x, *lnw, *lnb, *gw, *gb;                   // layer input, ln, gate Linear(D, 1)
+  const float *SH, *mval, *w2, *b2, *cw, *cb, *tx;         // v_gate
+  float *px, *mean, *rstd, *nx, *g, *ion, *kv, *m2;
+  int64_t rows, ldsh;
+  int M, Dh;
+  float eps, inv_sqrt_d;
+};
+
+// Per row: px = LayerNorm(x); nx = |x|; g = sigmoid(px . gw + gb); v_gate from SH and nx (as
+// vgate_fwd_kernel): ion = STE(cw0 softmax(S / (nx sqrt D)) . mval + cw1 (silu(h) . w2 + b2) + cb > tx).
+template <int E>
+__global__ __launch_bounds__(64 * RW) void msheath_row_fwd_kernel(MSRowFwd p) {
+  constexpr int D = 64 * E;
+  const int lane = threadIdx.x & 63;
+  float wv[E], bv[E], gwv[E], xn[E];
+  ld_lane<E>(p.lnw, lane, wv);
+  ld_lane<E>(p.lnb, lane, bv);
+  ld_lane<E>(p.gw, lane, gwv);
+  const float gbias = p.gb[0];
+  const float mv_l = lane < p.M ? p.mval[lane] : 0.f;
+  const float b2 = p.b2[0], cw0 = p.cw[0], cw1 = p.cw[1], cb = p.cb[0], tx = p.tx[0];
+  int64_t r = row_begin();
+  if (r < p.rows) ld_lane<E>(p.x + r * D, lane, xn);
+  for (; r < p.rows; r += row_step()) {
+    float xv[E];
+    float s = 0.f, q = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      xv[e] = xn[e];
+      s += xv[e];
+      q += xv[e] * xv[e];
+    }
+    if (r + row_step() < p.rows) ld_lane<E>(p.x + (r + row_step()) * D, lane, xn);
+    const float mu = wave_sum_dpp(s) * (1.0f / D);
+    const float nrm = sqrtf(wave_sum_dpp(q));
+    float v = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const float t = xv[e] - mu;
+      v += t * t;
+    }
+    const float rs = rsqrtf(wave_sum_dpp(v) * (1.0f / D) + p.eps);
+    float yv[E], gd = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      yv[e] = (xv[e] - mu) * rs * wv[e] + bv[e];
+      gd += yv[e] * gwv[e];
+    }
+    st_lane<E>(p.px + r * D, lane, yv);
+    const float gate = sigmoid_f(wave_sum_dpp(gd) + gbias);
+    // v_gate
+    const float* S = p.SH + r * p.ldsh;
+    const float* h = S + p.M;
+    const float inx = 1.0f / fmaxf(nrm, 1e-12f);
+    const float z = lane < p.M ? S[lane] * inx * p.inv_sqrt_d : -INFINITY;
+    const float zm = wave_max(z);
+    const float ez = lane < p.M ? expf(z - zm) : 0.f;
+    const float se = wave_sum(ez);
+    const float kv = wave_sum(lane < p.M ? ez / se * mv_l : 0.f);
+    float acc = 0.f;
+    for (int j = lane; j < p.Dh; j += 64) acc += silu_f(h[j]) * p.w2[j];
+    const float m2 = wave_sum(acc) + b2;
+    const float xval = cw0 * kv + cw1 * m2 + cb;
+    if (lane == 0) {
+      p.mean[r] = mu;
+      p.rstd[r] = rs;
+      p.nx[r] = nrm;
+      p.g[r] = gate;
+      p.ion[r] = xval > tx ? 1.f : 0.f;
+      p.kv[r] = kv;
+      p.m2[r] = m2;
+    }
+  }
+}
+
+struct MSRowBwd {
+  const float *dpx;                                        // gradient of the LayerNorm output (adapter path)
+  const float *x, *lnw, *lnb, *mean, *rstd;
+  const float *dg, *g, *gw;                                // gate: gradient of its output, output, weight
+  const float *dion, *SH, *nx, *mval, *w2, *cw, *kv, *m2;  // v_gate
+  float *dx;                                               // accumulated
+  float *dlnw, *dlnb, *dgw, *dgb;
+  float *dSH, *dmval, *dw2, *db2, *dcw, *dcb, *db1;
+  int64_t rows, ldsh;
+  int M, Dh;
+  float inv_sqrt_d;
+};
+
+// Per row, the backward of msheath_row_fwd: v_gate (dSH row with stride ldsh: dS already divided by
+// nx sqrt D, dh = dm2 w2 silu'(h)), the gate (dz = dg g (1 - g) onto px), the LayerNorm with the gate
+// term in its output gradient, and |x|'s gradient, all accumulated into dx; parameter gradients
+// (ln w/b, gate w/b, mval, mlp[2] w/b, concat w/b, mlp[0].bias) as workgroup partials + atomics.
+// Dynamic LDS: RW * (3 D + M + 2 Dh + 5) floats.
+template <int E>
+__global__ __launch_bounds__(64 * RW) void msheath_row_bwd_kernel(MSRowBwd p) {
+  constexpr int D = 64 * E;
+  extern __shared__ float part[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int M = p.M, Dh = p.Dh;
+  const int PN = M + 2 * Dh + 5;  // dmval[M] dw2[Dh] db1[Dh] db2 dcw0 dcw1 dcb dgb
+  float* pw = part + RW * 3 * D + wid * PN;
+  for (int j = lane; j < PN; j += 64) pw[j] = 0.f;
+  float wv[E], bv[E], gwv[E], aw[E], ab[E], ag[E];
+  ld_lane<E>(p.lnw, lane, wv);
+  ld_lane<E>(p.lnb, lane, bv);
+  ld_lane<E>(p.gw, lane, gwv);
+#pragma unroll
+  for (int e = 0; e < E; ++e) aw[e] = ab[e] = ag[e] = 0.f;
+  const float mv_l = lane < M ? p.mval[lane] : 0.f;
+  const float cw0 = p.cw[0], cw1 = p.cw[1];
+  for (int64_t r = row_begin(); r < p.rows; r += row_step()) {
+    // ---- v_gate backward (vgate_bwd_kernel)
+    const float gi = p.dion[r];
+    const float nxr = p.nx[r];
+    const float inx = 1.0f / fmaxf(nxr, 1e-12f);
+    const float* S = p.SH + r * p.ldsh;
+    const float* h = S + M;
+    float* dS = p.dSH + r * p.ldsh;
+    float* dh = dS + M;
+    const float sl = lane < M ? S[lane] : 0.f;
+    const float z = lane < M ? sl * inx * p.inv_sqrt_d : -INFINITY;
+    const float zm = wave_max(z);
+    const float ez = lane < M ? expf(z - zm) : 0.f;
+    const float key = ez / wave_sum(ez);
+    const float dkv = gi * cw0, dm2 = gi * cw1;
+    const float dkey = lane < M ? dkv * mv_l : 0.f;
+    const float dot = wave_sum(key * dkey);
+    const float dz = lane < M ? key * (dkey - dot) : 0.f;
+    if (lane < M) {
+      dS[lane] = dz * inx * p.inv_sqrt_d;
+      pw[lane] += dkv * key;
+    }
+    const float dinx = wave_sum(lane < M ? dz * sl * p.inv_sqrt_d : 0.f);
+    const float dnx = nxr > 1e-12f ? -dinx * inx * inx : 0.f;
+    for (int j = lane; j < Dh; j += 64) {
+      const float hv = h[j];
+      const float t = dm2 * p.w2[j] * silu_grad(hv);
+      dh[j] = t;
+      pw[M + j] += dm2 * silu_f(hv);
+      pw[M + Dh + j] += t;
+    }
+    // ---- gate + LayerNorm + |x| backward
+    const float gg = p.g[r];
+    const float dzg = p.dg[r] * gg * (1.f - gg);
+    if (lane == 0) {
+      pw[M + 2 * Dh + 0] += dm2;
+      pw[M + 2 * Dh + 1] += gi * p.kv[r];
+      pw[M + 2 * Dh + 2] += gi * p.m2[r];
+      pw[M + 2 * Dh + 3] += gi;
+      pw[M + 2 * Dh + 4] += dzg;
+    }
+    float xv[E], gv[E];
+    ld_lane<E>(p.x + r * D, lane, xv);
+    ld_lane<E>(p.dpx + r * D, lane, gv);
+    const float mu = p.mean[r], rs = p.rstd[r];
+    const float cn = nxr > 0.f ? dnx / nxr : 0.f;
+    float s1 = 0.f, s2 = 0.f, xh[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      xh[e] = (xv[e] - mu) * rs;
+      gv[e] += dzg * gwv[e];
+      const float t = gv[e] * wv[e];
+      s1 += t;
+      s2 += t * xh[e];
+      aw[e] += gv[e] * xh[e];
+      ab[e] += gv[e];
+      ag[e] += dzg * (xh[e] * wv[e] + bv[e]);
+    }
+    s1 = wave_sum_dpp(s1) * (1.0f / D);
+    s2 = wave_sum_dpp(s2) * (1.0f / D);
+    float dv[E];
+    ld_lane<E>(p.dx + r * D, lane, dv);
+#pragma unroll
+    for (int e = 0; e < E; ++e) dv[e] += rs * (gv[e] * wv[e] - s1 - xh[e] * s2) + cn * xv[e];
+    st_lane<E>(p.dx + r * D, lane, dv);
+  }
+  float* pl = part + wid * 3 * D;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    pl[lane * E + e] = aw[e];
+    pl[D + lane * E + e] = ab[e];
+    pl[2 * D + lane * E + e] = ag[e];
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < 3 * D; j += 64 * RW) {
+    float a = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < RW; ++ww) a += part[ww * 3 * D + j];
+    atomicAdd(j < D ? p.dlnw + j : j < 2 * D ? p.dlnb + (j - D) : p.dgw + (j - 2 * D), a);
+  }
+  const float* pv = part + RW * 3 * D;
+  for (int j = threadIdx.x; j < PN; j += 64 * RW) {
+    float a = 0.f;
+    for (int ww = 0; ww < RW; ++ww) a += pv[ww * PN + j];
+    float* dst = j < M ? p.dmval + j
+                 : j < M + Dh ? p.dw2 + (j - M)
+                 : j < M + 2 * Dh ? p.db1 + (j - M - Dh)
+                 : j == M + 2 * Dh ? p.db2
+                 : j == M + 2 * Dh + 1 ? p.dcw
+                 : j == M + 2 * Dh + 2 ? p.dcw + 1
+                 : j == M + 2 * Dh + 3 ? p.dcb
+                                       : p.dgb;
+    atomicAdd(dst, a);
   }
 }
 
@@ -1440,15 +1705,40 @@ int asrx_layernorm_fwd(const float* x, const float* w, const float* b, float* y,
   if (rows == 0) return 0;
   const bool al = ((((uintptr_t)x | (uintptr_t)w | (uintptr_t)b | (uintptr_t)y) & 7) == 0);
   switch (al ? d : 0) {
-    case 128: LAUNCH_ROWS(ln_fwd_t_kernel<2>, rows, 0, x, w, b, y, mean, rstd, rows, eps); break;
-    case 256: LAUNCH_ROWS(ln_fwd_t_kernel<4>, rows, 0, x, w, b, y, mean, rstd, rows, eps); break;
-    case 384: LAUNCH_ROWS(ln_fwd_t_kernel<6>, rows, 0, x, w, b, y, mean, rstd, rows, eps); break;
-    case 512: LAUNCH_ROWS(ln_fwd_t_kernel<8>, rows, 0, x, w, b, y, mean, rstd, rows, eps); break;
-    case 768: LAUNCH_ROWS(ln_fwd_t_kernel<12>, rows, 0, x, w, b, y, mean, rstd, rows, eps); break;
-    case 1024: LAUNCH_ROWS(ln_fwd_t_kernel<16>, rows, 0, x, w, b, y, mean, rstd, rows, eps); break;
+#define LNF(E) LAUNCH_ROWS(ln_fwd_t_kernel<E>, rows, 0, x, w, b, y, mean, rstd, rows, eps, nullptr, nullptr, nullptr, \
+                           nullptr, 0)
+    case 128: LNF(2); break;
+    case 256: LNF(4); break;
+    case 384: LNF(6); break;
+    case 512: LNF(8); break;
+    case 768: LNF(12); break;
+    case 1024: LNF(16); break;
+#undef LNF
     default: LAUNCH_ROWS(ln_fwd_kernel, rows, 0, x, w, b, y, mean, rstd, rows, (int)d, eps);
   }
   ASRX_LAUNCHED("asrx_layernorm_fwd");
+}
+
+// LayerNorm forward with the fused row outputs of ln_fwd_t_kernel (nrm and/or the sigmoid gate; each
+// may be null).  d must be one of 128, 256, 384, 512, 768, 1024.
+int asrx_layernorm_fwd2(const float* x, const float* w, const float* b, float* y, float* mean, float* rstd,
+                        float* nrm, const float* gw, const float* gb, float* gout, int gate_on_x, int64_t rows,
+                        int64_t d, float eps, hipStream_t stream) {
+  if (rows == 0) return 0;
+  const bool al = ((((uintptr_t)x | (uintptr_t)w | (uintptr_t)b | (uintptr_t)y | (uintptr_t)gw) & 7) == 0);
+  ASRX_REQUIRE(al, "asrx_layernorm_fwd2: 8-byte aligned rows required");
+  switch (d) {
+#define LNF(E) LAUNCH_ROWS(ln_fwd_t_kernel<E>, rows, 0, x, w, b, y, mean, rstd, rows, eps, nrm, gw, gb, gout, gate_on_x)
+    case 128: LNF(2); break;
+    case 256: LNF(4); break;
+    case 384: LNF(6); break;
+    case 512: LNF(8); break;
+    case 768: LNF(12); break;
+    case 1024: LNF(16); break;
+#undef LNF
+    default: ASRX_REQUIRE(false, "asrx_layernorm_fwd2: d=%ld unsupported", (long)d);
+  }
+  ASRX_LAUNCHED("asrx_layernorm_fwd2");
 }
 
 int asrx_layernorm_bwd_acc(const float* dy, const float* x, const float* w, const float* mean, const float* rstd,
@@ -1594,6 +1884,65 @@ int asrx_vgate_bwd(const float* dion, const float* S, const float* nx, const flo
                                                                     inv_sqrt_d);
   ASRX_LAUNCHED("asrx_vgate_bwd");
 }
+
+int asrx_vgate_weights(const float* mkey, const float* W1, const float* b1, float* Wc, float* bc, float* mkn,
+                       unsigned short* wb, int64_t M, int64_t Dh, int64_t D, hipStream_t stream) {
+  if (M + Dh == 0) return 0;
+  LAUNCH_ROWS(vgate_weights_kernel, M + Dh, 0, mkey, W1, b1, Wc, bc, mkn, wb, (int)M, (int)Dh, (int)D);
+  ASRX_LAUNCHED("asrx_vgate_weights");
+}
+
+#define MS_DISPATCH(KER, GRID, SHM, P)                                             \
+  switch (d) {                                                                     \
+    case 128: KER<2><<<GRID, 64 * RW, SHM, stream>>>(P); break;                    \
+    case 256: KER<4><<<GRID, 64 * RW, SHM, stream>>>(P); break;                    \
+    case 384: KER<6><<<GRID, 64 * RW, SHM, stream>>>(P); break;                    \
+    case 512: KER<8><<<GRID, 64 * RW, SHM, stream>>>(P); break;                    \
+    case 768: KER<12><<<GRID, 64 * RW, SHM, stream>>>(P); break;                   \
+    case 1024: KER<16><<<GRID, 64 * RW, SHM, stream>>>(P); break;                  \
+    default: ASRX_REQUIRE(false, #KER ": d=%ld unsupported", (long)d);             \
+  }
+
+static bool ms_aligned(std::initializer_list<const void*> ps) {
+  for (const void* q : ps)
+    if ((uintptr_t)q & 7) return false;
+  return true;
+}
+
+// Fused MSheath layer row pass (msheath_row_fwd_kernel); SH = [S | h] with row stride ldsh >= M + Dh.
+int asrx_msheath_row_fwd(const float* x, const float* lnw, const float* lnb, const float* gw, const float* gb,
+                         const float* SH, int64_t ldsh, const float* mval, const float* w2, const float* b2,
+                         const float* cw, const float* cb, const float* tx, float* px, float* mean, float* rstd,
+                         float* nx, float* g, float* ion, float* kv, float* m2, int64_t rows, int64_t d, int64_t M,
+                         int64_t Dh, float eps, float inv_sqrt_d, hipStream_t stream) {
+  ASRX_REQUIRE(M <= 64 && ldsh >= M + Dh, "asrx_msheath_row_fwd: M <= 64 and ldsh >= M + Dh required");
+  ASRX_REQUIRE(ms_aligned({x, lnw, lnb, gw, px}), "asrx_msheath_row_fwd: 8-byte aligned rows required");
+  if (rows == 0) return 0;
+  MSRowFwd p{x, lnw, lnb, gw, gb, SH, mval, w2, b2, cw, cb, tx, px, mean, rstd, nx, g, ion, kv, m2, rows, ldsh,
+             (int)M, (int)Dh, eps, inv_sqrt_d};
+  MS_DISPATCH(msheath_row_fwd_kernel, row_grid(rows), 0, p);
+  ASRX_LAUNCHED("asrx_msheath_row_fwd");
+}
+
+// Its backward (msheath_row_bwd_kernel).  dx is accumulated; every parameter gradient is accumulated
+// (atomics); dSH (stride ldsh) is written.
+int asrx_msheath_row_bwd(const float* dpx, const float* x, const float* lnw, const float* lnb, const float* mean,
+                         const float* rstd, const float* dg, const float* g, const float* gw, const float* dion,
+                         const float* SH, int64_t ldsh, const float* nx, const float* mval, const float* w2,
+                         const float* cw, const float* kv, const float* m2, float* dx, float* dlnw, float* dlnb,
+                         float* dgw, float* dgb, float* dSH, float* dmval, float* dw2, float* db2, float* dcw,
+                         float* dcb, float* db1, int64_t rows, int64_t d, int64_t M, int64_t Dh, float inv_sqrt_d,
+                         hipStream_t stream) {
+  ASRX_REQUIRE(M <= 64 && ldsh >= M + Dh, "asrx_msheath_row_bwd: M <= 64 and ldsh >= M + Dh required");
+  ASRX_REQUIRE(ms_aligned({dpx, x, lnw, lnb, gw, dx}), "asrx_msheath_row_bwd: 8-byte aligned rows required");
+  if (rows == 0) return 0;
+  MSRowBwd p{dpx, x, lnw, lnb, mean, rstd, dg, g, gw, dion, SH, nx, mval, w2, cw, kv, m2, dx, dlnw, dlnb, dgw, dgb,
+             dSH, dmval, dw2, db2, dcw, dcb, db1, rows, ldsh, (int)M, (int)Dh, inv_sqrt_d};
+  const size_t shm = (size_t)RW * (3 * d + M + 2 * Dh + 5) * sizeof(float);
+  MS_DISPATCH(msheath_row_bwd_kernel, row_grid(rows, 1024), shm, p);
+  ASRX_LAUNCHED("asrx_msheath_row_bwd");
+}
+#undef MS_DISPATCH
 
 int asrx_tgate_fwd(const float* G, const float* c, float* out, int64_t rows, int64_t D, hipStream_t stream) {
   if (rows == 0) return 0;

@@ -125,6 +125,13 @@ int asrx_layernorm_bwd(const float* dy, const float* x, const float* w, const fl
 int asrx_layernorm_bwd_acc(const float* dy, const float* x, const float* w, const float* mean, const float* rstd,
                            float* dx, float* dw, float* db, int64_t rows, int64_t d, int acc, asrx_stream_t stream);
 
+/* LayerNorm forward with fused row outputs (each may be NULL): nrm = |x| (v_gate's norm of the same
+ * x, model.py:347) and gout = sigmoid(v . gw + gb) with v = y, or v = x when gate_on_x (the Linear(D,1)
+ * gates at model.py:460, 503).  d in {128, 256, 384, 512, 768, 1024}. */
+int asrx_layernorm_fwd2(const float* x, const float* w, const float* b, float* y, float* mean, float* rstd,
+                        float* nrm, const float* gw, const float* gb, float* gout, int gate_on_x, int64_t rows,
+                        int64_t d, float eps, asrx_stream_t stream);
+
 /* ---- small-N linear (N <= 4): gate / mem_gate / mlp_gate Linear(D,1) (model.py:398, 406, 420),
  *      v_gate.mlp[2] (341), tgate.cs Linear(D,3) (530), MPNet's Linear(128,3) (381).
  *      act: 0 none, 3 sigmoid.  Backward: dx = beta*dx + dz W; dW/db accumulated. ------------------ */
@@ -165,6 +172,28 @@ int asrx_vgate_bwd(const float* dion, const float* S, const float* nx, const flo
                    const float* w2, const float* cw, const float* kv, const float* m2, float* dS, float* dnx,
                    float* dh, float* dmval, float* dw2, float* db2, float* dcw, float* dcb, int64_t rows, int64_t M,
                    int64_t Dh, float inv_sqrt_d, asrx_stream_t stream);
+
+/* ---- fused MSheath layer rows (asrx/msheath.py; model.py:346-351, 452-461).  v_gate's projections
+ *      as one GEMM against Wc = [normalize(mkey); mlp[0].weight] ((M+Dh) x D), bc = [0; mlp[0].bias]
+ *      (asrx_vgate_weights; wb = bf16 Wc or NULL, mkn = key norms), giving SH = [S | h] (row stride
+ *      ldsh).  asrx_msheath_row_fwd: per row px = LayerNorm(x), nx = |x|, g = sigmoid(px.gw + gb), the
+ *      v_gate outputs (ion, kv, m2).  asrx_msheath_row_bwd: its backward with dx accumulated, dSH
+ *      written and every parameter gradient accumulated; db1 is mlp[0].bias's gradient.  d in {128,
+ *      256, 384, 512, 768, 1024}, M <= 64. */
+int asrx_vgate_weights(const float* mkey, const float* W1, const float* b1, float* Wc, float* bc, float* mkn,
+                       unsigned short* wb, int64_t M, int64_t Dh, int64_t D, asrx_stream_t stream);
+int asrx_msheath_row_fwd(const float* x, const float* lnw, const float* lnb, const float* gw, const float* gb,
+                         const float* SH, int64_t ldsh, const float* mval, const float* w2, const float* b2,
+                         const float* cw, const float* cb, const float* tx, float* px, float* mean, float* rstd,
+                         float* nx, float* g, float* ion, float* kv, float* m2, int64_t rows, int64_t d, int64_t M,
+                         int64_t Dh, float eps, float inv_sqrt_d, asrx_stream_t stream);
+int asrx_msheath_row_bwd(const float* dpx, const float* x, const float* lnw, const float* lnb, const float* mean,
+                         const float* rstd, const float* dg, const float* g, const float* gw, const float* dion,
+                         const float* SH, int64_t ldsh, const float* nx, const float* mval, const float* w2,
+                         const float* cw, const float* kv, const float* m2, float* dx, float* dlnw, float* dlnb,
+                         float* dgw, float* dgb, float* dSH, float* dmval, float* dw2, float* db2, float* dcw,
+                         float* dcb, float* db1, int64_t rows, int64_t d, int64_t M, int64_t Dh, float inv_sqrt_d,
+                         asrx_stream_t stream);
 
 /* ---- tgate (model.py:532-535): G = sigmoid(x Wcat^T + b) (rows,3D) from asrx_gemm, c (rows,3). */
 int asrx_tgate_fwd(const float* G, const float* c, float* out, int64_t rows, int64_t D, asrx_stream_t stream);
@@ -211,6 +240,22 @@ int asrx_msheath_ctrl_bwd2(const float* g_alpha, const float* g_beta, const floa
                            const float* jump_s, const void* rec, int64_t layer_i, int64_t layers, int64_t B, int64_t D,
                            float* g_policy, int acc_policy, float* g_mem_v, float* g_mem_w, float* g_mem,
                            float* g_jump_s, int* has_orig, asrx_stream_t stream);
+/* ctrl with mem_v = sigmoid(mem . mg_w + mg_b) computed in the kernel (mem_gate, model.py:464; written
+ * to mem_v_out) and, backward, its gradient fused (g_mem += ..., g_mg_w / g_mg_b accumulated). */
+int asrx_msheath_ctrl_fwd3(const float* policy, const float* gpol, int64_t ld_gpol, const float* ion,
+                           const float* mg_w, const float* mg_b, float* mem_v_out, const float* mem_w,
+                           int64_t ld_mem_w, const float* mem, const float* jump_s, const float* next_i,
+                           int64_t layer_i, int64_t layers, int64_t B, int64_t L, int64_t D, float* alpha, float* beta,
+                           float* gam, float* mem_w_out, float* active, float* next_out, void* rec,
+                           asrx_stream_t stream);
+int asrx_msheath_ctrl_bwd3(const float* g_alpha, const float* g_beta, const float* g_gam, const float* g_mwo,
+                           const float* mem_v, const float* mem_w, int64_t ld_mem_w, const float* mem,
+                           const float* jump_s, const void* rec, int64_t layer_i, int64_t layers, int64_t B, int64_t D,
+                           float* g_policy, int acc_policy, float* g_mem_w, float* g_mem, float* g_jump_s,
+                           int* has_orig, const float* mg_w, float* g_mg_w, float* g_mg_b, asrx_stream_t stream);
+/* x_new = x + s1 s2 y and mem += (1/L) sum_l x_new per sample (mem zeroed by the caller), d <= 1024. */
+int asrx_axpy_row2_colsum(const float* x, const float* s1, const float* s2, const float* y, float* out, float* mem,
+                          int64_t B, int64_t L, int64_t d, asrx_stream_t stream);
 /* MSheath fused backward (asrx/msheath.py): jump_select backward in accumulate form (active: dxn =
  * alpha g, orig's gradient (+)= beta g on a jump; inactive: dx = g), the x_new/mem backward writing
  * x's gradient for active samples (g' = dxn + gm/L), and the final dx += orig grad + u broadcast. */
@@ -228,7 +273,8 @@ int asrx_axpy_row2(const float* x, const float* s1, const float* s2, const float
                    int64_t d, asrx_stream_t stream);
 int asrx_axpy_row2_bwd(const float* g, const float* s1, const float* s2, const float* y, float* dy, float* ds1,
                        float* ds2, int64_t rows, int64_t d, asrx_stream_t stream);
-/* float4 forms of asrx_jump_select(_bwd) for d % 4 == 0 (the backward zeroes dalpha/dbeta/dgam). */
+/* float4 forms of asrx_jump_select(_bwd) for d % 4 == 0 (the backward zeroes dalpha/dbeta/dgam: one
+ * memset when they are one block [dalpha | dbeta | dgam], as asrx_jump_select4_bwd_acc too). */
 int asrx_jump_select4(const float* xn, const float* orig, const float* xold, const float* act, const float* alpha,
                       const float* beta, const float* gam, float* out, int64_t B, int64_t L, int64_t d,
                       asrx_stream_t stream);

@@ -250,8 +250,8 @@ def test_tgate(cuda):
     assert _rel(gg[0], gr[0]) < 1e-4
 
 
-@pytest.mark.parametrize("fused", [True, False])
-def test_msheath(cuda, fused):
+@pytest.mark.parametrize("fused,D", [(True, 128), (True, 384), (False, 128), (False, 192)])
+def test_msheath(cuda, fused, D):
     """MSheath (model.py:387-507), the fused single-node path (asrx/msheath.py, hand-written backward)
     and the per-op composition, against the oracle's per-sample while-loop: output, input gradient and
     every parameter's gradient, with potentials spread around the 0.1 threshold so samples take
@@ -260,10 +260,13 @@ def test_msheath(cuda, fused):
     from asrx.model import MSheath
     from asrx.noise import NoiseCtx
 
+    from asrx import msheath as ms
+
     torch.manual_seed(3)
-    D, layer = 128, 4
+    layer = 4
     mod = MSheath(D, 2, layer).cuda()
     mod.fused = fused
+    assert ms.supported(mod, D) == (D in ms.ROW_DIMS)  # D=192: the composed path (no fused row kernel)
     with torch.no_grad():
         for i in range(layer):  # spread x_val around the 0.3 threshold so potentials vary per sample
             mod.layers[i]["v_gate"].concat.bias.fill_(0.3 + 0.1 * (i - 1))

@@ -1,7 +1,7 @@
 set -e
 R=${GRAFT_REPO_ROOT:-/root/repo}
 cd $R; mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "msheath or model_parity_fp32 or skip_dead or gradsync" > gpurun_out/t_ms.log 2>&1 || { tail -60 gpurun_out/t_ms.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${1:-msheath or model_parity_fp32 or skip_dead or gradsync}" > gpurun_out/t_ms.log 2>&1 || { grep -E "PASSED|FAILED|Error|error|assert" gpurun_out/t_ms.log | tail -40; exit 1; }
 grep -E "PASSED|FAILED|passed|failed" gpurun_out/t_ms.log | tail -20
 timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail -20 gpurun_out/bench.err; exit 1; }
 python -c "import json;d=json.load(open('gpurun_out/bench.json'));print(d['value'],d['ms_per_step'],d.get('dead_block_eliminated'))"
