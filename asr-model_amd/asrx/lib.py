@@ -59,11 +59,26 @@ SIGNATURES = {
     "asrx_zero": (_i32, [_p, _i64, _p]),
     "asrx_rotary_fwd": (_i32, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _f32, _p]),
     "asrx_rotary_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _f32, _p]),
+    "asrx_abby_bwd2": (_i32, [_p] * 10 + [_i64, _i64, _i32, _p]),
+    "asrx_rownorm_bwd2": (_i32, [_p, _p, _p, _p, _i64, _i64, _i32, _p]),
+    "asrx_colsum_ld": (_i32, [_p, _i64, _p, _i64, _i64, _p]),
+    "asrx_ce_fwd1": (_i32, [_p] * 6 + [_i64, _i64, _p]),
+    "asrx_ce_bwd2": (_i32, [_p] * 6 + [_i64, _i64, _p]),
+    "asrx_bn_running": (_i32, [_p] * 5 + [_i64, _i64, _i64, _f32, _f32, _p]),
+    "asrx_rsqrt_eps": (_i32, [_p, _p, _i64, _f32, _p]),
+    "asrx_conv3_weight": (_i32, [_p, _p, _i64, _i64] + [_p] * 6),
+    "asrx_conv3_weight_bwd": (_i32, [_p] * 4 + [_i64, _i64] + [_p] * 3),
+    "asrx_blend_fwd": (_i32, [_p] * 4 + [_i64, _p]),
+    "asrx_blend_bwd": (_i32, [_p] * 7 + [_i64, _p]),
+    "asrx_add_segments": (_i32, [_p, _i64, _p, _p, _p, _i64, _p]),
+    "asrx_cat3": (_i32, [_p] * 3 + [_i64, _p, _p]),
     "asrx_layernorm_fwd2": (_i32, [_p] * 10 + [_i32, _i64, _i64, _f32, _p]),
     "asrx_vgate_weights": (_i32, [_p] * 7 + [_i64, _i64, _i64, _p]),
     "asrx_msheath_row_fwd": (_i32, [_p] * 6 + [_i64] + [_p] * 14 + [_i64] * 4 + [_f32, _f32, _p]),
     "asrx_msheath_row_bwd": (_i32, [_p] * 11 + [_i64] + [_p] * 18 + [_i64] * 4 + [_f32, _p]),
-    "asrx_msheath_ctrl_fwd3": (_i32, [_p, _p, _i64, _p, _p, _p, _p, _p, _i64, _p, _p, _p] + [_i64] * 5 + [_p] * 8),
+    "asrx_msheath_ctrl_fwd3": (_i32, [_p, _p, _i64, _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p] + [_i64] * 5 + [_p] * 8),
+    "asrx_mem_chunks": (_i64, [_i64]),
+    "asrx_seg_colsum_det": (_i32, [_p, _p, _p, _i64, _i64, _i64, _f32, _p]),
     "asrx_msheath_ctrl_bwd3": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _p, _p, _p] + [_i64] * 4 + [_p, _i32] + [_p] * 8),
     "asrx_axpy_row2_colsum": (_i32, [_p] * 6 + [_i64] * 3 + [_p]),
     "asrx_vgate_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _f32, _p]),

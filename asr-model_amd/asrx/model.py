@@ -19,7 +19,7 @@ from torch import nn
 from torch.nn.utils.parametrizations import weight_norm
 
 from . import gemm as gemm_mod
-from . import ops
+from . import lib, ops
 from .config import Dimensions
 from .noise import NoiseCtx
 
@@ -121,6 +121,7 @@ class ConvLite(nn.Module):
     def run(self, x, noise: NoiseCtx, site: str, sid_base: int):
         """model.py:109-118 on channels-last (B, T, D)."""
         D = x.shape[-1]
+        x = ops.fork(x)  # read by point1 and the residual add
         res = x
         y = ops.linear(x, self.point1.weight.view(2 * D, D), self.point1.bias)
         y = ops.glu(y)
@@ -142,13 +143,12 @@ class ConvLite(nn.Module):
     def _update_running(self, stats, T):
         # batch-1 semantics: one update per clip would be applied by the reference; here the mean of
         # the per-clip statistics is applied once per stream group (running stats do not affect the
-        # train-mode output).
+        # train-mode output).  One kernel (asrx_bn_running) instead of the ATen update chain.
         mean, rstd = stats
-        var = (1.0 / (rstd * rstd) - self.bn.eps) * (T / max(T - 1, 1))
-        m = self.bn.momentum
-        self.bn.running_mean.mul_(1 - m).add_(mean.mean(0), alpha=m)
-        self.bn.running_var.mul_(1 - m).add_(var.mean(0), alpha=m)
-        self.bn.num_batches_tracked += 1
+        B, C = mean.shape
+        bn = self.bn
+        lib.call("asrx_bn_running", lib.ptr(mean), lib.ptr(rstd), lib.ptr(bn.running_mean), lib.ptr(bn.running_var),
+                 lib.ptr(bn.num_batches_tracked), B, C, T, float(bn.eps), float(bn.momentum), lib.stream())
 
 
 class AudioEncoder(nn.Module):
@@ -180,7 +180,7 @@ class AudioEncoder(nn.Module):
         B, C, T = x.shape
         if C > 1:
             xt = x.transpose(1, 2).contiguous()
-            return ops.Conv3.apply(xt, self.conv1[0].weight, self.conv1[0].bias)
+            return ops.conv3(xt, self.conv1[0])
         return ops.Stem1.apply(x.reshape(B, T), self.conv2[0].weight, self.conv2[0].bias)
 
     def layers(self, x, noise: NoiseCtx, sid_base: int):
@@ -190,7 +190,7 @@ class AudioEncoder(nn.Module):
             if not fused_lead:
                 x = ops.act(x, "gelu")
             fused_lead = False
-            x = ops.Conv3.apply(x, layer[1].weight, layer[1].bias)
+            x = ops.conv3(x, layer[1])
             x = ops.layer_norm(x, layer[2].gamma, layer[2].beta, layer[2].eps)
             x = layer[3].run(x, noise, f"enc.L{l}", sid_base)
             x = ops.act(x, "gelu")
@@ -215,8 +215,7 @@ class AudioEncoder(nn.Module):
                 j += 1
             x = stems[i] if j == i + 1 else torch.cat(stems[i:j], 0)
             y = self.layers(x, noise, i * B)
-            for s in range(i, j):
-                out[s] = y[(s - i) * B:(s - i + 1) * B]
+            out[i:j] = ops.split_rows(y, j - i)
             i = j
         return out
 
@@ -255,10 +254,9 @@ class attention(nn.Module):  # noqa: N801
         '(kv h d)' -> k: scale + rotary(|src|) + per-head AbbyNormal."""
         B, L, D = src.shape
         H, hd = self.head, D // self.head
+        src = ops.fork(src)  # read by the kv AbbyNormal and rotary's |src|
         kvn = self.kv[0].run(src, noise, site + ".kv", sid_base, L)
-        W, b = self.kv[1].weight, self.kv[1].bias
-        k = ops.linear(kvn, W[:D], b[:D])
-        v = ops.linear(kvn, W[D:], b[D:])
+        k, v = ops.kv_proj(kvn, self.kv[1].weight, self.kv[1].bias)
         k = ops.rotary(k, src, rotary_freqs(D, H, masked, src.device), hd, self.scale)
         k = self.ln.run(k.view(B, L, H, hd), noise, site + ".kh", sid_base, L, H)
         return k, v.view(B, L, H, hd)
@@ -275,6 +273,7 @@ class attention(nn.Module):  # noqa: N801
         """x: attention input (B, Lq, D); kv: None (self attention on x) or (k, v) of the cross
         source.  Returns the out-projected (B, Lq, D)."""
         B, L, D = x.shape
+        x = ops.fork(x)  # read by the q (and, self-attention, kv) AbbyNormal and rotary's |x|
         if kv is None:
             kv = self.project_kv(x, noise, site, sid_base, masked)
         q = self.project_q(x, noise, site, sid_base, masked)
@@ -424,12 +423,12 @@ class residual(nn.Module):  # noqa: N801  (model.py:559-583)
         """residual.forward with the cross source given as precomputed (k, v) (see xa_side)."""
         L = x.shape[1]
         h = self.ln.run(x, noise, site + ".ln0", sid_base, L)
-        x = self.jump.run(h, noise, site + ".jump", sid_base)
+        x = ops.fork(self.jump.run(h, noise, site + ".jump", sid_base))  # each x: an AbbyNormal + an add
         h = self.ln.run(x, noise, site + ".ln1", sid_base, L)
-        x = ops.add(x, self.attn.run(h, None, noise, site + ".sa", sid_base, masked))
+        x = ops.fork(ops.add(x, self.attn.run(h, None, noise, site + ".sa", sid_base, masked)))
         if kv is not None:
             h = self.ln.run(x, noise, site + ".ln2", sid_base, L)
-            x = ops.add(x, self.attn.run(h, kv, noise, site + ".ca", sid_base, False))
+            x = ops.fork(ops.add(x, self.attn.run(h, kv, noise, site + ".ca", sid_base, False)))
         m = self.ln.run(x, noise, site + ".mlp.ln0", sid_base, L)
         m = ops.tgate(self.mlp[1], m)
         m = ops.linear(m, self.mlp[2].weight, self.mlp[2].bias, act="gelu")
@@ -445,10 +444,6 @@ class residual(nn.Module):  # noqa: N801  (model.py:559-583)
         xa = self.ln.run(xa, noise, site + ".ln", sid_base, S)
         xa = self.jump.run(xa, noise, site + ".jump", sid_base)
         return self.attn.project_kv(xa, noise, site + ".ca", sid_base, False)
-
-
-def _split(t, B):
-    return [t[i * B:(i + 1) * B] for i in range(t.shape[0] // B)]
 
 
 class processor(nn.Module):  # noqa: N801  (model.py:585-629)
@@ -474,7 +469,7 @@ class processor(nn.Module):  # noqa: N801  (model.py:585-629)
     def forward(self, x, xa, noise: NoiseCtx, seq=False):
         B, T = x.shape
         xe = ops.Embedding.apply(x, self.token.weight)
-        x = ops.add_rows(xe, self.position[:T])
+        x = ops.add_rows(xe, self.position)
         A_in = [xa["a"], xa["b"], xa["c"]]
         nblk = len(self.block)
         side = None
@@ -491,7 +486,7 @@ class processor(nn.Module):  # noqa: N801  (model.py:585-629)
                     side = self._side
                     side.wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(side) if conc else contextlib.nullcontext():
-                    a = blk.call(x, noise, f"b{i}.ta", 0, masked=True)
+                    a = ops.fork(blk.call(x, noise, f"b{i}.ta", 0, masked=True))
                 A = self._audio(blk, A_in, noise, f"b{i}.audio", B, "call")
                 KV = self._audio(blk, A, noise, f"b{i}.xa", B, "xa")
                 if conc:
@@ -501,9 +496,9 @@ class processor(nn.Module):  # noqa: N801  (model.py:585-629)
                 with torch.cuda.stream(side) if conc else contextlib.nullcontext():
                     if conc:
                         side.wait_event(ev)
-                    b_ = blk.call(a, noise, f"b{i}.tb", 0, kv=KV[0])
-                    c_ = blk.call(b_, noise, f"b{i}.tc", 0, kv=KV[1])
-                    d = blk.call(c_, noise, f"b{i}.td", 0, kv=KV[2])
+                    b_ = ops.fork(blk.call(a, noise, f"b{i}.tb", 0, kv=KV[0]))
+                    c_ = ops.fork(blk.call(b_, noise, f"b{i}.tc", 0, kv=KV[1]))
+                    d = ops.fork(blk.call(c_, noise, f"b{i}.td", 0, kv=KV[2]))
                     e = ops.add(a, b_, c_)
                     kve = blk.xa_side(e, noise, f"b{i}.tg.xa", 0)
                     g = blk.call(d, noise, f"b{i}.tg", 0, kv=kve)
@@ -513,9 +508,8 @@ class processor(nn.Module):  # noqa: N801  (model.py:585-629)
         if seq:
             out = g
         else:
-            blend = torch.sigmoid(self.blend)
-            out = blend * d + (1 - blend) * g
-        out = self.ln.run(out.contiguous(), noise, "final.ln", 0, T)
+            out = ops.blend(d, g, self.blend)  # sigmoid(blend) d + (1 - sigmoid(blend)) g
+        out = self.ln.run(out, noise, "final.ln", 0, T)
         return ops.linear(out, self.token.weight)
 
     # ---- decoding (Model.generate): the y-independent audio side of the only live block, once
@@ -535,7 +529,7 @@ class processor(nn.Module):  # noqa: N801  (model.py:585-629)
         B, T = x.shape
         i = len(self.block) - 1
         blk = self.block[i]
-        h = ops.add_rows(ops.Embedding.apply(x, self.token.weight), self.position[:T])
+        h = ops.add_rows(ops.Embedding.apply(x, self.token.weight), self.position)
         a = blk.call(h, noise, f"b{i}.ta", 0, masked=True)
         b_ = blk.call(a, noise, f"b{i}.tb", 0, kv=kv[0])
         c_ = blk.call(b_, noise, f"b{i}.tc", 0, kv=kv[1])
@@ -554,14 +548,13 @@ class processor(nn.Module):  # noqa: N801  (model.py:585-629)
             j = i + 1
             while j < 3 and streams[j].shape[1] == streams[i].shape[1]:
                 j += 1
-            x = streams[i] if j == i + 1 else torch.cat(streams[i:j], 0)
+            x = ops.group(streams[i:j])  # the batched tensor itself when the streams are its views
             if kind == "call":
                 y = blk.call(x, noise, site, i * B)
-                for s, part in zip(range(i, j), _split(y, B)):
-                    out[s] = part
+                out[i:j] = ops.split_rows(y, j - i)
             else:
                 k, v = blk.xa_side(x, noise, site, i * B)
-                for s, kk, vv in zip(range(i, j), _split(k, B), _split(v, B)):
+                for s, kk, vv in zip(range(i, j), ops.split_rows(k, j - i), ops.split_rows(v, j - i)):
                     out[s] = (kk, vv)
             i = j
         return out
@@ -601,7 +594,8 @@ class Model(nn.Module):
 
         streams = [aborc(pitch, spectrogram, waveform), aborc(spectrogram, pitch, waveform),
                    aborc(waveform, pitch, spectrogram)]
-        streams = [s.to(torch.float32).contiguous() for s in streams]
+        # no .contiguous(): the stems read a (B, 128, F) spectrogram through its (B, F, 128) layout
+        streams = [s.to(torch.float32) for s in streams]
         B = first.shape[0]
         # how this step is batched decides how many gradient contributions each shared weight gets
         # (equal-length streams share one pass): asrx.dist.GradSync keys its event plans on it

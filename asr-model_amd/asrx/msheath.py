@@ -73,8 +73,10 @@ def forward(mod, x0, gpol, save):
     st = _S()
     sv = {} if save else None
     # policy = softmax(MPNet(mean_l x))            model.py:432-435, 375-385
+    nchunk = int(lib.load().asrx_mem_chunks(L))
+    part = _E(len(mod.layers) + 1, B, nchunk, D, device=dev)  # row-chunk column sums (deterministic means)
     pooled = _E(B, D, device=dev)
-    lib.call("asrx_seg_colsum", _P(x0), _P(pooled), B, L, D, 1.0 / L, 0, st)
+    lib.call("asrx_seg_colsum_det", _P(x0), _P(part[-1]), _P(pooled), B, L, D, 1.0 / L, st)
     net = mod.pnet.net
     zp = _E(B, net[0].weight.shape[0], device=dev) if save else None
     hp = G.linear_fwd(pooled, net[0].weight, net[0].bias, act="silu", preact=zp)
@@ -83,8 +85,6 @@ def forward(mod, x0, gpol, save):
     policy = _E(B, 3, device=dev)
     lib.call("asrx_softmax_small", _P(pl), _P(policy), B, 3, st)
     nl = len(mod.layers)
-    mem_all = _E(nl, B, D, device=dev)  # every layer's mem = mean_l x_new, accumulated by atomics
-    lib.call("asrx_zero", _P(mem_all), mem_all.numel() * 4, st)
     wide = G.use_wide(D)
     mg = mod.mem_gate[0]
     mem_w, ld_mw = mod.mem_w, 0
@@ -115,16 +115,15 @@ def forward(mod, x0, gpol, save):
         out = G.linear_fwd(px, lay["adapter"].weight, lay["adapter"].bias) if lay["adapter"] is not None else px
         # x_new = x + g * ion * out; mem = mean_l x_new   (461-463)
         x_new = _E(B, L, D, device=dev)
-        mem = mem_all[i]
-        lib.call("asrx_axpy_row2_colsum", _P(x), _P(gv), _P(ion), _P(out), _P(x_new), _P(mem), B, L, D, st)
+        lib.call("asrx_axpy_row2_colsum", _P(x), _P(gv), _P(ion), _P(out), _P(x_new), _P(part[i]), B, L, D, st)
         # mem_v = sigmoid(mem_gate(mem)); control; jump select   (464-501)
         alpha, beta, active, next_out, mem_v = (_E(B, device=dev) for _ in range(5))
-        gam, mwo = _E(B, D, device=dev), _E(B, D, device=dev)
+        gam, mwo, mem = _E(B, D, device=dev), _E(B, D, device=dev), _E(B, D, device=dev)
         rec = _E(B * rec_bytes, dtype=torch.uint8, device=dev)
         gp = gpol[:, i]
         lib.call("asrx_msheath_ctrl_fwd3", _P(policy), _P(gp), gp.stride(0), _P(ion), _P(mg.weight), _P(mg.bias),
-                 _P(mem_v), _P(mem_w), ld_mw, _P(mem), _P(mod.jump_s), _P(next_i), i, nl, B, L, D, _P(alpha),
-                 _P(beta), _P(gam), _P(mwo), _P(active), _P(next_out), _P(rec), st)
+                 _P(mem_v), _P(mem_w), ld_mw, _P(part[i]), _P(mem), _P(mod.jump_s), _P(next_i), i, nl, B, L, D,
+                 _P(alpha), _P(beta), _P(gam), _P(mwo), _P(active), _P(next_out), _P(rec), st)
         x_out = _E(B, L, D, device=dev)
         lib.call("asrx_jump_select4", _P(x_new), _P(x0), _P(x), _P(active), _P(alpha), _P(beta), _P(gam),
                  _P(x_out), B, L, D, st)

@@ -74,6 +74,118 @@ def _gret(p, g, direct):
             fn(p)
     return None
 
+# =============================================================================== multi-consumer activations
+# An activation read by several ops gets one gradient per consumer, which autograd sums with stock
+# add kernels.  fork(x) instead hands the consumers a GradSink: ops that support it (AbbyNormal,
+# Linear, rotary's |src|) accumulate x's gradient straight into the sink's buffer (the first writes,
+# later ones add: beta = 1 GEMMs, accumulate-mode row kernels) and return None to autograd;
+# ForkFn.backward, which autograd runs after every consumer, returns the buffer (plus, in one asrx
+# launch, the gradient of any consumer that did not use the sink).
+
+
+class GradSink:
+    __slots__ = ("buf",)
+
+    def __init__(self):
+        self.buf = None
+
+    def target(self, like):
+        """(buffer, acc): the first contributor writes its gradient (acc = 0), later ones add."""
+        if self.buf is None:
+            self.buf = _E(like.shape, device=like.device)
+            return self.buf, 0
+        return self.buf, 1
+
+
+class ForkFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, sink):
+        ctx.set_materialize_grads(False)
+        ctx.sink = sink
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        sink, ctx.sink = ctx.sink, None
+        buf, sink.buf = sink.buf, None
+        if buf is None:
+            return g, None
+        if g is not None:
+            g = _c(g)
+            lib.call("asrx_lincomb", _P(buf), _P(g), None, 1.0, 1.0, 0.0, _P(buf), buf.numel(), _S())
+        return buf, None
+
+
+def fork(x):
+    """x for several consumers whose gradients should meet in one buffer (see above)."""
+    if not (torch.is_grad_enabled() and x.requires_grad) or getattr(x, "_asrx_sink", None) is not None:
+        return x
+    sink = GradSink()
+    y = ForkFn.apply(x, sink)
+    y._asrx_sink = sink
+    return y
+
+
+def sink_of(x):
+    return getattr(x, "_asrx_sink", None)
+
+
+class SplitRows(torch.autograd.Function):
+    """A (n B, ...) stream group as n (B, ...) views (equal-length audio streams share one batched
+    pass); the backward joins the views' gradients in one kernel instead of autograd's zero-filled
+    full-size buffer per view plus an add."""
+
+    @staticmethod
+    def forward(ctx, x, n):
+        ctx.set_materialize_grads(False)
+        ctx.n = n
+        ctx.shape = x.shape
+        B = x.shape[0] // n
+        return tuple(x[i * B:(i + 1) * B] for i in range(n))
+
+    @staticmethod
+    def backward(ctx, *gs):
+        n = ctx.n
+        if all(g is None for g in gs):
+            return None, None
+        out = _E(ctx.shape, device=next(g for g in gs if g is not None).device)
+        per = out.numel() // n
+        if all(g is not None for g in gs) and n in (2, 3):
+            gs = [_c(g) for g in gs]
+            lib.call("asrx_cat3", _P(gs[0]), _P(gs[1]), _P(gs[2]) if n == 3 else None, per, _P(out), _S())
+            return out, None
+        of = out.view(n, per)
+        for i, g in enumerate(gs):
+            if g is None:
+                lib.call("asrx_zero", _P(of[i]), per * 4, _S())
+            else:
+                lib.call("asrx_lincomb", _P(_c(g)), None, None, 1.0, 0.0, 0.0, _P(of[i]), per, _S())
+        return out, None
+
+
+def split_rows(x, n):
+    """n views of a stream group, tagged so that group(...) can use the group tensor again."""
+    if n == 1:
+        return [x]
+    parts = SplitRows.apply(x, n) if (torch.is_grad_enabled() and x.requires_grad) else \
+        tuple(x[i * (x.shape[0] // n):(i + 1) * (x.shape[0] // n)] for i in range(n))
+    for i, t in enumerate(parts):
+        t._asrx_group = (x, i, n)
+    return list(parts)
+
+
+def group(parts):
+    """The batched tensor of consecutive stream views: the group they were split from when they are
+    exactly its parts in order, else one concatenation."""
+    if len(parts) == 1:
+        return parts[0]
+    g = getattr(parts[0], "_asrx_group", None)
+    if g is not None and g[2] == len(parts) and all(
+            getattr(t, "_asrx_group", (None, -1))[0] is g[0] and t._asrx_group[1] == i for i, t in enumerate(parts)):
+        return g[0]
+    return torch.cat(parts, 0)
+
+
 # =============================================================================== Linear (GEMM)
 
 
@@ -81,8 +193,9 @@ class Linear(torch.autograd.Function):
     """y = act(x W^T + b) on MFMA (nn.Linear / 1x1 Conv1d)."""
 
     @staticmethod
-    def forward(ctx, x, W, b, act="none", grad=True):
+    def forward(ctx, x, W, b, act="none", grad=True, sink=None):
         x = _c(x)
+        ctx.sink = sink
         # the pre-activation is kept only for a backward that will run (none in the reference's dead
         # blocks, eval or decoding: an N-wide fp32 write saved per call)
         z = _E(*x.shape[:-1], W.shape[0], device=x.device) if act != "none" and grad else None
@@ -103,13 +216,19 @@ class Linear(torch.autograd.Function):
             lib.call("asrx_act_bwd", _P(gy), _P(z), _P(gz), gy.numel(), ACT[ctx.act], _S())
         else:
             gz = gy
-        dx = G.linear_dgrad(gz, W) if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if ctx.sink is not None:
+                buf, acc = ctx.sink.target(x)
+                G.linear_dgrad(gz, W, out=buf, beta=float(acc))
+            else:
+                dx = G.linear_dgrad(gz, W)
         dW = db = None
         if ctx.needs_input_grad[1]:
             dW = _gret(W, G.linear_wgrad(gz, x, out=_gbuf(W, ctx.dW), accumulate=True), ctx.dW)
         if ctx.has_b and ctx.needs_input_grad[2]:
             db = _gret(b, colsum(gz, out=_gbuf(b, True) if ctx.db else None), ctx.db)
-        return dx, dW, db, None, None
+        return dx, dW, db, None, None, None
 
 
 def _grad_needed(*ts):
@@ -117,7 +236,62 @@ def _grad_needed(*ts):
 
 
 def linear(x, W, b=None, act="none"):
-    return Linear.apply(x, W, b, act, _grad_needed(x, W, b))
+    return Linear.apply(x, W, b, act, _grad_needed(x, W, b), sink_of(x))
+
+
+class KVProjFn(torch.autograd.Function):
+    """k, v = Linear(D, 2D) of the same normed source, split '(kv h d)' (model.py:261): two GEMMs on
+    the weight's row blocks (no copies), backward with both input gradients meeting in one buffer
+    (beta = 1) and the weight / bias gradients written into the blocks of p.grad."""
+
+    @staticmethod
+    def forward(ctx, x, W, b, sink):
+        x = _c(x)
+        D = W.shape[0] // 2
+        k = G.linear_fwd(x, W[:D], b[:D])
+        v = G.linear_fwd(x, W[D:], b[D:])
+        ctx.sink = sink
+        ctx.dW, ctx.db = _direct(ctx, 1, W), _direct(ctx, 2, b)
+        ctx.save_for_backward(x, W, b)
+        return k, v
+
+    @staticmethod
+    def backward(ctx, dk, dv):
+        x, W, b = ctx.saved_tensors
+        D = W.shape[0] // 2
+        dk = _c(dk) if dk is not None else None
+        dv = _c(dv) if dv is not None else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if ctx.sink is not None:
+                buf, acc = ctx.sink.target(x)
+            else:
+                buf, acc = _E(x.shape, device=x.device), 0
+            for gpart, Wp in ((dk, W[:D]), (dv, W[D:])):
+                if gpart is not None:
+                    G.linear_dgrad(gpart, Wp, out=buf, beta=float(acc))
+                    acc = 1
+            if acc == 0:
+                lib.call("asrx_zero", _P(buf), buf.numel() * 4, _S())
+            dx = None if ctx.sink is not None else buf
+        dWf = dbf = None
+        if ctx.needs_input_grad[1]:
+            gW = _gbuf(W, ctx.dW)
+            for i, gpart in enumerate((dk, dv)):
+                if gpart is not None:
+                    G.linear_wgrad(gpart, x, out=gW[i * D:(i + 1) * D], accumulate=True)
+            dWf = _gret(W, gW, ctx.dW)
+        if ctx.needs_input_grad[2]:
+            gb = _gbuf(b, ctx.db)
+            for i, gpart in enumerate((dk, dv)):
+                if gpart is not None:
+                    colsum(gpart.view(-1, D), out=gb[i * D:(i + 1) * D])
+            dbf = _gret(b, gb, ctx.db)
+        return dx, dWf, dbf, None
+
+
+def kv_proj(x, W, b):
+    return KVProjFn.apply(x, W, b, sink_of(x))
 
 
 def colsum(x2, out=None):
@@ -168,8 +342,9 @@ class AbbyNormalFn(torch.autograd.Function):
     """essentials.AbbyNormal (essentials.py:155-191): router GEMM on MFMA + fused row kernel."""
 
     @staticmethod
-    def forward(ctx, x, W1, b1, W2, b2, L, H, sid_base, key, use_noise, keep):
+    def forward(ctx, x, W1, b1, W2, b2, L, H, sid_base, key, use_noise, keep, sink=None):
         x = _c(x)
+        ctx.sink = sink
         d = x.shape[-1]
         rows = _rows(x)
         out = _E(x.shape, device=x.device)
@@ -196,16 +371,21 @@ class AbbyNormalFn(torch.autograd.Function):
         d = x.shape[-1]
         rows = _rows(x)
         fW1, fb1, fW2, fb2 = ctx.dp
-        dx = _E(x.shape, device=x.device)
+        if ctx.sink is not None:
+            dx, acc = ctx.sink.target(x)
+        else:
+            dx, acc = _E(x.shape, device=x.device), 0
         dh = _E(x.shape, device=x.device)
         dW2, db2 = _gbuf(W2, fW2), _gbuf(b2, fb2)
-        lib.call("asrx_abby_bwd", _P(gout), _P(x), _P(hpre), _P(W2), _P(ys), _P(idx), _P(dx), _P(dh), _P(dW2),
-                 _P(db2), rows, d, _S())
+        lib.call("asrx_abby_bwd2", _P(gout), _P(x), _P(hpre), _P(W2), _P(ys), _P(idx), _P(dx), _P(dh), _P(dW2),
+                 _P(db2), rows, d, acc, _S())
         G.linear_dgrad(dh, W1, out=dx, beta=1.0)
+        if ctx.sink is not None:
+            dx = None
         dW1 = G.linear_wgrad(dh, x, out=_gbuf(W1, fW1), accumulate=True)
         db1 = colsum(dh.view(-1, d), out=_gbuf(b1, fb1))
         return (dx, _gret(W1, dW1, fW1), _gret(b1, db1, fb1), _gret(W2, dW2, fW2), _gret(b2, db2, fb2),
-                None, None, None, None, None, None)
+                None, None, None, None, None, None, None)
 
 
 def abby_normal(mod, x, L, H, sid_base, key, use_noise=True):
@@ -214,7 +394,7 @@ def abby_normal(mod, x, L, H, sid_base, key, use_noise=True):
     r = mod.mode_router
     keep = torch.is_grad_enabled() and (x.requires_grad or r[0].weight.requires_grad)
     return AbbyNormalFn.apply(x, r[0].weight, r[0].bias, r[2].weight, r[2].bias, L, H, sid_base, key, use_noise,
-                              keep)
+                              keep, sink_of(x))
 
 
 # =============================================================================== LayerNorm
@@ -312,9 +492,10 @@ class RotaryFn(torch.autograd.Function):
     """rotary.forward (model.py:198-214) fused with the hd^-0.25 scale: x, src (B, L, D)."""
 
     @staticmethod
-    def forward(ctx, x, src, freqs, hd, scale):
+    def forward(ctx, x, src, freqs, hd, scale, sink=None):
         x = _c(x)
         src = _c(src)
+        ctx.sink = sink
         B, L, D = x.shape
         m = _E(B * L, device=x.device)
         lib.call("asrx_rownorm", _P(src), _P(m), B * L, D, _S())
@@ -330,16 +511,22 @@ class RotaryFn(torch.autograd.Function):
         gy = _c(gy)
         B, L, D = x.shape
         dx = _E(x.shape, device=x.device)
-        dm = torch.zeros(B * L, device=x.device)
+        dm = _E(B * L, device=x.device)  # written by the kernel
         lib.call("asrx_rotary_bwd", _P(gy), _P(x), _P(m), _P(freqs), _P(dx), _P(dm), B * L, L, D, ctx.hd,
                  float(ctx.scale), _S())
-        dsrc = torch.zeros_like(src)
-        lib.call("asrx_rownorm_bwd", _P(dm), _P(src), _P(m), _P(dsrc), B * L, D, _S())
-        return dx, dsrc, None, None, None
+        dsrc = None
+        if ctx.needs_input_grad[1]:
+            if ctx.sink is not None:
+                buf, acc = ctx.sink.target(src)
+            else:
+                buf, acc = _E(src.shape, device=src.device), 0
+            lib.call("asrx_rownorm_bwd2", _P(dm), _P(src), _P(m), _P(buf), B * L, D, acc, _S())
+            dsrc = None if ctx.sink is not None else buf
+        return dx, dsrc, None, None, None, None
 
 
 def rotary(x, src, freqs, hd, scale):
-    return RotaryFn.apply(x, src, freqs, hd, scale)
+    return RotaryFn.apply(x, src, freqs, hd, scale, sink_of(src))
 
 
 # =============================================================================== v_gate
@@ -409,25 +596,33 @@ def v_gate(mod, x):
 
 
 class TGateFn(torch.autograd.Function):
-    """tgate (model.py:532-535): one N=3D GEMM with sigmoid epilogue + softmax-weighted combine."""
+    """tgate (model.py:532-535): one N=3D GEMM with sigmoid epilogue + softmax-weighted combine.  The
+    three Linear(D, D) gates run as one Linear(D, 3D) over their concatenation (asrx_cat3, no ATen
+    cat); the backward's concatenated weight / bias gradients land in each gate's own p.grad
+    (asrx_add_segments / colsum over column blocks) instead of autograd's cat backward + adds."""
 
     @staticmethod
-    def forward(ctx, x, Wcat, bcat, Wcs, bcs):
+    def forward(ctx, x, W0, W1, W2, b0, b1, b2, Wcs, bcs):
         x = _c(x)
         D = x.shape[-1]
         rows = _rows(x)
+        Wcat = _E(3 * D, D, device=x.device)
+        bcat = _E(3 * D, device=x.device)
+        lib.call("asrx_cat3", _P(W0), _P(W1), _P(W2), D * D, _P(Wcat), _S())
+        lib.call("asrx_cat3", _P(b0), _P(b1), _P(b2), D, _P(bcat), _S())
         Gs = G.linear_fwd(x, Wcat, bcat, act="sigmoid")
         c = _E(rows, 3, device=x.device)
         lib.call("asrx_small_linear_fwd", _P(x), _P(Wcs), _P(bcs), _P(c), rows, D, 3, 0, _S())
         out = _E(x.shape, device=x.device)
         lib.call("asrx_tgate_fwd", _P(Gs), _P(c), _P(out), rows, D, _S())
-        ctx.dWcs, ctx.dbcs = _direct(ctx, 3, Wcs), _direct(ctx, 4, bcs)
-        ctx.save_for_backward(x, Wcat, Wcs, Gs, c, bcs)
+        ctx.dWcs, ctx.dbcs = _direct(ctx, 7, Wcs), _direct(ctx, 8, bcs)
+        ctx.dparts = all(_direct(ctx, k, t) for k, t in enumerate((W0, W1, W2, b0, b1, b2), 1))
+        ctx.save_for_backward(x, Wcat, Wcs, Gs, c, bcs, W0, W1, W2, b0, b1, b2)
         return out
 
     @staticmethod
     def backward(ctx, gout):
-        x, Wcat, Wcs, Gs, c, bcs = ctx.saved_tensors
+        x, Wcat, Wcs, Gs, c, bcs, W0, W1, W2, b0, b1, b2 = ctx.saved_tensors
         gout = _c(gout)
         D = x.shape[-1]
         rows = _rows(x)
@@ -438,15 +633,27 @@ class TGateFn(torch.autograd.Function):
         dWcs, dbcs = _gbuf(Wcs, ctx.dWcs), _gbuf(bcs, ctx.dbcs)
         lib.call("asrx_small_linear_bwd", _P(dc), None, _P(x), _P(Wcs), _P(dx), _P(dWcs), _P(dbcs), rows, D, 3, 0,
                  1.0, _S())
-        dWcat = G.linear_wgrad(dGz, x)
-        dbcat = colsum(dGz)
-        return dx.view(x.shape), dWcat, dbcat, _gret(Wcs, dWcs, ctx.dWcs), _gret(bcs, dbcs, ctx.dbcs)
+        dWcat = _E(3 * D, D, device=x.device)
+        lib.call("asrx_zero", _P(dWcat), dWcat.numel() * 4, _S())
+        G.linear_wgrad(dGz, x, out=dWcat, accumulate=True)
+        Ws, bs = (W0, W1, W2), (b0, b1, b2)
+        if ctx.dparts:
+            gw = [_gbuf(w, True) for w in Ws]
+            lib.call("asrx_add_segments", _P(dWcat), D * D, _P(gw[0]), _P(gw[1]), _P(gw[2]), 3, _S())
+            for k, bk in enumerate(bs):
+                lib.call("asrx_colsum_ld", _P(dGz[:, k * D:]), 3 * D, _P(_gbuf(bk, True)), rows, D, _S())
+            gW = [_gret(w, None, True) for w in Ws]
+            gB = [_gret(bk, None, True) for bk in bs]
+        else:  # not leaves (or DIRECT off): return the parts to autograd
+            gW = [dWcat[k * D:(k + 1) * D] for k in range(3)]
+            dbcat = colsum(dGz)
+            gB = [dbcat[k * D:(k + 1) * D] for k in range(3)]
+        return (dx.view(x.shape), *gW, *gB, _gret(Wcs, dWcs, ctx.dWcs), _gret(bcs, dbcs, ctx.dbcs))
 
 
 def tgate(mod, x):
-    Wcat = torch.cat([g[0].weight for g in mod.ga], 0)
-    bcat = torch.cat([g[0].bias for g in mod.ga], 0)
-    return TGateFn.apply(x, Wcat, bcat, mod.cs[0].weight, mod.cs[0].bias)
+    return TGateFn.apply(x, *[g[0].weight for g in mod.ga], *[g[0].bias for g in mod.ga], mod.cs[0].weight,
+                         mod.cs[0].bias)
 
 
 # =============================================================================== elementwise
@@ -592,14 +799,16 @@ class SegMean(torch.autograd.Function):
         x = _c(x)
         B, L, d = x.shape
         out = _E(B, d, device=x.device)
-        lib.call("asrx_seg_colsum", _P(x), _P(out), B, L, d, 1.0 / L, 0, _S())
+        part = _E(B * int(lib.load().asrx_mem_chunks(L)) * d, device=x.device)
+        lib.call("asrx_seg_colsum_det", _P(x), _P(part), _P(out), B, L, d, 1.0 / L, _S())  # no atomics
         ctx.shape = x.shape
         return out
 
     @staticmethod
     def backward(ctx, g):
         B, L, d = ctx.shape
-        u = _c(g) * (1.0 / L)
+        u = _E(B, d, device=g.device)
+        lib.call("asrx_lincomb", _P(_c(g)), None, None, 1.0 / L, 0.0, 0.0, _P(u), B * d, _S())
         dx = _E(B, L, d, device=g.device)
         lib.call("asrx_add_rows", None, None, _P(u), _P(dx), B, L, d, _S())
         return dx
@@ -613,13 +822,15 @@ class AddRows(torch.autograd.Function):
     """out[b, l] = x[b, l] + t[l]  (t: PE table or the learned position rows)."""
 
     @staticmethod
-    def forward(ctx, x, t):
-        x, t = _c(x), _c(t)
-        B, L, d = x.shape
+    def forward(ctx, x, t, L):
+        """t: the table; rows [0, L) are added (the reference's position[:T] slice)."""
+        x = _c(x)
+        B, Lx, d = x.shape
         out = _E(x.shape, device=x.device)
-        lib.call("asrx_add_rows", _P(x), _P(t), None, _P(out), B, L, d, _S())
-        ctx.tshape = t.shape
-        ctx.t_grad = t.requires_grad
+        lib.call("asrx_add_rows", _P(x), _P(t), None, _P(out), B, Lx, d, _S())
+        ctx.L, ctx.d = L, d
+        ctx.dt = _direct(ctx, 1, t)
+        ctx.save_for_backward(t if ctx.needs_input_grad[1] else None)
         return out
 
     @staticmethod
@@ -627,13 +838,20 @@ class AddRows(torch.autograd.Function):
         g = _c(g)
         dt = None
         if ctx.needs_input_grad[1]:
+            (t,) = ctx.saved_tensors
             B = g.shape[0]
-            dt = colsum(g.view(B, -1)).view(ctx.tshape)
-        return g, dt
+            gt = _gbuf(t, ctx.dt)
+            colsum(g.view(B, -1), out=gt.view(-1)[:ctx.L * ctx.d])
+            dt = _gret(t, gt, ctx.dt)
+        return g, dt, None
 
 
 def add_rows(x, t):
-    return AddRows.apply(x, t)
+    """x (B, L, d) + t[:L] (t: a (>= L, d) table, e.g. the learned position or the sinusoid PE)."""
+    L = x.shape[1]
+    if t.shape[0] != L and not t.is_contiguous():
+        t = t.contiguous()
+    return AddRows.apply(x, t, L)
 
 
 class LinComb(torch.autograd.Function):
@@ -883,7 +1101,8 @@ class BatchNormPS(torch.autograd.Function):
 def batch_norm_eval(x, w, b, rm, rv, eps):
     x = _c(x)
     B, T, C = x.shape
-    rstd = torch.rsqrt(rv + eps)
+    rstd = _E(rv.shape, device=x.device)
+    lib.call("asrx_rsqrt_eps", _P(_c(rv)), _P(rstd), rv.numel(), float(eps), _S())
     y = _E(x.shape, device=x.device)
     lib.call("asrx_bn_fwd", _P(x), _P(w), _P(b), _P(y), _P(_c(rm)), _P(rstd), B, T, C, float(eps), 0, _S())
     return y
@@ -891,48 +1110,82 @@ def batch_norm_eval(x, w, b, rm, rv, eps):
 
 class Conv3(torch.autograd.Function):
     """k3 / padding-1 Conv1d on channels-last (B, T, Cin) -> (B, T, Cout) via implicit-im2col GEMM.
-    W (Cout, Cin, 3) like nn.Conv1d."""
+    The weight is v (Cout, Cin, 3) like nn.Conv1d, weight-normed W = g v / |v| when g is given
+    (weight_norm(Conv1d), model.py:140): asrx_conv3_weight writes it straight into the GEMM's k-major
+    layout (bf16 in perf mode) and, for the input gradient, the flipped layout; the weight gradient
+    goes back through the weight norm into g.grad / v.grad (asrx_conv3_weight_bwd)."""
 
     @staticmethod
-    def forward(ctx, x, W, b):
+    def forward(ctx, x, g, v, b):
         x = _c(x)
         B, T, Ci = x.shape
-        Co = W.shape[0]
-        Wt = W.permute(0, 2, 1).reshape(Co, 3 * Ci).contiguous()
-        y = _E(B, T, Co, device=x.device)
-        if G.use_wide(3 * Ci):
-            G.gemm_wn(x, G.weight_bf16(Wt, cache=False), y, M=B * T, N=Co, K=3 * Ci, lda=Ci, ldc=Co, bias=b,
-                      conv=True, conv_F=T, conv_C=Ci)
+        Co = v.shape[0]
+        dev = x.device
+        nrm = _E(Co, device=dev) if g is not None else None
+        wide = G.use_wide(3 * Ci)
+        Wt = None if wide else _E(Co, 3 * Ci, device=dev)
+        Wtb = _E(Co, 3 * Ci, dtype=torch.int16, device=dev) if wide else None
+        lib.call("asrx_conv3_weight", _P(g), _P(_c(v)), Co, Ci, _P(Wt), _P(Wtb), None, None, _P(nrm), _S())
+        y = _E(B, T, Co, device=dev)
+        if wide:
+            G.gemm_wn(x, Wtb, y, M=B * T, N=Co, K=3 * Ci, lda=Ci, ldc=Co, bias=b, conv=True, conv_F=T, conv_C=Ci)
         else:
             G.gemm(x, Wt, y, M=B * T, N=Co, K=3 * Ci, lda=Ci, ldb=3 * Ci, ldc=Co, bias=b, conv_a=True, conv_F=T,
                    conv_C=Ci)
-        ctx.db = _direct(ctx, 2, b)
-        ctx.save_for_backward(x, W, b)
+        ctx.has_g = g is not None
+        ctx.dg = _direct(ctx, 1, g) if g is not None else False
+        ctx.dv, ctx.db = _direct(ctx, 2, v), _direct(ctx, 3, b)
+        ctx.save_for_backward(x, g, v, b, nrm)
         return y
 
     @staticmethod
-    def backward(ctx, g):
-        x, W, b = ctx.saved_tensors
-        g = _c(g)
+    def backward(ctx, gy):
+        x, g, v, b, nrm = ctx.saved_tensors
+        gy = _c(gy)
         B, T, Ci = x.shape
-        Co = W.shape[0]
+        Co = v.shape[0]
+        dev = x.device
+        v = _c(v)
         dx = None
         if ctx.needs_input_grad[0]:
-            Wf = W.flip(2).permute(1, 2, 0).reshape(Ci, 3 * Co).contiguous()
-            dx = _E(x.shape, device=x.device)
-            if G.use_wide(3 * Co):
-                G.gemm_wn(g, G.weight_bf16(Wf, cache=False), dx, M=B * T, N=Ci, K=3 * Co, lda=Co, ldc=Ci, conv=True,
-                          conv_F=T, conv_C=Co)
+            wide = G.use_wide(3 * Co)
+            Wf = None if wide else _E(Ci, 3 * Co, device=dev)
+            Wfb = _E(Ci, 3 * Co, dtype=torch.int16, device=dev) if wide else None
+            nr = _E(Co, device=dev) if g is not None else None
+            lib.call("asrx_conv3_weight", _P(g), _P(v), Co, Ci, None, None, _P(Wf), _P(Wfb), _P(nr), _S())
+            dx = _E(x.shape, device=dev)
+            if wide:
+                G.gemm_wn(gy, Wfb, dx, M=B * T, N=Ci, K=3 * Co, lda=Co, ldc=Ci, conv=True, conv_F=T, conv_C=Co)
             else:
-                G.gemm(g, Wf, dx, M=B * T, N=Ci, K=3 * Co, lda=Co, ldb=3 * Co, ldc=Ci, conv_a=True, conv_F=T,
+                G.gemm(gy, Wf, dx, M=B * T, N=Ci, K=3 * Co, lda=Co, ldb=3 * Co, ldc=Ci, conv_a=True, conv_F=T,
                        conv_C=Co)
-        dWt = torch.zeros(Co, 3 * Ci, device=x.device)
-        tiles = ((Co + 127) // 128) * ((3 * Ci + 127) // 128)
-        G.gemm(g, x, dWt, M=Co, N=3 * Ci, K=B * T, lda=Co, ldb=Ci, ldc=3 * Ci, a_kc=False, b_kc=False, conv_b=True,
-               conv_F=T, conv_C=Ci, beta=1.0, splitk=G._splitk_for(B * T, tiles))
-        dW = dWt.view(Co, 3, Ci).permute(0, 2, 1).contiguous()
-        db = _gret(b, colsum(g.view(-1, Co), out=_gbuf(b, True) if ctx.db else None), ctx.db)
-        return dx, dW, db
+        dgo = dvo = dbo = None
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            dWt = _E(Co, 3 * Ci, device=dev)
+            lib.call("asrx_zero", _P(dWt), dWt.numel() * 4, _S())
+            tiles = ((Co + 127) // 128) * ((3 * Ci + 127) // 128)
+            G.gemm(gy, x, dWt, M=Co, N=3 * Ci, K=B * T, lda=Co, ldb=Ci, ldc=3 * Ci, a_kc=False, b_kc=False,
+                   conv_b=True, conv_F=T, conv_C=Ci, beta=1.0, splitk=G._splitk_for(B * T, tiles))
+            gv = _gbuf(v, ctx.dv) if ctx.dv else torch.zeros(v.shape, device=dev)
+            gg = None
+            if ctx.has_g:
+                gg = _gbuf(g, ctx.dg) if ctx.dg else torch.zeros(g.shape, device=dev)
+            lib.call("asrx_conv3_weight_bwd", _P(dWt), _P(g), _P(v), _P(nrm), Co, Ci, _P(gg), _P(gv), _S())
+            dvo = _gret(v, gv, ctx.dv)
+            dgo = _gret(g, gg, ctx.dg) if ctx.has_g else None
+        if ctx.needs_input_grad[3]:
+            dbo = _gret(b, colsum(gy.view(-1, Co), out=_gbuf(b, True) if ctx.db else None), ctx.db)
+        return dx, dgo, dvo, dbo
+
+
+def conv3(x, conv):
+    """Conv1d(k=3, padding=1) module on channels-last x; weight_norm-parametrized modules read their
+    g (original0) and v (original1) directly, so torch's parametrization kernels never run."""
+    pz = getattr(conv, "parametrizations", None)
+    if pz is not None and "weight" in pz:
+        orig = pz.weight
+        return Conv3.apply(x, orig.original0, orig.original1, conv.bias)
+    return Conv3.apply(x, None, conv.weight, conv.bias)
 
 
 class Stem1(torch.autograd.Function):
@@ -980,7 +1233,9 @@ class Embedding(torch.autograd.Function):
 
 
 class CrossEntropy(torch.autograd.Function):
-    """F.cross_entropy(logits, labels, ignore_index=0), mean over non-ignored rows."""
+    """F.cross_entropy(logits, labels, ignore_index=0), mean over non-ignored rows (model.py:670):
+    one read of the logits (online log-sum-exp), the mean and the non-ignored count on the device;
+    the backward scale g / count is read on the device (no host sync, graph-capturable)."""
 
     @staticmethod
     def forward(ctx, logits, labels):
@@ -990,19 +1245,48 @@ class CrossEntropy(torch.autograd.Function):
         lab = _c(labels.reshape(-1))
         loss_r = _E(rows, device=z.device)
         lse = _E(rows, device=z.device)
-        lib.call("asrx_ce_fwd", _P(z), _P(lab), _P(loss_r), _P(lse), rows, V, _S())
-        count = (lab != 0).sum().clamp_min(1).to(torch.float32)
-        loss = loss_r.sum() / count
+        loss = _E((), device=z.device)
+        count = _E(1, device=z.device)
+        lib.call("asrx_ce_fwd1", _P(z), _P(lab), _P(loss_r), _P(lse), _P(loss), _P(count), rows, V, _S())
         ctx.save_for_backward(z, lab, lse, count)
         return loss
 
     @staticmethod
     def backward(ctx, g):
         z, lab, lse, count = ctx.saved_tensors
-        scale = (g / count).reshape(1).contiguous()
+        g = _c(g.reshape(1).to(torch.float32)) if g.dtype != torch.float32 or not g.is_contiguous() else g
         dz = _E(z.shape, device=z.device)
-        lib.call("asrx_ce_bwd", _P(z), _P(lab), _P(lse), _P(scale), _P(dz), _rows(z), z.shape[-1], _S())
+        lib.call("asrx_ce_bwd2", _P(z), _P(lab), _P(lse), _P(g), _P(count), _P(dz), _rows(z), z.shape[-1], _S())
         return dz, None
+
+
+class BlendFn(torch.autograd.Function):
+    """sigmoid(blend) d + (1 - sigmoid(blend)) g (processor output, model.py:628)."""
+
+    @staticmethod
+    def forward(ctx, d, g, blend):
+        d, g = _c(d), _c(g)
+        out = _E(d.shape, device=d.device)
+        lib.call("asrx_blend_fwd", _P(d), _P(g), _P(blend), _P(out), d.numel(), _S())
+        ctx.db = _direct(ctx, 2, blend)
+        ctx.save_for_backward(d, g, blend)
+        return out
+
+    @staticmethod
+    def backward(ctx, go):
+        d, g, blend = ctx.saved_tensors
+        go = _c(go)
+        dd = _E(d.shape, device=d.device) if ctx.needs_input_grad[0] else None
+        dg = _E(g.shape, device=g.device) if ctx.needs_input_grad[1] else None
+        dbl = None
+        if ctx.needs_input_grad[2]:
+            dbl = _gbuf(blend, ctx.db)
+        lib.call("asrx_blend_bwd", _P(go), _P(d), _P(g), _P(blend), _P(dd), _P(dg), _P(dbl), d.numel(), _S())
+        return dd, dg, (_gret(blend, dbl, ctx.db) if dbl is not None else None)
+
+
+def blend(d, g, b):
+    return BlendFn.apply(d, g, b)
 
 
 def policy_noise(B, layers, sid_base, key, device):

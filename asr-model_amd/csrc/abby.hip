@@ -29,6 +29,7 @@ struct AbbyGeom {
   int64_t sid_base;
   uint32_t key;
   int use_noise;
+  int acc;  // backward: dx += (one buffer collects every consumer's gradient of x)
 };
 
 // Per-row layout (MI355X design): lane l owns the E = d/64 CONSECUTIVE features [l E, l E + E), read
@@ -414,6 +415,12 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_bwd_kernel(
       accW[1][e] += dz1 * hs;
       accW[2][e] += dz2 * hs;
     }
+    if (g.acc) {
+      float old[E];
+      ld_row<E>(dx + r * S::D, lane, old);
+#pragma unroll
+      for (int e = 0; e < E; ++e) dxv[e] += old[e];
+    }
     st_row<E>(dx + r * S::D, lane, dxv);
     st_row<E>(dhpre + r * S::D, lane, dh);
     accb[0] += dz0;
@@ -681,6 +688,13 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_bwd64_kernel(
       accW[1][e] += dz1 * hs;
       accW[2][e] += dz2 * hs;
     }
+    if (g.acc) {
+      const float4 o = *reinterpret_cast<const float4*>(dx + r * 64 + 4 * l16);
+      dxv[0] += o.x;
+      dxv[1] += o.y;
+      dxv[2] += o.z;
+      dxv[3] += o.w;
+    }
     st64(dx + r * 64 + 4 * l16, dxv);
     st64(dhpre + r * 64 + 4 * l16, dh);
     accb[0] += dz0;
@@ -732,6 +746,7 @@ static AbbyGeom make_geom(int64_t rows, int64_t d, int64_t L, int64_t H, int64_t
   g.sid_base = sid_base;
   g.key = key;
   g.use_noise = use_noise;
+  g.acc = 0;
   return g;
 }
 
@@ -773,23 +788,31 @@ extern "C" int asrx_abby_fwd_logits(const float* x, const float* logits, const f
   ASRX_LAUNCHED("asrx_abby_fwd_logits");
 }
 
-// dW2 / db2 are accumulated (caller zeroes them).  dx, dhpre are overwritten.
-extern "C" int asrx_abby_bwd(const float* dout, const float* x, const float* hpre, const float* W2,
-                             const float* ys, const int* idx, float* dx, float* dhpre, float* dW2, float* db2,
-                             int64_t rows, int64_t d, hipStream_t stream) {
+// dW2 / db2 are accumulated (caller zeroes them).  dx (acc == 0) and dhpre are overwritten; acc != 0
+// adds x's gradient into dx.
+extern "C" int asrx_abby_bwd2(const float* dout, const float* x, const float* hpre, const float* W2,
+                              const float* ys, const int* idx, float* dx, float* dhpre, float* dW2, float* db2,
+                              int64_t rows, int64_t d, int acc, hipStream_t stream) {
   ASRX_REQUIRE(d % 64 == 0 && d >= 64 && d <= 1024, "AbbyNormal: d=%ld must be a multiple of 64 in [64,1024]",
                (long)d);
   if (rows == 0) return 0;
   const int E = (int)(d / 64);
   AbbyGeom g = make_geom(rows, d, 1, 1, 0, 0, 0);
+  g.acc = acc;
   const unsigned grid = (unsigned)std::min<int64_t>((rows + ABBY_WAVES - 1) / ABBY_WAVES, 1024);
   if (d == 64) {
     const unsigned g64 = (unsigned)std::min<int64_t>((rows + 4 * ABBY_WAVES - 1) / (4 * ABBY_WAVES), 1024);
     abby_bwd64_kernel<<<g64, 64 * ABBY_WAVES, 0, stream>>>(dout, x, hpre, W2, ys, idx, dx, dhpre, dW2, db2, g);
-    ASRX_LAUNCHED("asrx_abby_bwd");
+    ASRX_LAUNCHED("asrx_abby_bwd2");
   }
   ABBY_DISPATCH(abby_bwd_kernel, dout, x, hpre, W2, ys, idx, dx, dhpre, dW2, db2, g);
-  ASRX_LAUNCHED("asrx_abby_bwd");
+  ASRX_LAUNCHED("asrx_abby_bwd2");
+}
+
+extern "C" int asrx_abby_bwd(const float* dout, const float* x, const float* hpre, const float* W2,
+                             const float* ys, const int* idx, float* dx, float* dhpre, float* dW2, float* db2,
+                             int64_t rows, int64_t d, hipStream_t stream) {
+  return asrx_abby_bwd2(dout, x, hpre, W2, ys, idx, dx, dhpre, dW2, db2, rows, d, 0, stream);
 }
 
 ASRX_NOISE_EPOCH_SETTER(asrx_set_noise_epoch_abby)

@@ -29,9 +29,19 @@ __global__ __launch_bounds__(256) void msheath_ctrl_fwd_kernel(
     const float* __restrict__ jump_s, const float* __restrict__ next_i, int layer_i, int layers, int64_t L, int D,
     float* __restrict__ alpha, float* __restrict__ beta, float* __restrict__ gam, float* __restrict__ mem_w_out,
     float* __restrict__ active, float* __restrict__ next_out, CtrlRec* __restrict__ rec, int64_t ld_mem_w,
-    const float* __restrict__ mg_w, const float* __restrict__ mg_b, float* __restrict__ mem_v_out) {
+    const float* __restrict__ mg_w, const float* __restrict__ mg_b, float* __restrict__ mem_v_out,
+    const float* __restrict__ mem_part, int nchunk, float* __restrict__ mem_out) {
   __shared__ float red[4];
   const int64_t b = blockIdx.x;
+  if (mem_part) {  // mem = (1/L) sum over the row chunks of x_new, in chunk order (deterministic)
+    for (int c = threadIdx.x; c < D; c += 256) {
+      float t = 0.f;
+      for (int k = 0; k < nchunk; ++k) t += mem_part[((int64_t)b * nchunk + k) * D + c];
+      mem_out[b * D + c] = t * (1.0f / (float)L);
+    }
+    __syncthreads();
+    mem = mem_out;
+  }
   float s = 0.f;
   for (int64_t l = threadIdx.x; l < L; l += 256) s += ion[b * L + l];
   const float potential = block_sum<256>(s, red) / (float)L;  // ion.mean(dim=1), model.py:466
@@ -176,18 +186,21 @@ __global__ void axpy_row2_kernel(const float4* __restrict__ x, const float* __re
   }
 }
 
-// x_new = x + s1 s2 y (model.py:461) and mem += invL sum_l x_new (model.py:463, accumulated into a
-// zeroed mem) in one pass.  grid (B, ceil(L / lch)); the 256 threads are nrl = 256 / d4 row lanes x d4
-// float4 columns (d4 <= 256), so each thread keeps its column's partial sum in registers.
+// x_new = x + s1 s2 y (model.py:461) and the per-sample column sums for mem = mean_l x_new (463) in
+// one pass.  grid (B, ceil(L / 64)); the 256 threads are nrl = 256 / d4 row lanes x d4 float4 columns
+// (d4 <= 256), each keeping its column's partial sum in registers; the workgroup's sums go to
+// part[b][chunk][:] (no atomics: the control kernel adds the chunks in a fixed order, so the forward
+// is deterministic -- its hard decisions must not depend on atomic ordering).
+constexpr int MEM_CHUNK = 64;
 __global__ __launch_bounds__(256) void axpy_row2_colsum_kernel(const float4* __restrict__ x, const float* __restrict__ s1,
                                                                const float* __restrict__ s2, const float4* __restrict__ y,
-                                                               float4* __restrict__ out, float* __restrict__ mem,
-                                                               int64_t L, int d4, float invL, int lch) {
+                                                               float4* __restrict__ out, float4* __restrict__ part,
+                                                               int64_t L, int d4) {
   __shared__ float4 red[256];
   const int nrl = 256 / d4;
   const int c = threadIdx.x % d4, rl = threadIdx.x / d4;
   const int64_t b = blockIdx.x;
-  const int64_t l0 = (int64_t)blockIdx.y * lch, l1 = min<int64_t>(L, l0 + lch);
+  const int64_t l0 = (int64_t)blockIdx.y * MEM_CHUNK, l1 = min<int64_t>(L, l0 + MEM_CHUNK);
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   if (rl < nrl) {
     for (int64_t l = l0 + rl; l < l1; l += nrl) {
@@ -207,11 +220,7 @@ __global__ __launch_bounds__(256) void axpy_row2_colsum_kernel(const float4* __r
       const float4 t = red[k * d4 + c];
       acc.x += t.x; acc.y += t.y; acc.z += t.z; acc.w += t.w;
     }
-    float* m = mem + b * (int64_t)d4 * 4 + 4 * c;
-    atomicAdd(m + 0, acc.x * invL);
-    atomicAdd(m + 1, acc.y * invL);
-    atomicAdd(m + 2, acc.z * invL);
-    atomicAdd(m + 3, acc.w * invL);
+    part[((int64_t)b * gridDim.y + blockIdx.y) * d4 + c] = acc;
   }
 }
 
@@ -529,7 +538,7 @@ int asrx_msheath_ctrl_fwd(const float* policy, const float* gpol, int64_t ld_gpo
   msheath_ctrl_fwd_kernel<<<(unsigned)B, 256, 0, stream>>>(policy, gpol, ld_gpol, ion, mem_v, mem_w, mem, jump_s,
                                                            next_i, (int)layer_i, (int)layers, L, (int)D, alpha, beta,
                                                            gam, mem_w_out, active, next_out, (CtrlRec*)rec, D, nullptr,
-                                                           nullptr, nullptr);
+                                                           nullptr, nullptr, nullptr, 0, nullptr);
   ASRX_LAUNCHED("asrx_msheath_ctrl_fwd");
 }
 
@@ -544,23 +553,25 @@ int asrx_msheath_ctrl_fwd2(const float* policy, const float* gpol, int64_t ld_gp
   msheath_ctrl_fwd_kernel<<<(unsigned)B, 256, 0, stream>>>(policy, gpol, ld_gpol, ion, mem_v, mem_w, mem, jump_s,
                                                            next_i, (int)layer_i, (int)layers, L, (int)D, alpha, beta,
                                                            gam, mem_w_out, active, next_out, (CtrlRec*)rec, ld_mem_w,
-                                                           nullptr, nullptr, nullptr);
+                                                           nullptr, nullptr, nullptr, nullptr, 0, nullptr);
   ASRX_LAUNCHED("asrx_msheath_ctrl_fwd2");
 }
 
-// As asrx_msheath_ctrl_fwd2 with mem_v = sigmoid(mem . mg_w + mg_b) computed in the kernel (written
-// to mem_v_out for the backward) instead of read.
+// As asrx_msheath_ctrl_fwd2 with mem = (1/L) sum of the asrx_axpy_row2_colsum chunk partials
+// (written to mem) and mem_v = sigmoid(mem . mg_w + mg_b) computed in the kernel (written to
+// mem_v_out for the backward).
 int asrx_msheath_ctrl_fwd3(const float* policy, const float* gpol, int64_t ld_gpol, const float* ion,
                            const float* mg_w, const float* mg_b, float* mem_v_out, const float* mem_w,
-                           int64_t ld_mem_w, const float* mem, const float* jump_s, const float* next_i,
-                           int64_t layer_i, int64_t layers, int64_t B, int64_t L, int64_t D, float* alpha, float* beta,
-                           float* gam, float* mem_w_out, float* active, float* next_out, void* rec,
-                           hipStream_t stream) {
+                           int64_t ld_mem_w, const float* mem_part, float* mem, const float* jump_s,
+                           const float* next_i, int64_t layer_i, int64_t layers, int64_t B, int64_t L, int64_t D,
+                           float* alpha, float* beta, float* gam, float* mem_w_out, float* active, float* next_out,
+                           void* rec, hipStream_t stream) {
   if (B == 0) return 0;
+  const int nchunk = (int)((L + MEM_CHUNK - 1) / MEM_CHUNK);
   msheath_ctrl_fwd_kernel<<<(unsigned)B, 256, 0, stream>>>(policy, gpol, ld_gpol, ion, nullptr, mem_w, mem, jump_s,
                                                            next_i, (int)layer_i, (int)layers, L, (int)D, alpha, beta,
                                                            gam, mem_w_out, active, next_out, (CtrlRec*)rec, ld_mem_w,
-                                                           mg_w, mg_b, mem_v_out);
+                                                           mg_w, mg_b, mem_v_out, mem_part, nchunk, mem);
   ASRX_LAUNCHED("asrx_msheath_ctrl_fwd3");
 }
 
@@ -606,17 +617,17 @@ int asrx_msheath_ctrl_bwd3(const float* g_alpha, const float* g_beta, const floa
   ASRX_LAUNCHED("asrx_msheath_ctrl_bwd3");
 }
 
-int asrx_axpy_row2_colsum(const float* x, const float* s1, const float* s2, const float* y, float* out, float* mem,
+int64_t asrx_mem_chunks(int64_t L) { return (L + MEM_CHUNK - 1) / MEM_CHUNK; }
+
+int asrx_axpy_row2_colsum(const float* x, const float* s1, const float* s2, const float* y, float* out, float* part,
                           int64_t B, int64_t L, int64_t d, hipStream_t stream) {
   ASRX_REQUIRE(d % 4 == 0 && d <= 1024, "asrx_axpy_row2_colsum: d %% 4 == 0 and d <= 1024 required");
   ASRX_REQUIRE(s2 != nullptr, "asrx_axpy_row2_colsum: s2 required");
   if (B * L == 0) return 0;
   const int d4 = (int)(d / 4);
-  const int nrl = 256 / d4;
-  const int lch = std::max(nrl * 16, 32);
-  dim3 grid((unsigned)B, (unsigned)((L + lch - 1) / lch));
-  axpy_row2_colsum_kernel<<<grid, 256, 0, stream>>>((const float4*)x, s1, s2, (const float4*)y, (float4*)out, mem, L,
-                                                    d4, 1.0f / (float)L, lch);
+  dim3 grid((unsigned)B, (unsigned)asrx_mem_chunks(L));
+  axpy_row2_colsum_kernel<<<grid, 256, 0, stream>>>((const float4*)x, s1, s2, (const float4*)y, (float4*)out,
+                                                    (float4*)part, L, d4);
   ASRX_LAUNCHED("asrx_axpy_row2_colsum");
 }
 

@@ -330,12 +330,13 @@ __global__ __launch_bounds__(64 * RW) void rownorm_kernel(const float* __restric
 
 // dx[r] += dn[r] * x[r] / n[r]
 __global__ void rownorm_bwd_kernel(const float* __restrict__ dn, const float* __restrict__ x,
-                                   const float* __restrict__ n, float* __restrict__ dx, int64_t rows, int d) {
+                                   const float* __restrict__ n, float* __restrict__ dx, int64_t rows, int d, int acc) {
   const int64_t total = rows * d;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = i / d;
     const float nn = n[r];
-    if (nn > 0.f) dx[i] += dn[r] * x[i] / nn;
+    const float v = nn > 0.f ? dn[r] * x[i] / nn : 0.f;
+    dx[i] = acc ? dx[i] + v : v;
   }
 }
 
@@ -388,7 +389,7 @@ __global__ __launch_bounds__(64 * RW) void rotary_bwd_kernel(const float* __rest
       acc += gg.x * (v.x * cs - v.y * sn) + gg.y * (v.x * sn + v.y * cs);
     }
     acc = wave_sum(acc) * scale;
-    if (lane == 0) dm[r] += acc;
+    if (lane == 0) dm[r] = acc;  // written (one wave owns a row): no zero-filled dm needed
   }
 }
 
@@ -902,9 +903,39 @@ __global__ __launch_bounds__(256) void seg_colsum_kernel(const float* __restrict
   }
 }
 
+// Deterministic form (forward values feeding hard decisions, model.py:432 MPNet pooling): chunk sums
+// to part[b][chunk][:] with no atomics, then seg_reduce adds the chunks in order.
+__global__ __launch_bounds__(256) void seg_partial_kernel(const float* __restrict__ x, float* __restrict__ part,
+                                                          int64_t L, int d, int64_t chunk) {
+  __shared__ float red[4][64];
+  const int b = blockIdx.y;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int p4 = threadIdx.x >> 6;
+  const int64_t l0 = (int64_t)blockIdx.z * chunk, l1 = min(L, l0 + chunk);
+  float s = 0.f;
+  if (c < d)
+    for (int64_t l = l0 + p4; l < l1; l += 4) s += x[((int64_t)b * L + l) * d + c];
+  red[p4][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (p4 == 0 && c < d) {
+    const int t = threadIdx.x;
+    part[((int64_t)b * gridDim.z + blockIdx.z) * d + c] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+  }
+}
+
+__global__ void seg_reduce_kernel(const float* __restrict__ part, float* __restrict__ out, int B, int nchunk, int d,
+                                  float scale) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)B * d) return;
+  const int64_t b = i / d, c = i % d;
+  float t = 0.f;
+  for (int k = 0; k < nchunk; ++k) t += part[(b * nchunk + k) * d + c];
+  out[i] = t * scale;
+}
+
 // Column sums over many rows (bias gradients): out[c] += sum_r x[r, c].  grid (ceil(d/64), chunks).
 __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ x, float* __restrict__ out,
-                                                     int64_t rows, int d, int64_t chunk) {
+                                                     int64_t rows, int d, int64_t chunk, int64_t ld) {
   __shared__ float red[4][64];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int part = threadIdx.x >> 6;
@@ -915,10 +946,10 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ x
     int64_t r = r0 + part;
 #pragma unroll 4
     for (; r + 4 < r1; r += 8) {
-      s += x[r * d + c];
-      s2 += x[(r + 4) * d + c];
+      s += x[r * ld + c];
+      s2 += x[(r + 4) * ld + c];
     }
-    if (r < r1) s += x[r * d + c];
+    if (r < r1) s += x[r * ld + c];
   }
   s += s2;
   red[part][threadIdx.x & 63] = s;
@@ -1844,8 +1875,16 @@ int asrx_rownorm(const float* x, float* n, int64_t rows, int64_t d, hipStream_t 
 int asrx_rownorm_bwd(const float* dn, const float* x, const float* n, float* dx, int64_t rows, int64_t d,
                      hipStream_t stream) {
   if (rows == 0) return 0;
-  LAUNCH_EW(rownorm_bwd_kernel, rows * d, dn, x, n, dx, rows, (int)d);
+  LAUNCH_EW(rownorm_bwd_kernel, rows * d, dn, x, n, dx, rows, (int)d, 1);
   ASRX_LAUNCHED("asrx_rownorm_bwd");
+}
+
+// acc == 0: dx = the |x| gradient (written, not accumulated)
+int asrx_rownorm_bwd2(const float* dn, const float* x, const float* n, float* dx, int64_t rows, int64_t d, int acc,
+                      hipStream_t stream) {
+  if (rows == 0) return 0;
+  LAUNCH_EW(rownorm_bwd_kernel, rows * d, dn, x, n, dx, rows, (int)d, acc);
+  ASRX_LAUNCHED("asrx_rownorm_bwd2");
 }
 
 int asrx_rotary_fwd(const float* x, const float* m, const float* f, float* y, int64_t BL, int64_t L, int64_t D,
@@ -2006,14 +2045,36 @@ int asrx_seg_colsum(const float* x, float* out, int64_t B, int64_t L, int64_t d,
   ASRX_LAUNCHED("asrx_seg_colsum");
 }
 
+// out (B, d) = scale * sum_l x[b, l, :], deterministic; part: B * ceil(L / 64) * d floats of workspace.
+int asrx_seg_colsum_det(const float* x, float* part, float* out, int64_t B, int64_t L, int64_t d, float scale,
+                        hipStream_t stream) {
+  if (B == 0) return 0;
+  const int64_t chunk = 64, nchunk = (L + chunk - 1) / chunk;
+  dim3 grid((unsigned)((d + 63) / 64), (unsigned)B, (unsigned)nchunk);
+  seg_partial_kernel<<<grid, 256, 0, stream>>>(x, part, L, (int)d, chunk);
+  seg_reduce_kernel<<<(unsigned)((B * d + 255) / 256), 256, 0, stream>>>(part, out, (int)B, (int)nchunk, (int)d, scale);
+  ASRX_LAUNCHED("asrx_seg_colsum_det");
+}
+
 int asrx_colsum(const float* x, float* out, int64_t rows, int64_t d, hipStream_t stream) {
   if (rows == 0) return 0;
   int64_t chunks = std::min<int64_t>(std::max<int64_t>(rows / 512, 1), 1024);
   const int64_t chunk = (rows + chunks - 1) / chunks;
   chunks = (rows + chunk - 1) / chunk;
   dim3 grid((unsigned)((d + 63) / 64), (unsigned)chunks);
-  colsum_kernel<<<grid, 256, 0, stream>>>(x, out, rows, (int)d, chunk);
+  colsum_kernel<<<grid, 256, 0, stream>>>(x, out, rows, (int)d, chunk, d);
   ASRX_LAUNCHED("asrx_colsum");
+}
+
+// out[c] += sum_r x[r * ld + c]: the bias gradient of a column block of a wider GEMM output
+int asrx_colsum_ld(const float* x, int64_t ld, float* out, int64_t rows, int64_t d, hipStream_t stream) {
+  if (rows == 0) return 0;
+  int64_t chunks = std::min<int64_t>(std::max<int64_t>(rows / 512, 1), 1024);
+  const int64_t chunk = (rows + chunks - 1) / chunks;
+  chunks = (rows + chunk - 1) / chunk;
+  dim3 grid((unsigned)((d + 63) / 64), (unsigned)chunks);
+  colsum_kernel<<<grid, 256, 0, stream>>>(x, out, rows, (int)d, chunk, ld);
+  ASRX_LAUNCHED("asrx_colsum_ld");
 }
 
 int asrx_add_rows(const float* x, const float* t, const float* u, float* out, int64_t B, int64_t L, int64_t d,

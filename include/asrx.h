@@ -99,6 +99,10 @@ int asrx_abby_fwd_logits(const float* x, const float* logits, const float* b2, f
 int asrx_abby_bwd(const float* dout, const float* x, const float* hpre, const float* W2, const float* ys,
                   const int* idx, float* dx, float* dhpre, float* dW2, float* db2, int64_t rows, int64_t d,
                   asrx_stream_t stream);
+/* as asrx_abby_bwd; acc != 0 adds x's gradient into dx instead of writing it */
+int asrx_abby_bwd2(const float* dout, const float* x, const float* hpre, const float* W2, const float* ys,
+                   const int* idx, float* dx, float* dhpre, float* dW2, float* db2, int64_t rows, int64_t d, int acc,
+                   asrx_stream_t stream);
 
 /* ---- attention: F.scaled_dot_product_attention(q,k,v,is_causal) at model.py:307, head dim hd = 64
  *      (tiny/small/medium) or 128 (the reference's Dimensions(dims=512, head=4), model.py:746).
@@ -145,6 +149,9 @@ int asrx_small_linear_bwd(const float* dy, const float* y, const float* x, const
 int asrx_rownorm(const float* x, float* n, int64_t rows, int64_t d, asrx_stream_t stream);
 int asrx_rownorm_bwd(const float* dn, const float* x, const float* n, float* dx, int64_t rows, int64_t d,
                      asrx_stream_t stream);
+/* acc == 0: dx = the |x| gradient (written); acc != 0: accumulated like asrx_rownorm_bwd. */
+int asrx_rownorm_bwd2(const float* dn, const float* x, const float* n, float* dx, int64_t rows, int64_t d, int acc,
+                      asrx_stream_t stream);
 /* F.normalize(x, p=2, dim=-1) (v_gate's keys, model.py:347): y, n = max(|x|, 1e-12); backward
  * dx (+)= (dy - y (y.dy)) / n. */
 int asrx_row_normalize(const float* x, float* y, float* n, int64_t rows, int64_t d, asrx_stream_t stream);
@@ -240,21 +247,24 @@ int asrx_msheath_ctrl_bwd2(const float* g_alpha, const float* g_beta, const floa
                            const float* jump_s, const void* rec, int64_t layer_i, int64_t layers, int64_t B, int64_t D,
                            float* g_policy, int acc_policy, float* g_mem_v, float* g_mem_w, float* g_mem,
                            float* g_jump_s, int* has_orig, asrx_stream_t stream);
-/* ctrl with mem_v = sigmoid(mem . mg_w + mg_b) computed in the kernel (mem_gate, model.py:464; written
- * to mem_v_out) and, backward, its gradient fused (g_mem += ..., g_mg_w / g_mg_b accumulated). */
+/* ctrl with mem = (1/L) sum of the asrx_axpy_row2_colsum chunk partials mem_part (written to mem) and
+ * mem_v = sigmoid(mem . mg_w + mg_b) computed in the kernel (mem_gate, model.py:464; written to
+ * mem_v_out); backward with mem_v's gradient fused (g_mem += ..., g_mg_w / g_mg_b accumulated). */
 int asrx_msheath_ctrl_fwd3(const float* policy, const float* gpol, int64_t ld_gpol, const float* ion,
                            const float* mg_w, const float* mg_b, float* mem_v_out, const float* mem_w,
-                           int64_t ld_mem_w, const float* mem, const float* jump_s, const float* next_i,
-                           int64_t layer_i, int64_t layers, int64_t B, int64_t L, int64_t D, float* alpha, float* beta,
-                           float* gam, float* mem_w_out, float* active, float* next_out, void* rec,
-                           asrx_stream_t stream);
+                           int64_t ld_mem_w, const float* mem_part, float* mem, const float* jump_s,
+                           const float* next_i, int64_t layer_i, int64_t layers, int64_t B, int64_t L, int64_t D,
+                           float* alpha, float* beta, float* gam, float* mem_w_out, float* active, float* next_out,
+                           void* rec, asrx_stream_t stream);
 int asrx_msheath_ctrl_bwd3(const float* g_alpha, const float* g_beta, const float* g_gam, const float* g_mwo,
                            const float* mem_v, const float* mem_w, int64_t ld_mem_w, const float* mem,
                            const float* jump_s, const void* rec, int64_t layer_i, int64_t layers, int64_t B, int64_t D,
                            float* g_policy, int acc_policy, float* g_mem_w, float* g_mem, float* g_jump_s,
                            int* has_orig, const float* mg_w, float* g_mg_w, float* g_mg_b, asrx_stream_t stream);
-/* x_new = x + s1 s2 y and mem += (1/L) sum_l x_new per sample (mem zeroed by the caller), d <= 1024. */
-int asrx_axpy_row2_colsum(const float* x, const float* s1, const float* s2, const float* y, float* out, float* mem,
+/* x_new = x + s1 s2 y and per-sample column sums of x_new in row chunks of 64: part (B,
+ * asrx_mem_chunks(L), d), no atomics (deterministic forward), d <= 1024. */
+int64_t asrx_mem_chunks(int64_t L);
+int asrx_axpy_row2_colsum(const float* x, const float* s1, const float* s2, const float* y, float* out, float* part,
                           int64_t B, int64_t L, int64_t d, asrx_stream_t stream);
 /* MSheath fused backward (asrx/msheath.py): jump_select backward in accumulate form (active: dxn =
  * alpha g, orig's gradient (+)= beta g on a jump; inactive: dx = g), the x_new/mem backward writing
@@ -284,6 +294,11 @@ int asrx_jump_select4_bwd(const float* g, const float* xn, const float* orig, co
 int asrx_seg_colsum(const float* x, float* out, int64_t B, int64_t L, int64_t d, float scale, int accumulate,
                     asrx_stream_t stream);
 int asrx_colsum(const float* x, float* out, int64_t rows, int64_t d, asrx_stream_t stream);
+/* out (B, d) = scale sum_l x[b, l, :] without atomics (deterministic); part: B ceil(L/64) d floats */
+int asrx_seg_colsum_det(const float* x, float* part, float* out, int64_t B, int64_t L, int64_t d, float scale,
+                        asrx_stream_t stream);
+/* out[c] += sum_r x[r * ld + c] (a column block of a wider row-major tensor) */
+int asrx_colsum_ld(const float* x, int64_t ld, float* out, int64_t rows, int64_t d, asrx_stream_t stream);
 int asrx_add_rows(const float* x, const float* t, const float* u, float* out, int64_t B, int64_t L, int64_t d,
                   asrx_stream_t stream);
 int asrx_lincomb(const float* x, const float* y, const float* z, float a, float b, float c, float* out, int64_t n,
@@ -339,6 +354,36 @@ int asrx_ce_bwd(const float* z, const int64_t* labels, const float* lse, const f
 int asrx_maxfactor_param_bytes(void);
 int asrx_maxfactor_step(const void* table, int np, int64_t nrows, int64_t ncols, int64_t ncc, int64_t nmats,
                         int64_t nitems, float* ws, asrx_stream_t stream);
+
+
+/* ---- step glue (csrc/stepops.hip): ops that ran as stock ATen kernels on the hot path ------------
+ * Cross entropy (model.py:670, ignore_index 0): one-pass online log-sum-exp per row + on-device mean
+ * (loss, count are device scalars); backward dz = (g/count)(softmax - onehot) with g the device
+ * gradient of the loss, dz may alias z. */
+int asrx_ce_fwd1(const float* z, const int64_t* labels, float* loss_r, float* lse, float* loss, float* count,
+                 int64_t rows, int64_t V, asrx_stream_t stream);
+int asrx_ce_bwd2(const float* z, const int64_t* labels, const float* lse, const float* g, const float* count, float* dz,
+                 int64_t rows, int64_t V, asrx_stream_t stream);
+/* BatchNorm1d running statistics from per-clip (B, C) mean / rstd (ConvLite.bn, model.py:101);
+ * nbt (num_batches_tracked, int64) may be NULL.  asrx_rsqrt_eps: eval-mode rstd. */
+int asrx_bn_running(const float* mean, const float* rstd, float* rm, float* rv, int64_t* nbt, int64_t B, int64_t C,
+                    int64_t T, float eps, float momentum, asrx_stream_t stream);
+int asrx_rsqrt_eps(const float* v, float* out, int64_t n, float eps, asrx_stream_t stream);
+/* k3 Conv1d weight (Co, Ci, 3), weight-normed when g != NULL (W = g v/|v|, model.py:140), into the
+ * implicit-im2col GEMM layouts: Wt (Co, 3Ci) k-major and Wf (Ci, 3Co) flipped, fp32 and/or bf16 (each
+ * may be NULL); nrm (Co) = |v| per channel.  Backward from dWt (Co, 3Ci): dg, dv accumulated. */
+int asrx_conv3_weight(const float* g, const float* v, int64_t Co, int64_t Ci, float* Wt, unsigned short* Wtb, float* Wf,
+                      unsigned short* Wfb, float* nrm, asrx_stream_t stream);
+int asrx_conv3_weight_bwd(const float* dWt, const float* g, const float* v, const float* nrm, int64_t Co, int64_t Ci,
+                          float* dg, float* dv, asrx_stream_t stream);
+/* processor output blend (model.py:628): out = s d + (1-s) g, s = sigmoid(blend); backward writes dd,
+ * dg (each may be NULL) and accumulates d blend. */
+int asrx_blend_fwd(const float* d, const float* g, const float* blend, float* out, int64_t n, asrx_stream_t stream);
+int asrx_blend_bwd(const float* go, const float* d, const float* g, const float* blend, float* dd, float* dg,
+                   float* dblend, int64_t n, asrx_stream_t stream);
+/* dst_k += src[k n .. (k+1) n) for k < nseg <= 3; asrx_cat3: out = [a; b; c] (c may be NULL). */
+int asrx_add_segments(const float* src, int64_t n, float* d0, float* d1, float* d2, int64_t nseg, asrx_stream_t stream);
+int asrx_cat3(const float* a, const float* b, const float* c, int64_t n, float* out, asrx_stream_t stream);
 
 #ifdef __cplusplus
 }

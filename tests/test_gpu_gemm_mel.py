@@ -178,7 +178,7 @@ def test_wide_conv3_bf16(cuda):
     W = torch.randn(O, C, 3, generator=g) / (3 * C) ** 0.5
     bias = torch.randn(O, generator=g)
     with prec.precision("bf16"):
-        y = ops.Conv3.apply(x.transpose(1, 2).contiguous().to(cuda), W.to(cuda), bias.to(cuda)).cpu()
+        y = ops.Conv3.apply(x.transpose(1, 2).contiguous().to(cuda), None, W.to(cuda), bias.to(cuda)).cpu()
     ref = torch.nn.functional.conv1d(x.double(), W.double(), bias.double(), padding=1).transpose(1, 2)
     assert float((y.double() - ref).abs().max() / ref.abs().max()) < 2e-2
 

@@ -107,3 +107,28 @@ def test_skip_dead_blocks_is_output_identical(cuda):
         assert set(res[0][1]) == set(other[1])
         # gradients: equal up to the float-atomic accumulation order of split-K / column-sum kernels
         assert all(_rel(other[1][n], res[0][1][n]) < 1e-5 for n in res[0][1])
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_forward_is_deterministic(cuda, precision):
+    """The forward has no atomics (MSheath's pooled / mem means reduce fixed row chunks in order), so
+    two runs of the same step give bit-identical logits: the model's hard decisions (gumbel argmax,
+    v_gate thresholds, MSheath jumps) must not depend on float atomic ordering, or parity at the
+    benchmarked dims would change from run to run."""
+    from asrx import prec
+    from asrx.config import Dimensions
+    from asrx.model import Model
+
+    torch.manual_seed(0)
+    cfg = Dimensions(tokens=1000, mels=128, dims=384, head=6, layer=2, act="gelu", n_type="AbbyNormal")
+    model = Model(cfg).cuda().train()
+    spec, pitch, wav, ids, labels = _toy_inputs(B=2, T=16, S=1001)
+    outs = []
+    for _ in range(2):
+        model.set_noise(5, 2)
+        with prec.precision(precision):
+            out = model(labels=labels.cuda(), text_ids=ids.cuda(), spectrogram=spec.cuda(), pitch=pitch.cuda(),
+                        waveform=wav.cuda())
+        outs.append((out["logits"].detach().clone(), float(out["loss"])))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert outs[0][1] == outs[1][1]

@@ -244,10 +244,116 @@ def test_tgate(cuda):
     D = 128
     mod = tgate(D, num_types=3).cuda()
     x = torch.randn(3, 21, D)
-    P = {f"t.{k}": v.detach().cpu().double() for k, v in mod.state_dict().items()}
+    P = {f"t.{k}": v.detach().cpu().double().requires_grad_(True) for k, v in mod.state_dict().items()}
     yg, yr, gg, gr = _grads(lambda a: ops.tgate(mod, a), lambda a: om.tgate(P, "t", a), [x])
     assert _rel(yg, yr) < 1e-5
     assert _rel(gg[0], gr[0]) < 1e-4
+    # the three gates' weight / bias gradients land in their own p.grad (no cat backward)
+    for n, p in mod.named_parameters():
+        assert p.grad is not None, n
+        assert _rel(p.grad, P[f"t.{n}"].grad) < 1e-4, n
+
+
+def test_conv3_weight_norm(cuda):
+    """weight_norm(Conv1d(C, C, 3)) (model.py:140) through ops.conv3: g / v read directly (no torch
+    parametrization), forward and gradients of x, g, v, b against float64 torch."""
+    from asrx import ops
+    from torch.nn.utils.parametrizations import weight_norm
+
+    torch.manual_seed(4)
+    C, O, B, T = 64, 96, 2, 33
+    conv = weight_norm(torch.nn.Conv1d(C, O, kernel_size=3, padding=1))
+    with torch.no_grad():
+        conv.parametrizations.weight.original0.mul_(torch.rand(O, 1, 1) + 0.5)
+    ref = weight_norm(torch.nn.Conv1d(C, O, kernel_size=3, padding=1)).double()
+    ref.load_state_dict({k: v.double() for k, v in conv.state_dict().items()})
+    conv = conv.cuda()
+    x = torch.randn(B, T, C)
+    go = torch.randn(B, T, O)
+    xg = x.cuda().requires_grad_(True)
+    y = ops.conv3(xg, conv)
+    y.backward(go.cuda())
+    xr = x.double().requires_grad_(True)
+    yr = ref(xr.transpose(1, 2)).transpose(1, 2)
+    yr.backward(go.double())
+    assert _rel(y, yr) < 1e-5
+    assert _rel(xg.grad, xr.grad) < 1e-5
+    pg = dict(conv.named_parameters())
+    for n, p in ref.named_parameters():
+        assert _rel(pg[n].grad, p.grad) < 1e-4, n
+
+
+def test_cross_entropy_device_mean(cuda):
+    """F.cross_entropy(ignore_index=0) (model.py:670): one-pass log-sum-exp, on-device mean and count,
+    backward scaled by the device gradient; rows with label 0 ignored."""
+    from asrx import ops
+
+    torch.manual_seed(6)
+    R, V = 37, 1003
+    z = torch.randn(R, V) * 4
+    lab = torch.randint(1, V, (R,))
+    lab[::5] = 0
+    zg = z.cuda().requires_grad_(True)
+    loss = ops.CrossEntropy.apply(zg, lab.cuda())
+    (loss * 2.5).backward()
+    zr = z.double().requires_grad_(True)
+    lr = F.cross_entropy(zr, lab, ignore_index=0)
+    (lr * 2.5).backward()
+    assert abs(float(loss) - float(lr)) < 1e-5 * max(1.0, abs(float(lr)))
+    assert _rel(zg.grad, zr.grad) < 1e-5
+
+
+def test_blend(cuda):
+    from asrx import ops
+
+    torch.manual_seed(7)
+    d, g = torch.randn(2, 9, 64), torch.randn(2, 9, 64)
+    bl = torch.nn.Parameter(torch.tensor(0.3).cuda())
+    dg_, gg_ = d.cuda().requires_grad_(True), g.cuda().requires_grad_(True)
+    out = ops.blend(dg_, gg_, bl)
+    go = torch.randn(out.shape)
+    out.backward(go.cuda())
+    dr, gr_ = d.double().requires_grad_(True), g.double().requires_grad_(True)
+    br = torch.tensor(0.3, dtype=torch.float64, requires_grad=True)
+    s = torch.sigmoid(br)
+    outr = s * dr + (1 - s) * gr_
+    outr.backward(go.double())
+    assert _rel(out, outr) < 1e-6
+    assert _rel(dg_.grad, dr.grad) < 1e-6 and _rel(gg_.grad, gr_.grad) < 1e-6
+    assert abs(float(bl.grad) - float(br.grad)) < 1e-4 * max(1.0, abs(float(br.grad)))
+
+
+def test_fork_sink_and_stream_groups(cuda):
+    """ops.fork: consumers that accumulate into the sink (AbbyNormal, Linear, rotary |src|) plus one
+    that returns its gradient normally give x the summed gradient; split_rows / group: the views of a
+    stream group map back to the group tensor, and their gradients are joined in one kernel."""
+    from asrx import ops
+    from asrx.model import AbbyNormal
+
+    torch.manual_seed(8)
+    D, B, L = 128, 2, 19
+    ab = AbbyNormal(D).cuda()
+    W = torch.randn(D, D, device="cuda") / D ** 0.5
+    f = torch.rand(D // 4, device="cuda")
+    x0 = torch.randn(B, L, D, device="cuda")
+
+    def run(use_fork):
+        x = x0.clone().requires_grad_(True)
+        h = ops.fork(x) if use_fork else x
+        y = ops.abby_normal(ab, h, L, 1, 0, 0, False).sum() + ops.linear(h, W).pow(2).sum()
+        y = y + ops.rotary(ops.linear(h, W), h, f, 64, 0.5).sum() + (h * h).sum()
+        y.backward()
+        return x.grad
+
+    assert _rel(run(True), run(False)) < 1e-5
+    z = torch.randn(3 * B, L, D, device="cuda", requires_grad=True)
+    parts = ops.split_rows(z * 1.0, 3)
+    assert ops.group(parts) is parts[0]._asrx_group[0] and ops.group(parts[1:]).shape == (2 * B, L, D)
+    w = torch.randn(3, device="cuda")
+    (parts[0].sum() * w[0] + parts[1].pow(2).sum() * w[1] + parts[2].sum() * w[2]).backward()
+    ref = torch.cat([torch.full((B, L, D), float(w[0]), device="cuda"), 2 * float(w[1]) * z[B:2 * B].detach(),
+                     torch.full((B, L, D), float(w[2]), device="cuda")])
+    assert _rel(z.grad, ref) < 1e-6
 
 
 @pytest.mark.parametrize("fused,D", [(True, 128), (True, 384), (False, 128), (False, 192)])
