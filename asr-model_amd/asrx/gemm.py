@@ -106,15 +106,41 @@ def use_wide(K) -> bool:
     return prec.get() == prec.PREC_BF16 and K % 8 == 0
 
 
-def linear_fwd(x, W, b=None, act="none", out=None, preact=None, wbf=None):
-    """y = act(x @ W^T + b) for x (..., K), W (N, K); wbf: W's bf16 copy when the caller made it."""
+def gemm_wn_rows(A, Wb, C, *, M, N, K, lda, ldc, mtiles, bias=None, alpha=1.0, beta=0.0):
+    """gemm_wn on the 128-row tiles listed on the device (mtiles = (list, count) from row_tiles)."""
+    lib.require_gpu(A, Wb, C)
+    nj = _nj(M, N)
+    e0 = probe.begin("gemm")
+    lib.call("asrx_gemm_wn_rows", lib.ptr(A), lda, lib.ptr(Wb), Wb.stride(0), lib.ptr(C), ldc, lib.ptr(bias), None,
+             M, N, K, float(alpha), float(beta), ACT["none"], nj, lib.ptr(mtiles[0]), lib.ptr(mtiles[1]),
+             lib.stream())
+    probe.end("gemm", e0, 2.0 * M * N * K, ("wn_rows", M, N, K, nj, beta != 0))
+    return C
+
+
+def row_tiles(next_i, layer, L, M):
+    """(list, count) of the 128-row tiles of an M-row activation holding rows of samples at MSheath
+    layer `layer` (next_i[b] == layer, L rows per sample), built on the device."""
+    n = int(lib.load().asrx_row_tiles_max(M))
+    tl = torch.empty(n, dtype=torch.int32, device=next_i.device)
+    cnt = torch.empty(1, dtype=torch.int32, device=next_i.device)
+    lib.call("asrx_row_tiles", lib.ptr(next_i), layer, L, M, lib.ptr(tl), lib.ptr(cnt), lib.stream())
+    return tl, cnt
+
+
+def linear_fwd(x, W, b=None, act="none", out=None, preact=None, wbf=None, mtiles=None):
+    """y = act(x @ W^T + b) for x (..., K), W (N, K); wbf: W's bf16 copy when the caller made it;
+    mtiles: only these 128-row tiles (perf mode; the fp32 parity GEMM computes every row)."""
     x2 = _rows(x)
     if not x2.is_contiguous():
         x2 = x2.contiguous()
     M, K = x2.shape
     N = W.shape[0]
     y = out if out is not None else torch.empty(*x.shape[:-1], N, device=x.device, dtype=torch.float32)
-    if use_wide(K):
+    if use_wide(K) and mtiles is not None and act == "none" and preact is None:
+        gemm_wn_rows(x2, weight_bf16(W) if wbf is None else wbf, y, M=M, N=N, K=K, lda=K, ldc=N, bias=b,
+                     mtiles=mtiles)
+    elif use_wide(K):
         gemm_wn(x2, weight_bf16(W) if wbf is None else wbf, y, M=M, N=N, K=K, lda=K, ldc=N, bias=b, act=act,
                 Z=preact)
     else:
@@ -123,15 +149,17 @@ def linear_fwd(x, W, b=None, act="none", out=None, preact=None, wbf=None):
     return y
 
 
-def linear_dgrad(dy, W, out=None, beta=0.0):
-    """dx = dy @ W for dy (..., N), W (N, K)."""
+def linear_dgrad(dy, W, out=None, beta=0.0, mtiles=None):
+    """dx = dy @ W for dy (..., N), W (N, K); mtiles as in linear_fwd."""
     d2 = _rows(dy)
     if not d2.is_contiguous():
         d2 = d2.contiguous()
     M, N = d2.shape
     K = W.shape[1]
     dx = out if out is not None else torch.empty(*dy.shape[:-1], K, device=dy.device, dtype=torch.float32)
-    if use_wide(N):
+    if use_wide(N) and mtiles is not None:
+        gemm_wn_rows(d2, weight_bf16(W, trans=True), dx, M=M, N=K, K=N, lda=N, ldc=K, beta=beta, mtiles=mtiles)
+    elif use_wide(N):
         gemm_wn(d2, weight_bf16(W, trans=True), dx, M=M, N=K, K=N, lda=N, ldc=K, beta=beta)
     else:
         gemm(d2, W, dx, M=M, N=K, K=N, lda=N, ldb=K, ldc=K, a_kc=True, b_kc=False, beta=beta)

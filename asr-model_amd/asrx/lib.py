@@ -74,13 +74,17 @@ SIGNATURES = {
     "asrx_cat3": (_i32, [_p] * 3 + [_i64, _p, _p]),
     "asrx_layernorm_fwd2": (_i32, [_p] * 10 + [_i32, _i64, _i64, _f32, _p]),
     "asrx_vgate_weights": (_i32, [_p] * 7 + [_i64, _i64, _i64, _p]),
-    "asrx_msheath_row_fwd": (_i32, [_p] * 6 + [_i64] + [_p] * 14 + [_i64] * 4 + [_f32, _f32, _p]),
-    "asrx_msheath_row_bwd": (_i32, [_p] * 11 + [_i64] + [_p] * 18 + [_i64] * 4 + [_f32, _p]),
+    "asrx_msheath_row_fwd": (_i32, [_p] * 6 + [_i64] + [_p] * 14 + [_i64] * 4 + [_f32, _f32, _p, _i64, _i64, _p]),
+    "asrx_msheath_row_bwd": (_i32, [_p] * 11 + [_i64] + [_p] * 18 + [_i64] * 4 + [_f32, _p, _i64, _i64, _p]),
+    "asrx_gemm_wn_rows": (_i32, [_p, _i64, _p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _f32, _f32, _i32, _i32, _p,
+                                 _p, _p]),
+    "asrx_row_tiles_max": (_i64, [_i64]),
+    "asrx_row_tiles": (_i32, [_p, _i64, _i64, _i64, _p, _p, _p]),
     "asrx_msheath_ctrl_fwd3": (_i32, [_p, _p, _i64, _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p] + [_i64] * 5 + [_p] * 8),
     "asrx_mem_chunks": (_i64, [_i64]),
     "asrx_seg_colsum_det": (_i32, [_p, _p, _p, _i64, _i64, _i64, _f32, _p]),
     "asrx_msheath_ctrl_bwd3": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _p, _p, _p] + [_i64] * 4 + [_p, _i32] + [_p] * 8),
-    "asrx_axpy_row2_colsum": (_i32, [_p] * 6 + [_i64] * 3 + [_p]),
+    "asrx_axpy_row2_colsum": (_i32, [_p] * 6 + [_i64] * 3 + [_p, _i64, _p]),
     "asrx_vgate_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _f32, _p]),
     "asrx_vgate_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p,
                               _i64, _i64, _i64, _f32, _p]),

@@ -123,7 +123,7 @@ class ConvLite(nn.Module):
         D = x.shape[-1]
         x = ops.fork(x)  # read by point1 and the residual add
         res = x
-        y = ops.linear(x, self.point1.weight.view(2 * D, D), self.point1.bias)
+        y = ops.linear(x, self.point1.weight, self.point1.bias)  # (2D, D, 1) leaf: gradient straight into it
         y = ops.glu(y)
         y = ops.DWConv.apply(y, self.depth.weight, self.depth.bias)
         if self.training:
@@ -134,7 +134,7 @@ class ConvLite(nn.Module):
             y = ops.batch_norm_eval(y, self.bn.weight, self.bn.bias, self.bn.running_mean, self.bn.running_var,
                                     self.bn.eps)
         y = ops.act(y, "silu")
-        y = ops.linear(y, self.point2.weight.view(D, D), self.point2.bias)
+        y = ops.linear(y, self.point2.weight, self.point2.bias)
         if self.training:  # res + dropout(y) in one pass
             return ops.dropout_add(res, y, sid_base, noise.key(site + ".cl"), 0.1)
         return ops.add(res, y)

@@ -103,7 +103,10 @@ def forward(mod, x0, gpol, save):
         wb = _E(N, D, dtype=torch.int16, device=dev) if wide else None
         lib.call("asrx_vgate_weights", _P(vg.mkey), _P(vg.mlp[0].weight), _P(vg.mlp[0].bias), _P(Wc), _P(bc),
                  _P(mkn), _P(wb), M, Dh, D, st)
-        SH = G.linear_fwd(x, Wc, bc, wbf=wb)
+        # rows of samples not at this layer (next_i[b] != i; the reference never runs them) are skipped:
+        # by whole 128-row tiles in the GEMMs, by row in the row kernels
+        mt = G.row_tiles(next_i, i, L, rows) if (wide and next_i is not None) else None
+        SH = G.linear_fwd(x, Wc, bc, wbf=wb, mtiles=mt)
         # px = LayerNorm(x), |x|, g = sigmoid(gate(px)), ion = v_gate(x)   (346-351, 452-460)
         ln, gt = lay["ln"], lay["gate"][0]
         px = _E(B, L, D, device=dev)
@@ -111,11 +114,13 @@ def forward(mod, x0, gpol, save):
         lib.call("asrx_msheath_row_fwd", _P(x), _P(ln.weight), _P(ln.bias), _P(gt.weight), _P(gt.bias), _P(SH), N,
                  _P(vg.mval), _P(vg.mlp[2].weight), _P(vg.mlp[2].bias), _P(vg.concat.weight), _P(vg.concat.bias),
                  _P(vg.tx), _P(px), _P(mean), _P(rstd), _P(nx), _P(gv), _P(ion), _P(kv), _P(m2), rows, D, M, Dh,
-                 float(ln.eps), inv_sqrt_d, st)
-        out = G.linear_fwd(px, lay["adapter"].weight, lay["adapter"].bias) if lay["adapter"] is not None else px
+                 float(ln.eps), inv_sqrt_d, _P(next_i), i, L, st)
+        ad = lay["adapter"]
+        out = G.linear_fwd(px, ad.weight, ad.bias, mtiles=mt) if ad is not None else px
         # x_new = x + g * ion * out; mem = mean_l x_new   (461-463)
         x_new = _E(B, L, D, device=dev)
-        lib.call("asrx_axpy_row2_colsum", _P(x), _P(gv), _P(ion), _P(out), _P(x_new), _P(part[i]), B, L, D, st)
+        lib.call("asrx_axpy_row2_colsum", _P(x), _P(gv), _P(ion), _P(out), _P(x_new), _P(part[i]), B, L, D,
+                 _P(next_i), i, st)
         # mem_v = sigmoid(mem_gate(mem)); control; jump select   (464-501)
         alpha, beta, active, next_out, mem_v = (_E(B, device=dev) for _ in range(5))
         gam, mwo, mem = _E(B, D, device=dev), _E(B, D, device=dev), _E(B, D, device=dev)
@@ -130,7 +135,7 @@ def forward(mod, x0, gpol, save):
         if save:
             layers.append(dict(x=x, Wc=Wc, mkn=mkn, SH=SH, nx=nx, kv=kv, m2=m2, px=px, mean=mean, rstd=rstd,
                                out=out, g=gv, ion=ion, x_new=x_new, mem=mem, mem_v=mem_v, mem_w=mem_w, ld_mw=ld_mw,
-                               rec=rec, active=active, alpha=alpha, beta=beta))
+                               rec=rec, active=active, alpha=alpha, beta=beta, next_i=next_i, mt=mt))
         mem_w, ld_mw, next_i = mwo, D, next_out
         x = x_out
     # x + sigmoid(mlp_gate(x)) * mlp(mlp_ln(x))   (503-506): the gate from the LayerNorm's row pass
@@ -229,7 +234,7 @@ class MSheathFn(torch.autograd.Function):
             del dxn
             ad = lay["adapter"]
             if ad is not None:
-                dpx = G.linear_dgrad(dout, ad.weight)
+                dpx = G.linear_dgrad(dout, ad.weight, mtiles=s["mt"])  # rows off the layer: not read below
                 G.linear_wgrad(dout, s["px"], out=gb(ad.weight), accumulate=True)
                 ops.colsum(dout.view(rows, D), out=gb(ad.bias))
             else:
@@ -242,10 +247,11 @@ class MSheathFn(torch.autograd.Function):
                      _P(vg.mval), _P(vg.mlp[2].weight), _P(vg.concat.weight), _P(s["kv"]), _P(s["m2"]), _P(dxi),
                      _P(gb(ln.weight)), _P(gb(ln.bias)), _P(gb(gt.weight)), _P(gb(gt.bias)), _P(dSH),
                      _P(gb(vg.mval)), _P(gb(vg.mlp[2].weight)), _P(gb(vg.mlp[2].bias)), _P(gb(vg.concat.weight)),
-                     _P(gb(vg.concat.bias)), _P(gb(vg.mlp[0].bias)), rows, D, M, Dh, inv_sqrt_d, st)
+                     _P(gb(vg.concat.bias)), _P(gb(vg.mlp[0].bias)), rows, D, M, Dh, inv_sqrt_d, _P(s["next_i"]), i,
+                     L, st)
             del dout, dpx
             # x's gradient through both projections: one GEMM against [normalize(mkey); mlp[0].weight]
-            G.linear_dgrad(dSH, s["Wc"], out=dxi, beta=1.0)
+            G.linear_dgrad(dSH, s["Wc"], out=dxi, beta=1.0, mtiles=s["mt"])
             x2 = xi.view(rows, D)
             dmk = _E(M, D, device=dev)
             lib.call("asrx_zero", _P(dmk), dmk.numel() * 4, st)

@@ -199,7 +199,7 @@ class Linear(torch.autograd.Function):
         # the pre-activation is kept only for a backward that will run (none in the reference's dead
         # blocks, eval or decoding: an N-wide fp32 write saved per call)
         z = _E(*x.shape[:-1], W.shape[0], device=x.device) if act != "none" and grad else None
-        y = G.linear_fwd(x, W, b, act=act, preact=z)
+        y = G.linear_fwd(x, W.view(W.shape[0], -1), b, act=act, preact=z)  # (N, K, 1): a 1x1 Conv1d weight
         ctx.act = act
         ctx.has_b = b is not None
         if grad:
@@ -209,7 +209,8 @@ class Linear(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy):
-        x, W, z, b = ctx.saved_tensors
+        x, W3, z, b = ctx.saved_tensors
+        W = W3.view(W3.shape[0], -1)
         gy = _c(gy)
         if ctx.act != "none":
             gz = _E(gy.shape, device=gy.device)
@@ -225,7 +226,9 @@ class Linear(torch.autograd.Function):
                 dx = G.linear_dgrad(gz, W)
         dW = db = None
         if ctx.needs_input_grad[1]:
-            dW = _gret(W, G.linear_wgrad(gz, x, out=_gbuf(W, ctx.dW), accumulate=True), ctx.dW)
+            gW = _gbuf(W3, ctx.dW)
+            G.linear_wgrad(gz, x, out=gW.view(W.shape), accumulate=True)
+            dW = _gret(W3, gW, ctx.dW)
         if ctx.has_b and ctx.needs_input_grad[2]:
             db = _gret(b, colsum(gz, out=_gbuf(b, True) if ctx.db else None), ctx.db)
         return dx, dW, db, None, None, None

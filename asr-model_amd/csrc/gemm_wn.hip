@@ -48,6 +48,11 @@ struct Params {
   int act;
   const float* W2;  // router: Linear(d, 3) weight (3 x N) applied to SiLU(C) in the epilogue
   float* R;         // router: logits without bias (M x 3); C may be null (h_pre not kept)
+  // optional row-tile list (gemm_wr_kernel): only the BM-row tiles mtiles[0 .. *n_mtiles) are
+  // computed (MSheath layers skip the rows of samples that are not at the layer); other rows of C
+  // are left untouched
+  const int* mtiles;
+  const int* n_mtiles;
 };
 
 template <int NJ>
@@ -501,7 +506,7 @@ __device__ __forceinline__ void wr_store(const WrStage<NJ>& st, char* At, char* 
 }
 
 template <int NJ, bool CONV, bool RT>
-__global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) {
+__global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) {  // ntiles: all tiles
   typedef Cfg<NJ> CF;
   constexpr int BN = CF::BN, NT = 2 * NJ, BNR = CF::BNR;
   constexpr int AB = BM * BK * 2, BB = BN * BK * 2;  // bf16 images
@@ -522,6 +527,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
   const int nk = (p.K + BK - 1) / BK;
   const int G = gridDim.x, bid = blockIdx.x;
   const int r = (G % 8 == 0) ? (bid & 7) * (G >> 3) + (bid >> 3) : bid;  // XCD-grouped tile ranks
+  const int* mlist = p.mtiles;
+  if (mlist) ntiles = *p.n_mtiles * nN;  // device-side count (the list is built on the device)
   const int my = r < ntiles ? (ntiles - r + G - 1) / G : 0;
   const int S = my * nk;
   float* ep = ep_s + (threadIdx.x >> 6) * EpLds<NJ>::FLOATS;
@@ -533,7 +540,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
   auto coords = [&](int s, int& m0, int& n0, int& k0) __attribute__((always_inline)) {
     const int j = s / nk;
     const int t = j * G + r;
-    m0 = (t / nN) * BM;
+    // past this workgroup's tiles (prefetch only) the raw index is kept: in range or beyond M
+    m0 = ((mlist && t < ntiles) ? mlist[t / nN] : t / nN) * BM;
     n0 = (t % nN) * BN;
     k0 = (s - j * nk) * BK;
   };
@@ -754,6 +762,75 @@ extern "C" int asrx_gemm_wn(const float* A, int64_t lda, int conv, int64_t convF
     conv ? wn::launch<1, true, 3>(p, stream) : wn::launch<1, false, 3>(p, stream);
   }
   ASRX_LAUNCHED("asrx_gemm_wn");
+}
+
+// asrx_gemm_wn restricted to the BM-row tiles listed in mtiles (n_mtiles entries, both on the device,
+// from asrx_row_tiles); rows of other tiles are not written.
+extern "C" int asrx_gemm_wn_rows(const float* A, int64_t lda, const unsigned short* W, int64_t ldw, float* C,
+                                 int64_t ldc, const float* bias, float* Z, int64_t M, int64_t N, int64_t K,
+                                 float alpha, float beta, int act, int nj, const int* mtiles, const int* n_mtiles,
+                                 hipStream_t stream) {
+  ASRX_REQUIRE(M > 0 && N > 0 && K > 0, "asrx_gemm_wn_rows: empty problem");
+  ASRX_REQUIRE(((uintptr_t)A & 15) == 0 && ((uintptr_t)W & 15) == 0, "asrx_gemm_wn_rows: A/W must be 16-byte aligned");
+  ASRX_REQUIRE(K % 8 == 0 && lda % 4 == 0 && ldw % 8 == 0, "asrx_gemm_wn_rows: K%%8, lda%%4, ldw%%8 required");
+  ASRX_REQUIRE(M * lda < (1LL << 31) && N * ldw < (1LL << 31), "asrx_gemm_wn_rows: operand spans >= 2^31 elements");
+  ASRX_REQUIRE(mtiles && n_mtiles, "asrx_gemm_wn_rows: tile list required");
+  wn::Params p{A, (int)lda, W, (int)ldw, C, (int)ldc, bias, Z, (int)M, (int)N, (int)K, 1, 1, alpha, beta, act,
+               nullptr, nullptr, mtiles, n_mtiles};
+  if (nj == 3) wn::launch_wr<3, false>(p, stream);
+  else if (nj == 2) wn::launch_wr<2, false>(p, stream);
+  else wn::launch_wr<1, false>(p, stream);
+  ASRX_LAUNCHED("asrx_gemm_wn_rows");
+}
+
+// The BM-row tiles of an M-row activation whose rows r belong to a sample b = r / L that is at MSheath
+// layer `layer` (next_i[b] == layer): mtiles[0 .. *n_mtiles) in increasing order.  One workgroup.
+namespace asrx {
+__global__ __launch_bounds__(1024) void row_tiles_kernel(const float* __restrict__ next_i, int layer, int64_t L,
+                                                         int64_t M, int* __restrict__ mtiles, int* __restrict__ n_out) {
+  __shared__ int wsum[16];
+  __shared__ int base;
+  const int nm = (int)((M + wn::BM - 1) / wn::BM);
+  if (threadIdx.x == 0) base = 0;
+  __syncthreads();
+  for (int t0 = 0; t0 < nm; t0 += 1024) {
+    const int t = t0 + threadIdx.x;
+    int act = 0;
+    if (t < nm) {
+      const int64_t r0 = (int64_t)t * wn::BM, r1 = min<int64_t>(r0 + wn::BM, M) - 1;
+      for (int64_t b = r0 / L; b <= r1 / L && !act; ++b) act = next_i[b] == (float)layer;
+    }
+    // block exclusive scan of act
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int v = act;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = __shfl_up(v, o);
+      if (lane >= o) v += u;
+    }
+    if (lane == 63) wsum[w] = v;
+    __syncthreads();
+    int off = base;
+    for (int k = 0; k < w; ++k) off += wsum[k];
+    if (act) mtiles[off + v - 1] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int tot = 0;
+      for (int k = 0; k < 16; ++k) tot += wsum[k];
+      base += tot;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) n_out[0] = base;
+}
+}  // namespace asrx
+
+extern "C" int64_t asrx_row_tiles_max(int64_t M) { return (M + wn::BM - 1) / wn::BM; }
+
+extern "C" int asrx_row_tiles(const float* next_i, int64_t layer, int64_t L, int64_t M, int* mtiles, int* n_mtiles,
+                              hipStream_t stream) {
+  ASRX_REQUIRE(L > 0 && M > 0, "asrx_row_tiles: empty");
+  row_tiles_kernel<<<1, 1024, 0, stream>>>(next_i, (int)layer, L, M, mtiles, n_mtiles);
+  ASRX_LAUNCHED("asrx_row_tiles");
 }
 
 // AbbyNormal router (essentials.py:155-161) in one pass: h_pre = A W1^T + b1 (kept in hpre when

@@ -195,11 +195,16 @@ constexpr int MEM_CHUNK = 64;
 __global__ __launch_bounds__(256) void axpy_row2_colsum_kernel(const float4* __restrict__ x, const float* __restrict__ s1,
                                                                const float* __restrict__ s2, const float4* __restrict__ y,
                                                                float4* __restrict__ out, float4* __restrict__ part,
-                                                               int64_t L, int d4) {
+                                                               int64_t L, int d4, const float* __restrict__ next_i,
+                                                               int layer) {
   __shared__ float4 red[256];
   const int nrl = 256 / d4;
   const int c = threadIdx.x % d4, rl = threadIdx.x / d4;
   const int64_t b = blockIdx.x;
+  if (next_i && next_i[b] != (float)layer) {  // sample not at this layer: x_new unused, mem = 0
+    if (rl == 0) part[((int64_t)b * gridDim.y + blockIdx.y) * d4 + c] = make_float4(0.f, 0.f, 0.f, 0.f);
+    return;
+  }
   const int64_t l0 = (int64_t)blockIdx.y * MEM_CHUNK, l1 = min<int64_t>(L, l0 + MEM_CHUNK);
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   if (rl < nrl) {
@@ -620,14 +625,14 @@ int asrx_msheath_ctrl_bwd3(const float* g_alpha, const float* g_beta, const floa
 int64_t asrx_mem_chunks(int64_t L) { return (L + MEM_CHUNK - 1) / MEM_CHUNK; }
 
 int asrx_axpy_row2_colsum(const float* x, const float* s1, const float* s2, const float* y, float* out, float* part,
-                          int64_t B, int64_t L, int64_t d, hipStream_t stream) {
+                          int64_t B, int64_t L, int64_t d, const float* next_i, int64_t layer, hipStream_t stream) {
   ASRX_REQUIRE(d % 4 == 0 && d <= 1024, "asrx_axpy_row2_colsum: d %% 4 == 0 and d <= 1024 required");
   ASRX_REQUIRE(s2 != nullptr, "asrx_axpy_row2_colsum: s2 required");
   if (B * L == 0) return 0;
   const int d4 = (int)(d / 4);
   dim3 grid((unsigned)B, (unsigned)asrx_mem_chunks(L));
   axpy_row2_colsum_kernel<<<grid, 256, 0, stream>>>((const float4*)x, s1, s2, (const float4*)y, (float4*)out,
-                                                    (float4*)part, L, d4);
+                                                    (float4*)part, L, d4, next_i, (int)layer);
   ASRX_LAUNCHED("asrx_axpy_row2_colsum");
 }
 

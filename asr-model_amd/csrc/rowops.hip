@@ -531,6 +531,9 @@ struct MSRowFwd {
   int64_t rows, ldsh;
   int M, Dh;
   float eps, inv_sqrt_d;
+  const float* next_i;  // rows of samples b with next_i[b] != layer are not at this layer (null: all are)
+  int layer;
+  int64_t L;
 };
 
 // Per row: px = LayerNorm(x); nx = |x|; g = sigmoid(px . gw + gb); v_gate from SH and nx (as
@@ -546,9 +549,28 @@ __global__ __launch_bounds__(64 * RW) void msheath_row_fwd_kernel(MSRowFwd p) {
   const float gbias = p.gb[0];
   const float mv_l = lane < p.M ? p.mval[lane] : 0.f;
   const float b2 = p.b2[0], cw0 = p.cw[0], cw1 = p.cw[1], cb = p.cb[0], tx = p.tx[0];
+  auto at_layer = [&](int64_t rr) { return !p.next_i || p.next_i[rr / p.L] == (float)p.layer; };
   int64_t r = row_begin();
-  if (r < p.rows) ld_lane<E>(p.x + r * D, lane, xn);
+  if (r < p.rows && at_layer(r)) ld_lane<E>(p.x + r * D, lane, xn);
   for (; r < p.rows; r += row_step()) {
+    const int64_t rn = r + row_step();
+    if (!at_layer(r)) {  // sample not at this layer: no reads; zeros keep every later consumer finite
+      float z[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) z[e] = 0.f;
+      st_lane<E>(p.px + r * D, lane, z);
+      if (lane == 0) {
+        p.mean[r] = 0.f;
+        p.rstd[r] = 0.f;
+        p.nx[r] = 0.f;
+        p.g[r] = 0.f;
+        p.ion[r] = 0.f;
+        p.kv[r] = 0.f;
+        p.m2[r] = 0.f;
+      }
+      if (rn < p.rows && at_layer(rn)) ld_lane<E>(p.x + rn * D, lane, xn);
+      continue;
+    }
     float xv[E];
     float s = 0.f, q = 0.f;
 #pragma unroll
@@ -557,7 +579,7 @@ __global__ __launch_bounds__(64 * RW) void msheath_row_fwd_kernel(MSRowFwd p) {
       s += xv[e];
       q += xv[e] * xv[e];
     }
-    if (r + row_step() < p.rows) ld_lane<E>(p.x + (r + row_step()) * D, lane, xn);
+    if (rn < p.rows && at_layer(rn)) ld_lane<E>(p.x + rn * D, lane, xn);
     const float mu = wave_sum_dpp(s) * (1.0f / D);
     const float nrm = sqrtf(wave_sum_dpp(q));
     float v = 0.f;
@@ -611,6 +633,9 @@ struct MSRowBwd {
   int64_t rows, ldsh;
   int M, Dh;
   float inv_sqrt_d;
+  const float* next_i;  // as MSRowFwd: rows of samples not at this layer get dSH = 0 and nothing else
+  int layer;
+  int64_t L;
 };
 
 // Per row, the backward of msheath_row_fwd: v_gate (dSH row with stride ldsh: dS already divided by
@@ -636,6 +661,11 @@ __global__ __launch_bounds__(64 * RW) void msheath_row_bwd_kernel(MSRowBwd p) {
   const float mv_l = lane < M ? p.mval[lane] : 0.f;
   const float cw0 = p.cw[0], cw1 = p.cw[1];
   for (int64_t r = row_begin(); r < p.rows; r += row_step()) {
+    if (p.next_i && p.next_i[r / p.L] != (float)p.layer) {
+      float* dz = p.dSH + r * p.ldsh;  // zero rows: the weight-gradient GEMMs sum over every row
+      for (int j = lane; j < M + Dh; j += 64) dz[j] = 0.f;
+      continue;
+    }
     // ---- v_gate backward (vgate_bwd_kernel)
     const float gi = p.dion[r];
     const float nxr = p.nx[r];
@@ -1953,12 +1983,14 @@ int asrx_msheath_row_fwd(const float* x, const float* lnw, const float* lnb, con
                          const float* SH, int64_t ldsh, const float* mval, const float* w2, const float* b2,
                          const float* cw, const float* cb, const float* tx, float* px, float* mean, float* rstd,
                          float* nx, float* g, float* ion, float* kv, float* m2, int64_t rows, int64_t d, int64_t M,
-                         int64_t Dh, float eps, float inv_sqrt_d, hipStream_t stream) {
+                         int64_t Dh, float eps, float inv_sqrt_d, const float* next_i, int64_t layer, int64_t L,
+                         hipStream_t stream) {
   ASRX_REQUIRE(M <= 64 && ldsh >= M + Dh, "asrx_msheath_row_fwd: M <= 64 and ldsh >= M + Dh required");
   ASRX_REQUIRE(ms_aligned({x, lnw, lnb, gw, px}), "asrx_msheath_row_fwd: 8-byte aligned rows required");
+  ASRX_REQUIRE(!next_i || L > 0, "asrx_msheath_row_fwd: L > 0 required with next_i");
   if (rows == 0) return 0;
   MSRowFwd p{x, lnw, lnb, gw, gb, SH, mval, w2, b2, cw, cb, tx, px, mean, rstd, nx, g, ion, kv, m2, rows, ldsh,
-             (int)M, (int)Dh, eps, inv_sqrt_d};
+             (int)M, (int)Dh, eps, inv_sqrt_d, next_i, (int)layer, L > 0 ? L : 1};
   MS_DISPATCH(msheath_row_fwd_kernel, row_grid(rows), 0, p);
   ASRX_LAUNCHED("asrx_msheath_row_fwd");
 }
@@ -1971,12 +2003,14 @@ int asrx_msheath_row_bwd(const float* dpx, const float* x, const float* lnw, con
                          const float* cw, const float* kv, const float* m2, float* dx, float* dlnw, float* dlnb,
                          float* dgw, float* dgb, float* dSH, float* dmval, float* dw2, float* db2, float* dcw,
                          float* dcb, float* db1, int64_t rows, int64_t d, int64_t M, int64_t Dh, float inv_sqrt_d,
-                         hipStream_t stream) {
+                         const float* next_i, int64_t layer, int64_t L, hipStream_t stream) {
   ASRX_REQUIRE(M <= 64 && ldsh >= M + Dh, "asrx_msheath_row_bwd: M <= 64 and ldsh >= M + Dh required");
   ASRX_REQUIRE(ms_aligned({dpx, x, lnw, lnb, gw, dx}), "asrx_msheath_row_bwd: 8-byte aligned rows required");
+  ASRX_REQUIRE(!next_i || L > 0, "asrx_msheath_row_bwd: L > 0 required with next_i");
   if (rows == 0) return 0;
   MSRowBwd p{dpx, x, lnw, lnb, mean, rstd, dg, g, gw, dion, SH, nx, mval, w2, cw, kv, m2, dx, dlnw, dlnb, dgw, dgb,
-             dSH, dmval, dw2, db2, dcw, dcb, db1, rows, ldsh, (int)M, (int)Dh, inv_sqrt_d};
+             dSH, dmval, dw2, db2, dcw, dcb, db1, rows, ldsh, (int)M, (int)Dh, inv_sqrt_d, next_i, (int)layer,
+             L > 0 ? L : 1};
   const size_t shm = (size_t)RW * (3 * d + M + 2 * Dh + 5) * sizeof(float);
   MS_DISPATCH(msheath_row_bwd_kernel, row_grid(rows, 1024), shm, p);
   ASRX_LAUNCHED("asrx_msheath_row_bwd");

@@ -83,6 +83,15 @@ int asrx_gemm_wn_router(const float* A, int64_t lda, const unsigned short* W1, i
 int asrx_gemm_wn(const float* A, int64_t lda, int conv, int64_t convF, int64_t convC, const unsigned short* W,
                  int64_t ldw, float* C, int64_t ldc, const float* bias, float* Z, int64_t M, int64_t N, int64_t K,
                  float alpha, float beta, int act, int nj, asrx_stream_t stream);
+/* asrx_gemm_wn on the BM(=128)-row tiles listed on the device (mtiles[0 .. *n_mtiles)); other rows of
+ * C are not written.  asrx_row_tiles lists the tiles holding rows of samples at MSheath layer
+ * `layer` (next_i[b] == layer, L rows per sample), at most asrx_row_tiles_max(M) entries. */
+int asrx_gemm_wn_rows(const float* A, int64_t lda, const unsigned short* W, int64_t ldw, float* C, int64_t ldc,
+                      const float* bias, float* Z, int64_t M, int64_t N, int64_t K, float alpha, float beta, int act,
+                      int nj, const int* mtiles, const int* n_mtiles, asrx_stream_t stream);
+int64_t asrx_row_tiles_max(int64_t M);
+int asrx_row_tiles(const float* next_i, int64_t layer, int64_t L, int64_t M, int* mtiles, int* n_mtiles,
+                   asrx_stream_t stream);
 
 /* ---- AbbyNormal: essentials.py:140-191 (router SiLU-MLP, cv, gumbel hard decision, avg/max pool of
  *      x^2 along the feature axis, x / (1 + 1e-4 div)^0.75).  hpre = x @ W1^T + b1 from asrx_gemm.
@@ -186,21 +195,24 @@ int asrx_vgate_bwd(const float* dion, const float* S, const float* nx, const flo
  *      ldsh).  asrx_msheath_row_fwd: per row px = LayerNorm(x), nx = |x|, g = sigmoid(px.gw + gb), the
  *      v_gate outputs (ion, kv, m2).  asrx_msheath_row_bwd: its backward with dx accumulated, dSH
  *      written and every parameter gradient accumulated; db1 is mlp[0].bias's gradient.  d in {128,
- *      256, 384, 512, 768, 1024}, M <= 64. */
+ *      256, 384, 512, 768, 1024}, M <= 64.  With next_i (L rows per sample), rows of samples with
+ *      next_i[b] != layer are skipped (the reference never runs them): forward writes zeros, backward
+ *      dSH = 0 rows. */
 int asrx_vgate_weights(const float* mkey, const float* W1, const float* b1, float* Wc, float* bc, float* mkn,
                        unsigned short* wb, int64_t M, int64_t Dh, int64_t D, asrx_stream_t stream);
 int asrx_msheath_row_fwd(const float* x, const float* lnw, const float* lnb, const float* gw, const float* gb,
                          const float* SH, int64_t ldsh, const float* mval, const float* w2, const float* b2,
                          const float* cw, const float* cb, const float* tx, float* px, float* mean, float* rstd,
                          float* nx, float* g, float* ion, float* kv, float* m2, int64_t rows, int64_t d, int64_t M,
-                         int64_t Dh, float eps, float inv_sqrt_d, asrx_stream_t stream);
+                         int64_t Dh, float eps, float inv_sqrt_d, const float* next_i, int64_t layer, int64_t L,
+                         asrx_stream_t stream);
 int asrx_msheath_row_bwd(const float* dpx, const float* x, const float* lnw, const float* lnb, const float* mean,
                          const float* rstd, const float* dg, const float* g, const float* gw, const float* dion,
                          const float* SH, int64_t ldsh, const float* nx, const float* mval, const float* w2,
                          const float* cw, const float* kv, const float* m2, float* dx, float* dlnw, float* dlnb,
                          float* dgw, float* dgb, float* dSH, float* dmval, float* dw2, float* db2, float* dcw,
                          float* dcb, float* db1, int64_t rows, int64_t d, int64_t M, int64_t Dh, float inv_sqrt_d,
-                         asrx_stream_t stream);
+                         const float* next_i, int64_t layer, int64_t L, asrx_stream_t stream);
 
 /* ---- tgate (model.py:532-535): G = sigmoid(x Wcat^T + b) (rows,3D) from asrx_gemm, c (rows,3). */
 int asrx_tgate_fwd(const float* G, const float* c, float* out, int64_t rows, int64_t D, asrx_stream_t stream);
@@ -265,7 +277,7 @@ int asrx_msheath_ctrl_bwd3(const float* g_alpha, const float* g_beta, const floa
  * asrx_mem_chunks(L), d), no atomics (deterministic forward), d <= 1024. */
 int64_t asrx_mem_chunks(int64_t L);
 int asrx_axpy_row2_colsum(const float* x, const float* s1, const float* s2, const float* y, float* out, float* part,
-                          int64_t B, int64_t L, int64_t d, asrx_stream_t stream);
+                          int64_t B, int64_t L, int64_t d, const float* next_i, int64_t layer, asrx_stream_t stream);
 /* MSheath fused backward (asrx/msheath.py): jump_select backward in accumulate form (active: dxn =
  * alpha g, orig's gradient (+)= beta g on a jump; inactive: dx = g), the x_new/mem backward writing
  * x's gradient for active samples (g' = dxn + gm/L), and the final dx += orig grad + u broadcast. */

@@ -263,3 +263,34 @@ def test_abby_fused_router_matches_unfused(cuda):
              lib.ptr(idx), rows, d, 3000, 1, 0, 1234, 1, lib.stream())
     same = (fused - out).abs().max(dim=1).values <= 1e-5 * out.abs().max()
     assert float(same.float().mean()) > 0.999  # only near-tie gumbel picks may differ
+
+
+@pytest.mark.parametrize("L,N", [(300, 256), (129, 384), (1000, 64)])
+def test_wide_gemm_row_tiles(cuda, L, N):
+    """asrx_row_tiles + asrx_gemm_wn_rows (MSheath layers skip samples not at the layer): the tiles
+    holding rows of active samples equal the full GEMM, every other row is left untouched."""
+    from asrx import gemm as G, prec
+
+    g = torch.Generator().manual_seed(11)
+    B, K = 7, 384
+    M = B * L
+    x = torch.randn(M, K, generator=g).to(cuda)
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(cuda)
+    bias = torch.randn(N, generator=g).to(cuda)
+    next_i = torch.tensor([2.0, 1.0, 2.0, 3.0, 3.0, 2.0, 0.0], device=cuda)
+    layer = 2
+    with prec.precision("bf16"):
+        full = G.linear_fwd(x, W, bias)
+        mt = G.row_tiles(next_i, layer, L, M)
+        y = torch.full((M, N), 12345.0, device=cuda)
+        G.linear_fwd(x, W, bias, out=y, mtiles=mt)
+    tl, cnt = mt[0].cpu(), int(mt[1])
+    want = [t for t in range((M + 127) // 128)
+            if any(float(next_i[b]) == layer for b in range(t * 128 // L, (min(t * 128 + 128, M) - 1) // L + 1))]
+    assert tl[:cnt].tolist() == want
+    rows = torch.zeros(M, dtype=torch.bool)
+    for t in want:
+        rows[t * 128:min(t * 128 + 128, M)] = True
+    rows = rows.to(cuda)
+    assert torch.equal(y[rows], full[rows])
+    assert bool((y[~rows] == 12345.0).all())
