@@ -355,7 +355,7 @@ def main():
 
 def pmc_traffic(kernel_substr):
     """HBM bytes per launch of a kernel from the newest committed PMC table (profiles/
-    r01_pmc_traffic_v*.csv: separate rocprofv3 FETCH_SIZE and WRITE_SIZE passes over one eager step,
+    rNN_pmc_traffic_vM.csv, newest round then version: separate rocprofv3 FETCH_SIZE and WRITE_SIZE passes over one eager step,
     FETCH doubled per the gfx950 note, see tools/pmc_traffic.py), launch-weighted over every template
     instance whose name contains kernel_substr.  PMC counters cannot be read inside the timed run,
     so the figure comes from the profiling pass of the same step; null when no table is present."""
@@ -363,7 +363,7 @@ def pmc_traffic(kernel_substr):
     import glob
     tabs = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
                                          "r*_pmc_traffic_v*.csv")),
-                  key=lambda p: int(re.search(r"_v(\d+)\.csv$", p).group(1)))
+                  key=lambda p: tuple(int(v) for v in re.search(r"r(\d+)_pmc_traffic_v(\d+)\.csv$", p).groups()))
     if not tabs:
         return {"traffic": None}
     n, tot = 0, 0.0
