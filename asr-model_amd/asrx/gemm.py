@@ -33,16 +33,90 @@ def _rows(x):
 # bf16 copies of the weights used in this step (asrx_weight_to_bf16), keyed by storage, layout and
 # version; cleared at the start of every Model.forward so that updated weights are re-converted and
 # the conversions of a step stay inside that step (and inside its captured graph).
+#
+# Bulk plan: the parameter weights (and views of them) a step converted are recorded; from the next
+# step on, clear_weight_cache converts all of them in ONE launch (asrx_weights_to_bf16, ~200
+# launches fewer per tiny step) into a persistent arena on the current stream, at the start of the
+# forward -- before any side stream forks -- so the entries serve every stream.  Weights derived per
+# step (tgate's concatenation, v_gate's normalised keys) keep the lazy per-call conversion.
 _WCACHE: dict = {}
+_BULK: dict = {}       # (ptr, shape, stride, trans) -> bf16 arena view, valid for the current step
+_SEEN: dict = {}       # plan being recorded for the current owner: key -> (source tensor,)
+_PLANS: dict = {}      # id(owner model) -> (keys, sources, arena views, table, max_elems)
+_OWNER = None          # id of the model whose step is running (set by clear_weight_cache)
+_PLAN_OFF = False
 
 
-def clear_weight_cache():
+def _bulk_key(W, trans):
+    return (W.data_ptr(), tuple(W.shape), tuple(W.stride()), bool(trans))
+
+
+def _is_param_weight(W):
+    base = W._base if W._base is not None else W
+    return isinstance(base, torch.nn.Parameter) and W.is_cuda and W.stride(1) == 1
+
+
+def _build_plan():
+    if not _SEEN:
+        return None
+    keys = list(_SEEN)
+    srcs = [_SEEN[k][0] for k in keys]
+    _SEEN.clear()
+    sizes = [t.numel() for t in srcs]
+    dev = srcs[0].device
+    arena = torch.empty(sum(sizes), dtype=torch.int16, device=dev)
+    import numpy as np
+    nb = int(lib.load().asrx_wconv_entry_bytes())
+    rec = np.zeros(len(keys), dtype=np.dtype([("src", "<u8"), ("dst", "<u8"), ("ld", "<i8"), ("rows", "<i4"),
+                                              ("cols", "<i4"), ("trans", "<i4"), ("pad", "<i4")]))
+    assert rec.dtype.itemsize == nb, (rec.dtype.itemsize, nb)
+    views, off = [], 0
+    for i, (k, W) in enumerate(zip(keys, srcs)):
+        rows, cols = W.shape
+        trans = k[3]
+        v = arena[off:off + W.numel()].view((cols, rows) if trans else (rows, cols))
+        rec[i] = (W.data_ptr(), v.data_ptr(), W.stride(0), rows, cols, int(trans), 0)
+        views.append(v)
+        off += W.numel()
+    table = torch.from_numpy(rec.view(np.uint8).copy()).to(dev)
+    return (keys, srcs, views, table, max(sizes))
+
+
+def clear_weight_cache(owner=None):
+    """Start of a step of `owner` (a Model): drop the per-step copies, then convert the weights this
+    owner's previous steps used in one launch (its plan is recorded during its first wide step)."""
+    global _OWNER
     _WCACHE.clear()
+    _BULK.clear()
+    capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+    if _OWNER is not None and _SEEN and _OWNER not in _PLANS and not capturing:
+        _PLANS[_OWNER] = _build_plan()  # the previous step of that owner recorded its weights
+        # (never built inside a graph capture: the table upload is a synchronous copy)
+    _SEEN.clear()
+    _OWNER = id(owner) if owner is not None else None
+    if _PLAN_OFF or _OWNER is None:
+        return
+    plan = _PLANS.get(_OWNER)
+    if plan is None:
+        if _OWNER not in _PLANS:
+            import weakref
+            weakref.finalize(owner, _PLANS.pop, _OWNER, None)
+        return
+    keys, srcs, views, table, mx = plan
+    if not all(t.data_ptr() == k[0] for t, k in zip(srcs, keys)):  # parameters were reallocated
+        del _PLANS[_OWNER]
+        return
+    lib.call("asrx_weights_to_bf16", lib.ptr(table), len(keys), mx, lib.stream())
+    _BULK.update(zip(keys, views))
 
 
 def weight_bf16(W, trans=False, cache=True):
     """bf16 N x K copy of a weight: W is (N, K) (trans=False) or (K, N) (trans=True).  Cached per
     stream: a copy converted on one stream is never read by another before it is complete."""
+    if cache and _BULK:
+        hit = _BULK.get(_bulk_key(W, trans))
+        if hit is not None:
+            return hit
     key = (W.data_ptr(), tuple(W.shape), tuple(W.stride()), bool(trans), W._version,
            torch.cuda.current_stream(W.device).cuda_stream if W.is_cuda else 0) if cache else None
     if key is not None and key in _WCACHE:
@@ -57,6 +131,8 @@ def weight_bf16(W, trans=False, cache=True):
         # the entry holds the source tensor too, so its address cannot be recycled for another
         # tensor (which would alias the key) while the entry lives
         _WCACHE[key] = (src, out)
+        if _OWNER is not None and _PLANS.get(_OWNER) is None and not _PLAN_OFF and _is_param_weight(src):
+            _SEEN.setdefault(_bulk_key(src, trans), (src,))
     return out
 
 

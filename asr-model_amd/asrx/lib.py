@@ -79,6 +79,8 @@ SIGNATURES = {
     "asrx_gemm_wn_rows": (_i32, [_p, _i64, _p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _f32, _f32, _i32, _i32, _p,
                                  _p, _p]),
     "asrx_row_tiles_max": (_i64, [_i64]),
+    "asrx_wconv_entry_bytes": (_i64, []),
+    "asrx_weights_to_bf16": (_i32, [_p, _i64, _i64, _p]),
     "asrx_row_tiles": (_i32, [_p, _i64, _i64, _i64, _p, _p, _p]),
     "asrx_msheath_ctrl_fwd3": (_i32, [_p, _p, _i64, _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p] + [_i64] * 5 + [_p] * 8),
     "asrx_mem_chunks": (_i64, [_i64]),

@@ -600,7 +600,7 @@ class Model(nn.Module):
         # how this step is batched decides how many gradient contributions each shared weight gets
         # (equal-length streams share one pass): asrx.dist.GradSync keys its event plans on it
         self.grad_signature = (self.training, tuple(s.shape[-1] for s in streams))
-        gemm_mod.clear_weight_cache()
+        gemm_mod.clear_weight_cache(self)
         noise = NoiseCtx(self.noise_seed, self.noise_step, self.training)
         if self.training:
             self.noise_step += 1
@@ -638,7 +638,7 @@ class Model(nn.Module):
                    aborc(waveform, pitch, spectrogram)]
         streams = [s.to(torch.float32).contiguous() for s in streams]
         B = first.shape[0]
-        gemm_mod.clear_weight_cache()
+        gemm_mod.clear_weight_cache(self)
         noise = NoiseCtx(self.noise_seed, self.noise_step, False)
         enc = self.enc.encode(streams, noise, B)
         kv = self.processor.audio_cache({"a": enc[0], "b": enc[1], "c": enc[2]}, noise, B)

@@ -731,6 +731,51 @@ extern "C" int asrx_weight_to_bf16(const float* src, unsigned short* dst, int64_
   ASRX_LAUNCHED("asrx_weight_to_bf16");
 }
 
+// Every GEMM weight of a step converted in ONE launch (asrx/gemm.py bulk plan): entry e converts
+// src (rows x cols, row stride ld) to bf16 dst (N x K contiguous; trans as weight_to_bf16).  A
+// workgroup walks one entry's elements; grid (ceil(max elements / 4096), entries).
+struct WConv {
+  const float* src;
+  unsigned short* dst;
+  int64_t ld;
+  int rows, cols, trans, pad;
+};
+
+namespace asrx {
+__global__ __launch_bounds__(256) void weights_to_bf16_kernel(const WConv* __restrict__ tab) {
+  const WConv e = tab[blockIdx.y];
+  const int64_t total = (int64_t)e.rows * e.cols;
+  const int64_t i0 = (int64_t)blockIdx.x * 4096;
+  if (i0 >= total) return;
+  const int64_t i1 = min<int64_t>(total, i0 + 4096);
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += 256) {
+    int64_t r, c, o;
+    if (!e.trans) {
+      r = i / e.cols;
+      c = i % e.cols;
+      o = r * e.cols + c;
+    } else {
+      c = i / e.rows;
+      r = i % e.rows;
+      o = c * e.rows + r;
+    }
+    e.dst[o] = __builtin_bit_cast(unsigned short, (__bf16)e.src[r * e.ld + c]);
+  }
+}
+}  // namespace asrx
+
+extern "C" int64_t asrx_wconv_entry_bytes(void) { return (int64_t)sizeof(WConv); }
+
+// tab: n device-resident WConv entries (asrx_wconv_entry_bytes() each); max_elems: the largest
+// rows * cols among them.
+extern "C" int asrx_weights_to_bf16(const void* tab, int64_t n, int64_t max_elems, hipStream_t stream) {
+  if (n == 0) return 0;
+  ASRX_REQUIRE(n < 65536, "asrx_weights_to_bf16: too many entries");
+  dim3 grid((unsigned)((max_elems + 4095) / 4096), (unsigned)n);
+  weights_to_bf16_kernel<<<grid, 256, 0, stream>>>((const WConv*)tab);
+  ASRX_LAUNCHED("asrx_weights_to_bf16");
+}
+
 // Y (M x N, ldc) = act(alpha * A W^T + beta * Y + bias); A fp32 (M x K, lda) or its k3 im2col
 // (conv: lda = channels, K = 3 * channels, segment length convF); W bf16 (N x K, ldw).  nj selects
 // the tile width 128 * nj (1..3).

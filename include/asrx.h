@@ -75,6 +75,11 @@ int asrx_gemm(int prec, const float* A, int64_t lda, int64_t sA, int a_kc, int c
  * asrx_weight_to_bf16; nj in 1..3 selects the 128*nj-wide output tile. ------------------------- */
 int asrx_weight_to_bf16(const float* src, unsigned short* dst, int64_t rows, int64_t cols, int64_t ld, int trans,
                         asrx_stream_t stream);
+/* every weight of a step in one launch: tab = n device-resident entries {const float* src; uint16*
+ * dst; int64 ld; int32 rows, cols, trans, pad} (asrx_wconv_entry_bytes() each), max_elems = the
+ * largest rows*cols */
+int64_t asrx_wconv_entry_bytes(void);
+int asrx_weights_to_bf16(const void* tab, int64_t n, int64_t max_elems, asrx_stream_t stream);
 /* AbbyNormal router in one GEMM pass (essentials.py:155-161): hpre = A W1^T + b1 (stored when
  * hpre != NULL) and logits = SiLU(hpre) W2^T (M x 3, without b2); W1 bf16 (N x K), N <= 384. */
 int asrx_gemm_wn_router(const float* A, int64_t lda, const unsigned short* W1, int64_t ldw, const float* b1,
