@@ -142,18 +142,39 @@ class prepare_datasets(torch.utils.data.Dataset):  # noqa: N801  (reference clas
         return extract_features(batch_input, tokenizer=self.tokenizer, **self.extract_args)
 
 
-def extract_features_batch(batches, tokenizer=None, spectrogram=False, waveform=False, hop_length=160,
-                           sample_rate=16000, mels=128, **unsupported):
+def extract_features_batch(batches, tokenizer=None, spectrogram=False, waveform=False, pitch=False, phase=False,
+                           hop_length=160, sample_rate=16000, mels=128, **unsupported):
     """extract_features (essentials.py:423-521) over a list of {"audio": path, "transcription"|"sentence"}
     dicts, with the audio of all of them loaded by one load_batch (one H2D copy, device normalisation).
     Returns the same per-clip feature dicts as extract_features (for DataCollator)."""
     from . import mel as _mel
 
-    if any(unsupported.get(k) for k in ("pitch", "harmonics", "aperiodics", "phase", "pitch_tokens")):
-        raise NotImplementedError("pitch / harmonics / aperiodics / phase / pitch_tokens: see extract_features")
+    if any(unsupported.get(k) for k in ("harmonics", "aperiodics", "pitch_tokens")):
+        raise NotImplementedError("harmonics / aperiodics / pitch_tokens: see extract_features")
     if hop_length != _mel.HOP or sample_rate != _mel.SAMPLE_RATE or mels != _mel.N_MELS:
         raise NotImplementedError("the HIP front end is built for hop 160, 16 kHz, 128 mels")
     wave, lengths, _ = load_batch([b["audio"] for b in batches])
+    pitch_of, phase_of = {}, {}
+    if pitch or phase:  # one batched GPU dio (+ stonemask) per group of equal-length clips
+        from .pitch import dio, stonemask
+
+        groups = {}
+        for i in range(len(batches)):
+            groups.setdefault(int(lengths[i]), []).append(i)
+        for n, idx in groups.items():
+            x = wave[idx, 0, :n].contiguous()
+            if pitch:  # dio(x, fs, frame_period) binds frame_period to f0_floor (asrx/pitch.py)
+                fp = hop_length / sample_rate * 1000
+                f0, t = dio(x, sample_rate, fp)
+                f0 = stonemask(x, f0, t, sample_rate)
+                for j, i in enumerate(idx):
+                    pitch_of[i] = f0[j].to(torch.float32).unsqueeze(0)
+            if phase:
+                f0, t = dio(x, sample_rate, frame_period=hop_length / sample_rate * 1000)
+                tframe = torch.mean(t[1:] - t[:-1])
+                ph = torch.remainder(torch.cumsum(2 * torch.pi * f0 * tframe, dim=-1), 2 * torch.pi)
+                for j, i in enumerate(idx):
+                    phase_of[i] = ph[j].to(torch.float32)
     out = []
     for i, b in enumerate(batches):
         n = int(lengths[i])
@@ -168,6 +189,6 @@ def extract_features_batch(batches, tokenizer=None, spectrogram=False, waveform=
                 _, w_tensor = _mel.logmel(audio.unsqueeze(0), layout="BMF", pool=True)
             else:
                 w_tensor = torch.nn.functional.adaptive_avg_pool1d(audio.view(1, 1, -1), target)[0]
-        out.append({"waveform": w_tensor, "spectrogram": s_tensor, "pitch_tokens": None, "pitch": None,
-                    "harmonic": None, "aperiodic": None, "labels": labels, "phase": None})
+        out.append({"waveform": w_tensor, "spectrogram": s_tensor, "pitch_tokens": None, "pitch": pitch_of.get(i),
+                    "harmonic": None, "aperiodic": None, "labels": labels, "phase": phase_of.get(i)})
     return out

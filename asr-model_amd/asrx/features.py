@@ -1,8 +1,9 @@
 """Drop-in replacements for the reference's feature boundary (essentials.py:423-574):
 `extract_features(batch, tokenizer, ...)` and `DataCollator(tokenizer)(features)`, same signatures,
-keys and layouts.  The spectrogram and waveform features run on the HIP log-mel kernel; the
-pyworld-based streams (pitch, harmonics, aperiodics, phase, pitch tokens) are out of scope
-(CPU vocoder analysis, pyworld is not installed) and raise.
+keys and layouts.  The spectrogram and waveform features run on the HIP log-mel kernel; pitch (dio +
+stonemask, essentials.py:451-455) and phase (dio, 458-467) on the GPU pitch kernels (asrx/pitch.py);
+harmonics / aperiodics (cheaptrick / d4c) and pitch tokens stay out of scope and
+raise.
 """
 from __future__ import annotations
 
@@ -88,16 +89,27 @@ def load_wave(audio, sample_rate=16000):
 def extract_features(batch, tokenizer=None, spectrogram=False, pitch=False, waveform=False, harmonics=False,
                      aperiodics=False, phase=False, hilbert=False, pitch_tokens=False, hop_length=160,
                      sample_rate=16000, mels=128):
-    if pitch or harmonics or aperiodics or phase or pitch_tokens:
-        raise NotImplementedError("pitch / harmonics / aperiodics / phase / pitch_tokens use pyworld "
-                                  "(essentials.py:360-467): out of scope, pass a precomputed f0 track instead")
+    if harmonics or aperiodics or pitch_tokens:
+        raise NotImplementedError("harmonics / aperiodics / pitch_tokens use pyworld's cheaptrick / d4c "
+                                  "(essentials.py:360-421): out of scope")
     if hop_length != _mel.HOP or sample_rate != _mel.SAMPLE_RATE or mels != _mel.N_MELS:
         raise NotImplementedError("the HIP front end is built for hop 160, 16 kHz, 128 mels (the reference's "
                                   "only configuration, model.py:733-744)")
     labels = tokenizer.encode(batch["transcription" if "transcription" in batch else "sentence"])
     audio, _ = load_wave(batch["audio"], sample_rate)
     audio = audio.to(_DEVICE, torch.float32).contiguous()
-    s_tensor = w_tensor = None
+    s_tensor = w_tensor = p_tensor = ph_tensor = None
+    if pitch:  # essentials.py:451-455, dio's third positional argument is f0_floor (asrx/pitch.py)
+        from .pitch import reference_pitch
+
+        p_tensor = reference_pitch(audio, sample_rate, hop_length).to(torch.float32).unsqueeze(0)
+    if phase:  # essentials.py:458-467: dio at the hop's frame period, phase of the integrated f0
+        from .pitch import dio
+
+        f0, t = dio(audio, sample_rate, frame_period=hop_length / sample_rate * 1000)
+        tframe = torch.mean(t[1:] - t[:-1])
+        phi = torch.cumsum(2 * torch.pi * f0 * tframe, dim=0)
+        ph_tensor = torch.remainder(phi, 2 * torch.pi).to(torch.float32)
     if spectrogram:
         s_tensor = _mel.logmel(audio.unsqueeze(0), layout="BMF")[0]  # (128, 1 + N // 160)
     if waveform:
@@ -111,8 +123,8 @@ def extract_features(batch, tokenizer=None, spectrogram=False, pitch=False, wave
         else:
             w_tensor = torch.nn.functional.interpolate(audio.view(1, 1, -1), size=target, mode="linear",
                                                        align_corners=False)[0]
-    return {"waveform": w_tensor, "spectrogram": s_tensor, "pitch_tokens": None, "pitch": None, "harmonic": None,
-            "aperiodic": None, "labels": labels, "phase": None}
+    return {"waveform": w_tensor, "spectrogram": s_tensor, "pitch_tokens": None, "pitch": p_tensor, "harmonic": None,
+            "aperiodic": None, "labels": labels, "phase": ph_tensor}
 
 
 @dataclass

@@ -402,6 +402,22 @@ int asrx_blend_bwd(const float* go, const float* d, const float* g, const float*
 int asrx_add_segments(const float* src, int64_t n, float* d0, float* d1, float* d2, int64_t nseg, asrx_stream_t stream);
 int asrx_cat3(const float* a, const float* b, const float* c, int64_t n, float* out, asrx_stream_t stream);
 
+
+/* ---- pitch: pyworld dio + stonemask as extract_features calls them
+ *      (essentials.py:451-455), float64 on the device over B equal-length float32 clips.  Filter
+ *      taps and the band table come from asrx/pitch.py (lc: 2c+1 low-cut taps; nut: the bands' Nuttall
+ *      windows, band i at nut_off[i] with nut_len[i] taps; nut_off / nut_len / bf0 are HOST arrays of
+ *      nb entries).  Workspace: mean (B), hp (B, N+1+2c), f (B, N+1), ev (B, 4, cap), cand / score
+ *      (B, nb, F), work (B, 3F); f0 (B, F) out, F = 1 + 1000 N / fs / fp.  stonemask refines f0 at the
+ *      uniform frame times j fp / 1000. */
+int asrx_pitch_dio(const float* x, int64_t ldx, int64_t B, int64_t N, double fs, double f0_floor, double f0_ceil,
+                   double fp, double allowed_range, const double* lc, int64_t c, const double* nut,
+                   const int64_t* nut_off, const int64_t* nut_len, const double* bf0, int64_t nb, double* mean,
+                   double* hp, double* f, double* ev, int64_t cap, double* cand, double* score, double* work,
+                   double* f0, int64_t F, asrx_stream_t stream);
+int asrx_pitch_stonemask(const float* x, int64_t ldx, int64_t B, int64_t N, double fs, const double* f0, double fp,
+                         int64_t F, double* out, asrx_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -26,9 +26,10 @@ def test_data_collator_padding():
 def test_extract_features_out_of_scope_streams():
     from asrx.features import extract_features
 
-    with pytest.raises(NotImplementedError):
-        extract_features({"audio": {"array": np.zeros(160), "sampling_rate": 16000}, "sentence": "a"},
-                         tokenizer=_Tok(), pitch=True)
+    for kw in ("harmonics", "aperiodics", "pitch_tokens"):  # cheaptrick / d4c streams stay out of scope
+        with pytest.raises(NotImplementedError):
+            extract_features({"audio": {"array": np.zeros(160), "sampling_rate": 16000}, "sentence": "a"},
+                             tokenizer=_Tok(), **{kw: True})
 
 
 @pytest.mark.gpu
