@@ -249,15 +249,30 @@ def _splitk_for(m_rows: int, tiles: int) -> int:
     return int(max(1, min(want, m_rows // 256)))
 
 
+def _wgrad(A, lda, x2, out, M, K, rows):
+    """out (M, K) += A^T x2 over `rows` rows (A: (rows, >= M) with row stride lda, x2: (rows, K))."""
+    tiles = ((M + 127) // 128) * ((K + 127) // 128)
+    sk = _splitk_for(rows, tiles)
+    ok4 = M % 4 == 0 and K % 4 == 0 and lda % 4 == 0 and A.data_ptr() % 16 == 0 and x2.data_ptr() % 16 == 0
+    # register-staged bf16 kernel with transpose reads (csrc/gemm_wg.hip): faster where the output
+    # has few tiles (D x D weights, 1.2-2.6x on the 8192-row text side); the wide 1152/1536 outputs at
+    # 192k rows stay on the split-K LDS-DMA kernel (5-12 % faster there, tools/wgrad_bench.py)
+    if prec.get() == prec.PREC_BF16 and ok4 and x2.stride(0) == K and (tiles <= 9 or rows <= 16384):
+        lib.require_gpu(A, x2, out)
+        e0 = probe.begin("gemm")
+        lib.call("asrx_wgrad_bf16", lib.ptr(A), lda, lib.ptr(x2), K, lib.ptr(out), out.stride(0), M, K, rows, sk,
+                 lib.stream())
+        probe.end("gemm", e0, 2.0 * M * K * rows, ("wgrad", M, K, rows, sk))
+        return out
+    gemm(A, x2, out, M=M, N=K, K=rows, lda=lda, ldb=K, ldc=K, a_kc=False, b_kc=False, beta=1.0, splitk=sk)
+    return out
+
+
 def wgrad_cols(dy, c0, n, x, out):
     """out (n, K) += dy[:, c0:c0+n]^T @ x for row-major dy (rows, ld) and x (rows, K): the weight
     gradient of one column block of a GEMM output, read in place (no copy of the block)."""
     rows, ld = dy.shape
-    K = x.shape[1]
-    tiles = ((n + 127) // 128) * ((K + 127) // 128)
-    gemm(dy[:, c0:], x, out, M=n, N=K, K=rows, lda=ld, ldb=K, ldc=K, a_kc=False, b_kc=False, beta=1.0,
-         splitk=_splitk_for(rows, tiles))
-    return out
+    return _wgrad(dy[:, c0:], ld, x, out, n, x.shape[1], rows)
 
 
 def linear_wgrad(dy, x, out=None, accumulate=False):
@@ -274,7 +289,4 @@ def linear_wgrad(dy, x, out=None, accumulate=False):
         out = torch.zeros(N, K, device=dy.device, dtype=torch.float32)
     elif not accumulate:
         out.zero_()
-    tiles = ((N + 127) // 128) * ((K + 127) // 128)
-    gemm(d2, x2, out, M=N, N=K, K=M, lda=N, ldb=K, ldc=K, a_kc=False, b_kc=False, beta=1.0,
-         splitk=_splitk_for(M, tiles))
-    return out
+    return _wgrad(d2, N, x2, out, N, K, M)

@@ -79,6 +79,7 @@ SIGNATURES = {
     "asrx_gemm_wn_rows": (_i32, [_p, _i64, _p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _f32, _f32, _i32, _i32, _p,
                                  _p, _p]),
     "asrx_row_tiles_max": (_i64, [_i64]),
+    "asrx_wgrad_bf16": (_i32, [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _p]),
     "asrx_pitch_dio": (_i32, [_p, _i64, _i64, _i64] + [ctypes.c_double] * 5 + [_p, _i64, _p, _p, _p, _p, _i64]
                        + [_p] * 4 + [_i64] + [_p] * 4 + [_i64, _p]),
     "asrx_pitch_stonemask": (_i32, [_p, _i64, _i64, _i64, ctypes.c_double, _p, ctypes.c_double, _i64, _p, _p]),

@@ -1,0 +1,181 @@
+// Weight-gradient GEMM, perf (bf16) mode: dW (M x N) += dY^T X summed over R rows, with dY (R x M)
+// and X (R x N) the row-major fp32 activations of a Linear's backward (the feature index is the
+// contiguous one on both sides).  Replaces gemm_kernel's split-K LDS-DMA path for these GEMMs
+// (asrx/gemm.py linear_wgrad / wgrad_cols): 288 launches and ~27 ms of the tiny step.
+//
+// Design (MI355X): the row (reduction) index is the MFMA k.  Operand slabs of 32 rows x 128
+// features travel global -> VGPR -> LDS as float4 loads issued two k-steps ahead (register staging,
+// as gemm_wr_kernel), are rounded to bf16 on the way and stored row-major ([32 k][128 features],
+// 256-B rows with an XOR chunk swizzle), and the MFMA fragments -- 8 consecutive k of one feature --
+// come back through ds_read_b64_tr_b16 (the hardware transpose read), so neither operand is ever
+// transposed in registers.  128 x 128 output tiles, 4 waves (2 x 2) of 64 x 64 on
+// v_mfma_f32_16x16x32_bf16, LDS double-buffered with one barrier per k-step.  The rows are split
+// over work items (split-K) dealt out XCD-contiguously; each item adds its partial tile into dW
+// with float atomics (dW holds the gradient accumulated so far: beta = 1 by construction).
+#include "common.h"
+
+namespace asrx {
+namespace wg {
+
+constexpr int TM = 128, TN = 128, TK = 32, NT = 256;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+
+__device__ __attribute__((aligned(16))) float zero16[4];
+
+struct Params {
+  const float* A;  // dY  (R x M, lda)
+  const float* B;  // X   (R x N, ldb)
+  float* C;        // dW  (M x N, ldc), accumulated
+  int64_t lda, ldb, ldc;
+  int M, N;
+  int64_t R, kchunk;
+  int splitk;
+};
+
+// byte offset of 16-B chunk ch (8 features) of k-row `row` in a [32][128] bf16 image
+__device__ __forceinline__ int off(int row, int ch) { return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3))); }
+
+struct Stage {
+  float4 a[4], b[4];  // rows (t >> 5) + 8 i, features 4 (t & 31) .. +3
+};
+
+__device__ __forceinline__ void load(const Params& p, Stage& st, int64_t r0, int64_t rend, int m0, int n0) {
+  const int t = threadIdx.x;
+  const int c = 4 * (t & 31);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t r = r0 + (t >> 5) + 8 * i;
+    const bool okr = r < rend;
+    // unconditional loads from clamped addresses (a branch would make the compiler drain vmcnt)
+    st.a[i] = *reinterpret_cast<const float4*>((okr && m0 + c < p.M) ? (const void*)(p.A + r * p.lda + m0 + c)
+                                                                     : (const void*)zero16);
+    st.b[i] = *reinterpret_cast<const float4*>((okr && n0 + c < p.N) ? (const void*)(p.B + r * p.ldb + n0 + c)
+                                                                     : (const void*)zero16);
+  }
+}
+
+__device__ __forceinline__ void store(const Stage& st, char* Ai, char* Bi) {
+  const int t = threadIdx.x;
+  const int c = 4 * (t & 31);
+  const int ch = c >> 3, hb = (c >> 2) & 1;
+  typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (t >> 5) + 8 * i;
+    bf16x4 ha, hb4;
+    ha[0] = (__bf16)st.a[i].x; ha[1] = (__bf16)st.a[i].y; ha[2] = (__bf16)st.a[i].z; ha[3] = (__bf16)st.a[i].w;
+    hb4[0] = (__bf16)st.b[i].x; hb4[1] = (__bf16)st.b[i].y; hb4[2] = (__bf16)st.b[i].z; hb4[3] = (__bf16)st.b[i].w;
+    *reinterpret_cast<bf16x4*>(Ai + off(row, ch) + 8 * hb) = ha;
+    *reinterpret_cast<bf16x4*>(Bi + off(row, ch) + 8 * hb) = hb4;
+  }
+}
+
+// MFMA 16x16x32 operand of features c0 .. c0+15: lane l gets feature c0 + (l & 15), k = 8 (l >> 4) .. +7
+__device__ __forceinline__ bf16x8 frag(const char* img, int c0, int lane) {
+  const int g = lane >> 4, gi = lane & 15, q = gi >> 2, p = gi & 3;
+  const int col = c0 + 4 * p;
+  const int ch = col >> 3, hb = (col >> 2) & 1;
+  const v4i16 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(img + off(8 * g + q, ch) + 8 * hb));
+  const v4i16 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(img + off(8 * g + 4 + q, ch) + 8 * hb));
+  typedef short v8i16 __attribute__((ext_vector_type(8)));
+  const v8i16 a8 = {t1[0], t1[1], t1[2], t1[3], t2[0], t2[1], t2[2], t2[3]};
+  return __builtin_bit_cast(bf16x8, a8);
+}
+
+// work item -> XCD-contiguous runs (blocks b and b+8 share an XCD): the output tiles of one row
+// slice run on one XCD together and share its L2
+__device__ __forceinline__ int xcd_item(int bid, int nblk) {
+  const int xcd = bid & 7, q = nblk >> 3, r = nblk & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+__global__ __launch_bounds__(NT, 2) void wgrad_wr_kernel(Params p) {
+  __shared__ __attribute__((aligned(16))) char Ai[2][TK * TM * 2];
+  __shared__ __attribute__((aligned(16))) char Bi[2][TK * TN * 2];
+  const int nN = (p.N + TN - 1) / TN, nM = (p.M + TM - 1) / TM;
+  const int ntile = nM * nN;
+  const int item = xcd_item(blockIdx.x, gridDim.x);
+  const int split = item / ntile, tile = item % ntile;
+  const int m0 = (tile / nN) * TM, n0 = (tile % nN) * TN;
+  const int64_t rb = (int64_t)split * p.kchunk, re = min<int64_t>(p.R, rb + p.kchunk);
+  const int nk = rb < re ? (int)((re - rb + TK - 1) / TK) : 0;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  Stage s0, s1;
+  load(p, s0, rb, re, m0, n0);
+  load(p, s1, rb + TK, re, m0, n0);
+  store(s0, Ai[0], Bi[0]);
+  __syncthreads();
+
+  auto kstep = [&](int s, Stage& cur, const Stage& nxt) __attribute__((always_inline)) {
+    load(p, cur, rb + (int64_t)(s + 2) * TK, re, m0, n0);  // past the end: zero page, counts stay uniform
+    const char* At = Ai[s & 1];
+    const char* Bt = Bi[s & 1];
+    bf16x8 a[4], b[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) a[mt] = frag(At, wm * 64 + mt * 16, lane);
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) b[nt] = frag(Bt, wn * 64 + nt * 16, lane);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt], b[nt], acc[mt][nt], 0, 0, 0);
+    if (s + 1 < nk) store(nxt, Ai[(s + 1) & 1], Bi[(s + 1) & 1]);
+    __syncthreads();
+  };
+  for (int s = 0; s < nk; s += 2) {
+    kstep(s, s0, s1);
+    if (s + 1 < nk) kstep(s + 1, s1, s0);
+  }
+
+  // D map of the 16x16 MFMA: n = lane & 15, m = 4 (lane >> 4) + r
+  const int ln = lane & 15, lm = 4 * (lane >> 4);
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int n = n0 + wn * 64 + nt * 16 + ln;
+      if (n >= p.N) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * 64 + mt * 16 + lm + r;
+        if (m < p.M && nk > 0) atomicAdd(p.C + (int64_t)m * p.ldc + n, acc[mt][nt][r]);
+      }
+    }
+}
+
+}  // namespace wg
+}  // namespace asrx
+
+using namespace asrx;
+
+// dW (M x N, ldc) += dY^T X over R rows; dY (R x M, lda), X (R x N, ldb) fp32 row-major; the rows
+// split over `splitk` work items (bf16 operands, fp32 accumulate).  M, N, lda, ldb multiples of 4,
+// 16-byte aligned operands.
+extern "C" int asrx_wgrad_bf16(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
+                               int64_t M, int64_t N, int64_t R, int64_t splitk, hipStream_t stream) {
+  ASRX_REQUIRE(M > 0 && N > 0 && R >= 0, "asrx_wgrad_bf16: empty problem");
+  ASRX_REQUIRE(M % 4 == 0 && N % 4 == 0 && lda % 4 == 0 && ldb % 4 == 0, "asrx_wgrad_bf16: M, N, lda, ldb %% 4 required");
+  ASRX_REQUIRE((((uintptr_t)A | (uintptr_t)B) & 15) == 0, "asrx_wgrad_bf16: operands must be 16-byte aligned");
+  if (R == 0) return 0;
+  if (splitk < 1) splitk = 1;
+  int64_t kchunk = (R + splitk - 1) / splitk;
+  kchunk = (kchunk + wg::TK - 1) / wg::TK * wg::TK;
+  splitk = (R + kchunk - 1) / kchunk;
+  wg::Params p{A, B, C, lda, ldb, ldc, (int)M, (int)N, R, kchunk, (int)splitk};
+  const int64_t items = ((M + wg::TM - 1) / wg::TM) * ((N + wg::TN - 1) / wg::TN) * splitk;
+  ASRX_REQUIRE(items < (1LL << 31), "asrx_wgrad_bf16: too many work items");
+  wg::wgrad_wr_kernel<<<(unsigned)items, wg::NT, 0, stream>>>(p);
+  ASRX_LAUNCHED("asrx_wgrad_bf16");
+}

@@ -91,6 +91,11 @@ int asrx_gemm_wn(const float* A, int64_t lda, int conv, int64_t convF, int64_t c
 /* asrx_gemm_wn on the BM(=128)-row tiles listed on the device (mtiles[0 .. *n_mtiles)); other rows of
  * C are not written.  asrx_row_tiles lists the tiles holding rows of samples at MSheath layer
  * `layer` (next_i[b] == layer, L rows per sample), at most asrx_row_tiles_max(M) entries. */
+/* weight gradient in perf mode: dW (M x N, ldc) += dY^T X over R rows (dY: R x M, lda; X: R x N, ldb;
+ * fp32 row-major, rounded to bf16 for the MFMA, fp32 accumulate, split over `splitk` row slices
+ * with float atomics).  M, N, lda, ldb multiples of 4; 16-byte aligned operands. */
+int asrx_wgrad_bf16(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M,
+                    int64_t N, int64_t R, int64_t splitk, asrx_stream_t stream);
 int asrx_gemm_wn_rows(const float* A, int64_t lda, const unsigned short* W, int64_t ldw, float* C, int64_t ldc,
                       const float* bias, float* Z, int64_t M, int64_t N, int64_t K, float alpha, float beta, int act,
                       int nj, const int* mtiles, const int* n_mtiles, asrx_stream_t stream);

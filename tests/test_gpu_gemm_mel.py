@@ -294,3 +294,28 @@ def test_wide_gemm_row_tiles(cuda, L, N):
     rows = rows.to(cuda)
     assert torch.equal(y[rows], full[rows])
     assert bool((y[~rows] == 12345.0).all())
+
+
+@pytest.mark.parametrize("R,M,N,ld_extra", [(8192, 384, 384, 0), (777, 64, 200, 0), (30000, 1152, 384, 0),
+                                            (5000, 192, 384, 64), (33, 4, 8, 0)])
+def test_wgrad_bf16_register_staged(cuda, R, M, N, ld_extra):
+    """asrx_wgrad_bf16 (csrc/gemm_wg.hip): dW += dY^T X over R rows, bf16 operands / fp32 accumulate,
+    against float64 on the same bf16-rounded operands; accumulates into the existing dW; a column block
+    of a wider dY (row stride > M) as wgrad_cols reads it."""
+    from asrx import gemm as G, prec
+
+    g = torch.Generator().manual_seed(R + M)
+    dyw = torch.randn(R, M + ld_extra, generator=g)
+    x = torch.randn(R, N, generator=g)
+    w0 = torch.randn(M, N, generator=g)
+    out = w0.clone().to(cuda)
+    with prec.precision("bf16"):
+        if ld_extra:
+            G.wgrad_cols(dyw.to(cuda), ld_extra, M, x.to(cuda), out)
+            dy = dyw[:, ld_extra:]
+        else:
+            G.linear_wgrad(dyw.to(cuda), x.to(cuda), out=out, accumulate=True)
+            dy = dyw
+    ref = w0.double() + _bf(dy).t() @ _bf(x)
+    err = float((out.cpu().double() - ref).abs().max() / (_bf(dy).t().abs() @ _bf(x).abs()).max())
+    assert err < 1e-5, err
