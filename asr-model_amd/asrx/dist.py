@@ -53,9 +53,13 @@ class _Bucket:
 
 
 class GradSync:
-    def __init__(self, model: torch.nn.Module, bucket_mb: float = 64.0, group=None, signature=None):
+    def __init__(self, model: torch.nn.Module, bucket_mb: float = 64.0, group=None, signature=None,
+                 reduce_single: bool = False):
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        # reduce_single: run the bucket all-reduces even in a 1-rank group (exercises the RCCL launch,
+        # comm-stream overlap and join on a one-GPU box; the sum over one rank is the identity)
+        self.active = self.world > 1 or (reduce_single and dist.is_initialized())
         self.params = [p for p in model.parameters() if p.requires_grad]
         self.bucket_bytes = int(bucket_mb * 1024 * 1024)
         self.buckets: list[_Bucket] | None = None
@@ -123,7 +127,7 @@ class GradSync:
         self._started = True
         self._sig = self._signature()
         plan = self.bucket_plans.get(self._sig)
-        self._overlap = self.buckets is not None and plan is not None and self.world > 1
+        self._overlap = self.buckets is not None and plan is not None and self.active
         if self._overlap:
             for b, n in zip(self.buckets, plan):
                 b.expected = b.pending = n
@@ -175,7 +179,7 @@ class GradSync:
                 self.plans[self._sig] = {i: max(n, self._seen.get(i, 0)) for i, n in plan.items()} | \
                     {i: n for i, n in self._seen.items() if i not in plan}
                 self._learn(self._sig)
-        if self.world > 1:
+        if self.active:
             for b in self.buckets:
                 if not b.launched:
                     self._launch(b)

@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--same-device", action="store_true", help="every rank on cuda:0 (rehearsal only)")
     ap.add_argument("--eager", action="store_true", help="launch every kernel from Python instead of replaying "
                     "the captured HIP graph of the step")
+    ap.add_argument("--dist-single", action="store_true", help="N=1 through the N>1 code path: a 1-rank "
+                    "process group (RCCL) and GradSync's bucket all-reduces on the comm stream (a rehearsal of "
+                    "the multi-GPU step on a one-GPU box; never the headline)")
     ap.add_argument("--no-dead-block-line", action="store_true", help="skip the extra measurement with the "
                     "reference's dead decoder blocks eliminated (reported beside, never as, the headline)")
     return ap.parse_args()
@@ -87,6 +90,16 @@ def cpu_baseline(model, cfg_name, budget_s=10.0, max_clips=3):
                       f"batch 1, {t_total:.1f} s of CPU time"}
 
 
+def free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
 def self_launch(n):
     """`bench.py --gpus N` without a launcher: start N ranks with torch.distributed.run (one process per
     GPU, rendezvous on 127.0.0.1) as a child and exit with its status.  Runs before anything touches
@@ -116,7 +129,10 @@ def main():
         local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    distributed = world > 1 or args.dist_single
+    if args.dist_single and world == 1 and "MASTER_ADDR" not in os.environ:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), RANK="0", WORLD_SIZE="1")
+    if distributed:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -132,9 +148,9 @@ def main():
     cfg = CONFIGS[args.config]
     torch.manual_seed(0)
     model = Model(cfg).to(dev).train()
-    if world > 1:
+    if distributed:
         broadcast_parameters(model)
-    gsync = GradSync(model)
+    gsync = GradSync(model, reduce_single=args.dist_single)
     model.set_noise(seed=0, step=rank * 1_000_000)
 
     B = args.batch
@@ -154,7 +170,7 @@ def main():
         gsync.finish()
         return out["loss"]
 
-    use_graph = not args.eager and world == 1
+    use_graph = not args.eager and not distributed
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):  # warmup off the default stream (graph-capture requirement)
@@ -171,7 +187,7 @@ def main():
         with torch.cuda.graph(graph):
             loss = step()
         torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -185,7 +201,7 @@ def main():
         else:
             loss = step()
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if graph is not None:
@@ -220,7 +236,7 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         opt_ms = e0.elapsed_time(e1) / 5
-    if world > 1:
+    if distributed:
         # replicas must hold identical averaged gradients after the all-reduce
         gsum = torch.stack([p.grad.double().norm() for p in model.parameters() if p.grad is not None]).sum()
         lo, hi = gsum.clone(), gsum.clone()
@@ -253,7 +269,9 @@ def main():
                    "model": args.config, "global_batch": world * B, "seq_len": 3001, "text_len": args.text_len,
                    "parallelism": f"dp{world}"},
         "per_gpu": round(value / world, 3),
-        **({"grad_sync_rel_spread": grad_spread} if world > 1 else {}),
+        **({"grad_sync_rel_spread": grad_spread} if distributed else {}),
+        **({"dist_single": "1-rank RCCL group through the N>1 path (eager, bucket all-reduces on the comm "
+                           "stream); a rehearsal, not the headline"} if args.dist_single else {}),
         "loss": loss_v,
     }
     if recs is not None:
@@ -312,7 +330,7 @@ def main():
     result["launch"] = "hip-graph replay" if graph is not None else "eager"
     if recs is not None:
         result["probe"] = "per-kernel HIP events on one eager pass of the same step after the timed steps"
-    if not args.no_dead_block_line and world == 1:
+    if not args.no_dead_block_line and not distributed:
         # SURVEY.md §7 "Only the last block reaches the output": processor.forward computes blocks
         # 0..L-2 and discards them.  The headline keeps that work (faithful); this line measures the
         # same step with them skipped (output-identical under keyed noise), labelled as such.
@@ -346,7 +364,7 @@ def main():
                     "output-identical, NOT the headline"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(model, args.config)
-    if world > 1:
+    if distributed:
         dist.barrier()
         dist.destroy_process_group()
     if rank == 0:
