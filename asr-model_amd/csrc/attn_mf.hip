@@ -132,8 +132,19 @@ __device__ __forceinline__ void store_rowT(float* yr, const f32x16 (&acc)[HD / 3
     }
 }
 
-template <int HD>
-__global__ __launch_bounds__(NTHR, 1) void attn_fwd_mf_kernel(const float* __restrict__ q, const float* __restrict__ k,
+// logical workgroup of hardware workgroup `bid` of G: consecutive logical ids on one XCD (hardware
+// ids are dealt to the 8 XCDs round-robin), so the query blocks of one (b, h) share that XCD's L2
+// copy of their K / V rows
+__device__ __forceinline__ int64_t xcd_logical(int64_t bid, int64_t G) {
+  const int64_t per = G / 8, rem = G % 8, x = bid % 8, q = bid / 8;
+  return (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + q;
+}
+
+// WPE: waves per SIMD the register budget is sized for (1: one 8-wave workgroup per CU; 4: two).
+// XCD: 1-D grid remapped with xcd_logical.  PRIO: MFMA issue at raised wave priority (s_setprio),
+// so a SIMD's other wave fills the matrix-core gaps with its softmax VALU work.
+template <int HD, int WPE = 1, bool XCD = false, bool PRIO = false>
+__global__ __launch_bounds__(NTHR, WPE) void attn_fwd_mf_kernel(const float* __restrict__ q, const float* __restrict__ k,
                                                               const float* __restrict__ v, float* __restrict__ o,
                                                               float* __restrict__ lse, AttnStridesMF sq,
                                                               AttnStridesMF sk, AttnStridesMF sv, AttnStridesMF so,
@@ -143,8 +154,19 @@ __global__ __launch_bounds__(NTHR, 1) void attn_fwd_mf_kernel(const float* __res
   __shared__ __attribute__((aligned(16))) unsigned short Ks[2][NH * HALF];
   __shared__ __attribute__((aligned(16))) unsigned short Vs[2][NH * HALF];
 
-  const int b = blockIdx.z, h = blockIdx.y;
-  const int64_t q0 = (int64_t)blockIdx.x * QB;
+  int b, h;
+  int64_t q0;
+  if (XCD) {
+    const int64_t nqb = (Lq + QB - 1) / QB;
+    const int64_t G = (int64_t)gridDim.x, L = xcd_logical(blockIdx.x, G);
+    q0 = (L % nqb) * QB;
+    h = (int)((L / nqb) % H);
+    b = (int)(L / (nqb * H));
+  } else {
+    b = blockIdx.z;
+    h = blockIdx.y;
+    q0 = (int64_t)blockIdx.x * QB;
+  }
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int j = lane & 31, hi = lane >> 5;
   const int64_t qi = q0 + wid * 32 + j;  // this lane's query row
@@ -194,12 +216,14 @@ __global__ __launch_bounds__(NTHR, 1) void attn_fwd_mf_kernel(const float* __res
 
     // ---- S^T = K Q^T : two 32-key blocks
     f32x16 sacc[2];
+    if (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kb2 = 0; kb2 < 2; ++kb2) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) sacc[kb2][r] = 0.f;
       dot_rows<HD>(sacc[kb2], Kt, 32 * kb2 + j, hi, qf);
     }
+    if (PRIO) __builtin_amdgcn_s_setprio(0);
 
     // ---- mask + online softmax (lane = query j, keys crow(r, hi) of each block)
     const bool need_mask = (k0 + KT > Lk) || (causal && k0 + KT - 1 > q0 + wid * 32);
@@ -248,6 +272,7 @@ __global__ __launch_bounds__(NTHR, 1) void attn_fwd_mf_kernel(const float* __res
     l += lsum;
 
     // ---- O^T += V^T P^T
+    if (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kb2 = 0; kb2 < 2; ++kb2)
 #pragma unroll
@@ -256,6 +281,7 @@ __global__ __launch_bounds__(NTHR, 1) void attn_fwd_mf_kernel(const float* __res
         for (int d = 0; d < HD / 32; ++d)
           oacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Vt + (d >> 1) * HALF, lane, kb2, s2, d & 1),
                                                             pb[kb2][s2], oacc[d], 0, 0, 0);
+    if (PRIO) __builtin_amdgcn_s_setprio(0);
 
     if (t + 1 < ntiles) {  // every wave finished reading buf^1 (tile t-1) before the last barrier
 #pragma unroll
@@ -311,8 +337,10 @@ __global__ __launch_bounds__(BwdCfg<HD>::NT, 1) void attn_bwd_dkdv_mf_kernel(
   __shared__ __attribute__((aligned(16))) unsigned short Dr[2][NH * HALF], Dt[2][NH * HALF];
   __shared__ __attribute__((aligned(16))) float2 LD[2][BQT];  // (lse * log2e or +inf past Lq, Delta)
 
-  const int b = blockIdx.z, h = blockIdx.y;
-  const int64_t k0 = (int64_t)blockIdx.x * (32 * C::NW);
+  // 1-D grid, key blocks of one (b, h) contiguous on one XCD (xcd_logical)
+  const int64_t nkb = (Lk + 32 * C::NW - 1) / (32 * C::NW), L = xcd_logical(blockIdx.x, gridDim.x);
+  const int b = (int)(L / (nkb * H)), h = (int)((L / nkb) % H);
+  const int64_t k0 = (L % nkb) * (32 * C::NW);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int j = lane & 31, hi = lane >> 5;
   const int64_t key = k0 + wid * 32 + j;  // this lane's key
@@ -440,8 +468,10 @@ __global__ __launch_bounds__(BwdCfg<HD>::NT, 1) void attn_bwd_dq_mf_kernel(
   constexpr int NH = HD / 64;
   __shared__ __attribute__((aligned(16))) unsigned short Kr[2][NH * HALF], Kt2[2][NH * HALF], Vr[2][NH * HALF];
 
-  const int b = blockIdx.z, h = blockIdx.y;
-  const int64_t q0 = (int64_t)blockIdx.x * (32 * C::NW);
+  // 1-D grid, query blocks of one (b, h) contiguous on one XCD (xcd_logical)
+  const int64_t nqb = (Lq + 32 * C::NW - 1) / (32 * C::NW), L = xcd_logical(blockIdx.x, gridDim.x);
+  const int b = (int)(L / (nqb * H)), h = (int)((L / nqb) % H);
+  const int64_t q0 = (L % nqb) * (32 * C::NW);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int j = lane & 31, hi = lane >> 5;
   const int64_t qi = q0 + wid * 32 + j;  // this lane's query row
@@ -548,9 +578,16 @@ int attn_fwd_mf(const float* q, const int64_t* sq, const float* k, const int64_t
                 int64_t Lk, int64_t hd, int causal, float scale, hipStream_t stream) {
   dim3 g((unsigned)((Lq + amf::QB - 1) / amf::QB), (unsigned)H, (unsigned)B);
   AttnStridesMF Sq{sq[0], sq[1], sq[2]}, Sk{sk[0], sk[1], sk[2]}, Sv{sv[0], sv[1], sv[2]}, So{so[0], so[1], so[2]};
-  if (hd == 64)
-    amf::attn_fwd_mf_kernel<64><<<g, amf::NTHR, 0, stream>>>(q, k, v, o, lse, Sq, Sk, Sv, So, H, Lq, Lk, causal, scale);
-  else
+  // query blocks of one (b, h) on one XCD when there are several (3.6 % at 3001 x 3001, H = 6,
+  // B = 64; profiles/r02_attn_fwd_variants.txt, which also records the rejected 4-waves-per-SIMD
+  // and s_setprio variants)
+  if (hd == 64) {
+    if (g.x > 1)
+      amf::attn_fwd_mf_kernel<64, 1, true><<<dim3((unsigned)((int64_t)g.x * g.y * g.z)), amf::NTHR, 0, stream>>>(
+          q, k, v, o, lse, Sq, Sk, Sv, So, H, Lq, Lk, causal, scale);
+    else
+      amf::attn_fwd_mf_kernel<64><<<g, amf::NTHR, 0, stream>>>(q, k, v, o, lse, Sq, Sk, Sv, So, H, Lq, Lk, causal, scale);
+  } else
     amf::attn_fwd_mf_kernel<128><<<g, amf::NTHR, 0, stream>>>(q, k, v, o, lse, Sq, Sk, Sv, So, H, Lq, Lk, causal, scale);
   return 0;
 }
@@ -562,10 +599,10 @@ static void attn_bwd_mf_t(const float* q, AttnStridesMF Sq, const float* k, Attn
                           int64_t B, int64_t H, int64_t Lq, int64_t Lk, int causal, float scale, hipStream_t stream) {
   typedef amf::BwdCfg<HD> C;
   const int64_t rows_per_wg = 32 * C::NW;
-  dim3 gk((unsigned)((Lk + rows_per_wg - 1) / rows_per_wg), (unsigned)H, (unsigned)B);
+  dim3 gk((unsigned)(((Lk + rows_per_wg - 1) / rows_per_wg) * H * B));
   amf::attn_bwd_dkdv_mf_kernel<HD><<<gk, C::NT, 0, stream>>>(q, k, v, dO, lse, delta, dk, dv, Sq, Sk, Sv, Sd, Sdk, Sdv,
                                                              H, Lq, Lk, causal, scale);
-  dim3 gq((unsigned)((Lq + rows_per_wg - 1) / rows_per_wg), (unsigned)H, (unsigned)B);
+  dim3 gq((unsigned)(((Lq + rows_per_wg - 1) / rows_per_wg) * H * B));
   amf::attn_bwd_dq_mf_kernel<HD><<<gq, C::NT, 0, stream>>>(q, k, v, dO, lse, delta, dq, Sq, Sk, Sv, Sd, Sdq, H, Lq, Lk,
                                                            causal, scale);
 }

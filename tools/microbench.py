@@ -182,6 +182,26 @@ def attn_bench():
         del q, k, v
 
 
+def attnf_bench():
+    """bf16 attention forward only (ASRX_ATTN_VARIANT picks the kernel variant), with its error vs fp32 SDPA."""
+    from asrx import ops, prec
+
+    dev = torch.device("cuda:0")
+    v = os.environ.get("ASRX_ATTN_VARIANT", "0")
+    for (B, H, Lq, Lk, causal) in [(64, 6, 3001, 3001, False), (32, 6, 256, 3001, False)]:
+        g = torch.Generator(device=dev).manual_seed(0)
+        q, k, vv = (torch.randn(B, L, H, 64, device=dev, generator=g) for L in (Lq, Lk, Lk))
+        fl = 4.0 * B * H * Lq * Lk * 64
+        with prec.precision("bf16"):
+            t = timeit(lambda: ops.attention(q, k, vv, causal), iters=10)
+            y = ops.attention(q, k, vv, causal)
+        ref = torch.nn.functional.scaled_dot_product_attention(q[:2].transpose(1, 2), k[:2].transpose(1, 2),
+                                                               vv[:2].transpose(1, 2)).transpose(1, 2)
+        err = float((y[:2] - ref).abs().max() / ref.abs().max())
+        print(f"variant {v} attn fwd B={B} H={H} Lq={Lq} Lk={Lk}: {t*1e6:.1f} us {fl/t/1e12:.1f} TF/s "
+              f"err {err:.3e} sum {float(y.double().sum()):.6f}", flush=True)
+
+
 if __name__ == "__main__":
     what = sys.argv[1:] or ["gemm", "mel"]
     if "mel" in what:
@@ -192,6 +212,8 @@ if __name__ == "__main__":
         rowops_bench()
     if "attn" in what:
         attn_bench()
+    if "attnf" in what:
+        attnf_bench()
     if "abby" in what:
         abby_bench()
     if "norm" in what:
