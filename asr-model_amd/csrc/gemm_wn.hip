@@ -447,6 +447,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wn_kernel(Params p, int ntiles) 
 #ifndef WR_DEPTH
 #define WR_DEPTH 3  // register stages in flight (k-steps of prefetch)
 #endif
+// DEP (template): stages for launches of at most one workgroup per CU, where nothing else hides a
+// workgroup's load latency -- the text side's 8192-row GEMMs (0 = WR_DEPTH)
 
 template <int NJ>
 struct WrStage {
@@ -505,7 +507,7 @@ __device__ __forceinline__ void wr_store(const WrStage<NJ>& st, char* At, char* 
   }
 }
 
-template <int NJ, bool CONV, bool RT>
+template <int NJ, bool CONV, bool RT, int DEP = 0>
 __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) {  // ntiles: all tiles
   typedef Cfg<NJ> CF;
   constexpr int BN = CF::BN, NT = 2 * NJ, BNR = CF::BNR;
@@ -568,22 +570,16 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
 
   // stage register sets are named variables (an array, even constant-indexed after unrolling,
   // ends up in scratch)
-  WrStage<NJ> st0, st1, st2;
-#if WR_DEPTH >= 4
-  WrStage<NJ> st3;
-#endif
-#if WR_DEPTH >= 5
-  WrStage<NJ> st4;
-#endif
+  constexpr int DEPTH = DEP ? DEP : WR_DEPTH;
+  static_assert(DEPTH >= 3 && DEPTH <= 5, "stage sets are written out for depths 3..5");
+  WrStage<NJ> st0, st1, st2, st3, st4;  // st3 / st4 unused (eliminated) below depth 4 / 5
   if (S > 0) load(0, st0);
   if (S > 1) load(1, st1);
   if (S > 2) load(2, st2);
-#if WR_DEPTH >= 4
-  if (S > 3) load(3, st3);
-#endif
-#if WR_DEPTH >= 5
-  if (S > 4) load(4, st4);
-#endif
+  if constexpr (DEPTH >= 4)
+    if (S > 3) load(3, st3);
+  if constexpr (DEPTH >= 5)
+    if (S > 4) load(4, st4);
   if (S > 0) store(0, st0);
   __syncthreads();
 
@@ -593,7 +589,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
     // unconditional: past the last step the A rows fall beyond M and read the zero page, so the
     // number of loads in flight is the same on every path and the compiler's vmcnt waits stay
     // counted (a conditional load here would force vmcnt(0) at every later wait)
-    load(s + WR_DEPTH, cur);
+    load(s + DEPTH, cur);
     const char* At = a_img[s & 1];
     const char* Bt = b_img[s & 1];
     bf16x8 a[4], b[NT];
@@ -640,24 +636,23 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
     __syncthreads();
   };
 
-  static_assert(WR_DEPTH >= 3 && WR_DEPTH <= 5, "stage sets are written out for depths 3..5");
-  for (int s = 0; s < S; s += WR_DEPTH) {
-#if WR_DEPTH == 3
-    kstep(s, st0, st1);
-    if (s + 1 < S) kstep(s + 1, st1, st2);
-    if (s + 2 < S) kstep(s + 2, st2, st0);
-#elif WR_DEPTH == 4
-    kstep(s, st0, st1);
-    if (s + 1 < S) kstep(s + 1, st1, st2);
-    if (s + 2 < S) kstep(s + 2, st2, st3);
-    if (s + 3 < S) kstep(s + 3, st3, st0);
-#else
-    kstep(s, st0, st1);
-    if (s + 1 < S) kstep(s + 1, st1, st2);
-    if (s + 2 < S) kstep(s + 2, st2, st3);
-    if (s + 3 < S) kstep(s + 3, st3, st4);
-    if (s + 4 < S) kstep(s + 4, st4, st0);
-#endif
+  for (int s = 0; s < S; s += DEPTH) {
+    if constexpr (DEPTH == 3) {
+      kstep(s, st0, st1);
+      if (s + 1 < S) kstep(s + 1, st1, st2);
+      if (s + 2 < S) kstep(s + 2, st2, st0);
+    } else if constexpr (DEPTH == 4) {
+      kstep(s, st0, st1);
+      if (s + 1 < S) kstep(s + 1, st1, st2);
+      if (s + 2 < S) kstep(s + 2, st2, st3);
+      if (s + 3 < S) kstep(s + 3, st3, st0);
+    } else {
+      kstep(s, st0, st1);
+      if (s + 1 < S) kstep(s + 1, st1, st2);
+      if (s + 2 < S) kstep(s + 2, st2, st3);
+      if (s + 3 < S) kstep(s + 3, st3, st4);
+      if (s + 4 < S) kstep(s + 4, st4, st0);
+    }
   }
 }
 
@@ -674,7 +669,10 @@ static void launch_wr(const Params& p, hipStream_t s) {
   }
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + Cfg<NJ>::BN - 1) / Cfg<NJ>::BN);
   const int grid = std::min(tiles, resident);
-  gemm_wr_kernel<NJ, CONV, RT><<<grid, NTHR, 0, s>>>(p, tiles);
+  if (NJ == 1 && !p.mtiles && tiles <= 256)  // one workgroup per CU at most: a deeper register pipeline
+    gemm_wr_kernel<NJ, CONV, RT, 5><<<grid, NTHR, 0, s>>>(p, tiles);
+  else
+    gemm_wr_kernel<NJ, CONV, RT><<<grid, NTHR, 0, s>>>(p, tiles);
 }
 
 // fp32 (rows x cols, row stride ld) -> bf16 N x K contiguous.  trans == 0: N = rows, K = cols;

@@ -34,16 +34,39 @@ __global__ __launch_bounds__(256) void msheath_ctrl_fwd_kernel(
   __shared__ float red[4];
   const int64_t b = blockIdx.x;
   if (mem_part) {  // mem = (1/L) sum over the row chunks of x_new, in chunk order (deterministic)
+    // the chunk partials are loaded 16 at a time before they are added (in chunk order, so the sum
+    // is bit-identical to the sequential loop): a dependent load-add chain over ~47 chunks left
+    // every load's latency exposed (24 us per launch at B = 32)
+    const float* mp = mem_part + (int64_t)b * nchunk * D;
     for (int c = threadIdx.x; c < D; c += 256) {
       float t = 0.f;
-      for (int k = 0; k < nchunk; ++k) t += mem_part[((int64_t)b * nchunk + k) * D + c];
+      int k = 0;
+      for (; k + 16 <= nchunk; k += 16) {
+        float v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = mp[(int64_t)(k + j) * D + c];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) t += v[j];
+      }
+      for (; k < nchunk; ++k) t += mp[(int64_t)k * D + c];
       mem_out[b * D + c] = t * (1.0f / (float)L);
     }
     __syncthreads();
     mem = mem_out;
   }
   float s = 0.f;
-  for (int64_t l = threadIdx.x; l < L; l += 256) s += ion[b * L + l];
+  {
+    const float* ib = ion + b * L;
+    int64_t l = threadIdx.x;
+    for (; l + 7 * 256 < L; l += 8 * 256) {  // 8 loads in flight, added in the same order
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = ib[l + 256 * j];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[j];
+    }
+    for (; l < L; l += 256) s += ib[l];
+  }
   const float potential = block_sum<256>(s, red) / (float)L;  // ion.mean(dim=1), model.py:466
   float mv;
   if (mg_w) {  // mem_v = sigmoid(mem_gate(mem)) computed here (model.py:464)
