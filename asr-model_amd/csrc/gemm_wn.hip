@@ -447,8 +447,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wn_kernel(Params p, int ntiles) 
 #ifndef WR_DEPTH
 #define WR_DEPTH 3  // register stages in flight (k-steps of prefetch)
 #endif
-// DEP (template): stages for launches of at most one workgroup per CU, where nothing else hides a
-// workgroup's load latency -- the text side's 8192-row GEMMs (0 = WR_DEPTH)
+// DEP (template): register stages, 0 = WR_DEPTH
 
 template <int NJ>
 struct WrStage {
@@ -669,10 +668,9 @@ static void launch_wr(const Params& p, hipStream_t s) {
   }
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + Cfg<NJ>::BN - 1) / Cfg<NJ>::BN);
   const int grid = std::min(tiles, resident);
-  if (NJ == 1 && !p.mtiles && tiles <= 256)  // one workgroup per CU at most: a deeper register pipeline
-    gemm_wr_kernel<NJ, CONV, RT, 5><<<grid, NTHR, 0, s>>>(p, tiles);
-  else
-    gemm_wr_kernel<NJ, CONV, RT><<<grid, NTHR, 0, s>>>(p, tiles);
+  // a 5-deep pipeline (DEP = 5) for the one-wave 8192-row text-side launches measured 32.4 us vs
+  // 30.1 us at depth 3 (profiles/r02_bench_v8_kernel_stats.csv): their time is not load latency
+  gemm_wr_kernel<NJ, CONV, RT><<<grid, NTHR, 0, s>>>(p, tiles);
 }
 
 // fp32 (rows x cols, row stride ld) -> bf16 N x K contiguous.  trans == 0: N = rows, K = cols;
