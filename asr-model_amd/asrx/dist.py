@@ -1,29 +1,34 @@
 """Data-parallel gradient synchronisation: bucketed all-reduce overlapped with backward
-(SURVEY.md §8(e)).  One process per GPU, torch.distributed with backend "nccl" (= RCCL on ROCm)
-over xGMI; "gloo" works the same way on CPU for the tests.
+(the seam is the reference's backward -> optimizer step, essentials.py:772-821).
+One process per GPU, torch.distributed with backend "nccl" (= RCCL on ROCm) over xGMI; "gloo" works
+the same way on CPU for the tests.
 
 Design (MI355X-first, not a translation of DDP's call pattern):
-  * the bucket plan covers exactly the parameters that receive gradients in this model (found on
-    the first step: dead blocks, the unused attn.c / rot.lin / router / span_scale / pitch_tokens
-    never do), in reverse registration order = roughly the order backward produces them;
-  * gradients live in the flat bucket buffers (p.grad is a view), so no copy is needed;
+  * gradients live in flat bucket buffers (p.grad is a view), so no copy is needed;
+  * the bucket plan covers exactly the parameters that receive gradients (dead blocks and the unused
+    attn.c / rot.lin / router / span_scale / pitch_tokens never do), found on the first step and
+    made identical on every rank: the live masks are max-reduced and rank 0's backward completion
+    order (the order in which each parameter took its last gradient of that step) is broadcast, so
+    bucket 0 holds what backward finishes first (the processor) and the last bucket the encoder;
+  * the first bucket is small (bucket_mb / 4) so the first all-reduce starts early in backward;
+  * COLLECTIVE ORDER IS RANK-INDEPENDENT BY CONSTRUCTION: bucket i is launched only after buckets
+    0..i-1 (the next-bucket rule): a bucket that completes early waits for its predecessors, and
+    finish() launches whatever is left in index order.  Every rank therefore issues the same
+    sequence of all-reduces of the same sizes, whether it launched them from backward hooks (a
+    known step signature) or from finish() (a new one), so ranks that see different signatures in
+    the same step -- DataCollator pads each rank's batch to its own maximum -- cannot pair buckets
+    of different sizes or hang;
   * readiness is counted in gradient events: autograd's post-accumulate-grad hook, and each
     contribution the asrx kernels accumulate straight into p.grad (asrx.ops.GRAD_LISTENERS).  How
-    many events a parameter receives depends on how the step was batched (asrx Model runs equal-
-    length audio streams as one pass, so a pitch track whose length differs from the spectrogram's
-    means one more pass per shared weight).  The counts are therefore learned PER STEP SIGNATURE
-    (`model.grad_signature`, set by Model.forward: the stream lengths): a step with a new signature
-    counts its events and reduces every bucket in finish(); a step with a known signature launches a
-    bucket's all-reduce as soon as the bucket has seen all of its events -- a comm stream waits on
-    the compute stream and the all-reduce then runs under the rest of backward;
+    many events a parameter receives depends on how the step was batched (equal-length audio
+    streams share one pass), so the counts are learned PER STEP SIGNATURE (`model.grad_signature`:
+    the train flag and the stream GROUPING, not raw lengths, so variable-length data keeps one
+    signature per grouping and overlap engages);
   * an event that arrives after its bucket's all-reduce was launched means the launch read a
     partial gradient: that raises (it cannot happen while event counts are a function of the
     signature, and the check keeps it from ever passing silently);
   * finish() joins the comm stream; buckets a step left incomplete are reduced there with their
-    missing slots zero (variable unused parameters);
-  * bucket size defaults to 64 MB: one 8-GPU ring step over 7 xGMI links moves bucket/8 per link
-    per step, large enough that per-call latency is amortised at the 96 MB (tiny) .. 1 GB (medium)
-    payloads, small enough that the first bucket launches early in backward.
+    missing slots zero (variable unused parameters).
 """
 from __future__ import annotations
 
@@ -36,7 +41,7 @@ from . import ops
 
 
 class _Bucket:
-    __slots__ = ("params", "buf", "pending", "expected", "work", "launched", "offsets")
+    __slots__ = ("params", "buf", "pending", "expected", "work", "launched", "complete", "offsets")
 
     def __init__(self, params, device):
         self.params = params
@@ -50,11 +55,12 @@ class _Bucket:
         self.expected = self.pending = len(params)
         self.work = None
         self.launched = False
+        self.complete = False
 
 
 class GradSync:
     def __init__(self, model: torch.nn.Module, bucket_mb: float = 64.0, group=None, signature=None,
-                 reduce_single: bool = False):
+                 reduce_single: bool = False, first_bucket_mb: float | None = None):
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         # reduce_single: run the bucket all-reduces even in a 1-rank group (exercises the RCCL launch,
@@ -62,16 +68,21 @@ class GradSync:
         self.active = self.world > 1 or (reduce_single and dist.is_initialized())
         self.params = [p for p in model.parameters() if p.requires_grad]
         self.bucket_bytes = int(bucket_mb * 1024 * 1024)
+        fb = bucket_mb / 4 if first_bucket_mb is None else first_bucket_mb
+        self.first_bucket_bytes = int(fb * 1024 * 1024)
         self.buckets: list[_Bucket] | None = None
         self.where: dict[int, tuple[_Bucket, int]] = {}
         dev = self.params[0].device
         self.cuda = dev.type == "cuda"
+        self.device = dev
         self.comm = torch.cuda.Stream(device=dev) if self.cuda else None
         self.hooks = [p.register_post_accumulate_grad_hook(self._ready) for p in self.params]
         # step signature -> learned gradient events per parameter (id) / per bucket
         self._signature = signature if signature is not None else (lambda: getattr(model, "grad_signature", None))
         self.plans: dict = {}
         self.bucket_plans: dict = {}
+        self._last_event: dict[int, int] = {}  # first step: event clock of each parameter's last event
+        self._clock = 0
         self._reset_step()
         self._listener = weakref.WeakMethod(self._ready)
         ops.GRAD_LISTENERS.append(self._listener)
@@ -81,31 +92,55 @@ class GradSync:
         self._sig = None
         self._started = False
         self._overlap = False  # this step launches buckets from the hooks (known signature)
+        self._next = 0  # index of the next bucket to launch (buckets launch strictly in index order)
 
     # ------------------------------------------------------------------ plan
+    def _agree_layout(self, live_idx, order_key):
+        """Rank-identical live set and parameter order: the union of the ranks' live masks, ordered by
+        rank 0's backward completion (ties and parameters rank 0 did not see: reverse registration)."""
+        n = len(self.params)
+        comm_dev = self.device if (self.cuda and dist.get_backend(self.group) == "nccl") else torch.device("cpu")
+        mask = torch.zeros(n, dtype=torch.int32, device=comm_dev)
+        mask[live_idx] = 1
+        key = torch.tensor([order_key.get(i, 1 << 40) for i in range(n)], dtype=torch.int64, device=comm_dev)
+        if self.world > 1 or self.active:
+            dist.all_reduce(mask, op=dist.ReduceOp.MAX, group=self.group)
+            src = dist.get_global_rank(self.group, 0) if self.group is not None else 0
+            dist.broadcast(key, src, group=self.group)
+        mask, key = mask.cpu().tolist(), key.cpu().tolist()
+        live = [i for i in range(n) if mask[i]]
+        return sorted(live, key=lambda i: (key[i], -i))
+
     def _build(self):
-        live = [p for p in self.params if p.grad is not None]
+        live_idx = [i for i, p in enumerate(self.params) if p.grad is not None]
+        order = {i: self._last_event.get(id(self.params[i]), 1 << 40) for i in live_idx}
+        if dist.is_initialized() and (self.world > 1 or self.active):
+            idx = self._agree_layout(live_idx, order)
+        else:
+            idx = sorted(live_idx, key=lambda i: (order[i], -i))
         buckets, cur, size = [], [], 0
-        for p in reversed(live):
+        for i in idx:
+            p = self.params[i]
             cur.append(p)
             size += p.numel() * 4
-            if size >= self.bucket_bytes:
+            if size >= (self.first_bucket_bytes if not buckets else self.bucket_bytes):
                 buckets.append(cur)
                 cur, size = [], 0
         if cur:
             buckets.append(cur)
-        dev = live[0].device
-        self.buckets = [_Bucket(ps, dev) for ps in buckets]
+        self.buckets = [_Bucket(ps, self.device) for ps in buckets]
         for b in self.buckets:
             for p, off in zip(b.params, b.offsets):
                 self.where[id(p)] = (b, off)
-                b.buf[off:off + p.numel()].copy_(p.grad.reshape(-1))
+                if p.grad is not None:
+                    b.buf[off:off + p.numel()].copy_(p.grad.reshape(-1))
                 p.grad = b.buf[off:off + p.numel()].view_as(p)
+        self._last_event.clear()
 
-    def _learn(self, sig):
-        """Record this step's event counts as the plan of its signature."""
-        self.plans[sig] = dict(self._seen)
-        self.bucket_plans[sig] = [sum(max(1, self._seen.get(id(p), 0)) for p in b.params) for b in self.buckets]
+    def _learn(self, sig, counts):
+        """Record `counts` (events per parameter id) as the plan of signature `sig`."""
+        self.plans[sig] = dict(counts)
+        self.bucket_plans[sig] = [sum(max(1, counts.get(id(p), 0)) for p in b.params) for b in self.buckets]
 
     def zero_grad(self):
         """Zero the bucket buffers (the grads are views of them) before the next backward."""
@@ -118,6 +153,7 @@ class GradSync:
             b.buf.zero_()
             b.work = None
             b.launched = False
+            b.complete = False
             for p, off in zip(b.params, b.offsets):
                 if p.grad is None or p.grad.data_ptr() != b.buf[off:].data_ptr():
                     p.grad = b.buf[off:off + p.numel()].view_as(p)
@@ -136,6 +172,9 @@ class GradSync:
         if not self._started:
             self._start_step()
         self._seen[id(p)] = self._seen.get(id(p), 0) + 1
+        if self.buckets is None:  # first step: remember the completion order for the bucket layout
+            self._clock += 1
+            self._last_event[id(p)] = self._clock
         if not self._overlap:
             return
         entry = self.where.get(id(p))
@@ -144,12 +183,19 @@ class GradSync:
         b = entry[0]
         b.pending -= 1
         if b.pending == 0:
-            self._launch(b)
+            b.complete = True
+            self._launch_ready()
         elif b.pending < 0:
             raise RuntimeError(
                 "GradSync: a gradient event arrived after its bucket's all-reduce was launched (step "
                 f"signature {self._sig!r} delivered more events than the learned plan); the all-reduce read a "
                 "partial gradient")
+
+    def _launch_ready(self):
+        """The next-bucket rule: launch the run of complete buckets starting at the next index."""
+        while self._next < len(self.buckets) and self.buckets[self._next].complete:
+            self._launch(self.buckets[self._next])
+            self._next += 1
 
     def _launch(self, b: _Bucket):
         if b.launched:
@@ -171,18 +217,19 @@ class GradSync:
         if self.buckets is None:
             self._build()  # first step: nothing overlapped yet
         if self._sig not in self.bucket_plans:
-            self._learn(self._sig)
+            self._learn(self._sig, self._seen)
         elif self._overlap:
             plan = self.plans[self._sig]
-            extra = [i for i, n in self._seen.items() if n > plan.get(i, 0)]
-            if extra:  # would have raised in _ready for an overlapped bucket; a bucket not yet launched is fine
-                self.plans[self._sig] = {i: max(n, self._seen.get(i, 0)) for i, n in plan.items()} | \
-                    {i: n for i, n in self._seen.items() if i not in plan}
-                self._learn(self._sig)
+            if any(n > plan.get(i, 0) for i, n in self._seen.items()):
+                # would have raised in _ready for a launched bucket; a bucket not yet launched is fine
+                merged = dict(plan)
+                for i, n in self._seen.items():
+                    merged[i] = max(n, merged.get(i, 0))
+                self._learn(self._sig, merged)
         if self.active:
-            for b in self.buckets:
-                if not b.launched:
-                    self._launch(b)
+            for b in self.buckets[self._next:]:  # the rest, in index order
+                self._launch(b)
+            self._next = len(self.buckets)
             for b in self.buckets:
                 b.work.wait()
             if self.cuda:

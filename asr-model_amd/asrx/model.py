@@ -560,6 +560,18 @@ class processor(nn.Module):  # noqa: N801  (model.py:585-629)
         return out
 
 
+def stream_grouping(lengths):
+    """Group id of each audio stream: consecutive streams of equal length share one batched pass
+    (AudioEncoder.encode, processor._audio), e.g. (0, 0, 1) for pitch and spectrogram at 3001 frames
+    and the waveform feature at 3000."""
+    out, gid = [], 0
+    for i, n in enumerate(lengths):
+        if i and n != lengths[i - 1]:
+            gid += 1
+        out.append(gid)
+    return tuple(out)
+
+
 class Model(nn.Module):
     """model.py:631-701."""
 
@@ -598,8 +610,9 @@ class Model(nn.Module):
         streams = [s.to(torch.float32) for s in streams]
         B = first.shape[0]
         # how this step is batched decides how many gradient contributions each shared weight gets
-        # (equal-length streams share one pass): asrx.dist.GradSync keys its event plans on it
-        self.grad_signature = (self.training, tuple(s.shape[-1] for s in streams))
+        # (runs of consecutive equal-length streams share one pass): asrx.dist.GradSync keys its event
+        # plans on that grouping -- not on the raw lengths, which vary from batch to batch
+        self.grad_signature = (self.training, stream_grouping([s.shape[-1] for s in streams]))
         gemm_mod.clear_weight_cache(self)
         noise = NoiseCtx(self.noise_seed, self.noise_step, self.training)
         if self.training:

@@ -449,6 +449,14 @@ int asrx_flac_info(const uint8_t* buf, int64_t n, int64_t* frames, int* channels
       return 2;
     }
   }
+  // a frame (>= 10 bytes: sync + header + CRC-8 + one subframe header + CRC-16) holds at most 65535
+  // samples per channel, so a stream of n bytes cannot hold more than ~6.6 k samples per byte: a
+  // STREAMINFO claiming more is corrupt or hostile (the caller allocates channels x total up front)
+  if (total > (n / 10 + 1) * 65536) {
+    asrx::set_error("asrx_flac_info: STREAMINFO claims %lld samples, more than %lld bytes can hold",
+                    (long long)total, (long long)n);
+    return 2;
+  }
   *frames = total;
   *channels = si.channels;
   *rate = si.rate;

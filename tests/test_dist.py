@@ -234,3 +234,97 @@ def test_gradsync_event_plans_per_signature(sig_override):
         assert err is not None and "partial" in err, (out, err)
         assert [o[0] for o in out] == [1, 1]  # the first 3-pass step raised
         assert all(o[2] for o in out)
+
+
+def _worker_mixed(rank, world, port, q, schedule):
+    """Ranks whose step signatures differ IN THE SAME STEP (one rank's batch needs 3 passes of the
+    shared weight, the other's 1; one rank knows its signature, the other sees it for the first time):
+    both must issue the same all-reduce sequence (next-bucket rule), complete, and end with the
+    average of the two ranks' local gradients."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "asr-model_amd")]
+    from asrx.dist import GradSync, broadcast_parameters
+
+    torch.manual_seed(rank)
+    model = ToyVarying()
+    broadcast_parameters(model)
+    twin = ToyVarying()  # local gradients (no hooks)
+    twin.load_state_dict(model.state_dict())
+    sync = GradSync(model, bucket_mb=0.0005)
+    launches = []
+    orig_launch = sync._launch
+
+    def logged(b):
+        launches[-1].append(sync.buckets.index(b))
+        orig_launch(b)
+
+    sync._launch = logged
+    out = []
+    for step, passes_by_rank in enumerate(schedule):
+        model.passes = twin.passes = passes_by_rank[rank]
+        launches.append([])
+        sync.zero_grad()
+        x = torch.randn(5, 16, generator=torch.Generator().manual_seed(100 * step + rank))
+        (model(x).pow(2).sum() * (rank + 1)).backward()
+        overlapped = sum(int(b.launched) for b in sync.buckets or [])
+        sync.finish()
+        synced = {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None}
+        twin.zero_grad(set_to_none=True)
+        (twin(x).pow(2).sum() * (rank + 1)).backward()
+        avg = {}
+        for n, p in twin.named_parameters():
+            t = p.grad.clone()
+            dist.all_reduce(t)
+            avg[n] = t / world
+        ok = set(synced) == set(avg) and all(torch.allclose(synced[n], avg[n], atol=1e-5) for n in avg)
+        out.append((passes_by_rank[rank], overlapped, ok, list(launches[-1]), len(sync.buckets)))
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gradsync_ranks_with_different_signatures_same_step():
+    # (rank 0 passes, rank 1 passes) per step: step 1 rank 0 new / rank 1 known, step 2 the reverse,
+    # step 3 both known but different, step 4 both new
+    schedule = [(1, 1), (3, 1), (1, 3), (3, 1), (2, 2)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_mixed, args=(r, 2, port, q, schedule)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r, out = q.get(timeout=120)
+        res[r] = out
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in (0, 1):
+        for step, (passes, overlapped, ok, order, nb) in enumerate(res[r]):
+            assert ok, (r, step, res[r])
+            assert order == list(range(nb)), (r, step, order)  # every rank: index order, every bucket
+    # a rank that knows its signature launches from backward even when the other rank does not
+    assert res[1][1][1] > 0 and res[0][1][1] == 0, res
+    assert res[0][2][1] > 0 and res[1][2][1] == 0, res
+    assert res[0][3][1] > 0 and res[1][3][1] > 0, res
+    assert res[0][4][1] == 0 and res[1][4][1] == 0, res
+
+
+def test_stream_grouping_signature():
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "asr-model_amd")]
+    from asrx.model import stream_grouping
+
+    assert stream_grouping([3001, 3001, 3000]) == (0, 0, 1)
+    assert stream_grouping([2450, 2450, 2449]) == (0, 0, 1)  # other clip lengths: same signature
+    assert stream_grouping([6001, 3001, 3000]) == (0, 1, 2)
+    assert stream_grouping([3000, 3001, 3000]) == (0, 1, 2)  # only consecutive streams share a pass
+    assert stream_grouping([101, 101, 101]) == (0, 0, 0)

@@ -146,3 +146,16 @@ def test_prepare_datasets_reads_flac_rows(tmp_path, monkeypatch):
     assert len(ds) == 1 and ds[0] == {"ok": True}
     assert seen["batch"]["transcription"] == "hello world" and seen["kw"] == {"spectrogram": True}
     assert os.path.basename(seen["batch"]["audio"]) == "a.flac" and seen["wave"].shape == (1600,)
+
+
+def test_streaminfo_total_is_bounded_by_stream_size():
+    """A STREAMINFO claiming ~2^36 samples (hostile or corrupt) is refused before the caller allocates
+    channels x total samples (the decode would only fail after that allocation)."""
+    pcm = _signal(1, 4000, 16, 5)
+    data = bytearray(fe.encode(pcm, 16000, 16, block=1024))
+    si = 8  # "fLaC" + 4-byte metadata block header
+    word = int.from_bytes(data[si + 10:si + 18], "big")  # rate 20 | channels-1 3 | bps-1 5 | total 36
+    word |= (1 << 36) - 1
+    data[si + 10:si + 18] = word.to_bytes(8, "big")
+    with pytest.raises(RuntimeError, match="claims"):
+        _decode(bytes(data))

@@ -24,11 +24,13 @@ def _free_port():
 
 
 def _inputs(step, rank, B=2, S=101, T=8, V=500):
+    """kind 0: pitch as long as the spectrogram (grouping (0, 0, 1)); kind 1: a shorter pitch track
+    ((0, 1, 2)); kind 3: shorter pitch and a waveform feature as long as the spectrogram ((0, 1, 1))."""
     g = torch.Generator().manual_seed(1000 * step + rank)
-    Sp = S if step != 1 else S - 20  # step 1: a shorter pitch track -> different stream grouping
+    Sp = S if step == 0 else S - 20
     spec = torch.randn(B, 128, S, generator=g)
     pitch = torch.rand(B, 1, Sp, generator=g) * 200
-    wav = torch.randn(B, 1, S - 1, generator=g) * 0.1
+    wav = torch.randn(B, 1, S if step == 3 else S - 1, generator=g) * 0.1
     ids = torch.randint(3, V, (B, T), generator=g)
     ids[:, 0] = 1
     labels = torch.cat([ids[:, 1:], torch.full((B, 1), 2)], 1)
@@ -56,8 +58,12 @@ def _worker(rank, world, port, q, root):
     ref.load_state_dict(model.state_dict())
     sync = GradSync(model, bucket_mb=1.0)
     out = []
+    # per step: the input kind of (rank 0, rank 1).  Steps 4 and 5 give the ranks DIFFERENT groupings
+    # in the same step (step 4: both known; step 5: rank 0 known, rank 1 new)
+    schedule = [(0, 0), (1, 1), (0, 0), (1, 1), (0, 1), (0, 3)]
     with prec.precision("fp32"):
-        for step in (0, 1, 0, 1):
+        for kinds in schedule:
+            step = kinds[rank]
             spec, pitch, wav, ids, labels = (t.to(dev) for t in _inputs(step, rank))
             model.set_noise(11, step)
             sync.zero_grad()
@@ -107,8 +113,10 @@ def test_gradsync_asrx_model_two_ranks(cuda):
         for step, overlapped, nb, err, same_set, _ in out:
             assert same_set
             assert err < 1e-5, (r, step, err)
-        # first sight of each signature reduces in finish(); the repeats launch from backward
-        assert [o[1] > 0 for o in out] == [False, False, True, True], out
+        # first sight of each signature reduces in finish(); the repeats launch from backward, also
+        # when the other rank runs a different (step 4) or a new (step 5) grouping in the same step
+        want = [False, False, True, True, True, r == 0]
+        assert [o[1] > 0 for o in out] == want, out
 
 
 def _rccl_worker(port, q, root):
