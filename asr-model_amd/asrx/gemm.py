@@ -11,10 +11,20 @@ from . import lib, prec, probe
 ACT = {"none": 0, "gelu": 1, "silu": 2, "sigmoid": 3, "relu": 4}
 
 
+BF16 = torch.bfloat16
+
+
+def is_bf16(t) -> bool:
+    return t is not None and t.dtype == BF16
+
+
 def gemm(A, B, C, *, M, N, K, lda, ldb, ldc, a_kc=True, b_kc=True, batch=1, sA=0, sB=0, sC=0,
          bias=None, Z=None, alpha=1.0, beta=0.0, act="none", conv_a=False, conv_b=False,
          conv_F=0, conv_C=0, splitk=1, precision=None):
+    """The generic fp32-storage GEMM (csrc/gemm.hip): every operand fp32 in HBM."""
     lib.require_gpu(A, B, C)
+    if is_bf16(A) or is_bf16(B) or is_bf16(C):
+        raise RuntimeError("asrx_gemm takes fp32 operands; bf16-stored activations go through the wide GEMM")
     p = prec.get() if precision is None else precision
     e0 = probe.begin("gemm")
     lib.call("asrx_gemm", p, lib.ptr(A), lda, sA, int(a_kc), int(conv_a), lib.ptr(B), ldb, sB,
@@ -152,14 +162,19 @@ def _nj(M, N):
 
 
 def gemm_wn(A, Wb, C, *, M, N, K, lda, ldc, bias=None, Z=None, alpha=1.0, beta=0.0, act="none",
-            conv=False, conv_F=0, conv_C=0):
-    """C = act(alpha A Wb^T + beta C + bias); Wb bf16 (N, K) from weight_bf16."""
+            conv=False, conv_F=0, conv_C=0, mtiles=None):
+    """C = act(alpha A Wb^T + beta C + bias); Wb bf16 (N, K) from weight_bf16.  A and C are stored fp32
+    or bf16 (their dtype; a bf16 C takes beta = 0); mtiles: only these 128-row tiles (row_tiles)."""
     lib.require_gpu(A, Wb, C)
+    nj = _nj(M, N)
+    ab, cb = int(is_bf16(A)), int(is_bf16(C))
     e0 = probe.begin("gemm")
-    lib.call("asrx_gemm_wn", lib.ptr(A), lda, int(conv), conv_F, conv_C, lib.ptr(Wb), Wb.stride(0), lib.ptr(C),
-             ldc, lib.ptr(bias), lib.ptr(Z), M, N, K, float(alpha), float(beta), ACT[act], _nj(M, N),
+    lib.call("asrx_gemm_wn_ex", lib.ptr(A), ab, lda, int(conv), conv_F, conv_C, lib.ptr(Wb), Wb.stride(0),
+             lib.ptr(C), cb, ldc, lib.ptr(bias), lib.ptr(Z), M, N, K, float(alpha), float(beta), ACT[act], nj,
+             lib.ptr(mtiles[0]) if mtiles is not None else None, lib.ptr(mtiles[1]) if mtiles is not None else None,
              lib.stream())
-    probe.end("gemm", e0, 2.0 * M * N * K, ("wn", M, N, K, _nj(M, N), int(conv), act, Z is not None, beta != 0))
+    probe.end("gemm", e0, 2.0 * M * N * K,
+              ("wn", M, N, K, nj, int(conv), act, Z is not None, beta != 0, ab, cb, mtiles is not None))
     return C
 
 
@@ -184,14 +199,7 @@ def use_wide(K) -> bool:
 
 def gemm_wn_rows(A, Wb, C, *, M, N, K, lda, ldc, mtiles, bias=None, alpha=1.0, beta=0.0):
     """gemm_wn on the 128-row tiles listed on the device (mtiles = (list, count) from row_tiles)."""
-    lib.require_gpu(A, Wb, C)
-    nj = _nj(M, N)
-    e0 = probe.begin("gemm")
-    lib.call("asrx_gemm_wn_rows", lib.ptr(A), lda, lib.ptr(Wb), Wb.stride(0), lib.ptr(C), ldc, lib.ptr(bias), None,
-             M, N, K, float(alpha), float(beta), ACT["none"], nj, lib.ptr(mtiles[0]), lib.ptr(mtiles[1]),
-             lib.stream())
-    probe.end("gemm", e0, 2.0 * M * N * K, ("wn_rows", M, N, K, nj, beta != 0))
-    return C
+    return gemm_wn(A, Wb, C, M=M, N=N, K=K, lda=lda, ldc=ldc, bias=bias, alpha=alpha, beta=beta, mtiles=mtiles)
 
 
 def row_tiles(next_i, layer, L, M):
@@ -204,16 +212,21 @@ def row_tiles(next_i, layer, L, M):
     return tl, cnt
 
 
-def linear_fwd(x, W, b=None, act="none", out=None, preact=None, wbf=None, mtiles=None):
-    """y = act(x @ W^T + b) for x (..., K), W (N, K); wbf: W's bf16 copy when the caller made it;
-    mtiles: only these 128-row tiles (perf mode; the fp32 parity GEMM computes every row)."""
+def linear_fwd(x, W, b=None, act="none", out=None, preact=None, wbf=None, mtiles=None, out_bf16=False):
+    """y = act(x @ W^T + b) for x (..., K) (fp32 or bf16-stored), W (N, K); wbf: W's bf16 copy when the
+    caller made it; mtiles: only these 128-row tiles (perf mode; the fp32 parity GEMM computes every
+    row); out_bf16: store y bf16 (perf mode, when y only feeds GEMM operands)."""
     x2 = _rows(x)
     if not x2.is_contiguous():
         x2 = x2.contiguous()
     M, K = x2.shape
     N = W.shape[0]
-    y = out if out is not None else torch.empty(*x.shape[:-1], N, device=x.device, dtype=torch.float32)
-    if use_wide(K) and mtiles is not None and act == "none" and preact is None:
+    wide = use_wide(K)
+    if is_bf16(x2) and not wide:
+        x2 = x2.float()  # the fp32 GEMM (parity mode / K % 8 != 0) reads fp32
+    odt = BF16 if (out_bf16 and wide and N % 4 == 0) else torch.float32
+    y = out if out is not None else torch.empty(*x.shape[:-1], N, device=x.device, dtype=odt)
+    if wide and mtiles is not None and act == "none" and preact is None:
         gemm_wn_rows(x2, weight_bf16(W) if wbf is None else wbf, y, M=M, N=N, K=K, lda=K, ldc=N, bias=b,
                      mtiles=mtiles)
     elif use_wide(K):
@@ -226,6 +239,7 @@ def linear_fwd(x, W, b=None, act="none", out=None, preact=None, wbf=None, mtiles
 
 
 def linear_dgrad(dy, W, out=None, beta=0.0, mtiles=None):
+    """dx = dy @ W (fp32 dx)."""
     """dx = dy @ W for dy (..., N), W (N, K); mtiles as in linear_fwd."""
     d2 = _rows(dy)
     if not d2.is_contiguous():
@@ -250,9 +264,21 @@ def _splitk_for(m_rows: int, tiles: int) -> int:
 
 
 def _wgrad(A, lda, x2, out, M, K, rows):
-    """out (M, K) += A^T x2 over `rows` rows (A: (rows, >= M) with row stride lda, x2: (rows, K))."""
+    """out (M, K) += A^T x2 over `rows` rows (A: (rows, >= M) with row stride lda, x2: (rows, K), fp32 or
+    bf16-stored)."""
     tiles = ((M + 127) // 128) * ((K + 127) // 128)
     sk = _splitk_for(rows, tiles)
+    if is_bf16(x2):
+        # a bf16-stored activation: the register-staged bf16 kernel at every shape (its X bytes halve)
+        if M % 4 or K % 8 or lda % 4 or x2.stride(0) != K or A.data_ptr() % 16:
+            x2 = x2.float()
+        else:
+            lib.require_gpu(A, x2, out)
+            e0 = probe.begin("gemm")
+            lib.call("asrx_wgrad_bf16_ex", lib.ptr(A), lda, lib.ptr(x2), 1, K, lib.ptr(out), out.stride(0), M, K,
+                     rows, sk, lib.stream())
+            probe.end("gemm", e0, 2.0 * M * K * rows, ("wgrad", M, K, rows, sk, 1))
+            return out
     ok4 = M % 4 == 0 and K % 4 == 0 and lda % 4 == 0 and A.data_ptr() % 16 == 0 and x2.data_ptr() % 16 == 0
     # register-staged bf16 kernel with transpose reads (csrc/gemm_wg.hip): faster where the output
     # has few tiles (D x D weights, 1.2-2.6x on the 8192-row text side); the wide 1152/1536 outputs at

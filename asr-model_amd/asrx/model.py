@@ -19,7 +19,7 @@ from torch import nn
 from torch.nn.utils.parametrizations import weight_norm
 
 from . import gemm as gemm_mod
-from . import lib, ops
+from . import lib, ops, prec
 from .config import Dimensions
 from .noise import NoiseCtx
 
@@ -77,8 +77,9 @@ class AbbyNormal(nn.Module):
         self.size, self.alpha, self.beta, self.k, self.tx = size, alpha, beta, k, threshold
         self.mode_router = nn.Sequential(nn.Linear(dims, dims), nn.SiLU(), nn.Linear(dims, 3))
 
-    def run(self, x, noise: NoiseCtx, site: str, sid_base: int, L: int, H: int = 1):
-        return ops.abby_normal(self, x, L, H, sid_base, noise.key(site), True)
+    def run(self, x, noise: NoiseCtx, site: str, sid_base: int, L: int, H: int = 1, out_bf16: bool = False):
+        """out_bf16: the output only feeds GEMM / attention operands (stored bf16 in perf mode)."""
+        return ops.abby_normal(self, x, L, H, sid_base, noise.key(site), True, out_bf16)
 
 
 class LayerNorm(nn.Module):
@@ -255,19 +256,19 @@ class attention(nn.Module):  # noqa: N801
         B, L, D = src.shape
         H, hd = self.head, D // self.head
         src = ops.fork(src)  # read by the kv AbbyNormal and rotary's |src|
-        kvn = self.kv[0].run(src, noise, site + ".kv", sid_base, L)
+        kvn = self.kv[0].run(src, noise, site + ".kv", sid_base, L, out_bf16=True)
         k, v = ops.kv_proj(kvn, self.kv[1].weight, self.kv[1].bias)
         k = ops.rotary(k, src, rotary_freqs(D, H, masked, src.device), hd, self.scale)
-        k = self.ln.run(k.view(B, L, H, hd), noise, site + ".kh", sid_base, L, H)
+        k = self.ln.run(k.view(B, L, H, hd), noise, site + ".kh", sid_base, L, H, out_bf16=prec.attn_bf16_io())
         return k, v.view(B, L, H, hd)
 
     def project_q(self, x, noise, site, sid_base, masked):
         B, L, D = x.shape
         H, hd = self.head, D // self.head
-        qn = self.q[0].run(x, noise, site + ".q", sid_base, L)
+        qn = self.q[0].run(x, noise, site + ".q", sid_base, L, out_bf16=True)
         q = ops.linear(qn, self.q[1].weight, self.q[1].bias)
         q = ops.rotary(q, x, rotary_freqs(D, H, masked, x.device), hd, self.scale)
-        return self.ln.run(q.view(B, L, H, hd), noise, site + ".qh", sid_base, L, H)
+        return self.ln.run(q.view(B, L, H, hd), noise, site + ".qh", sid_base, L, H, out_bf16=prec.attn_bf16_io())
 
     def run(self, x, kv, noise, site, sid_base, masked):
         """x: attention input (B, Lq, D); kv: None (self attention on x) or (k, v) of the cross
@@ -277,7 +278,7 @@ class attention(nn.Module):  # noqa: N801
         if kv is None:
             kv = self.project_kv(x, noise, site, sid_base, masked)
         q = self.project_q(x, noise, site, sid_base, masked)
-        o = ops.attention(q, kv[0], kv[1], masked)
+        o = ops.attention(q, kv[0], kv[1], masked, out_bf16=True)
         return ops.linear(o.view(B, L, D), self.out[1].weight, self.out[1].bias)
 
 
@@ -351,7 +352,7 @@ class MSheath(nn.Module):
 
         if self.fused and ops.DIRECT and _ms.supported(self, x.shape[-1]):
             gpol = ops.policy_noise(x.shape[0], self.layer, sid_base, noise.key(site), x.device)
-            return _ms.msheath(self, x, gpol)
+            return _ms.msheath(self, x, gpol, tag=(noise.key(site), sid_base))
         return self.run_composed(x, noise, site, sid_base)
 
     def run_composed(self, x, noise: NoiseCtx, site: str, sid_base: int):
@@ -429,9 +430,9 @@ class residual(nn.Module):  # noqa: N801  (model.py:559-583)
         if kv is not None:
             h = self.ln.run(x, noise, site + ".ln2", sid_base, L)
             x = ops.fork(ops.add(x, self.attn.run(h, kv, noise, site + ".ca", sid_base, False)))
-        m = self.ln.run(x, noise, site + ".mlp.ln0", sid_base, L)
-        m = ops.tgate(self.mlp[1], m)
-        m = ops.linear(m, self.mlp[2].weight, self.mlp[2].bias, act="gelu")
+        m = self.ln.run(x, noise, site + ".mlp.ln0", sid_base, L, out_bf16=True)  # feeds only tgate's GEMMs
+        m = ops.tgate(self.mlp[1], m, out_bf16=True)
+        m = ops.linear(m, self.mlp[2].weight, self.mlp[2].bias, act="gelu", out_bf16=True)
         m = ops.linear(m, self.mlp[4].weight, self.mlp[4].bias)
         m = self.ln.run(m, noise, site + ".mlp.ln1", sid_base, L)
         return ops.add(x, m)
@@ -509,7 +510,7 @@ class processor(nn.Module):  # noqa: N801  (model.py:585-629)
             out = g
         else:
             out = ops.blend(d, g, self.blend)  # sigmoid(blend) d + (1 - sigmoid(blend)) g
-        out = self.ln.run(out, noise, "final.ln", 0, T)
+        out = self.ln.run(out, noise, "final.ln", 0, T, out_bf16=True)
         return ops.linear(out, self.token.weight)
 
     # ---- decoding (Model.generate): the y-independent audio side of the only live block, once
@@ -536,7 +537,7 @@ class processor(nn.Module):  # noqa: N801  (model.py:585-629)
         d = blk.call(c_, noise, f"b{i}.td", 0, kv=kv[2])
         e = ops.add(a, b_, c_)
         g = blk.call(d, noise, f"b{i}.tg", 0, kv=blk.xa_side(e, noise, f"b{i}.tg.xa", 0))
-        out = self.ln.run(g.contiguous(), noise, "final.ln", 0, T)
+        out = self.ln.run(g.contiguous(), noise, "final.ln", 0, T, out_bf16=True)
         return ops.linear(out, self.token.weight)
 
     @staticmethod

@@ -26,7 +26,7 @@ import math
 import torch
 
 from . import gemm as G
-from . import lib, ops
+from . import decisions, lib, ops, prec
 
 _E = torch.empty
 _P = lib.ptr
@@ -65,8 +65,9 @@ def _params(mod):
     return ps
 
 
-def forward(mod, x0, gpol, save):
-    """MSheath forward on (B, L, D) x0 with policy noise gpol (B, layers, 3).  Returns (out, saved)."""
+def forward(mod, x0, gpol, save, tag=None):
+    """MSheath forward on (B, L, D) x0 with policy noise gpol (B, layers, 3).  Returns (out, saved).
+    tag: (noise site key, sid_base) of the call, for asrx.decisions."""
     B, L, D = x0.shape
     rows = B * L
     dev = x0.device
@@ -109,13 +110,15 @@ def forward(mod, x0, gpol, save):
         SH = G.linear_fwd(x, Wc, bc, wbf=wb, mtiles=mt)
         # px = LayerNorm(x), |x|, g = sigmoid(gate(px)), ion = v_gate(x)   (346-351, 452-460)
         ln, gt = lay["ln"], lay["gate"][0]
-        px = _E(B, L, D, device=dev)
-        mean, rstd, nx, gv, ion, kv, m2 = (_E(rows, device=dev) for _ in range(7))
-        lib.call("asrx_msheath_row_fwd", _P(x), _P(ln.weight), _P(ln.bias), _P(gt.weight), _P(gt.bias), _P(SH), N,
-                 _P(vg.mval), _P(vg.mlp[2].weight), _P(vg.mlp[2].bias), _P(vg.concat.weight), _P(vg.concat.bias),
-                 _P(vg.tx), _P(px), _P(mean), _P(rstd), _P(nx), _P(gv), _P(ion), _P(kv), _P(m2), rows, D, M, Dh,
-                 float(ln.eps), inv_sqrt_d, _P(next_i), i, L, st)
         ad = lay["adapter"]
+        # px feeds only the adapter GEMM on even layers (bf16-stored); on odd layers it is the update itself
+        pxb = int(ad is not None and wide and prec.bf16_storage())
+        px = _E(B, L, D, device=dev, dtype=torch.bfloat16 if pxb else torch.float32)
+        mean, rstd, nx, gv, ion, kv, m2 = (_E(rows, device=dev) for _ in range(7))
+        lib.call("asrx_msheath_row_fwd2", _P(x), _P(ln.weight), _P(ln.bias), _P(gt.weight), _P(gt.bias), _P(SH), N,
+                 _P(vg.mval), _P(vg.mlp[2].weight), _P(vg.mlp[2].bias), _P(vg.concat.weight), _P(vg.concat.bias),
+                 _P(vg.tx), _P(px), pxb, _P(mean), _P(rstd), _P(nx), _P(gv), _P(ion), _P(kv), _P(m2), rows, D, M, Dh,
+                 float(ln.eps), inv_sqrt_d, _P(next_i), i, L, st)
         out = G.linear_fwd(px, ad.weight, ad.bias, mtiles=mt) if ad is not None else px
         # x_new = x + g * ion * out; mem = mean_l x_new   (461-463)
         x_new = _E(B, L, D, device=dev)
@@ -129,6 +132,8 @@ def forward(mod, x0, gpol, save):
         lib.call("asrx_msheath_ctrl_fwd3", _P(policy), _P(gp), gp.stride(0), _P(ion), _P(mg.weight), _P(mg.bias),
                  _P(mem_v), _P(mem_w), ld_mw, _P(part[i]), _P(mem), _P(mod.jump_s), _P(next_i), i, nl, B, L, D,
                  _P(alpha), _P(beta), _P(gam), _P(mwo), _P(active), _P(next_out), _P(rec), st)
+        if tag is not None and decisions.active():
+            decisions.msheath_layer(tag[0], tag[1], i, ion.view(B, L), rec.view(torch.float32).view(B, -1))
         x_out = _E(B, L, D, device=dev)
         lib.call("asrx_jump_select4", _P(x_new), _P(x0), _P(x), _P(active), _P(alpha), _P(beta), _P(gam),
                  _P(x_out), B, L, D, st)
@@ -140,12 +145,14 @@ def forward(mod, x0, gpol, save):
         x = x_out
     # x + sigmoid(mlp_gate(x)) * mlp(mlp_ln(x))   (503-506): the gate from the LayerNorm's row pass
     gate = _E(rows, device=dev)
-    hln, mean2, rstd2 = _E(B, L, D, device=dev), _E(rows, device=dev), _E(rows, device=dev)
-    lib.call("asrx_layernorm_fwd2", _P(x), _P(mod.mlp_ln.weight), _P(mod.mlp_ln.bias), _P(hln), _P(mean2),
+    hb = int(wide and prec.bf16_storage())  # hln only feeds mlp[0]
+    hln = _E(B, L, D, device=dev, dtype=torch.bfloat16 if hb else torch.float32)
+    mean2, rstd2 = _E(rows, device=dev), _E(rows, device=dev)
+    lib.call("asrx_layernorm_fwd3", _P(x), _P(mod.mlp_ln.weight), _P(mod.mlp_ln.bias), _P(hln), hb, _P(mean2),
              _P(rstd2), None, _P(mod.mlp_gate[0].weight), _P(mod.mlp_gate[0].bias), _P(gate), 1, rows, D,
              float(mod.mlp_ln.eps), st)
     z1 = _E(B, L, mod.mlp[0].weight.shape[0], device=dev) if save else None
-    a1 = G.linear_fwd(hln, mod.mlp[0].weight, mod.mlp[0].bias, act="silu", preact=z1)
+    a1 = G.linear_fwd(hln, mod.mlp[0].weight, mod.mlp[0].bias, act="silu", preact=z1, out_bf16=prec.bf16_storage())
     hh = G.linear_fwd(a1, mod.mlp[2].weight, mod.mlp[2].bias)
     y = _E(B, L, D, device=dev)
     lib.call("asrx_axpy_row", _P(x), _P(gate), _P(hh), _P(y), rows, D, st)
@@ -157,9 +164,9 @@ def forward(mod, x0, gpol, save):
 
 class MSheathFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x0, gpol, mod, *params):
+    def forward(ctx, x0, gpol, mod, tag, *params):
         x0 = x0 if x0.is_contiguous() else x0.contiguous()
-        y, sv = forward(mod, x0, gpol, save=True)
+        y, sv = forward(mod, x0, gpol, save=True, tag=tag)
         ctx.mod, ctx.sv = mod, sv
         return y
 
@@ -283,13 +290,13 @@ class MSheathFn(torch.autograd.Function):
             if id(p) not in seen:
                 seen.add(id(p))
                 ops._gret(p, p.grad, True)
-        return (dx, None, None) + (None,) * len(ctx.needs_input_grad[3:])
+        return (dx, None, None, None) + (None,) * len(ctx.needs_input_grad[4:])
 
 
-def msheath(mod, x, gpol):
+def msheath(mod, x, gpol, tag=None):
     """Fused MSheath call.  Without autograd (the reference's dead blocks, eval, decoding) the forward
-    runs without saving anything for a backward."""
+    runs without saving anything for a backward.  tag: (noise site key, sid_base) for asrx.decisions."""
     params = _params(mod)
     if not torch.is_grad_enabled() or not (x.requires_grad or any(p.requires_grad for p in params)):
-        return forward(mod, x if x.is_contiguous() else x.contiguous(), gpol, save=False)[0]
-    return MSheathFn.apply(x, gpol, mod, *params)
+        return forward(mod, x if x.is_contiguous() else x.contiguous(), gpol, save=False, tag=tag)[0]
+    return MSheathFn.apply(x, gpol, mod, tag, *params)

@@ -1,7 +1,9 @@
 """Autograd functions over the HIP C-ABI.  Forward and backward of every function run asrx kernels
 (csrc/*.hip); PyTorch supplies memory, streams and the autograd tape only.
 
-All activations are contiguous float32 device tensors; "rows" means the flattened leading dims.
+Activations are contiguous device tensors, float32 -- or bfloat16 where an activation's only consumers
+are GEMM / attention operands and the perf mode stores it that way (asrx.prec.bf16_storage: the
+consumers round to bf16 anyway); "rows" means the flattened leading dims.
 """
 from __future__ import annotations
 
@@ -11,6 +13,7 @@ import weakref
 
 import torch
 
+from . import decisions
 from . import gemm as G
 from . import lib, prec, probe
 
@@ -193,13 +196,14 @@ class Linear(torch.autograd.Function):
     """y = act(x W^T + b) on MFMA (nn.Linear / 1x1 Conv1d)."""
 
     @staticmethod
-    def forward(ctx, x, W, b, act="none", grad=True, sink=None):
+    def forward(ctx, x, W, b, act="none", grad=True, sink=None, out_bf16=False):
         x = _c(x)
         ctx.sink = sink
         # the pre-activation is kept only for a backward that will run (none in the reference's dead
         # blocks, eval or decoding: an N-wide fp32 write saved per call)
         z = _E(*x.shape[:-1], W.shape[0], device=x.device) if act != "none" and grad else None
-        y = G.linear_fwd(x, W.view(W.shape[0], -1), b, act=act, preact=z)  # (N, K, 1): a 1x1 Conv1d weight
+        y = G.linear_fwd(x, W.view(W.shape[0], -1), b, act=act, preact=z,  # (N, K, 1): a 1x1 Conv1d weight
+                         out_bf16=out_bf16 and prec.bf16_storage())
         ctx.act = act
         ctx.has_b = b is not None
         if grad:
@@ -231,15 +235,16 @@ class Linear(torch.autograd.Function):
             dW = _gret(W3, gW, ctx.dW)
         if ctx.has_b and ctx.needs_input_grad[2]:
             db = _gret(b, colsum(gz, out=_gbuf(b, True) if ctx.db else None), ctx.db)
-        return dx, dW, db, None, None, None
+        return dx, dW, db, None, None, None, None
 
 
 def _grad_needed(*ts):
     return torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts)
 
 
-def linear(x, W, b=None, act="none"):
-    return Linear.apply(x, W, b, act, _grad_needed(x, W, b), sink_of(x))
+def linear(x, W, b=None, act="none", out_bf16=False):
+    """nn.Linear (+ act) on MFMA; out_bf16: the output only feeds GEMM operands (stored bf16 in perf mode)."""
+    return Linear.apply(x, W, b, act, _grad_needed(x, W, b), sink_of(x), out_bf16)
 
 
 class KVProjFn(torch.autograd.Function):
@@ -248,11 +253,11 @@ class KVProjFn(torch.autograd.Function):
     (beta = 1) and the weight / bias gradients written into the blocks of p.grad."""
 
     @staticmethod
-    def forward(ctx, x, W, b, sink):
+    def forward(ctx, x, W, b, sink, v_bf16=False):
         x = _c(x)
         D = W.shape[0] // 2
         k = G.linear_fwd(x, W[:D], b[:D])
-        v = G.linear_fwd(x, W[D:], b[D:])
+        v = G.linear_fwd(x, W[D:], b[D:], out_bf16=v_bf16)  # v only feeds attention
         ctx.sink = sink
         ctx.dW, ctx.db = _direct(ctx, 1, W), _direct(ctx, 2, b)
         ctx.save_for_backward(x, W, b)
@@ -290,11 +295,11 @@ class KVProjFn(torch.autograd.Function):
                 if gpart is not None:
                     colsum(gpart.view(-1, D), out=gb[i * D:(i + 1) * D])
             dbf = _gret(b, gb, ctx.db)
-        return dx, dWf, dbf, None
+        return dx, dWf, dbf, None, None
 
 
 def kv_proj(x, W, b):
-    return KVProjFn.apply(x, W, b, sink_of(x))
+    return KVProjFn.apply(x, W, b, sink_of(x), prec.attn_bf16_io())
 
 
 def colsum(x2, out=None):
@@ -345,24 +350,27 @@ class AbbyNormalFn(torch.autograd.Function):
     """essentials.AbbyNormal (essentials.py:155-191): router GEMM on MFMA + fused row kernel."""
 
     @staticmethod
-    def forward(ctx, x, W1, b1, W2, b2, L, H, sid_base, key, use_noise, keep, sink=None):
+    def forward(ctx, x, W1, b1, W2, b2, L, H, sid_base, key, use_noise, keep, sink=None, out_bf16=False):
         x = _c(x)
         ctx.sink = sink
         d = x.shape[-1]
         rows = _rows(x)
-        out = _E(x.shape, device=x.device)
+        ob = int(out_bf16 and prec.bf16_storage())
+        out = _E(x.shape, device=x.device, dtype=torch.bfloat16 if ob else torch.float32)
         ys = _E(rows, 3, device=x.device)
         idx = _E(rows, dtype=torch.int32, device=x.device)
         if G.use_wide(d) and d <= 384:
             # perf mode: the router's d x d GEMM also applies SiLU and Linear(d, 3) in its epilogue,
             # so h_pre never makes the HBM round trip unless the backward needs it
             hpre, logits = G.router_fwd(x.view(rows, d), W1, b1, W2, keep)
-            lib.call("asrx_abby_fwd_logits", _P(x), _P(logits), _P(b2), _P(out), _P(ys), _P(idx), rows, d, L, H,
+            lib.call("asrx_abby_fwd_logits2", _P(x), _P(logits), _P(b2), _P(out), ob, _P(ys), _P(idx), rows, d, L, H,
                      sid_base, key & 0xFFFFFFFF, int(use_noise), _S())
         else:
             hpre = G.linear_fwd(x, W1, b1)
-            lib.call("asrx_abby_fwd", _P(x), _P(hpre), _P(W2), _P(b2), _P(out), _P(ys), _P(idx), rows, d, L, H,
+            lib.call("asrx_abby_fwd2", _P(x), _P(hpre), _P(W2), _P(b2), _P(out), ob, _P(ys), _P(idx), rows, d, L, H,
                      sid_base, key & 0xFFFFFFFF, int(use_noise), _S())
+        if decisions.active():
+            decisions.abby(key & 0xFFFFFFFF, sid_base, L, H, idx)
         ctx.dp = [_direct(ctx, i, t) for i, t in ((1, W1), (2, b1), (3, W2), (4, b2))]
         ctx.save_for_backward(x, hpre, W1, W2, ys, idx, b1, b2)
         return out
@@ -388,16 +396,17 @@ class AbbyNormalFn(torch.autograd.Function):
         dW1 = G.linear_wgrad(dh, x, out=_gbuf(W1, fW1), accumulate=True)
         db1 = colsum(dh.view(-1, d), out=_gbuf(b1, fb1))
         return (dx, _gret(W1, dW1, fW1), _gret(b1, db1, fb1), _gret(W2, dW2, fW2), _gret(b2, db2, fb2),
-                None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None)
 
 
-def abby_normal(mod, x, L, H, sid_base, key, use_noise=True):
+def abby_normal(mod, x, L, H, sid_base, key, use_noise=True, out_bf16=False):
+    """AbbyNormal(x); out_bf16: the output only feeds GEMM / attention operands (bf16-stored in perf mode)."""
     if use_noise:
         _noise_rows_ok(sid_base + _rows(x) // max(L * H, 1), H, L, 3)
     r = mod.mode_router
     keep = torch.is_grad_enabled() and (x.requires_grad or r[0].weight.requires_grad)
     return AbbyNormalFn.apply(x, r[0].weight, r[0].bias, r[2].weight, r[2].bias, L, H, sid_base, key, use_noise,
-                              keep, sink_of(x))
+                              keep, sink_of(x), out_bf16)
 
 
 # =============================================================================== LayerNorm
@@ -447,22 +456,31 @@ def _addr(arr):
 
 
 class AttentionFn(torch.autograd.Function):
-    """SDPA(q, k, v, is_causal) (model.py:307) on (B, L, H, 64) views; scale 1/sqrt(64)."""
+    """SDPA(q, k, v, is_causal) (model.py:307) on (B, L, H, hd) views; scale 1/sqrt(hd).  q / k / v are
+    stored fp32 or bf16 (all the same); o is stored bf16 when out_bf16 (it only feeds the out
+    projection) -- bf16 storage needs the bf16 flash kernels."""
 
     @staticmethod
-    def forward(ctx, q, k, v, causal):
+    def forward(ctx, q, k, v, causal, out_bf16=False):
         B, Lq, H, hd = q.shape
         Lk = k.shape[1]
-        o = _E(B, Lq, H, hd, device=q.device)
+        ap = prec.attention_prec()
+        ib = G.is_bf16(q)
+        if not (G.is_bf16(k) == ib and G.is_bf16(v) == ib) or (ib and ap != prec.PREC_BF16):
+            q, k, v = q.float(), k.float(), v.float()  # mixed or non-bf16-kernel: fp32 storage
+            ib = False
+        ob = bool(out_bf16) and ap == prec.PREC_BF16 and prec.bf16_storage()
+        o = _E(B, Lq, H, hd, device=q.device, dtype=torch.bfloat16 if ob else torch.float32)
         lse = _E(B, H, Lq, device=q.device)
         sq, sk, sv, so = _st3(q), _st3(k), _st3(v), _st3(o)
-        p = prec.get()
+        io = int(ib) | (2 * int(ob))
         e0 = probe.begin("attn")
-        lib.call("asrx_attn_fwd", prec.attention_prec(), _P(q), _addr(sq), _P(k), _addr(sk), _P(v), _addr(sv), _P(o), _addr(so),
+        lib.call("asrx_attn_fwd2", ap, io, _P(q), _addr(sq), _P(k), _addr(sk), _P(v), _addr(sv), _P(o), _addr(so),
                  _P(lse), B, H, Lq, Lk, hd, int(causal), 1.0 / math.sqrt(hd), _S())
-        probe.end("attn", e0, 4.0 * B * H * Lq * Lk * hd * (0.5 if causal else 1.0))
+        probe.end("attn", e0, 4.0 * B * H * Lq * Lk * hd * (0.5 if causal else 1.0), ("attn", Lq, Lk, io))
         ctx.causal = causal
-        ctx.prec = p
+        ctx.prec = prec.get()
+        ctx.io = io
         ctx.save_for_backward(q, k, v, o, lse)
         return o
 
@@ -476,16 +494,17 @@ class AttentionFn(torch.autograd.Function):
         dk = _E(k.shape, device=q.device)
         dv = _E(v.shape, device=q.device)
         delta = _E(B, H, Lq, device=q.device)
+        io = ctx.io | (4 * int(G.is_bf16(go)))
         arrs = [_st3(t) for t in (q, k, v, o, go, dq, dk, dv)]
-        lib.call("asrx_attn_bwd", ctx.prec, _P(q), _addr(arrs[0]), _P(k), _addr(arrs[1]), _P(v), _addr(arrs[2]),
+        lib.call("asrx_attn_bwd2", ctx.prec, io, _P(q), _addr(arrs[0]), _P(k), _addr(arrs[1]), _P(v), _addr(arrs[2]),
                  _P(o), _addr(arrs[3]), _P(go), _addr(arrs[4]), _P(lse), _P(delta), _P(dq), _addr(arrs[5]), _P(dk),
                  _addr(arrs[6]), _P(dv), _addr(arrs[7]), B, H, Lq, Lk, hd, int(ctx.causal), 1.0 / math.sqrt(hd),
                  _S())
-        return dq, dk, dv, None
+        return dq, dk, dv, None, None
 
 
-def attention(q, k, v, causal):
-    return AttentionFn.apply(q, k, v, causal)
+def attention(q, k, v, causal, out_bf16=False):
+    return AttentionFn.apply(q, k, v, causal, out_bf16)
 
 
 # =============================================================================== rotary
@@ -605,7 +624,7 @@ class TGateFn(torch.autograd.Function):
     (asrx_add_segments / colsum over column blocks) instead of autograd's cat backward + adds."""
 
     @staticmethod
-    def forward(ctx, x, W0, W1, W2, b0, b1, b2, Wcs, bcs):
+    def forward(ctx, x, W0, W1, W2, b0, b1, b2, Wcs, bcs, out_bf16=False):
         x = _c(x)
         D = x.shape[-1]
         rows = _rows(x)
@@ -615,9 +634,11 @@ class TGateFn(torch.autograd.Function):
         lib.call("asrx_cat3", _P(b0), _P(b1), _P(b2), D, _P(bcat), _S())
         Gs = G.linear_fwd(x, Wcat, bcat, act="sigmoid")
         c = _E(rows, 3, device=x.device)
-        lib.call("asrx_small_linear_fwd", _P(x), _P(Wcs), _P(bcs), _P(c), rows, D, 3, 0, _S())
-        out = _E(x.shape, device=x.device)
-        lib.call("asrx_tgate_fwd", _P(Gs), _P(c), _P(out), rows, D, _S())
+        xb = int(G.is_bf16(x))
+        lib.call("asrx_small_linear_fwd2", _P(x), xb, _P(Wcs), _P(bcs), _P(c), rows, D, 3, 0, _S())
+        ob = int(out_bf16 and prec.bf16_storage())
+        out = _E(x.shape, device=x.device, dtype=torch.bfloat16 if ob else torch.float32)
+        lib.call("asrx_tgate_fwd2", _P(Gs), _P(c), _P(out), ob, rows, D, _S())
         ctx.dWcs, ctx.dbcs = _direct(ctx, 7, Wcs), _direct(ctx, 8, bcs)
         ctx.dparts = all(_direct(ctx, k, t) for k, t in enumerate((W0, W1, W2, b0, b1, b2), 1))
         ctx.save_for_backward(x, Wcat, Wcs, Gs, c, bcs, W0, W1, W2, b0, b1, b2)
@@ -634,8 +655,8 @@ class TGateFn(torch.autograd.Function):
         lib.call("asrx_tgate_bwd", _P(gout), _P(Gs), _P(c), _P(dGz), _P(dc), rows, D, _S())
         dx = G.linear_dgrad(dGz, Wcat)
         dWcs, dbcs = _gbuf(Wcs, ctx.dWcs), _gbuf(bcs, ctx.dbcs)
-        lib.call("asrx_small_linear_bwd", _P(dc), None, _P(x), _P(Wcs), _P(dx), _P(dWcs), _P(dbcs), rows, D, 3, 0,
-                 1.0, _S())
+        lib.call("asrx_small_linear_bwd2", _P(dc), None, _P(x), int(G.is_bf16(x)), _P(Wcs), _P(dx), _P(dWcs), _P(dbcs),
+                 rows, D, 3, 0, 1.0, _S())
         dWcat = _E(3 * D, D, device=x.device)
         lib.call("asrx_zero", _P(dWcat), dWcat.numel() * 4, _S())
         G.linear_wgrad(dGz, x, out=dWcat, accumulate=True)
@@ -651,12 +672,13 @@ class TGateFn(torch.autograd.Function):
             gW = [dWcat[k * D:(k + 1) * D] for k in range(3)]
             dbcat = colsum(dGz)
             gB = [dbcat[k * D:(k + 1) * D] for k in range(3)]
-        return (dx.view(x.shape), *gW, *gB, _gret(Wcs, dWcs, ctx.dWcs), _gret(bcs, dbcs, ctx.dbcs))
+        return (dx.view(x.shape), *gW, *gB, _gret(Wcs, dWcs, ctx.dWcs), _gret(bcs, dbcs, ctx.dbcs), None)
 
 
-def tgate(mod, x):
+def tgate(mod, x, out_bf16=False):
+    """tgate (model.py:525-535); x fp32 or bf16-stored; out_bf16: the output only feeds a GEMM."""
     return TGateFn.apply(x, *[g[0].weight for g in mod.ga], *[g[0].bias for g in mod.ga], mod.cs[0].weight,
-                         mod.cs[0].bias)
+                         mod.cs[0].bias, out_bf16)
 
 
 # =============================================================================== elementwise

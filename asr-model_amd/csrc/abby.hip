@@ -71,6 +71,19 @@ __device__ __forceinline__ void ld_row(const float* __restrict__ src, int lane, 
   }
 }
 
+// bf16 storage (the output of an AbbyNormal whose only consumers are GEMM / attention operands)
+__device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
+  return (unsigned)__builtin_bit_cast(unsigned short, (__bf16)a) |
+         ((unsigned)__builtin_bit_cast(unsigned short, (__bf16)b) << 16);
+}
+template <int E>
+__device__ __forceinline__ void st_row(unsigned short* __restrict__ dst, int lane, const float (&v)[E]) {
+  static_assert(E % 2 == 0, "bf16 rows store feature pairs");
+  unsigned* d2 = reinterpret_cast<unsigned*>(dst + lane * E);
+#pragma unroll
+  for (int e = 0; e < E / 2; ++e) d2[e] = pack_bf16x2(v[2 * e], v[2 * e + 1]);
+}
+
 template <int E>
 __device__ __forceinline__ void st_row(float* __restrict__ dst, int lane, const float (&v)[E]) {
   if constexpr (E % 2 == 0) {
@@ -162,12 +175,12 @@ __device__ __forceinline__ float abby_denom(float div, float& base) {
   return __builtin_amdgcn_exp2f(0.75f * __builtin_amdgcn_logf(base));  // base^0.75, base >= 1
 }
 
-template <int E>
+template <int E, typename TO = float>
 __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_fwd_kernel(const float* __restrict__ x,
                                                                   const float* __restrict__ hpre,
                                                                   const float* __restrict__ W2,
                                                                   const float* __restrict__ b2,
-                                                                  float* __restrict__ out, float* __restrict__ ys,
+                                                                  TO* __restrict__ out, float* __restrict__ ys,
                                                                   int* __restrict__ idx_out, AbbyGeom g,
                                                                   const float* __restrict__ logits) {
   typedef AbbyShape<E> S;
@@ -496,6 +509,9 @@ __device__ __forceinline__ Row64 ld64(const float* p) {
 __device__ __forceinline__ void st64(float* p, const float (&v)[4]) {
   *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
 }
+__device__ __forceinline__ void st64(unsigned short* p, const float (&v)[4]) {
+  *reinterpret_cast<uint2*>(p) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+}
 
 // x^2 halo of the lane's 4 features: h[0] = feature 4l - 1, h[1..4] own, h[5] = feature 4l + 4
 __device__ __forceinline__ void halo64(const float (&sq)[4], float (&h)[6]) {
@@ -517,11 +533,12 @@ __device__ __forceinline__ void stats64(const float (&xv)[4], float& mu, float& 
   sd = sqrtf(row16_sum(v) / 63.f);
 }
 
+template <typename TO = float>
 __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_fwd64_kernel(const float* __restrict__ x,
                                                                     const float* __restrict__ hpre,
                                                                     const float* __restrict__ W2,
                                                                     const float* __restrict__ b2,
-                                                                    float* __restrict__ out, float* __restrict__ ys,
+                                                                    TO* __restrict__ out, float* __restrict__ ys,
                                                                     int* __restrict__ idx_out, AbbyGeom g,
                                                                     const float* __restrict__ logits) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, l16 = lane & 15;
@@ -724,6 +741,17 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_bwd64_kernel(
 
 using namespace asrx;
 
+#define ABBY_DISPATCH_T(KERNEL, TO, ...)                                                      \
+  switch (E) {                                                                               \
+    case 2: KERNEL<2, TO><<<grid, 64 * ABBY_WAVES, 0, stream>>>(__VA_ARGS__); break;         \
+    case 4: KERNEL<4, TO><<<grid, 64 * ABBY_WAVES, 0, stream>>>(__VA_ARGS__); break;         \
+    case 6: KERNEL<6, TO><<<grid, 64 * ABBY_WAVES, 0, stream>>>(__VA_ARGS__); break;         \
+    case 8: KERNEL<8, TO><<<grid, 64 * ABBY_WAVES, 0, stream>>>(__VA_ARGS__); break;         \
+    case 12: KERNEL<12, TO><<<grid, 64 * ABBY_WAVES, 0, stream>>>(__VA_ARGS__); break;       \
+    case 16: KERNEL<16, TO><<<grid, 64 * ABBY_WAVES, 0, stream>>>(__VA_ARGS__); break;       \
+    default: set_error("AbbyNormal: unsupported d=%ld", (long)d); return 2;                  \
+  }
+
 #define ABBY_DISPATCH(KERNEL, ...)                                                 \
   switch (E) {                                                                     \
     case 1: KERNEL<1><<<grid, 64 * ABBY_WAVES, 0, stream>>>(__VA_ARGS__); break;   \
@@ -750,10 +778,11 @@ static AbbyGeom make_geom(int64_t rows, int64_t d, int64_t L, int64_t H, int64_t
   return g;
 }
 
-// x, hpre: (rows, d); W2 (3, d), b2 (3); out (rows, d); ys (rows, 3); idx (rows) int32.
-extern "C" int asrx_abby_fwd(const float* x, const float* hpre, const float* W2, const float* b2, float* out,
-                             float* ys, int* idx, int64_t rows, int64_t d, int64_t L, int64_t H,
-                             int64_t sid_base, uint32_t key, int use_noise, hipStream_t stream) {
+// x, hpre: (rows, d); W2 (3, d), b2 (3); out (rows, d) fp32 (out_bf16 = 0) or bf16 (1); ys (rows, 3);
+// idx (rows) int32.
+extern "C" int asrx_abby_fwd2(const float* x, const float* hpre, const float* W2, const float* b2, void* out,
+                              int out_bf16, float* ys, int* idx, int64_t rows, int64_t d, int64_t L, int64_t H,
+                              int64_t sid_base, uint32_t key, int use_noise, hipStream_t stream) {
   ASRX_REQUIRE(d % 64 == 0 && d >= 64 && d <= 1024, "AbbyNormal: d=%ld must be a multiple of 64 in [64,1024]",
                (long)d);
   if (rows == 0) return 0;
@@ -762,17 +791,32 @@ extern "C" int asrx_abby_fwd(const float* x, const float* hpre, const float* W2,
   const unsigned grid = (unsigned)std::min<int64_t>((rows + ABBY_WAVES - 1) / ABBY_WAVES, 4096);
   if (d == 64) {
     const unsigned g64 = (unsigned)std::min<int64_t>((rows + 4 * ABBY_WAVES - 1) / (4 * ABBY_WAVES), 4096);
-    abby_fwd64_kernel<<<g64, 64 * ABBY_WAVES, 0, stream>>>(x, hpre, W2, b2, out, ys, idx, g, nullptr);
+    if (out_bf16)
+      abby_fwd64_kernel<unsigned short><<<g64, 64 * ABBY_WAVES, 0, stream>>>(x, hpre, W2, b2, (unsigned short*)out, ys,
+                                                                           idx, g, nullptr);
+    else
+      abby_fwd64_kernel<float><<<g64, 64 * ABBY_WAVES, 0, stream>>>(x, hpre, W2, b2, (float*)out, ys, idx, g, nullptr);
     ASRX_LAUNCHED("asrx_abby_fwd");
   }
-  ABBY_DISPATCH(abby_fwd_kernel, x, hpre, W2, b2, out, ys, idx, g, nullptr);
+  if (out_bf16) {
+    ABBY_DISPATCH_T(abby_fwd_kernel, unsigned short, x, hpre, W2, b2, (unsigned short*)out, ys, idx, g, nullptr);
+  } else {
+    ABBY_DISPATCH_T(abby_fwd_kernel, float, x, hpre, W2, b2, (float*)out, ys, idx, g, nullptr);
+  }
   ASRX_LAUNCHED("asrx_abby_fwd");
 }
 
-// Same, with the router logits (rows x 3, without b2) precomputed by asrx_gemm_wn_router.
-extern "C" int asrx_abby_fwd_logits(const float* x, const float* logits, const float* b2, float* out, float* ys,
-                                    int* idx, int64_t rows, int64_t d, int64_t L, int64_t H, int64_t sid_base,
-                                    uint32_t key, int use_noise, hipStream_t stream) {
+extern "C" int asrx_abby_fwd(const float* x, const float* hpre, const float* W2, const float* b2, float* out,
+                             float* ys, int* idx, int64_t rows, int64_t d, int64_t L, int64_t H,
+                             int64_t sid_base, uint32_t key, int use_noise, hipStream_t stream) {
+  return asrx_abby_fwd2(x, hpre, W2, b2, out, 0, ys, idx, rows, d, L, H, sid_base, key, use_noise, stream);
+}
+
+// Same, with the router logits (rows x 3, without b2) precomputed by asrx_gemm_wn_router; out is stored
+// fp32 (out_bf16 = 0) or bf16 (1).
+extern "C" int asrx_abby_fwd_logits2(const float* x, const float* logits, const float* b2, void* out, int out_bf16,
+                                     float* ys, int* idx, int64_t rows, int64_t d, int64_t L, int64_t H,
+                                     int64_t sid_base, uint32_t key, int use_noise, hipStream_t stream) {
   ASRX_REQUIRE(d % 64 == 0 && d >= 64 && d <= 1024, "AbbyNormal: d=%ld must be a multiple of 64 in [64,1024]",
                (long)d);
   if (rows == 0) return 0;
@@ -781,11 +825,26 @@ extern "C" int asrx_abby_fwd_logits(const float* x, const float* logits, const f
   const unsigned grid = (unsigned)std::min<int64_t>((rows + ABBY_WAVES - 1) / ABBY_WAVES, 4096);
   if (d == 64) {
     const unsigned g64 = (unsigned)std::min<int64_t>((rows + 4 * ABBY_WAVES - 1) / (4 * ABBY_WAVES), 4096);
-    abby_fwd64_kernel<<<g64, 64 * ABBY_WAVES, 0, stream>>>(x, nullptr, nullptr, b2, out, ys, idx, g, logits);
+    if (out_bf16)
+      abby_fwd64_kernel<unsigned short><<<g64, 64 * ABBY_WAVES, 0, stream>>>(x, nullptr, nullptr, b2,
+                                                                           (unsigned short*)out, ys, idx, g, logits);
+    else
+      abby_fwd64_kernel<float><<<g64, 64 * ABBY_WAVES, 0, stream>>>(x, nullptr, nullptr, b2, (float*)out, ys, idx, g,
+                                                                  logits);
     ASRX_LAUNCHED("asrx_abby_fwd_logits");
   }
-  ABBY_DISPATCH(abby_fwd_kernel, x, nullptr, nullptr, b2, out, ys, idx, g, logits);
+  if (out_bf16) {
+    ABBY_DISPATCH_T(abby_fwd_kernel, unsigned short, x, nullptr, nullptr, b2, (unsigned short*)out, ys, idx, g, logits);
+  } else {
+    ABBY_DISPATCH_T(abby_fwd_kernel, float, x, nullptr, nullptr, b2, (float*)out, ys, idx, g, logits);
+  }
   ASRX_LAUNCHED("asrx_abby_fwd_logits");
+}
+
+extern "C" int asrx_abby_fwd_logits(const float* x, const float* logits, const float* b2, float* out, float* ys,
+                                    int* idx, int64_t rows, int64_t d, int64_t L, int64_t H, int64_t sid_base,
+                                    uint32_t key, int use_noise, hipStream_t stream) {
+  return asrx_abby_fwd_logits2(x, logits, b2, out, 0, ys, idx, rows, d, L, H, sid_base, key, use_noise, stream);
 }
 
 // dW2 / db2 are accumulated (caller zeroes them).  dx (acc == 0) and dhpre are overwritten; acc != 0

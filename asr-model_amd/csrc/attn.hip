@@ -188,9 +188,15 @@ __global__ __launch_bounds__(256) void attn_fwd_f32_kernel(const float* __restri
   }
 }
 
-// delta[b,h,i] = sum_d dO[b,i,h,d] * O[b,i,h,d]   (one wave per row, HD/64 elements per lane)
-template <int HD>
-__global__ __launch_bounds__(256) void attn_delta_kernel(const float* __restrict__ o, const float* __restrict__ dO,
+__device__ __forceinline__ float ld_f(const float* p) { return *p; }
+__device__ __forceinline__ float ld_f(const unsigned short* p) {
+  return __uint_as_float((unsigned)*p << 16);
+}
+
+// delta[b,h,i] = sum_d dO[b,i,h,d] * O[b,i,h,d]   (one wave per row, HD/64 elements per lane);
+// o / dO stored fp32 or bf16 (unsigned short)
+template <int HD, typename TO = float, typename TD = float>
+__global__ __launch_bounds__(256) void attn_delta_kernel(const TO* __restrict__ o, const TD* __restrict__ dO,
                                                          float* __restrict__ delta, AttnStrides so, AttnStrides sd,
                                                          int64_t B, int64_t H, int64_t Lq) {
   const int lane = threadIdx.x & 63;
@@ -200,7 +206,8 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const float* __restrict
     float s = 0.f;
 #pragma unroll
     for (int e = 0; e < HD / 64; ++e)
-      s += o[bb * so.b + i * so.l + hh * so.h + 64 * e + lane] * dO[bb * sd.b + i * sd.l + hh * sd.h + 64 * e + lane];
+      s += ld_f(o + bb * so.b + i * so.l + hh * so.h + 64 * e + lane) *
+           ld_f(dO + bb * sd.b + i * sd.l + hh * sd.h + 64 * e + lane);
     s = wave_sum(s);
     if (lane == 0) delta[r] = s;
   }
@@ -370,11 +377,11 @@ static bool attn_ok(const int64_t* st) { return st[0] % 4 == 0 && st[1] % 4 == 0
 
 // Strides are passed as int64[3] = {batch, seq, head} in elements; the head-dim stride must be 1.
 namespace asrx {
-int attn_fwd_mf(const float* q, const int64_t* sq, const float* k, const int64_t* sk, const float* v,
-                const int64_t* sv, float* o, const int64_t* so, float* lse, int64_t B, int64_t H, int64_t Lq,
+int attn_fwd_mf(int io, const void* q, const int64_t* sq, const void* k, const int64_t* sk, const void* v,
+                const int64_t* sv, void* o, const int64_t* so, float* lse, int64_t B, int64_t H, int64_t Lq,
                 int64_t Lk, int64_t hd, int causal, float scale, hipStream_t stream);
-int attn_bwd_mf(const float* q, const int64_t* sq, const float* k, const int64_t* sk, const float* v,
-                const int64_t* sv, const float* dO, const int64_t* sd, const float* lse, const float* delta,
+int attn_bwd_mf(int io, const void* q, const int64_t* sq, const void* k, const int64_t* sk, const void* v,
+                const int64_t* sv, const void* dO, const int64_t* sd, const float* lse, const float* delta,
                 float* dq, const int64_t* sdq, float* dk, const int64_t* sdk, float* dv, const int64_t* sdv,
                 int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t hd, int causal, float scale,
                 hipStream_t stream);
@@ -405,10 +412,13 @@ static void attn_bwd_f32(const float* q, AttnStrides Sq, const float* k, AttnStr
                                                      causal, scale);
 }
 
-extern "C" int asrx_attn_fwd(int prec, const float* q, const int64_t* sq, const float* k, const int64_t* sk,
-                             const float* v, const int64_t* sv, float* o, const int64_t* so, float* lse, int64_t B,
-                             int64_t H, int64_t Lq, int64_t Lk, int64_t hd, int causal, float scale,
-                             hipStream_t stream) {
+extern "C" int asrx_attn_fwd2(int prec, int io, const void* q_, const int64_t* sq, const void* k_, const int64_t* sk,
+                              const void* v_, const int64_t* sv, void* o_, const int64_t* so, float* lse, int64_t B,
+                              int64_t H, int64_t Lq, int64_t Lk, int64_t hd, int causal, float scale,
+                              hipStream_t stream) {
+  const float *q = (const float*)q_, *k = (const float*)k_, *v = (const float*)v_;
+  float* o = (float*)o_;
+  ASRX_REQUIRE(io == 0 || prec == PREC_BF16, "attention: bf16 storage (io %d) is a bf16-mode layout", io);
   ASRX_REQUIRE(hd == 64 || hd == 128, "attention: head dim %ld unsupported (64 or 128)", (long)hd);
   ASRX_REQUIRE(attn_ok(sq) && attn_ok(sk) && attn_ok(sv) && attn_ok(so), "attention: strides must be multiples of 4");
   ASRX_REQUIRE(H < 65536 && B < 65536, "attention: grid too large");
@@ -421,7 +431,7 @@ extern "C" int asrx_attn_fwd(int prec, const float* q, const int64_t* sq, const 
   if (prec == PREC_FP8ATT)
     attn_fwd_f8(q, sq, k, sk, v, sv, o, so, lse, B, H, Lq, Lk, hd, causal, scale, stream);
   else if (prec == PREC_BF16)
-    attn_fwd_mf(q, sq, k, sk, v, sv, o, so, lse, B, H, Lq, Lk, hd, causal, scale, stream);
+    attn_fwd_mf(io, q, sq, k, sk, v, sv, o, so, lse, B, H, Lq, Lk, hd, causal, scale, stream);
   else if (hd == 64)
     attn_fwd_f32<64>(q, Sq, k, Sk, v, Sv, o, So, lse, B, H, Lq, Lk, causal, scale, stream);
   else
@@ -429,12 +439,22 @@ extern "C" int asrx_attn_fwd(int prec, const float* q, const int64_t* sq, const 
   ASRX_LAUNCHED("asrx_attn_fwd");
 }
 
+extern "C" int asrx_attn_fwd(int prec, const float* q, const int64_t* sq, const float* k, const int64_t* sk,
+                             const float* v, const int64_t* sv, float* o, const int64_t* so, float* lse, int64_t B,
+                             int64_t H, int64_t Lq, int64_t Lk, int64_t hd, int causal, float scale,
+                             hipStream_t stream) {
+  return asrx_attn_fwd2(prec, 0, q, sq, k, sk, v, sv, o, so, lse, B, H, Lq, Lk, hd, causal, scale, stream);
+}
+
 // delta_ws: workspace of B*H*Lq floats.
-extern "C" int asrx_attn_bwd(int prec, const float* q, const int64_t* sq, const float* k, const int64_t* sk,
-                             const float* v, const int64_t* sv, const float* o, const int64_t* so, const float* dO,
-                             const int64_t* sd, const float* lse, float* delta_ws, float* dq, const int64_t* sdq,
-                             float* dk, const int64_t* sdk, float* dv, const int64_t* sdv, int64_t B, int64_t H,
-                             int64_t Lq, int64_t Lk, int64_t hd, int causal, float scale, hipStream_t stream) {
+extern "C" int asrx_attn_bwd2(int prec, int io, const void* q_, const int64_t* sq, const void* k_, const int64_t* sk,
+                              const void* v_, const int64_t* sv, const void* o_, const int64_t* so, const void* dO_,
+                              const int64_t* sd, const float* lse, float* delta_ws, float* dq, const int64_t* sdq,
+                              float* dk, const int64_t* sdk, float* dv, const int64_t* sdv, int64_t B, int64_t H,
+                              int64_t Lq, int64_t Lk, int64_t hd, int causal, float scale, hipStream_t stream) {
+  const float *q = (const float*)q_, *k = (const float*)k_, *v = (const float*)v_, *o = (const float*)o_;
+  const float* dO = (const float*)dO_;
+  ASRX_REQUIRE(io == 0 || prec == PREC_BF16, "attention backward: bf16 storage (io %d) is a bf16-mode layout", io);
   ASRX_REQUIRE(prec == PREC_F32 || prec == PREC_BF16, "attention backward: precision %d (fp8 is forward only)", prec);
   ASRX_REQUIRE(hd == 64 || hd == 128, "attention: head dim %ld unsupported (64 or 128)", (long)hd);
   ASRX_REQUIRE(attn_ok(sq) && attn_ok(sk) && attn_ok(sv) && attn_ok(sd) && attn_ok(sdq) && attn_ok(sdk) &&
@@ -447,16 +467,31 @@ extern "C" int asrx_attn_bwd(int prec, const float* q, const int64_t* sq, const 
       Sdv{sdv[0], sdv[1], sdv[2]};
   const int64_t rows = B * H * Lq;
   const unsigned gd = (unsigned)std::min<int64_t>((rows + 3) / 4, 8192);
-  if (hd == 64)
-    attn_delta_kernel<64><<<gd, 256, 0, stream>>>(o, dO, delta_ws, So, Sd, B, H, Lq);
-  else
-    attn_delta_kernel<128><<<gd, 256, 0, stream>>>(o, dO, delta_ws, So, Sd, B, H, Lq);
+#define ASRX_DL(HDV, TO, TD) \
+  attn_delta_kernel<HDV, TO, TD><<<gd, 256, 0, stream>>>((const TO*)o_, (const TD*)dO_, delta_ws, So, Sd, B, H, Lq)
+  const int dsel = ((io >> 1) & 1) | ((io >> 1) & 2);  // bit 0: o bf16, bit 1: dO bf16
+  if (hd == 64) {
+    switch (dsel) {
+      case 0: ASRX_DL(64, float, float); break;
+      case 1: ASRX_DL(64, unsigned short, float); break;
+      case 2: ASRX_DL(64, float, unsigned short); break;
+      default: ASRX_DL(64, unsigned short, unsigned short); break;
+    }
+  } else {
+    switch (dsel) {
+      case 0: ASRX_DL(128, float, float); break;
+      case 1: ASRX_DL(128, unsigned short, float); break;
+      case 2: ASRX_DL(128, float, unsigned short); break;
+      default: ASRX_DL(128, unsigned short, unsigned short); break;
+    }
+  }
+#undef ASRX_DL
   const bool al16 = (((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)dO | (uintptr_t)dq | (uintptr_t)dk |
                        (uintptr_t)dv) & 15) == 0;
   ASRX_REQUIRE(prec == PREC_F32 || al16, "attention backward: bf16 mode needs 16-byte aligned tensors");
   if (prec == PREC_BF16)
-    attn_bwd_mf(q, sq, k, sk, v, sv, dO, sd, lse, delta_ws, dq, sdq, dk, sdk, dv, sdv, B, H, Lq, Lk, hd, causal, scale,
-                stream);
+    attn_bwd_mf(io, q, sq, k, sk, v, sv, dO, sd, lse, delta_ws, dq, sdq, dk, sdk, dv, sdv, B, H, Lq, Lk, hd, causal,
+                scale, stream);
   else if (hd == 64)
     attn_bwd_f32<64>(q, Sq, k, Sk, v, Sv, dO, Sd, lse, delta_ws, dq, Sdq, dk, Sdk, dv, Sdv, B, H, Lq, Lk, causal, scale,
                      stream);
@@ -464,4 +499,13 @@ extern "C" int asrx_attn_bwd(int prec, const float* q, const int64_t* sq, const 
     attn_bwd_f32<128>(q, Sq, k, Sk, v, Sv, dO, Sd, lse, delta_ws, dq, Sdq, dk, Sdk, dv, Sdv, B, H, Lq, Lk, causal,
                       scale, stream);
   ASRX_LAUNCHED("asrx_attn_bwd");
+}
+
+extern "C" int asrx_attn_bwd(int prec, const float* q, const int64_t* sq, const float* k, const int64_t* sk,
+                             const float* v, const int64_t* sv, const float* o, const int64_t* so, const float* dO,
+                             const int64_t* sd, const float* lse, float* delta_ws, float* dq, const int64_t* sdq,
+                             float* dk, const int64_t* sdk, float* dv, const int64_t* sdv, int64_t B, int64_t H,
+                             int64_t Lq, int64_t Lk, int64_t hd, int causal, float scale, hipStream_t stream) {
+  return asrx_attn_bwd2(prec, 0, q, sq, k, sk, v, sv, o, so, dO, sd, lse, delta_ws, dq, sdq, dk, sdk, dv, sdv, B, H, Lq,
+                        Lk, hd, causal, scale, stream);
 }

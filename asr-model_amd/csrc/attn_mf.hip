@@ -55,23 +55,51 @@ __device__ __forceinline__ bf16x8 pack8(const float (&v)[8]) {
   return __builtin_bit_cast(bf16x8, u);
 }
 
-// one 16-byte chunk (8 consecutive d of half `hf`) of one key row of a K or V tile: fp32 -> bf16
-// -> LDS.  Rows past Lk load the last row (always in bounds) and are zeroed, so there is no branch.
-__device__ __forceinline__ void stage_load(const float* base, AttnStridesMF st, int64_t key, int64_t Lk, int hf,
-                                           int c, float4& a, float4& b) {
+// Storage types of the attention operands: float (fp32) or bf16 (`bf16s`, the raw 16-bit pattern).
+// q / k / v in bf16 are what the producers (per-head AbbyNormal, the k/v projection) write when
+// attention is their only consumer: the kernels round fp32 inputs to bf16 anyway, so the products are
+// bit-identical and a bf16 input halves the bytes and drops the per-tile conversions.
+typedef unsigned short bf16s;
+
+// 8 consecutive elements of one row, as staged through registers
+template <typename T>
+struct Row8 {
+  float4 a, b;
+};
+template <>
+struct Row8<bf16s> {
+  uint4 u;
+};
+
+// one 16-byte chunk (8 consecutive d of half `hf`) of one key row of a K or V tile -> registers.
+// Rows past Lk load the last row (always in bounds) and are zeroed, so there is no branch.
+template <typename T>
+__device__ __forceinline__ void stage_load(const T* base, AttnStridesMF st, int64_t key, int64_t Lk, int hf, int c,
+                                           Row8<T>& x) {
   const int64_t kc = key < Lk ? key : Lk - 1;
-  const float* p = base + kc * st.l + 64 * hf + 8 * c;
-  a = *reinterpret_cast<const float4*>(p);
-  b = *reinterpret_cast<const float4*>(p + 4);
-  if (key >= Lk) {
-    a = make_float4(0.f, 0.f, 0.f, 0.f);
-    b = a;
+  const T* p = base + kc * st.l + 64 * hf + 8 * c;
+  if constexpr (sizeof(T) == 4) {
+    x.a = *reinterpret_cast<const float4*>(p);
+    x.b = *reinterpret_cast<const float4*>(p + 4);
+    if (key >= Lk) {
+      x.a = make_float4(0.f, 0.f, 0.f, 0.f);
+      x.b = x.a;
+    }
+  } else {
+    x.u = *reinterpret_cast<const uint4*>(p);
+    if (key >= Lk) x.u = make_uint4(0u, 0u, 0u, 0u);
   }
 }
-__device__ __forceinline__ void stage_store(unsigned short* tile, int key, int pc, const float4& a, const float4& b) {
+// registers -> the bf16 LDS image (fp32 rounded here)
+template <typename T>
+__device__ __forceinline__ void stage_store(unsigned short* tile, int key, int pc, const Row8<T>& x) {
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  u32x4 u = {pack2(a.x, a.y), pack2(a.z, a.w), pack2(b.x, b.y), pack2(b.z, b.w)};
-  *reinterpret_cast<u32x4*>(tile + key * 64 + 8 * pc) = u;
+  if constexpr (sizeof(T) == 4) {
+    u32x4 u = {pack2(x.a.x, x.a.y), pack2(x.a.z, x.a.w), pack2(x.b.x, x.b.y), pack2(x.b.z, x.b.w)};
+    *reinterpret_cast<u32x4*>(tile + key * 64 + 8 * pc) = u;
+  } else {
+    *reinterpret_cast<uint4*>(tile + key * 64 + 8 * pc) = x.u;
+  }
 }
 
 // A operand of X^T (d rows 32 dd.. of one 64-wide half, k = 16 rows of X in the MFMA-output order
@@ -91,18 +119,23 @@ __device__ __forceinline__ bf16x8 tr_frag(const unsigned short* X, int lane, int
 
 // register fragments (B operand of a d-contraction): row `row` of X, f[s] = d 64 (s/4) + 16 (s%4)
 // + 8 hi .. +7, as bf16; rows past `rows` are zero
-template <int HD>
-__device__ __forceinline__ void row_frags(const float* base, int64_t stride_l, int64_t row, int64_t rows, int hi,
+template <int HD, typename T>
+__device__ __forceinline__ void row_frags(const T* base, int64_t stride_l, int64_t row, int64_t rows, int hi,
                                           bf16x8 (&f)[HD / 16]) {
 #pragma unroll
   for (int s = 0; s < HD / 16; ++s) {
-    float t[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (row < rows) {
-      const float* p = base + row * stride_l + 64 * (s >> 2) + 16 * (s & 3) + 8 * hi;
-      const float4 x = *reinterpret_cast<const float4*>(p), y = *reinterpret_cast<const float4*>(p + 4);
-      t[0] = x.x; t[1] = x.y; t[2] = x.z; t[3] = x.w; t[4] = y.x; t[5] = y.y; t[6] = y.z; t[7] = y.w;
+    const T* p = base + row * stride_l + 64 * (s >> 2) + 16 * (s & 3) + 8 * hi;
+    if constexpr (sizeof(T) == 4) {
+      float t[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (row < rows) {
+        const float4 x = *reinterpret_cast<const float4*>(p), y = *reinterpret_cast<const float4*>(p + 4);
+        t[0] = x.x; t[1] = x.y; t[2] = x.z; t[3] = x.w; t[4] = y.x; t[5] = y.y; t[6] = y.z; t[7] = y.w;
+      }
+      f[s] = pack8(t);
+    } else {
+      const uint4 u = row < rows ? *reinterpret_cast<const uint4*>(p) : make_uint4(0u, 0u, 0u, 0u);
+      f[s] = __builtin_bit_cast(bf16x8, u);
     }
-    f[s] = pack8(t);
   }
 }
 
@@ -120,15 +153,20 @@ __device__ __forceinline__ void dot_rows(f32x16& acc, const unsigned short* X, i
 }
 
 // store a (32 rows on the lane) x HD accumulator set scaled by `sc` to row `r` of Y
-template <int HD>
-__device__ __forceinline__ void store_rowT(float* yr, const f32x16 (&acc)[HD / 32], float sc, int hi) {
+template <int HD, typename T = float>
+__device__ __forceinline__ void store_rowT(T* yr, const f32x16 (&acc)[HD / 32], float sc, int hi) {
 #pragma unroll
   for (int dd = 0; dd < HD / 32; ++dd)
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
       const int c = 64 * (dd >> 1) + 32 * (dd & 1) + 8 * g4 + 4 * hi;
-      *reinterpret_cast<float4*>(yr + c) =
-          make_float4(acc[dd][4 * g4] * sc, acc[dd][4 * g4 + 1] * sc, acc[dd][4 * g4 + 2] * sc, acc[dd][4 * g4 + 3] * sc);
+      if constexpr (sizeof(T) == 4) {
+        *reinterpret_cast<float4*>(yr + c) = make_float4(acc[dd][4 * g4] * sc, acc[dd][4 * g4 + 1] * sc,
+                                                         acc[dd][4 * g4 + 2] * sc, acc[dd][4 * g4 + 3] * sc);
+      } else {
+        *reinterpret_cast<uint2*>(yr + c) = make_uint2(pack2(acc[dd][4 * g4] * sc, acc[dd][4 * g4 + 1] * sc),
+                                                       pack2(acc[dd][4 * g4 + 2] * sc, acc[dd][4 * g4 + 3] * sc));
+      }
     }
 }
 
@@ -143,9 +181,10 @@ __device__ __forceinline__ int64_t xcd_logical(int64_t bid, int64_t G) {
 // WPE: waves per SIMD the register budget is sized for (1: one 8-wave workgroup per CU; 4: two).
 // XCD: 1-D grid remapped with xcd_logical.  PRIO: MFMA issue at raised wave priority (s_setprio),
 // so a SIMD's other wave fills the matrix-core gaps with its softmax VALU work.
-template <int HD, int WPE = 1, bool XCD = false, bool PRIO = false>
-__global__ __launch_bounds__(NTHR, WPE) void attn_fwd_mf_kernel(const float* __restrict__ q, const float* __restrict__ k,
-                                                              const float* __restrict__ v, float* __restrict__ o,
+// TI: storage type of q / k / v, TO: of o (float or bf16s).
+template <int HD, int WPE = 1, bool XCD = false, bool PRIO = false, typename TI = float, typename TO = float>
+__global__ __launch_bounds__(NTHR, WPE) void attn_fwd_mf_kernel(const TI* __restrict__ q, const TI* __restrict__ k,
+                                                              const TI* __restrict__ v, TO* __restrict__ o,
                                                               float* __restrict__ lse, AttnStridesMF sq,
                                                               AttnStridesMF sk, AttnStridesMF sv, AttnStridesMF so,
                                                               int64_t H, int64_t Lq, int64_t Lk, int causal,
@@ -170,8 +209,8 @@ __global__ __launch_bounds__(NTHR, WPE) void attn_fwd_mf_kernel(const float* __r
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int j = lane & 31, hi = lane >> 5;
   const int64_t qi = q0 + wid * 32 + j;  // this lane's query row
-  const float* kb = k + b * sk.b + h * sk.h;
-  const float* vb = v + b * sv.b + h * sv.h;
+  const TI* kb = k + b * sk.b + h * sk.h;
+  const TI* vb = v + b * sv.b + h * sv.h;
   const float c = scale * LOG2E;
 
   // Q^T fragments (B operand): lane (q = j, hi) holds Q[q][64 hf + 16 s + 8 hi .. +7]
@@ -183,13 +222,13 @@ __global__ __launch_bounds__(NTHR, WPE) void attn_fwd_mf_kernel(const float* __r
   const int ntiles = (int)((kend + KT - 1) / KT);
   const int skey = tid >> 3, sc = tid & 7;  // staging: one 16-B chunk of each half of one key row
 
-  float4 ka[NH], kb4[NH], va[NH], vb4[NH];
+  Row8<TI> ka[NH], va[NH];
 #pragma unroll
   for (int hf = 0; hf < NH; ++hf) {
-    stage_load(kb, sk, skey, Lk, hf, sc, ka[hf], kb4[hf]);
-    stage_load(vb, sv, skey, Lk, hf, sc, va[hf], vb4[hf]);
-    stage_store(Ks[0] + hf * HALF, skey, sc ^ kswz(skey), ka[hf], kb4[hf]);
-    stage_store(Vs[0] + hf * HALF, skey, sc ^ vswz(skey), va[hf], vb4[hf]);
+    stage_load(kb, sk, skey, Lk, hf, sc, ka[hf]);
+    stage_load(vb, sv, skey, Lk, hf, sc, va[hf]);
+    stage_store(Ks[0] + hf * HALF, skey, sc ^ kswz(skey), ka[hf]);
+    stage_store(Vs[0] + hf * HALF, skey, sc ^ vswz(skey), va[hf]);
   }
   __syncthreads();
 
@@ -207,8 +246,8 @@ __global__ __launch_bounds__(NTHR, WPE) void attn_fwd_mf_kernel(const float* __r
     if (t + 1 < ntiles) {  // next tile's loads fly under this tile's MFMAs
 #pragma unroll
       for (int hf = 0; hf < NH; ++hf) {
-        stage_load(kb, sk, k0 + KT + skey, Lk, hf, sc, ka[hf], kb4[hf]);
-        stage_load(vb, sv, k0 + KT + skey, Lk, hf, sc, va[hf], vb4[hf]);
+        stage_load(kb, sk, k0 + KT + skey, Lk, hf, sc, ka[hf]);
+        stage_load(vb, sv, k0 + KT + skey, Lk, hf, sc, va[hf]);
       }
     }
     const unsigned short* Kt = Ks[buf];
@@ -286,8 +325,8 @@ __global__ __launch_bounds__(NTHR, WPE) void attn_fwd_mf_kernel(const float* __r
     if (t + 1 < ntiles) {  // every wave finished reading buf^1 (tile t-1) before the last barrier
 #pragma unroll
       for (int hf = 0; hf < NH; ++hf) {
-        stage_store(Ks[buf ^ 1] + hf * HALF, skey, sc ^ kswz(skey), ka[hf], kb4[hf]);
-        stage_store(Vs[buf ^ 1] + hf * HALF, skey, sc ^ vswz(skey), va[hf], vb4[hf]);
+        stage_store(Ks[buf ^ 1] + hf * HALF, skey, sc ^ kswz(skey), ka[hf]);
+        stage_store(Vs[buf ^ 1] + hf * HALF, skey, sc ^ vswz(skey), va[hf]);
       }
     }
     __syncthreads();
@@ -296,7 +335,7 @@ __global__ __launch_bounds__(NTHR, WPE) void attn_fwd_mf_kernel(const float* __r
   // ---- finalize: l over both halves, O = O^T / l, lse in natural log
   const float lt = l + __shfl_xor(l, 32);
   if (qi < Lq) {
-    store_rowT<HD>(o + b * so.b + h * so.h + qi * so.l, oacc, 1.0f / lt, hi);
+    store_rowT<HD, TO>(o + b * so.b + h * so.h + qi * so.l, oacc, 1.0f / lt, hi);
     if (hi == 0) lse[((int64_t)b * H + h) * Lq + qi] = (m * c + __builtin_amdgcn_logf(lt)) * LN2;
   }
 }
@@ -324,10 +363,11 @@ struct BwdCfg {
 
 constexpr int BQT = 64;  // queries per tile of the dkdv loop
 
-template <int HD>
+// TI: storage type of q / k / v, TD: of dO (float or bf16s).
+template <int HD, typename TI = float, typename TD = float>
 __global__ __launch_bounds__(BwdCfg<HD>::NT, 1) void attn_bwd_dkdv_mf_kernel(
-    const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v,
-    const float* __restrict__ dO, const float* __restrict__ lse, const float* __restrict__ delta,
+    const TI* __restrict__ q, const TI* __restrict__ k, const TI* __restrict__ v,
+    const TD* __restrict__ dO, const float* __restrict__ lse, const float* __restrict__ delta,
     float* __restrict__ dk, float* __restrict__ dv, AttnStridesMF sq, AttnStridesMF sk, AttnStridesMF sv,
     AttnStridesMF sd, AttnStridesMF sdk, AttnStridesMF sdv, int64_t H, int64_t Lq, int64_t Lk, int causal,
     float scale) {
@@ -344,8 +384,8 @@ __global__ __launch_bounds__(BwdCfg<HD>::NT, 1) void attn_bwd_dkdv_mf_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int j = lane & 31, hi = lane >> 5;
   const int64_t key = k0 + wid * 32 + j;  // this lane's key
-  const float* qb = q + b * sq.b + h * sq.h;
-  const float* gb = dO + b * sd.b + h * sd.h;
+  const TI* qb = q + b * sq.b + h * sq.h;
+  const TD* gb = dO + b * sd.b + h * sd.h;
   const float* lb = lse + ((int64_t)b * H + h) * Lq;
   const float* db = delta + ((int64_t)b * H + h) * Lq;
   const float c = scale * LOG2E;
@@ -357,7 +397,8 @@ __global__ __launch_bounds__(BwdCfg<HD>::NT, 1) void attn_bwd_dkdv_mf_kernel(
   const int64_t qt0 = causal ? k0 / BQT : 0;  // causal: tiles entirely before the block's keys are masked
   const int ntiles = (int)((Lq + BQT - 1) / BQT - qt0);
   const int srow = tid >> 3, sc = tid & 7;
-  float4 qa[C::RI][NH], qb4[C::RI][NH], ga[C::RI][NH], gb4[C::RI][NH];
+  Row8<TI> qa[C::RI][NH];
+  Row8<TD> ga[C::RI][NH];
   float2 ld = make_float2(0.f, 0.f);
   auto stage_ld = [&](int t) {
     const int64_t q0 = (qt0 + t) * BQT;
@@ -365,8 +406,8 @@ __global__ __launch_bounds__(BwdCfg<HD>::NT, 1) void attn_bwd_dkdv_mf_kernel(
     for (int i = 0; i < C::RI; ++i)
 #pragma unroll
       for (int hf = 0; hf < NH; ++hf) {
-        stage_load(qb, sq, q0 + srow + i * (C::NT / 8), Lq, hf, sc, qa[i][hf], qb4[i][hf]);
-        stage_load(gb, sd, q0 + srow + i * (C::NT / 8), Lq, hf, sc, ga[i][hf], gb4[i][hf]);
+        stage_load(qb, sq, q0 + srow + i * (C::NT / 8), Lq, hf, sc, qa[i][hf]);
+        stage_load(gb, sd, q0 + srow + i * (C::NT / 8), Lq, hf, sc, ga[i][hf]);
       }
     if (tid < BQT) {
       const int64_t qi = q0 + tid;
@@ -379,10 +420,10 @@ __global__ __launch_bounds__(BwdCfg<HD>::NT, 1) void attn_bwd_dkdv_mf_kernel(
 #pragma unroll
       for (int hf = 0; hf < NH; ++hf) {
         const int row = srow + i * (C::NT / 8);
-        stage_store(Qr[buf] + hf * HALF, row, sc ^ kswz(row), qa[i][hf], qb4[i][hf]);
-        stage_store(Qt[buf] + hf * HALF, row, sc ^ vswz(row), qa[i][hf], qb4[i][hf]);
-        stage_store(Dr[buf] + hf * HALF, row, sc ^ kswz(row), ga[i][hf], gb4[i][hf]);
-        stage_store(Dt[buf] + hf * HALF, row, sc ^ vswz(row), ga[i][hf], gb4[i][hf]);
+        stage_store(Qr[buf] + hf * HALF, row, sc ^ kswz(row), qa[i][hf]);
+        stage_store(Qt[buf] + hf * HALF, row, sc ^ vswz(row), qa[i][hf]);
+        stage_store(Dr[buf] + hf * HALF, row, sc ^ kswz(row), ga[i][hf]);
+        stage_store(Dt[buf] + hf * HALF, row, sc ^ vswz(row), ga[i][hf]);
       }
     if (tid < BQT) LD[buf][tid] = ld;
   };
@@ -458,10 +499,10 @@ __global__ __launch_bounds__(BwdCfg<HD>::NT, 1) void attn_bwd_dkdv_mf_kernel(
   }
 }
 
-template <int HD>
+template <int HD, typename TI = float, typename TD = float>
 __global__ __launch_bounds__(BwdCfg<HD>::NT, 1) void attn_bwd_dq_mf_kernel(
-    const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v,
-    const float* __restrict__ dO, const float* __restrict__ lse, const float* __restrict__ delta,
+    const TI* __restrict__ q, const TI* __restrict__ k, const TI* __restrict__ v,
+    const TD* __restrict__ dO, const float* __restrict__ lse, const float* __restrict__ delta,
     float* __restrict__ dq, AttnStridesMF sq, AttnStridesMF sk, AttnStridesMF sv, AttnStridesMF sd,
     AttnStridesMF sdq, int64_t H, int64_t Lq, int64_t Lk, int causal, float scale) {
   typedef BwdCfg<HD> C;
@@ -475,8 +516,8 @@ __global__ __launch_bounds__(BwdCfg<HD>::NT, 1) void attn_bwd_dq_mf_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int j = lane & 31, hi = lane >> 5;
   const int64_t qi = q0 + wid * 32 + j;  // this lane's query row
-  const float* kbp = k + b * sk.b + h * sk.h;
-  const float* vbp = v + b * sv.b + h * sv.h;
+  const TI* kbp = k + b * sk.b + h * sk.h;
+  const TI* vbp = v + b * sv.b + h * sv.h;
   const float c = scale * LOG2E;
 
   bf16x8 qf[HD / 16], gf[HD / 16];
@@ -490,14 +531,14 @@ __global__ __launch_bounds__(BwdCfg<HD>::NT, 1) void attn_bwd_dq_mf_kernel(
   const int ntiles = (int)((kend + KT - 1) / KT);
   const int skey = tid >> 3, sc = tid & 7;
 
-  float4 ka[C::RI][NH], kb4[C::RI][NH], va[C::RI][NH], vb4[C::RI][NH];
+  Row8<TI> ka[C::RI][NH], va[C::RI][NH];
   auto stage_ld = [&](int64_t k0) {
 #pragma unroll
     for (int i = 0; i < C::RI; ++i)
 #pragma unroll
       for (int hf = 0; hf < NH; ++hf) {
-        stage_load(kbp, sk, k0 + skey + i * (C::NT / 8), Lk, hf, sc, ka[i][hf], kb4[i][hf]);
-        stage_load(vbp, sv, k0 + skey + i * (C::NT / 8), Lk, hf, sc, va[i][hf], vb4[i][hf]);
+        stage_load(kbp, sk, k0 + skey + i * (C::NT / 8), Lk, hf, sc, ka[i][hf]);
+        stage_load(vbp, sv, k0 + skey + i * (C::NT / 8), Lk, hf, sc, va[i][hf]);
       }
   };
   auto stage_st = [&](int buf) {
@@ -506,9 +547,9 @@ __global__ __launch_bounds__(BwdCfg<HD>::NT, 1) void attn_bwd_dq_mf_kernel(
 #pragma unroll
       for (int hf = 0; hf < NH; ++hf) {
         const int row = skey + i * (C::NT / 8);
-        stage_store(Kr[buf] + hf * HALF, row, sc ^ kswz(row), ka[i][hf], kb4[i][hf]);
-        stage_store(Kt2[buf] + hf * HALF, row, sc ^ vswz(row), ka[i][hf], kb4[i][hf]);
-        stage_store(Vr[buf] + hf * HALF, row, sc ^ kswz(row), va[i][hf], vb4[i][hf]);
+        stage_store(Kr[buf] + hf * HALF, row, sc ^ kswz(row), ka[i][hf]);
+        stage_store(Kt2[buf] + hf * HALF, row, sc ^ vswz(row), ka[i][hf]);
+        stage_store(Vr[buf] + hf * HALF, row, sc ^ kswz(row), va[i][hf]);
       }
   };
   stage_ld(0);
@@ -572,55 +613,97 @@ __global__ __launch_bounds__(BwdCfg<HD>::NT, 1) void attn_bwd_dq_mf_kernel(
 
 }  // namespace amf
 
-// bf16 flash-attention forward (see header); called by asrx_attn_fwd for prec == PREC_BF16.
-int attn_fwd_mf(const float* q, const int64_t* sq, const float* k, const int64_t* sk, const float* v,
-                const int64_t* sv, float* o, const int64_t* so, float* lse, int64_t B, int64_t H, int64_t Lq,
-                int64_t Lk, int64_t hd, int causal, float scale, hipStream_t stream) {
+template <int HD, typename TI, typename TO>
+static void attn_fwd_mf_t(const void* q, AttnStridesMF Sq, const void* k, AttnStridesMF Sk, const void* v,
+                          AttnStridesMF Sv, void* o, AttnStridesMF So, float* lse, int64_t B, int64_t H, int64_t Lq,
+                          int64_t Lk, int causal, float scale, hipStream_t stream) {
+  const TI *qq = (const TI*)q, *kk = (const TI*)k, *vv = (const TI*)v;
+  TO* oo = (TO*)o;
   dim3 g((unsigned)((Lq + amf::QB - 1) / amf::QB), (unsigned)H, (unsigned)B);
-  AttnStridesMF Sq{sq[0], sq[1], sq[2]}, Sk{sk[0], sk[1], sk[2]}, Sv{sv[0], sv[1], sv[2]}, So{so[0], so[1], so[2]};
   // query blocks of one (b, h) on one XCD when there are several (3.6 % at 3001 x 3001, H = 6,
   // B = 64; profiles/r02_attn_fwd_variants.txt, which also records the rejected 4-waves-per-SIMD
   // and s_setprio variants)
+  if (HD == 64 && g.x > 1)
+    amf::attn_fwd_mf_kernel<HD, 1, true, false, TI, TO><<<dim3((unsigned)((int64_t)g.x * g.y * g.z)), amf::NTHR, 0,
+                                                          stream>>>(qq, kk, vv, oo, lse, Sq, Sk, Sv, So, H, Lq, Lk,
+                                                                    causal, scale);
+  else
+    amf::attn_fwd_mf_kernel<HD, 1, false, false, TI, TO><<<g, amf::NTHR, 0, stream>>>(qq, kk, vv, oo, lse, Sq, Sk, Sv,
+                                                                                     So, H, Lq, Lk, causal, scale);
+}
+
+// bf16 flash-attention forward (see header); called by asrx_attn_fwd for prec == PREC_BF16.  io: bit 0
+// q / k / v stored bf16, bit 1 o stored bf16.
+int attn_fwd_mf(int io, const void* q, const int64_t* sq, const void* k, const int64_t* sk, const void* v,
+                const int64_t* sv, void* o, const int64_t* so, float* lse, int64_t B, int64_t H, int64_t Lq,
+                int64_t Lk, int64_t hd, int causal, float scale, hipStream_t stream) {
+  AttnStridesMF Sq{sq[0], sq[1], sq[2]}, Sk{sk[0], sk[1], sk[2]}, Sv{sv[0], sv[1], sv[2]}, So{so[0], so[1], so[2]};
+#define ASRX_AF(HDV, TI, TO) attn_fwd_mf_t<HDV, TI, TO>(q, Sq, k, Sk, v, Sv, o, So, lse, B, H, Lq, Lk, causal, scale, stream)
   if (hd == 64) {
-    if (g.x > 1)
-      amf::attn_fwd_mf_kernel<64, 1, true><<<dim3((unsigned)((int64_t)g.x * g.y * g.z)), amf::NTHR, 0, stream>>>(
-          q, k, v, o, lse, Sq, Sk, Sv, So, H, Lq, Lk, causal, scale);
-    else
-      amf::attn_fwd_mf_kernel<64><<<g, amf::NTHR, 0, stream>>>(q, k, v, o, lse, Sq, Sk, Sv, So, H, Lq, Lk, causal, scale);
-  } else
-    amf::attn_fwd_mf_kernel<128><<<g, amf::NTHR, 0, stream>>>(q, k, v, o, lse, Sq, Sk, Sv, So, H, Lq, Lk, causal, scale);
+    switch (io & 3) {
+      case 0: ASRX_AF(64, float, float); break;
+      case 1: ASRX_AF(64, amf::bf16s, float); break;
+      case 2: ASRX_AF(64, float, amf::bf16s); break;
+      default: ASRX_AF(64, amf::bf16s, amf::bf16s); break;
+    }
+  } else {
+    switch (io & 3) {
+      case 0: ASRX_AF(128, float, float); break;
+      case 1: ASRX_AF(128, amf::bf16s, float); break;
+      case 2: ASRX_AF(128, float, amf::bf16s); break;
+      default: ASRX_AF(128, amf::bf16s, amf::bf16s); break;
+    }
+  }
+#undef ASRX_AF
   return 0;
 }
 
-template <int HD>
-static void attn_bwd_mf_t(const float* q, AttnStridesMF Sq, const float* k, AttnStridesMF Sk, const float* v,
-                          AttnStridesMF Sv, const float* dO, AttnStridesMF Sd, const float* lse, const float* delta,
+template <int HD, typename TI, typename TD>
+static void attn_bwd_mf_t(const void* q, AttnStridesMF Sq, const void* k, AttnStridesMF Sk, const void* v,
+                          AttnStridesMF Sv, const void* dO, AttnStridesMF Sd, const float* lse, const float* delta,
                           float* dq, AttnStridesMF Sdq, float* dk, AttnStridesMF Sdk, float* dv, AttnStridesMF Sdv,
                           int64_t B, int64_t H, int64_t Lq, int64_t Lk, int causal, float scale, hipStream_t stream) {
   typedef amf::BwdCfg<HD> C;
+  const TI *qq = (const TI*)q, *kk = (const TI*)k, *vv = (const TI*)v;
+  const TD* gg = (const TD*)dO;
   const int64_t rows_per_wg = 32 * C::NW;
   dim3 gk((unsigned)(((Lk + rows_per_wg - 1) / rows_per_wg) * H * B));
-  amf::attn_bwd_dkdv_mf_kernel<HD><<<gk, C::NT, 0, stream>>>(q, k, v, dO, lse, delta, dk, dv, Sq, Sk, Sv, Sd, Sdk, Sdv,
-                                                             H, Lq, Lk, causal, scale);
+  amf::attn_bwd_dkdv_mf_kernel<HD, TI, TD><<<gk, C::NT, 0, stream>>>(qq, kk, vv, gg, lse, delta, dk, dv, Sq, Sk, Sv, Sd,
+                                                                     Sdk, Sdv, H, Lq, Lk, causal, scale);
   dim3 gq((unsigned)(((Lq + rows_per_wg - 1) / rows_per_wg) * H * B));
-  amf::attn_bwd_dq_mf_kernel<HD><<<gq, C::NT, 0, stream>>>(q, k, v, dO, lse, delta, dq, Sq, Sk, Sv, Sd, Sdq, H, Lq, Lk,
-                                                           causal, scale);
+  amf::attn_bwd_dq_mf_kernel<HD, TI, TD><<<gq, C::NT, 0, stream>>>(qq, kk, vv, gg, lse, delta, dq, Sq, Sk, Sv, Sd, Sdq,
+                                                                   H, Lq, Lk, causal, scale);
 }
 
 // bf16 flash-attention backward (dkdv + dq kernels above); delta = rowsum(dO * O) already computed.
-int attn_bwd_mf(const float* q, const int64_t* sq, const float* k, const int64_t* sk, const float* v,
-                const int64_t* sv, const float* dO, const int64_t* sd, const float* lse, const float* delta,
+// io: bit 0 q / k / v stored bf16, bit 2 dO stored bf16.
+int attn_bwd_mf(int io, const void* q, const int64_t* sq, const void* k, const int64_t* sk, const void* v,
+                const int64_t* sv, const void* dO, const int64_t* sd, const float* lse, const float* delta,
                 float* dq, const int64_t* sdq, float* dk, const int64_t* sdk, float* dv, const int64_t* sdv,
                 int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t hd, int causal, float scale,
                 hipStream_t stream) {
   AttnStridesMF Sq{sq[0], sq[1], sq[2]}, Sk{sk[0], sk[1], sk[2]}, Sv{sv[0], sv[1], sv[2]}, Sd{sd[0], sd[1], sd[2]};
   AttnStridesMF Sdq{sdq[0], sdq[1], sdq[2]}, Sdk{sdk[0], sdk[1], sdk[2]}, Sdv{sdv[0], sdv[1], sdv[2]};
-  if (hd == 64)
-    attn_bwd_mf_t<64>(q, Sq, k, Sk, v, Sv, dO, Sd, lse, delta, dq, Sdq, dk, Sdk, dv, Sdv, B, H, Lq, Lk, causal, scale,
-                      stream);
-  else
-    attn_bwd_mf_t<128>(q, Sq, k, Sk, v, Sv, dO, Sd, lse, delta, dq, Sdq, dk, Sdk, dv, Sdv, B, H, Lq, Lk, causal, scale,
-                       stream);
+#define ASRX_AB(HDV, TI, TD)                                                                                       \
+  attn_bwd_mf_t<HDV, TI, TD>(q, Sq, k, Sk, v, Sv, dO, Sd, lse, delta, dq, Sdq, dk, Sdk, dv, Sdv, B, H, Lq, Lk, causal, \
+                             scale, stream)
+  const int sel = (io & 1) | ((io >> 1) & 2);
+  if (hd == 64) {
+    switch (sel) {
+      case 0: ASRX_AB(64, float, float); break;
+      case 1: ASRX_AB(64, amf::bf16s, float); break;
+      case 2: ASRX_AB(64, float, amf::bf16s); break;
+      default: ASRX_AB(64, amf::bf16s, amf::bf16s); break;
+    }
+  } else {
+    switch (sel) {
+      case 0: ASRX_AB(128, float, float); break;
+      case 1: ASRX_AB(128, amf::bf16s, float); break;
+      case 2: ASRX_AB(128, float, amf::bf16s); break;
+      default: ASRX_AB(128, amf::bf16s, amf::bf16s); break;
+    }
+  }
+#undef ASRX_AB
   return 0;
 }
 

@@ -38,13 +38,32 @@ struct Params {
 // byte offset of 16-B chunk ch (8 features) of k-row `row` in a [32][128] bf16 image
 __device__ __forceinline__ int off(int row, int ch) { return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3))); }
 
+// BBF: X stored bf16 (an activation whose only consumers are GEMM operands): 16-byte loads of 8
+// features, rows (t >> 4) + 16 i, already in the image's element type
+template <bool BBF>
 struct Stage {
   float4 a[4], b[4];  // rows (t >> 5) + 8 i, features 4 (t & 31) .. +3
 };
+template <>
+struct Stage<true> {
+  float4 a[4];
+  uint4 bh[2];  // rows (t >> 4) + 16 i, features 8 (t & 15) .. +7
+};
 
-__device__ __forceinline__ void load(const Params& p, Stage& st, int64_t r0, int64_t rend, int m0, int n0) {
+template <bool BBF>
+__device__ __forceinline__ void load(const Params& p, Stage<BBF>& st, int64_t r0, int64_t rend, int m0, int n0) {
   const int t = threadIdx.x;
   const int c = 4 * (t & 31);
+  if constexpr (BBF) {
+    const unsigned short* Bh = reinterpret_cast<const unsigned short*>(p.B);
+    const int cb = 8 * (t & 15);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int64_t r = r0 + (t >> 4) + 16 * i;
+      st.bh[i] = *reinterpret_cast<const uint4*>((r < rend && n0 + cb < p.N) ? (const void*)(Bh + r * p.ldb + n0 + cb)
+                                                                            : (const void*)zero16);
+    }
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int64_t r = r0 + (t >> 5) + 8 * i;
@@ -52,12 +71,14 @@ __device__ __forceinline__ void load(const Params& p, Stage& st, int64_t r0, int
     // unconditional loads from clamped addresses (a branch would make the compiler drain vmcnt)
     st.a[i] = *reinterpret_cast<const float4*>((okr && m0 + c < p.M) ? (const void*)(p.A + r * p.lda + m0 + c)
                                                                      : (const void*)zero16);
-    st.b[i] = *reinterpret_cast<const float4*>((okr && n0 + c < p.N) ? (const void*)(p.B + r * p.ldb + n0 + c)
-                                                                     : (const void*)zero16);
+    if constexpr (!BBF)
+      st.b[i] = *reinterpret_cast<const float4*>((okr && n0 + c < p.N) ? (const void*)(p.B + r * p.ldb + n0 + c)
+                                                                       : (const void*)zero16);
   }
 }
 
-__device__ __forceinline__ void store(const Stage& st, char* Ai, char* Bi) {
+template <bool BBF>
+__device__ __forceinline__ void store(const Stage<BBF>& st, char* Ai, char* Bi) {
   const int t = threadIdx.x;
   const int c = 4 * (t & 31);
   const int ch = c >> 3, hb = (c >> 2) & 1;
@@ -65,11 +86,18 @@ __device__ __forceinline__ void store(const Stage& st, char* Ai, char* Bi) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int row = (t >> 5) + 8 * i;
-    bf16x4 ha, hb4;
+    bf16x4 ha;
     ha[0] = (__bf16)st.a[i].x; ha[1] = (__bf16)st.a[i].y; ha[2] = (__bf16)st.a[i].z; ha[3] = (__bf16)st.a[i].w;
-    hb4[0] = (__bf16)st.b[i].x; hb4[1] = (__bf16)st.b[i].y; hb4[2] = (__bf16)st.b[i].z; hb4[3] = (__bf16)st.b[i].w;
     *reinterpret_cast<bf16x4*>(Ai + off(row, ch) + 8 * hb) = ha;
-    *reinterpret_cast<bf16x4*>(Bi + off(row, ch) + 8 * hb) = hb4;
+    if constexpr (!BBF) {
+      bf16x4 hb4;
+      hb4[0] = (__bf16)st.b[i].x; hb4[1] = (__bf16)st.b[i].y; hb4[2] = (__bf16)st.b[i].z; hb4[3] = (__bf16)st.b[i].w;
+      *reinterpret_cast<bf16x4*>(Bi + off(row, ch) + 8 * hb) = hb4;
+    }
+  }
+  if constexpr (BBF) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) *reinterpret_cast<uint4*>(Bi + off((t >> 4) + 16 * i, t & 15)) = st.bh[i];
   }
 }
 
@@ -92,6 +120,7 @@ __device__ __forceinline__ int xcd_item(int bid, int nblk) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
+template <bool BBF>
 __global__ __launch_bounds__(NT, 2) void wgrad_wr_kernel(Params p) {
   __shared__ __attribute__((aligned(16))) char Ai[2][TK * TM * 2];
   __shared__ __attribute__((aligned(16))) char Bi[2][TK * TN * 2];
@@ -111,13 +140,13 @@ __global__ __launch_bounds__(NT, 2) void wgrad_wr_kernel(Params p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  Stage s0, s1;
+  Stage<BBF> s0, s1;
   load(p, s0, rb, re, m0, n0);
   load(p, s1, rb + TK, re, m0, n0);
   store(s0, Ai[0], Bi[0]);
   __syncthreads();
 
-  auto kstep = [&](int s, Stage& cur, const Stage& nxt) __attribute__((always_inline)) {
+  auto kstep = [&](int s, Stage<BBF>& cur, const Stage<BBF>& nxt) __attribute__((always_inline)) {
     load(p, cur, rb + (int64_t)(s + 2) * TK, re, m0, n0);  // past the end: zero page, counts stay uniform
     const char* At = Ai[s & 1];
     const char* Bt = Bi[s & 1];
@@ -163,19 +192,34 @@ using namespace asrx;
 // dW (M x N, ldc) += dY^T X over R rows; dY (R x M, lda), X (R x N, ldb) fp32 row-major; the rows
 // split over `splitk` work items (bf16 operands, fp32 accumulate).  M, N, lda, ldb multiples of 4,
 // 16-byte aligned operands.
-extern "C" int asrx_wgrad_bf16(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
-                               int64_t M, int64_t N, int64_t R, int64_t splitk, hipStream_t stream) {
+static int wgrad_launch(const float* A, int64_t lda, const void* B, int b_bf16, int64_t ldb, float* C, int64_t ldc,
+                        int64_t M, int64_t N, int64_t R, int64_t splitk, hipStream_t stream) {
   ASRX_REQUIRE(M > 0 && N > 0 && R >= 0, "asrx_wgrad_bf16: empty problem");
   ASRX_REQUIRE(M % 4 == 0 && N % 4 == 0 && lda % 4 == 0 && ldb % 4 == 0, "asrx_wgrad_bf16: M, N, lda, ldb %% 4 required");
+  ASRX_REQUIRE(!b_bf16 || (N % 8 == 0 && ldb % 8 == 0), "asrx_wgrad_bf16: a bf16 X needs N, ldb %% 8");
   ASRX_REQUIRE((((uintptr_t)A | (uintptr_t)B) & 15) == 0, "asrx_wgrad_bf16: operands must be 16-byte aligned");
   if (R == 0) return 0;
   if (splitk < 1) splitk = 1;
   int64_t kchunk = (R + splitk - 1) / splitk;
   kchunk = (kchunk + wg::TK - 1) / wg::TK * wg::TK;
   splitk = (R + kchunk - 1) / kchunk;
-  wg::Params p{A, B, C, lda, ldb, ldc, (int)M, (int)N, R, kchunk, (int)splitk};
+  wg::Params p{A, (const float*)B, C, lda, ldb, ldc, (int)M, (int)N, R, kchunk, (int)splitk};
   const int64_t items = ((M + wg::TM - 1) / wg::TM) * ((N + wg::TN - 1) / wg::TN) * splitk;
   ASRX_REQUIRE(items < (1LL << 31), "asrx_wgrad_bf16: too many work items");
-  wg::wgrad_wr_kernel<<<(unsigned)items, wg::NT, 0, stream>>>(p);
+  if (b_bf16)
+    wg::wgrad_wr_kernel<true><<<(unsigned)items, wg::NT, 0, stream>>>(p);
+  else
+    wg::wgrad_wr_kernel<false><<<(unsigned)items, wg::NT, 0, stream>>>(p);
   ASRX_LAUNCHED("asrx_wgrad_bf16");
+}
+
+extern "C" int asrx_wgrad_bf16(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
+                               int64_t M, int64_t N, int64_t R, int64_t splitk, hipStream_t stream) {
+  return wgrad_launch(A, lda, B, 0, ldb, C, ldc, M, N, R, splitk, stream);
+}
+
+// asrx_wgrad_bf16 with X (B) stored fp32 (b_bf16 = 0) or bf16 (1; N, ldb multiples of 8).
+extern "C" int asrx_wgrad_bf16_ex(const float* A, int64_t lda, const void* B, int b_bf16, int64_t ldb, float* C,
+                                  int64_t ldc, int64_t M, int64_t N, int64_t R, int64_t splitk, hipStream_t stream) {
+  return wgrad_launch(A, lda, B, b_bf16, ldb, C, ldc, M, N, R, splitk, stream);
 }

@@ -1,677 +1,10 @@
-// Wide-N GEMM for activation x weight products (perf mode): every nn.Linear / 1x1 / k3 conv forward
-// and input-gradient on the hot path (model.py:96-147, 242-245, 341, 398-425, 529-574;
-// essentials.py:149-153), i.e. Y = act(alpha * A W^T + beta * Y + bias) with
-//   A  fp32 activations (M x K, row-major, or the implicit k3 im2col of a channels-last sequence),
-//   W  the weight pre-converted to bf16, stored N x K (K contiguous) -- asrx_weight_to_bf16.
-//
-// At the model's shapes (M = 8k..192k rows, N, K = 64..1536) the kernel is bound by bytes moved
-// (A from HBM, W from L2, C back to HBM), not by MFMA.  Design:
-//  * 128 x BN tiles, BN = 128 * NJ up to 384, so an activation row panel is read once per 384
-//    output columns; 512 threads = 8 waves (2 x 4), each 64 x 32*NJ of the output.
-//  * Persistent workgroups (grid = resident capacity) walk their tiles in an XCD-grouped order;
-//    the LDS-DMA ring (A fp32 16 KB + W bf16 8*NJ KB per 32-deep k-step) runs across tile
-//    boundaries, so the next tile's first k-steps are in flight while this tile's epilogue stores
-//    drain.  The bias slice of each tile rides the ring as one extra dword DMA per lane.
-//  * LDS-DMA from inline asm (common.h glds16): the compiler's own waitcnt logic would otherwise
-//    drain the ring (vmcnt(0)) before every ds_read.  Completion is counted by hand.
-//  * Images are XOR-swizzled through the per-lane source address so the ds_read_b128 fragment
-//    reads are bank-conflict-free under gfx950's 64-bank, 16-lane-group rule.
-//  * MFMA 16x16x32 bf16 with the W fragment as the row operand: each lane ends up owning 4
-//    consecutive output columns of one row, so the epilogue stores float4.
-// Two pipelines share the tiles, swizzles and epilogues: gemm_wr_kernel (production: operands
-// global -> VGPR -> LDS, A converted to bf16 on the way in, 3 k-steps of register prefetch) and
-// gemm_wn_kernel (LDS-DMA ring; ASRX_WN_IMPL=dma selects it for A/B timing).  Measured on MI355X
-// at M = 192064, N = 384: K = 384 195 us vs 219 us, K = 1536 454 us vs 560 us (tools/exp).
-#include "common.h"
+// Entry points of the wide GEMM (kernel and design: gemm_wr.h), the bulk weight conversion to
+// bf16 and the MSheath row-tile lists.
+#include "gemm_wr.h"
+#include <string>
 
 namespace asrx {
-
 namespace wn {
-
-constexpr int BM = 128, BK = 32, NTHR = 512;
-constexpr int A_BYTES = BM * BK * 4;  // 16 KB fp32
-
-__device__ __attribute__((aligned(16))) float zero_page[4];
-
-struct Params {
-  const float* A;
-  int lda;
-  const unsigned short* W;  // bf16 N x K
-  int ldw;
-  float* C;
-  int ldc;
-  const float* bias;
-  float* Z;
-  int M, N, K;
-  int convF, convC;
-  float alpha, beta;
-  int act;
-  const float* W2;  // router: Linear(d, 3) weight (3 x N) applied to SiLU(C) in the epilogue
-  float* R;         // router: logits without bias (M x 3); C may be null (h_pre not kept)
-  // optional row-tile list (gemm_wr_kernel): only the BM-row tiles mtiles[0 .. *n_mtiles) are
-  // computed (MSheath layers skip the rows of samples that are not at the layer); other rows of C
-  // are left untouched
-  const int* mtiles;
-  const int* n_mtiles;
-};
-
-template <int NJ>
-struct Cfg {
-  static constexpr int BN = 128 * NJ;
-  static constexpr int B_BYTES = BN * BK * 2;  // bf16
-  static constexpr int STAGE = A_BYTES + B_BYTES;
-  static constexpr int PIECES = 2 + NJ;  // 1 KB DMAs per wave per k-step: A 2, W NJ
-  static constexpr int BNR = (BN + NTHR - 1) / NTHR * NTHR;  // bias slice in whole DMA rounds
-  static constexpr int BIAS_OPS = BNR / NTHR;
-};
-
-// conflict-free swizzles (chunk XOR by row) for the A image (rows of 8 x 16 B) and the W image
-// (rows of 4 x 16 B) under ds_read_b128 lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31}, ...
-__device__ __forceinline__ int swa(int row) { return ((row >> 1) & 1) | (((row >> 3) & 1) << 2); }
-__device__ __forceinline__ int swb(int n) { return ((n >> 3) & 1) << 1; }
-
-template <int NJ, bool CONV>
-struct Loader {
-  uint32_t aoff[2];
-  int akk[2], apos[2];
-  bool aok[2];
-  uint32_t boff[NJ];
-  int bkc[NJ];
-  bool bok[NJ];
-
-  __device__ __forceinline__ void init(const Params& p, int m0, int n0) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {  // A: [128 rows][8 chunks of 4 fp32]; piece q = 8 rows
-      const int q = wid * 2 + i;
-      const int row = 8 * q + (lane >> 3);
-      const int c = (lane & 7) ^ swa(row);
-      const int r = m0 + row;
-      aok[i] = r < p.M;
-      aoff[i] = (uint32_t)r * (uint32_t)p.lda + 4 * c;
-      akk[i] = 4 * c;
-      apos[i] = CONV ? r % p.convF : 0;
-    }
-#pragma unroll
-    for (int i = 0; i < NJ; ++i) {  // W: [BN rows][4 chunks of 8 bf16]; piece q = 16 rows
-      const int q = wid * NJ + i;
-      const int row = 16 * q + (lane >> 2);
-      const int c = (lane & 3) ^ swb(row);
-      const int n = n0 + row;
-      bok[i] = n < p.N;
-      boff[i] = (uint32_t)n * (uint32_t)p.ldw + 8 * c;
-      bkc[i] = 8 * c;
-    }
-  }
-
-  __device__ __forceinline__ void issue(const Params& p, char* st, int k0) const {
-    const int wid = threadIdx.x >> 6;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int k = k0 + akk[i];
-      bool ok = aok[i] && k < p.K;
-      uint32_t o = aoff[i] + (uint32_t)k0;
-      if (CONV) {
-        const int pos = apos[i] + k / p.convC - 1;
-        ok = ok && pos >= 0 && pos < p.convF;
-        o -= (uint32_t)p.convC;
-      }
-      glds16(ok ? (const void*)(p.A + o) : (const void*)zero_page, lds_addr(st + (wid * 2 + i) * 1024));
-    }
-    char* bt = st + A_BYTES;
-#pragma unroll
-    for (int i = 0; i < NJ; ++i) {
-      const bool ok = bok[i] && k0 + bkc[i] < p.K;
-      glds16(ok ? (const void*)(p.W + boff[i] + k0) : (const void*)zero_page, lds_addr(bt + (wid * NJ + i) * 1024));
-    }
-  }
-};
-
-__device__ __forceinline__ bool vec_ok(const Params& p) {
-  return ((p.N | p.ldc) & 3) == 0 && ((uintptr_t)p.C & 15) == 0 && ((uintptr_t)p.Z & 15) == 0;
-}
-
-template <int ACT>
-__device__ __forceinline__ float act_t(float x) {
-  if constexpr (ACT == ACT_GELU) return gelu_f(x);
-  else if constexpr (ACT == ACT_SILU) return silu_f(x);
-  else if constexpr (ACT == ACT_SIGMOID) return sigmoid_f(x);
-  else if constexpr (ACT == ACT_RELU) return x > 0.f ? x : 0.f;
-  else return x;
-}
-
-// Tile epilogue: v = alpha * acc + bias (+ beta * C); Z <- v (pre-activation); C <- act(v).
-// Full float4 rows go out as non-temporal stores (streaming writes that would otherwise sit dirty
-// in L2 ahead of the next tile's loads: -8 % at M = 192064, N = K = 384).
-template <int NJ, int ACT>
-__device__ __forceinline__ void epilogue(const Params& p, f32x4 (&acc)[4][2 * NJ], const float* bsl, int m0, int n0,
-                                         int wm, int wn, int lr, int lk) {
-  constexpr int NT = 2 * NJ;
-  const bool vec = vec_ok(p);
-#pragma unroll
-  for (int nt = 0; nt < NT; ++nt) {
-    const int nl = wn * (32 * NJ) + nt * 16 + 4 * lk;
-    const int col = n0 + nl;
-    if (col >= p.N) continue;
-    float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (p.bias) bv = *reinterpret_cast<const float4*>(bsl + nl);
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      const int row = m0 + wm * 64 + mt * 16 + lr;
-      if (row >= p.M) continue;
-      float v[4] = {p.alpha * acc[mt][nt][0] + bv.x, p.alpha * acc[mt][nt][1] + bv.y,
-                    p.alpha * acc[mt][nt][2] + bv.z, p.alpha * acc[mt][nt][3] + bv.w};
-      float* dst = p.C + (int64_t)row * p.ldc + col;
-      float* zdst = p.Z ? p.Z + (int64_t)row * p.ldc + col : nullptr;
-      if (vec) {
-        if (p.beta != 0.f) {
-          const float4 o = *reinterpret_cast<const float4*>(dst);
-          v[0] += p.beta * o.x; v[1] += p.beta * o.y; v[2] += p.beta * o.z; v[3] += p.beta * o.w;
-        }
-        if (zdst) __builtin_nontemporal_store(f32x4{v[0], v[1], v[2], v[3]}, reinterpret_cast<f32x4*>(zdst));
-        __builtin_nontemporal_store(f32x4{act_t<ACT>(v[0]), act_t<ACT>(v[1]), act_t<ACT>(v[2]), act_t<ACT>(v[3])},
-                                    reinterpret_cast<f32x4*>(dst));
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          if (col + r >= p.N) break;
-          float x = v[r];
-          if (p.beta != 0.f) x += p.beta * dst[r];
-          if (zdst) zdst[r] = x;
-          dst[r] = act_t<ACT>(x);
-        }
-      }
-    }
-  }
-}
-
-// The same epilogue staged through a per-wave LDS slab, one 16-row slice (mt) at a time: the MFMA
-// layout gives each lane 4 columns of one row, so a direct store instruction writes 16 rows x 64 B;
-// re-read from LDS, every store instruction writes whole contiguous row segments (32*NJ floats per
-// row: 384 B at NJ = 3).  Requires vec_ok(p) (float4-aligned C/Z, N % 4 == 0).
-constexpr int EP_PAD = 4;
-template <int NJ>
-struct EpLds {
-  static constexpr int W = 32 * NJ;           // columns of a wave's sub-tile
-  static constexpr int LD = W + EP_PAD;       // slab row stride (floats)
-  static constexpr int FLOATS = 16 * LD;      // one 16-row slice
-};
-template <int NJ, int ACT>
-__device__ __forceinline__ void epilogue_lds(const Params& p, f32x4 (&acc)[4][2 * NJ], const float* bsl, int m0,
-                                             int n0, int wm, int wn, int lr, int lk, float* ep) {
-  constexpr int NT = 2 * NJ, W = EpLds<NJ>::W, LD = EpLds<NJ>::LD, W4 = W / 4;
-  constexpr int PER = 16 * W4 / 64;  // float4 per lane per slice
-  static_assert((16 * W4) % 64 == 0, "slice must split evenly over the wave");
-  const int lane = threadIdx.x & 63;
-  const int cbase = n0 + wn * W;
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) {
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      const int nl = nt * 16 + 4 * lk;
-      float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (p.bias) bv = *reinterpret_cast<const float4*>(bsl + wn * W + nl);
-      *reinterpret_cast<float4*>(ep + lr * LD + nl) =
-          make_float4(p.alpha * acc[mt][nt][0] + bv.x, p.alpha * acc[mt][nt][1] + bv.y,
-                      p.alpha * acc[mt][nt][2] + bv.z, p.alpha * acc[mt][nt][3] + bv.w);
-    }
-    __builtin_amdgcn_wave_barrier();
-    const int rbase = m0 + wm * 64 + mt * 16;
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const int f = j * 64 + lane, r = f / W4, c = 4 * (f % W4);
-      float4 x = *reinterpret_cast<const float4*>(ep + r * LD + c);
-      const int row = rbase + r, col = cbase + c;
-      if (row >= p.M || col >= p.N) continue;
-      float* dst = p.C + (int64_t)row * p.ldc + col;
-      if (p.beta != 0.f) {
-        const float4 o = *reinterpret_cast<const float4*>(dst);
-        x.x += p.beta * o.x; x.y += p.beta * o.y; x.z += p.beta * o.z; x.w += p.beta * o.w;
-      }
-      if (p.Z)
-        __builtin_nontemporal_store(f32x4{x.x, x.y, x.z, x.w},
-                                    reinterpret_cast<f32x4*>(p.Z + (int64_t)row * p.ldc + col));
-      __builtin_nontemporal_store(f32x4{act_t<ACT>(x.x), act_t<ACT>(x.y), act_t<ACT>(x.z), act_t<ACT>(x.w)},
-                                  reinterpret_cast<f32x4*>(dst));
-    }
-    __builtin_amdgcn_wave_barrier();  // the next slice overwrites the slab
-  }
-}
-
-// AbbyNormal router epilogue (essentials.py:155-161): h = alpha*acc + bias is h_pre; the tile holds
-// whole rows (N <= BN), so logits[row][k] = sum_n SiLU(h[row][n]) W2[k][n] reduce in-tile: over
-// each lane's 4 columns and NT sub-tiles, across the 4 lanes of a row (shuffles) and across the 4
-// column waves (LDS).  h_pre is stored only when C != null (it is needed by the backward).
-template <int NJ>
-__device__ __forceinline__ void epilogue_router(const Params& p, f32x4 (&acc)[4][2 * NJ], const float* bsl,
-                                                const float* w2s, float* red, int m0, int wm, int wn, int lr,
-                                                int lk) {
-  constexpr int NT = 2 * NJ, BNL = 128 * NJ;
-  const bool vec = vec_ok(p);
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) {
-    const int row = m0 + wm * 64 + mt * 16 + lr;
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      const int nl = wn * (32 * NJ) + nt * 16 + 4 * lk;
-      if (nl >= p.N) continue;
-      float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (p.bias) bv = *reinterpret_cast<const float4*>(bsl + nl);
-      const float v[4] = {p.alpha * acc[mt][nt][0] + bv.x, p.alpha * acc[mt][nt][1] + bv.y,
-                          p.alpha * acc[mt][nt][2] + bv.z, p.alpha * acc[mt][nt][3] + bv.w};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (nl + q < p.N) {
-          const float h = silu_f(v[q]);
-          s0 += h * w2s[nl + q];
-          s1 += h * w2s[BNL + nl + q];
-          s2 += h * w2s[2 * BNL + nl + q];
-        }
-      }
-      if (p.C && row < p.M) {
-        float* dst = p.C + (int64_t)row * p.ldc + nl;
-        if (vec) {
-          *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
-        } else {
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            if (nl + q < p.N) dst[q] = v[q];
-        }
-      }
-    }
-    s0 += __shfl_xor(s0, 16); s1 += __shfl_xor(s1, 16); s2 += __shfl_xor(s2, 16);
-    s0 += __shfl_xor(s0, 32); s1 += __shfl_xor(s1, 32); s2 += __shfl_xor(s2, 32);
-    if (lk == 0) {
-      float* rr = red + ((wm * 64 + mt * 16 + lr) * 4 + wn) * 3;
-      rr[0] = s0; rr[1] = s1; rr[2] = s2;
-    }
-  }
-  // LDS writes visible, then barrier -- not __syncthreads(), whose fence would emit vmcnt(0) and
-  // drain the next tile's LDS-DMA prefetch
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  for (int i = threadIdx.x; i < BM * 3; i += NTHR) {
-    const int rl = i / 3, k = i % 3;
-    const int row = m0 + rl;
-    if (row < p.M) {
-      const float* rr = red + rl * 12 + k;
-      p.R[(int64_t)row * 3 + k] = rr[0] + rr[3] + rr[6] + rr[9];
-    }
-  }
-}
-
-template <int NJ, bool CONV, int NS, bool RT>
-__global__ __launch_bounds__(NTHR, 1) void gemm_wn_kernel(Params p, int ntiles) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  typedef Cfg<NJ> CF;
-  constexpr int BN = CF::BN, NT = 2 * NJ, BNR = CF::BNR;
-  float* bias_s = reinterpret_cast<float*>(smem + NS * CF::STAGE);  // [2][BNR]
-  float* w2s = bias_s + 2 * BNR;   // RT: W2 (3 x BN), staged once
-  float* red = w2s + 3 * BN;       // RT: [BM][4][3] cross-wave logit partials
-  if constexpr (RT) {  // before any LDS-DMA is in flight, so the compiler's own waits cost nothing
-    for (int i = threadIdx.x; i < 3 * BN; i += NTHR) {
-      const int k = i / BN, n = i % BN;
-      w2s[i] = n < p.N ? p.W2[k * p.N + n] : 0.f;
-    }
-    __syncthreads();
-  }
-
-  const int nN = (p.N + BN - 1) / BN;
-  const int nk = (p.K + BK - 1) / BK;
-  const int G = gridDim.x, bid = blockIdx.x;
-  const int r = (G % 8 == 0) ? (bid & 7) * (G >> 3) + (bid >> 3) : bid;  // XCD-grouped tile ranks
-  const int my = r < ntiles ? (ntiles - r + G - 1) / G : 0;
-  const int S = my * nk;  // this workgroup's k-steps over all its tiles
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int wm = wid >> 2, wn = wid & 3;
-  const int lr = lane & 15, lk = lane >> 4;
-  const bool has_bias = p.bias != nullptr;
-  // store instructions per wave in one full-tile float4 epilogue (partial or scalar epilogues
-  // drain with vmcnt(0) instead, so this count never over-states what is in flight)
-  const int E = RT ? (p.C ? 4 * NT : 0) : 4 * NT * (p.Z ? 2 : 1);
-  const bool vec = vec_ok(p);
-
-  auto coords = [&](int j, int& m0, int& n0) __attribute__((always_inline)) {
-    const int t = j * G + r;
-    m0 = (t / nN) * BM;
-    n0 = (t % nN) * BN;
-  };
-
-  Loader<NJ, CONV> ld;
-  int ld_tile = -1;
-  auto issue = [&](int s) {
-    const int j = s / nk, kt = s - j * nk;
-    int m0, n0;
-    coords(j, m0, n0);
-    if (j != ld_tile) {
-      ld.init(p, m0, n0);
-      ld_tile = j;
-    }
-    ld.issue(p, smem + (s % NS) * CF::STAGE, kt * BK);
-    if (kt == 0 && has_bias) {  // every lane of every wave issues: uniform op count per wave
-      float* dst = bias_s + (j & 1) * BNR;
-#pragma unroll
-      for (int c0 = 0; c0 < BNR; c0 += NTHR) {
-        const int c = c0 + threadIdx.x;
-        glds4((c < BN && n0 + c < p.N) ? (const void*)(p.bias + n0 + c) : (const void*)zero_page,
-              lds_addr(dst + c0 + wid * 64));
-      }
-    }
-  };
-  auto ops_of = [&](int s) { return CF::PIECES + ((s % nk == 0 && has_bias) ? CF::BIAS_OPS : 0); };
-
-  f32x4 acc[4][NT];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-#pragma unroll
-  for (int s = 0; s < NS - 1; ++s)
-    if (s < S) issue(s);
-
-  for (int s = 0; s < S; ++s) {
-    // this wave's vector-memory ops younger than step s: later k-steps already issued and the
-    // epilogue stores of tiles that ended after step s was issued
-    int younger = 0;
-    for (int q = s + 1; q <= min(s + NS - 2, S - 1); ++q) younger += ops_of(q);
-    for (int it = max(s - NS + 1, 0); it < s; ++it)
-      if (it % nk == nk - 1) younger += E;
-    wait_vm_le(younger);
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (s + NS - 1 < S) issue(s + NS - 1);  // refills the slot every wave finished reading
-    const char* At = smem + (s % NS) * CF::STAGE;
-    const char* Bt = At + A_BYTES;
-    bf16x8 a[4], b[NT];
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      const int rr = wm * 64 + mt * 16 + lr;
-      const int sw = swa(rr);
-      const char* row = At + rr * 128;
-      const float4 x = *reinterpret_cast<const float4*>(row + 16 * ((2 * lk) ^ sw));
-      const float4 y = *reinterpret_cast<const float4*>(row + 16 * ((2 * lk + 1) ^ sw));
-      bf16x8 v;
-      v[0] = (__bf16)x.x; v[1] = (__bf16)x.y; v[2] = (__bf16)x.z; v[3] = (__bf16)x.w;
-      v[4] = (__bf16)y.x; v[5] = (__bf16)y.y; v[6] = (__bf16)y.z; v[7] = (__bf16)y.w;
-      a[mt] = v;
-    }
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      const int n = wn * (32 * NJ) + nt * 16 + lr;
-      b[nt] = *reinterpret_cast<const bf16x8*>(Bt + n * 64 + 16 * (lk ^ swb(n)));
-    }
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nt], a[mt], acc[mt][nt], 0, 0, 0);
-
-    if (s % nk == nk - 1) {  // tile done: D[n][m] layout -> lane owns C[m = lr][n = 4 lk .. 4 lk + 3]
-      const int j = s / nk;
-      int m0, n0;
-      coords(j, m0, n0);
-      const float* bsl = bias_s + (j & 1) * BNR;
-      if constexpr (RT) {
-        epilogue_router<NJ>(p, acc, bsl, w2s, red, m0, wm, wn, lr, lk);
-      } else switch (p.act) {
-        case ACT_GELU: epilogue<NJ, ACT_GELU>(p, acc, bsl, m0, n0, wm, wn, lr, lk); break;
-        case ACT_SILU: epilogue<NJ, ACT_SILU>(p, acc, bsl, m0, n0, wm, wn, lr, lk); break;
-        case ACT_SIGMOID: epilogue<NJ, ACT_SIGMOID>(p, acc, bsl, m0, n0, wm, wn, lr, lk); break;
-        case ACT_RELU: epilogue<NJ, ACT_RELU>(p, acc, bsl, m0, n0, wm, wn, lr, lk); break;
-        default: epilogue<NJ, ACT_NONE>(p, acc, bsl, m0, n0, wm, wn, lr, lk); break;
-      }
-      if (!vec || m0 + BM > p.M || n0 + BN > p.N) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int q = 0; q < NT; ++q) acc[i][q] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-// ---------------------------------------------------------------------------------------------
-// Register-staged variant (gemm_wr_kernel): the same tiles, waves, MFMA and epilogues, but both
-// operands travel global -> VGPR -> LDS with plain dwordx4 loads issued DEPTH k-steps ahead (the
-// compiler counts their vmcnt), A is converted to bf16 once on the way into LDS (the four waves
-// that share an A fragment no longer convert it four times, and the A image halves to 8 KB), and
-// the LDS images are double-buffered with one barrier per k-step.  An LDS-DMA piece costs ~100+
-// issue cycles per KB on gfx950 (MI355X_MICROARCH.md constants table); a dwordx4 load + ds_write
-// moves the same KB for a fraction of that, which is what bounded gemm_wn_kernel's pipeline.
-#ifndef WR_EPI_LDS
-#define WR_EPI_LDS 1  // LDS-staged epilogue (whole row segments per store instruction)
-#endif
-#ifndef WR_DEPTH
-#define WR_DEPTH 3  // register stages in flight (k-steps of prefetch)
-#endif
-// DEP (template): register stages, 0 = WR_DEPTH
-
-template <int NJ>
-struct WrStage {
-  float4 a[2];     // 2 x 4 fp32 of the A tile (row q/8, k chunk q%8), q = tid + 512 i
-  uint4 b[NJ];     // NJ x 8 bf16 of the W tile (row q/4, k chunk q%4), q = tid + 512 i
-};
-
-template <int NJ, bool CONV>
-__device__ __forceinline__ void wr_load(const Params& p, WrStage<NJ>& st, int m0, int n0, int k0) {
-  const int t = threadIdx.x;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int q = t + NTHR * i;
-    const int row = q >> 3, c = q & 7;
-    const int r = m0 + row, k = k0 + 4 * c;
-    bool ok = r < p.M && k < p.K;
-    int64_t o = (int64_t)r * p.lda + k;
-    if (CONV) {
-      const int pos = r % p.convF + k / p.convC - 1;
-      ok = ok && pos >= 0 && pos < p.convF;
-      o -= p.convC;
-    }
-    // unconditional load from a clamped address (a branch around the load would make the
-    // compiler drain vmcnt at the join, serialising the prefetch)
-    st.a[i] = *reinterpret_cast<const float4*>(ok ? (const void*)(p.A + o) : (const void*)zero_page);
-  }
-#pragma unroll
-  for (int i = 0; i < NJ; ++i) {
-    const int q = t + NTHR * i;
-    const int n = n0 + (q >> 2), k = k0 + 8 * (q & 3);
-    st.b[i] = *reinterpret_cast<const uint4*>((n < p.N && k < p.K) ? (const void*)(p.W + (int64_t)n * p.ldw + k)
-                                                                  : (const void*)zero_page);
-  }
-}
-
-// A image: [128 rows][4 chunks of 8 bf16] (64 B rows), W image: [BN rows][4 chunks], both with the
-// chunk XOR swizzle swb(row) (conflict-free ds_read_b128 fragment reads).
-template <int NJ>
-__device__ __forceinline__ void wr_store(const WrStage<NJ>& st, char* At, char* Bt) {
-  const int t = threadIdx.x;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int q = t + NTHR * i;
-    const int row = q >> 3, c = q & 7;
-    const float4 v = st.a[i];
-    typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-    bf16x4 h;
-    h[0] = (__bf16)v.x; h[1] = (__bf16)v.y; h[2] = (__bf16)v.z; h[3] = (__bf16)v.w;
-    *reinterpret_cast<bf16x4*>(At + row * 64 + 16 * ((c >> 1) ^ swb(row)) + 8 * (c & 1)) = h;
-  }
-#pragma unroll
-  for (int i = 0; i < NJ; ++i) {
-    const int q = t + NTHR * i;
-    const int n = q >> 2, c = q & 3;
-    *reinterpret_cast<uint4*>(Bt + n * 64 + 16 * (c ^ swb(n))) = st.b[i];
-  }
-}
-
-template <int NJ, bool CONV, bool RT, int DEP = 0>
-__global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) {  // ntiles: all tiles
-  typedef Cfg<NJ> CF;
-  constexpr int BN = CF::BN, NT = 2 * NJ, BNR = CF::BNR;
-  constexpr int AB = BM * BK * 2, BB = BN * BK * 2;  // bf16 images
-  __shared__ __attribute__((aligned(16))) char a_img[2][AB];
-  __shared__ __attribute__((aligned(16))) char b_img[2][BB];
-  __shared__ __attribute__((aligned(16))) float bias_s[2][BNR];
-  __shared__ float w2s[RT ? 3 * BN : 1];
-  __shared__ float red[RT ? BM * 12 : 1];
-  __shared__ __attribute__((aligned(16))) float ep_s[RT ? 1 : 8 * EpLds<NJ>::FLOATS];
-  if constexpr (RT) {
-    for (int i = threadIdx.x; i < 3 * BN; i += NTHR) {
-      const int k = i / BN, n = i % BN;
-      w2s[i] = n < p.N ? p.W2[k * p.N + n] : 0.f;
-    }
-  }
-
-  const int nN = (p.N + BN - 1) / BN;
-  const int nk = (p.K + BK - 1) / BK;
-  const int G = gridDim.x, bid = blockIdx.x;
-  const int r = (G % 8 == 0) ? (bid & 7) * (G >> 3) + (bid >> 3) : bid;  // XCD-grouped tile ranks
-  const int* mlist = p.mtiles;
-  if (mlist) ntiles = *p.n_mtiles * nN;  // device-side count (the list is built on the device)
-  const int my = r < ntiles ? (ntiles - r + G - 1) / G : 0;
-  const int S = my * nk;
-  float* ep = ep_s + (threadIdx.x >> 6) * EpLds<NJ>::FLOATS;
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int wm = wid >> 2, wn = wid & 3;
-  const int lr = lane & 15, lk = lane >> 4;
-  const bool vec = vec_ok(p);
-
-  auto coords = [&](int s, int& m0, int& n0, int& k0) __attribute__((always_inline)) {
-    const int j = s / nk;
-    const int t = j * G + r;
-    // past this workgroup's tiles (prefetch only) the raw index is kept: in range or beyond M
-    m0 = ((mlist && t < ntiles) ? mlist[t / nN] : t / nN) * BM;
-    n0 = (t % nN) * BN;
-    k0 = (s - j * nk) * BK;
-  };
-  auto load = [&](int s, WrStage<NJ>& st) __attribute__((always_inline)) {
-    int m0, n0, k0;
-    coords(s, m0, n0, k0);
-    wr_load<NJ, CONV>(p, st, m0, n0, k0);
-  };
-  auto store = [&](int s, const WrStage<NJ>& st) __attribute__((always_inline)) {
-    wr_store<NJ>(st, a_img[s & 1], b_img[s & 1]);
-    if (s % nk == 0) {  // first k-step of a tile: its bias slice (read by the tile's epilogue)
-      int m0, n0, k0;
-      coords(s, m0, n0, k0);
-      float* dst = bias_s[(s / nk) & 1];
-      for (int c = threadIdx.x; c < BN; c += NTHR) dst[c] = (p.bias && n0 + c < p.N) ? p.bias[n0 + c] : 0.f;
-    }
-  };
-
-  f32x4 acc[4][NT];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // stage register sets are named variables (an array, even constant-indexed after unrolling,
-  // ends up in scratch)
-  constexpr int DEPTH = DEP ? DEP : WR_DEPTH;
-  static_assert(DEPTH >= 3 && DEPTH <= 5, "stage sets are written out for depths 3..5");
-  WrStage<NJ> st0, st1, st2, st3, st4;  // st3 / st4 unused (eliminated) below depth 4 / 5
-  if (S > 0) load(0, st0);
-  if (S > 1) load(1, st1);
-  if (S > 2) load(2, st2);
-  if constexpr (DEPTH >= 4)
-    if (S > 3) load(3, st3);
-  if constexpr (DEPTH >= 5)
-    if (S > 4) load(4, st4);
-  if (S > 0) store(0, st0);
-  __syncthreads();
-
-  // one k-step: `cur` held step s (already in LDS) and is refilled with step s + 3; `nxt` holds
-  // step s + 1, which goes into the other LDS image after this step's MFMAs
-  auto kstep = [&](int s, WrStage<NJ>& cur, const WrStage<NJ>& nxt) __attribute__((always_inline)) {
-    // unconditional: past the last step the A rows fall beyond M and read the zero page, so the
-    // number of loads in flight is the same on every path and the compiler's vmcnt waits stay
-    // counted (a conditional load here would force vmcnt(0) at every later wait)
-    load(s + DEPTH, cur);
-    const char* At = a_img[s & 1];
-    const char* Bt = b_img[s & 1];
-    bf16x8 a[4], b[NT];
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      const int rr = wm * 64 + mt * 16 + lr;
-      a[mt] = *reinterpret_cast<const bf16x8*>(At + rr * 64 + 16 * (lk ^ swb(rr)));
-    }
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      const int n = wn * (32 * NJ) + nt * 16 + lr;
-      b[nt] = *reinterpret_cast<const bf16x8*>(Bt + n * 64 + 16 * (lk ^ swb(n)));
-    }
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nt], a[mt], acc[mt][nt], 0, 0, 0);
-    if (s + 1 < S) store(s + 1, nxt);
-    if (s % nk == nk - 1) {
-      int m0, n0, k0;
-      coords(s, m0, n0, k0);
-      const float* bsl = bias_s[(s / nk) & 1];
-      if constexpr (RT) {
-        epilogue_router<NJ>(p, acc, bsl, w2s, red, m0, wm, wn, lr, lk);
-      } else if (WR_EPI_LDS && vec) switch (p.act) {
-        case ACT_GELU: epilogue_lds<NJ, ACT_GELU>(p, acc, bsl, m0, n0, wm, wn, lr, lk, ep); break;
-        case ACT_SILU: epilogue_lds<NJ, ACT_SILU>(p, acc, bsl, m0, n0, wm, wn, lr, lk, ep); break;
-        case ACT_SIGMOID: epilogue_lds<NJ, ACT_SIGMOID>(p, acc, bsl, m0, n0, wm, wn, lr, lk, ep); break;
-        case ACT_RELU: epilogue_lds<NJ, ACT_RELU>(p, acc, bsl, m0, n0, wm, wn, lr, lk, ep); break;
-        default: epilogue_lds<NJ, ACT_NONE>(p, acc, bsl, m0, n0, wm, wn, lr, lk, ep); break;
-      } else switch (p.act) {
-        case ACT_GELU: epilogue<NJ, ACT_GELU>(p, acc, bsl, m0, n0, wm, wn, lr, lk); break;
-        case ACT_SILU: epilogue<NJ, ACT_SILU>(p, acc, bsl, m0, n0, wm, wn, lr, lk); break;
-        case ACT_SIGMOID: epilogue<NJ, ACT_SIGMOID>(p, acc, bsl, m0, n0, wm, wn, lr, lk); break;
-        case ACT_RELU: epilogue<NJ, ACT_RELU>(p, acc, bsl, m0, n0, wm, wn, lr, lk); break;
-        default: epilogue<NJ, ACT_NONE>(p, acc, bsl, m0, n0, wm, wn, lr, lk); break;
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int q = 0; q < NT; ++q) acc[i][q] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    __syncthreads();
-  };
-
-  for (int s = 0; s < S; s += DEPTH) {
-    if constexpr (DEPTH == 3) {
-      kstep(s, st0, st1);
-      if (s + 1 < S) kstep(s + 1, st1, st2);
-      if (s + 2 < S) kstep(s + 2, st2, st0);
-    } else if constexpr (DEPTH == 4) {
-      kstep(s, st0, st1);
-      if (s + 1 < S) kstep(s + 1, st1, st2);
-      if (s + 2 < S) kstep(s + 2, st2, st3);
-      if (s + 3 < S) kstep(s + 3, st3, st0);
-    } else {
-      kstep(s, st0, st1);
-      if (s + 1 < S) kstep(s + 1, st1, st2);
-      if (s + 2 < S) kstep(s + 2, st2, st3);
-      if (s + 3 < S) kstep(s + 3, st3, st4);
-      if (s + 4 < S) kstep(s + 4, st4, st0);
-    }
-  }
-}
-
-template <int NJ, bool CONV, bool RT = false>
-static void launch_wr(const Params& p, hipStream_t s) {
-  static int resident = 0;
-  const void* fn = (const void*)gemm_wr_kernel<NJ, CONV, RT>;
-  if (!resident) {
-    int per_cu = 0, dev = 0, cus = 0;
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, NTHR, 0);
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    resident = std::max(1, per_cu) * std::max(1, cus);
-  }
-  const int tiles = ((p.M + BM - 1) / BM) * ((p.N + Cfg<NJ>::BN - 1) / Cfg<NJ>::BN);
-  const int grid = std::min(tiles, resident);
-  // a 5-deep pipeline (DEP = 5) for the one-wave 8192-row text-side launches measured 32.4 us vs
-  // 30.1 us at depth 3 (profiles/r02_bench_v8_kernel_stats.csv): their time is not load latency
-  gemm_wr_kernel<NJ, CONV, RT><<<grid, NTHR, 0, s>>>(p, tiles);
-}
 
 // fp32 (rows x cols, row stride ld) -> bf16 N x K contiguous.  trans == 0: N = rows, K = cols;
 // trans == 1: N = cols, K = rows (the weight is used transposed, e.g. dgrad's dY W).
@@ -692,25 +25,6 @@ __global__ void weight_to_bf16_kernel(const float* __restrict__ src, unsigned sh
     __bf16 h = (__bf16)src[r * ld + c];
     dst[o] = __builtin_bit_cast(unsigned short, h);
   }
-}
-
-template <int NJ, bool CONV, int NS, bool RT = false>
-static void launch(const Params& p, hipStream_t s) {
-  typedef Cfg<NJ> CF;
-  static int resident = 0;
-  const int shm = NS * CF::STAGE + 2 * CF::BNR * 4 + (RT ? (3 * CF::BN + BM * 12) * 4 : 0);
-  if (!resident) {
-    (void)hipFuncSetAttribute((const void*)gemm_wn_kernel<NJ, CONV, NS, RT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              shm);
-    int per_cu = 0, dev = 0, cus = 0;
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)gemm_wn_kernel<NJ, CONV, NS, RT>, NTHR, shm);
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    resident = std::max(1, per_cu) * std::max(1, cus);
-  }
-  const int tiles = ((p.M + BM - 1) / BM) * ((p.N + CF::BN - 1) / CF::BN);
-  const int grid = std::min(tiles, resident);
-  gemm_wn_kernel<NJ, CONV, NS, RT><<<grid, NTHR, shm, s>>>(p, tiles);
 }
 
 }  // namespace wn
@@ -786,23 +100,38 @@ extern "C" int asrx_gemm_wn(const float* A, int64_t lda, int conv, int64_t convF
   ASRX_REQUIRE(!conv || (convF > 0 && convC % 4 == 0), "asrx_gemm_wn: conv needs F > 0 and C %% 4 == 0");
   wn::Params p{A, (int)lda, W, (int)ldw, C, (int)ldc, bias, Z, (int)M, (int)N, (int)K,
                (int)(convF > 0 ? convF : 1), (int)(convC > 0 ? convC : 1), alpha, beta, act, nullptr, nullptr};
-  static const bool use_dma = getenv("ASRX_WN_IMPL") && std::string(getenv("ASRX_WN_IMPL")) == "dma";
-  if (!use_dma) {
-    if (nj == 3) conv ? wn::launch_wr<3, true>(p, stream) : wn::launch_wr<3, false>(p, stream);
-    else if (nj == 2) conv ? wn::launch_wr<2, true>(p, stream) : wn::launch_wr<2, false>(p, stream);
-    else conv ? wn::launch_wr<1, true>(p, stream) : wn::launch_wr<1, false>(p, stream);
-    ASRX_LAUNCHED("asrx_gemm_wn");
-  }
-  // ring depth: 3 stages for short K (more tile switches to hide), 2 for long K (measured)
-  if (nj == 3) {
-    if (K <= 512) conv ? wn::launch<3, true, 3>(p, stream) : wn::launch<3, false, 3>(p, stream);
-    else conv ? wn::launch<3, true, 2>(p, stream) : wn::launch<3, false, 2>(p, stream);
-  } else if (nj == 2) {
-    conv ? wn::launch<2, true, 2>(p, stream) : wn::launch<2, false, 2>(p, stream);
-  } else {
-    conv ? wn::launch<1, true, 3>(p, stream) : wn::launch<1, false, 3>(p, stream);
-  }
+  if (nj == 3) conv ? wn::launch_wr<3, true>(p, stream) : wn::launch_wr<3, false>(p, stream);
+  else if (nj == 2) conv ? wn::launch_wr<2, true>(p, stream) : wn::launch_wr<2, false>(p, stream);
+  else conv ? wn::launch_wr<1, true>(p, stream) : wn::launch_wr<1, false>(p, stream);
   ASRX_LAUNCHED("asrx_gemm_wn");
+}
+
+// asrx_gemm_wn with storage types: A fp32 (a_bf16 = 0) or bf16 (1); C fp32 (c_bf16 = 0) or bf16 (1,
+// beta = 0; Z, when given, stays fp32); optionally restricted to the device tile list mtiles (as
+// asrx_gemm_wn_rows, non-conv only).
+extern "C" int asrx_gemm_wn_ex(const void* A, int a_bf16, int64_t lda, int conv, int64_t convF, int64_t convC,
+                               const unsigned short* W, int64_t ldw, void* C, int c_bf16, int64_t ldc,
+                               const float* bias, float* Z, int64_t M, int64_t N, int64_t K, float alpha, float beta,
+                               int act, int nj, const int* mtiles, const int* n_mtiles, hipStream_t stream) {
+  ASRX_REQUIRE(M > 0 && N > 0 && K > 0, "asrx_gemm_wn_ex: empty problem");
+  ASRX_REQUIRE(((uintptr_t)A & 15) == 0 && ((uintptr_t)W & 15) == 0, "asrx_gemm_wn_ex: A/W must be 16-byte aligned");
+  ASRX_REQUIRE(K % 8 == 0 && lda % (a_bf16 ? 8 : 4) == 0 && ldw % 8 == 0,
+               "asrx_gemm_wn_ex: K%%8, lda%%4 (fp32) / lda%%8 (bf16), ldw%%8 required");
+  ASRX_REQUIRE(M * lda < (1LL << 31) && N * ldw < (1LL << 31), "asrx_gemm_wn_ex: operand spans >= 2^31 elements");
+  ASRX_REQUIRE(!conv || (convF > 0 && convC % (a_bf16 ? 8 : 4) == 0), "asrx_gemm_wn_ex: conv needs F > 0 and C %% 4 (8 for bf16)");
+  ASRX_REQUIRE(!c_bf16 || beta == 0.f, "asrx_gemm_wn_ex: a bf16 output takes beta = 0");
+  ASRX_REQUIRE(!(conv && mtiles), "asrx_gemm_wn_ex: tile lists are for plain GEMMs");
+  wn::Params p{(const float*)A, (int)lda, W, (int)ldw, c_bf16 ? nullptr : (float*)C, (int)ldc, bias, Z, (int)M,
+               (int)N, (int)K, (int)(convF > 0 ? convF : 1), (int)(convC > 0 ? convC : 1), alpha, beta, act,
+               nullptr, nullptr, mtiles, n_mtiles, c_bf16 ? (unsigned short*)C : nullptr};
+#define ASRX_WN_EX(NJV)                                                                              \
+  if (a_bf16) conv ? wn::launch_wr<NJV, true, false, true>(p, stream) : wn::launch_wr<NJV, false, false, true>(p, stream); \
+  else conv ? wn::launch_wr<NJV, true>(p, stream) : wn::launch_wr<NJV, false>(p, stream);
+  if (nj == 3) { ASRX_WN_EX(3) }
+  else if (nj == 2) { ASRX_WN_EX(2) }
+  else { ASRX_WN_EX(1) }
+#undef ASRX_WN_EX
+  ASRX_LAUNCHED("asrx_gemm_wn_ex");
 }
 
 // asrx_gemm_wn restricted to the BM-row tiles listed in mtiles (n_mtiles entries, both on the device,
@@ -886,16 +215,8 @@ extern "C" int asrx_gemm_wn_router(const float* A, int64_t lda, const unsigned s
   ASRX_REQUIRE(M * lda < (1LL << 31), "asrx_gemm_wn_router: operand spans >= 2^31 elements");
   wn::Params p{A, (int)lda, W1, (int)ldw, hpre, (int)ldc, b1, nullptr, (int)M, (int)N, (int)K, 1, 1, 1.f, 0.f,
                ACT_NONE, W2, logits};
-  static const bool use_dma = getenv("ASRX_WN_IMPL") && std::string(getenv("ASRX_WN_IMPL")) == "dma";
-  if (!use_dma) {
-    if (N <= 128) wn::launch_wr<1, false, true>(p, stream);
-    else if (N <= 256) wn::launch_wr<2, false, true>(p, stream);
-    else wn::launch_wr<3, false, true>(p, stream);
-    ASRX_LAUNCHED("asrx_gemm_wn_router");
-  }
-  if (N <= 128) wn::launch<1, false, 3, true>(p, stream);
-  else if (N <= 256) wn::launch<2, false, 2, true>(p, stream);
-  else if (K <= 512) wn::launch<3, false, 3, true>(p, stream);
-  else wn::launch<3, false, 2, true>(p, stream);
+  if (N <= 128) wn::launch_wr<1, false, true>(p, stream);
+  else if (N <= 256) wn::launch_wr<2, false, true>(p, stream);
+  else wn::launch_wr<3, false, true>(p, stream);
   ASRX_LAUNCHED("asrx_gemm_wn_router");
 }

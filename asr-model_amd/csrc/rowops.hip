@@ -39,29 +39,46 @@ __device__ __forceinline__ void flush_partials(float* part, int n, float* dst) {
 // Register-resident variants for d = 64 E (E even): a lane owns E consecutive features (float2
 // I/O), the row is read once, statistics by DPP wave sums, the next row is prefetched; the backward
 // keeps its dw / db partials in registers.  The generic kernels below remain for other d.
+// Row layout of the one-wave-per-row kernels (LayerNorm, MSheath row passes): lane l owns the E
+// features 128 j + 2 l + {0, 1}, j < E / 2, so each float2 load / store instruction of the wave moves
+// 512 contiguous bytes (fully coalesced).  Only reductions and per-feature maps run in this layout; every
+// per-feature operand (x, w, b, gw, px, dx, the LDS partials) uses the same mapping.
+template <int E>
+__device__ __forceinline__ int lane_feat(int lane, int e) {
+  static_assert(E % 2 == 0, "row kernels take E = D / 64 even");
+  return 128 * (e >> 1) + 2 * lane + (e & 1);
+}
 template <int E>
 __device__ __forceinline__ void ld_lane(const float* __restrict__ src, int lane, float (&v)[E]) {
-  const float2* s2 = reinterpret_cast<const float2*>(src + lane * E);
+  const float2* s2 = reinterpret_cast<const float2*>(src);
 #pragma unroll
   for (int e = 0; e < E / 2; ++e) {
-    const float2 t = s2[e];
+    const float2 t = s2[64 * e + lane];
     v[2 * e] = t.x;
     v[2 * e + 1] = t.y;
   }
 }
 template <int E>
 __device__ __forceinline__ void st_lane(float* __restrict__ dst, int lane, const float (&v)[E]) {
-  float2* d2 = reinterpret_cast<float2*>(dst + lane * E);
+  float2* d2 = reinterpret_cast<float2*>(dst);
 #pragma unroll
-  for (int e = 0; e < E / 2; ++e) d2[e] = make_float2(v[2 * e], v[2 * e + 1]);
+  for (int e = 0; e < E / 2; ++e) d2[64 * e + lane] = make_float2(v[2 * e], v[2 * e + 1]);
+}
+template <int E>
+__device__ __forceinline__ void st_lane(unsigned short* __restrict__ dst, int lane, const float (&v)[E]) {
+  unsigned* d2 = reinterpret_cast<unsigned*>(dst);
+#pragma unroll
+  for (int e = 0; e < E / 2; ++e)
+    d2[64 * e + lane] = (unsigned)__builtin_bit_cast(unsigned short, (__bf16)v[2 * e]) |
+                        ((unsigned)__builtin_bit_cast(unsigned short, (__bf16)v[2 * e + 1]) << 16);
 }
 
 // Optional fused row outputs (MSheath, asrx/msheath.py): nrm[r] = |x_r|_2 (v_gate's normalisation of
 // the same x, model.py:347) and gout[r] = sigmoid(y_r . gw + gb) (the Linear(D, 1) gate on the
 // normalised row: layers[i].gate at model.py:460, mlp_gate at 503 on x itself when gate_on_x).
-template <int E>
+template <int E, typename TY = float>
 __global__ __launch_bounds__(64 * RW) void ln_fwd_t_kernel(const float* __restrict__ x, const float* __restrict__ w,
-                                                           const float* __restrict__ b, float* __restrict__ y,
+                                                           const float* __restrict__ b, TY* __restrict__ y,
                                                            float* __restrict__ mean, float* __restrict__ rstd,
                                                            int64_t rows, float eps, float* __restrict__ nrm,
                                                            const float* __restrict__ gw, const float* __restrict__ gb,
@@ -155,8 +172,8 @@ __global__ __launch_bounds__(64 * RW) void ln_bwd_t_kernel(const float* __restri
   }
 #pragma unroll
   for (int e = 0; e < E; ++e) {
-    part[wid][lane * E + e] = aw[e];
-    part[wid][D + lane * E + e] = ab[e];
+    part[wid][lane_feat<E>(lane, e)] = aw[e];
+    part[wid][D + lane_feat<E>(lane, e)] = ab[e];
   }
   __syncthreads();
   for (int j = threadIdx.x; j < D; j += 64 * RW) {
@@ -242,20 +259,24 @@ __global__ __launch_bounds__(64 * RW) void ln_bwd_kernel(const float* __restrict
 // y[r, n] = act(x[r] . W[n] + b[n]) for N <= 4 outputs: gate / mem_gate / mlp_gate Linear(D, 1)
 // (model.py:398, 406, 420), v_gate.mlp[2] Linear(D/2, 1) and concat (model.py:341, 344),
 // tgate.cs Linear(D, 3) (model.py:530), MPNet's Linear(128, 3) (model.py:381).
-template <int NS>
-__global__ __launch_bounds__(64 * RW) void small_linear_fwd_kernel(const float* __restrict__ x,
+// x stored fp32 or bf16 (TX = unsigned short: tgate's input is a bf16-stored AbbyNormal output)
+__device__ __forceinline__ float ldx(const float* p) { return *p; }
+__device__ __forceinline__ float ldx(const unsigned short* p) { return __uint_as_float((unsigned)*p << 16); }
+
+template <int NS, typename TX = float>
+__global__ __launch_bounds__(64 * RW) void small_linear_fwd_kernel(const TX* __restrict__ x,
                                                                    const float* __restrict__ W,
                                                                    const float* __restrict__ b,
                                                                    float* __restrict__ y, int64_t rows, int K,
                                                                    int act) {
   const int lane = threadIdx.x & 63;
   for (int64_t r = row_begin(); r < rows; r += row_step()) {
-    const float* xr = x + r * K;
+    const TX* xr = x + r * K;
     float acc[NS];
 #pragma unroll
     for (int n = 0; n < NS; ++n) acc[n] = 0.f;
     for (int k = lane; k < K; k += 64) {
-      const float xv = xr[k];
+      const float xv = ldx(xr + k);
 #pragma unroll
       for (int n = 0; n < NS; ++n) acc[n] += xv * W[n * K + k];
     }
@@ -268,9 +289,9 @@ __global__ __launch_bounds__(64 * RW) void small_linear_fwd_kernel(const float* 
 }
 
 // dy is the gradient of the post-activation output; y the saved output (for sigmoid').
-template <int NS>
+template <int NS, typename TX = float>
 __global__ __launch_bounds__(64 * RW) void small_linear_bwd_kernel(
-    const float* __restrict__ dy, const float* __restrict__ y, const float* __restrict__ x,
+    const float* __restrict__ dy, const float* __restrict__ y, const TX* __restrict__ x,
     const float* __restrict__ W, float* __restrict__ dx, float* __restrict__ dW, float* __restrict__ db,
     int64_t rows, int K, int act, float beta) {
   extern __shared__ float part[];  // [RW][NS*K + NS]
@@ -289,10 +310,10 @@ __global__ __launch_bounds__(64 * RW) void small_linear_bwd_kernel(
       }
       dz[n] = g;
     }
-    const float* xr = x + r * K;
+    const TX* xr = x + r * K;
     float* dxr = dx ? dx + r * K : nullptr;
     for (int k = lane; k < K; k += 64) {
-      const float xv = xr[k];
+      const float xv = ldx(xr + k);
       float s = 0.f;
 #pragma unroll
       for (int n = 0; n < NS; ++n) {
@@ -534,6 +555,7 @@ struct MSRowFwd {
   const float* next_i;  // rows of samples b with next_i[b] != layer are not at this layer (null: all are)
   int layer;
   int64_t L;
+  unsigned short* pxb;  // non-null: px stored bf16 here instead (it only feeds the adapter GEMM)
 };
 
 // Per row: px = LayerNorm(x); nx = |x|; g = sigmoid(px . gw + gb); v_gate from SH and nx (as
@@ -558,7 +580,8 @@ __global__ __launch_bounds__(64 * RW) void msheath_row_fwd_kernel(MSRowFwd p) {
       float z[E];
 #pragma unroll
       for (int e = 0; e < E; ++e) z[e] = 0.f;
-      st_lane<E>(p.px + r * D, lane, z);
+      if (p.pxb) st_lane<E>(p.pxb + r * D, lane, z);
+      else st_lane<E>(p.px + r * D, lane, z);
       if (lane == 0) {
         p.mean[r] = 0.f;
         p.rstd[r] = 0.f;
@@ -595,7 +618,8 @@ __global__ __launch_bounds__(64 * RW) void msheath_row_fwd_kernel(MSRowFwd p) {
       yv[e] = (xv[e] - mu) * rs * wv[e] + bv[e];
       gd += yv[e] * gwv[e];
     }
-    st_lane<E>(p.px + r * D, lane, yv);
+    if (p.pxb) st_lane<E>(p.pxb + r * D, lane, yv);
+    else st_lane<E>(p.px + r * D, lane, yv);
     const float gate = sigmoid_f(wave_sum_dpp(gd) + gbias);
     // v_gate
     const float* S = p.SH + r * p.ldsh;
@@ -734,9 +758,9 @@ __global__ __launch_bounds__(64 * RW) void msheath_row_bwd_kernel(MSRowBwd p) {
   float* pl = part + wid * 3 * D;
 #pragma unroll
   for (int e = 0; e < E; ++e) {
-    pl[lane * E + e] = aw[e];
-    pl[D + lane * E + e] = ab[e];
-    pl[2 * D + lane * E + e] = ag[e];
+    pl[lane_feat<E>(lane, e)] = aw[e];
+    pl[D + lane_feat<E>(lane, e)] = ab[e];
+    pl[2 * D + lane_feat<E>(lane, e)] = ag[e];
   }
   __syncthreads();
   for (int j = threadIdx.x; j < 3 * D; j += 64 * RW) {
@@ -763,8 +787,9 @@ __global__ __launch_bounds__(64 * RW) void msheath_row_bwd_kernel(MSRowBwd p) {
 
 // ============================================================================ tgate
 // model.py:532-535 (num_types=3): out[d] = sum_k G[k*D + d] * softmax(c)[k], G = sigmoid(...)
+template <typename TO = float>
 __global__ __launch_bounds__(64 * RW) void tgate_fwd_kernel(const float* __restrict__ G, const float* __restrict__ c,
-                                                            float* __restrict__ out, int64_t rows, int D) {
+                                                            TO* __restrict__ out, int64_t rows, int D) {
   const int lane = threadIdx.x & 63;
   for (int64_t r = row_begin(); r < rows; r += row_step()) {
     const float c0 = c[r * 3], c1 = c[r * 3 + 1], c2 = c[r * 3 + 2];
@@ -773,7 +798,11 @@ __global__ __launch_bounds__(64 * RW) void tgate_fwd_kernel(const float* __restr
     const float inv = 1.f / (e0 + e1 + e2);
     const float t0 = e0 * inv, t1 = e1 * inv, t2 = e2 * inv;
     const float* gr = G + r * 3 * D;
-    for (int j = lane; j < D; j += 64) out[r * D + j] = gr[j] * t0 + gr[D + j] * t1 + gr[2 * D + j] * t2;
+    for (int j = lane; j < D; j += 64) {
+      const float v = gr[j] * t0 + gr[D + j] * t1 + gr[2 * D + j] * t2;
+      if constexpr (sizeof(TO) == 4) out[r * D + j] = v;
+      else out[r * D + j] = __builtin_bit_cast(unsigned short, (__bf16)v);
+    }
   }
 }
 
@@ -1782,14 +1811,21 @@ int asrx_layernorm_fwd(const float* x, const float* w, const float* b, float* y,
 
 // LayerNorm forward with the fused row outputs of ln_fwd_t_kernel (nrm and/or the sigmoid gate; each
 // may be null).  d must be one of 128, 256, 384, 512, 768, 1024.
-int asrx_layernorm_fwd2(const float* x, const float* w, const float* b, float* y, float* mean, float* rstd,
+// y stored fp32 (y_bf16 = 0) or bf16 (1: MSheath's mlp_ln output only feeds mlp[0], model.py:503-506)
+int asrx_layernorm_fwd3(const float* x, const float* w, const float* b, void* y, int y_bf16, float* mean, float* rstd,
                         float* nrm, const float* gw, const float* gb, float* gout, int gate_on_x, int64_t rows,
                         int64_t d, float eps, hipStream_t stream) {
   if (rows == 0) return 0;
   const bool al = ((((uintptr_t)x | (uintptr_t)w | (uintptr_t)b | (uintptr_t)y | (uintptr_t)gw) & 7) == 0);
   ASRX_REQUIRE(al, "asrx_layernorm_fwd2: 8-byte aligned rows required");
   switch (d) {
-#define LNF(E) LAUNCH_ROWS(ln_fwd_t_kernel<E>, rows, 0, x, w, b, y, mean, rstd, rows, eps, nrm, gw, gb, gout, gate_on_x)
+#define LNF(E)                                                                                                    \
+  if (y_bf16)                                                                                                     \
+    LAUNCH_ROWS((ln_fwd_t_kernel<E, unsigned short>), rows, 0, x, w, b, (unsigned short*)y, mean, rstd, rows, eps, \
+                nrm, gw, gb, gout, gate_on_x);                                                                    \
+  else                                                                                                            \
+    LAUNCH_ROWS((ln_fwd_t_kernel<E, float>), rows, 0, x, w, b, (float*)y, mean, rstd, rows, eps, nrm, gw, gb, gout, \
+                gate_on_x)
     case 128: LNF(2); break;
     case 256: LNF(4); break;
     case 384: LNF(6); break;
@@ -1800,6 +1836,12 @@ int asrx_layernorm_fwd2(const float* x, const float* w, const float* b, float* y
     default: ASRX_REQUIRE(false, "asrx_layernorm_fwd2: d=%ld unsupported", (long)d);
   }
   ASRX_LAUNCHED("asrx_layernorm_fwd2");
+}
+
+int asrx_layernorm_fwd2(const float* x, const float* w, const float* b, float* y, float* mean, float* rstd,
+                        float* nrm, const float* gw, const float* gb, float* gout, int gate_on_x, int64_t rows,
+                        int64_t d, float eps, hipStream_t stream) {
+  return asrx_layernorm_fwd3(x, w, b, y, 0, mean, rstd, nrm, gw, gb, gout, gate_on_x, rows, d, eps, stream);
 }
 
 int asrx_layernorm_bwd_acc(const float* dy, const float* x, const float* w, const float* mean, const float* rstd,
@@ -1829,33 +1871,67 @@ int asrx_layernorm_bwd(const float* dy, const float* x, const float* w, const fl
   return asrx_layernorm_bwd_acc(dy, x, w, mean, rstd, dx, dw, db, rows, d, 0, stream);
 }
 
-int asrx_small_linear_fwd(const float* x, const float* W, const float* b, float* y, int64_t rows, int64_t K,
-                          int64_t N, int act, hipStream_t stream) {
-  if (rows == 0) return 0;
+}  // extern "C"
+template <typename TX>
+static int small_linear_fwd_t(const TX* x, const float* W, const float* b, float* y, int64_t rows, int64_t K,
+                              int64_t N, int act, hipStream_t stream) {
   switch (N) {
-    case 1: LAUNCH_ROWS(small_linear_fwd_kernel<1>, rows, 0, x, W, b, y, rows, (int)K, act); break;
-    case 2: LAUNCH_ROWS(small_linear_fwd_kernel<2>, rows, 0, x, W, b, y, rows, (int)K, act); break;
-    case 3: LAUNCH_ROWS(small_linear_fwd_kernel<3>, rows, 0, x, W, b, y, rows, (int)K, act); break;
-    case 4: LAUNCH_ROWS(small_linear_fwd_kernel<4>, rows, 0, x, W, b, y, rows, (int)K, act); break;
+    case 1: LAUNCH_ROWS((small_linear_fwd_kernel<1, TX>), rows, 0, x, W, b, y, rows, (int)K, act); break;
+    case 2: LAUNCH_ROWS((small_linear_fwd_kernel<2, TX>), rows, 0, x, W, b, y, rows, (int)K, act); break;
+    case 3: LAUNCH_ROWS((small_linear_fwd_kernel<3, TX>), rows, 0, x, W, b, y, rows, (int)K, act); break;
+    case 4: LAUNCH_ROWS((small_linear_fwd_kernel<4, TX>), rows, 0, x, W, b, y, rows, (int)K, act); break;
     default: ASRX_REQUIRE(false, "small_linear: N=%ld not in 1..4", (long)N);
   }
+  return 0;
+}
+
+extern "C" {
+// x stored fp32 (x_bf16 = 0) or bf16 (1)
+int asrx_small_linear_fwd2(const void* x, int x_bf16, const float* W, const float* b, float* y, int64_t rows,
+                           int64_t K, int64_t N, int act, hipStream_t stream) {
+  if (rows == 0) return 0;
+  const int rc = x_bf16 ? small_linear_fwd_t((const unsigned short*)x, W, b, y, rows, K, N, act, stream)
+                        : small_linear_fwd_t((const float*)x, W, b, y, rows, K, N, act, stream);
+  if (rc) return rc;
   ASRX_LAUNCHED("asrx_small_linear_fwd");
 }
 
-int asrx_small_linear_bwd(const float* dy, const float* y, const float* x, const float* W, float* dx, float* dW,
-                          float* db, int64_t rows, int64_t K, int64_t N, int act, float beta, hipStream_t stream) {
-  if (rows == 0) return 0;
+int asrx_small_linear_fwd(const float* x, const float* W, const float* b, float* y, int64_t rows, int64_t K,
+                          int64_t N, int act, hipStream_t stream) {
+  return asrx_small_linear_fwd2(x, 0, W, b, y, rows, K, N, act, stream);
+}
+
+}  // extern "C"
+template <typename TX>
+static int small_linear_bwd_t(const float* dy, const float* y, const TX* x, const float* W, float* dx, float* dW,
+                              float* db, int64_t rows, int64_t K, int64_t N, int act, float beta, hipStream_t stream) {
   const size_t shm = (size_t)RW * (N * K + N) * sizeof(float);
   ASRX_REQUIRE(shm <= 64 * 1024, "small_linear_bwd: K too large");
   const unsigned g = row_grid(rows, 1024);
   switch (N) {
-    case 1: small_linear_bwd_kernel<1><<<g, 64 * RW, shm, stream>>>(dy, y, x, W, dx, dW, db, rows, (int)K, act, beta); break;
-    case 2: small_linear_bwd_kernel<2><<<g, 64 * RW, shm, stream>>>(dy, y, x, W, dx, dW, db, rows, (int)K, act, beta); break;
-    case 3: small_linear_bwd_kernel<3><<<g, 64 * RW, shm, stream>>>(dy, y, x, W, dx, dW, db, rows, (int)K, act, beta); break;
-    case 4: small_linear_bwd_kernel<4><<<g, 64 * RW, shm, stream>>>(dy, y, x, W, dx, dW, db, rows, (int)K, act, beta); break;
+    case 1: small_linear_bwd_kernel<1, TX><<<g, 64 * RW, shm, stream>>>(dy, y, x, W, dx, dW, db, rows, (int)K, act, beta); break;
+    case 2: small_linear_bwd_kernel<2, TX><<<g, 64 * RW, shm, stream>>>(dy, y, x, W, dx, dW, db, rows, (int)K, act, beta); break;
+    case 3: small_linear_bwd_kernel<3, TX><<<g, 64 * RW, shm, stream>>>(dy, y, x, W, dx, dW, db, rows, (int)K, act, beta); break;
+    case 4: small_linear_bwd_kernel<4, TX><<<g, 64 * RW, shm, stream>>>(dy, y, x, W, dx, dW, db, rows, (int)K, act, beta); break;
     default: ASRX_REQUIRE(false, "small_linear: N=%ld not in 1..4", (long)N);
   }
+  return 0;
+}
+
+extern "C" {
+int asrx_small_linear_bwd2(const float* dy, const float* y, const void* x, int x_bf16, const float* W, float* dx,
+                           float* dW, float* db, int64_t rows, int64_t K, int64_t N, int act, float beta,
+                           hipStream_t stream) {
+  if (rows == 0) return 0;
+  const int rc = x_bf16 ? small_linear_bwd_t(dy, y, (const unsigned short*)x, W, dx, dW, db, rows, K, N, act, beta, stream)
+                        : small_linear_bwd_t(dy, y, (const float*)x, W, dx, dW, db, rows, K, N, act, beta, stream);
+  if (rc) return rc;
   ASRX_LAUNCHED("asrx_small_linear_bwd");
+}
+
+int asrx_small_linear_bwd(const float* dy, const float* y, const float* x, const float* W, float* dx, float* dW,
+                          float* db, int64_t rows, int64_t K, int64_t N, int act, float beta, hipStream_t stream) {
+  return asrx_small_linear_bwd2(dy, y, x, 0, W, dx, dW, db, rows, K, N, act, beta, stream);
 }
 
 int asrx_row_normalize(const float* x, float* y, float* n, int64_t rows, int64_t d, hipStream_t stream) {
@@ -1979,20 +2055,31 @@ static bool ms_aligned(std::initializer_list<const void*> ps) {
 }
 
 // Fused MSheath layer row pass (msheath_row_fwd_kernel); SH = [S | h] with row stride ldsh >= M + Dh.
+int asrx_msheath_row_fwd2(const float* x, const float* lnw, const float* lnb, const float* gw, const float* gb,
+                          const float* SH, int64_t ldsh, const float* mval, const float* w2, const float* b2,
+                          const float* cw, const float* cb, const float* tx, void* px, int px_bf16, float* mean,
+                          float* rstd, float* nx, float* g, float* ion, float* kv, float* m2, int64_t rows, int64_t d,
+                          int64_t M, int64_t Dh, float eps, float inv_sqrt_d, const float* next_i, int64_t layer,
+                          int64_t L, hipStream_t stream) {
+  ASRX_REQUIRE(M <= 64 && ldsh >= M + Dh, "asrx_msheath_row_fwd: M <= 64 and ldsh >= M + Dh required");
+  ASRX_REQUIRE(ms_aligned({x, lnw, lnb, gw, (const float*)px}), "asrx_msheath_row_fwd: 8-byte aligned rows required");
+  ASRX_REQUIRE(!next_i || L > 0, "asrx_msheath_row_fwd: L > 0 required with next_i");
+  if (rows == 0) return 0;
+  MSRowFwd p{x, lnw, lnb, gw, gb, SH, mval, w2, b2, cw, cb, tx, px_bf16 ? nullptr : (float*)px, mean, rstd, nx, g,
+             ion, kv, m2, rows, ldsh, (int)M, (int)Dh, eps, inv_sqrt_d, next_i, (int)layer, L > 0 ? L : 1,
+             px_bf16 ? (unsigned short*)px : nullptr};
+  MS_DISPATCH(msheath_row_fwd_kernel, row_grid(rows), 0, p);
+  ASRX_LAUNCHED("asrx_msheath_row_fwd");
+}
+
 int asrx_msheath_row_fwd(const float* x, const float* lnw, const float* lnb, const float* gw, const float* gb,
                          const float* SH, int64_t ldsh, const float* mval, const float* w2, const float* b2,
                          const float* cw, const float* cb, const float* tx, float* px, float* mean, float* rstd,
                          float* nx, float* g, float* ion, float* kv, float* m2, int64_t rows, int64_t d, int64_t M,
                          int64_t Dh, float eps, float inv_sqrt_d, const float* next_i, int64_t layer, int64_t L,
                          hipStream_t stream) {
-  ASRX_REQUIRE(M <= 64 && ldsh >= M + Dh, "asrx_msheath_row_fwd: M <= 64 and ldsh >= M + Dh required");
-  ASRX_REQUIRE(ms_aligned({x, lnw, lnb, gw, px}), "asrx_msheath_row_fwd: 8-byte aligned rows required");
-  ASRX_REQUIRE(!next_i || L > 0, "asrx_msheath_row_fwd: L > 0 required with next_i");
-  if (rows == 0) return 0;
-  MSRowFwd p{x, lnw, lnb, gw, gb, SH, mval, w2, b2, cw, cb, tx, px, mean, rstd, nx, g, ion, kv, m2, rows, ldsh,
-             (int)M, (int)Dh, eps, inv_sqrt_d, next_i, (int)layer, L > 0 ? L : 1};
-  MS_DISPATCH(msheath_row_fwd_kernel, row_grid(rows), 0, p);
-  ASRX_LAUNCHED("asrx_msheath_row_fwd");
+  return asrx_msheath_row_fwd2(x, lnw, lnb, gw, gb, SH, ldsh, mval, w2, b2, cw, cb, tx, px, 0, mean, rstd, nx, g, ion,
+                               kv, m2, rows, d, M, Dh, eps, inv_sqrt_d, next_i, layer, L, stream);
 }
 
 // Its backward (msheath_row_bwd_kernel).  dx is accumulated; every parameter gradient is accumulated
@@ -2017,10 +2104,18 @@ int asrx_msheath_row_bwd(const float* dpx, const float* x, const float* lnw, con
 }
 #undef MS_DISPATCH
 
-int asrx_tgate_fwd(const float* G, const float* c, float* out, int64_t rows, int64_t D, hipStream_t stream) {
+int asrx_tgate_fwd2(const float* G, const float* c, void* out, int out_bf16, int64_t rows, int64_t D,
+                    hipStream_t stream) {
   if (rows == 0) return 0;
-  LAUNCH_ROWS(tgate_fwd_kernel, rows, 0, G, c, out, rows, (int)D);
+  if (out_bf16)
+    LAUNCH_ROWS(tgate_fwd_kernel<unsigned short>, rows, 0, G, c, (unsigned short*)out, rows, (int)D);
+  else
+    LAUNCH_ROWS(tgate_fwd_kernel<float>, rows, 0, G, c, (float*)out, rows, (int)D);
   ASRX_LAUNCHED("asrx_tgate_fwd");
+}
+
+int asrx_tgate_fwd(const float* G, const float* c, float* out, int64_t rows, int64_t D, hipStream_t stream) {
+  return asrx_tgate_fwd2(G, c, out, 0, rows, D, stream);
 }
 
 int asrx_tgate_bwd(const float* dout, const float* G, const float* c, float* dGz, float* dc, int64_t rows, int64_t D,

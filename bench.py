@@ -280,24 +280,26 @@ def main():
         achieved = flops / sec / 1e12 if sec > 0 else 0.0
         step_s = elapsed / args.steps
         # dominant kernel: the wide bf16-weight GEMM (asrx_gemm_wn -> gemm_wr_kernel, every activation x weight product
-        # of the forward and of the input gradients; the top kernel of the rocprof summary).  With
-        # fp32 activations at K, N <= 1536 its arithmetic intensity (<= ~190 flop/B) is below the
-        # MI355X ridge point (2500 TF/s / 8 TB/s = 312 flop/B), so its roofline is HBM bandwidth:
-        # algorithmic bytes per launch = A (4 M K) + W (2 N K) + C (4 M N) [+ 4 M N if beta, + 4 M N if
-        # the pre-activation is saved].
+        # of the forward and of the input gradients; the top kernel of the rocprof summary).  At K, N <= 1536 its
+        # arithmetic intensity is below the MI355X ridge point (2500 TF/s / 8 TB/s = 312 flop/B), so its roofline
+        # is HBM bandwidth: algorithmic bytes per launch = A (M K x 4 B fp32 / 2 B bf16-stored) + W (2 N K) +
+        # C (M N x 4 / 2 B) [+ the same again if beta != 0] [+ 4 M N if the fp32 pre-activation is saved].
         wn_n, wn_bytes, wn_flops, wn_sec = 0, 0.0, 0.0, 0.0
         for tag, (cnt, fl, sc) in probe.by_tag(recs["gemm"]).items():
             if not tag or tag[0] != "wn":
                 continue
-            _, M, N, K, _nj, _conv, _act, has_z, has_beta = tag
-            per = 4 * M * K + 2 * N * K + 4 * M * N * (1 + int(has_z) + int(has_beta))
+            _, M, N, K, _nj, _conv, _act, has_z, has_beta, a_bf16, c_bf16, row_list = tag
+            if row_list:  # MSheath launches over a device-built subset of row tiles: bytes not known here
+                continue
+            ea, ec = (2 if a_bf16 else 4), (2 if c_bf16 else 4)
+            per = ea * M * K + 2 * N * K + ec * M * N * (1 + int(has_beta)) + 4 * M * N * int(has_z)
             wn_n += cnt
             wn_bytes += cnt * per
             wn_flops += fl
             wn_sec += sc
         if wn_sec > 0:
             gbs = wn_bytes / wn_sec / 1e9
-            result["roofline"] = {"kernel": "asrx::wn::gemm_wr_kernel (wide bf16-weight MFMA GEMM, fp32 activations)",
+            result["roofline"] = {"kernel": "asrx::wn::gemm_wr_kernel (wide bf16-weight MFMA GEMM, fp32 / bf16-stored activations)",
                                   "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                   "frac": round(gbs / HBM_PEAK_GBS, 4), **pmc_traffic("gemm_wr_kernel"),
                                   "algorithmic_bytes_per_launch": round(wn_bytes / wn_n),

@@ -99,6 +99,19 @@ int asrx_wgrad_bf16(const float* A, int64_t lda, const float* B, int64_t ldb, fl
 int asrx_gemm_wn_rows(const float* A, int64_t lda, const unsigned short* W, int64_t ldw, float* C, int64_t ldc,
                       const float* bias, float* Z, int64_t M, int64_t N, int64_t K, float alpha, float beta, int act,
                       int nj, const int* mtiles, const int* n_mtiles, asrx_stream_t stream);
+/* bf16 activation storage (perf mode; an activation whose only consumers are GEMM operands is stored
+ * bf16 by its producer -- the GEMMs round it to bf16 anyway, so the products are unchanged).
+ * asrx_gemm_wn_ex: asrx_gemm_wn with A stored fp32 (a_bf16 = 0) or bf16 (1: lda % 8, conv C % 8) and C
+ * stored fp32 (c_bf16 = 0) or bf16 (1: beta = 0; Z stays fp32), optionally on a device tile list
+ * (mtiles / n_mtiles as asrx_gemm_wn_rows, non-conv; NULL = every tile).  Replaces F.linear / 1x1 / k3
+ * conv1d at the call sites listed for asrx_gemm (model.py:96-147, 242-245, 341, 398-425, 529-574).
+ * asrx_wgrad_bf16_ex: asrx_wgrad_bf16 with X (B) stored fp32 (b_bf16 = 0) or bf16 (1: N, ldb % 8). */
+int asrx_gemm_wn_ex(const void* A, int a_bf16, int64_t lda, int conv, int64_t convF, int64_t convC,
+                    const unsigned short* W, int64_t ldw, void* C, int c_bf16, int64_t ldc, const float* bias,
+                    float* Z, int64_t M, int64_t N, int64_t K, float alpha, float beta, int act, int nj,
+                    const int* mtiles, const int* n_mtiles, asrx_stream_t stream);
+int asrx_wgrad_bf16_ex(const float* A, int64_t lda, const void* B, int b_bf16, int64_t ldb, float* C, int64_t ldc,
+                       int64_t M, int64_t N, int64_t R, int64_t splitk, asrx_stream_t stream);
 int64_t asrx_row_tiles_max(int64_t M);
 int asrx_row_tiles(const float* next_i, int64_t layer, int64_t L, int64_t M, int* mtiles, int* n_mtiles,
                    asrx_stream_t stream);
@@ -115,6 +128,15 @@ int asrx_abby_fwd(const float* x, const float* hpre, const float* W2, const floa
 int asrx_abby_fwd_logits(const float* x, const float* logits, const float* b2, float* out, float* ys, int* idx,
                          int64_t rows, int64_t d, int64_t L, int64_t H, int64_t sid_base, uint32_t key,
                          int use_noise, asrx_stream_t stream);
+/* asrx_abby_fwd / asrx_abby_fwd_logits with out stored fp32 (out_bf16 = 0) or bf16 (1: the AbbyNormal
+ * output feeds only a projection GEMM or attention -- attention.q[0] / kv[0] and the per-head norm,
+ * model.py:244-245, 248; the final norm before the tied logits, model.py:629). */
+int asrx_abby_fwd2(const float* x, const float* hpre, const float* W2, const float* b2, void* out, int out_bf16,
+                   float* ys, int* idx, int64_t rows, int64_t d, int64_t L, int64_t H, int64_t sid_base, uint32_t key,
+                   int use_noise, asrx_stream_t stream);
+int asrx_abby_fwd_logits2(const float* x, const float* logits, const float* b2, void* out, int out_bf16, float* ys,
+                          int* idx, int64_t rows, int64_t d, int64_t L, int64_t H, int64_t sid_base, uint32_t key,
+                          int use_noise, asrx_stream_t stream);
 int asrx_abby_bwd(const float* dout, const float* x, const float* hpre, const float* W2, const float* ys,
                   const int* idx, float* dx, float* dhpre, float* dW2, float* db2, int64_t rows, int64_t d,
                   asrx_stream_t stream);
@@ -131,6 +153,17 @@ int asrx_abby_bwd2(const float* dout, const float* x, const float* hpre, const f
 int asrx_attn_fwd(int prec, const float* q, const int64_t* sq, const float* k, const int64_t* sk, const float* v,
                   const int64_t* sv, float* o, const int64_t* so, float* lse, int64_t B, int64_t H, int64_t Lq,
                   int64_t Lk, int64_t hd, int causal, float scale, asrx_stream_t stream);
+/* asrx_attn_fwd / _bwd with storage types (prec 1 only when io != 0): io bit 0 = q / k / v stored bf16
+ * (what the per-head AbbyNormal and the v projection write when attention is their only consumer),
+ * bit 1 = o stored bf16 (it only feeds the out projection, model.py:316-317), bit 2 = dO stored bf16. */
+int asrx_attn_fwd2(int prec, int io, const void* q, const int64_t* sq, const void* k, const int64_t* sk,
+                   const void* v, const int64_t* sv, void* o, const int64_t* so, float* lse, int64_t B, int64_t H,
+                   int64_t Lq, int64_t Lk, int64_t hd, int causal, float scale, asrx_stream_t stream);
+int asrx_attn_bwd2(int prec, int io, const void* q, const int64_t* sq, const void* k, const int64_t* sk,
+                   const void* v, const int64_t* sv, const void* o, const int64_t* so, const void* dO,
+                   const int64_t* sd, const float* lse, float* delta_ws, float* dq, const int64_t* sdq, float* dk,
+                   const int64_t* sdk, float* dv, const int64_t* sdv, int64_t B, int64_t H, int64_t Lq, int64_t Lk,
+                   int64_t hd, int causal, float scale, asrx_stream_t stream);
 /* delta_ws: B*H*Lq floats of workspace. */
 int asrx_attn_bwd(int prec, const float* q, const int64_t* sq, const float* k, const int64_t* sk, const float* v,
                   const int64_t* sv, const float* o, const int64_t* so, const float* dO, const int64_t* sd,
@@ -154,6 +187,11 @@ int asrx_layernorm_bwd_acc(const float* dy, const float* x, const float* w, cons
 int asrx_layernorm_fwd2(const float* x, const float* w, const float* b, float* y, float* mean, float* rstd,
                         float* nrm, const float* gw, const float* gb, float* gout, int gate_on_x, int64_t rows,
                         int64_t d, float eps, asrx_stream_t stream);
+/* asrx_layernorm_fwd2 with y stored fp32 (y_bf16 = 0) or bf16 (1: MSheath's mlp_ln output only feeds
+ * mlp[0], model.py:503-506) */
+int asrx_layernorm_fwd3(const float* x, const float* w, const float* b, void* y, int y_bf16, float* mean, float* rstd,
+                        float* nrm, const float* gw, const float* gb, float* gout, int gate_on_x, int64_t rows,
+                        int64_t d, float eps, asrx_stream_t stream);
 
 /* ---- small-N linear (N <= 4): gate / mem_gate / mlp_gate Linear(D,1) (model.py:398, 406, 420),
  *      v_gate.mlp[2] (341), tgate.cs Linear(D,3) (530), MPNet's Linear(128,3) (381).
@@ -163,6 +201,13 @@ int asrx_small_linear_fwd(const float* x, const float* W, const float* b, float*
 int asrx_small_linear_bwd(const float* dy, const float* y, const float* x, const float* W, float* dx, float* dW,
                           float* db, int64_t rows, int64_t K, int64_t N, int act, float beta,
                           asrx_stream_t stream);
+/* the same with x stored fp32 (x_bf16 = 0) or bf16 (1: tgate.cs over a bf16-stored AbbyNormal output,
+ * model.py:530) */
+int asrx_small_linear_fwd2(const void* x, int x_bf16, const float* W, const float* b, float* y, int64_t rows,
+                           int64_t K, int64_t N, int act, asrx_stream_t stream);
+int asrx_small_linear_bwd2(const float* dy, const float* y, const void* x, int x_bf16, const float* W, float* dx,
+                           float* dW, float* db, int64_t rows, int64_t K, int64_t N, int act, float beta,
+                           asrx_stream_t stream);
 
 /* ---- row L2 norms: torch.norm in rotary (model.py:201), F.normalize in v_gate (347). ---------- */
 int asrx_rownorm(const float* x, float* n, int64_t rows, int64_t d, asrx_stream_t stream);
@@ -216,6 +261,14 @@ int asrx_msheath_row_fwd(const float* x, const float* lnw, const float* lnb, con
                          float* nx, float* g, float* ion, float* kv, float* m2, int64_t rows, int64_t d, int64_t M,
                          int64_t Dh, float eps, float inv_sqrt_d, const float* next_i, int64_t layer, int64_t L,
                          asrx_stream_t stream);
+/* px stored fp32 (px_bf16 = 0) or bf16 (1: on layers with an adapter px only feeds the adapter GEMM,
+ * model.py:455-457) */
+int asrx_msheath_row_fwd2(const float* x, const float* lnw, const float* lnb, const float* gw, const float* gb,
+                          const float* SH, int64_t ldsh, const float* mval, const float* w2, const float* b2,
+                          const float* cw, const float* cb, const float* tx, void* px, int px_bf16, float* mean,
+                          float* rstd, float* nx, float* g, float* ion, float* kv, float* m2, int64_t rows, int64_t d,
+                          int64_t M, int64_t Dh, float eps, float inv_sqrt_d, const float* next_i, int64_t layer,
+                          int64_t L, asrx_stream_t stream);
 int asrx_msheath_row_bwd(const float* dpx, const float* x, const float* lnw, const float* lnb, const float* mean,
                          const float* rstd, const float* dg, const float* g, const float* gw, const float* dion,
                          const float* SH, int64_t ldsh, const float* nx, const float* mval, const float* w2,
@@ -226,6 +279,9 @@ int asrx_msheath_row_bwd(const float* dpx, const float* x, const float* lnw, con
 
 /* ---- tgate (model.py:532-535): G = sigmoid(x Wcat^T + b) (rows,3D) from asrx_gemm, c (rows,3). */
 int asrx_tgate_fwd(const float* G, const float* c, float* out, int64_t rows, int64_t D, asrx_stream_t stream);
+/* tgate combine with out stored bf16 (out_bf16 = 1: it only feeds mlp's Linear(D, 3D), model.py:573) */
+int asrx_tgate_fwd2(const float* G, const float* c, void* out, int out_bf16, int64_t rows, int64_t D,
+                    asrx_stream_t stream);
 int asrx_tgate_bwd(const float* dout, const float* G, const float* c, float* dGz, float* dc, int64_t rows,
                    int64_t D, asrx_stream_t stream);
 

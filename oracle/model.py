@@ -67,6 +67,52 @@ class Noise:
         return torch.from_numpy(keep).to(self.dtype)
 
 
+class Decisions:
+    """Record / replay of the forward's hard decisions (keys as asrx/decisions.py):
+      ("abby", key, sid) -> int64 (L, H) AbbyNormal mode index (gumbel argmax, essentials.py:170)
+      ("ion", key, sid, layer) -> (L,) v_gate STthreshold output (model.py:330-334, 351)
+      ("action", key, sid, layer) -> (action, forced) MSheath jump (model.py:476-482)
+    record: every decision taken is stored in `rec`.  replay: a decision found in `table` is used
+    instead of the one this forward would take (the continuous values -- soft gumbel probabilities,
+    STE paths -- are still this forward's own), so the oracle follows the HIP path's discrete
+    trajectory and its gradients can be compared without decision flips."""
+
+    def __init__(self, table=None):
+        self.rec: dict = {}
+        self.table = table
+        self.replayed = 0
+        self.overridden = 0
+
+
+_DEC: Decisions | None = None
+
+
+def use_decisions(dec: Decisions | None):
+    """Install (or remove, None) the decision recorder / replayer for the following forwards."""
+    global _DEC
+    _DEC = dec
+
+
+def _decide_abby(index, dkey, heads: bool):
+    """index: (B, L, 1) or (B, H, L, 1) argmax; dkey = (site key, sids)."""
+    if _DEC is None or dkey is None:
+        return index
+    key, sids = dkey
+    out = index.clone()
+    for s, sid in enumerate(sids):
+        got = index[s, ..., 0].t() if heads else index[s]  # (L, H)
+        _DEC.rec[("abby", int(key), int(sid))] = got.clone()
+        if _DEC.table is not None and ("abby", int(key), int(sid)) in _DEC.table:
+            want = _DEC.table[("abby", int(key), int(sid))].to(index.dtype)
+            _DEC.overridden += int((want != got).sum())
+            _DEC.replayed += 1
+            if heads:
+                out[s, ..., 0] = want.t()
+            else:
+                out[s] = want
+    return out
+
+
 def _lin(P, name, x):
     b = P.get(name + ".bias")
     return F.linear(x, P[name + ".weight"], b)
@@ -75,9 +121,9 @@ def _lin(P, name, x):
 # ------------------------------------------------------------------------------- norms
 
 
-def abby_normal(P, pre, x, g):
+def abby_normal(P, pre, x, g, dkey=None):
     """essentials.py:155-191 (AbbyNormal.forward, confidence=None).  g: gumbel noise, shape of
-    the router logits."""
+    the router logits.  dkey: (site key, sids) of the call for the decision recorder."""
     d = x.size(-1)
     size = max(3, int(d * 0.05))
     if size % 2 == 0:
@@ -90,7 +136,7 @@ def abby_normal(P, pre, x, g):
     cv = std_val / (mean_val + 1e-6)
     # F.gumbel_softmax(logits + cv, tau=1, hard=True) with gumbels = g
     y_soft = torch.softmax(logits + cv + g, dim=-1)
-    index = y_soft.argmax(dim=-1, keepdim=True)
+    index = _decide_abby(y_soft.argmax(dim=-1, keepdim=True), dkey, x.dim() == 4)
     y_hard = torch.zeros_like(y_soft).scatter_(-1, index, 1.0)
     dec = y_hard - y_soft.detach() + y_soft
     rows = div.reshape(-1, 1, d)  # pooling runs along the feature axis (essentials.py:171-172)
@@ -107,7 +153,7 @@ def abby_normal(P, pre, x, g):
 def abby_rows(P, pre, x, noise, site, sids):
     """AbbyNormal on (B, L, D) with noise rows (sid, l)."""
     g = noise.abby(site, sids, 1, x.shape[1])[:, 0]
-    return abby_normal(P, pre, x, g)
+    return abby_normal(P, pre, x, g, (noise.key(site), sids))
 
 
 def channel_layer_norm(P, pre, x):
@@ -230,8 +276,8 @@ def attention(P, pre, x, xa, masked, cfg, noise, site_q, sids_q, site_kv, sids_k
     k = rotary(k, src, D, H, masked)
     gq = noise.abby(site_q + ".qh", sids_q, H, Lq)
     gk = noise.abby(site_kv + ".kh", sids_kv, H, Lk)
-    q = abby_normal(P, pre + ".ln", q, gq)
-    k = abby_normal(P, pre + ".ln", k, gk)
+    q = abby_normal(P, pre + ".ln", q, gq, (noise.key(site_q + ".qh"), sids_q))
+    k = abby_normal(P, pre + ".ln", k, gk, (noise.key(site_kv + ".kh"), sids_kv))
     s = (q @ k.transpose(-1, -2)) / math.sqrt(hd)
     if masked:
         s = s.masked_fill(torch.ones(Lq, Lk, dtype=torch.bool).triu(1), float("-inf"))
@@ -243,14 +289,16 @@ def attention(P, pre, x, xa, masked, cfg, noise, site_q, sids_q, site_kv, sids_k
 # ------------------------------------------------------------------------------- gates
 
 
-def v_gate(P, pre, x):
-    """model.py:346-351 -> (ion, x_val)."""
+def v_gate(P, pre, x, hard_override=None):
+    """model.py:346-351 -> (ion, x_val).  hard_override: the thresholded value to use (replay)."""
     D = x.shape[-1]
     key = torch.softmax(F.normalize(x, p=2, dim=-1) @ F.normalize(P[pre + ".mkey"], p=2, dim=-1).t()
                         / math.sqrt(D), dim=-1)
     m = _lin(P, pre + ".mlp.2", F.silu(_lin(P, pre + ".mlp.0", x)))
     x_val = _lin(P, pre + ".concat", torch.cat((key @ P[pre + ".mval"], m), dim=-1))
     hard = (x_val > P[pre + ".tx"]).to(x.dtype)
+    if hard_override is not None:
+        hard = hard_override.to(x.dtype).reshape(hard.shape)
     ion = hard + (x_val - x_val.detach())  # STthreshold: binary forward, identity backward
     return ion, x_val
 
@@ -259,8 +307,9 @@ def _ln(P, pre, x):
     return F.layer_norm(x, (x.shape[-1],), P[pre + ".weight"], P[pre + ".bias"], 1e-5)
 
 
-def msheath(P, pre, x, layer, g_pol):
-    """MSheath.forward (model.py:429-507) at batch 1, run per sample.  g_pol: (B, layer, 3)."""
+def msheath(P, pre, x, layer, g_pol, dkey=None):
+    """MSheath.forward (model.py:429-507) at batch 1, run per sample.  g_pol: (B, layer, 3).
+    dkey: (site key, sids) of the call for the decision recorder."""
     outs = []
     D = x.shape[-1]
     for s in range(x.shape[0]):
@@ -273,7 +322,17 @@ def msheath(P, pre, x, layer, g_pol):
         i = 0
         while i < layer:
             lp = f"{pre}.layers.{i}"
-            ion, _ = v_gate(P, lp + ".v_gate", xs)
+            dk = None if (_DEC is None or dkey is None) else (int(dkey[0]), int(dkey[1][s]), i)
+            rep = None
+            if dk is not None and _DEC.table is not None and ("ion",) + dk in _DEC.table:
+                rep = _DEC.table[("ion",) + dk]
+            ion, x_val = v_gate(P, lp + ".v_gate", xs, rep)
+            if dk is not None:
+                own = (x_val > P[lp + ".v_gate.tx"]).to(x_val.dtype).reshape(-1)
+                _DEC.rec[("ion",) + dk] = own.detach().clone()
+                if rep is not None:
+                    _DEC.replayed += 1
+                    _DEC.overridden += int((rep.reshape(-1).to(own.dtype) != own).sum())
             mlayer = ion.expand(-1, ctx, D)
             px = _ln(P, lp + ".ln", xs)
             out = _lin(P, lp + ".adapter", px) if i % 2 == 0 else px
@@ -284,16 +343,26 @@ def msheath(P, pre, x, layer, g_pol):
             mem_w = mem_v * mem_w + (1 - mem_v) * mem
             potential = ion.mean()
             jump_g = 1.0
-            if potential < 0.1 and i < layer - 1:
+            forced = bool(potential < 0.1 and i < layer - 1)
+            want = None
+            if dk is not None and _DEC.table is not None and ("action",) + dk in _DEC.table:
+                want = _DEC.table[("action",) + dk]
+            if want is not None:
+                forced = want[1]
+            if forced and i < layer - 1:
                 action = 1
             elif i < layer - 1:
                 ys = torch.softmax(policy + g_pol[s:s + 1, i], dim=-1)  # gumbel_softmax(policy, hard)
                 idx = ys.argmax(dim=-1, keepdim=True)
+                if want is not None:
+                    idx = torch.full_like(idx, int(want[0]))
                 jump = torch.zeros_like(ys).scatter_(-1, idx, 1.0) - ys.detach() + ys
                 action = int(jump.argmax(dim=-1).item())
                 jump_g = jump[0, action]
             else:
                 action = 0
+            if dk is not None:
+                _DEC.rec[("action",) + dk] = (action, forced and i < layer - 1)
             if action > 0:
                 i_next = min(i + action + 1, layer)
                 jump_w = P[pre + ".jump_s"][min(action - 1, 2)]
@@ -334,14 +403,15 @@ def residual(P, i, x, cfg, noise, site, sids, xa=None, xa_site=None, xa_sids=Non
     pre = f"processor.block.{i}"
     L = cfg["layer"]
     x = abby_rows(P, pre + ".ln", x, noise, site + ".ln0", sids)
-    x = msheath(P, pre + ".jump", x, L, noise.policy(site + ".jump", sids, L))
+    x = msheath(P, pre + ".jump", x, L, noise.policy(site + ".jump", sids, L), (noise.key(site + ".jump"), sids))
     h = abby_rows(P, pre + ".ln", x, noise, site + ".ln1", sids)
     x = router(P, pre + ".router", x) + attention(P, pre + ".attn", h, None, masked, cfg, noise,
                                                    site + ".sa", sids, site + ".sa", sids)
     if xa is not None:
         xa = xa + sinusoids(xa.shape[1], xa.shape[-1], xa.dtype)
         xa = abby_rows(P, pre + ".ln", xa, noise, xa_site + ".ln", xa_sids)
-        xa = msheath(P, pre + ".jump", xa, L, noise.policy(xa_site + ".jump", xa_sids, L))
+        xa = msheath(P, pre + ".jump", xa, L, noise.policy(xa_site + ".jump", xa_sids, L),
+                     (noise.key(xa_site + ".jump"), xa_sids))
         h = abby_rows(P, pre + ".ln", x, noise, site + ".ln2", sids)
         x = x + attention(P, pre + ".attn", h, router(P, pre + ".router", xa), False, cfg, noise,
                           site + ".ca", sids, xa_site + ".ca", xa_sids)

@@ -8,6 +8,11 @@ tools/parity_probe.py.  The metrics follow SURVEY.md §8(d) "Parity gates":
   argmax      fraction of text positions whose argmax token id agrees
   loss        |loss_HIP - loss_oracle| / |loss_oracle|
   grads       max |g_HIP - g_oracle| / max |g_oracle| for selected parameters
+  decisions   agreement rates of the hard decisions (AbbyNormal modes, v_gate thresholds, MSheath
+              actions) between the HIP path and the oracle on the same inputs (asrx/decisions.py)
+  replay      the oracle re-run CONSUMING the HIP path's decisions (oracle.model.Decisions): with the
+              discrete trajectory shared, every parameter gradient is compared (grads_all_max) --
+              differences left are rounding, not decision flips
 """
 from __future__ import annotations
 
@@ -28,16 +33,20 @@ GRAD_PARAMS = ["processor.token.weight", "processor.position", "processor.ln.mod
                "enc.encoder.{L1}.1.parametrizations.weight.original1"]
 
 
-def inputs(B: int, seconds: float, T: int, vocab: int, seed: int = 0):
+def inputs(B: int, seconds: float, T: int, vocab: int, seed: int = 0, pitch_frames=None):
     """Synthetic clips (asrx.synth) -> the reference's feature dict through the float64
-    oracle front end: spectrogram (B, 128, S), pitch (B, 1, S), waveform (B, 1, S - 1), text."""
+    oracle front end: spectrogram (B, 128, S), pitch (B, 1, S or pitch_frames), waveform (B, 1, S - 1),
+    text.  pitch_frames = 2 S - 1 is the reference's own pitch stream (pw.dio(x, sr, frame_period) binds
+    frame_period to f0_floor and keeps dio's 5 ms default frames, essentials.py:451-455: 6001 frames for
+    a 30 s clip)."""
     from asrx import synth
 
     wav = synth.waveform(B, seconds, first_seed=1000 + seed)
     spec = torch.stack([torch.from_numpy(omel.log_mel(w.numpy().astype(np.float64))).float() for w in wav])
     wf = torch.stack([torch.from_numpy(omel.waveform_feature(w.numpy())).float() for w in wav])  # (B, 1, S-1)
     S = spec.shape[-1]
-    pitch = synth.pitch(B, frames=S, first_seed=1000 + seed, mask_seed=2000 + seed)
+    pitch = synth.pitch(B, frames=S if pitch_frames is None else pitch_frames, first_seed=1000 + seed,
+                        mask_seed=2000 + seed)
     ids, labels = synth.text(B, T, vocab, seed=7 + seed)
     return {"spectrogram": spec, "pitch": pitch, "waveform": wf, "text_ids": ids, "labels": labels}
 
@@ -49,9 +58,47 @@ def _rel_max(a, b):
     return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
 
 
+def agreement(hip: dict, ref: dict) -> dict:
+    """Agreement of two decision tables on their common keys: per kind, the fraction of equal entries
+    (AbbyNormal modes and v_gate thresholds per position, MSheath actions per (sample, layer))."""
+    out = {}
+    for kind in ("abby", "ion", "action"):
+        keys = [k for k in hip if k[0] == kind and k in ref]
+        eq = tot = 0
+        for k in keys:
+            a, b = hip[k], ref[k]
+            if kind == "action":
+                eq += int(a[0] == b[0])
+                tot += 1
+            else:
+                a, b = a.reshape(-1).double(), b.reshape(-1).double()
+                eq += int((a == b).sum())
+                tot += a.numel()
+        out[kind] = (eq / tot) if tot else None
+        out[kind + "_n"] = tot
+    return out
+
+
+def _hip_mel_inputs(x, B, seconds, seed, device):
+    """The benchmarked front end: the HIP log-mel and waveform pool of the same synthetic clips (the
+    oracle keeps its own float64 mel)."""
+    from asrx import synth
+    from asrx.mel import logmel
+
+    wav = synth.waveform(B, seconds, first_seed=1000 + seed).to(device)
+    spec, wf = logmel(wav, layout="BMF", pool=True)
+    y = dict(x)
+    y["hip_spectrogram"], y["hip_waveform"] = spec, wf.unsqueeze(1)
+    return y
+
+
 def compare(cfg, B=1, seconds=30.0, T=256, precision="bf16", train=True, grads=True, seed=0, noise=(7, 3),
-            model_seed=0, device="cuda"):
-    """Run the HIP Model and the oracle on the same inputs; return a dict of metrics."""
+            model_seed=0, device="cuda", decisions=False, replay=False, hip_mel=False, pitch_frames=None):
+    """Run the HIP Model and the oracle on the same inputs; return a dict of metrics.
+    decisions: record both sides' hard decisions and report their agreement.  replay: re-run the oracle
+    consuming the HIP decisions and compare every parameter gradient.  hip_mel: feed the HIP model the
+    HIP log-mel of the clips (the benchmarked chain), the oracle its float64 mel."""
+    from asrx import decisions as hdec
     from asrx import prec
     from asrx.model import Model
 
@@ -59,28 +106,66 @@ def compare(cfg, B=1, seconds=30.0, T=256, precision="bf16", train=True, grads=T
     model = Model(cfg).to(device)
     model.train(train)
     sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
-    x = inputs(B, seconds, T, cfg.tokens, seed)
+    x = inputs(B, seconds, T, cfg.tokens, seed, pitch_frames)
+    if hip_mel:
+        x = _hip_mel_inputs(x, B, seconds, seed, device)
     model.set_noise(*noise)
+    if decisions or replay:
+        hdec.enable()
     t0 = time.perf_counter()
-    with prec.precision(precision):
-        out = model(labels=x["labels"].to(device), text_ids=x["text_ids"].to(device),
-                    spectrogram=x["spectrogram"].to(device), pitch=x["pitch"].to(device),
-                    waveform=x["waveform"].to(device))
-        if grads:
-            out["loss"].backward()
-    torch.cuda.synchronize()
+    try:
+        with prec.precision(precision):
+            out = model(labels=x["labels"].to(device), text_ids=x["text_ids"].to(device),
+                        spectrogram=(x["hip_spectrogram"] if hip_mel else x["spectrogram"]).to(device),
+                        pitch=x["pitch"].to(device),
+                        waveform=(x["hip_waveform"] if hip_mel else x["waveform"]).to(device))
+            if grads:
+                out["loss"].backward()
+        torch.cuda.synchronize()
+    finally:
+        hip_dec = hdec.disable() if (decisions or replay) else None
     t_gpu = time.perf_counter() - t0
-    ck = (repr(cfg), B, seconds, T, train, seed, noise, model_seed)
-    t0 = time.perf_counter()
-    if ck not in _ORACLE_CACHE:  # the oracle depends on the case only, not on the HIP precision
+    ocfg = {"dims": cfg.dims, "head": cfg.head, "layer": cfg.layer}
+
+    def run_oracle(dec):
         P = {k: (v.double().requires_grad_(True) if v.is_floating_point() else v) for k, v in sd.items()}
-        ref = om.forward(P, {"dims": cfg.dims, "head": cfg.head, "layer": cfg.layer}, x["text_ids"], x["labels"],
-                         spectrogram=x["spectrogram"], pitch=x["pitch"], waveform=x["waveform"], seed=noise[0],
-                         step=noise[1], training=train, live_only=True)
-        ref["loss"].backward()
-        _ORACLE_CACHE[ck] = (P, {"logits": ref["logits"].detach(), "loss": float(ref["loss"])})
-    P, ref = _ORACLE_CACHE[ck]
+        om.use_decisions(dec)
+        try:
+            r = om.forward(P, ocfg, x["text_ids"], x["labels"], spectrogram=x["spectrogram"], pitch=x["pitch"],
+                           waveform=x["waveform"], seed=noise[0], step=noise[1], training=train, live_only=True)
+            r["loss"].backward()
+        finally:
+            om.use_decisions(None)
+        return P, {"logits": r["logits"].detach(), "loss": float(r["loss"])}
+
+    ck = (repr(cfg), B, seconds, T, train, seed, noise, model_seed, pitch_frames)
+    t0 = time.perf_counter()
+    ref_dec = None
+    if decisions:
+        rec = om.Decisions()
+        P, ref = run_oracle(rec)
+        ref_dec = rec.rec
+    elif replay:
+        P = ref = None
+    else:
+        if ck not in _ORACLE_CACHE:  # the oracle depends on the case only, not on the HIP precision
+            _ORACLE_CACHE[ck] = run_oracle(None)
+        P, ref = _ORACLE_CACHE[ck]
     t_ref = time.perf_counter() - t0
+    res_extra = {}
+    if decisions:
+        res_extra["decisions"] = agreement(hip_dec, ref_dec)
+    if replay:
+        rp = om.Decisions(table=hip_dec)
+        P_r, ref_r = run_oracle(rp)
+        res_extra["replayed"] = rp.replayed
+        res_extra["overridden"] = rp.overridden
+        if P is None:
+            P, ref = P_r, ref_r
+        else:
+            res_extra["replay_logits_max"] = _rel_max(out["logits"].detach().double().cpu(), ref_r["logits"])
+            res_extra["replay_loss"] = abs(float(out["loss"]) - ref_r["loss"]) / abs(ref_r["loss"])
+            P, ref = P_r, ref_r
     lg = out["logits"].detach().double().cpu()
     lr = ref["logits"].detach()
     res = {"dims": cfg.dims, "head": cfg.head, "layer": cfg.layer, "tokens": cfg.tokens, "B": B, "S": x["pitch"].shape[-1],
@@ -90,7 +175,25 @@ def compare(cfg, B=1, seconds=30.0, T=256, precision="bf16", train=True, grads=T
            "argmax": float((lg.argmax(-1) == lr.argmax(-1)).double().mean()),
            "loss": abs(float(out["loss"]) - ref["loss"]) / abs(ref["loss"]),
            "loss_hip": float(out["loss"]), "loss_ref": ref["loss"],
-           "t_gpu_s": round(t_gpu, 2), "t_oracle_s": round(t_ref, 2)}
+           "t_gpu_s": round(t_gpu, 2), "t_oracle_s": round(t_ref, 2), **res_extra}
+    if grads and replay:  # every parameter that receives a gradient on both sides
+        names = dict(model.named_parameters())
+        worst, wname = 0.0, None
+        missing = []
+        for n, p in names.items():
+            pg, rg = p.grad, P[n].grad if n in P else None
+            if (pg is None) != (rg is None or float(rg.abs().max()) == 0.0):
+                if pg is None or float(pg.abs().max()) != 0.0:
+                    missing.append(n)
+                continue
+            if pg is None:
+                continue
+            e = _rel_max(pg.double().cpu(), rg)
+            if e > worst:
+                worst, wname = e, n
+        res["grads_all_max"] = worst
+        res["grads_all_worst"] = wname
+        res["grads_missing"] = missing
     if grads:
         names = dict(model.named_parameters())
         ge = {}
