@@ -146,8 +146,10 @@ SIGNATURES = {
     "asrx_gemm_wn_ex": (_i32, [_p, _i32, _i64, _i32, _i64, _i64, _p, _i64, _p, _i32, _i64, _p, _p, _i64, _i64, _i64,
                                _f32, _f32, _i32, _i32, _p, _p, _p]),
     "asrx_wgrad_bf16_ex": (_i32, [_p, _i64, _p, _i32, _i64, _p, _i64, _i64, _i64, _i64, _i64, _p]),
-    "asrx_abby_fwd2": (_i32, [_p, _p, _p, _p, _p, _i32, _p, _p, _i64, _i64, _i64, _i64, _i64, _u32, _i32, _p]),
-    "asrx_abby_fwd_logits2": (_i32, [_p, _p, _p, _p, _i32, _p, _p, _i64, _i64, _i64, _i64, _i64, _u32, _i32, _p]),
+    "asrx_abby_fwd2": (_i32, [_p, _p, _p, _p, _p, _i32, _p, _p, _i64, _i64, _i64, _i64, _i64, _u32, _i32, _p, _p, _p,
+                              _p]),
+    "asrx_abby_fwd_logits2": (_i32, [_p, _p, _p, _p, _i32, _p, _p, _i64, _i64, _i64, _i64, _i64, _u32, _i32, _p, _p,
+                                     _p, _p]),
     "asrx_attn_fwd2": (_i32, [_i32, _i32, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i32, _f32,
                               _p]),
     "asrx_attn_bwd2": (_i32, [_i32, _i32, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p,
@@ -158,6 +160,7 @@ SIGNATURES = {
     "asrx_msheath_row_fwd2": (_i32, [_p] * 6 + [_i64] + [_p] * 7 + [_i32] + [_p] * 7 + [_i64] * 4
                                     + [_f32, _f32, _p, _i64, _i64, _p]),
     "asrx_layernorm_fwd3": (_i32, [_p, _p, _p, _p, _i32] + [_p] * 6 + [_i32, _i64, _i64, _f32, _p]),
+    "asrx_jump_axpy_inplace": (_i32, [_p] * 10 + [_i64, _i64, _i64, _p]),
     "asrx_maxfactor_param_bytes": (_i32, []),
     "asrx_maxfactor_step": (_i32, [_p, _i32, _i64, _i64, _i64, _i64, _i64, _p, _p]),
 }

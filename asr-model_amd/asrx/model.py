@@ -77,9 +77,11 @@ class AbbyNormal(nn.Module):
         self.size, self.alpha, self.beta, self.k, self.tx = size, alpha, beta, k, threshold
         self.mode_router = nn.Sequential(nn.Linear(dims, dims), nn.SiLU(), nn.Linear(dims, 3))
 
-    def run(self, x, noise: NoiseCtx, site: str, sid_base: int, L: int, H: int = 1, out_bf16: bool = False):
-        """out_bf16: the output only feeds GEMM / attention operands (stored bf16 in perf mode)."""
-        return ops.abby_normal(self, x, L, H, sid_base, noise.key(site), True, out_bf16)
+    def run(self, x, noise: NoiseCtx, site: str, sid_base: int, L: int, H: int = 1, out_bf16: bool = False,
+            tgate=None):
+        """out_bf16: the output only feeds GEMM / attention operands (stored bf16 in perf mode); tgate: the
+        consuming tgate (its cs Linear(d, 3) is evaluated inside the norm's kernel)."""
+        return ops.abby_normal(self, x, L, H, sid_base, noise.key(site), True, out_bf16, tgate)
 
 
 class LayerNorm(nn.Module):
@@ -260,7 +262,10 @@ class attention(nn.Module):  # noqa: N801
         k, v = ops.kv_proj(kvn, self.kv[1].weight, self.kv[1].bias)
         k = ops.rotary(k, src, rotary_freqs(D, H, masked, src.device), hd, self.scale)
         k = self.ln.run(k.view(B, L, H, hd), noise, site + ".kh", sid_base, L, H, out_bf16=prec.attn_bf16_io())
-        return k, v.view(B, L, H, hd)
+        vh = v.view(B, L, H, hd)
+        if ops.sink_of(v) is not None:  # v is bf16-stored: attention adds its gradient into v's sink
+            vh._asrx_sink = ops.sink_of(v)
+        return k, vh
 
     def project_q(self, x, noise, site, sid_base, masked):
         B, L, D = x.shape
@@ -278,8 +283,8 @@ class attention(nn.Module):  # noqa: N801
         if kv is None:
             kv = self.project_kv(x, noise, site, sid_base, masked)
         q = self.project_q(x, noise, site, sid_base, masked)
-        o = ops.attention(q, kv[0], kv[1], masked, out_bf16=True)
-        return ops.linear(o.view(B, L, D), self.out[1].weight, self.out[1].bias)
+        o = ops.attention(q, kv[0], kv[1], masked, out_bf16=True, merge_heads=True)
+        return ops.linear(o, self.out[1].weight, self.out[1].bias)  # o: (B, L, D), heads merged
 
 
 # ------------------------------------------------------------------------------- MSheath
@@ -430,7 +435,7 @@ class residual(nn.Module):  # noqa: N801  (model.py:559-583)
         if kv is not None:
             h = self.ln.run(x, noise, site + ".ln2", sid_base, L)
             x = ops.fork(ops.add(x, self.attn.run(h, kv, noise, site + ".ca", sid_base, False)))
-        m = self.ln.run(x, noise, site + ".mlp.ln0", sid_base, L, out_bf16=True)  # feeds only tgate's GEMMs
+        m = self.ln.run(x, noise, site + ".mlp.ln0", sid_base, L, out_bf16=True, tgate=self.mlp[1])
         m = ops.tgate(self.mlp[1], m, out_bf16=True)
         m = ops.linear(m, self.mlp[2].weight, self.mlp[2].bias, act="gelu", out_bf16=True)
         m = ops.linear(m, self.mlp[4].weight, self.mlp[4].bias)

@@ -120,8 +120,9 @@ def forward(mod, x0, gpol, save, tag=None):
                  _P(vg.tx), _P(px), pxb, _P(mean), _P(rstd), _P(nx), _P(gv), _P(ion), _P(kv), _P(m2), rows, D, M, Dh,
                  float(ln.eps), inv_sqrt_d, _P(next_i), i, L, st)
         out = G.linear_fwd(px, ad.weight, ad.bias, mtiles=mt) if ad is not None else px
-        # x_new = x + g * ion * out; mem = mean_l x_new   (461-463)
-        x_new = _E(B, L, D, device=dev)
+        # x_new = x + g * ion * out; mem = mean_l x_new   (461-463).  Without a backward x_new is not
+        # materialised: the column sums are taken here and the jump step below recomputes it
+        x_new = _E(B, L, D, device=dev) if save else None
         lib.call("asrx_axpy_row2_colsum", _P(x), _P(gv), _P(ion), _P(out), _P(x_new), _P(part[i]), B, L, D,
                  _P(next_i), i, st)
         # mem_v = sigmoid(mem_gate(mem)); control; jump select   (464-501)
@@ -134,9 +135,14 @@ def forward(mod, x0, gpol, save, tag=None):
                  _P(alpha), _P(beta), _P(gam), _P(mwo), _P(active), _P(next_out), _P(rec), st)
         if tag is not None and decisions.active():
             decisions.msheath_layer(tag[0], tag[1], i, ion.view(B, L), rec.view(torch.float32).view(B, -1))
-        x_out = _E(B, L, D, device=dev)
-        lib.call("asrx_jump_select4", _P(x_new), _P(x0), _P(x), _P(active), _P(alpha), _P(beta), _P(gam),
-                 _P(x_out), B, L, D, st)
+        if save:
+            x_out = _E(B, L, D, device=dev)
+            lib.call("asrx_jump_select4", _P(x_new), _P(x0), _P(x), _P(active), _P(alpha), _P(beta), _P(gam),
+                     _P(x_out), B, L, D, st)
+        else:  # one pass, in place from layer 1 on (samples not at the layer keep their rows untouched)
+            x_out = _E(B, L, D, device=dev) if i == 0 else x
+            lib.call("asrx_jump_axpy_inplace", _P(x), _P(x_out), _P(gv), _P(ion), _P(out), _P(x0), _P(active),
+                     _P(alpha), _P(beta), _P(gam), B, L, D, st)
         if save:
             layers.append(dict(x=x, Wc=Wc, mkn=mkn, SH=SH, nx=nx, kv=kv, m2=m2, px=px, mean=mean, rstd=rstd,
                                out=out, g=gv, ion=ion, x_new=x_new, mem=mem, mem_v=mem_v, mem_w=mem_w, ld_mw=ld_mw,
@@ -152,7 +158,8 @@ def forward(mod, x0, gpol, save, tag=None):
              _P(rstd2), None, _P(mod.mlp_gate[0].weight), _P(mod.mlp_gate[0].bias), _P(gate), 1, rows, D,
              float(mod.mlp_ln.eps), st)
     z1 = _E(B, L, mod.mlp[0].weight.shape[0], device=dev) if save else None
-    a1 = G.linear_fwd(hln, mod.mlp[0].weight, mod.mlp[0].bias, act="silu", preact=z1, out_bf16=prec.bf16_storage())
+    a1 = G.linear_fwd(hln, mod.mlp[0].weight, mod.mlp[0].bias, act="silu", preact=z1,
+                      out_bf16=prec.bf16_storage())
     hh = G.linear_fwd(a1, mod.mlp[2].weight, mod.mlp[2].bias)
     y = _E(B, L, D, device=dev)
     lib.call("asrx_axpy_row", _P(x), _P(gate), _P(hh), _P(y), rows, D, st)

@@ -100,6 +100,22 @@ class GradSink:
         return self.buf, 1
 
 
+class PartSink:
+    """The sink of one part (rows [i B, (i+1) B)) of a stream group whose own sink is `parent` (a split
+    bf16-stored group, e.g. the cross-attention k / v of equal-length audio streams): contributions land in
+    the slice of the parent's buffer, which is allocated zero-filled so every contributor adds."""
+    __slots__ = ("parent", "i", "n", "shape")
+
+    def __init__(self, parent, i, n, shape):
+        self.parent, self.i, self.n, self.shape = parent, i, n, shape
+
+    def target(self, like):
+        if self.parent.buf is None:
+            self.parent.buf = torch.zeros(self.shape, device=like.device)
+        B = self.shape[0] // self.n
+        return self.parent.buf[self.i * B:(self.i + 1) * B].view(like.shape), 1
+
+
 class ForkFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, sink):
@@ -110,13 +126,7 @@ class ForkFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         sink, ctx.sink = ctx.sink, None
-        buf, sink.buf = sink.buf, None
-        if buf is None:
-            return g, None
-        if g is not None:
-            g = _c(g)
-            lib.call("asrx_lincomb", _P(buf), _P(g), None, 1.0, 1.0, 0.0, _P(buf), buf.numel(), _S())
-        return buf, None
+        return grad_in(g, sink), None
 
 
 def fork(x):
@@ -131,6 +141,50 @@ def fork(x):
 
 def sink_of(x):
     return getattr(x, "_asrx_sink", None)
+
+
+# =============================================================================== bf16-stored outputs
+# A Function whose output is stored bf16 (asrx.prec.bf16_storage) must not receive its gradient through
+# autograd: the engine casts every gradient to the dtype of the tensor it belongs to, so it would arrive
+# rounded to bf16 (and the kernels take fp32 gradients).  Such an output carries a GradSink instead:
+# its consumers (Linear, KVProj, TGate, attention) accumulate their exact fp32 input gradient into the
+# sink and return None, and the producer's backward reads the sink (plus, converted, whatever autograd
+# delivered from a consumer without sink support).
+
+
+def out_sink(y, sink):
+    """Attach `sink` to the producer's output y (a bf16-stored activation) and return y."""
+    if sink is not None and y.requires_grad:
+        y._asrx_sink = sink
+    return y
+
+
+def new_sink(out_bf16: bool):
+    """A sink for a producer about to store its output bf16 (None when no backward will run)."""
+    return GradSink() if (out_bf16 and torch.is_grad_enabled() and prec.bf16_storage()) else None
+
+
+def grad_in(g, sink):
+    """The full fp32 gradient of an output: the sink's buffer (sink-capable consumers) plus the
+    autograd-delivered part (None, fp32 or bf16)."""
+    buf = None
+    if sink is not None:
+        buf, sink.buf = sink.buf, None
+    if g is not None:
+        g = g.float() if g.dtype != torch.float32 else g
+        g = _c(g)
+    if buf is None:
+        return g
+    if g is not None:
+        lib.call("asrx_lincomb", _P(buf), _P(g), None, 1.0, 1.0, 0.0, _P(buf), buf.numel(), _S())
+    return buf
+
+
+def _f32(g):
+    """An incoming gradient as fp32 (autograd delivers bf16 for a bf16 tensor's gradient)."""
+    if g is None:
+        return None
+    return _c(g.float() if g.dtype != torch.float32 else g)
 
 
 class SplitRows(torch.autograd.Function):
@@ -149,6 +203,7 @@ class SplitRows(torch.autograd.Function):
     @staticmethod
     def backward(ctx, *gs):
         n = ctx.n
+        gs = [_f32(g) for g in gs]  # views of a bf16-stored group get bf16 gradients from autograd
         if all(g is None for g in gs):
             return None, None
         out = _E(ctx.shape, device=next(g for g in gs if g is not None).device)
@@ -172,8 +227,11 @@ def split_rows(x, n):
         return [x]
     parts = SplitRows.apply(x, n) if (torch.is_grad_enabled() and x.requires_grad) else \
         tuple(x[i * (x.shape[0] // n):(i + 1) * (x.shape[0] // n)] for i in range(n))
+    sk = sink_of(x)
     for i, t in enumerate(parts):
         t._asrx_group = (x, i, n)
+        if sk is not None and t.requires_grad:  # consumers of a part add into its slice of x's sink
+            t._asrx_sink = PartSink(sk, i, n, tuple(x.shape))
     return list(parts)
 
 
@@ -196,9 +254,11 @@ class Linear(torch.autograd.Function):
     """y = act(x W^T + b) on MFMA (nn.Linear / 1x1 Conv1d)."""
 
     @staticmethod
-    def forward(ctx, x, W, b, act="none", grad=True, sink=None, out_bf16=False):
+    def forward(ctx, x, W, b, act="none", grad=True, sink=None, out_bf16=False, osink=None):
         x = _c(x)
         ctx.sink = sink
+        ctx.osink = osink
+        ctx.set_materialize_grads(False)
         # the pre-activation is kept only for a backward that will run (none in the reference's dead
         # blocks, eval or decoding: an N-wide fp32 write saved per call)
         z = _E(*x.shape[:-1], W.shape[0], device=x.device) if act != "none" and grad else None
@@ -215,7 +275,9 @@ class Linear(torch.autograd.Function):
     def backward(ctx, gy):
         x, W3, z, b = ctx.saved_tensors
         W = W3.view(W3.shape[0], -1)
-        gy = _c(gy)
+        gy = grad_in(gy, ctx.osink)
+        if gy is None:
+            return None, None, None, None, None, None, None, None
         if ctx.act != "none":
             gz = _E(gy.shape, device=gy.device)
             lib.call("asrx_act_bwd", _P(gy), _P(z), _P(gz), gy.numel(), ACT[ctx.act], _S())
@@ -235,7 +297,7 @@ class Linear(torch.autograd.Function):
             dW = _gret(W3, gW, ctx.dW)
         if ctx.has_b and ctx.needs_input_grad[2]:
             db = _gret(b, colsum(gz, out=_gbuf(b, True) if ctx.db else None), ctx.db)
-        return dx, dW, db, None, None, None, None
+        return dx, dW, db, None, None, None, None, None
 
 
 def _grad_needed(*ts):
@@ -244,7 +306,9 @@ def _grad_needed(*ts):
 
 def linear(x, W, b=None, act="none", out_bf16=False):
     """nn.Linear (+ act) on MFMA; out_bf16: the output only feeds GEMM operands (stored bf16 in perf mode)."""
-    return Linear.apply(x, W, b, act, _grad_needed(x, W, b), sink_of(x), out_bf16)
+    grad = _grad_needed(x, W, b)
+    osink = new_sink(out_bf16) if grad else None
+    return out_sink(Linear.apply(x, W, b, act, grad, sink_of(x), out_bf16, osink), osink)
 
 
 class KVProjFn(torch.autograd.Function):
@@ -253,11 +317,13 @@ class KVProjFn(torch.autograd.Function):
     (beta = 1) and the weight / bias gradients written into the blocks of p.grad."""
 
     @staticmethod
-    def forward(ctx, x, W, b, sink, v_bf16=False):
+    def forward(ctx, x, W, b, sink, v_bf16=False, vsink=None):
         x = _c(x)
         D = W.shape[0] // 2
         k = G.linear_fwd(x, W[:D], b[:D])
         v = G.linear_fwd(x, W[D:], b[D:], out_bf16=v_bf16)  # v only feeds attention
+        ctx.vsink = vsink
+        ctx.set_materialize_grads(False)
         ctx.sink = sink
         ctx.dW, ctx.db = _direct(ctx, 1, W), _direct(ctx, 2, b)
         ctx.save_for_backward(x, W, b)
@@ -267,8 +333,12 @@ class KVProjFn(torch.autograd.Function):
     def backward(ctx, dk, dv):
         x, W, b = ctx.saved_tensors
         D = W.shape[0] // 2
-        dk = _c(dk) if dk is not None else None
-        dv = _c(dv) if dv is not None else None
+        dk = _f32(dk)
+        dv = grad_in(dv, ctx.vsink)
+        if dk is not None:
+            dk = dk.reshape(*x.shape[:-1], D)
+        if dv is not None:
+            dv = dv.reshape(*x.shape[:-1], D)  # a sink buffer may hold the (B, L, H, hd) view's shape
         dx = None
         if ctx.needs_input_grad[0]:
             if ctx.sink is not None:
@@ -295,11 +365,14 @@ class KVProjFn(torch.autograd.Function):
                 if gpart is not None:
                     colsum(gpart.view(-1, D), out=gb[i * D:(i + 1) * D])
             dbf = _gret(b, gb, ctx.db)
-        return dx, dWf, dbf, None, None
+        return dx, dWf, dbf, None, None, None
 
 
 def kv_proj(x, W, b):
-    return KVProjFn.apply(x, W, b, sink_of(x), prec.attn_bf16_io())
+    vb = prec.attn_bf16_io()
+    vsink = new_sink(vb) if _grad_needed(x, W, b) else None
+    k, v = KVProjFn.apply(x, W, b, sink_of(x), vb, vsink)
+    return k, out_sink(v, vsink)
 
 
 def colsum(x2, out=None):
@@ -350,25 +423,33 @@ class AbbyNormalFn(torch.autograd.Function):
     """essentials.AbbyNormal (essentials.py:155-191): router GEMM on MFMA + fused row kernel."""
 
     @staticmethod
-    def forward(ctx, x, W1, b1, W2, b2, L, H, sid_base, key, use_noise, keep, sink=None, out_bf16=False):
+    def forward(ctx, x, W1, b1, W2, b2, L, H, sid_base, key, use_noise, keep, sink=None, out_bf16=False,
+                osink=None, tw=None, tb=None, side=None):
         x = _c(x)
         ctx.sink = sink
+        ctx.osink = osink
+        ctx.set_materialize_grads(False)
         d = x.shape[-1]
         rows = _rows(x)
         ob = int(out_bf16 and prec.bf16_storage())
         out = _E(x.shape, device=x.device, dtype=torch.bfloat16 if ob else torch.float32)
         ys = _E(rows, 3, device=x.device)
         idx = _E(rows, dtype=torch.int32, device=x.device)
+        # tw / tb: the consuming tgate's cs Linear(d, 3), evaluated on the fp32 output rows in the kernel
+        # (a constant for this node: tgate's own backward differentiates it)
+        tc = _E(rows, 3, device=x.device) if tw is not None else None
+        if side is not None:
+            side["tgate_c"] = tc
         if G.use_wide(d) and d <= 384:
             # perf mode: the router's d x d GEMM also applies SiLU and Linear(d, 3) in its epilogue,
             # so h_pre never makes the HBM round trip unless the backward needs it
             hpre, logits = G.router_fwd(x.view(rows, d), W1, b1, W2, keep)
             lib.call("asrx_abby_fwd_logits2", _P(x), _P(logits), _P(b2), _P(out), ob, _P(ys), _P(idx), rows, d, L, H,
-                     sid_base, key & 0xFFFFFFFF, int(use_noise), _S())
+                     sid_base, key & 0xFFFFFFFF, int(use_noise), _P(tw), _P(tb), _P(tc), _S())
         else:
             hpre = G.linear_fwd(x, W1, b1)
             lib.call("asrx_abby_fwd2", _P(x), _P(hpre), _P(W2), _P(b2), _P(out), ob, _P(ys), _P(idx), rows, d, L, H,
-                     sid_base, key & 0xFFFFFFFF, int(use_noise), _S())
+                     sid_base, key & 0xFFFFFFFF, int(use_noise), _P(tw), _P(tb), _P(tc), _S())
         if decisions.active():
             decisions.abby(key & 0xFFFFFFFF, sid_base, L, H, idx)
         ctx.dp = [_direct(ctx, i, t) for i, t in ((1, W1), (2, b1), (3, W2), (4, b2))]
@@ -378,7 +459,9 @@ class AbbyNormalFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gout):
         x, hpre, W1, W2, ys, idx, b1, b2 = ctx.saved_tensors
-        gout = _c(gout)
+        gout = grad_in(gout, ctx.osink)
+        if gout is None:
+            return (None,) * 17
         d = x.shape[-1]
         rows = _rows(x)
         fW1, fb1, fW2, fb2 = ctx.dp
@@ -396,17 +479,27 @@ class AbbyNormalFn(torch.autograd.Function):
         dW1 = G.linear_wgrad(dh, x, out=_gbuf(W1, fW1), accumulate=True)
         db1 = colsum(dh.view(-1, d), out=_gbuf(b1, fb1))
         return (dx, _gret(W1, dW1, fW1), _gret(b1, db1, fb1), _gret(W2, dW2, fW2), _gret(b2, db2, fb2),
-                None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None, None, None, None)
 
 
-def abby_normal(mod, x, L, H, sid_base, key, use_noise=True, out_bf16=False):
-    """AbbyNormal(x); out_bf16: the output only feeds GEMM / attention operands (bf16-stored in perf mode)."""
+def abby_normal(mod, x, L, H, sid_base, key, use_noise=True, out_bf16=False, tgate=None):
+    """AbbyNormal(x); out_bf16: the output only feeds GEMM / attention operands (bf16-stored in perf mode);
+    tgate: the consuming tgate module, whose cs Linear(d, 3) the kernel evaluates on the fp32 output (the
+    output is then attached to the result for ops.tgate)."""
     if use_noise:
         _noise_rows_ok(sid_base + _rows(x) // max(L * H, 1), H, L, 3)
     r = mod.mode_router
     keep = torch.is_grad_enabled() and (x.requires_grad or r[0].weight.requires_grad)
-    return AbbyNormalFn.apply(x, r[0].weight, r[0].bias, r[2].weight, r[2].bias, L, H, sid_base, key, use_noise,
-                              keep, sink_of(x), out_bf16)
+    osink = new_sink(out_bf16) if keep else None
+    tw = tb = None
+    if tgate is not None and H == 1 and x.shape[-1] >= 128:
+        tw, tb = tgate.cs[0].weight, tgate.cs[0].bias
+    side = {}
+    y = AbbyNormalFn.apply(x, r[0].weight, r[0].bias, r[2].weight, r[2].bias, L, H, sid_base, key, use_noise,
+                           keep, sink_of(x), out_bf16, osink, tw, tb, side)
+    if tw is not None:
+        y._asrx_tgate_c = (side["tgate_c"], tw)  # tgate's cs logits of these rows, for ops.tgate
+    return out_sink(y, osink)
 
 
 # =============================================================================== LayerNorm
@@ -461,7 +554,9 @@ class AttentionFn(torch.autograd.Function):
     projection) -- bf16 storage needs the bf16 flash kernels."""
 
     @staticmethod
-    def forward(ctx, q, k, v, causal, out_bf16=False):
+    def forward(ctx, q, k, v, causal, out_bf16=False, sinks=(None, None, None), osink=None, merge=False):
+        ctx.set_materialize_grads(False)
+        ctx.sinks, ctx.osink = sinks, osink
         B, Lq, H, hd = q.shape
         Lk = k.shape[1]
         ap = prec.attention_prec()
@@ -482,17 +577,35 @@ class AttentionFn(torch.autograd.Function):
         ctx.prec = prec.get()
         ctx.io = io
         ctx.save_for_backward(q, k, v, o, lse)
-        return o
+        # merge: heads merged '(h d)' (model.py:316), the out projection's input
+        return o.view(B, Lq, H * hd) if merge else o
 
     @staticmethod
     def backward(ctx, go):
         q, k, v, o, lse = ctx.saved_tensors
-        go = _c(go)
+        go = grad_in(go, ctx.osink)
+        if go is None:
+            return None, None, None, None, None, None, None, None
         B, Lq, H, hd = q.shape
+        go = go.view(B, Lq, H, hd)
         Lk = k.shape[1]
-        dq = _E(q.shape, device=q.device)
-        dk = _E(k.shape, device=q.device)
-        dv = _E(v.shape, device=q.device)
+        # an input with a sink (bf16-stored q / k / v): its gradient goes into the sink -- written by the
+        # kernel when this is the first contributor, added otherwise
+        outs, adds = [], []
+        for t, sk in zip((q, k, v), ctx.sinks):
+            if sk is not None:
+                buf, acc = sk.target(t)
+                if acc == 0:
+                    outs.append(buf.view(t.shape))
+                    adds.append(None)
+                    continue
+                tmp = _E(t.shape, device=q.device)
+                outs.append(tmp)
+                adds.append(buf)
+            else:
+                outs.append(_E(t.shape, device=q.device))
+                adds.append(None)
+        dq, dk, dv = outs
         delta = _E(B, H, Lq, device=q.device)
         io = ctx.io | (4 * int(G.is_bf16(go)))
         arrs = [_st3(t) for t in (q, k, v, o, go, dq, dk, dv)]
@@ -500,11 +613,21 @@ class AttentionFn(torch.autograd.Function):
                  _P(o), _addr(arrs[3]), _P(go), _addr(arrs[4]), _P(lse), _P(delta), _P(dq), _addr(arrs[5]), _P(dk),
                  _addr(arrs[6]), _P(dv), _addr(arrs[7]), B, H, Lq, Lk, hd, int(ctx.causal), 1.0 / math.sqrt(hd),
                  _S())
-        return dq, dk, dv, None, None
+        res = []
+        for g, buf, sk in zip((dq, dk, dv), adds, ctx.sinks):
+            if buf is not None:
+                lib.call("asrx_lincomb", _P(buf), _P(g), None, 1.0, 1.0, 0.0, _P(buf), buf.numel(), _S())
+            res.append(None if sk is not None else g)
+        return res[0], res[1], res[2], None, None, None, None, None
 
 
-def attention(q, k, v, causal, out_bf16=False):
-    return AttentionFn.apply(q, k, v, causal, out_bf16)
+def attention(q, k, v, causal, out_bf16=False, merge_heads=False):
+    """SDPA (model.py:307) on (B, L, H, hd) -> (B, Lq, H, hd), or (B, Lq, H * hd) with merge_heads;
+    out_bf16: the output only feeds the out projection (stored bf16 in perf mode)."""
+    grad = _grad_needed(q, k, v)
+    osink = new_sink(out_bf16) if grad else None
+    sinks = tuple(sink_of(t) for t in (q, k, v)) if grad else (None, None, None)
+    return out_sink(AttentionFn.apply(q, k, v, causal, out_bf16, sinks, osink, merge_heads), osink)
 
 
 # =============================================================================== rotary
@@ -624,8 +747,10 @@ class TGateFn(torch.autograd.Function):
     (asrx_add_segments / colsum over column blocks) instead of autograd's cat backward + adds."""
 
     @staticmethod
-    def forward(ctx, x, W0, W1, W2, b0, b1, b2, Wcs, bcs, out_bf16=False):
+    def forward(ctx, x, W0, W1, W2, b0, b1, b2, Wcs, bcs, out_bf16=False, sink=None, osink=None, c_pre=None):
         x = _c(x)
+        ctx.sink, ctx.osink = sink, osink
+        ctx.set_materialize_grads(False)
         D = x.shape[-1]
         rows = _rows(x)
         Wcat = _E(3 * D, D, device=x.device)
@@ -633,9 +758,11 @@ class TGateFn(torch.autograd.Function):
         lib.call("asrx_cat3", _P(W0), _P(W1), _P(W2), D * D, _P(Wcat), _S())
         lib.call("asrx_cat3", _P(b0), _P(b1), _P(b2), D, _P(bcat), _S())
         Gs = G.linear_fwd(x, Wcat, bcat, act="sigmoid")
-        c = _E(rows, 3, device=x.device)
-        xb = int(G.is_bf16(x))
-        lib.call("asrx_small_linear_fwd2", _P(x), xb, _P(Wcs), _P(bcs), _P(c), rows, D, 3, 0, _S())
+        if c_pre is not None:  # cs = Linear(D, 3)(x) evaluated by the producing AbbyNormal on fp32 x
+            c = c_pre
+        else:
+            c = _E(rows, 3, device=x.device)
+            lib.call("asrx_small_linear_fwd2", _P(x), int(G.is_bf16(x)), _P(Wcs), _P(bcs), _P(c), rows, D, 3, 0, _S())
         ob = int(out_bf16 and prec.bf16_storage())
         out = _E(x.shape, device=x.device, dtype=torch.bfloat16 if ob else torch.float32)
         lib.call("asrx_tgate_fwd2", _P(Gs), _P(c), _P(out), ob, rows, D, _S())
@@ -647,13 +774,19 @@ class TGateFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gout):
         x, Wcat, Wcs, Gs, c, bcs, W0, W1, W2, b0, b1, b2 = ctx.saved_tensors
-        gout = _c(gout)
+        gout = grad_in(gout, ctx.osink)
+        if gout is None:
+            return (None,) * 13
         D = x.shape[-1]
         rows = _rows(x)
         dGz = _E(rows, 3 * D, device=x.device)
         dc = _E(rows, 3, device=x.device)
         lib.call("asrx_tgate_bwd", _P(gout), _P(Gs), _P(c), _P(dGz), _P(dc), rows, D, _S())
-        dx = G.linear_dgrad(dGz, Wcat)
+        if ctx.sink is not None:  # x's gradient straight into its sink (x may be bf16-stored)
+            dx, acc = ctx.sink.target(x)
+            G.linear_dgrad(dGz, Wcat, out=dx.view(rows, D), beta=float(acc))
+        else:
+            dx = G.linear_dgrad(dGz, Wcat)
         dWcs, dbcs = _gbuf(Wcs, ctx.dWcs), _gbuf(bcs, ctx.dbcs)
         lib.call("asrx_small_linear_bwd2", _P(dc), None, _P(x), int(G.is_bf16(x)), _P(Wcs), _P(dx), _P(dWcs), _P(dbcs),
                  rows, D, 3, 0, 1.0, _S())
@@ -672,13 +805,18 @@ class TGateFn(torch.autograd.Function):
             gW = [dWcat[k * D:(k + 1) * D] for k in range(3)]
             dbcat = colsum(dGz)
             gB = [dbcat[k * D:(k + 1) * D] for k in range(3)]
-        return (dx.view(x.shape), *gW, *gB, _gret(Wcs, dWcs, ctx.dWcs), _gret(bcs, dbcs, ctx.dbcs), None)
+        dxr = None if ctx.sink is not None else dx.view(x.shape)
+        return (dxr, *gW, *gB, _gret(Wcs, dWcs, ctx.dWcs), _gret(bcs, dbcs, ctx.dbcs), None, None, None, None)
 
 
 def tgate(mod, x, out_bf16=False):
     """tgate (model.py:525-535); x fp32 or bf16-stored; out_bf16: the output only feeds a GEMM."""
-    return TGateFn.apply(x, *[g[0].weight for g in mod.ga], *[g[0].bias for g in mod.ga], mod.cs[0].weight,
-                         mod.cs[0].bias, out_bf16)
+    ps = [g[0].weight for g in mod.ga] + [g[0].bias for g in mod.ga] + [mod.cs[0].weight, mod.cs[0].bias]
+    osink = new_sink(out_bf16) if _grad_needed(x, *ps) else None
+    pre = getattr(x, "_asrx_tgate_c", None)
+    c_pre = pre[0] if (pre is not None and pre[1] is mod.cs[0].weight) else None
+    y = TGateFn.apply(x, *ps, out_bf16, sink_of(x), osink, c_pre)
+    return out_sink(y, osink)
 
 
 # =============================================================================== elementwise

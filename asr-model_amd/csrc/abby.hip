@@ -96,6 +96,37 @@ __device__ __forceinline__ void st_row(float* __restrict__ dst, int lane, const 
   }
 }
 
+// Coalesced layout for global memory: lane l holds features 128 j + 2 l + {0, 1} (j < E / 2), so every
+// float2 access of the wave covers 512 contiguous bytes.  The window pools need E consecutive features
+// per lane, so the forward keeps the pool arithmetic in the consecutive layout and exchanges through
+// the per-wave LDS rows (x^2 in, denominators out).
+template <int E>
+__device__ __forceinline__ int cfeat(int lane, int e) {
+  return 128 * (e >> 1) + 2 * lane + (e & 1);
+}
+template <int E>
+__device__ __forceinline__ void ld_rowc(const float* __restrict__ src, int lane, float (&v)[E]) {
+  const float2* s2 = reinterpret_cast<const float2*>(src);
+#pragma unroll
+  for (int j = 0; j < E / 2; ++j) {
+    const float2 t = s2[64 * j + lane];
+    v[2 * j] = t.x;
+    v[2 * j + 1] = t.y;
+  }
+}
+template <int E>
+__device__ __forceinline__ void st_rowc(float* __restrict__ dst, int lane, const float (&v)[E]) {
+  float2* d2 = reinterpret_cast<float2*>(dst);
+#pragma unroll
+  for (int j = 0; j < E / 2; ++j) d2[64 * j + lane] = make_float2(v[2 * j], v[2 * j + 1]);
+}
+template <int E>
+__device__ __forceinline__ void st_rowc(unsigned short* __restrict__ dst, int lane, const float (&v)[E]) {
+  unsigned* d2 = reinterpret_cast<unsigned*>(dst);
+#pragma unroll
+  for (int j = 0; j < E / 2; ++j) d2[64 * j + lane] = pack_bf16x2(v[2 * j], v[2 * j + 1]);
+}
+
 // row statistics (cv = std(x, unbiased) / (mean|x| + 1e-6)) from the lane-contiguous values
 template <int E>
 __device__ __forceinline__ void abby_row_stats(const float (&xv)[E], float& mu, float& sd, float& mabs) {
@@ -182,24 +213,40 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_fwd_kernel(const float* 
                                                                   const float* __restrict__ b2,
                                                                   TO* __restrict__ out, float* __restrict__ ys,
                                                                   int* __restrict__ idx_out, AbbyGeom g,
-                                                                  const float* __restrict__ logits) {
+                                                                  const float* __restrict__ logits,
+                                                                  const float* __restrict__ tw,
+                                                                  const float* __restrict__ tb,
+                                                                  float* __restrict__ tc) {
   typedef AbbyShape<E> S;
-  __shared__ __attribute__((aligned(16))) float rows_all[ABBY_WAVES][S::ROW];
+  // tw / tb / tc (optional): the consumer tgate's cs = Linear(d, 3) (model.py:530) applied to the fp32
+  // output row here, so the output itself can be stored bf16 for the consumer's GEMM
+  float twv[3][E];
+  if (tw) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) ld_rowc<E>(tw + k * S::D, threadIdx.x & 63, twv[k]);
+  }
+  // x^2 row: feature f at P0 + f (P0 = PAD rounded up to even, so the coalesced float2 writes stay
+  // 8-byte aligned), pads of -1 (below every x^2) on both sides; den row: the denominators by feature
+  constexpr int P0 = (S::PAD + 1) & ~1;
+  constexpr int ROWC = P0 + S::D + S::PAD + 1;
+  __shared__ __attribute__((aligned(16))) float rows_all[ABBY_WAVES][ROWC];
+  __shared__ __attribute__((aligned(16))) float den_all[ABBY_WAVES][S::D];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   float* row = rows_all[wid];
-  for (int i = lane; i < S::PAD; i += 64) {  // pads: -1 (below every x^2)
-    row[i] = -1.f;
-    row[S::PAD + S::D + i] = -1.f;
+  float* drow = den_all[wid];
+  for (int i = lane; i < S::PAD; i += 64) {
+    row[P0 - S::PAD + i] = -1.f;
+    row[P0 + S::D + i] = -1.f;
   }
   const int64_t stride = (int64_t)gridDim.x * ABBY_WAVES;
   int64_t r = (int64_t)blockIdx.x * ABBY_WAVES + wid;
-  float xn[E];  // next row's x, loaded while this row is processed
-  if (r < g.rows) ld_row<E>(x + r * S::D, lane, xn);
+  float xn[E];  // next row's x (coalesced layout), loaded while this row is processed
+  if (r < g.rows) ld_rowc<E>(x + r * S::D, lane, xn);
   for (; r < g.rows; r += stride) {
     float xv[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) xv[e] = xn[e];
-    if (r + stride < g.rows) ld_row<E>(x + (r + stride) * S::D, lane, xn);
+    if (r + stride < g.rows) ld_rowc<E>(x + (r + stride) * S::D, lane, xn);
     float l0, l1, l2;
     if (logits) {  // router logits from the GEMM epilogue (asrx_gemm_wn_router)
       l0 = logits[r * 3 + 0];
@@ -207,11 +254,11 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_fwd_kernel(const float* 
       l2 = logits[r * 3 + 2];
     } else {
       float hv[E];
-      ld_row<E>(hpre + r * S::D, lane, hv);
+      ld_rowc<E>(hpre + r * S::D, lane, hv);
       l0 = l1 = l2 = 0.f;
 #pragma unroll
       for (int e = 0; e < E; ++e) {
-        const int j = lane * E + e;
+        const int j = cfeat<E>(lane, e);
         const float hs = silu_f(hv[e]);
         l0 += hs * W2[j];
         l1 += hs * W2[S::D + j];
@@ -247,9 +294,17 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_fwd_kernel(const float* 
       ys[r * 3 + 2] = y2;
       idx_out[r] = sel;
     }
+    // x^2 in (coalesced layout) -> halo of the lane's E consecutive features -> pools -> denominators
+#pragma unroll
+    for (int j = 0; j < E / 2; ++j)
+      *reinterpret_cast<float2*>(row + P0 + 128 * j + 2 * lane) =
+          make_float2(xv[2 * j] * xv[2 * j], xv[2 * j + 1] * xv[2 * j + 1]);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     float h[S::HL];
-    abby_halo<E>(row, lane, xv, h);
-    float avg[E], ov[E];
+#pragma unroll
+    for (int i = 0; i < S::HL; ++i) h[i] = row[P0 - S::PAD + lane * E + i];
+    float avg[E];
     abby_wsum<E>(h, avg);
     if (sel == 1) {  // wave-uniform: mode 2 (max pool where max > 2 avg)
       float mx[E];
@@ -261,9 +316,37 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_fwd_kernel(const float* 
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       float base;
-      ov[e] = xv[e] / abby_denom(avg[e], base);
+      drow[lane * E + e] = abby_denom(avg[e], base);
     }
-    st_row<E>(out + r * S::D, lane, ov);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    float ov[E];
+#pragma unroll
+    for (int j = 0; j < E / 2; ++j) {
+      const float2 dn = *reinterpret_cast<const float2*>(drow + 128 * j + 2 * lane);
+      ov[2 * j] = xv[2 * j] / dn.x;
+      ov[2 * j + 1] = xv[2 * j + 1] / dn.y;
+    }
+    st_rowc<E>(out + r * S::D, lane, ov);
+    if (tw) {
+      float c0 = 0.f, c1 = 0.f, c2 = 0.f;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        c0 += ov[e] * twv[0][e];
+        c1 += ov[e] * twv[1][e];
+        c2 += ov[e] * twv[2][e];
+      }
+      c0 = wave_sum_dpp(c0);
+      c1 = wave_sum_dpp(c1);
+      c2 = wave_sum_dpp(c2);
+      if (lane == 0) {
+        tc[r * 3 + 0] = c0 + tb[0];
+        tc[r * 3 + 1] = c1 + tb[1];
+        tc[r * 3 + 2] = c2 + tb[2];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // the next row overwrites both LDS rows
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   }
 }
 
@@ -277,11 +360,17 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_bwd_kernel(
   __shared__ __attribute__((aligned(16))) float rows_all[ABBY_WAVES][S::ROW];   // x^2, then q coefA / w
   __shared__ __attribute__((aligned(16))) float cm_all[ABBY_WAVES][S::ROW];     // q coefM (sel == 1)
   __shared__ __attribute__((aligned(16))) int am_all[ABBY_WAVES][S::ROW];       // argmax (halo offset + base)
+  // layout exchange rows: global memory is read and written in the coalesced layout (cfeat), the pool
+  // arithmetic runs on E consecutive features per lane
+  __shared__ __attribute__((aligned(16))) float xr_all[ABBY_WAVES][S::D];  // x, then dx (pool part)
+  __shared__ __attribute__((aligned(16))) float gr_all[ABBY_WAVES][S::D];  // dout
   __shared__ float red[ABBY_WAVES][3];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   float* row = rows_all[wid];
   float* cmr = cm_all[wid];
   int* amr = am_all[wid];
+  float* xr = xr_all[wid];
+  float* gr = gr_all[wid];
   float accW[3][E];
   float accb[3] = {0.f, 0.f, 0.f};
 #pragma unroll
@@ -291,21 +380,30 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_bwd_kernel(
 
   const int64_t stride = (int64_t)gridDim.x * ABBY_WAVES;
   int64_t r = (int64_t)blockIdx.x * ABBY_WAVES + wid;
-  float xn[E], gn[E];  // next row's x and dout, loaded while this row is processed
+  float xn[E], gn[E];  // next row's x and dout (coalesced layout), loaded while this row is processed
   if (r < g.rows) {
-    ld_row<E>(x + r * S::D, lane, xn);
-    ld_row<E>(dout + r * S::D, lane, gn);
+    ld_rowc<E>(x + r * S::D, lane, xn);
+    ld_rowc<E>(dout + r * S::D, lane, gn);
   }
   for (; r < g.rows; r += stride) {
-    float xv[E], gv[E];
+    float xc[E], xv[E], gv[E];  // xc: coalesced layout; xv, gv: the lane's E consecutive features
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-      xv[e] = xn[e];
-      gv[e] = gn[e];
+    for (int j = 0; j < E / 2; ++j) {
+      xc[2 * j] = xn[2 * j];
+      xc[2 * j + 1] = xn[2 * j + 1];
+      *reinterpret_cast<float2*>(xr + 128 * j + 2 * lane) = make_float2(xn[2 * j], xn[2 * j + 1]);
+      *reinterpret_cast<float2*>(gr + 128 * j + 2 * lane) = make_float2(gn[2 * j], gn[2 * j + 1]);
     }
     if (r + stride < g.rows) {
-      ld_row<E>(x + (r + stride) * S::D, lane, xn);
-      ld_row<E>(dout + (r + stride) * S::D, lane, gn);
+      ld_rowc<E>(x + (r + stride) * S::D, lane, xn);
+      ld_rowc<E>(dout + (r + stride) * S::D, lane, gn);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      xv[e] = xr[lane * E + e];
+      gv[e] = gr[lane * E + e];
     }
     const int sel = idx_in[r];
     const float y0 = ys[r * 3 + 0], y1 = ys[r * 3 + 1], y2 = ys[r * 3 + 2];
@@ -407,20 +505,31 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_bwd_kernel(
     const float dcv = dz0 + dz1 + dz2;
     // cv = sd / (mabs + 1e-6)
     float mu, sd, mabs;
-    abby_row_stats<E>(xv, mu, sd, mabs);
+    abby_row_stats<E>(xc, mu, sd, mabs);
     const float den = mabs + 1e-6f;
     const float dsd = dcv / den;
     const float dmabs = -dcv * sd / (den * den);
     const float csd = sd > 0.f ? dsd / ((S::D - 1) * sd) : 0.f;
     const float cma = dmabs / S::D;
-    float hv[E], dh[E], w2v[3][E];
-    ld_row<E>(hpre + r * S::D, lane, hv);
+    // the pool part of dx back to the coalesced layout; everything below is elementwise in it
 #pragma unroll
-    for (int k = 0; k < 3; ++k) ld_row<E>(W2 + k * S::D, lane, w2v[k]);  // L1-resident
+    for (int e = 0; e < E; ++e) xr[lane * E + e] = dxv[e];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    float dxc[E], hv[E], dh[E], w2v[3][E];
+#pragma unroll
+    for (int j = 0; j < E / 2; ++j) {
+      const float2 t = *reinterpret_cast<const float2*>(xr + 128 * j + 2 * lane);
+      dxc[2 * j] = t.x;
+      dxc[2 * j + 1] = t.y;
+    }
+    ld_rowc<E>(hpre + r * S::D, lane, hv);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) ld_rowc<E>(W2 + k * S::D, lane, w2v[k]);  // L1-resident
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      const float sgn = xv[e] > 0.f ? 1.f : (xv[e] < 0.f ? -1.f : 0.f);
-      dxv[e] += csd * (xv[e] - mu) + cma * sgn;
+      const float sgn = xc[e] > 0.f ? 1.f : (xc[e] < 0.f ? -1.f : 0.f);
+      dxc[e] += csd * (xc[e] - mu) + cma * sgn;
       const float wsum = dz0 * w2v[0][e] + dz1 * w2v[1][e] + dz2 * w2v[2][e];
       dh[e] = silu_grad(hv[e]) * wsum;
       const float hs = silu_f(hv[e]);
@@ -430,12 +539,14 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_bwd_kernel(
     }
     if (g.acc) {
       float old[E];
-      ld_row<E>(dx + r * S::D, lane, old);
+      ld_rowc<E>(dx + r * S::D, lane, old);
 #pragma unroll
-      for (int e = 0; e < E; ++e) dxv[e] += old[e];
+      for (int e = 0; e < E; ++e) dxc[e] += old[e];
     }
-    st_row<E>(dx + r * S::D, lane, dxv);
-    st_row<E>(dhpre + r * S::D, lane, dh);
+    st_rowc<E>(dx + r * S::D, lane, dxc);
+    st_rowc<E>(dhpre + r * S::D, lane, dh);
+    __builtin_amdgcn_wave_barrier();  // the next row overwrites the exchange rows
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     accb[0] += dz0;
     accb[1] += dz1;
     accb[2] += dz2;
@@ -454,8 +565,8 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_bwd_kernel(
 #pragma unroll
       for (int k = 0; k < 3; ++k)
 #pragma unroll
-        for (int e = 0; e < E; ++e) {
-          float* sl = slot(k, lane * E + e);
+        for (int e = 0; e < E; ++e) {  // accW is in the coalesced layout
+          float* sl = slot(k, cfeat<E>(lane, e));
           *sl = (ww == 0 ? 0.f : *sl) + accW[k][e];
         }
     }
@@ -754,7 +865,6 @@ using namespace asrx;
 
 #define ABBY_DISPATCH(KERNEL, ...)                                                 \
   switch (E) {                                                                     \
-    case 1: KERNEL<1><<<grid, 64 * ABBY_WAVES, 0, stream>>>(__VA_ARGS__); break;   \
     case 2: KERNEL<2><<<grid, 64 * ABBY_WAVES, 0, stream>>>(__VA_ARGS__); break;   \
     case 4: KERNEL<4><<<grid, 64 * ABBY_WAVES, 0, stream>>>(__VA_ARGS__); break;   \
     case 6: KERNEL<6><<<grid, 64 * ABBY_WAVES, 0, stream>>>(__VA_ARGS__); break;   \
@@ -782,7 +892,9 @@ static AbbyGeom make_geom(int64_t rows, int64_t d, int64_t L, int64_t H, int64_t
 // idx (rows) int32.
 extern "C" int asrx_abby_fwd2(const float* x, const float* hpre, const float* W2, const float* b2, void* out,
                               int out_bf16, float* ys, int* idx, int64_t rows, int64_t d, int64_t L, int64_t H,
-                              int64_t sid_base, uint32_t key, int use_noise, hipStream_t stream) {
+                              int64_t sid_base, uint32_t key, int use_noise, const float* tw, const float* tb,
+                              float* tc, hipStream_t stream) {
+  ASRX_REQUIRE(!tw || d >= 128, "AbbyNormal: the fused tgate cs needs d >= 128");
   ASRX_REQUIRE(d % 64 == 0 && d >= 64 && d <= 1024, "AbbyNormal: d=%ld must be a multiple of 64 in [64,1024]",
                (long)d);
   if (rows == 0) return 0;
@@ -799,9 +911,10 @@ extern "C" int asrx_abby_fwd2(const float* x, const float* hpre, const float* W2
     ASRX_LAUNCHED("asrx_abby_fwd");
   }
   if (out_bf16) {
-    ABBY_DISPATCH_T(abby_fwd_kernel, unsigned short, x, hpre, W2, b2, (unsigned short*)out, ys, idx, g, nullptr);
+    ABBY_DISPATCH_T(abby_fwd_kernel, unsigned short, x, hpre, W2, b2, (unsigned short*)out, ys, idx, g, nullptr, tw,
+                    tb, tc);
   } else {
-    ABBY_DISPATCH_T(abby_fwd_kernel, float, x, hpre, W2, b2, (float*)out, ys, idx, g, nullptr);
+    ABBY_DISPATCH_T(abby_fwd_kernel, float, x, hpre, W2, b2, (float*)out, ys, idx, g, nullptr, tw, tb, tc);
   }
   ASRX_LAUNCHED("asrx_abby_fwd");
 }
@@ -809,14 +922,17 @@ extern "C" int asrx_abby_fwd2(const float* x, const float* hpre, const float* W2
 extern "C" int asrx_abby_fwd(const float* x, const float* hpre, const float* W2, const float* b2, float* out,
                              float* ys, int* idx, int64_t rows, int64_t d, int64_t L, int64_t H,
                              int64_t sid_base, uint32_t key, int use_noise, hipStream_t stream) {
-  return asrx_abby_fwd2(x, hpre, W2, b2, out, 0, ys, idx, rows, d, L, H, sid_base, key, use_noise, stream);
+  return asrx_abby_fwd2(x, hpre, W2, b2, out, 0, ys, idx, rows, d, L, H, sid_base, key, use_noise, nullptr, nullptr,
+                        nullptr, stream);
 }
 
 // Same, with the router logits (rows x 3, without b2) precomputed by asrx_gemm_wn_router; out is stored
 // fp32 (out_bf16 = 0) or bf16 (1).
 extern "C" int asrx_abby_fwd_logits2(const float* x, const float* logits, const float* b2, void* out, int out_bf16,
                                      float* ys, int* idx, int64_t rows, int64_t d, int64_t L, int64_t H,
-                                     int64_t sid_base, uint32_t key, int use_noise, hipStream_t stream) {
+                                     int64_t sid_base, uint32_t key, int use_noise, const float* tw,
+                                     const float* tb, float* tc, hipStream_t stream) {
+  ASRX_REQUIRE(!tw || d >= 128, "AbbyNormal: the fused tgate cs needs d >= 128");
   ASRX_REQUIRE(d % 64 == 0 && d >= 64 && d <= 1024, "AbbyNormal: d=%ld must be a multiple of 64 in [64,1024]",
                (long)d);
   if (rows == 0) return 0;
@@ -834,9 +950,10 @@ extern "C" int asrx_abby_fwd_logits2(const float* x, const float* logits, const 
     ASRX_LAUNCHED("asrx_abby_fwd_logits");
   }
   if (out_bf16) {
-    ABBY_DISPATCH_T(abby_fwd_kernel, unsigned short, x, nullptr, nullptr, b2, (unsigned short*)out, ys, idx, g, logits);
+    ABBY_DISPATCH_T(abby_fwd_kernel, unsigned short, x, nullptr, nullptr, b2, (unsigned short*)out, ys, idx, g, logits,
+                    tw, tb, tc);
   } else {
-    ABBY_DISPATCH_T(abby_fwd_kernel, float, x, nullptr, nullptr, b2, (float*)out, ys, idx, g, logits);
+    ABBY_DISPATCH_T(abby_fwd_kernel, float, x, nullptr, nullptr, b2, (float*)out, ys, idx, g, logits, tw, tb, tc);
   }
   ASRX_LAUNCHED("asrx_abby_fwd_logits");
 }
@@ -844,7 +961,8 @@ extern "C" int asrx_abby_fwd_logits2(const float* x, const float* logits, const 
 extern "C" int asrx_abby_fwd_logits(const float* x, const float* logits, const float* b2, float* out, float* ys,
                                     int* idx, int64_t rows, int64_t d, int64_t L, int64_t H, int64_t sid_base,
                                     uint32_t key, int use_noise, hipStream_t stream) {
-  return asrx_abby_fwd_logits2(x, logits, b2, out, 0, ys, idx, rows, d, L, H, sid_base, key, use_noise, stream);
+  return asrx_abby_fwd_logits2(x, logits, b2, out, 0, ys, idx, rows, d, L, H, sid_base, key, use_noise, nullptr,
+                               nullptr, nullptr, stream);
 }
 
 // dW2 / db2 are accumulated (caller zeroes them).  dx (acc == 0) and dhpre are overwritten; acc != 0

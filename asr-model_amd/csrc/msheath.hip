@@ -236,8 +236,9 @@ __global__ __launch_bounds__(256) void axpy_row2_colsum_kernel(const float4* __r
       const float sc = s1[r] * s2[r];
       const int64_t i = r * d4 + c;
       const float4 a = x[i], v = y[i];
-      const float4 o = make_float4(a.x + sc * v.x, a.y + sc * v.y, a.z + sc * v.z, a.w + sc * v.w);
-      out[i] = o;
+      const float4 o = make_float4(__builtin_fmaf(sc, v.x, a.x), __builtin_fmaf(sc, v.y, a.y),
+                                   __builtin_fmaf(sc, v.z, a.z), __builtin_fmaf(sc, v.w, a.w));
+      if (out) out[i] = o;  // null: column sums only (the in-place no-grad MSheath recomputes x_new)
       acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
     }
   }
@@ -288,11 +289,46 @@ __global__ void jump_select4_kernel(const float4* __restrict__ xn, const float4*
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     if (a) {
       const float4 u = xn[base + i], v = orig[base + i], w = gam[b * d4 + i % d4];
-      out[base + i] = make_float4(al * u.x + be * v.x + w.x, al * u.y + be * v.y + w.y, al * u.z + be * v.z + w.z,
-                                  al * u.w + be * v.w + w.w);
+      out[base + i] = make_float4(__builtin_fmaf(al, u.x, __builtin_fmaf(be, v.x, w.x)),
+                                  __builtin_fmaf(al, u.y, __builtin_fmaf(be, v.y, w.y)),
+                                  __builtin_fmaf(al, u.z, __builtin_fmaf(be, v.z, w.z)),
+                                  __builtin_fmaf(al, u.w, __builtin_fmaf(be, v.w, w.w)));
     } else {
       out[base + i] = xold[base + i];
     }
+  }
+}
+
+// No-grad MSheath layer step (the reference's dead blocks, eval, decoding: nothing is saved for a
+// backward): for a sample at this layer xout <- alpha (xin + s1 s2 y) + beta orig + gam, i.e. x_new
+// (model.py:461) and the jump select (489-501) in one pass without materialising x_new.  In place
+// (xin == xout) a sample not at the layer is not touched -- its x already is the layer's output; otherwise
+// it is copied.  Same arithmetic as axpy_row2_colsum + jump_select4 (explicit fma): bit-identical.
+__global__ void jump_axpy_inplace_kernel(const float4* xin, float4* xout, const float* __restrict__ s1,
+                                         const float* __restrict__ s2, const float4* __restrict__ y,
+                                         const float4* __restrict__ orig, const float* __restrict__ act,
+                                         const float* __restrict__ alpha, const float* __restrict__ beta,
+                                         const float4* __restrict__ gam, int64_t L, int d4) {
+  const int64_t b = blockIdx.y;
+  const int64_t n = L * d4;
+  const int64_t base = b * n;
+  if (act[b] == 0.f) {
+    if (xin != xout)
+      for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        xout[base + i] = xin[base + i];
+    return;
+  }
+  const float al = alpha[b], be = beta[b];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = b * L + i / d4;
+    const float sc = s1[r] * s2[r];
+    const float4 a = xin[base + i], v = y[base + i], o = orig[base + i], w = gam[b * d4 + i % d4];
+    const float4 u = make_float4(__builtin_fmaf(sc, v.x, a.x), __builtin_fmaf(sc, v.y, a.y), __builtin_fmaf(sc, v.z, a.z),
+                                 __builtin_fmaf(sc, v.w, a.w));
+    xout[base + i] = make_float4(__builtin_fmaf(al, u.x, __builtin_fmaf(be, o.x, w.x)),
+                                 __builtin_fmaf(al, u.y, __builtin_fmaf(be, o.y, w.y)),
+                                 __builtin_fmaf(al, u.z, __builtin_fmaf(be, o.z, w.z)),
+                                 __builtin_fmaf(al, u.w, __builtin_fmaf(be, o.w, w.w)));
   }
 }
 
@@ -678,6 +714,20 @@ int asrx_axpy_row2_bwd(const float* g, const float* s1, const float* s2, const f
   axpy_row2_bwd_kernel<<<(unsigned)std::min<int64_t>((rows + 3) / 4, 8192), 256, 0, stream>>>(
       (const float4*)g, s1, s2, (const float4*)y, (float4*)dy, ds1, ds2, rows, (int)(d / 4));
   ASRX_LAUNCHED("asrx_axpy_row2_bwd");
+}
+
+int asrx_jump_axpy_inplace(const float* xin, float* xout, const float* s1, const float* s2, const float* y,
+                           const float* orig, const float* act, const float* alpha, const float* beta, const float* gam,
+                           int64_t B, int64_t L, int64_t d, hipStream_t stream) {
+  ASRX_REQUIRE(d % 4 == 0, "asrx_jump_axpy_inplace: d % 4 != 0");
+  ASRX_REQUIRE(xout != orig, "asrx_jump_axpy_inplace: xout must not alias orig");
+  if (B * L == 0) return 0;
+  const int64_t n = L * d / 4;
+  dim3 grid((unsigned)std::min<int64_t>((n + 255) / 256, 512), (unsigned)B);
+  jump_axpy_inplace_kernel<<<grid, 256, 0, stream>>>((const float4*)xin, (float4*)xout, s1, s2, (const float4*)y,
+                                                     (const float4*)orig, act, alpha, beta, (const float4*)gam, L,
+                                                     (int)(d / 4));
+  ASRX_LAUNCHED("asrx_jump_axpy_inplace");
 }
 
 int asrx_jump_select4(const float* xn, const float* orig, const float* xold, const float* act, const float* alpha,

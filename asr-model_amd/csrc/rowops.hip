@@ -110,8 +110,10 @@ __global__ __launch_bounds__(64 * RW) void ln_fwd_t_kernel(const float* __restri
     }
     const float rs = rsqrtf(wave_sum_dpp(v) * (1.0f / D) + eps);
     float yv[E];
+    // explicit fma: the fp32- and bf16-output instantiations must round identically (a contraction the
+    // compiler chooses per instantiation would move some bf16 roundings by one ulp)
 #pragma unroll
-    for (int e = 0; e < E; ++e) yv[e] = (xv[e] - mu) * rs * wv[e] + bv[e];
+    for (int e = 0; e < E; ++e) yv[e] = __builtin_fmaf((xv[e] - mu) * rs, wv[e], bv[e]);
     st_lane<E>(y + r * D, lane, yv);
     if (nrm) {
       float q = 0.f;
@@ -615,7 +617,7 @@ __global__ __launch_bounds__(64 * RW) void msheath_row_fwd_kernel(MSRowFwd p) {
     float yv[E], gd = 0.f;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      yv[e] = (xv[e] - mu) * rs * wv[e] + bv[e];
+      yv[e] = __builtin_fmaf((xv[e] - mu) * rs, wv[e], bv[e]);  // explicit: as ln_fwd_t_kernel
       gd += yv[e] * gwv[e];
     }
     if (p.pxb) st_lane<E>(p.pxb + r * D, lane, yv);
@@ -799,7 +801,8 @@ __global__ __launch_bounds__(64 * RW) void tgate_fwd_kernel(const float* __restr
     const float t0 = e0 * inv, t1 = e1 * inv, t2 = e2 * inv;
     const float* gr = G + r * 3 * D;
     for (int j = lane; j < D; j += 64) {
-      const float v = gr[j] * t0 + gr[D + j] * t1 + gr[2 * D + j] * t2;
+      // explicit fma chain: identical rounding in the fp32- and bf16-output instantiations
+      const float v = __builtin_fmaf(gr[2 * D + j], t2, __builtin_fmaf(gr[D + j], t1, gr[j] * t0));
       if constexpr (sizeof(TO) == 4) out[r * D + j] = v;
       else out[r * D + j] = __builtin_bit_cast(unsigned short, (__bf16)v);
     }

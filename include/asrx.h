@@ -130,13 +130,15 @@ int asrx_abby_fwd_logits(const float* x, const float* logits, const float* b2, f
                          int use_noise, asrx_stream_t stream);
 /* asrx_abby_fwd / asrx_abby_fwd_logits with out stored fp32 (out_bf16 = 0) or bf16 (1: the AbbyNormal
  * output feeds only a projection GEMM or attention -- attention.q[0] / kv[0] and the per-head norm,
- * model.py:244-245, 248; the final norm before the tied logits, model.py:629). */
+ * model.py:244-245, 248; the final norm before the tied logits, model.py:629; mlp's first norm, 573).
+ * tw (3 x d) / tb (3) / tc (rows x 3), optional (d >= 128): the consuming tgate's cs = Linear(d, 3)
+ * (model.py:530) evaluated on the fp32 output rows, so that output can be stored bf16. */
 int asrx_abby_fwd2(const float* x, const float* hpre, const float* W2, const float* b2, void* out, int out_bf16,
                    float* ys, int* idx, int64_t rows, int64_t d, int64_t L, int64_t H, int64_t sid_base, uint32_t key,
-                   int use_noise, asrx_stream_t stream);
+                   int use_noise, const float* tw, const float* tb, float* tc, asrx_stream_t stream);
 int asrx_abby_fwd_logits2(const float* x, const float* logits, const float* b2, void* out, int out_bf16, float* ys,
                           int* idx, int64_t rows, int64_t d, int64_t L, int64_t H, int64_t sid_base, uint32_t key,
-                          int use_noise, asrx_stream_t stream);
+                          int use_noise, const float* tw, const float* tb, float* tc, asrx_stream_t stream);
 int asrx_abby_bwd(const float* dout, const float* x, const float* hpre, const float* W2, const float* ys,
                   const int* idx, float* dx, float* dhpre, float* dW2, float* db2, int64_t rows, int64_t d,
                   asrx_stream_t stream);
@@ -363,6 +365,12 @@ int asrx_axpy_row2_bwd(const float* g, const float* s1, const float* s2, const f
                        float* ds2, int64_t rows, int64_t d, asrx_stream_t stream);
 /* float4 forms of asrx_jump_select(_bwd) for d % 4 == 0 (the backward zeroes dalpha/dbeta/dgam: one
  * memset when they are one block [dalpha | dbeta | dgam], as asrx_jump_select4_bwd_acc too). */
+/* No-grad MSheath layer step (dead blocks, eval, decoding): for samples at this layer
+ * xout = alpha (xin + s1 s2 y) + beta orig + gam (x_new, model.py:461, and the jump select, 489-501, in
+ * one pass, x_new never stored); in place (xin == xout) other samples are untouched, else copied. */
+int asrx_jump_axpy_inplace(const float* xin, float* xout, const float* s1, const float* s2, const float* y,
+                           const float* orig, const float* act, const float* alpha, const float* beta, const float* gam,
+                           int64_t B, int64_t L, int64_t d, asrx_stream_t stream);
 int asrx_jump_select4(const float* xn, const float* orig, const float* xold, const float* act, const float* alpha,
                       const float* beta, const float* gam, float* out, int64_t B, int64_t L, int64_t d,
                       asrx_stream_t stream);

@@ -155,3 +155,28 @@ def test_model_forward_unchanged_by_bf16_storage(cuda):
     worst = max(float((res[1][2][n] - res[0][2][n]).abs().max() / res[0][2][n].abs().max().clamp_min(1e-20))
                 for n in res[0][2])
     assert worst < 5e-2, worst
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_msheath_nograd_inplace_step_is_exact(cuda, precision):
+    """MSheath without a backward (dead blocks, eval, decoding) skips x_new and updates x in place
+    (asrx_jump_axpy_inplace); its output must equal the saving path's bit for bit, with jumps taken
+    (samples skipping layers) and the caller's input left untouched."""
+    from asrx import msheath, ops, prec
+    from asrx.model import MSheath
+
+    torch.manual_seed(2)
+    mod = MSheath(384, 6, 4).cuda()
+    with torch.no_grad():
+        mod.pnet.net[2].bias.copy_(torch.tensor([0.0, 2.0, 2.0]))  # favour jumps
+    g = torch.Generator().manual_seed(3)
+    x = (torch.randn(5, 300, 384, generator=g) * 2).cuda()
+    x_copy = x.clone()
+    gpol = ops.policy_noise(5, 4, 0, 1234, x.device)
+    with prec.precision(precision), torch.no_grad():
+        y0, _ = msheath.forward(mod, x, gpol, save=False)
+        y1, sv = msheath.forward(mod, x, gpol, save=True)
+    assert torch.equal(x, x_copy)
+    assert torch.equal(y0, y1)
+    acts = torch.stack([s["active"] for s in sv["layers"]]).cpu()
+    assert bool((acts == 0).any()), acts  # some sample skipped a layer

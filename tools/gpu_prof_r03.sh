@@ -1,0 +1,16 @@
+#!/bin/bash
+# GPU call: round-3 evidence -- rocprofv3 kernel trace + stats of the bench (graph replay, 1 warmup + 3
+# timed = 4 executed steps), separate FETCH_SIZE / WRITE_SIZE passes over one eager step, and an MFMA
+# busy pass (SQ_VALU_MFMA_BUSY_CYCLES with GRBM_GUI_ACTIVE) over one eager step.
+set -e
+R=${GRAFT_REPO_ROOT:-/root/repo}
+TAG=${1:-r03}
+mkdir -p $R/gpurun_out
+cd /tmp && export TMPDIR=/tmp
+B="$R/bench.py --no-cpu-baseline --no-probe --no-optimizer --no-dead-block-line"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$TAG -o run --output-format csv -- python3 $B --steps 3 --warmup 1 > $R/gpurun_out/prof_$TAG.log 2>&1
+tail -1 $R/gpurun_out/prof_$TAG.log | cut -c1-300
+timeout -s KILL 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $R/gpurun_out/pmcf_$TAG -o run --output-format csv -- python3 $B --steps 1 --warmup 0 --eager > $R/gpurun_out/pmcf_$TAG.log 2>&1
+timeout -s KILL 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $R/gpurun_out/pmcw_$TAG -o run --output-format csv -- python3 $B --steps 1 --warmup 0 --eager > $R/gpurun_out/pmcw_$TAG.log 2>&1
+timeout -s KILL 300 rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE -d $R/gpurun_out/pmcm_$TAG -o run --output-format csv -- python3 $B --steps 1 --warmup 0 --eager > $R/gpurun_out/pmcm_$TAG.log 2>&1
+echo prof-ok
