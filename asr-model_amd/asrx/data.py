@@ -188,7 +188,7 @@ def extract_features_batch(batches, tokenizer=None, spectrogram=False, waveform=
             if n > target and n == target * hop_length:
                 _, w_tensor = _mel.logmel(audio.unsqueeze(0), layout="BMF", pool=True)
             else:
-                w_tensor = torch.nn.functional.adaptive_avg_pool1d(audio.view(1, 1, -1), target)[0]
+                w_tensor = _mel.wave_pool(audio.unsqueeze(0), target)
         out.append({"waveform": w_tensor, "spectrogram": s_tensor, "pitch_tokens": None, "pitch": pitch_of.get(i),
                     "harmonic": None, "aperiodic": None, "labels": labels, "phase": phase_of.get(i)})
     return out

@@ -118,8 +118,8 @@ def extract_features(batch, tokenizer=None, spectrogram=False, pitch=False, wave
         if n > target and n == target * hop_length:
             _, pooled = _mel.logmel(audio.unsqueeze(0), layout="BMF", pool=True)
             w_tensor = pooled  # (1, target)
-        elif n > target:
-            w_tensor = torch.nn.functional.adaptive_avg_pool1d(audio.view(1, 1, -1), target)[0]
+        elif n > target and target > 0:
+            w_tensor = _mel.wave_pool(audio.unsqueeze(0), target)  # (1, target), any clip length
         else:
             w_tensor = torch.nn.functional.interpolate(audio.view(1, 1, -1), size=target, mode="linear",
                                                        align_corners=False)[0]

@@ -161,6 +161,7 @@ SIGNATURES = {
                                     + [_f32, _f32, _p, _i64, _i64, _p]),
     "asrx_layernorm_fwd3": (_i32, [_p, _p, _p, _p, _i32] + [_p] * 6 + [_i32, _i64, _i64, _f32, _p]),
     "asrx_jump_axpy_inplace": (_i32, [_p] * 10 + [_i64, _i64, _i64, _p]),
+    "asrx_wave_pool": (_i32, [_p, _i64, _i64, _i64, _i64, _p, _p]),
     "asrx_maxfactor_param_bytes": (_i32, []),
     "asrx_maxfactor_step": (_i32, [_p, _i32, _i64, _i64, _i64, _i64, _i64, _p, _p]),
 }

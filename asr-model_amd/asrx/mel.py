@@ -171,3 +171,17 @@ def logmel(wav: torch.Tensor, layout: str = "BFM", pool: bool = False):
              lib.ptr(fbs), lib.ptr(out), lay, F * N_MELS, lib.ptr(ws), lib.ptr(pooled), T, lib.stream())
     probe.end("logmel", e0, algorithmic_bytes(B, N, pool))
     return (out, pooled) if pool else out
+
+
+def wave_pool(wav: torch.Tensor, T: int) -> torch.Tensor:
+    """adaptive_avg_pool1d of (B, N) float32 device audio to T bins (essentials.py:493-510) for any N
+    (asrx_wave_pool; logmel(pool=True) fuses the 160 | N case into the mel pass)."""
+    lib.require_gpu(wav)
+    if wav.dim() == 1:
+        wav = wav.unsqueeze(0)
+    if wav.dtype != torch.float32 or wav.stride(-1) != 1:
+        raise ValueError("wave_pool expects float32 audio with unit inner stride")
+    B, N = wav.shape
+    out = torch.empty(B, T, device=wav.device, dtype=torch.float32)
+    lib.call("asrx_wave_pool", lib.ptr(wav), B, N, wav.stride(0), T, lib.ptr(out), lib.stream())
+    return out

@@ -7,7 +7,7 @@ c=waveform 2) uses s*B + b.  The oracle restates this independently (oracle/keys
 """
 from __future__ import annotations
 
-LSTRIDE = 4096
+LSTRIDE = 8192
 
 
 def site_key(seed: int, step: int, site: str) -> int:

@@ -1168,13 +1168,13 @@ class DropoutAdd(torch.autograd.Function):
 
 
 def _noise_rows_ok(sid_end, C, T, k=1):
-    """Keyed-noise element indices ((sid * C + c) * 4096 + t for dropout, ((sid * H + h) * 4096 + l) * 3 + k
-    for the gumbel draws, oracle/keys.py) are uint32 and assume positions < 4096 (clips up to ~40.9 s
+    """Keyed-noise element indices ((sid * C + c) * 8192 + t for dropout, ((sid * H + h) * 8192 + l) * 3 + k
+    for the gumbel draws, oracle/keys.py) are uint32 and assume positions < 8192 (clips up to ~81.9 s
     at hop 160): refuse shapes that would alias draws instead of silently reusing them."""
     from .noise import LSTRIDE
 
     if T > LSTRIDE:
-        raise ValueError(f"keyed noise: sequence length {T} > {LSTRIDE} positions (clips longer than ~40.9 s) "
+        raise ValueError(f"keyed noise: sequence length {T} > {LSTRIDE} positions (clips longer than ~81.9 s) "
                          "would alias dropout/gumbel draws")
     if sid_end * C * LSTRIDE * k >= 1 << 32:
         raise ValueError(f"keyed noise: {sid_end} streams x {C} channels overflow the 32-bit noise index")

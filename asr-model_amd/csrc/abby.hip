@@ -10,7 +10,7 @@
 //
 // One wave per row (d % 64 == 0, d <= 1024); each lane owns d/64 consecutive features and reads
 // its window halo of x^2 from a padded per-wave LDS row (see AbbyShape).
-// Noise: gumbel g_k = -log(-log(u)) with u = noise_uniform(key, ((sid*H + h)*4096 + l)*3 + k); the
+// Noise: gumbel g_k = -log(-log(u)) with u = noise_uniform(key, ((sid*H + h)*8192 + l)*3 + k); the
 // row r (kernel order: sample-major, then position, then head) maps to sid = sid_base + r/(L*H),
 // l = (r % (L*H)) / H, h = r % H.
 //
@@ -52,7 +52,7 @@ __device__ __forceinline__ uint32_t abby_noise_idx(const AbbyGeom& g, int64_t r,
   const int64_t sid = g.sid_base + r / per;
   const int64_t q = r % per;
   const int64_t l = q / g.H, h = q % g.H;
-  return (uint32_t)(((sid * g.H + h) * 4096 + l) * 3 + k);
+  return (uint32_t)(((sid * g.H + h) * 8192 + l) * 3 + k);
 }
 
 template <int E>

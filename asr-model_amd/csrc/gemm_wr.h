@@ -291,15 +291,19 @@ __device__ __forceinline__ void epilogue_router(const Params& p, f32x4 (&acc)[4]
 
 // ABF: A is stored bf16 (M x K, lda in elements): one 16-byte chunk of 8 k per thread and k-step
 // (row t/4, k chunk t%4), already in the image's element type -- half the bytes, no conversion
+// stage registers are native vectors: a HIP_vector_type (uint4 / float4) copy lowers to a memcpy
+// that keeps the whole stage in scratch (measured: 80-144 B/lane of scratch plus an LDS-promoted
+// stage in the bf16-A instantiations)
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 template <int NJ, bool ABF>
 struct WrStage {
   float4 a[2];     // 2 x 4 fp32 of the A tile (row q/8, k chunk q%8), q = tid + 512 i
-  uint4 b[NJ];     // NJ x 8 bf16 of the W tile (row q/4, k chunk q%4), q = tid + 512 i
+  u32x4 b[NJ];     // NJ x 8 bf16 of the W tile (row q/4, k chunk q%4), q = tid + 512 i
 };
 template <int NJ>
 struct WrStage<NJ, true> {
-  uint4 ah;        // 8 bf16 of the A tile (row tid/4, k chunk tid%4)
-  uint4 b[NJ];
+  u32x4 ah;        // 8 bf16 of the A tile (row tid/4, k chunk tid%4)
+  u32x4 b[NJ];
 };
 
 template <int NJ, bool CONV, bool ABF>
@@ -316,7 +320,7 @@ __device__ __forceinline__ void wr_load(const Params& p, WrStage<NJ, ABF>& st, i
       o -= p.convC;
     }
     const unsigned short* Ah = reinterpret_cast<const unsigned short*>(p.A);
-    st.ah = *reinterpret_cast<const uint4*>(ok ? (const void*)(Ah + o) : (const void*)zero_page);
+    st.ah = *reinterpret_cast<const u32x4*>(ok ? (const void*)(Ah + o) : (const void*)zero_page);
   } else
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -338,7 +342,7 @@ __device__ __forceinline__ void wr_load(const Params& p, WrStage<NJ, ABF>& st, i
   for (int i = 0; i < NJ; ++i) {
     const int q = t + NTHR * i;
     const int n = n0 + (q >> 2), k = k0 + 8 * (q & 3);
-    st.b[i] = *reinterpret_cast<const uint4*>((n < p.N && k < p.K) ? (const void*)(p.W + (int64_t)n * p.ldw + k)
+    st.b[i] = *reinterpret_cast<const u32x4*>((n < p.N && k < p.K) ? (const void*)(p.W + (int64_t)n * p.ldw + k)
                                                                   : (const void*)zero_page);
   }
 }
@@ -350,7 +354,7 @@ __device__ __forceinline__ void wr_store(const WrStage<NJ, ABF>& st, char* At, c
   const int t = threadIdx.x;
   if constexpr (ABF) {
     const int row = t >> 2, c = t & 3;
-    *reinterpret_cast<uint4*>(At + row * 64 + 16 * (c ^ swb(row))) = st.ah;
+    *reinterpret_cast<u32x4*>(At + row * 64 + 16 * (c ^ swb(row))) = st.ah;
   } else
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -366,7 +370,7 @@ __device__ __forceinline__ void wr_store(const WrStage<NJ, ABF>& st, char* At, c
   for (int i = 0; i < NJ; ++i) {
     const int q = t + NTHR * i;
     const int n = q >> 2, c = q & 3;
-    *reinterpret_cast<uint4*>(Bt + n * 64 + 16 * (c ^ swb(n))) = st.b[i];
+    *reinterpret_cast<u32x4*>(Bt + n * 64 + 16 * (c ^ swb(n))) = st.b[i];
   }
 }
 

@@ -401,3 +401,34 @@ extern "C" int asrx_logmel(const float* wav, int64_t B, int64_t N, int64_t ld_wa
 }
 
 extern "C" int asrx_mel_frames(int64_t N) { return (int)(1 + N / MEL_HOP); }
+
+// ---------------------------------------------------------------------------------------------
+// Waveform feature for any clip length (essentials.py:493-510): adaptive_avg_pool1d(audio, T) with
+// T = int(N / 160) bins, bin i = mean of samples [floor(i N / T), ceil((i + 1) N / T)) -- the general
+// case of the fused pool above (which needs 160 | N).  One wave per bin: the <= 161-sample window is
+// read coalesced, summed in a wave reduction, and divided once.
+namespace asrx {
+__global__ __launch_bounds__(256) void wave_pool_kernel(const float* __restrict__ wav, int64_t N, int64_t ld_wav,
+                                                        int64_t T, int64_t B, float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); w < B * T; w += nw) {
+    const int64_t b = w / T, i = w % T;
+    const int64_t s = (i * N) / T, e = ((i + 1) * N + T - 1) / T;
+    const float* x = wav + b * ld_wav;
+    float acc = 0.f;
+    for (int64_t j = s + lane; j < e; j += 64) acc += x[j];
+    acc = wave_sum(acc);
+    if (lane == 0) out[w] = acc / (float)(e - s);
+  }
+}
+}  // namespace asrx
+
+extern "C" int asrx_wave_pool(const float* wav, int64_t B, int64_t N, int64_t ld_wav, int64_t T, float* out,
+                              hipStream_t stream) {
+  ASRX_REQUIRE(B > 0 && N > 0 && T > 0 && T <= N, "asrx_wave_pool: need 0 < T <= N (N=%ld T=%ld)", (long)N, (long)T);
+  const int64_t waves = B * T;
+  const unsigned grid = (unsigned)std::min<int64_t>((waves + 3) / 4, 65536);
+  asrx::wave_pool_kernel<<<grid, 256, 0, stream>>>(wav, N, ld_wav, T, B, out);
+  ASRX_LAUNCHED("asrx_wave_pool");
+}

@@ -1093,7 +1093,7 @@ __global__ void glu_bwd_kernel(const float* __restrict__ g, const float* __restr
 }
 
 // nn.Dropout(0.1) in train mode (model.py:107, 147) with keyed masks on channels-last (B, T, C):
-// keep iff noise_uniform(key, (sid*C + c)*4096 + t) >= p, scaled by 1/(1-p).  Same kernel for
+// keep iff noise_uniform(key, (sid*C + c)*8192 + t) >= p, scaled by 1/(1-p).  Same kernel for
 // backward (the mask is recomputed).
 __global__ void dropout_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t B, int64_t T, int C,
                                int64_t sid_base, uint32_t key, float p) {
@@ -1103,7 +1103,7 @@ __global__ void dropout_kernel(const float* __restrict__ x, float* __restrict__ 
     const int64_t c = i % C;
     const int64_t t = (i / C) % T;
     const int64_t b = i / ((int64_t)T * C);
-    const uint32_t idx = (uint32_t)(((sid_base + b) * C + c) * 4096 + t);
+    const uint32_t idx = (uint32_t)(((sid_base + b) * C + c) * 8192 + t);
     y[i] = noise_uniform(key, idx) >= p ? x[i] * sc : 0.f;
   }
 }
@@ -1139,7 +1139,7 @@ __global__ void act_dropout4_kernel(const float4* __restrict__ g, const float4* 
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
     const uint32_t row = i / C4, c0 = (i - row * C4) * 4u;
     const uint32_t t = row % T, b = row / T;
-    const uint32_t base = ((sid_base + b) * C + c0) * 4096u + t;
+    const uint32_t base = ((sid_base + b) * C + c0) * 8192u + t;
     const float4 v = z[i];
     float r[4] = {v.x, v.y, v.z, v.w};
     float gg[4] = {0.f, 0.f, 0.f, 0.f};
@@ -1149,7 +1149,7 @@ __global__ void act_dropout4_kernel(const float4* __restrict__ g, const float4* 
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const bool keep = noise_uniform(key, base + (uint32_t)j * 4096u) >= p;
+      const bool keep = noise_uniform(key, base + (uint32_t)j * 8192u) >= p;
       if (BWD) {
         float gj = gg[j];
         if (act2 != ACT_NONE) gj = gj * act_grad(act2, keep ? apply_act(act, r[j]) * sc : 0.f);

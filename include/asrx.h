@@ -40,6 +40,10 @@ int asrx_mel_frames(int64_t n_samples); /* 1 + N/160 (host) */
 int asrx_logmel(const float* wav, int64_t B, int64_t N, int64_t ld_wav, const float* consts,
                 const float* fbw, const int* fbs, float* out, int layout, int64_t ld_out,
                 int* clip_max_ws, float* pool, int64_t T_pool, asrx_stream_t stream);
+/* waveform feature for any clip length: adaptive_avg_pool1d(audio, T) (essentials.py:493-510), bin i the
+ * mean of samples [floor(i N / T), ceil((i + 1) N / T)); wav (B, N) at row stride ld_wav, out (B, T). */
+int asrx_wave_pool(const float* wav, int64_t B, int64_t N, int64_t ld_wav, int64_t T, float* out,
+                   asrx_stream_t stream);
 
 /* ---- audio IO: load_wave's soundfile.read + peak normalisation,
  *      essentials.py:301-319, for the prepare_datasets path (998-1026). -------------------------

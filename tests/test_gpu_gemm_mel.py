@@ -319,3 +319,24 @@ def test_wgrad_bf16_register_staged(cuda, R, M, N, ld_extra):
     ref = w0.double() + _bf(dy).t() @ _bf(x)
     err = float((out.cpu().double() - ref).abs().max() / (_bf(dy).t().abs() @ _bf(x).abs()).max())
     assert err < 1e-5, err
+
+
+@pytest.mark.parametrize("n", [12345, 16001, 480077, 160 * 3000])
+def test_wave_pool_any_length(cuda, n):
+    """asrx_wave_pool (adaptive_avg_pool1d to int(N/160) bins for any N, essentials.py:493-510) against
+    the float64 oracle, and equal to the fused pool of the log-mel pass when 160 | N."""
+    import numpy as np
+
+    from asrx import mel
+    from oracle import mel as omel
+
+    g = torch.Generator().manual_seed(n)
+    x = torch.randn(2, n, generator=g)
+    T = n // 160
+    got = mel.wave_pool(x.to(cuda), T).cpu()
+    for b in range(2):
+        ref = torch.from_numpy(omel.waveform_feature(x[b].numpy().astype(np.float64))[0])
+        assert float((got[b].double() - ref).abs().max()) < 1e-6
+    if n % 160 == 0:
+        _, fused = mel.logmel(x.to(cuda), layout="BMF", pool=True)
+        assert float((fused.cpu() - got).abs().max()) < 1e-6

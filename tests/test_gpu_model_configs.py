@@ -103,6 +103,7 @@ def test_decision_agreement_and_replayed_gradients(cuda, name, precision):
     assert r["replayed"] > 0
     assert not r["grads_missing"], r["grads_missing"]
     assert r["grads_all_max"] < REPLAY_GRAD_TOL[precision], (r["grads_all_max"], r["grads_all_worst"])
+    assert r["zero_grad_residue"] < (1e-5 if precision == "fp32" else 1e-3), r["zero_grad_residue"]
 
 
 def test_hip_mel_end_to_end(cuda):

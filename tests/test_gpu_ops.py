@@ -545,7 +545,7 @@ def test_attention_fp8_mode_forward_only(cuda):
                                                      (1, 33, 8, 5, "none", "none"), (2, 50, 384, 3, "gelu", "gelu")])
 def test_act_dropout_fused(cuda, B, T, C, sid_base, act, act2):
     """Fused act + dropout (encoder layer tail) and the float4 dropout: masks equal the oracle's keyed
-    mask (keep iff uniform(key, (sid*C + c)*4096 + t) >= p, oracle/keys.py), forward/backward
+    mask (keep iff uniform(key, (sid*C + c)*8192 + t) >= p, oracle/keys.py), forward/backward
     bit-identical to Act then Dropout."""
     import numpy as np
 
@@ -567,7 +567,7 @@ def test_act_dropout_fused(cuda, B, T, C, sid_base, act, act2):
     if act2 != "none":
         return
     b, t, c = np.meshgrid(np.arange(B), np.arange(T), np.arange(C), indexing="ij")
-    idx = (((sid_base + b) * C + c) * 4096 + t).astype(np.uint64) & 0xFFFFFFFF
+    idx = (((sid_base + b) * C + c) * 8192 + t).astype(np.uint64) & 0xFFFFFFFF
     keep = torch.from_numpy(np.asarray(onoise.uniform(key, idx.ravel())).reshape(B, T, C) >= p)
     assert torch.equal((y.detach().cpu() != 0), keep & (z.detach().cpu() != 0))
 

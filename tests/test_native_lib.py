@@ -93,14 +93,14 @@ def test_attention_mode_switch():
 
 
 def test_keyed_noise_index_guards():
-    """Sequences past 4096 positions (or streams x channels past the 32-bit index) would alias keyed
+    """Sequences past 8192 positions (or streams x channels past the 32-bit index) would alias keyed
     noise draws: refused before any kernel runs."""
     import pytest
 
     from asrx import ops
 
     ops._noise_rows_ok(96, 1024, 3001)  # tiny/medium 30 s, B = 32 x 3 streams: fine
-    with pytest.raises(ValueError, match="4096"):
-        ops._noise_rows_ok(2, 384, 4097)
+    with pytest.raises(ValueError, match="8192"):
+        ops._noise_rows_ok(2, 384, 8193)
     with pytest.raises(ValueError, match="32-bit"):
         ops._noise_rows_ok(2000, 1024, 3001)
