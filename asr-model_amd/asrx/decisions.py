@@ -13,6 +13,7 @@ replay the HIP decisions inside the oracle (oracle/model.py Decisions).
 
 Entries (all CPU tensors):
   ("abby", key, sid)          -> int64 (L, H) mode index per position (and head)
+  ("cond", key, sid)          -> bool (L, H, d) mode 2's max-vs-avg choice per feature (rows in mode 2)
   ("ion", key, sid, layer)    -> float (L,) v_gate output of a sample at that MSheath layer
   ("action", key, sid, layer) -> (action, forced) of a sample at that layer
 where key is the noise site key of the AbbyNormal call / of the MSheath call ("<site>.jump").
@@ -37,13 +38,18 @@ def active() -> bool:
     return _REC is not None
 
 
-def abby(key: int, sid_base: int, L: int, H: int, idx):
-    """idx: the kernel's (rows,) int32 mode index, rows ordered (sample, position, head)."""
+def abby(key: int, sid_base: int, L: int, H: int, idx, cond=None):
+    """idx: the kernel's (rows,) int32 mode index, rows ordered (sample, position, head); cond: (rows, d)
+    uint8, mode 2's per-feature choice max > 2 avg (essentials.py:176-177) for the rows that picked mode 2
+    (zero elsewhere) -- a discrete choice too, flipped by rounding when max is within ~1e-7 of 2 avg."""
     if _REC is None:
         return
     a = idx.detach().to("cpu").long().view(-1, L, H)
+    c = cond.detach().to("cpu").bool().view(a.shape[0], L, H, -1) if cond is not None else None
     for s in range(a.shape[0]):
         _REC[("abby", int(key), sid_base + s)] = a[s].clone()
+        if c is not None:
+            _REC[("cond", int(key), sid_base + s)] = c[s].clone()
 
 
 def msheath_layer(key: int, sid_base: int, layer: int, ion, rec_f32):

@@ -268,6 +268,17 @@ def _wgrad(A, lda, x2, out, M, K, rows):
     bf16-stored)."""
     tiles = ((M + 127) // 128) * ((K + 127) // 128)
     sk = _splitk_for(rows, tiles)
+    if is_bf16(A):
+        # a bf16-stored dY (the tied logits' gradient from the fused cross entropy): both operands bf16
+        if M % 8 or K % 8 or lda % 8 or x2.stride(0) != K or not is_bf16(x2):
+            A = A.float()
+        else:
+            lib.require_gpu(A, x2, out)
+            e0 = probe.begin("gemm")
+            lib.call("asrx_wgrad_bf16_ab", lib.ptr(A), lda, lib.ptr(x2), K, lib.ptr(out), out.stride(0), M, K, rows,
+                     sk, lib.stream())
+            probe.end("gemm", e0, 2.0 * M * K * rows, ("wgrad", M, K, rows, sk, 2))
+            return out
     if is_bf16(x2):
         # a bf16-stored activation: the register-staged bf16 kernel at every shape (its X bytes halve)
         if M % 4 or K % 8 or lda % 4 or x2.stride(0) != K or A.data_ptr() % 16:

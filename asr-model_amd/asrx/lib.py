@@ -164,6 +164,11 @@ SIGNATURES = {
     "asrx_wave_pool": (_i32, [_p, _i64, _i64, _i64, _i64, _p, _p]),
     "asrx_maxfactor_param_bytes": (_i32, []),
     "asrx_maxfactor_step": (_i32, [_p, _i32, _i64, _i64, _i64, _i64, _i64, _p, _p]),
+    "asrx_abby_record_cond": (_i32, [_p]),
+    "asrx_gemm_wn_ce": (_i32, [_p, _i64, _p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i32, _p]),
+    "asrx_ce_part_fwd": (_i32, [_p, _i64] + [_p] * 6 + [_i64, _i64, _p]),
+    "asrx_ce_bwd_bf16": (_i32, [_p] * 6 + [_i64, _i64, _p]),
+    "asrx_wgrad_bf16_ab": (_i32, [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _p]),
 }
 
 _lib = None

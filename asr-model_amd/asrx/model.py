@@ -176,15 +176,15 @@ class AudioEncoder(nn.Module):
                 act_fn,
                 nn.Conv1d(dims, dims, kernel_size=3, stride=1, padding=1, groups=dims), act_fn, nn.Dropout(0.1)))
 
-    def stem(self, x):
+    def stem(self, x, out=None):
         """(B, C, T) -> (B, T, D): Conv1d(mels, D, 3) for C > 1, Conv1d(1, D, 3) otherwise (model.py:150-155)."""
         if x.dim() == 2:
             x = x.unsqueeze(0)
         B, C, T = x.shape
         if C > 1:
             xt = x.transpose(1, 2).contiguous()
-            return ops.conv3(xt, self.conv1[0])
-        return ops.Stem1.apply(x.reshape(B, T), self.conv2[0].weight, self.conv2[0].bias)
+            return ops.conv3(xt, self.conv1[0], out=out)
+        return ops.Stem1.apply(x.reshape(B, T), self.conv2[0].weight, self.conv2[0].bias, out)
 
     def layers(self, x, noise: NoiseCtx, sid_base: int):
         n = len(self.encoder)
@@ -209,14 +209,25 @@ class AudioEncoder(nn.Module):
     def encode(self, streams, noise: NoiseCtx, B: int):
         """streams: list of 3 (B, C, T) tensors (a, b, c).  Returns 3 (B, T, D) encodings; streams
         of equal length share one batched pass (sample ids stay s*B + b)."""
-        stems = [self.stem(s) for s in streams]
-        out = [None] * len(stems)
+        # runs of consecutive equal-length streams share one pass: their stems write straight into the
+        # row blocks of one group buffer (no concatenation copy)
+        lens = [s.shape[-1] for s in streams]
+        out = [None] * len(streams)
         i = 0
-        while i < len(stems):
+        while i < len(streams):
             j = i + 1
-            while j < len(stems) and stems[j].shape[1] == stems[i].shape[1]:
+            while j < len(streams) and lens[j] == lens[i]:
                 j += 1
-            x = stems[i] if j == i + 1 else torch.cat(stems[i:j], 0)
+            if j == i + 1:
+                x = self.stem(streams[i])
+            else:
+                Bs = [s.shape[0] if s.dim() == 3 else 1 for s in streams[i:j]]
+                buf = torch.empty(sum(Bs), lens[i], self.conv1[0].weight.shape[0], device=streams[i].device)
+                parts, r0 = [], 0
+                for s, b in zip(streams[i:j], Bs):
+                    parts.append(self.stem(s, out=buf[r0:r0 + b]))
+                    r0 += b
+                x = ops.join_group(buf, parts)
             y = self.layers(x, noise, i * B)
             out[i:j] = ops.split_rows(y, j - i)
             i = j
@@ -283,7 +294,13 @@ class attention(nn.Module):  # noqa: N801
         if kv is None:
             kv = self.project_kv(x, noise, site, sid_base, masked)
         q = self.project_q(x, noise, site, sid_base, masked)
-        o = ops.attention(q, kv[0], kv[1], masked, out_bf16=True, merge_heads=True)
+        # o feeds only the out projection, which rounds it to bf16 anyway -- but when a backward runs,
+        # the attention backward's Delta = rowsum(dO * o) needs o at fp32: dS = P (dP - Delta) subtracts
+        # two nearly equal terms when the values barely vary over the keys, and a bf16 o turned that
+        # cancellation into errors of several times the largest parameter gradient (tools/
+        # debug_storage_grad.py).  So o is stored bf16 only without a backward (dead blocks, eval).
+        o = ops.attention(q, kv[0], kv[1], masked, out_bf16=not ops._grad_needed(q, kv[0], kv[1]),
+                          merge_heads=True)
         return ops.linear(o, self.out[1].weight, self.out[1].bias)  # o: (B, L, D), heads merged
 
 
@@ -472,7 +489,9 @@ class processor(nn.Module):  # noqa: N801  (model.py:585-629)
         self.concurrent_dead_text = True
         self._side = None
 
-    def forward(self, x, xa, noise: NoiseCtx, seq=False):
+    def forward(self, x, xa, noise: NoiseCtx, seq=False, features=False):
+        """features: return the final norm's output instead of the tied logits (Model.forward then runs
+        the logits fused with the cross entropy, ops.logits_ce)."""
         B, T = x.shape
         xe = ops.Embedding.apply(x, self.token.weight)
         x = ops.add_rows(xe, self.position)
@@ -516,6 +535,8 @@ class processor(nn.Module):  # noqa: N801  (model.py:585-629)
         else:
             out = ops.blend(d, g, self.blend)  # sigmoid(blend) d + (1 - sigmoid(blend)) g
         out = self.ln.run(out, noise, "final.ln", 0, T, out_bf16=True)
+        if features:
+            return out
         return ops.linear(out, self.token.weight)
 
     # ---- decoding (Model.generate): the y-independent audio side of the only live block, once
@@ -595,6 +616,9 @@ class Model(nn.Module):
         self.layer = sum(1 for name, _ in self.named_modules() if name != "")
         self.noise_seed = 0
         self.noise_step = 0
+        # perf mode: the tied logits and the cross entropy run fused (ops.LogitsCE: logits stored bf16,
+        # the loss from the GEMM's per-tile statistics); False: logits GEMM then ops.CrossEntropy
+        self.fused_ce = True
 
     def set_noise(self, seed: int, step: int):
         self.noise_seed, self.noise_step = int(seed), int(step)
@@ -624,7 +648,15 @@ class Model(nn.Module):
         if self.training:
             self.noise_step += 1
         enc = self.enc.encode(streams, noise, B)
-        logits = self.processor(text_ids, {"a": enc[0], "b": enc[1], "c": enc[2]}, noise, seq=False)
+        xa = {"a": enc[0], "b": enc[1], "c": enc[2]}
+        if labels is not None and self.fused_ce:
+            h = self.processor(text_ids, xa, noise, seq=False, features=True)
+            if ops.logits_ce_ok(h, self.processor.token.weight):
+                logits, loss = ops.logits_ce(h, self.processor.token.weight, labels)
+                return {"logits": logits, "loss": loss}
+            logits = ops.linear(h, self.processor.token.weight)
+        else:
+            logits = self.processor(text_ids, xa, noise, seq=False)
         loss = None
         if labels is not None:
             loss = ops.CrossEntropy.apply(logits, labels)

@@ -440,6 +440,10 @@ class AbbyNormalFn(torch.autograd.Function):
         tc = _E(rows, 3, device=x.device) if tw is not None else None
         if side is not None:
             side["tgate_c"] = tc
+        cond = None
+        if decisions.active():  # record mode 2's per-feature max-vs-avg choices of this call
+            cond = torch.zeros(rows, d, dtype=torch.uint8, device=x.device)
+            lib.call("asrx_abby_record_cond", _P(cond))
         if G.use_wide(d) and d <= 384:
             # perf mode: the router's d x d GEMM also applies SiLU and Linear(d, 3) in its epilogue,
             # so h_pre never makes the HBM round trip unless the backward needs it
@@ -450,8 +454,9 @@ class AbbyNormalFn(torch.autograd.Function):
             hpre = G.linear_fwd(x, W1, b1)
             lib.call("asrx_abby_fwd2", _P(x), _P(hpre), _P(W2), _P(b2), _P(out), ob, _P(ys), _P(idx), rows, d, L, H,
                      sid_base, key & 0xFFFFFFFF, int(use_noise), _P(tw), _P(tb), _P(tc), _S())
-        if decisions.active():
-            decisions.abby(key & 0xFFFFFFFF, sid_base, L, H, idx)
+        if cond is not None:
+            lib.call("asrx_abby_record_cond", None)
+            decisions.abby(key & 0xFFFFFFFF, sid_base, L, H, idx, cond)
         ctx.dp = [_direct(ctx, i, t) for i, t in ((1, W1), (2, b1), (3, W2), (4, b2))]
         ctx.save_for_backward(x, hpre, W1, W2, ys, idx, b1, b2)
         return out
@@ -1279,7 +1284,7 @@ class Conv3(torch.autograd.Function):
     goes back through the weight norm into g.grad / v.grad (asrx_conv3_weight_bwd)."""
 
     @staticmethod
-    def forward(ctx, x, g, v, b):
+    def forward(ctx, x, g, v, b, out=None):
         x = _c(x)
         B, T, Ci = x.shape
         Co = v.shape[0]
@@ -1289,7 +1294,7 @@ class Conv3(torch.autograd.Function):
         Wt = None if wide else _E(Co, 3 * Ci, device=dev)
         Wtb = _E(Co, 3 * Ci, dtype=torch.int16, device=dev) if wide else None
         lib.call("asrx_conv3_weight", _P(g), _P(_c(v)), Co, Ci, _P(Wt), _P(Wtb), None, None, _P(nrm), _S())
-        y = _E(B, T, Co, device=dev)
+        y = _E(B, T, Co, device=dev) if out is None else out  # out: this stream's rows of a group buffer
         if wide:
             G.gemm_wn(x, Wtb, y, M=B * T, N=Co, K=3 * Ci, lda=Ci, ldc=Co, bias=b, conv=True, conv_F=T, conv_C=Ci)
         else:
@@ -1338,28 +1343,66 @@ class Conv3(torch.autograd.Function):
             dgo = _gret(g, gg, ctx.dg) if ctx.has_g else None
         if ctx.needs_input_grad[3]:
             dbo = _gret(b, colsum(gy.view(-1, Co), out=_gbuf(b, True) if ctx.db else None), ctx.db)
-        return dx, dgo, dvo, dbo
+        return dx, dgo, dvo, dbo, None
 
 
-def conv3(x, conv):
+def conv3(x, conv, out=None):
     """Conv1d(k=3, padding=1) module on channels-last x; weight_norm-parametrized modules read their
-    g (original0) and v (original1) directly, so torch's parametrization kernels never run."""
+    g (original0) and v (original1) directly, so torch's parametrization kernels never run.  out: write
+    into these rows of a stream-group buffer (see join_group)."""
     pz = getattr(conv, "parametrizations", None)
     if pz is not None and "weight" in pz:
         orig = pz.weight
-        return Conv3.apply(x, orig.original0, orig.original1, conv.bias)
-    return Conv3.apply(x, None, conv.weight, conv.bias)
+        return Conv3.apply(x, orig.original0, orig.original1, conv.bias, out)
+    return Conv3.apply(x, None, conv.weight, conv.bias, out)
+
+
+class _Holder:
+    __slots__ = ("buf",)
+
+    def __init__(self, buf):
+        self.buf = buf
+
+
+class JoinGroup(torch.autograd.Function):
+    """The stream-group buffer whose row blocks the parts were written into (the encoder stems of the
+    equal-length audio streams, AudioEncoder.encode): the group enters the shared encoder pass without a
+    concatenation copy (was torch.cat: 590 MB of HBM traffic per step at the tiny config); the
+    backward hands each part its rows of the group gradient (views, no copy)."""
+
+    @staticmethod
+    def forward(ctx, holder, *parts):
+        ctx.set_materialize_grads(False)
+        ctx.n, ctx.B = len(parts), parts[0].shape[0]
+        return holder.buf
+
+    @staticmethod
+    def backward(ctx, g):
+        if g is None:
+            return (None,) * (ctx.n + 1)
+        B = ctx.B
+        return (None,) + tuple(g[i * B:(i + 1) * B] for i in range(ctx.n))
+
+
+def join_group(buf, parts):
+    """buf (n B, ...) whose row blocks are exactly `parts` (written in place by their producers)."""
+    for i, t in enumerate(parts):
+        B = t.shape[0]
+        assert t.data_ptr() == buf[i * B].data_ptr() and t.shape[1:] == buf.shape[1:], "parts must be buf's rows"
+    if not (torch.is_grad_enabled() and any(t.requires_grad for t in parts)):
+        return buf
+    return JoinGroup.apply(_Holder(buf), *parts)
 
 
 class Stem1(torch.autograd.Function):
     """Conv1d(1, D, 3, padding=1) (model.py:133) on (B, T) single-channel streams -> (B, T, D)."""
 
     @staticmethod
-    def forward(ctx, x, W, b):
+    def forward(ctx, x, W, b, out=None):
         x = _c(x)
         B, T = x.shape
         D = W.shape[0]
-        y = _E(B, T, D, device=x.device)
+        y = _E(B, T, D, device=x.device) if out is None else out  # out: rows of a stream-group buffer
         lib.call("asrx_stem1_fwd", _P(x), _P(W), _P(b), _P(y), B, T, D, _S())
         ctx.dW, ctx.db = _direct(ctx, 1, W), _direct(ctx, 2, b)
         ctx.save_for_backward(x, W, b)
@@ -1372,7 +1415,7 @@ class Stem1(torch.autograd.Function):
         D = W.shape[0]
         dW, db = _gbuf(W, ctx.dW), _gbuf(b, ctx.db)
         lib.call("asrx_stem1_bwd", _P(_c(g)), _P(x), _P(dW), _P(db), B, T, D, _S())
-        return None, _gret(W, dW, ctx.dW), _gret(b, db, ctx.db)
+        return None, _gret(W, dW, ctx.dW), _gret(b, db, ctx.db), None
 
 
 class Embedding(torch.autograd.Function):
@@ -1421,6 +1464,79 @@ class CrossEntropy(torch.autograd.Function):
         dz = _E(z.shape, device=z.device)
         lib.call("asrx_ce_bwd2", _P(z), _P(lab), _P(lse), _P(g), _P(count), _P(dz), _rows(z), z.shape[-1], _S())
         return dz, None
+
+
+class LogitsCE(torch.autograd.Function):
+    """Tied logits + F.cross_entropy(logits, labels, ignore_index=0) fused (perf mode with bf16 storage;
+    model.py:629 logits = x @ token.weight^T, model.py:670 the loss).  One GEMM writes the logits bf16
+    (as autocast's bf16 Linear does) and, per row and column tile, the (max, sum exp) of the bf16
+    logits; a per-row merge gives the log-sum-exp and the loss, reading only the label's logit.  The
+    backward writes dz = (g/count)(softmax - onehot) bf16 from the bf16 logits and feeds it to the
+    input-gradient GEMM and the embedding's weight-gradient GEMM.  The logits stay an output with a
+    gradient path (a gradient arriving for them is added to dz)."""
+
+    @staticmethod
+    def forward(ctx, h, W, labels, sink):
+        h = _c(h)
+        ctx.set_materialize_grads(False)
+        ctx.sink = sink
+        rows, D = _rows(h), h.shape[-1]
+        V = W.shape[0]
+        nj = G._nj(rows, V)
+        nparts = (V + 128 * nj - 1) // (128 * nj)
+        zb = _E(*h.shape[:-1], V, dtype=torch.bfloat16, device=h.device)
+        part = _E(rows, nparts, 2, device=h.device)
+        Wb = G.weight_bf16(W)
+        lib.require_gpu(h, Wb, zb)
+        e0 = probe.begin("gemm")
+        lib.call("asrx_gemm_wn_ce", _P(h), D, _P(Wb), Wb.stride(0), _P(zb), V, _P(part), rows, V, D, nj, _S())
+        probe.end("gemm", e0, 2.0 * rows * V * D, ("wn", rows, V, D, nj, 0, "none", False, False, 1, 1, False))
+        lab = _c(labels.reshape(-1))
+        loss_r = _E(rows, device=h.device)
+        lse = _E(rows, device=h.device)
+        loss = _E((), device=h.device)
+        count = _E(1, device=h.device)
+        lib.call("asrx_ce_part_fwd", _P(part), nparts, _P(zb), _P(lab), _P(loss_r), _P(lse), _P(loss), _P(count),
+                 rows, V, _S())
+        ctx.dW = _direct(ctx, 1, W)
+        ctx.save_for_backward(h, W, zb, lab, lse, count)
+        return zb, loss
+
+    @staticmethod
+    def backward(ctx, g_logits, g_loss):
+        h, W, zb, lab, lse, count = ctx.saved_tensors
+        rows, V = _rows(zb), zb.shape[-1]
+        if g_loss is None:
+            g_loss = torch.zeros(1, device=zb.device)
+        g_loss = _c(g_loss.reshape(1).float())
+        dz = _E(zb.shape, dtype=torch.bfloat16, device=zb.device)
+        lib.call("asrx_ce_bwd_bf16", _P(zb), _P(lab), _P(lse), _P(g_loss), _P(count), _P(dz), rows, V, _S())
+        if g_logits is not None:  # a gradient for the logits themselves (not the training path)
+            dz = dz.float() + g_logits.float()
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if ctx.sink is not None:
+                buf, acc = ctx.sink.target(h)
+                G.linear_dgrad(dz, W, out=buf, beta=float(acc))
+            else:
+                dx = G.linear_dgrad(dz, W)
+        dW = None
+        if ctx.needs_input_grad[1]:
+            gW = _gbuf(W, ctx.dW)
+            G.linear_wgrad(dz, h, out=gW, accumulate=True)
+            dW = _gret(W, gW, ctx.dW)
+        return dx, dW, None, None
+
+
+def logits_ce_ok(h, W) -> bool:
+    """The fused tied-logits + cross entropy applies: perf mode with the final norm stored bf16."""
+    return (h.dtype == torch.bfloat16 and W.dim() == 2 and W.shape[0] % 8 == 0 and h.shape[-1] % 8 == 0
+            and prec.get() == prec.PREC_BF16)
+
+
+def logits_ce(h, W, labels):
+    """(logits bf16, loss) = (h W^T, F.cross_entropy(., labels, ignore_index=0)) through LogitsCE."""
+    return LogitsCE.apply(h, W, labels, sink_of(h))
 
 
 class BlendFn(torch.autograd.Function):

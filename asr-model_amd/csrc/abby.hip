@@ -30,6 +30,9 @@ struct AbbyGeom {
   uint32_t key;
   int use_noise;
   int acc;  // backward: dx += (one buffer collects every consumer's gradient of x)
+  // decision recorder (parity tests only, null otherwise): the forward writes mode 2's per-feature
+  // choice (max > 2 avg, essentials.py:176-177) of every row that picked mode 2, cond[r * d + f]
+  unsigned char* cond;
 };
 
 // Per-row layout (MI355X design): lane l owns the E = d/64 CONSECUTIVE features [l E, l E + E), read
@@ -240,19 +243,35 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_fwd_kernel(const float* 
   }
   const int64_t stride = (int64_t)gridDim.x * ABBY_WAVES;
   int64_t r = (int64_t)blockIdx.x * ABBY_WAVES + wid;
-  float xn[E];  // next row's x (coalesced layout), loaded while this row is processed
-  if (r < g.rows) ld_rowc<E>(x + r * S::D, lane, xn);
+  // the next TWO rows' x (coalesced layout) and router logits are in flight while this row is
+  // processed: one row of prefetch left the kernel latency-bound at ~2.5 TB/s (1.5 KB per wave in
+  // flight); loads past the end re-read the last row (unconditional, so the wait counts stay uniform)
+  float xn1[E], xn2[E], ln1[3] = {0.f, 0.f, 0.f}, ln2[3] = {0.f, 0.f, 0.f};
+  auto fetch = [&](int64_t rr, float (&xb)[E], float (&lb)[3]) __attribute__((always_inline)) {
+    const int64_t rc = rr < g.rows ? rr : g.rows - 1;
+    ld_rowc<E>(x + rc * S::D, lane, xb);
+    if (logits) {
+      lb[0] = logits[rc * 3 + 0];
+      lb[1] = logits[rc * 3 + 1];
+      lb[2] = logits[rc * 3 + 2];
+    }
+  };
+  if (r < g.rows) {
+    fetch(r, xn1, ln1);
+    fetch(r + stride, xn2, ln2);
+  }
   for (; r < g.rows; r += stride) {
     float xv[E];
+    float l0 = ln1[0], l1 = ln1[1], l2 = ln1[2];
 #pragma unroll
-    for (int e = 0; e < E; ++e) xv[e] = xn[e];
-    if (r + stride < g.rows) ld_rowc<E>(x + (r + stride) * S::D, lane, xn);
-    float l0, l1, l2;
-    if (logits) {  // router logits from the GEMM epilogue (asrx_gemm_wn_router)
-      l0 = logits[r * 3 + 0];
-      l1 = logits[r * 3 + 1];
-      l2 = logits[r * 3 + 2];
-    } else {
+    for (int e = 0; e < E; ++e) {
+      xv[e] = xn1[e];
+      xn1[e] = xn2[e];
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) ln1[k] = ln2[k];
+    fetch(r + 2 * stride, xn2, ln2);
+    if (!logits) {
       float hv[E];
       ld_rowc<E>(hpre + r * S::D, lane, hv);
       l0 = l1 = l2 = 0.f;
@@ -310,6 +329,10 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_fwd_kernel(const float* 
       float mx[E];
       int am[E];
       abby_wmax<E, false>(h, mx, am);
+      if (g.cond) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) g.cond[r * S::D + lane * E + e] = mx[e] > 2.0f * avg[e] ? 1 : 0;
+      }
 #pragma unroll
       for (int e = 0; e < E; ++e) avg[e] = mx[e] > 2.0f * avg[e] ? mx[e] : avg[e];
     }
@@ -380,24 +403,33 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_bwd_kernel(
 
   const int64_t stride = (int64_t)gridDim.x * ABBY_WAVES;
   int64_t r = (int64_t)blockIdx.x * ABBY_WAVES + wid;
-  float xn[E], gn[E];  // next row's x and dout (coalesced layout), loaded while this row is processed
+  // x and dout of the next TWO rows (coalesced layout) are in flight while this row is processed
+  // (one row ahead left the kernel latency-bound); past the end the last row is re-read
+  float xn1[E], gn1[E], xn2[E], gn2[E];
+  auto fetch = [&](int64_t rr, float (&xb)[E], float (&gb)[E]) __attribute__((always_inline)) {
+    const int64_t rc = rr < g.rows ? rr : g.rows - 1;
+    ld_rowc<E>(x + rc * S::D, lane, xb);
+    ld_rowc<E>(dout + rc * S::D, lane, gb);
+  };
   if (r < g.rows) {
-    ld_rowc<E>(x + r * S::D, lane, xn);
-    ld_rowc<E>(dout + r * S::D, lane, gn);
+    fetch(r, xn1, gn1);
+    fetch(r + stride, xn2, gn2);
   }
   for (; r < g.rows; r += stride) {
     float xc[E], xv[E], gv[E];  // xc: coalesced layout; xv, gv: the lane's E consecutive features
 #pragma unroll
     for (int j = 0; j < E / 2; ++j) {
-      xc[2 * j] = xn[2 * j];
-      xc[2 * j + 1] = xn[2 * j + 1];
-      *reinterpret_cast<float2*>(xr + 128 * j + 2 * lane) = make_float2(xn[2 * j], xn[2 * j + 1]);
-      *reinterpret_cast<float2*>(gr + 128 * j + 2 * lane) = make_float2(gn[2 * j], gn[2 * j + 1]);
+      xc[2 * j] = xn1[2 * j];
+      xc[2 * j + 1] = xn1[2 * j + 1];
+      *reinterpret_cast<float2*>(xr + 128 * j + 2 * lane) = make_float2(xn1[2 * j], xn1[2 * j + 1]);
+      *reinterpret_cast<float2*>(gr + 128 * j + 2 * lane) = make_float2(gn1[2 * j], gn1[2 * j + 1]);
     }
-    if (r + stride < g.rows) {
-      ld_rowc<E>(x + (r + stride) * S::D, lane, xn);
-      ld_rowc<E>(dout + (r + stride) * S::D, lane, gn);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      xn1[e] = xn2[e];
+      gn1[e] = gn2[e];
     }
+    fetch(r + 2 * stride, xn2, gn2);
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
 #pragma unroll
@@ -714,6 +746,7 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_fwd64_kernel(const float
       const float avg = (fmaxf(h[e], 0.f) + h[e + 1] + fmaxf(h[e + 2], 0.f)) * (1.0f / 3.0f);
       const float mx = fmaxf(h[e], fmaxf(h[e + 1], h[e + 2]));
       const float div = (sel == 1 && mx > 2.0f * avg) ? mx : avg;
+      if (g.cond && sel == 1) g.cond[r * 64 + 4 * l16 + e] = mx > 2.0f * avg ? 1 : 0;
       float base;
       ov[e] = xv[e] / abby_denom(div, base);
     }
@@ -874,9 +907,13 @@ using namespace asrx;
     default: set_error("AbbyNormal: unsupported d=%ld", (long)d); return 2;        \
   }
 
+// host-side decision recorder target (asrx_abby_record_cond; parity tests, eager only)
+static unsigned char* g_cond_record = nullptr;
+
 static AbbyGeom make_geom(int64_t rows, int64_t d, int64_t L, int64_t H, int64_t sid_base, uint32_t key,
                           int use_noise) {
   AbbyGeom g;
+  g.cond = nullptr;
   g.rows = rows;
   g.d = d;
   g.L = L > 0 ? L : 1;
@@ -900,6 +937,7 @@ extern "C" int asrx_abby_fwd2(const float* x, const float* hpre, const float* W2
   if (rows == 0) return 0;
   const int E = (int)(d / 64);
   AbbyGeom g = make_geom(rows, d, L, H, sid_base, key, use_noise);
+  g.cond = g_cond_record;
   const unsigned grid = (unsigned)std::min<int64_t>((rows + ABBY_WAVES - 1) / ABBY_WAVES, 4096);
   if (d == 64) {
     const unsigned g64 = (unsigned)std::min<int64_t>((rows + 4 * ABBY_WAVES - 1) / (4 * ABBY_WAVES), 4096);
@@ -938,6 +976,7 @@ extern "C" int asrx_abby_fwd_logits2(const float* x, const float* logits, const 
   if (rows == 0) return 0;
   const int E = (int)(d / 64);
   AbbyGeom g = make_geom(rows, d, L, H, sid_base, key, use_noise);
+  g.cond = g_cond_record;
   const unsigned grid = (unsigned)std::min<int64_t>((rows + ABBY_WAVES - 1) / ABBY_WAVES, 4096);
   if (d == 64) {
     const unsigned g64 = (unsigned)std::min<int64_t>((rows + 4 * ABBY_WAVES - 1) / (4 * ABBY_WAVES), 4096);
@@ -990,6 +1029,14 @@ extern "C" int asrx_abby_bwd(const float* dout, const float* x, const float* hpr
                              const float* ys, const int* idx, float* dx, float* dhpre, float* dW2, float* db2,
                              int64_t rows, int64_t d, hipStream_t stream) {
   return asrx_abby_bwd2(dout, x, hpre, W2, ys, idx, dx, dhpre, dW2, db2, rows, d, 0, stream);
+}
+
+// Decision recorder for the parity tests: while buf != NULL, every AbbyNormal forward writes mode 2's
+// per-feature max-vs-avg choice of its rows that picked mode 2 into buf (rows x d bytes, caller-zeroed,
+// large enough for the next call); NULL turns it off.  Not for graph capture.
+extern "C" int asrx_abby_record_cond(unsigned char* buf) {
+  g_cond_record = buf;
+  return 0;
 }
 
 ASRX_NOISE_EPOCH_SETTER(asrx_set_noise_epoch_abby)

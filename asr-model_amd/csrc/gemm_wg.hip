@@ -39,65 +39,87 @@ struct Params {
 __device__ __forceinline__ int off(int row, int ch) { return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3))); }
 
 // BBF: X stored bf16 (an activation whose only consumers are GEMM operands): 16-byte loads of 8
-// features, rows (t >> 4) + 16 i, already in the image's element type
-template <bool BBF>
+// features, rows (t >> 4) + 16 i, already in the image's element type.  ABF: dY stored bf16 the same
+// way (the tied-logits gradient, written bf16 by the fused cross entropy).  The bf16 halves are
+// native vectors (a HIP_vector_type copy can keep a stage in scratch).
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+template <bool ABF, bool BBF>
 struct Stage {
   float4 a[4], b[4];  // rows (t >> 5) + 8 i, features 4 (t & 31) .. +3
 };
 template <>
-struct Stage<true> {
+struct Stage<false, true> {
   float4 a[4];
-  uint4 bh[2];  // rows (t >> 4) + 16 i, features 8 (t & 15) .. +7
+  u32x4 bh[2];  // rows (t >> 4) + 16 i, features 8 (t & 15) .. +7
+};
+template <>
+struct Stage<true, true> {
+  u32x4 ah[2], bh[2];
 };
 
-template <bool BBF>
-__device__ __forceinline__ void load(const Params& p, Stage<BBF>& st, int64_t r0, int64_t rend, int m0, int n0) {
+template <bool ABF, bool BBF>
+__device__ __forceinline__ void load(const Params& p, Stage<ABF, BBF>& st, int64_t r0, int64_t rend, int m0, int n0) {
   const int t = threadIdx.x;
   const int c = 4 * (t & 31);
+  const int cb = 8 * (t & 15);
   if constexpr (BBF) {
     const unsigned short* Bh = reinterpret_cast<const unsigned short*>(p.B);
-    const int cb = 8 * (t & 15);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int64_t r = r0 + (t >> 4) + 16 * i;
-      st.bh[i] = *reinterpret_cast<const uint4*>((r < rend && n0 + cb < p.N) ? (const void*)(Bh + r * p.ldb + n0 + cb)
+      st.bh[i] = *reinterpret_cast<const u32x4*>((r < rend && n0 + cb < p.N) ? (const void*)(Bh + r * p.ldb + n0 + cb)
                                                                             : (const void*)zero16);
     }
   }
+  if constexpr (ABF) {
+    const unsigned short* Ah = reinterpret_cast<const unsigned short*>(p.A);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int64_t r = r0 + (t >> 5) + 8 * i;
-    const bool okr = r < rend;
-    // unconditional loads from clamped addresses (a branch would make the compiler drain vmcnt)
-    st.a[i] = *reinterpret_cast<const float4*>((okr && m0 + c < p.M) ? (const void*)(p.A + r * p.lda + m0 + c)
-                                                                     : (const void*)zero16);
-    if constexpr (!BBF)
-      st.b[i] = *reinterpret_cast<const float4*>((okr && n0 + c < p.N) ? (const void*)(p.B + r * p.ldb + n0 + c)
+    for (int i = 0; i < 2; ++i) {
+      const int64_t r = r0 + (t >> 4) + 16 * i;
+      st.ah[i] = *reinterpret_cast<const u32x4*>((r < rend && m0 + cb < p.M) ? (const void*)(Ah + r * p.lda + m0 + cb)
+                                                                            : (const void*)zero16);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t r = r0 + (t >> 5) + 8 * i;
+      const bool okr = r < rend;
+      // unconditional loads from clamped addresses (a branch would make the compiler drain vmcnt)
+      st.a[i] = *reinterpret_cast<const float4*>((okr && m0 + c < p.M) ? (const void*)(p.A + r * p.lda + m0 + c)
                                                                        : (const void*)zero16);
+      if constexpr (!BBF)
+        st.b[i] = *reinterpret_cast<const float4*>((okr && n0 + c < p.N) ? (const void*)(p.B + r * p.ldb + n0 + c)
+                                                                         : (const void*)zero16);
+    }
   }
 }
 
-template <bool BBF>
-__device__ __forceinline__ void store(const Stage<BBF>& st, char* Ai, char* Bi) {
+template <bool ABF, bool BBF>
+__device__ __forceinline__ void store(const Stage<ABF, BBF>& st, char* Ai, char* Bi) {
   const int t = threadIdx.x;
   const int c = 4 * (t & 31);
   const int ch = c >> 3, hb = (c >> 2) & 1;
   typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+  if constexpr (ABF) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = (t >> 5) + 8 * i;
-    bf16x4 ha;
-    ha[0] = (__bf16)st.a[i].x; ha[1] = (__bf16)st.a[i].y; ha[2] = (__bf16)st.a[i].z; ha[3] = (__bf16)st.a[i].w;
-    *reinterpret_cast<bf16x4*>(Ai + off(row, ch) + 8 * hb) = ha;
-    if constexpr (!BBF) {
-      bf16x4 hb4;
-      hb4[0] = (__bf16)st.b[i].x; hb4[1] = (__bf16)st.b[i].y; hb4[2] = (__bf16)st.b[i].z; hb4[3] = (__bf16)st.b[i].w;
-      *reinterpret_cast<bf16x4*>(Bi + off(row, ch) + 8 * hb) = hb4;
+    for (int i = 0; i < 2; ++i) *reinterpret_cast<u32x4*>(Ai + off((t >> 4) + 16 * i, t & 15)) = st.ah[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = (t >> 5) + 8 * i;
+      bf16x4 ha;
+      ha[0] = (__bf16)st.a[i].x; ha[1] = (__bf16)st.a[i].y; ha[2] = (__bf16)st.a[i].z; ha[3] = (__bf16)st.a[i].w;
+      *reinterpret_cast<bf16x4*>(Ai + off(row, ch) + 8 * hb) = ha;
+      if constexpr (!BBF) {
+        bf16x4 hb4;
+        hb4[0] = (__bf16)st.b[i].x; hb4[1] = (__bf16)st.b[i].y; hb4[2] = (__bf16)st.b[i].z; hb4[3] = (__bf16)st.b[i].w;
+        *reinterpret_cast<bf16x4*>(Bi + off(row, ch) + 8 * hb) = hb4;
+      }
     }
   }
   if constexpr (BBF) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) *reinterpret_cast<uint4*>(Bi + off((t >> 4) + 16 * i, t & 15)) = st.bh[i];
+    for (int i = 0; i < 2; ++i) *reinterpret_cast<u32x4*>(Bi + off((t >> 4) + 16 * i, t & 15)) = st.bh[i];
   }
 }
 
@@ -120,7 +142,7 @@ __device__ __forceinline__ int xcd_item(int bid, int nblk) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
-template <bool BBF>
+template <bool ABF, bool BBF>
 __global__ __launch_bounds__(NT, 2) void wgrad_wr_kernel(Params p) {
   __shared__ __attribute__((aligned(16))) char Ai[2][TK * TM * 2];
   __shared__ __attribute__((aligned(16))) char Bi[2][TK * TN * 2];
@@ -140,13 +162,13 @@ __global__ __launch_bounds__(NT, 2) void wgrad_wr_kernel(Params p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  Stage<BBF> s0, s1;
+  Stage<ABF, BBF> s0, s1;
   load(p, s0, rb, re, m0, n0);
   load(p, s1, rb + TK, re, m0, n0);
   store(s0, Ai[0], Bi[0]);
   __syncthreads();
 
-  auto kstep = [&](int s, Stage<BBF>& cur, const Stage<BBF>& nxt) __attribute__((always_inline)) {
+  auto kstep = [&](int s, Stage<ABF, BBF>& cur, const Stage<ABF, BBF>& nxt) __attribute__((always_inline)) {
     load(p, cur, rb + (int64_t)(s + 2) * TK, re, m0, n0);  // past the end: zero page, counts stay uniform
     const char* At = Ai[s & 1];
     const char* Bt = Bi[s & 1];
@@ -192,34 +214,44 @@ using namespace asrx;
 // dW (M x N, ldc) += dY^T X over R rows; dY (R x M, lda), X (R x N, ldb) fp32 row-major; the rows
 // split over `splitk` work items (bf16 operands, fp32 accumulate).  M, N, lda, ldb multiples of 4,
 // 16-byte aligned operands.
-static int wgrad_launch(const float* A, int64_t lda, const void* B, int b_bf16, int64_t ldb, float* C, int64_t ldc,
-                        int64_t M, int64_t N, int64_t R, int64_t splitk, hipStream_t stream) {
+static int wgrad_launch(const void* A, int a_bf16, int64_t lda, const void* B, int b_bf16, int64_t ldb, float* C,
+                        int64_t ldc, int64_t M, int64_t N, int64_t R, int64_t splitk, hipStream_t stream) {
   ASRX_REQUIRE(M > 0 && N > 0 && R >= 0, "asrx_wgrad_bf16: empty problem");
   ASRX_REQUIRE(M % 4 == 0 && N % 4 == 0 && lda % 4 == 0 && ldb % 4 == 0, "asrx_wgrad_bf16: M, N, lda, ldb %% 4 required");
   ASRX_REQUIRE(!b_bf16 || (N % 8 == 0 && ldb % 8 == 0), "asrx_wgrad_bf16: a bf16 X needs N, ldb %% 8");
+  ASRX_REQUIRE(!a_bf16 || (b_bf16 && M % 8 == 0 && lda % 8 == 0), "asrx_wgrad_bf16: a bf16 dY needs a bf16 X and M, lda %% 8");
   ASRX_REQUIRE((((uintptr_t)A | (uintptr_t)B) & 15) == 0, "asrx_wgrad_bf16: operands must be 16-byte aligned");
   if (R == 0) return 0;
   if (splitk < 1) splitk = 1;
   int64_t kchunk = (R + splitk - 1) / splitk;
   kchunk = (kchunk + wg::TK - 1) / wg::TK * wg::TK;
   splitk = (R + kchunk - 1) / kchunk;
-  wg::Params p{A, (const float*)B, C, lda, ldb, ldc, (int)M, (int)N, R, kchunk, (int)splitk};
+  wg::Params p{(const float*)A, (const float*)B, C, lda, ldb, ldc, (int)M, (int)N, R, kchunk, (int)splitk};
   const int64_t items = ((M + wg::TM - 1) / wg::TM) * ((N + wg::TN - 1) / wg::TN) * splitk;
   ASRX_REQUIRE(items < (1LL << 31), "asrx_wgrad_bf16: too many work items");
-  if (b_bf16)
-    wg::wgrad_wr_kernel<true><<<(unsigned)items, wg::NT, 0, stream>>>(p);
+  if (a_bf16)
+    wg::wgrad_wr_kernel<true, true><<<(unsigned)items, wg::NT, 0, stream>>>(p);
+  else if (b_bf16)
+    wg::wgrad_wr_kernel<false, true><<<(unsigned)items, wg::NT, 0, stream>>>(p);
   else
-    wg::wgrad_wr_kernel<false><<<(unsigned)items, wg::NT, 0, stream>>>(p);
+    wg::wgrad_wr_kernel<false, false><<<(unsigned)items, wg::NT, 0, stream>>>(p);
   ASRX_LAUNCHED("asrx_wgrad_bf16");
 }
 
 extern "C" int asrx_wgrad_bf16(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
                                int64_t M, int64_t N, int64_t R, int64_t splitk, hipStream_t stream) {
-  return wgrad_launch(A, lda, B, 0, ldb, C, ldc, M, N, R, splitk, stream);
+  return wgrad_launch(A, 0, lda, B, 0, ldb, C, ldc, M, N, R, splitk, stream);
 }
 
 // asrx_wgrad_bf16 with X (B) stored fp32 (b_bf16 = 0) or bf16 (1; N, ldb multiples of 8).
 extern "C" int asrx_wgrad_bf16_ex(const float* A, int64_t lda, const void* B, int b_bf16, int64_t ldb, float* C,
                                   int64_t ldc, int64_t M, int64_t N, int64_t R, int64_t splitk, hipStream_t stream) {
-  return wgrad_launch(A, lda, B, b_bf16, ldb, C, ldc, M, N, R, splitk, stream);
+  return wgrad_launch(A, 0, lda, B, b_bf16, ldb, C, ldc, M, N, R, splitk, stream);
+}
+
+// asrx_wgrad_bf16 with both dY (A) and X (B) stored bf16 (M, N, lda, ldb multiples of 8): the tied
+// token embedding's gradient from the bf16 logits gradient (model.py:629 tied logits).
+extern "C" int asrx_wgrad_bf16_ab(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, int64_t ldc,
+                                  int64_t M, int64_t N, int64_t R, int64_t splitk, hipStream_t stream) {
+  return wgrad_launch(A, 1, lda, B, 1, ldb, C, ldc, M, N, R, splitk, stream);
 }

@@ -134,6 +134,30 @@ extern "C" int asrx_gemm_wn_ex(const void* A, int a_bf16, int64_t lda, int conv,
   ASRX_LAUNCHED("asrx_gemm_wn_ex");
 }
 
+// Tied logits with the cross entropy's statistics fused (model.py:629 logits = x @ token.weight^T,
+// model.py:670 F.cross_entropy): Zb (M x N, ldc) = bf16(A W^T) for a bf16-stored A, and per row and
+// 128*nj-column tile the (max, sum exp(z - max)) of the tile's bf16 logits in part[row * nparts + tile]
+// (float2, nparts = ceil(N / (128 nj))) -- asrx_ce_part_fwd turns them into the loss without re-reading
+// the logits.
+extern "C" int asrx_gemm_wn_ce(const void* A, int64_t lda, const unsigned short* W, int64_t ldw, unsigned short* Zb,
+                               int64_t ldc, float* part, int64_t M, int64_t N, int64_t K, int nj, hipStream_t stream) {
+  ASRX_REQUIRE(M > 0 && N > 0 && K > 0, "asrx_gemm_wn_ce: empty problem");
+  ASRX_REQUIRE(((uintptr_t)A & 15) == 0 && ((uintptr_t)W & 15) == 0 && ((uintptr_t)Zb & 7) == 0 &&
+                   ((uintptr_t)part & 7) == 0,
+               "asrx_gemm_wn_ce: A/W 16-byte, Zb/part 8-byte aligned");
+  ASRX_REQUIRE(K % 8 == 0 && lda % 8 == 0 && ldw % 8 == 0 && N % 4 == 0 && ldc % 4 == 0,
+               "asrx_gemm_wn_ce: K, lda, ldw %% 8 and N, ldc %% 4 required");
+  ASRX_REQUIRE(M * lda < (1LL << 31) && N * ldw < (1LL << 31), "asrx_gemm_wn_ce: operand spans >= 2^31 elements");
+  ASRX_REQUIRE(nj >= 1 && nj <= 3, "asrx_gemm_wn_ce: nj in 1..3");
+  wn::Params p{(const float*)A, (int)lda, W, (int)ldw, nullptr, (int)ldc, nullptr, nullptr, (int)M, (int)N, (int)K,
+               1, 1, 1.f, 0.f, ACT_NONE, nullptr, nullptr, nullptr, nullptr, Zb, (float2*)part,
+               (int)((N + 128 * nj - 1) / (128 * nj))};
+  if (nj == 3) wn::launch_wr<3, false, false, true, true>(p, stream);
+  else if (nj == 2) wn::launch_wr<2, false, false, true, true>(p, stream);
+  else wn::launch_wr<1, false, false, true, true>(p, stream);
+  ASRX_LAUNCHED("asrx_gemm_wn_ce");
+}
+
 // asrx_gemm_wn restricted to the BM-row tiles listed in mtiles (n_mtiles entries, both on the device,
 // from asrx_row_tiles); rows of other tiles are not written.
 extern "C" int asrx_gemm_wn_rows(const float* A, int64_t lda, const unsigned short* W, int64_t ldw, float* C,

@@ -56,6 +56,12 @@ struct Params {
   // bf16 output (gemm_wr_kernel): when non-null, act(v) is written here as bf16 instead of to C
   // (an activation whose only consumers are GEMM operands -- they round it to bf16 anyway); beta = 0
   unsigned short* Cb;
+  // fused cross-entropy statistics (gemm_wr_kernel<..., CE>): the tied-logits GEMM (model.py:629) writes
+  // the logits bf16 (Cb) and, per row and BN-column tile, the (max, sum exp(z - max)) of the tile's
+  // bf16-rounded logits into ce_part[row * ce_ld + tile] (float2), so the cross entropy never re-reads
+  // the logits for its log-sum-exp (asrx_ce_part_fwd merges the partials)
+  float2* ce_part;
+  int ce_ld;
 };
 
 __device__ __forceinline__ void st_bf16x4(unsigned short* dst, float a, float b, float c, float d) {
@@ -206,6 +212,83 @@ __device__ __forceinline__ void epilogue_lds(const Params& p, f32x4 (&acc)[4][2 
                                   reinterpret_cast<f32x4*>(dst));
     }
     __builtin_amdgcn_wave_barrier();  // the next slice overwrites the slab
+  }
+}
+
+// Tied-logits epilogue with cross-entropy statistics: the epilogue_lds bf16 store (alpha * acc, no
+// bias / activation), and from the same LDS slab each row's (max, sum exp) over the wave's 32*NJ
+// columns of the bf16-ROUNDED values (what the backward will read back): lane -> row lane/4, quarter
+// lane%4 of the columns, merged over the 4 lanes by shuffles and over the 4 column waves through LDS
+// (red: BM x 4 float2); threads < BM then write the tile's partial of their row.
+template <int NJ>
+__device__ __forceinline__ void epilogue_ce(const Params& p, f32x4 (&acc)[4][2 * NJ], int m0, int n0, int wm, int wn,
+                                            int lr, int lk, float* ep, float2* red) {
+  constexpr int NT = 2 * NJ, W = EpLds<NJ>::W, LD = EpLds<NJ>::LD, W4 = W / 4, Q = W / 4;
+  constexpr int PER = 16 * W4 / 64;
+  const int lane = threadIdx.x & 63;
+  const int cbase = n0 + wn * W;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int nl = nt * 16 + 4 * lk;
+      *reinterpret_cast<float4*>(ep + lr * LD + nl) =
+          make_float4(p.alpha * acc[mt][nt][0], p.alpha * acc[mt][nt][1], p.alpha * acc[mt][nt][2],
+                      p.alpha * acc[mt][nt][3]);
+    }
+    __builtin_amdgcn_wave_barrier();
+    const int rbase = m0 + wm * 64 + mt * 16;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int f = j * 64 + lane, r = f / W4, c = 4 * (f % W4);
+      const float4 x = *reinterpret_cast<const float4*>(ep + r * LD + c);
+      const int row = rbase + r, col = cbase + c;
+      if (row >= p.M || col >= p.N) continue;
+      st_bf16x4(p.Cb + (int64_t)row * p.ldc + col, x.x, x.y, x.z, x.w);
+    }
+    {
+      const int rr = lane >> 2, q = lane & 3;
+      const float* src = ep + rr * LD + q * Q;
+      const int c0 = cbase + q * Q;
+      float m = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < Q; ++i)
+        if (c0 + i < p.N) m = fmaxf(m, (float)(__bf16)src[i]);
+      float sm = 0.f;
+      if (m != -INFINITY) {
+#pragma unroll
+        for (int i = 0; i < Q; ++i)
+          if (c0 + i < p.N) sm += __expf((float)(__bf16)src[i] - m);
+      }
+#pragma unroll
+      for (int o = 1; o <= 2; o <<= 1) {
+        const float mo = __shfl_xor(m, o), so = __shfl_xor(sm, o);
+        const float mn = fmaxf(m, mo);
+        sm = (m == -INFINITY ? 0.f : sm * __expf(m - mn)) + (mo == -INFINITY ? 0.f : so * __expf(mo - mn));
+        m = mn;
+      }
+      if (q == 0) red[(wm * 64 + mt * 16 + rr) * 4 + wn] = make_float2(m, sm);
+    }
+    __builtin_amdgcn_wave_barrier();  // the next slice overwrites the slab
+  }
+  // every column wave's row partials in LDS, then one merge per row -- s_barrier without
+  // __syncthreads()'s vmcnt(0) fence (the next tile's operand loads stay in flight)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if (threadIdx.x < BM) {
+    const int row = m0 + threadIdx.x;
+    if (row < p.M) {
+      float m = -INFINITY, sm = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const float2 v = red[threadIdx.x * 4 + w];
+        const float mn = fmaxf(m, v.x);
+        sm = (m == -INFINITY ? 0.f : sm * __expf(m - mn)) + (v.x == -INFINITY ? 0.f : v.y * __expf(v.x - mn));
+        m = mn;
+      }
+      p.ce_part[(int64_t)row * p.ce_ld + n0 / Cfg<NJ>::BN] = make_float2(m, sm);
+    }
   }
 }
 
@@ -374,7 +457,7 @@ __device__ __forceinline__ void wr_store(const WrStage<NJ, ABF>& st, char* At, c
   }
 }
 
-template <int NJ, bool CONV, bool RT, int DEP = 0, bool ABF = false>
+template <int NJ, bool CONV, bool RT, int DEP = 0, bool ABF = false, bool CE = false>
 __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) {  // ntiles: all tiles
   typedef Cfg<NJ> CF;
   constexpr int BN = CF::BN, NT = 2 * NJ, BNR = CF::BNR;
@@ -383,7 +466,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
   __shared__ __attribute__((aligned(16))) char b_img[2][BB];
   __shared__ __attribute__((aligned(16))) float bias_s[2][BNR];
   __shared__ float w2s[RT ? 3 * BN : 1];
-  __shared__ float red[RT ? BM * 12 : 1];
+  __shared__ __attribute__((aligned(16))) float red[RT ? BM * 12 : (CE ? BM * 8 : 1)];
   __shared__ __attribute__((aligned(16))) float ep_s[RT ? 1 : 8 * EpLds<NJ>::FLOATS];
   if constexpr (RT) {
     for (int i = threadIdx.x; i < 3 * BN; i += NTHR) {
@@ -482,6 +565,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
       const float* bsl = bias_s[(s / nk) & 1];
       if constexpr (RT) {
         epilogue_router<NJ>(p, acc, bsl, w2s, red, m0, wm, wn, lr, lk);
+      } else if constexpr (CE) {
+        epilogue_ce<NJ>(p, acc, m0, n0, wm, wn, lr, lk, ep, reinterpret_cast<float2*>(red));
       } else if (WR_EPI_LDS && vec) switch (p.act) {
         case ACT_GELU: epilogue_lds<NJ, ACT_GELU>(p, acc, bsl, m0, n0, wm, wn, lr, lk, ep); break;
         case ACT_SILU: epilogue_lds<NJ, ACT_SILU>(p, acc, bsl, m0, n0, wm, wn, lr, lk, ep); break;
@@ -523,10 +608,16 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
   }
 }
 
-template <int NJ, bool CONV, bool RT = false, bool ABF = false>
+// bf16-stored A: a k-step's A slab is 8 KB instead of 16, so the bytes in flight per CU (the limit of
+// this kernel) need a deeper register pipeline: 4 k-steps (32 KB of A) instead of 3 (245
+// VGPRs; 5 spills)
+template <bool ABF>
+constexpr int wr_dep() { return ABF ? 4 : 0; }
+
+template <int NJ, bool CONV, bool RT = false, bool ABF = false, bool CE = false>
 void launch_wr(const Params& p, hipStream_t s) {
   static int resident = 0;
-  const void* fn = (const void*)gemm_wr_kernel<NJ, CONV, RT, 0, ABF>;
+  const void* fn = (const void*)gemm_wr_kernel<NJ, CONV, RT, wr_dep<ABF>(), ABF, CE>;
   if (!resident) {
     int per_cu = 0, dev = 0, cus = 0;
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, NTHR, 0);
@@ -538,7 +629,7 @@ void launch_wr(const Params& p, hipStream_t s) {
   const int grid = std::min(tiles, resident);
   // a 5-deep pipeline (DEP = 5) for the one-wave 8192-row text-side launches measured 32.4 us vs
   // 30.1 us at depth 3 (profiles/r02_bench_v8_kernel_stats.csv): their time is not load latency
-  gemm_wr_kernel<NJ, CONV, RT, 0, ABF><<<grid, NTHR, 0, s>>>(p, tiles);
+  gemm_wr_kernel<NJ, CONV, RT, wr_dep<ABF>(), ABF, CE><<<grid, NTHR, 0, s>>>(p, tiles);
 }
 
 }  // namespace wn
@@ -548,8 +639,10 @@ void launch_wr(const Params& p, hipStream_t s) {
 // declare them.
 #ifndef ASRX_WR_INSTANTIATE
 #define ASRX_WR_DECL(NJ, CONV, RT, ABF) extern template void asrx::wn::launch_wr<NJ, CONV, RT, ABF>(const asrx::wn::Params&, hipStream_t);
+#define ASRX_WR_DECL_CE(NJ) extern template void asrx::wn::launch_wr<NJ, false, false, true, true>(const asrx::wn::Params&, hipStream_t);
 #else
 #define ASRX_WR_DECL(NJ, CONV, RT, ABF) template void asrx::wn::launch_wr<NJ, CONV, RT, ABF>(const asrx::wn::Params&, hipStream_t);
+#define ASRX_WR_DECL_CE(NJ) template void asrx::wn::launch_wr<NJ, false, false, true, true>(const asrx::wn::Params&, hipStream_t);
 #endif
 #define ASRX_WR_SET(NJ) ASRX_WR_DECL(NJ, false, false, false) ASRX_WR_DECL(NJ, true, false, false) \
   ASRX_WR_DECL(NJ, false, false, true) ASRX_WR_DECL(NJ, true, false, true) ASRX_WR_DECL(NJ, false, true, false)
@@ -557,4 +650,7 @@ void launch_wr(const Params& p, hipStream_t s) {
 ASRX_WR_SET(1)
 ASRX_WR_SET(2)
 ASRX_WR_SET(3)
+ASRX_WR_DECL_CE(1)
+ASRX_WR_DECL_CE(2)
+ASRX_WR_DECL_CE(3)
 #endif

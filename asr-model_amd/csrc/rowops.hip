@@ -574,8 +574,21 @@ __global__ __launch_bounds__(64 * RW) void msheath_row_fwd_kernel(MSRowFwd p) {
   const float mv_l = lane < p.M ? p.mval[lane] : 0.f;
   const float b2 = p.b2[0], cw0 = p.cw[0], cw1 = p.cw[1], cb = p.cb[0], tx = p.tx[0];
   auto at_layer = [&](int64_t rr) { return !p.next_i || p.next_i[rr / p.L] == (float)p.layer; };
+  // the next row's x AND its v_gate projections (S[lane], h) are loaded while this row is processed
+  // (the SH row -- M + Dh floats -- was read only after the LayerNorm, its latency exposed per row)
+  constexpr int HQ = (E + 1) / 2;  // h values per lane (Dh = D / 2 <= 64 HQ)
+  float sn = 0.f, hn[HQ];
+  auto fetch = [&](int64_t rr) __attribute__((always_inline)) {
+    if (rr < p.rows && at_layer(rr)) {
+      ld_lane<E>(p.x + rr * D, lane, xn);
+      const float* S = p.SH + rr * p.ldsh;
+      sn = lane < p.M ? S[lane] : 0.f;
+#pragma unroll
+      for (int i = 0; i < HQ; ++i) hn[i] = lane + 64 * i < p.Dh ? S[p.M + lane + 64 * i] : 0.f;
+    }
+  };
   int64_t r = row_begin();
-  if (r < p.rows && at_layer(r)) ld_lane<E>(p.x + r * D, lane, xn);
+  fetch(r);
   for (; r < p.rows; r += row_step()) {
     const int64_t rn = r + row_step();
     if (!at_layer(r)) {  // sample not at this layer: no reads; zeros keep every later consumer finite
@@ -593,10 +606,11 @@ __global__ __launch_bounds__(64 * RW) void msheath_row_fwd_kernel(MSRowFwd p) {
         p.kv[r] = 0.f;
         p.m2[r] = 0.f;
       }
-      if (rn < p.rows && at_layer(rn)) ld_lane<E>(p.x + rn * D, lane, xn);
+      fetch(rn);
       continue;
     }
-    float xv[E];
+    float xv[E], hv[HQ];
+    const float sv = sn;
     float s = 0.f, q = 0.f;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -604,7 +618,9 @@ __global__ __launch_bounds__(64 * RW) void msheath_row_fwd_kernel(MSRowFwd p) {
       s += xv[e];
       q += xv[e] * xv[e];
     }
-    if (rn < p.rows && at_layer(rn)) ld_lane<E>(p.x + rn * D, lane, xn);
+#pragma unroll
+    for (int i = 0; i < HQ; ++i) hv[i] = hn[i];
+    fetch(rn);
     const float mu = wave_sum_dpp(s) * (1.0f / D);
     const float nrm = sqrtf(wave_sum_dpp(q));
     float v = 0.f;
@@ -624,16 +640,16 @@ __global__ __launch_bounds__(64 * RW) void msheath_row_fwd_kernel(MSRowFwd p) {
     else st_lane<E>(p.px + r * D, lane, yv);
     const float gate = sigmoid_f(wave_sum_dpp(gd) + gbias);
     // v_gate
-    const float* S = p.SH + r * p.ldsh;
-    const float* h = S + p.M;
     const float inx = 1.0f / fmaxf(nrm, 1e-12f);
-    const float z = lane < p.M ? S[lane] * inx * p.inv_sqrt_d : -INFINITY;
+    const float z = lane < p.M ? sv * inx * p.inv_sqrt_d : -INFINITY;
     const float zm = wave_max(z);
     const float ez = lane < p.M ? expf(z - zm) : 0.f;
     const float se = wave_sum(ez);
     const float kv = wave_sum(lane < p.M ? ez / se * mv_l : 0.f);
     float acc = 0.f;
-    for (int j = lane; j < p.Dh; j += 64) acc += silu_f(h[j]) * p.w2[j];
+#pragma unroll
+    for (int i = 0; i < HQ; ++i)
+      if (lane + 64 * i < p.Dh) acc += silu_f(hv[i]) * p.w2[lane + 64 * i];
     const float m2 = wave_sum(acc) + b2;
     const float xval = cw0 * kv + cw1 * m2 + cb;
     if (lane == 0) {
@@ -686,21 +702,52 @@ __global__ __launch_bounds__(64 * RW) void msheath_row_bwd_kernel(MSRowBwd p) {
   for (int e = 0; e < E; ++e) aw[e] = ab[e] = ag[e] = 0.f;
   const float mv_l = lane < M ? p.mval[lane] : 0.f;
   const float cw0 = p.cw[0], cw1 = p.cw[1];
-  for (int64_t r = row_begin(); r < p.rows; r += row_step()) {
-    if (p.next_i && p.next_i[r / p.L] != (float)p.layer) {
+  // every input of the next row (x, dpx, dx, the v_gate projections and the row scalars) is loaded
+  // while this row is processed: without it each row's loads were a dependent latency chain
+  constexpr int HQ = (E + 1) / 2;  // h values per lane (Dh <= 64 HQ)
+  struct Pre {
+    float x[E], gp[E], dx[E], h[HQ];
+    float s, gi, nx, g, dg, mu, rs, kv, m2;
+  };
+  Pre nx_;
+  auto at_layer = [&](int64_t rr) { return !p.next_i || p.next_i[rr / p.L] == (float)p.layer; };
+  auto fetch = [&](int64_t rr) __attribute__((always_inline)) {
+    if (rr < p.rows && at_layer(rr)) {
+      const float* S = p.SH + rr * p.ldsh;
+      nx_.s = lane < M ? S[lane] : 0.f;
+#pragma unroll
+      for (int i = 0; i < HQ; ++i) nx_.h[i] = lane + 64 * i < Dh ? S[M + lane + 64 * i] : 0.f;
+      ld_lane<E>(p.x + rr * D, lane, nx_.x);
+      ld_lane<E>(p.dpx + rr * D, lane, nx_.gp);
+      ld_lane<E>(p.dx + rr * D, lane, nx_.dx);
+      nx_.gi = p.dion[rr];
+      nx_.nx = p.nx[rr];
+      nx_.g = p.g[rr];
+      nx_.dg = p.dg[rr];
+      nx_.mu = p.mean[rr];
+      nx_.rs = p.rstd[rr];
+      nx_.kv = p.kv[rr];
+      nx_.m2 = p.m2[rr];
+    }
+  };
+  int64_t r = row_begin();
+  fetch(r);
+  for (; r < p.rows; r += row_step()) {
+    if (!at_layer(r)) {
       float* dz = p.dSH + r * p.ldsh;  // zero rows: the weight-gradient GEMMs sum over every row
       for (int j = lane; j < M + Dh; j += 64) dz[j] = 0.f;
+      fetch(r + row_step());
       continue;
     }
+    const Pre c = nx_;
+    fetch(r + row_step());
     // ---- v_gate backward (vgate_bwd_kernel)
-    const float gi = p.dion[r];
-    const float nxr = p.nx[r];
+    const float gi = c.gi;
+    const float nxr = c.nx;
     const float inx = 1.0f / fmaxf(nxr, 1e-12f);
-    const float* S = p.SH + r * p.ldsh;
-    const float* h = S + M;
     float* dS = p.dSH + r * p.ldsh;
     float* dh = dS + M;
-    const float sl = lane < M ? S[lane] : 0.f;
+    const float sl = c.s;
     const float z = lane < M ? sl * inx * p.inv_sqrt_d : -INFINITY;
     const float zm = wave_max(z);
     const float ez = lane < M ? expf(z - zm) : 0.f;
@@ -715,27 +762,34 @@ __global__ __launch_bounds__(64 * RW) void msheath_row_bwd_kernel(MSRowBwd p) {
     }
     const float dinx = wave_sum(lane < M ? dz * sl * p.inv_sqrt_d : 0.f);
     const float dnx = nxr > 1e-12f ? -dinx * inx * inx : 0.f;
-    for (int j = lane; j < Dh; j += 64) {
-      const float hv = h[j];
-      const float t = dm2 * p.w2[j] * silu_grad(hv);
-      dh[j] = t;
-      pw[M + j] += dm2 * silu_f(hv);
-      pw[M + Dh + j] += t;
+#pragma unroll
+    for (int i = 0; i < HQ; ++i) {
+      const int j = lane + 64 * i;
+      if (j < Dh) {
+        const float hv = c.h[i];
+        const float t = dm2 * p.w2[j] * silu_grad(hv);
+        dh[j] = t;
+        pw[M + j] += dm2 * silu_f(hv);
+        pw[M + Dh + j] += t;
+      }
     }
     // ---- gate + LayerNorm + |x| backward
-    const float gg = p.g[r];
-    const float dzg = p.dg[r] * gg * (1.f - gg);
+    const float gg = c.g;
+    const float dzg = c.dg * gg * (1.f - gg);
     if (lane == 0) {
       pw[M + 2 * Dh + 0] += dm2;
-      pw[M + 2 * Dh + 1] += gi * p.kv[r];
-      pw[M + 2 * Dh + 2] += gi * p.m2[r];
+      pw[M + 2 * Dh + 1] += gi * c.kv;
+      pw[M + 2 * Dh + 2] += gi * c.m2;
       pw[M + 2 * Dh + 3] += gi;
       pw[M + 2 * Dh + 4] += dzg;
     }
     float xv[E], gv[E];
-    ld_lane<E>(p.x + r * D, lane, xv);
-    ld_lane<E>(p.dpx + r * D, lane, gv);
-    const float mu = p.mean[r], rs = p.rstd[r];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      xv[e] = c.x[e];
+      gv[e] = c.gp[e];
+    }
+    const float mu = c.mu, rs = c.rs;
     const float cn = nxr > 0.f ? dnx / nxr : 0.f;
     float s1 = 0.f, s2 = 0.f, xh[E];
 #pragma unroll
@@ -752,9 +806,8 @@ __global__ __launch_bounds__(64 * RW) void msheath_row_bwd_kernel(MSRowBwd p) {
     s1 = wave_sum_dpp(s1) * (1.0f / D);
     s2 = wave_sum_dpp(s2) * (1.0f / D);
     float dv[E];
-    ld_lane<E>(p.dx + r * D, lane, dv);
 #pragma unroll
-    for (int e = 0; e < E; ++e) dv[e] += rs * (gv[e] * wv[e] - s1 - xh[e] * s2) + cn * xv[e];
+    for (int e = 0; e < E; ++e) dv[e] = c.dx[e] + rs * (gv[e] * wv[e] - s1 - xh[e] * s2) + cn * xv[e];
     st_lane<E>(p.dx + r * D, lane, dv);
   }
   float* pl = part + wid * 3 * D;
@@ -2065,6 +2118,7 @@ int asrx_msheath_row_fwd2(const float* x, const float* lnw, const float* lnb, co
                           int64_t M, int64_t Dh, float eps, float inv_sqrt_d, const float* next_i, int64_t layer,
                           int64_t L, hipStream_t stream) {
   ASRX_REQUIRE(M <= 64 && ldsh >= M + Dh, "asrx_msheath_row_fwd: M <= 64 and ldsh >= M + Dh required");
+  ASRX_REQUIRE(Dh <= 64 * ((d / 64 + 1) / 2), "asrx_msheath_row_fwd: v_gate hidden size Dh <= d / 2 required");
   ASRX_REQUIRE(ms_aligned({x, lnw, lnb, gw, (const float*)px}), "asrx_msheath_row_fwd: 8-byte aligned rows required");
   ASRX_REQUIRE(!next_i || L > 0, "asrx_msheath_row_fwd: L > 0 required with next_i");
   if (rows == 0) return 0;
@@ -2095,6 +2149,7 @@ int asrx_msheath_row_bwd(const float* dpx, const float* x, const float* lnw, con
                          float* dcb, float* db1, int64_t rows, int64_t d, int64_t M, int64_t Dh, float inv_sqrt_d,
                          const float* next_i, int64_t layer, int64_t L, hipStream_t stream) {
   ASRX_REQUIRE(M <= 64 && ldsh >= M + Dh, "asrx_msheath_row_bwd: M <= 64 and ldsh >= M + Dh required");
+  ASRX_REQUIRE(Dh <= 64 * ((d / 64 + 1) / 2), "asrx_msheath_row_bwd: v_gate hidden size Dh <= d / 2 required");
   ASRX_REQUIRE(ms_aligned({dpx, x, lnw, lnb, gw, dx}), "asrx_msheath_row_bwd: 8-byte aligned rows required");
   ASRX_REQUIRE(!next_i || L > 0, "asrx_msheath_row_bwd: L > 0 required with next_i");
   if (rows == 0) return 0;

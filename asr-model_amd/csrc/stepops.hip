@@ -52,8 +52,80 @@ __global__ __launch_bounds__(256) void ce_fwd1_kernel(const float* __restrict__ 
     for (int w = 0; w < 4; ++w) S += rs[w] * __expf(rm[w] - M);
     const float l = M + logf(S);
     lse[r] = l;
-    loss[r] = y == 0 ? 0.f : l - zr[y];
+    // a label outside [0, V) (the reference's F.cross_entropy raises) makes the loss NaN instead of
+    // reading outside the row
+    loss[r] = (y < 0 || y >= V) ? __builtin_nanf("") : (y == 0 ? 0.f : l - zr[y]);
   }
+}
+
+// The cross entropy from the fused logits GEMM's partials (asrx_gemm_wn_ce): per row, merge the
+// nparts (max, sum exp) pairs of its column tiles into the log-sum-exp and read the label's bf16 logit
+// (2 bytes) -- the 40000-wide row itself is not re-read.  One wave per row, 4 rows per workgroup.
+__global__ __launch_bounds__(256) void ce_part_fwd_kernel(const float2* __restrict__ part, int nparts,
+                                                          const unsigned short* __restrict__ zb,
+                                                          const int64_t* __restrict__ labels, float* __restrict__ loss,
+                                                          float* __restrict__ lse, int64_t rows, int64_t V) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  float m = -INFINITY, s = 0.f;
+  for (int j = lane; j < nparts; j += 64) {
+    const float2 v = part[r * nparts + j];
+    const float mn = fmaxf(m, v.x);
+    s = (m == -INFINITY ? 0.f : s * __expf(m - mn)) + (v.x == -INFINITY ? 0.f : v.y * __expf(v.x - mn));
+    m = mn;
+  }
+  for (int o = 32; o >= 1; o >>= 1) {
+    const float mo = __shfl_xor(m, o), so = __shfl_xor(s, o);
+    const float mn = fmaxf(m, mo);
+    s = (m == -INFINITY ? 0.f : s * __expf(m - mn)) + (mo == -INFINITY ? 0.f : so * __expf(mo - mn));
+    m = mn;
+  }
+  if (lane == 0) {
+    const int64_t y = labels[r];
+    const float l = m + logf(s);
+    lse[r] = l;
+    float lr = 0.f;
+    if (y < 0 || y >= V) lr = __builtin_nanf("");
+    else if (y != 0) lr = l - __builtin_bit_cast(float, (uint32_t)zb[r * V + y] << 16);
+    loss[r] = lr;
+  }
+}
+
+// dz = (g / count) (softmax(z) - onehot(y)) from the bf16 logits, stored bf16 (it only feeds the two
+// gradient GEMMs, which round their operands to bf16 anyway).  One row per workgroup, 8 logits per
+// 16-byte load.
+__global__ __launch_bounds__(256) void ce_bwd_bf16_kernel(const unsigned short* __restrict__ zb,
+                                                          const int64_t* __restrict__ labels,
+                                                          const float* __restrict__ lse, const float* __restrict__ g,
+                                                          const float* __restrict__ count,
+                                                          unsigned short* __restrict__ dzb, int64_t V) {
+  const int64_t r = blockIdx.x;
+  const int64_t y = labels[r];
+  const bool bad = y < 0 || y >= V;
+  const float sc = bad ? __builtin_nanf("") : (y == 0 ? 0.f : g[0] / count[0]);
+  const float l = lse[r];
+  const unsigned short* zr = zb + r * V;
+  unsigned short* dr = dzb + r * V;
+  auto f = [&](unsigned short h, int64_t j) {
+    const float v = __builtin_bit_cast(float, (uint32_t)h << 16);
+    return __builtin_bit_cast(unsigned short, (__bf16)(sc * (__expf(v - l) - (j == y ? 1.f : 0.f))));
+  };
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const bool vec = V % 8 == 0 && (((uintptr_t)zr | (uintptr_t)dr) & 15) == 0;
+  const int64_t V8 = vec ? V / 8 : 0;
+  for (int64_t j = threadIdx.x; j < V8; j += 256) {
+    const u32x4 in = reinterpret_cast<const u32x4*>(zr)[j];
+    u32x4 out;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const unsigned short lo = f((unsigned short)(in[q] & 0xFFFF), 8 * j + 2 * q);
+      const unsigned short hi = f((unsigned short)(in[q] >> 16), 8 * j + 2 * q + 1);
+      out[q] = (unsigned)lo | ((unsigned)hi << 16);
+    }
+    reinterpret_cast<u32x4*>(dr)[j] = out;
+  }
+  for (int64_t j = 8 * V8 + threadIdx.x; j < V; j += 256) dr[j] = f(zr[j], j);
 }
 
 // loss = sum_r loss_r / max(#{labels != 0}, 1); count kept for the backward.  One workgroup.
@@ -81,7 +153,7 @@ __global__ __launch_bounds__(256) void ce_bwd2_kernel(const float* z, const int6
                                                       const float* __restrict__ count, float* dz, int64_t V) {
   const int64_t r = blockIdx.x;
   const int64_t y = labels[r];
-  const float sc = (y == 0) ? 0.f : g[0] / count[0];
+  const float sc = (y < 0 || y >= V) ? __builtin_nanf("") : ((y == 0) ? 0.f : g[0] / count[0]);
   const float l = lse[r];
   const float* zr = z + r * V;
   float* dr = dz + r * V;
@@ -265,6 +337,24 @@ int asrx_ce_bwd2(const float* z, const int64_t* labels, const float* lse, const 
   if (rows == 0) return 0;
   ce_bwd2_kernel<<<(unsigned)rows, 256, 0, stream>>>(z, labels, lse, g, count, dz, V);
   ASRX_LAUNCHED("asrx_ce_bwd2");
+}
+
+int asrx_ce_part_fwd(const float* part, int64_t nparts, const unsigned short* zb, const int64_t* labels, float* loss_r,
+                     float* lse, float* loss, float* count, int64_t rows, int64_t V, hipStream_t stream) {
+  if (rows == 0) return 0;
+  ASRX_REQUIRE(nparts > 0 && rows < (1LL << 33), "asrx_ce_part_fwd: bad shape");
+  ce_part_fwd_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, stream>>>((const float2*)part, (int)nparts, zb, labels,
+                                                                     loss_r, lse, rows, V);
+  ce_reduce_kernel<<<1, 1024, 0, stream>>>(loss_r, labels, rows, loss, count);
+  ASRX_LAUNCHED("asrx_ce_part_fwd");
+}
+
+int asrx_ce_bwd_bf16(const unsigned short* zb, const int64_t* labels, const float* lse, const float* g,
+                     const float* count, unsigned short* dzb, int64_t rows, int64_t V, hipStream_t stream) {
+  if (rows == 0) return 0;
+  ASRX_REQUIRE(rows < (1LL << 31), "asrx_ce_bwd_bf16: too many rows");
+  ce_bwd_bf16_kernel<<<(unsigned)rows, 256, 0, stream>>>(zb, labels, lse, g, count, dzb, V);
+  ASRX_LAUNCHED("asrx_ce_bwd_bf16");
 }
 
 int asrx_bn_running(const float* mean, const float* rstd, float* rm, float* rv, int64_t* nbt, int64_t B, int64_t C,

@@ -122,8 +122,12 @@ int asrx_row_tiles(const float* next_i, int64_t layer, int64_t L, int64_t M, int
 
 /* ---- AbbyNormal: essentials.py:140-191 (router SiLU-MLP, cv, gumbel hard decision, avg/max pool of
  *      x^2 along the feature axis, x / (1 + 1e-4 div)^0.75).  hpre = x @ W1^T + b1 from asrx_gemm.
- *      Rows are (sample, position, head)-major; noise index ((sid*H+h)*4096+l)*3+k, sid = sid_base + b.
+ *      Rows are (sample, position, head)-major; noise index ((sid*H+h)*8192+l)*3+k, sid = sid_base + b.
  *      ys (rows,3) / idx (rows) int32 are saved for backward. ----------------------------------- */
+/* decision recorder (parity tests, eager only): while buf != NULL every AbbyNormal forward writes mode
+ * 2's per-feature choice max > 2 avg (essentials.py:176-177) of its mode-2 rows into buf (rows x d
+ * bytes, caller-zeroed) */
+int asrx_abby_record_cond(unsigned char* buf);
 int asrx_abby_fwd(const float* x, const float* hpre, const float* W2, const float* b2, float* out, float* ys,
                   int* idx, int64_t rows, int64_t d, int64_t L, int64_t H, int64_t sid_base, uint32_t key,
                   int use_noise, asrx_stream_t stream);
@@ -454,6 +458,22 @@ int asrx_ce_fwd1(const float* z, const int64_t* labels, float* loss_r, float* ls
                  int64_t rows, int64_t V, asrx_stream_t stream);
 int asrx_ce_bwd2(const float* z, const int64_t* labels, const float* lse, const float* g, const float* count, float* dz,
                  int64_t rows, int64_t V, asrx_stream_t stream);
+/* Fused tied logits + cross entropy (perf mode; model.py:629 logits, model.py:670 F.cross_entropy):
+ * asrx_gemm_wn_ce (csrc/gemm_wn.hip) writes the logits bf16 and per row / 128*nj-column tile the
+ * (max, sum exp) of the tile's bf16 logits (part: rows x nparts float2, nparts = ceil(V / (128 nj)));
+ * asrx_ce_part_fwd merges them into lse and the loss (reads the label's logit only); asrx_ce_bwd_bf16
+ * writes dz = (g/count)(softmax - onehot) bf16 from the bf16 logits.  A label outside [0, V) gives a
+ * NaN loss / gradient (the reference raises). */
+int asrx_gemm_wn_ce(const void* A, int64_t lda, const unsigned short* W, int64_t ldw, unsigned short* Zb, int64_t ldc,
+                    float* part, int64_t M, int64_t N, int64_t K, int nj, asrx_stream_t stream);
+int asrx_ce_part_fwd(const float* part, int64_t nparts, const unsigned short* zb, const int64_t* labels, float* loss_r,
+                     float* lse, float* loss, float* count, int64_t rows, int64_t V, asrx_stream_t stream);
+int asrx_ce_bwd_bf16(const unsigned short* zb, const int64_t* labels, const float* lse, const float* g,
+                     const float* count, unsigned short* dzb, int64_t rows, int64_t V, asrx_stream_t stream);
+/* asrx_wgrad_bf16 with dY and X both stored bf16 (M, N, lda, ldb % 8): the tied token embedding's
+ * gradient from the bf16 logits gradient. */
+int asrx_wgrad_bf16_ab(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, int64_t ldc, int64_t M,
+                       int64_t N, int64_t R, int64_t splitk, asrx_stream_t stream);
 /* BatchNorm1d running statistics from per-clip (B, C) mean / rstd (ConvLite.bn, model.py:101);
  * nbt (num_batches_tracked, int64) may be NULL.  asrx_rsqrt_eps: eval-mode rstd. */
 int asrx_bn_running(const float* mean, const float* rstd, float* rm, float* rv, int64_t* nbt, int64_t B, int64_t C,

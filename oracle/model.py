@@ -72,6 +72,8 @@ class Decisions:
       ("abby", key, sid) -> int64 (L, H) AbbyNormal mode index (gumbel argmax, essentials.py:170)
       ("ion", key, sid, layer) -> (L,) v_gate STthreshold output (model.py:330-334, 351)
       ("action", key, sid, layer) -> (action, forced) MSheath jump (model.py:476-482)
+      ("cond", key, sid) -> bool (L, H, d) AbbyNormal mode 2's max > 2 avg per feature (rows in mode 2,
+                            essentials.py:176-177)
     record: every decision taken is stored in `rec`.  replay: a decision found in `table` is used
     instead of the one this forward would take (the continuous values -- soft gumbel probabilities,
     STE paths -- are still this forward's own), so the oracle follows the HIP path's discrete
@@ -82,6 +84,7 @@ class Decisions:
         self.table = table
         self.replayed = 0
         self.overridden = 0
+        self.cond_overridden = 0
 
 
 _DEC: Decisions | None = None
@@ -110,6 +113,27 @@ def _decide_abby(index, dkey, heads: bool):
                 out[s, ..., 0] = want.t()
             else:
                 out[s] = want
+    return out
+
+
+def _decide_cond(cond, index, dkey, heads: bool):
+    """AbbyNormal mode 2's per-feature choice cond = max > 2 avg (essentials.py:176-177), (B, L, d) or
+    (B, H, L, d) bool; index the (replayed) mode per row.  Recorded for the rows in mode 2 as (L, H, d);
+    replayed from ("cond", key, sid) on the rows the replayed mode puts in mode 2."""
+    if _DEC is None or dkey is None:
+        return cond
+    key, sids = dkey
+    out = cond.clone()
+    for s, sid in enumerate(sids):
+        m1 = index[s, ..., 0] == 1  # (L,) or (H, L)
+        own = cond[s] & m1.unsqueeze(-1)
+        _DEC.rec[("cond", int(key), int(sid))] = (own.permute(1, 0, 2) if heads else own.unsqueeze(1)).clone()
+        want = _DEC.table.get(("cond", int(key), int(sid))) if _DEC.table is not None else None
+        if want is not None:
+            want = (want.permute(1, 0, 2) if heads else want[:, 0, :]).to(cond.device)
+            new = torch.where(m1.unsqueeze(-1), want, cond[s])
+            _DEC.cond_overridden += int((new != cond[s]).sum())
+            out[s] = new
     return out
 
 
@@ -142,7 +166,7 @@ def abby_normal(P, pre, x, g, dkey=None):
     rows = div.reshape(-1, 1, d)  # pooling runs along the feature axis (essentials.py:171-172)
     avg_d = F.avg_pool1d(rows, kernel_size=size, stride=1, padding=pad).reshape(div.shape)
     max_d = F.max_pool1d(rows, kernel_size=size, stride=1, padding=pad).reshape(div.shape)
-    cond = (max_d > 2.0 * avg_d).to(x.dtype)
+    cond = _decide_cond(max_d > 2.0 * avg_d, index, dkey, x.dim() == 4).to(x.dtype)
     mode2 = cond * max_d + (1 - cond) * avg_d
     mode3 = avg_d
     div = dec[..., 0:1] * avg_d + dec[..., 1:2] * mode2 + dec[..., 2:3] * mode3

@@ -62,6 +62,17 @@ def agreement(hip: dict, ref: dict) -> dict:
     """Agreement of two decision tables on their common keys: per kind, the fraction of equal entries
     (AbbyNormal modes and v_gate thresholds per position, MSheath actions per (sample, layer))."""
     out = {}
+    # mode 2's per-feature max-vs-avg choice, on the rows both sides put in mode 2
+    eq = tot = 0
+    for k in hip:
+        if k[0] != "cond" or k not in ref or ("abby",) + k[1:] not in ref:
+            continue
+        both = (hip[("abby",) + k[1:]] == 1) & (ref[("abby",) + k[1:]] == 1)  # (L, H)
+        a, b = hip[k][both], ref[k][both]
+        eq += int((a == b).sum())
+        tot += a.numel()
+    out["cond"] = (eq / tot) if tot else None
+    out["cond_n"] = tot
     for kind in ("abby", "ion", "action"):
         keys = [k for k in hip if k[0] == kind and k in ref]
         eq = tot = 0
@@ -168,6 +179,7 @@ def compare(cfg, B=1, seconds=30.0, T=256, precision="bf16", train=True, grads=T
         P_r, ref_r = run_oracle(rp)
         res_extra["replayed"] = rp.replayed
         res_extra["overridden"] = rp.overridden
+        res_extra["cond_overridden"] = rp.cond_overridden
         if P is None:
             P, ref = P_r, ref_r
         else:
@@ -186,8 +198,8 @@ def compare(cfg, B=1, seconds=30.0, T=256, precision="bf16", train=True, grads=T
            "t_gpu_s": round(t_gpu, 2), "t_oracle_s": round(t_ref, 2), **res_extra}
     if grads and replay:  # every parameter that receives a gradient on both sides
         names = dict(model.named_parameters())
-        worst, wname = 0.0, None
-        missing, residue = [], {}
+        worst, wname, gworst, gwname = 0.0, None, 0.0, None
+        missing, residue, per = [], {}, {}
         gscale = max(float(P[n].grad.abs().max()) for n in names if n in P and P[n].grad is not None)
         for n, p in names.items():
             pg, rg = p.grad, P[n].grad if n in P else None
@@ -203,11 +215,20 @@ def compare(cfg, B=1, seconds=30.0, T=256, precision="bf16", train=True, grads=T
                 continue
             if pg is None:
                 continue
-            e = _rel_max(pg.double().cpu(), rg)
+            d = float((pg.double().cpu() - rg).abs().max())
+            e = d / max(float(rg.abs().max()), 1e-30)
+            per[n] = (e, d / gscale, float(rg.abs().max()) / gscale)
             if e > worst:
                 worst, wname = e, n
+            if d / gscale > gworst:
+                gworst, gwname = d / gscale, n
+        # own: max|dg| / max|g_ref| of that parameter; global: max|dg| / the largest gradient of the model
         res["grads_all_max"] = worst
         res["grads_all_worst"] = wname
+        res["grads_all_global"] = gworst
+        res["grads_all_global_worst"] = gwname
+        res["grads_all_top"] = sorted(((round(v[0], 6), round(v[1], 9), round(v[2], 6), k) for k, v in per.items()),
+                                      reverse=True)[:8]
         res["grads_missing"] = missing
         res["zero_grad_residue"] = max(residue.values(), default=0.0)
     if grads:

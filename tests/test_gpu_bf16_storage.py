@@ -152,9 +152,16 @@ def test_model_forward_unchanged_by_bf16_storage(cuda):
     assert torch.equal(res[0][0], res[1][0])
     assert res[0][1] == res[1][1]
     assert set(res[0][2]) == set(res[1][2])
-    worst = max(float((res[1][2][n] - res[0][2][n]).abs().max() / res[0][2][n].abs().max().clamp_min(1e-20))
-                for n in res[0][2])
-    assert worst < 5e-2, worst
+    # measured against the model's largest gradient; the analytically-zero gradients (identity router,
+    # the depthwise-conv bias ahead of the per-sample BatchNorm: rounding residue only) are skipped
+    from model_parity import ANALYTIC_ZERO
+
+    gmax = max(float(g.abs().max()) for g in res[0][2].values())
+    errs = {n: float((res[1][2][n] - res[0][2][n]).abs().max()) / gmax for n in res[0][2]
+            if not any(z in n for z in ANALYTIC_ZERO)}
+    worst = max(errs, key=errs.get)
+    print("bf16 storage on/off: worst gradient difference", errs[worst], worst)
+    assert errs[worst] < 2e-2, (errs[worst], worst)
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])

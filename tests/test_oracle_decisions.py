@@ -39,7 +39,7 @@ def test_replay_own_decisions_is_identity():
     rec = om.Decisions()
     r0, P0 = _run(cfg, sd, x, ids, labels, rec)
     kinds = {k[0] for k in rec.rec}
-    assert kinds == {"abby", "ion", "action"}, kinds
+    assert kinds == {"abby", "cond", "ion", "action"}, kinds
     rep = om.Decisions(table=rec.rec)
     r1, P1 = _run(cfg, sd, x, ids, labels, rep)
     assert rep.replayed > 0 and rep.overridden == 0

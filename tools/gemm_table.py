@@ -54,8 +54,13 @@ for kind in ("gemm", "attn", "logmel"):
           f"({100*tsum/total:.1f}% of step), {sum(v[1] for v in tab.values())/max(tsum,1e-12)/1e12:.1f} TF/s")
     for tag, (n, w, sec) in sorted(tab.items(), key=lambda kv: -kv[1][2]):
         extra = ""
-        if kind == "gemm" and tag and tag[0] in ("wn", "router"):
+        if kind == "gemm" and tag and tag[0] == "wn":
+            _, M, N, K, _nj, _conv, _act, has_z, has_beta, a_bf16, c_bf16, row_list = tag
+            ea, ec = (2 if a_bf16 else 4), (2 if c_bf16 else 4)
+            byts = ea * M * K + 2 * N * K + ec * M * N * (1 + int(has_beta)) + 4 * M * N * int(has_z)
+            extra = f" {byts*n/sec/1e9:7.0f} GB/s {byts/1e6:8.1f} MB"
+        elif kind == "gemm" and tag and tag[0] == "router":
             M, N, K = tag[1], tag[2], tag[3]
-            byts = 4 * M * K + 4 * M * N + 2 * N * K
-            extra = f" {byts*n/sec/1e9:7.0f} GB/s(fp32 A+C)"
+            byts = 4 * M * K + 2 * N * K + 12 * M + 4 * M * N * int(tag[4])
+            extra = f" {byts*n/sec/1e9:7.0f} GB/s {byts/1e6:8.1f} MB"
         print(f"{n:5d} x {sec/n*1e6:8.1f} us = {sec*1e3:7.2f} ms  {w/sec/1e12:7.1f} TF/s{extra}  {tag}")

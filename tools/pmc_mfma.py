@@ -19,10 +19,10 @@ rows = []
 for k, c in vals.items():
     n = max(len(disp[k]), 1)
     busy, insts, gui = c["SQ_VALU_MFMA_BUSY_CYCLES"], c["SQ_INSTS_MFMA"], c["GRBM_GUI_ACTIVE"]
-    if insts == 0:
+    if busy == 0:
         continue
     util = busy / (gui / 8.0 * 1024.0) if gui > 0 else 0.0
-    rows.append((busy, k, n, util, busy / insts, gui / 8.0 / n))
+    rows.append((busy, k, n, util, busy / insts if insts else float('nan'), gui / 8.0 / n))
 print("kernel,launches,mfma_util,busy_cycles_per_mfma,avg_kernel_cycles,share_of_mfma_busy")
 tot = sum(r[0] for r in rows)
 for busy, k, n, util, cpm, cyc in sorted(rows, reverse=True):
