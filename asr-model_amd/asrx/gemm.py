@@ -269,15 +269,17 @@ def _wgrad(A, lda, x2, out, M, K, rows):
     tiles = ((M + 127) // 128) * ((K + 127) // 128)
     sk = _splitk_for(rows, tiles)
     if is_bf16(A):
-        # a bf16-stored dY (the tied logits' gradient from the fused cross entropy): both operands bf16
-        if M % 8 or K % 8 or lda % 8 or x2.stride(0) != K or not is_bf16(x2):
+        # a bf16-stored dY (the tied logits' gradient from the fused cross entropy, an activation's bf16
+        # gradient from asrx_act_bwd_bias); X fp32 or bf16
+        xb = is_bf16(x2)
+        if M % 8 or K % (8 if xb else 4) or lda % 8 or x2.stride(0) != K or A.data_ptr() % 16 or x2.data_ptr() % 16:
             A = A.float()
         else:
             lib.require_gpu(A, x2, out)
             e0 = probe.begin("gemm")
-            lib.call("asrx_wgrad_bf16_ab", lib.ptr(A), lda, lib.ptr(x2), K, lib.ptr(out), out.stride(0), M, K, rows,
-                     sk, lib.stream())
-            probe.end("gemm", e0, 2.0 * M * K * rows, ("wgrad", M, K, rows, sk, 2))
+            lib.call("asrx_wgrad_bf16_ab", lib.ptr(A), lda, lib.ptr(x2), int(xb), K, lib.ptr(out), out.stride(0), M, K,
+                     rows, sk, lib.stream())
+            probe.end("gemm", e0, 2.0 * M * K * rows, ("wgrad", M, K, rows, sk, 2 + int(xb)))
             return out
     if is_bf16(x2):
         # a bf16-stored activation: the register-staged bf16 kernel at every shape (its X bytes halve)

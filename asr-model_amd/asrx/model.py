@@ -78,10 +78,11 @@ class AbbyNormal(nn.Module):
         self.mode_router = nn.Sequential(nn.Linear(dims, dims), nn.SiLU(), nn.Linear(dims, 3))
 
     def run(self, x, noise: NoiseCtx, site: str, sid_base: int, L: int, H: int = 1, out_bf16: bool = False,
-            tgate=None):
+            tgate=None, residual=None):
         """out_bf16: the output only feeds GEMM / attention operands (stored bf16 in perf mode); tgate: the
-        consuming tgate (its cs Linear(d, 3) is evaluated inside the norm's kernel)."""
-        return ops.abby_normal(self, x, L, H, sid_base, noise.key(site), True, out_bf16, tgate)
+        consuming tgate (its cs Linear(d, 3) is evaluated inside the norm's kernel); residual: returns
+        residual + AbbyNormal(x) (the add fused into the norm's kernel in perf mode)."""
+        return ops.abby_normal(self, x, L, H, sid_base, noise.key(site), True, out_bf16, tgate, residual)
 
 
 class LayerNorm(nn.Module):
@@ -286,9 +287,10 @@ class attention(nn.Module):  # noqa: N801
         q = ops.rotary(q, x, rotary_freqs(D, H, masked, x.device), hd, self.scale)
         return self.ln.run(q.view(B, L, H, hd), noise, site + ".qh", sid_base, L, H, out_bf16=prec.attn_bf16_io())
 
-    def run(self, x, kv, noise, site, sid_base, masked):
+    def run(self, x, kv, noise, site, sid_base, masked, residual=None):
         """x: attention input (B, Lq, D); kv: None (self attention on x) or (k, v) of the cross
-        source.  Returns the out-projected (B, Lq, D)."""
+        source.  Returns the out-projected (B, Lq, D), plus `residual` when given (the residual add
+        of model.py:578-580 fused into the out projection's epilogue)."""
         B, L, D = x.shape
         x = ops.fork(x)  # read by the q (and, self-attention, kv) AbbyNormal and rotary's |x|
         if kv is None:
@@ -301,6 +303,8 @@ class attention(nn.Module):  # noqa: N801
         # debug_storage_grad.py).  So o is stored bf16 only without a backward (dead blocks, eval).
         o = ops.attention(q, kv[0], kv[1], masked, out_bf16=not ops._grad_needed(q, kv[0], kv[1]),
                           merge_heads=True)
+        if residual is not None:
+            return ops.linear_residual(residual, o, self.out[1].weight, self.out[1].bias)
         return ops.linear(o, self.out[1].weight, self.out[1].bias)  # o: (B, L, D), heads merged
 
 
@@ -448,16 +452,15 @@ class residual(nn.Module):  # noqa: N801  (model.py:559-583)
         h = self.ln.run(x, noise, site + ".ln0", sid_base, L)
         x = ops.fork(self.jump.run(h, noise, site + ".jump", sid_base))  # each x: an AbbyNormal + an add
         h = self.ln.run(x, noise, site + ".ln1", sid_base, L)
-        x = ops.fork(ops.add(x, self.attn.run(h, None, noise, site + ".sa", sid_base, masked)))
+        x = ops.fork(self.attn.run(h, None, noise, site + ".sa", sid_base, masked, residual=x))
         if kv is not None:
             h = self.ln.run(x, noise, site + ".ln2", sid_base, L)
-            x = ops.fork(ops.add(x, self.attn.run(h, kv, noise, site + ".ca", sid_base, False)))
+            x = ops.fork(self.attn.run(h, kv, noise, site + ".ca", sid_base, False, residual=x))
         m = self.ln.run(x, noise, site + ".mlp.ln0", sid_base, L, out_bf16=True, tgate=self.mlp[1])
         m = ops.tgate(self.mlp[1], m, out_bf16=True)
         m = ops.linear(m, self.mlp[2].weight, self.mlp[2].bias, act="gelu", out_bf16=True)
         m = ops.linear(m, self.mlp[4].weight, self.mlp[4].bias)
-        m = self.ln.run(m, noise, site + ".mlp.ln1", sid_base, L)
-        return ops.add(x, m)
+        return self.ln.run(m, noise, site + ".mlp.ln1", sid_base, L, residual=x)  # x + mlp(x), model.py:583
 
     def xa_side(self, xa, noise: NoiseCtx, site: str, sid_base: int):
         """The cross source of residual.forward (model.py:579-582): xa + PE -> AbbyNormal -> MSheath

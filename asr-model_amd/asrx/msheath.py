@@ -206,10 +206,18 @@ class MSheathFn(torch.autograd.Function):
         da1 = G.linear_dgrad(dhh, m2l.weight)
         G.linear_wgrad(dhh, sv["a1"], out=gb(m2l.weight), accumulate=True)
         ops.colsum(dhh.view(rows, D), out=gb(m2l.bias))
-        lib.call("asrx_act_bwd", _P(da1), _P(sv["z1"]), _P(da1), da1.numel(), SILU, st)
+        H1 = da1.shape[-1]
+        if prec.get() == prec.PREC_BF16 and H1 % 8 == 0 and G.use_wide(H1):
+            # perf mode: silu' applied, the gradient stored bf16 for both GEMMs, mlp[0]'s bias gradient
+            # summed in the same pass
+            ga1 = _E(da1.shape, dtype=torch.bfloat16, device=dev)
+            lib.call("asrx_act_bwd_bias", _P(da1), _P(sv["z1"]), _P(ga1), _P(gb(m0.bias)), rows, H1, SILU, st)
+            da1 = ga1
+        else:
+            lib.call("asrx_act_bwd", _P(da1), _P(sv["z1"]), _P(da1), da1.numel(), SILU, st)
+            ops.colsum(da1.view(rows, -1), out=gb(m0.bias))
         dhln = G.linear_dgrad(da1, m0.weight)
         G.linear_wgrad(da1, sv["hln"], out=gb(m0.weight), accumulate=True)
-        ops.colsum(da1.view(rows, -1), out=gb(m0.bias))
         lib.call("asrx_layernorm_bwd_acc", _P(dhln), _P(x), _P(mod.mlp_ln.weight), _P(sv["mean2"]), _P(sv["rstd2"]),
                  _P(dx), _P(gb(mod.mlp_ln.weight)), _P(gb(mod.mlp_ln.bias)), rows, D, 1, st)
         del dhh, da1, dhln

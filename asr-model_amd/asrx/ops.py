@@ -278,7 +278,16 @@ class Linear(torch.autograd.Function):
         gy = grad_in(gy, ctx.osink)
         if gy is None:
             return None, None, None, None, None, None, None, None
-        if ctx.act != "none":
+        db_done = None
+        N = gy.shape[-1]
+        if ctx.act in ("gelu", "silu", "sigmoid") and prec.get() == prec.PREC_BF16 and N % 8 == 0 and G.use_wide(N):
+            # perf mode: act' applied, gz stored bf16 for the two GEMMs and the bias gradient summed in
+            # the same pass (no fp32 gz round trip, no separate column-sum pass)
+            gz = _E(gy.shape, dtype=torch.bfloat16, device=gy.device)
+            if ctx.has_b and ctx.needs_input_grad[2]:
+                db_done = _gbuf(b, True) if ctx.db else torch.zeros(N, device=gy.device)
+            lib.call("asrx_act_bwd_bias", _P(_c(gy)), _P(z), _P(gz), _P(db_done), _rows(gy), N, ACT[ctx.act], _S())
+        elif ctx.act != "none":
             gz = _E(gy.shape, device=gy.device)
             lib.call("asrx_act_bwd", _P(gy), _P(z), _P(gz), gy.numel(), ACT[ctx.act], _S())
         else:
@@ -295,7 +304,9 @@ class Linear(torch.autograd.Function):
             gW = _gbuf(W3, ctx.dW)
             G.linear_wgrad(gz, x, out=gW.view(W.shape), accumulate=True)
             dW = _gret(W3, gW, ctx.dW)
-        if ctx.has_b and ctx.needs_input_grad[2]:
+        if db_done is not None:
+            db = _gret(b, db_done, ctx.db)
+        elif ctx.has_b and ctx.needs_input_grad[2]:
             db = _gret(b, colsum(gz, out=_gbuf(b, True) if ctx.db else None), ctx.db)
         return dx, dW, db, None, None, None, None, None
 
@@ -309,6 +320,66 @@ def linear(x, W, b=None, act="none", out_bf16=False):
     grad = _grad_needed(x, W, b)
     osink = new_sink(out_bf16) if grad else None
     return out_sink(Linear.apply(x, W, b, act, grad, sink_of(x), out_bf16, osink), osink)
+
+
+class LinearRes(torch.autograd.Function):
+    """y = r + x W^T + b: the residual add around an out projection (model.py:578-580 x = x +
+    attn(...)) in the GEMM's epilogue (perf mode) -- no separate add pass; backward: r's gradient is y's
+    (passed through), x / W / b as Linear."""
+
+    @staticmethod
+    def forward(ctx, r, x, W, b, sink=None):
+        x, r = _c(x), _c(r)
+        ctx.sink = sink
+        ctx.set_materialize_grads(False)
+        x2 = x.view(-1, x.shape[-1])
+        if G.is_bf16(x2):
+            raise RuntimeError("LinearRes: the residual epilogue takes an fp32 x (use ops.linear_residual)")
+        M, K = x2.shape
+        N = W.shape[0]
+        y = _E(r.shape, device=r.device)
+        Wb = G.weight_bf16(W)
+        nj = G._nj(M, N)
+        e0 = probe.begin("gemm")
+        lib.call("asrx_gemm_wn_res", _P(x2), K, _P(Wb), Wb.stride(0), _P(y), N, _P(b), _P(r), N, M, N, K, nj, _S())
+        probe.end("gemm", e0, 2.0 * M * N * K, ("wn", M, N, K, nj, 0, "none", False, True, 0, 0, False))
+        ctx.dW, ctx.db = _direct(ctx, 2, W), _direct(ctx, 3, b)
+        ctx.save_for_backward(x, W, b if ctx.db else None)
+        ctx.has_b = b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, W, b = ctx.saved_tensors
+        if gy is None:
+            return None, None, None, None, None
+        gy = _f32(gy)
+        dx = None
+        if ctx.needs_input_grad[1]:
+            if ctx.sink is not None:
+                buf, acc = ctx.sink.target(x)
+                G.linear_dgrad(gy, W, out=buf, beta=float(acc))
+            else:
+                dx = G.linear_dgrad(gy, W)
+        dW = db = None
+        if ctx.needs_input_grad[2]:
+            gW = _gbuf(W, ctx.dW)
+            G.linear_wgrad(gy, x, out=gW, accumulate=True)
+            dW = _gret(W, gW, ctx.dW)
+        if ctx.has_b and ctx.needs_input_grad[3]:
+            db = _gret(b, colsum(gy, out=_gbuf(b, True) if ctx.db else None), ctx.db)
+        return gy if ctx.needs_input_grad[0] else None, dx, dW, db, None
+
+
+def linear_residual(r, x, W, b=None):
+    """r + nn.Linear(x): fused in perf mode (LinearRes), else add(r, linear(x))."""
+    N = W.shape[0]
+    K = x.shape[-1]
+    M = x.numel() // max(K, 1)
+    if (prec.get() == prec.PREC_BF16 and G.use_wide(K) and N % 4 == 0 and r.dtype == torch.float32
+            and x.dtype == torch.float32 and r.shape[-1] == N and x.is_cuda and G._nj(M, N) in (1, 3)):
+        return LinearRes.apply(r, x, W, b, sink_of(x))
+    return add(r, linear(x, W, b))
 
 
 class KVProjFn(torch.autograd.Function):
@@ -424,8 +495,9 @@ class AbbyNormalFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, W1, b1, W2, b2, L, H, sid_base, key, use_noise, keep, sink=None, out_bf16=False,
-                osink=None, tw=None, tb=None, side=None):
+                osink=None, tw=None, tb=None, side=None, res=None):
         x = _c(x)
+        ctx.has_res = res is not None
         ctx.sink = sink
         ctx.osink = osink
         ctx.set_materialize_grads(False)
@@ -444,7 +516,15 @@ class AbbyNormalFn(torch.autograd.Function):
         if decisions.active():  # record mode 2's per-feature max-vs-avg choices of this call
             cond = torch.zeros(rows, d, dtype=torch.uint8, device=x.device)
             lib.call("asrx_abby_record_cond", _P(cond))
-        if G.use_wide(d) and d <= 384:
+        if res is not None:  # out = res + AbbyNormal(x): the residual add in the same row pass
+            res = _c(res)
+            if G.use_wide(d) and d <= 384:
+                hpre, logits = G.router_fwd(x.view(rows, d), W1, b1, W2, keep)
+            else:
+                hpre, logits = G.linear_fwd(x, W1, b1), None
+            lib.call("asrx_abby_fwd_res", _P(x), _P(hpre), _P(W2), _P(logits), _P(b2), _P(res), _P(out), _P(ys),
+                     _P(idx), rows, d, L, H, sid_base, key & 0xFFFFFFFF, int(use_noise), _S())
+        elif G.use_wide(d) and d <= 384:
             # perf mode: the router's d x d GEMM also applies SiLU and Linear(d, 3) in its epilogue,
             # so h_pre never makes the HBM round trip unless the backward needs it
             hpre, logits = G.router_fwd(x.view(rows, d), W1, b1, W2, keep)
@@ -466,7 +546,7 @@ class AbbyNormalFn(torch.autograd.Function):
         x, hpre, W1, W2, ys, idx, b1, b2 = ctx.saved_tensors
         gout = grad_in(gout, ctx.osink)
         if gout is None:
-            return (None,) * 17
+            return (None,) * 18
         d = x.shape[-1]
         rows = _rows(x)
         fW1, fb1, fW2, fb2 = ctx.dp
@@ -484,13 +564,18 @@ class AbbyNormalFn(torch.autograd.Function):
         dW1 = G.linear_wgrad(dh, x, out=_gbuf(W1, fW1), accumulate=True)
         db1 = colsum(dh.view(-1, d), out=_gbuf(b1, fb1))
         return (dx, _gret(W1, dW1, fW1), _gret(b1, db1, fb1), _gret(W2, dW2, fW2), _gret(b2, db2, fb2),
-                None, None, None, None, None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None, None, None, None,
+                gout if ctx.has_res and ctx.needs_input_grad[17] else None)
 
 
-def abby_normal(mod, x, L, H, sid_base, key, use_noise=True, out_bf16=False, tgate=None):
+def abby_normal(mod, x, L, H, sid_base, key, use_noise=True, out_bf16=False, tgate=None, residual=None):
     """AbbyNormal(x); out_bf16: the output only feeds GEMM / attention operands (bf16-stored in perf mode);
     tgate: the consuming tgate module, whose cs Linear(d, 3) the kernel evaluates on the fp32 output (the
-    output is then attached to the result for ops.tgate)."""
+    output is then attached to the result for ops.tgate); residual: return residual + AbbyNormal(x),
+    the add fused into the kernel (perf mode, H == 1, d >= 128)."""
+    if residual is not None and not (prec.get() == prec.PREC_BF16 and H == 1 and x.shape[-1] >= 128
+                                     and not out_bf16 and tgate is None and residual.dtype == torch.float32):
+        return add(residual, abby_normal(mod, x, L, H, sid_base, key, use_noise, out_bf16, tgate))
     if use_noise:
         _noise_rows_ok(sid_base + _rows(x) // max(L * H, 1), H, L, 3)
     r = mod.mode_router
@@ -501,7 +586,7 @@ def abby_normal(mod, x, L, H, sid_base, key, use_noise=True, out_bf16=False, tga
         tw, tb = tgate.cs[0].weight, tgate.cs[0].bias
     side = {}
     y = AbbyNormalFn.apply(x, r[0].weight, r[0].bias, r[2].weight, r[2].bias, L, H, sid_base, key, use_noise,
-                           keep, sink_of(x), out_bf16, osink, tw, tb, side)
+                           keep, sink_of(x), out_bf16, osink, tw, tb, side, residual)
     if tw is not None:
         y._asrx_tgate_c = (side["tgate_c"], tw)  # tgate's cs logits of these rows, for ops.tgate
     return out_sink(y, osink)

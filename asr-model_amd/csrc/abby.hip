@@ -33,6 +33,9 @@ struct AbbyGeom {
   // decision recorder (parity tests only, null otherwise): the forward writes mode 2's per-feature
   // choice (max > 2 avg, essentials.py:176-177) of every row that picked mode 2, cond[r * d + f]
   unsigned char* cond;
+  // residual input (d >= 128 forward, fp32 out): out = res + x / denom -- the block's closing residual
+  // add (model.py:583 x + mlp(x) with mlp's last AbbyNormal) without a separate add pass
+  const float* res;
 };
 
 // Per-row layout (MI355X design): lane l owns the E = d/64 CONSECUTIVE features [l E, l E + E), read
@@ -349,6 +352,12 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_fwd_kernel(const float* 
       const float2 dn = *reinterpret_cast<const float2*>(drow + 128 * j + 2 * lane);
       ov[2 * j] = xv[2 * j] / dn.x;
       ov[2 * j + 1] = xv[2 * j + 1] / dn.y;
+    }
+    if (g.res) {
+      float rv[E];
+      ld_rowc<E>(g.res + r * S::D, lane, rv);
+#pragma unroll
+      for (int e = 0; e < E; ++e) ov[e] += rv[e];
     }
     st_rowc<E>(out + r * S::D, lane, ov);
     if (tw) {
@@ -914,6 +923,7 @@ static AbbyGeom make_geom(int64_t rows, int64_t d, int64_t L, int64_t H, int64_t
                           int use_noise) {
   AbbyGeom g;
   g.cond = nullptr;
+  g.res = nullptr;
   g.rows = rows;
   g.d = d;
   g.L = L > 0 ? L : 1;
@@ -995,6 +1005,26 @@ extern "C" int asrx_abby_fwd_logits2(const float* x, const float* logits, const 
     ABBY_DISPATCH_T(abby_fwd_kernel, float, x, nullptr, nullptr, b2, (float*)out, ys, idx, g, logits, tw, tb, tc);
   }
   ASRX_LAUNCHED("asrx_abby_fwd_logits");
+}
+
+// asrx_abby_fwd_logits2 / asrx_abby_fwd2 (hpre given, logits NULL) with a residual input: out = res +
+// AbbyNormal(x) (fp32 out, d >= 128).
+extern "C" int asrx_abby_fwd_res(const float* x, const float* hpre, const float* W2, const float* logits,
+                                 const float* b2, const float* res, float* out, float* ys, int* idx, int64_t rows,
+                                 int64_t d, int64_t L, int64_t H, int64_t sid_base, uint32_t key, int use_noise,
+                                 hipStream_t stream) {
+  ASRX_REQUIRE(d % 64 == 0 && d >= 128 && d <= 1024, "asrx_abby_fwd_res: d=%ld must be a multiple of 64 in [128,1024]",
+               (long)d);
+  ASRX_REQUIRE(res && res != out && (logits || (hpre && W2)), "asrx_abby_fwd_res: res (!= out) and logits or hpre/W2");
+  if (rows == 0) return 0;
+  const int E = (int)(d / 64);
+  AbbyGeom g = make_geom(rows, d, L, H, sid_base, key, use_noise);
+  g.cond = g_cond_record;
+  g.res = res;
+  const unsigned grid = (unsigned)std::min<int64_t>((rows + ABBY_WAVES - 1) / ABBY_WAVES, 4096);
+  ABBY_DISPATCH_T(abby_fwd_kernel, float, x, logits ? nullptr : hpre, logits ? nullptr : W2, b2, out, ys, idx, g,
+                  logits, nullptr, nullptr, nullptr);
+  ASRX_LAUNCHED("asrx_abby_fwd_res");
 }
 
 extern "C" int asrx_abby_fwd_logits(const float* x, const float* logits, const float* b2, float* out, float* ys,

@@ -7,6 +7,8 @@
 // This file holds the entry points and the exact-fp32 PARITY-mode kernels (v_mfma_f32_16x16x4f32,
 // no rounding of any operand); the perf modes live in attn_mf.hip (bf16) and attn_f8.hip (fp8 QK^T).
 //
+// Parity kernels use the accurate expf (not __expf): the model's scores reach ~1e3-1e4 (rotary scales q/k by
+// the source row norm), where the fast exp's argument rounding is visible in the whole-model parity.
 // Parity kernels: workgroup = 4 waves x 16 rows = 64 rows of one (b, h).  Every wave keeps the
 // A-operand fragments of its own 16 rows in registers for the whole sweep (HD/4 floats per lane per
 // operand: Q in the forward and dQ kernels, K and V in the dK/dV kernel); the swept operand is
@@ -147,7 +149,7 @@ __global__ __launch_bounds__(256) void attn_fwd_f32_kernel(const float* __restri
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float mn = fmaxf(m[r], tmax[r]);
-      alpha[r] = __expf(m[r] - mn);
+      alpha[r] = expf(m[r] - mn);
       m[r] = mn;
       rs[r] = 0.f;
     }
@@ -156,7 +158,7 @@ __global__ __launch_bounds__(256) void attn_fwd_f32_kernel(const float* __restri
     for (int n = 0; n < 4; ++n) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = __expf(s[n][r] - m[r]);
+        const float p = expf(s[n][r] - m[r]);
         rs[r] += p;
         P[(lr4 + r) * PST + n * 16 + lc] = p;
       }
@@ -194,8 +196,11 @@ __device__ __forceinline__ float ld_f(const unsigned short* p) {
 }
 
 // delta[b,h,i] = sum_d dO[b,i,h,d] * O[b,i,h,d]   (one wave per row, HD/64 elements per lane);
-// o / dO stored fp32 or bf16 (unsigned short)
-template <int HD, typename TO = float, typename TD = float>
+// o / dO stored fp32 or bf16 (unsigned short).  RD (bf16 mode): dO rounded to bf16 first, as the backward's
+// dP = dO V^T MFMA sees it -- dS = P (dP - delta) relies on sum_j P_ij dP_ij == delta_i, and an fp32
+// delta against a bf16 dP leaves a systematic row error that dominates dQ / dK where the values barely
+// vary over the keys
+template <int HD, typename TO = float, typename TD = float, bool RD = false>
 __global__ __launch_bounds__(256) void attn_delta_kernel(const TO* __restrict__ o, const TD* __restrict__ dO,
                                                          float* __restrict__ delta, AttnStrides so, AttnStrides sd,
                                                          int64_t B, int64_t H, int64_t Lq) {
@@ -205,9 +210,11 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const TO* __restrict__ 
     const int64_t i = r % Lq, bh = r / Lq, hh = bh % H, bb = bh / H;
     float s = 0.f;
 #pragma unroll
-    for (int e = 0; e < HD / 64; ++e)
-      s += ld_f(o + bb * so.b + i * so.l + hh * so.h + 64 * e + lane) *
-           ld_f(dO + bb * sd.b + i * sd.l + hh * sd.h + 64 * e + lane);
+    for (int e = 0; e < HD / 64; ++e) {
+      float g = ld_f(dO + bb * sd.b + i * sd.l + hh * sd.h + 64 * e + lane);
+      if constexpr (RD) g = (float)(__bf16)g;
+      s += ld_f(o + bb * so.b + i * so.l + hh * so.h + 64 * e + lane) * g;
+    }
     s = wave_sum(s);
     if (lane == 0) delta[r] = s;
   }
@@ -271,7 +278,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_f32_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int64_t key = kw + lr4 + r;
-        float p = __expf(st[r] * scale - lse_s[qcol]);
+        float p = expf(st[r] * scale - lse_s[qcol]);
         if (qi >= Lq || key >= Lk || (causal && key > qi)) p = 0.f;
         P[(lr4 + r) * PST + qcol] = p;
         D[(lr4 + r) * PST + qcol] = p * (dp[r] - del_s[qcol]);
@@ -349,7 +356,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_f32_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int64_t qi = qw + lr4 + r;
-        float p = __expf(s[r] * scale - lsev[r]);
+        float p = expf(s[r] * scale - lsev[r]);
         if (qi >= Lq || key >= Lk || (causal && key > qi)) p = 0.f;
         D[(lr4 + r) * PST + n * 16 + lc] = p * (dp[r] - delv[r]);
       }
@@ -467,22 +474,23 @@ extern "C" int asrx_attn_bwd2(int prec, int io, const void* q_, const int64_t* s
       Sdv{sdv[0], sdv[1], sdv[2]};
   const int64_t rows = B * H * Lq;
   const unsigned gd = (unsigned)std::min<int64_t>((rows + 3) / 4, 8192);
-#define ASRX_DL(HDV, TO, TD) \
-  attn_delta_kernel<HDV, TO, TD><<<gd, 256, 0, stream>>>((const TO*)o_, (const TD*)dO_, delta_ws, So, Sd, B, H, Lq)
+#define ASRX_DL(HDV, TO, TD, RD) \
+  attn_delta_kernel<HDV, TO, TD, RD><<<gd, 256, 0, stream>>>((const TO*)o_, (const TD*)dO_, delta_ws, So, Sd, B, H, Lq)
   const int dsel = ((io >> 1) & 1) | ((io >> 1) & 2);  // bit 0: o bf16, bit 1: dO bf16
+  const bool rd = prec == PREC_BF16;                  // fp32 dO rounded as the bf16 dP MFMA sees it
   if (hd == 64) {
     switch (dsel) {
-      case 0: ASRX_DL(64, float, float); break;
-      case 1: ASRX_DL(64, unsigned short, float); break;
-      case 2: ASRX_DL(64, float, unsigned short); break;
-      default: ASRX_DL(64, unsigned short, unsigned short); break;
+      case 0: if (rd) ASRX_DL(64, float, float, true); else ASRX_DL(64, float, float, false); break;
+      case 1: if (rd) ASRX_DL(64, unsigned short, float, true); else ASRX_DL(64, unsigned short, float, false); break;
+      case 2: ASRX_DL(64, float, unsigned short, false); break;
+      default: ASRX_DL(64, unsigned short, unsigned short, false); break;
     }
   } else {
     switch (dsel) {
-      case 0: ASRX_DL(128, float, float); break;
-      case 1: ASRX_DL(128, unsigned short, float); break;
-      case 2: ASRX_DL(128, float, unsigned short); break;
-      default: ASRX_DL(128, unsigned short, unsigned short); break;
+      case 0: if (rd) ASRX_DL(128, float, float, true); else ASRX_DL(128, float, float, false); break;
+      case 1: if (rd) ASRX_DL(128, unsigned short, float, true); else ASRX_DL(128, unsigned short, float, false); break;
+      case 2: ASRX_DL(128, float, unsigned short, false); break;
+      default: ASRX_DL(128, unsigned short, unsigned short, false); break;
     }
   }
 #undef ASRX_DL

@@ -56,6 +56,11 @@ template <>
 struct Stage<true, true> {
   u32x4 ah[2], bh[2];
 };
+template <>
+struct Stage<true, false> {
+  u32x4 ah[2];
+  float4 b[4];
+};
 
 template <bool ABF, bool BBF>
 __device__ __forceinline__ void load(const Params& p, Stage<ABF, BBF>& st, int64_t r0, int64_t rend, int m0, int n0) {
@@ -78,6 +83,14 @@ __device__ __forceinline__ void load(const Params& p, Stage<ABF, BBF>& st, int64
       const int64_t r = r0 + (t >> 4) + 16 * i;
       st.ah[i] = *reinterpret_cast<const u32x4*>((r < rend && m0 + cb < p.M) ? (const void*)(Ah + r * p.lda + m0 + cb)
                                                                             : (const void*)zero16);
+    }
+    if constexpr (!BBF) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t r = r0 + (t >> 5) + 8 * i;
+        st.b[i] = *reinterpret_cast<const float4*>((r < rend && n0 + c < p.N) ? (const void*)(p.B + r * p.ldb + n0 + c)
+                                                                              : (const void*)zero16);
+      }
     }
   } else {
 #pragma unroll
@@ -103,6 +116,15 @@ __device__ __forceinline__ void store(const Stage<ABF, BBF>& st, char* Ai, char*
   if constexpr (ABF) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) *reinterpret_cast<u32x4*>(Ai + off((t >> 4) + 16 * i, t & 15)) = st.ah[i];
+    if constexpr (!BBF) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = (t >> 5) + 8 * i;
+        bf16x4 hb4;
+        hb4[0] = (__bf16)st.b[i].x; hb4[1] = (__bf16)st.b[i].y; hb4[2] = (__bf16)st.b[i].z; hb4[3] = (__bf16)st.b[i].w;
+        *reinterpret_cast<bf16x4*>(Bi + off(row, ch) + 8 * hb) = hb4;
+      }
+    }
   } else {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -219,7 +241,7 @@ static int wgrad_launch(const void* A, int a_bf16, int64_t lda, const void* B, i
   ASRX_REQUIRE(M > 0 && N > 0 && R >= 0, "asrx_wgrad_bf16: empty problem");
   ASRX_REQUIRE(M % 4 == 0 && N % 4 == 0 && lda % 4 == 0 && ldb % 4 == 0, "asrx_wgrad_bf16: M, N, lda, ldb %% 4 required");
   ASRX_REQUIRE(!b_bf16 || (N % 8 == 0 && ldb % 8 == 0), "asrx_wgrad_bf16: a bf16 X needs N, ldb %% 8");
-  ASRX_REQUIRE(!a_bf16 || (b_bf16 && M % 8 == 0 && lda % 8 == 0), "asrx_wgrad_bf16: a bf16 dY needs a bf16 X and M, lda %% 8");
+  ASRX_REQUIRE(!a_bf16 || (M % 8 == 0 && lda % 8 == 0), "asrx_wgrad_bf16: a bf16 dY needs M, lda %% 8");
   ASRX_REQUIRE((((uintptr_t)A | (uintptr_t)B) & 15) == 0, "asrx_wgrad_bf16: operands must be 16-byte aligned");
   if (R == 0) return 0;
   if (splitk < 1) splitk = 1;
@@ -229,8 +251,10 @@ static int wgrad_launch(const void* A, int a_bf16, int64_t lda, const void* B, i
   wg::Params p{(const float*)A, (const float*)B, C, lda, ldb, ldc, (int)M, (int)N, R, kchunk, (int)splitk};
   const int64_t items = ((M + wg::TM - 1) / wg::TM) * ((N + wg::TN - 1) / wg::TN) * splitk;
   ASRX_REQUIRE(items < (1LL << 31), "asrx_wgrad_bf16: too many work items");
-  if (a_bf16)
+  if (a_bf16 && b_bf16)
     wg::wgrad_wr_kernel<true, true><<<(unsigned)items, wg::NT, 0, stream>>>(p);
+  else if (a_bf16)
+    wg::wgrad_wr_kernel<true, false><<<(unsigned)items, wg::NT, 0, stream>>>(p);
   else if (b_bf16)
     wg::wgrad_wr_kernel<false, true><<<(unsigned)items, wg::NT, 0, stream>>>(p);
   else
@@ -249,9 +273,10 @@ extern "C" int asrx_wgrad_bf16_ex(const float* A, int64_t lda, const void* B, in
   return wgrad_launch(A, 0, lda, B, b_bf16, ldb, C, ldc, M, N, R, splitk, stream);
 }
 
-// asrx_wgrad_bf16 with both dY (A) and X (B) stored bf16 (M, N, lda, ldb multiples of 8): the tied
-// token embedding's gradient from the bf16 logits gradient (model.py:629 tied logits).
-extern "C" int asrx_wgrad_bf16_ab(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, int64_t ldc,
-                                  int64_t M, int64_t N, int64_t R, int64_t splitk, hipStream_t stream) {
-  return wgrad_launch(A, 1, lda, B, 1, ldb, C, ldc, M, N, R, splitk, stream);
+// asrx_wgrad_bf16 with dY (A) stored bf16 (M, lda multiples of 8) and X (B) stored fp32 (b_bf16 = 0) or
+// bf16 (1; N, ldb multiples of 8): the tied token embedding's gradient from the bf16 logits gradient
+// (model.py:629) and the weight gradients under an activation (asrx_act_bwd_bias's bf16 gz).
+extern "C" int asrx_wgrad_bf16_ab(const void* A, int64_t lda, const void* B, int b_bf16, int64_t ldb, float* C,
+                                  int64_t ldc, int64_t M, int64_t N, int64_t R, int64_t splitk, hipStream_t stream) {
+  return wgrad_launch(A, 1, lda, B, b_bf16, ldb, C, ldc, M, N, R, splitk, stream);
 }

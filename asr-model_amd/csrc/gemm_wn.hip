@@ -158,6 +158,28 @@ extern "C" int asrx_gemm_wn_ce(const void* A, int64_t lda, const unsigned short*
   ASRX_LAUNCHED("asrx_gemm_wn_ce");
 }
 
+// Out projection with its residual add (model.py:578-580 x = x + attn(...).out): C = R + A W^T + bias, A, C
+// and R fp32 (R may not alias C), 16-byte aligned rows; nj 1 or 3 (the residual epilogue is compiled into
+// dedicated instantiations only, so the other GEMMs keep their register budget).
+extern "C" int asrx_gemm_wn_res(const float* A, int64_t lda, const unsigned short* W, int64_t ldw, float* C, int64_t ldc,
+                                const float* bias, const float* R, int64_t ldr, int64_t M, int64_t N, int64_t K, int nj,
+                                hipStream_t stream) {
+  ASRX_REQUIRE(M > 0 && N > 0 && K > 0, "asrx_gemm_wn_res: empty problem");
+  ASRX_REQUIRE(((uintptr_t)A & 15) == 0 && ((uintptr_t)W & 15) == 0 && ((uintptr_t)C & 15) == 0 &&
+                   ((uintptr_t)R & 15) == 0,
+               "asrx_gemm_wn_res: A/W/C/R must be 16-byte aligned");
+  ASRX_REQUIRE(K % 8 == 0 && lda % 4 == 0 && ldw % 8 == 0 && N % 4 == 0 && ldc % 4 == 0 && ldr % 4 == 0,
+               "asrx_gemm_wn_res: K, ldw %% 8; lda, N, ldc, ldr %% 4");
+  ASRX_REQUIRE(M * lda < (1LL << 31) && N * ldw < (1LL << 31), "asrx_gemm_wn_res: operand spans >= 2^31 elements");
+  ASRX_REQUIRE(R && R != C, "asrx_gemm_wn_res: a residual input distinct from C is required");
+  ASRX_REQUIRE(nj == 1 || nj == 3, "asrx_gemm_wn_res: nj 1 or 3");
+  wn::Params p{A, (int)lda, W, (int)ldw, C, (int)ldc, bias, nullptr, (int)M, (int)N, (int)K, 1, 1, 1.f, 0.f,
+               ACT_NONE, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, R, (int)ldr};
+  if (nj == 3) wn::launch_wr<3, false, false, false, false, true>(p, stream);
+  else wn::launch_wr<1, false, false, false, false, true>(p, stream);
+  ASRX_LAUNCHED("asrx_gemm_wn_res");
+}
+
 // asrx_gemm_wn restricted to the BM-row tiles listed in mtiles (n_mtiles entries, both on the device,
 // from asrx_row_tiles); rows of other tiles are not written.
 extern "C" int asrx_gemm_wn_rows(const float* A, int64_t lda, const unsigned short* W, int64_t ldw, float* C,

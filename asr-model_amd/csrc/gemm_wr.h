@@ -62,6 +62,10 @@ struct Params {
   // the logits for its log-sum-exp (asrx_ce_part_fwd merges the partials)
   float2* ce_part;
   int ce_ld;
+  // residual input (gemm_wr epilogues, act none, fp32 C): C = R + alpha A W^T + bias -- the residual add
+  // around an out projection (model.py:578-580 x = x + attn(...)) without a separate add pass
+  const float* Rres;
+  int ldr;
 };
 
 __device__ __forceinline__ void st_bf16x4(unsigned short* dst, float a, float b, float c, float d) {
@@ -137,6 +141,7 @@ __device__ __forceinline__ void epilogue(const Params& p, f32x4 (&acc)[4][2 * NJ
           const float4 o = *reinterpret_cast<const float4*>(dst);
           v[0] += p.beta * o.x; v[1] += p.beta * o.y; v[2] += p.beta * o.z; v[3] += p.beta * o.w;
         }
+
         if (zdst) __builtin_nontemporal_store(f32x4{v[0], v[1], v[2], v[3]}, reinterpret_cast<f32x4*>(zdst));
         __builtin_nontemporal_store(f32x4{act_t<ACT>(v[0]), act_t<ACT>(v[1]), act_t<ACT>(v[2]), act_t<ACT>(v[3])},
                                     reinterpret_cast<f32x4*>(dst));
@@ -165,7 +170,7 @@ struct EpLds {
   static constexpr int LD = W + EP_PAD;       // slab row stride (floats)
   static constexpr int FLOATS = 16 * LD;      // one 16-row slice
 };
-template <int NJ, int ACT>
+template <int NJ, int ACT, bool RES = false>
 __device__ __forceinline__ void epilogue_lds(const Params& p, f32x4 (&acc)[4][2 * NJ], const float* bsl, int m0,
                                              int n0, int wm, int wn, int lr, int lk, float* ep) {
   constexpr int NT = 2 * NJ, W = EpLds<NJ>::W, LD = EpLds<NJ>::LD, W4 = W / 4;
@@ -204,6 +209,10 @@ __device__ __forceinline__ void epilogue_lds(const Params& p, f32x4 (&acc)[4][2 
       if (p.beta != 0.f) {
         const float4 o = *reinterpret_cast<const float4*>(dst);
         x.x += p.beta * o.x; x.y += p.beta * o.y; x.z += p.beta * o.z; x.w += p.beta * o.w;
+      }
+      if constexpr (RES) {  // the residual add of an out projection (RES instantiations only)
+        const float4 o = *reinterpret_cast<const float4*>(p.Rres + (int64_t)row * p.ldr + col);
+        x.x += o.x; x.y += o.y; x.z += o.z; x.w += o.w;
       }
       if (p.Z)
         __builtin_nontemporal_store(f32x4{x.x, x.y, x.z, x.w},
@@ -457,7 +466,7 @@ __device__ __forceinline__ void wr_store(const WrStage<NJ, ABF>& st, char* At, c
   }
 }
 
-template <int NJ, bool CONV, bool RT, int DEP = 0, bool ABF = false, bool CE = false>
+template <int NJ, bool CONV, bool RT, int DEP = 0, bool ABF = false, bool CE = false, bool RES = false>
 __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) {  // ntiles: all tiles
   typedef Cfg<NJ> CF;
   constexpr int BN = CF::BN, NT = 2 * NJ, BNR = CF::BNR;
@@ -567,6 +576,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
         epilogue_router<NJ>(p, acc, bsl, w2s, red, m0, wm, wn, lr, lk);
       } else if constexpr (CE) {
         epilogue_ce<NJ>(p, acc, m0, n0, wm, wn, lr, lk, ep, reinterpret_cast<float2*>(red));
+      } else if constexpr (RES) {  // act none, vec_ok (checked by the launcher)
+        epilogue_lds<NJ, ACT_NONE, true>(p, acc, bsl, m0, n0, wm, wn, lr, lk, ep);
       } else if (WR_EPI_LDS && vec) switch (p.act) {
         case ACT_GELU: epilogue_lds<NJ, ACT_GELU>(p, acc, bsl, m0, n0, wm, wn, lr, lk, ep); break;
         case ACT_SILU: epilogue_lds<NJ, ACT_SILU>(p, acc, bsl, m0, n0, wm, wn, lr, lk, ep); break;
@@ -614,10 +625,10 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
 template <bool ABF>
 constexpr int wr_dep() { return ABF ? 4 : 0; }
 
-template <int NJ, bool CONV, bool RT = false, bool ABF = false, bool CE = false>
+template <int NJ, bool CONV, bool RT = false, bool ABF = false, bool CE = false, bool RES = false>
 void launch_wr(const Params& p, hipStream_t s) {
   static int resident = 0;
-  const void* fn = (const void*)gemm_wr_kernel<NJ, CONV, RT, wr_dep<ABF>(), ABF, CE>;
+  const void* fn = (const void*)gemm_wr_kernel<NJ, CONV, RT, wr_dep<ABF>(), ABF, CE, RES>;
   if (!resident) {
     int per_cu = 0, dev = 0, cus = 0;
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, NTHR, 0);
@@ -629,7 +640,7 @@ void launch_wr(const Params& p, hipStream_t s) {
   const int grid = std::min(tiles, resident);
   // a 5-deep pipeline (DEP = 5) for the one-wave 8192-row text-side launches measured 32.4 us vs
   // 30.1 us at depth 3 (profiles/r02_bench_v8_kernel_stats.csv): their time is not load latency
-  gemm_wr_kernel<NJ, CONV, RT, wr_dep<ABF>(), ABF, CE><<<grid, NTHR, 0, s>>>(p, tiles);
+  gemm_wr_kernel<NJ, CONV, RT, wr_dep<ABF>(), ABF, CE, RES><<<grid, NTHR, 0, s>>>(p, tiles);
 }
 
 }  // namespace wn
@@ -640,9 +651,11 @@ void launch_wr(const Params& p, hipStream_t s) {
 #ifndef ASRX_WR_INSTANTIATE
 #define ASRX_WR_DECL(NJ, CONV, RT, ABF) extern template void asrx::wn::launch_wr<NJ, CONV, RT, ABF>(const asrx::wn::Params&, hipStream_t);
 #define ASRX_WR_DECL_CE(NJ) extern template void asrx::wn::launch_wr<NJ, false, false, true, true>(const asrx::wn::Params&, hipStream_t);
+#define ASRX_WR_DECL_RES(NJ) extern template void asrx::wn::launch_wr<NJ, false, false, false, false, true>(const asrx::wn::Params&, hipStream_t);
 #else
 #define ASRX_WR_DECL(NJ, CONV, RT, ABF) template void asrx::wn::launch_wr<NJ, CONV, RT, ABF>(const asrx::wn::Params&, hipStream_t);
 #define ASRX_WR_DECL_CE(NJ) template void asrx::wn::launch_wr<NJ, false, false, true, true>(const asrx::wn::Params&, hipStream_t);
+#define ASRX_WR_DECL_RES(NJ) template void asrx::wn::launch_wr<NJ, false, false, false, false, true>(const asrx::wn::Params&, hipStream_t);
 #endif
 #define ASRX_WR_SET(NJ) ASRX_WR_DECL(NJ, false, false, false) ASRX_WR_DECL(NJ, true, false, false) \
   ASRX_WR_DECL(NJ, false, false, true) ASRX_WR_DECL(NJ, true, false, true) ASRX_WR_DECL(NJ, false, true, false)
@@ -653,4 +666,6 @@ ASRX_WR_SET(3)
 ASRX_WR_DECL_CE(1)
 ASRX_WR_DECL_CE(2)
 ASRX_WR_DECL_CE(3)
+ASRX_WR_DECL_RES(1)
+ASRX_WR_DECL_RES(3)
 #endif

@@ -1126,6 +1126,51 @@ __global__ void act_bwd_kernel(const float* __restrict__ g, const float* __restr
   }
 }
 
+// Backward of act(x W^T + b) below the GEMM, perf mode: gz = g * act'(z) stored bf16 (it only feeds the
+// input- and weight-gradient GEMMs, which round it to bf16 anyway) and the bias gradient
+// db += sum_rows gz (fp32, before rounding) in the same pass -- replaces act_bwd (fp32 gz) plus a
+// separate colsum pass over it.  grid (ceil(N / 256), row chunks); lane -> 4 consecutive columns,
+// the 4 waves of a workgroup take rows r0 + w, r0 + w + 4, ...; N % 4 == 0.
+template <int ACT>
+__global__ __launch_bounds__(256) void act_bwd_bias_kernel(const float* __restrict__ g, const float* __restrict__ z,
+                                                           unsigned short* __restrict__ gz, float* __restrict__ db,
+                                                           int64_t rows, int N, int64_t chunk) {
+  __shared__ float4 red[4][64];
+  const int lane = threadIdx.x & 63, part = threadIdx.x >> 6;
+  const int c = 4 * (blockIdx.x * 64 + lane);
+  const int64_t r0 = (int64_t)blockIdx.y * chunk, r1 = min(rows, r0 + chunk);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto dact = [](float v) {
+    if constexpr (ACT == ACT_GELU) return gelu_grad(v);
+    else if constexpr (ACT == ACT_SILU) return silu_grad(v);
+    else {
+      const float sg = sigmoid_f(v);
+      return sg * (1.f - sg);
+    }
+  };
+  if (c < N) {
+#pragma unroll 2
+    for (int64_t r = r0 + part; r < r1; r += 4) {
+      const float4 gv = *reinterpret_cast<const float4*>(g + r * N + c);
+      const float4 zv = *reinterpret_cast<const float4*>(z + r * N + c);
+      const float4 o = make_float4(gv.x * dact(zv.x), gv.y * dact(zv.y), gv.z * dact(zv.z), gv.w * dact(zv.w));
+      acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
+      typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+      const bf16x4 h = {(__bf16)o.x, (__bf16)o.y, (__bf16)o.z, (__bf16)o.w};
+      *reinterpret_cast<bf16x4*>(gz + r * N + c) = h;
+    }
+  }
+  red[part][lane] = acc;
+  __syncthreads();
+  if (part == 0 && c < N && db) {
+    const float4 a = red[0][lane], b = red[1][lane], cc = red[2][lane], d = red[3][lane];
+    atomicAdd(db + c + 0, a.x + b.x + cc.x + d.x);
+    atomicAdd(db + c + 1, a.y + b.y + cc.y + d.y);
+    atomicAdd(db + c + 2, a.z + b.z + cc.z + d.z);
+    atomicAdd(db + c + 3, a.w + b.w + cc.w + d.w);
+  }
+}
+
 // GLU over channels (nn.GLU(dim=1), model.py:97) on channels-last rows of 2C: out = a * sigmoid(b)
 __global__ void glu_fwd_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t rows, int C) {
   const int64_t total = rows * C;
@@ -2288,6 +2333,23 @@ int asrx_act_bwd(const float* g, const float* x, float* dx, int64_t n, int act, 
   if (n == 0) return 0;
   LAUNCH_EW(act_bwd_kernel, n, g, x, dx, n, act);
   ASRX_LAUNCHED("asrx_act_bwd");
+}
+
+int asrx_act_bwd_bias(const float* g, const float* z, unsigned short* gz, float* db, int64_t rows, int64_t N, int act,
+                      hipStream_t stream) {
+  ASRX_REQUIRE(N % 4 == 0 && (((uintptr_t)g | (uintptr_t)z) & 15) == 0 && ((uintptr_t)gz & 7) == 0,
+               "asrx_act_bwd_bias: N %% 4 == 0 and aligned rows required");
+  ASRX_REQUIRE(act == ACT_GELU || act == ACT_SILU || act == ACT_SIGMOID, "asrx_act_bwd_bias: gelu/silu/sigmoid only");
+  if (rows == 0) return 0;
+  const int gx = (int)((N / 4 + 63) / 64);
+  int64_t chunks = std::max<int64_t>(1, std::min<int64_t>((rows + 63) / 64, 2048 / gx));
+  const int64_t chunk = (rows + chunks - 1) / chunks;
+  chunks = (rows + chunk - 1) / chunk;
+  const dim3 grid((unsigned)gx, (unsigned)chunks);
+  if (act == ACT_GELU) act_bwd_bias_kernel<ACT_GELU><<<grid, 256, 0, stream>>>(g, z, gz, db, rows, (int)N, chunk);
+  else if (act == ACT_SILU) act_bwd_bias_kernel<ACT_SILU><<<grid, 256, 0, stream>>>(g, z, gz, db, rows, (int)N, chunk);
+  else act_bwd_bias_kernel<ACT_SIGMOID><<<grid, 256, 0, stream>>>(g, z, gz, db, rows, (int)N, chunk);
+  ASRX_LAUNCHED("asrx_act_bwd_bias");
 }
 
 int asrx_glu_fwd(const float* x, float* y, int64_t rows, int64_t C, hipStream_t stream) {

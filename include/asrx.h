@@ -131,6 +131,12 @@ int asrx_abby_record_cond(unsigned char* buf);
 int asrx_abby_fwd(const float* x, const float* hpre, const float* W2, const float* b2, float* out, float* ys,
                   int* idx, int64_t rows, int64_t d, int64_t L, int64_t H, int64_t sid_base, uint32_t key,
                   int use_noise, asrx_stream_t stream);
+/* AbbyNormal with a residual input: out = res + AbbyNormal(x) (fp32, d >= 128), router logits given (rows x 3,
+ * no b2) or computed from hpre / W2 (logits NULL) -- the closing residual add of residual.forward
+ * (model.py:583) fused into the mlp's last norm. */
+int asrx_abby_fwd_res(const float* x, const float* hpre, const float* W2, const float* logits, const float* b2,
+                      const float* res, float* out, float* ys, int* idx, int64_t rows, int64_t d, int64_t L, int64_t H,
+                      int64_t sid_base, uint32_t key, int use_noise, asrx_stream_t stream);
 /* dx, dhpre overwritten; dW2 (3,d) / db2 (3) accumulated. */
 /* AbbyNormal forward from precomputed router logits (rows x 3, no b2) -- asrx_gemm_wn_router. */
 int asrx_abby_fwd_logits(const float* x, const float* logits, const float* b2, float* out, float* ys, int* idx,
@@ -470,10 +476,21 @@ int asrx_ce_part_fwd(const float* part, int64_t nparts, const unsigned short* zb
                      float* lse, float* loss, float* count, int64_t rows, int64_t V, asrx_stream_t stream);
 int asrx_ce_bwd_bf16(const unsigned short* zb, const int64_t* labels, const float* lse, const float* g,
                      const float* count, unsigned short* dzb, int64_t rows, int64_t V, asrx_stream_t stream);
-/* asrx_wgrad_bf16 with dY and X both stored bf16 (M, N, lda, ldb % 8): the tied token embedding's
- * gradient from the bf16 logits gradient. */
-int asrx_wgrad_bf16_ab(const void* A, int64_t lda, const void* B, int64_t ldb, float* C, int64_t ldc, int64_t M,
-                       int64_t N, int64_t R, int64_t splitk, asrx_stream_t stream);
+/* out projection with its residual add (model.py:578-580): C = R + A W^T + bias; A, C, R fp32, R != C,
+ * 16-byte aligned rows, nj 1 or 3. */
+int asrx_gemm_wn_res(const float* A, int64_t lda, const unsigned short* W, int64_t ldw, float* C, int64_t ldc,
+                     const float* bias, const float* R, int64_t ldr, int64_t M, int64_t N, int64_t K, int nj,
+                     asrx_stream_t stream);
+/* act(x W^T + b) backward in perf mode (model.py:147, 505, 573): gz = g * act'(z) stored bf16 (rows x N,
+ * it only feeds the gradient GEMMs) and db += column sums of gz (fp32; db may be NULL); act gelu /
+ * silu / sigmoid, N % 4 == 0. */
+int asrx_act_bwd_bias(const float* g, const float* z, unsigned short* gz, float* db, int64_t rows, int64_t N, int act,
+                      asrx_stream_t stream);
+/* asrx_wgrad_bf16 with dY stored bf16 (M, lda % 8) and X stored fp32 (b_bf16 = 0) or bf16 (1: N, ldb % 8):
+ * the tied token embedding's gradient from the bf16 logits gradient, weight gradients under an
+ * activation (asrx_act_bwd_bias). */
+int asrx_wgrad_bf16_ab(const void* A, int64_t lda, const void* B, int b_bf16, int64_t ldb, float* C, int64_t ldc,
+                       int64_t M, int64_t N, int64_t R, int64_t splitk, asrx_stream_t stream);
 /* BatchNorm1d running statistics from per-clip (B, C) mean / rstd (ConvLite.bn, model.py:101);
  * nbt (num_batches_tracked, int64) may be NULL.  asrx_rsqrt_eps: eval-mode rstd. */
 int asrx_bn_running(const float* mean, const float* rstd, float* rm, float* rv, int64_t* nbt, int64_t B, int64_t C,

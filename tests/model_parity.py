@@ -112,11 +112,15 @@ ANALYTIC_ZERO = (".router.", ".depth.bias")
 
 
 def compare(cfg, B=1, seconds=30.0, T=256, precision="bf16", train=True, grads=True, seed=0, noise=(7, 3),
-            model_seed=0, device="cuda", decisions=False, replay=False, hip_mel=False, pitch_frames=None):
+            model_seed=0, device="cuda", decisions=False, replay=False, hip_mel=False, pitch_frames=None,
+            yardstick=False):
     """Run the HIP Model and the oracle on the same inputs; return a dict of metrics.
     decisions: record both sides' hard decisions and report their agreement.  replay: re-run the oracle
     consuming the HIP decisions and compare every parameter gradient.  hip_mel: feed the HIP model the
-    HIP log-mel of the clips (the benchmarked chain), the oracle its float64 mel."""
+    HIP log-mel of the clips (the benchmarked chain), the oracle its float64 mel.  yardstick (with
+    replay): also run the oracle in float32 on the same replayed trajectory -- the reference's own
+    arithmetic at fp32 -- and report its distance from the float64 oracle (yard_*): the model's fp32
+    conditioning, against which the HIP fp32 path is gated."""
     from asrx import decisions as hdec
     from asrx import prec
     from asrx.model import Model
@@ -146,16 +150,17 @@ def compare(cfg, B=1, seconds=30.0, T=256, precision="bf16", train=True, grads=T
     t_gpu = time.perf_counter() - t0
     ocfg = {"dims": cfg.dims, "head": cfg.head, "layer": cfg.layer}
 
-    def run_oracle(dec):
-        P = {k: (v.double().requires_grad_(True) if v.is_floating_point() else v) for k, v in sd.items()}
+    def run_oracle(dec, dtype=torch.float64):
+        P = {k: (v.to(dtype).requires_grad_(True) if v.is_floating_point() else v) for k, v in sd.items()}
         om.use_decisions(dec)
         try:
-            r = om.forward(P, ocfg, x["text_ids"], x["labels"], spectrogram=x["spectrogram"], pitch=x["pitch"],
-                           waveform=x["waveform"], seed=noise[0], step=noise[1], training=train, live_only=True)
+            r = om.forward(P, ocfg, x["text_ids"], x["labels"], spectrogram=x["spectrogram"].to(dtype),
+                           pitch=x["pitch"].to(dtype), waveform=x["waveform"].to(dtype), seed=noise[0],
+                           step=noise[1], training=train, live_only=True, dtype=dtype)
             r["loss"].backward()
         finally:
             om.use_decisions(None)
-        return P, {"logits": r["logits"].detach(), "loss": float(r["loss"])}
+        return P, {"logits": r["logits"].detach().double(), "loss": float(r["loss"].detach())}
 
     ck = (repr(cfg), B, seconds, T, train, seed, noise, model_seed, pitch_frames)
     t0 = time.perf_counter()
@@ -174,9 +179,12 @@ def compare(cfg, B=1, seconds=30.0, T=256, precision="bf16", train=True, grads=T
     res_extra = {}
     if decisions:
         res_extra["decisions"] = agreement(hip_dec, ref_dec)
+    P32 = ref32 = None
     if replay:
         rp = om.Decisions(table=hip_dec)
         P_r, ref_r = run_oracle(rp)
+        if yardstick:
+            P32, ref32 = run_oracle(om.Decisions(table=hip_dec), torch.float32)
         res_extra["replayed"] = rp.replayed
         res_extra["overridden"] = rp.overridden
         res_extra["cond_overridden"] = rp.cond_overridden
@@ -231,6 +239,21 @@ def compare(cfg, B=1, seconds=30.0, T=256, precision="bf16", train=True, grads=T
                                       reverse=True)[:8]
         res["grads_missing"] = missing
         res["zero_grad_residue"] = max(residue.values(), default=0.0)
+        # one number over the whole model: cosine of the concatenated gradients
+        kept = [n for n in per]
+        a = torch.cat([names[n].grad.double().cpu().reshape(-1) for n in kept])
+        b = torch.cat([P[n].grad.reshape(-1) for n in kept])
+        res["grads_cos"] = float((a @ b) / (a.norm() * b.norm()).clamp_min(1e-300))
+        if P32 is not None:
+            yg, yo = 0.0, 0.0
+            for n in kept:
+                d = float((P32[n].grad.double() - P[n].grad).abs().max())
+                yg = max(yg, d / gscale)
+                yo = max(yo, d / max(float(P[n].grad.abs().max()), 1e-30))
+            res["yard_logits"] = _rel_max(ref32["logits"], ref["logits"])
+            res["yard_loss"] = abs(ref32["loss"] - ref["loss"]) / abs(ref["loss"])
+            res["yard_grads_global"] = yg
+            res["yard_grads_own"] = yo
     if grads:
         names = dict(model.named_parameters())
         ge = {}

@@ -131,6 +131,7 @@ def test_model_forward_unchanged_by_bf16_storage(cuda):
     torch.manual_seed(0)
     cfg = Dimensions(tokens=1000, mels=128, dims=384, head=6, layer=2, act="gelu", n_type="AbbyNormal")
     model = Model(cfg).cuda().train()
+    model.fused_ce = False  # the fused logits + CE stores bf16 logits (tests/test_gpu_ce_fused.py)
     g = torch.Generator().manual_seed(4)
     B, T, S = 2, 16, 1001
     spec = torch.randn(B, 128, S, generator=g).cuda()

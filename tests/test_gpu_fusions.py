@@ -1,0 +1,125 @@
+"""Perf-mode fusions against their unfused compositions (bf16 mode, same kernels otherwise):
+  * LinearRes: r + x W^T + b with the residual add in the out projection's GEMM epilogue (model.py:578-580)
+    == add(r, linear(x)) bit for bit in the forward, same gradients;
+  * asrx_act_bwd_bias: act' applied, gz stored bf16, bias gradient summed in the same pass ==
+    bf16(act_bwd) bit for bit, bias gradient == colsum of the fp32 act_bwd within 1e-5;
+  * the encoder stems written straight into the group buffer (ops.join_group) == torch.cat of separate
+    stems, gradients identical."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("M,N,K,fused_expected", [(40000, 384, 384, True), (8192, 384, 384, True),
+                                                  (700, 512, 512, True), (3001, 768, 384, False)])
+def test_linear_residual_matches_add(cuda, M, N, K, fused_expected):
+    from asrx import gemm as G
+    from asrx import ops, prec
+
+    assert (G._nj(M, N) in (1, 3)) == fused_expected  # nj 2 falls back to add(r, linear(x))
+    g = torch.Generator().manual_seed(M + N + K)
+    r = torch.randn(M, N, generator=g).to(cuda)
+    x = torch.randn(M, K, generator=g).to(cuda)
+    W = (torch.randn(N, K, generator=g) * 0.05).to(cuda)
+    b = (torch.randn(N, generator=g) * 0.1).to(cuda)
+    gy = torch.randn(M, N, generator=g).to(cuda)
+    res = []
+    for fused in (True, False):
+        rr = r.clone().requires_grad_(True)
+        xx = x.clone().requires_grad_(True)
+        WW = W.clone().requires_grad_(True)
+        bb = b.clone().requires_grad_(True)
+        with prec.precision("bf16"):
+            y = ops.linear_residual(rr, xx, WW, bb) if fused else ops.add(rr, ops.linear(xx, WW, bb))
+            if fused:
+                assert ("LinearRes" in type(y.grad_fn).__name__) == fused_expected, type(y.grad_fn).__name__
+            y.backward(gy)
+        res.append((y.detach(), rr.grad, xx.grad, WW.grad, bb.grad))
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1])
+    for a, c in zip(res[0][2:], res[1][2:]):
+        assert float((a - c).abs().max() / c.abs().max()) < 1e-5
+
+
+@pytest.mark.parametrize("act", ["gelu", "silu", "sigmoid"])
+@pytest.mark.parametrize("rows,N", [(5000, 1536), (333, 1152), (64, 384)])
+def test_act_bwd_bias_matches_unfused(cuda, act, rows, N):
+    from asrx import lib, ops
+
+    g = torch.Generator().manual_seed(rows + N)
+    gy = torch.randn(rows, N, generator=g).to(cuda)
+    z = (torch.randn(rows, N, generator=g) * 2).to(cuda)
+    gz_ref = torch.empty_like(gy)
+    lib.call("asrx_act_bwd", lib.ptr(gy), lib.ptr(z), lib.ptr(gz_ref), gy.numel(), ops.ACT[act], lib.stream())
+    db_ref = gz_ref.double().sum(0)
+    gz = torch.empty(rows, N, dtype=torch.bfloat16, device=cuda)
+    db = torch.zeros(N, device=cuda)
+    lib.call("asrx_act_bwd_bias", lib.ptr(gy), lib.ptr(z), lib.ptr(gz), lib.ptr(db), rows, N, ops.ACT[act],
+             lib.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(gz, gz_ref.to(torch.bfloat16))
+    assert float((db.double() - db_ref).abs().max() / db_ref.abs().max()) < 1e-5
+
+
+def test_stem_group_matches_cat(cuda):
+    from asrx import ops, prec
+    from asrx.config import Dimensions
+    from asrx.model import AudioEncoder
+
+    torch.manual_seed(0)
+    cfg = Dimensions(tokens=1000, mels=128, dims=384, head=6, layer=2, act="gelu", n_type="AbbyNormal")
+    enc = AudioEncoder(cfg.mels, cfg.dims, cfg.head, cfg.layer, cfg.act, cfg.n_type, norm=False, enc=False).to(cuda)
+    g = torch.Generator().manual_seed(1)
+    B, T = 2, 501
+    pitch = (torch.rand(B, 1, T, generator=g) * 200).to(cuda)
+    spec = torch.randn(B, 128, T, generator=g).to(cuda)
+    gy = torch.randn(2 * B, T, cfg.dims, generator=g).to(cuda)
+    res = []
+    for grouped in (True, False):
+        enc.zero_grad(set_to_none=True)
+        with prec.precision("bf16"):
+            if grouped:
+                buf = torch.empty(2 * B, T, cfg.dims, device=cuda)
+                x = ops.join_group(buf, [enc.stem(pitch, out=buf[:B]), enc.stem(spec, out=buf[B:])])
+            else:
+                x = torch.cat([enc.stem(pitch), enc.stem(spec)], 0)
+            x.backward(gy)
+        res.append((x.detach().clone(), {n: p.grad.clone() for n, p in enc.named_parameters() if p.grad is not None}))
+    assert torch.equal(res[0][0], res[1][0])
+    assert set(res[0][1]) == set(res[1][1]) and len(res[0][1]) >= 4
+    for n in res[0][1]:
+        a, c = res[0][1][n], res[1][1][n]
+        assert float((a - c).abs().max() / c.abs().max().clamp_min(1e-30)) < 1e-5, n
+
+
+@pytest.mark.parametrize("d,rows", [(384, 3001), (512, 700), (768, 200)])
+def test_abby_residual_matches_add(cuda, d, rows):
+    """residual + AbbyNormal(x) with the add in the AbbyNormal kernel (model.py:583) == add(residual,
+    AbbyNormal(x)) bit for bit, same gradients (keyed noise identical)."""
+    from asrx import ops, prec
+    from asrx.model import AbbyNormal
+
+    torch.manual_seed(0)
+    mod = AbbyNormal(d).to(cuda)
+    g = torch.Generator().manual_seed(d + rows)
+    x = (torch.randn(2, rows // 2, d, generator=g) * 3).to(cuda)
+    r = torch.randn(2, rows // 2, d, generator=g).to(cuda)
+    gy = torch.randn(2, rows // 2, d, generator=g).to(cuda)
+    res = []
+    for fused in (True, False):
+        mod.zero_grad(set_to_none=True)
+        xx, rr = x.clone().requires_grad_(True), r.clone().requires_grad_(True)
+        with prec.precision("bf16"):
+            if fused:
+                y = ops.abby_normal(mod, xx, rows // 2, 1, 0, 1234, True, residual=rr)
+            else:
+                y = ops.add(rr, ops.abby_normal(mod, xx, rows // 2, 1, 0, 1234, True))
+            y.backward(gy)
+        res.append((y.detach(), xx.grad, rr.grad, {n: p.grad.clone() for n, p in mod.named_parameters()}))
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][2], res[1][2])
+    assert float((res[0][1] - res[1][1]).abs().max() / res[1][1].abs().max()) < 1e-6
+    for n in res[0][3]:
+        a, c = res[0][3][n], res[1][3][n]
+        assert float((a - c).abs().max() / c.abs().max().clamp_min(1e-30)) < 1e-5, n

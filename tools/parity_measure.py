@@ -24,9 +24,10 @@ for name in names:
     cfg, B, sec, T, pf = CASES[name]
     for precision in ("fp32", "bf16"):
         r = mp.compare(CONFIGS[cfg], B=B, seconds=sec, T=T, precision=precision, grads=True, pitch_frames=pf,
-                       decisions=True, replay=True)
+                       decisions=True, replay=True, yardstick=precision == "fp32")
         r.pop("grads", None)
         print(json.dumps({"case": name, **r}), flush=True)
-r = mp.compare(CONFIGS["tiny"], B=1, seconds=10.0, T=64, precision="fp32", grads=True, replay=True, hip_mel=True)
+r = mp.compare(CONFIGS["tiny"], B=1, seconds=10.0, T=64, precision="fp32", grads=True, replay=True, hip_mel=True,
+               yardstick=True)
 r.pop("grads", None)
 print(json.dumps({"case": "hip_mel_e2e", **r}), flush=True)
