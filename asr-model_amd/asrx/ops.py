@@ -490,6 +490,12 @@ def small_linear(x, W, b=None, act="none"):
 # =============================================================================== AbbyNormal
 
 
+# The router-epilogue GEMM keeps a whole d-wide row per tile (one 128-row x 384 tile per workgroup): below
+# this many rows it runs on too few workgroups (64 at the text side's 8192 rows, 40-48 us per launch), and
+# the plain GEMM (128 x 128 tiles, 3x the workgroups) + the row kernel's own SiLU / Linear(d, 3) is faster
+ROUTER_FUSED_MIN_ROWS = 32768
+
+
 class AbbyNormalFn(torch.autograd.Function):
     """essentials.AbbyNormal (essentials.py:155-191): router GEMM on MFMA + fused row kernel."""
 
@@ -518,13 +524,13 @@ class AbbyNormalFn(torch.autograd.Function):
             lib.call("asrx_abby_record_cond", _P(cond))
         if res is not None:  # out = res + AbbyNormal(x): the residual add in the same row pass
             res = _c(res)
-            if G.use_wide(d) and d <= 384:
+            if G.use_wide(d) and d <= 384 and rows >= ROUTER_FUSED_MIN_ROWS:
                 hpre, logits = G.router_fwd(x.view(rows, d), W1, b1, W2, keep)
             else:
                 hpre, logits = G.linear_fwd(x, W1, b1), None
             lib.call("asrx_abby_fwd_res", _P(x), _P(hpre), _P(W2), _P(logits), _P(b2), _P(res), _P(out), _P(ys),
                      _P(idx), rows, d, L, H, sid_base, key & 0xFFFFFFFF, int(use_noise), _S())
-        elif G.use_wide(d) and d <= 384:
+        elif G.use_wide(d) and d <= 384 and rows >= ROUTER_FUSED_MIN_ROWS:
             # perf mode: the router's d x d GEMM also applies SiLU and Linear(d, 3) in its epilogue,
             # so h_pre never makes the HBM round trip unless the backward needs it
             hpre, logits = G.router_fwd(x.view(rows, d), W1, b1, W2, keep)

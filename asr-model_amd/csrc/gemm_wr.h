@@ -619,11 +619,12 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
   }
 }
 
-// bf16-stored A: a k-step's A slab is 8 KB instead of 16, so the bytes in flight per CU (the limit of
-// this kernel) need a deeper register pipeline: 4 k-steps (32 KB of A) instead of 3 (245
-// VGPRs; 5 spills)
+// Register pipeline depth per instantiation (0 = WR_DEPTH = 3).  A bf16-stored A halves a k-step's A slab,
+// but a deeper pipeline for it measured no faster on the 192k-row launches (166 us at 3 and at 4 k-steps)
+// and slower on the 8192-row ones (28 -> 35 us; depth 5 spills): the bf16-A kernel is not bound by the A
+// bytes in flight (profiles/r03_kernel_stats_*.csv)
 template <bool ABF>
-constexpr int wr_dep() { return ABF ? 4 : 0; }
+constexpr int wr_dep() { return 0; }
 
 template <int NJ, bool CONV, bool RT = false, bool ABF = false, bool CE = false, bool RES = false>
 void launch_wr(const Params& p, hipStream_t s) {

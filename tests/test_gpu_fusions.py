@@ -12,12 +12,12 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("M,N,K,fused_expected", [(40000, 384, 384, True), (8192, 384, 384, True),
-                                                  (700, 512, 512, True), (3001, 768, 384, False)])
+                                                  (700, 512, 512, True), (30000, 256, 384, False)])
 def test_linear_residual_matches_add(cuda, M, N, K, fused_expected):
     from asrx import gemm as G
     from asrx import ops, prec
 
-    assert (G._nj(M, N) in (1, 3)) == fused_expected  # nj 2 falls back to add(r, linear(x))
+    assert (G._nj(M, N) in (1, 3)) == fused_expected, G._nj(M, N)  # nj 2 falls back to add(r, linear(x))
     g = torch.Generator().manual_seed(M + N + K)
     r = torch.randn(M, N, generator=g).to(cuda)
     x = torch.randn(M, K, generator=g).to(cuda)
@@ -36,7 +36,8 @@ def test_linear_residual_matches_add(cuda, M, N, K, fused_expected):
                 assert ("LinearRes" in type(y.grad_fn).__name__) == fused_expected, type(y.grad_fn).__name__
             y.backward(gy)
         res.append((y.detach(), rr.grad, xx.grad, WW.grad, bb.grad))
-    assert torch.equal(res[0][0], res[1][0])
+    d = (res[0][0] - res[1][0]).abs()
+    assert torch.equal(res[0][0], res[1][0]), (float(d.max()), int((d > 0).sum()), d.nonzero()[:4].tolist())
     assert torch.equal(res[0][1], res[1][1])
     for a, c in zip(res[0][2:], res[1][2:]):
         assert float((a - c).abs().max() / c.abs().max()) < 1e-5

@@ -14,7 +14,7 @@ from asrx.config import CONFIGS  # noqa: E402
 CASES = {
     "tiny_full": ("tiny", 1, 30.0, 256, None),
     "tiny_full_refpitch": ("tiny", 1, 30.0, 256, 6001),
-    "tiny_b2": ("tiny", 2, 10.0, 64, None),
+    "tiny_b2": ("tiny", 2, 5.0, 64, None),
     "small": ("small", 1, 3.0, 32, None),
     "medium": ("medium", 1, 2.0, 32, None),
     "refmain": ("reference_main", 2, 5.0, 64, None),
