@@ -111,16 +111,57 @@ def _hip_mel_inputs(x, B, seconds, seed, device):
 ANALYTIC_ZERO = (".router.", ".depth.bias")
 
 
+def oracle_run(sd, ocfg, x, dec, dtype=torch.float64, noise=(7, 3), train=True):
+    """The oracle forward + backward on state dict sd (fresh leaf copies in dtype) with decision
+    table dec; returns (params with .grad, {"logits", "loss"})."""
+    P = {k: (v.to(dtype).requires_grad_(True) if v.is_floating_point() else v) for k, v in sd.items()}
+    om.use_decisions(dec)
+    try:
+        r = om.forward(P, ocfg, x["text_ids"], x["labels"], spectrogram=x["spectrogram"].to(dtype),
+                       pitch=x["pitch"].to(dtype), waveform=x["waveform"].to(dtype), seed=noise[0],
+                       step=noise[1], training=train, live_only=True, dtype=dtype)
+        r["loss"].backward()
+    finally:
+        om.use_decisions(None)
+    return P, {"logits": r["logits"].detach().double(), "loss": float(r["loss"].detach())}
+
+
+def ulp_nudge(sd, seed):
+    """sd with every floating weight scaled by (1 + u 2^-24), u uniform in [-1, 1): inputs an fp32
+    implementation cannot tell apart from sd."""
+    g = torch.Generator().manual_seed(1000 + seed)
+    return {k: (v.double() * (1 + (torch.rand(v.shape, generator=g, dtype=torch.float64) * 2 - 1) * 2.0 ** -24)
+                if v.is_floating_point() else v) for k, v in sd.items()}
+
+
+def grad_distance(Pa, Pb):
+    """(max over parameters of max|ga - gb| / the largest |gb| of the model, that parameter, cosine of
+    the concatenated gradients); analytically-zero gradients skipped."""
+    names = [n for n in Pb if torch.is_tensor(Pb[n]) and Pb[n].grad is not None and Pa[n].grad is not None
+             and not any(z in n for z in ANALYTIC_ZERO)]
+    gscale = max(float(Pb[n].grad.abs().max()) for n in names)
+    worst, wname = 0.0, None
+    for n in names:
+        d = float((Pa[n].grad.double() - Pb[n].grad.double()).abs().max()) / gscale
+        if d > worst:
+            worst, wname = d, n
+    a = torch.cat([Pa[n].grad.double().reshape(-1) for n in names])
+    b = torch.cat([Pb[n].grad.double().reshape(-1) for n in names])
+    return worst, wname, float((a @ b) / (a.norm() * b.norm()).clamp_min(1e-300))
+
+
 def compare(cfg, B=1, seconds=30.0, T=256, precision="bf16", train=True, grads=True, seed=0, noise=(7, 3),
             model_seed=0, device="cuda", decisions=False, replay=False, hip_mel=False, pitch_frames=None,
-            yardstick=False):
+            yardstick=False, sensitivity=0):
     """Run the HIP Model and the oracle on the same inputs; return a dict of metrics.
     decisions: record both sides' hard decisions and report their agreement.  replay: re-run the oracle
     consuming the HIP decisions and compare every parameter gradient.  hip_mel: feed the HIP model the
     HIP log-mel of the clips (the benchmarked chain), the oracle its float64 mel.  yardstick (with
     replay): also run the oracle in float32 on the same replayed trajectory -- the reference's own
     arithmetic at fp32 -- and report its distance from the float64 oracle (yard_*): the model's fp32
-    conditioning, against which the HIP fp32 path is gated."""
+    conditioning, against which the HIP fp32 path is gated.  sensitivity=K (with replay): K float64
+    oracle runs on weights nudged by one fp32 ulp (ulp_nudge), the largest gradient move reported as
+    ulp_grads_global -- the gradient's conditioning at fp32 input precision."""
     from asrx import decisions as hdec
     from asrx import prec
     from asrx.model import Model
@@ -151,16 +192,7 @@ def compare(cfg, B=1, seconds=30.0, T=256, precision="bf16", train=True, grads=T
     ocfg = {"dims": cfg.dims, "head": cfg.head, "layer": cfg.layer}
 
     def run_oracle(dec, dtype=torch.float64):
-        P = {k: (v.to(dtype).requires_grad_(True) if v.is_floating_point() else v) for k, v in sd.items()}
-        om.use_decisions(dec)
-        try:
-            r = om.forward(P, ocfg, x["text_ids"], x["labels"], spectrogram=x["spectrogram"].to(dtype),
-                           pitch=x["pitch"].to(dtype), waveform=x["waveform"].to(dtype), seed=noise[0],
-                           step=noise[1], training=train, live_only=True, dtype=dtype)
-            r["loss"].backward()
-        finally:
-            om.use_decisions(None)
-        return P, {"logits": r["logits"].detach().double(), "loss": float(r["loss"].detach())}
+        return oracle_run(sd, ocfg, x, dec, dtype, noise, train)
 
     ck = (repr(cfg), B, seconds, T, train, seed, noise, model_seed, pitch_frames)
     t0 = time.perf_counter()
@@ -185,6 +217,12 @@ def compare(cfg, B=1, seconds=30.0, T=256, precision="bf16", train=True, grads=T
         P_r, ref_r = run_oracle(rp)
         if yardstick:
             P32, ref32 = run_oracle(om.Decisions(table=hip_dec), torch.float32)
+        if sensitivity:
+            moves = [grad_distance(oracle_run(ulp_nudge(sd, k), ocfg, x, om.Decisions(table=hip_dec),
+                                              torch.float64, noise, train)[0], P_r)
+                     for k in range(sensitivity)]
+            res_extra["ulp_grads_global"] = max(m[0] for m in moves)
+            res_extra["ulp_grads_worst"] = max(moves)[1]
         res_extra["replayed"] = rp.replayed
         res_extra["overridden"] = rp.overridden
         res_extra["cond_overridden"] = rp.cond_overridden

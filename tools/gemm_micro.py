@@ -1,0 +1,41 @@
+"""GPU micro-benchmark of the wide GEMM in isolation (no other stream competing): average kernel time of
+back-to-back launches per (M, N, K, A dtype, nj), to separate a shape's own cost from the interference
+seen in the step's kernel trace.  usage: python tools/gemm_micro.py"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "asr-model_amd")]
+import torch  # noqa: E402
+
+from asrx import gemm as G  # noqa: E402
+from asrx import prec  # noqa: E402
+
+prec.set_precision("bf16")
+dev = torch.device("cuda:0")
+SHAPES = [(8192, 384, 384), (8192, 384, 1536), (8192, 1536, 384), (8192, 1152, 384), (32, 128, 384),
+          (192064, 384, 384), (192064, 1536, 384), (192064, 384, 1536)]
+for M, N, K in SHAPES:
+    for abf in (False, True):
+        A = torch.randn(M, K, device=dev).to(torch.bfloat16 if abf else torch.float32)
+        W = torch.randn(N, K, device=dev) * 0.05
+        Wb = G.weight_bf16(W, cache=False)
+        C = torch.empty(M, N, device=dev)
+        for nj in (1, 2, 3):
+            if 128 * nj > ((N + 127) // 128) * 128:
+                continue
+            G._nj_override = nj
+            for _ in range(3):
+                G.gemm_wn(A, Wb, C, M=M, N=N, K=K, lda=K, ldc=N)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            n = 50
+            e0.record()
+            for _ in range(n):
+                G.gemm_wn(A, Wb, C, M=M, N=N, K=K, lda=K, ldc=N)
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / n
+            print(f"M{M:7d} N{N:5d} K{K:5d} A{'bf16' if abf else 'fp32'} nj{nj}: {us:8.1f} us "
+                  f"{2.0 * M * N * K / us / 1e6:7.1f} TF/s", flush=True)
+        G._nj_override = 0
