@@ -114,7 +114,9 @@ ANALYTIC_ZERO = (".router.", ".depth.bias")
 def oracle_run(sd, ocfg, x, dec, dtype=torch.float64, noise=(7, 3), train=True):
     """The oracle forward + backward on state dict sd (fresh leaf copies in dtype) with decision
     table dec; returns (params with .grad, {"logits", "loss"})."""
-    P = {k: (v.to(dtype).requires_grad_(True) if v.is_floating_point() else v) for k, v in sd.items()}
+    # a copy even when sd already holds dtype (requires_grad_ on sd's own tensors would leak into later runs)
+    P = {k: (v.detach().to(dtype, copy=True).requires_grad_(True) if v.is_floating_point() else v)
+         for k, v in sd.items()}
     om.use_decisions(dec)
     try:
         r = om.forward(P, ocfg, x["text_ids"], x["labels"], spectrogram=x["spectrogram"].to(dtype),
@@ -130,7 +132,7 @@ def ulp_nudge(sd, seed):
     """sd with every floating weight scaled by (1 + u 2^-24), u uniform in [-1, 1): inputs an fp32
     implementation cannot tell apart from sd."""
     g = torch.Generator().manual_seed(1000 + seed)
-    return {k: (v.double() * (1 + (torch.rand(v.shape, generator=g, dtype=torch.float64) * 2 - 1) * 2.0 ** -24)
+    return {k: (v.detach().double() * (1 + (torch.rand(v.shape, generator=g, dtype=torch.float64) * 2 - 1) * 2.0 ** -24)
                 if v.is_floating_point() else v) for k, v in sd.items()}
 
 
