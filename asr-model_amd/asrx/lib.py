@@ -203,7 +203,19 @@ def check(rc: int, name: str) -> None:
         raise RuntimeError(f"{name} failed (code {rc}): {msg}")
 
 
+# launch census (tools/call_census.py): when a Counter is installed here, every call is counted by
+# (entry point, calling file:line) with the sum of its integer arguments' largest value (a size proxy)
+CENSUS = None
+
+
 def call(name: str, *args) -> None:
+    if CENSUS is not None:
+        import sys as _sys
+
+        f = _sys._getframe(1)
+        key = (name, f"{os.path.basename(f.f_code.co_filename)}:{f.f_lineno}")
+        CENSUS[key + ("n",)] += 1
+        CENSUS[key + ("size",)] += max((a for a in args if isinstance(a, int) and a < 1 << 40), default=0)
     check(getattr(load(), name)(*args), name)
 
 

@@ -54,11 +54,24 @@ struct AbbyShape {
 };
 
 __device__ __forceinline__ uint32_t abby_noise_idx(const AbbyGeom& g, int64_t r, int k) {
-  const int64_t per = g.L * g.H;
-  const int64_t sid = g.sid_base + r / per;
-  const int64_t q = r % per;
-  const int64_t l = q / g.H, h = q % g.H;
-  return (uint32_t)(((sid * g.H + h) * 8192 + l) * 3 + k);
+  // 32-bit index arithmetic (rows < 2^32; the index is taken mod 2^32 either way): the 64-bit
+  // divisions cost ~3x the instructions
+  const uint32_t per = (uint32_t)(g.L * g.H), H = (uint32_t)g.H, rr = (uint32_t)r;
+  const uint32_t sid = (uint32_t)g.sid_base + rr / per;
+  const uint32_t q = rr % per;
+  const uint32_t l = q / H, h = q % H;
+  return ((sid * H + h) * 8192u + l) * 3u + (uint32_t)k;
+}
+
+// the row's three gumbel draws, one per lane (lanes 0-2; the others repeat draw 0) and broadcast: a
+// third of the hash / log work of every lane computing all three
+__device__ __forceinline__ void abby_gumbel3(const AbbyGeom& g, int64_t r, int lane, float& z0, float& z1,
+                                             float& z2) {
+  const float gk = noise_gumbel(g.key, abby_noise_idx(g, r, lane < 3 ? lane : 0));
+  const int gi = __builtin_bit_cast(int, gk);
+  z0 += __builtin_bit_cast(float, __builtin_amdgcn_readlane(gi, 0));
+  z1 += __builtin_bit_cast(float, __builtin_amdgcn_readlane(gi, 1));
+  z2 += __builtin_bit_cast(float, __builtin_amdgcn_readlane(gi, 2));
 }
 
 template <int E>
@@ -190,6 +203,42 @@ __device__ __forceinline__ void abby_wsum(const float (&h)[AbbyShape<E>::HL], fl
 template <int E, bool ARG>
 __device__ __forceinline__ void abby_wmax(const float (&h)[AbbyShape<E>::HL], float (&mx)[E], int (&am)[E]) {
   typedef AbbyShape<E> S;
+  if constexpr (S::W >= E && E > 1) {
+    // the E windows h[e, e + W) share the core h[E - 1, W): its max once, then a suffix scan of the
+    // left parts h[e, E - 1) and a prefix scan of the right parts h[W, W + e) -- ~3 ops per output
+    // instead of W - 1.  max is exact and the first-argmax order is kept (left parts win ties against
+    // the core, the core against the right parts), so the results are identical to the plain scan.
+    float cm = h[E - 1];
+    int ca = E - 1;
+#pragma unroll
+    for (int i = E; i < S::W; ++i) {
+      if (ARG) ca = h[i] > cm ? i : ca;
+      cm = fmaxf(cm, h[i]);
+    }
+    float lm[E];
+    int la[E];
+    lm[E - 1] = cm;
+    la[E - 1] = ca;
+#pragma unroll
+    for (int e = E - 2; e >= 0; --e) {
+      if (ARG) la[e] = h[e] >= lm[e + 1] ? e : la[e + 1];
+      lm[e] = fmaxf(lm[e + 1], h[e]);
+    }
+    mx[0] = lm[0];
+    if (ARG) am[0] = la[0];
+    float rm = h[S::W];
+    int ra = S::W;
+#pragma unroll
+    for (int e = 1; e < E; ++e) {
+      if (e > 1) {
+        if (ARG) ra = h[S::W + e - 1] > rm ? S::W + e - 1 : ra;
+        rm = fmaxf(rm, h[S::W + e - 1]);
+      }
+      if (ARG) am[e] = rm > lm[e] ? ra : la[e];
+      mx[e] = fmaxf(lm[e], rm);
+    }
+    return;
+  }
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     float m = h[e];
@@ -294,11 +343,7 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_fwd_kernel(const float* 
     abby_row_stats<E>(xv, mu, sd, mabs);
     const float cv = sd / (mabs + 1e-6f);
     float z0 = l0 + b2[0] + cv, z1 = l1 + b2[1] + cv, z2 = l2 + b2[2] + cv;
-    if (g.use_noise) {
-      z0 += noise_gumbel(g.key, abby_noise_idx(g, r, 0));
-      z1 += noise_gumbel(g.key, abby_noise_idx(g, r, 1));
-      z2 += noise_gumbel(g.key, abby_noise_idx(g, r, 2));
-    }
+    if (g.use_noise) abby_gumbel3(g, r, lane, z0, z1, z2);
     const float zm = fmaxf(z0, fmaxf(z1, z2));
     const float e0 = expf(z0 - zm), e1 = expf(z1 - zm), e2 = expf(z2 - zm);
     const float inv = 1.0f / (e0 + e1 + e2);
@@ -724,10 +769,12 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_fwd64_kernel(const float
     stats64(xv, mu, sd, mabs);
     const float cv = sd / (mabs + 1e-6f);
     float z0 = l0 + b2[0] + cv, z1 = l1 + b2[1] + cv, z2 = l2 + b2[2] + cv;
-    if (g.use_noise) {
-      z0 += noise_gumbel(g.key, abby_noise_idx(g, r, 0));
-      z1 += noise_gumbel(g.key, abby_noise_idx(g, r, 1));
-      z2 += noise_gumbel(g.key, abby_noise_idx(g, r, 2));
+    if (g.use_noise) {  // lanes 0-2 of the 16-lane row draw one gumbel each, then broadcast in the row
+      const float gk = noise_gumbel(g.key, abby_noise_idx(g, r, l16 < 3 ? l16 : 0));
+      const int base = lane & 48;
+      z0 += __shfl(gk, base + 0);
+      z1 += __shfl(gk, base + 1);
+      z2 += __shfl(gk, base + 2);
     }
     const float zm = fmaxf(z0, fmaxf(z1, z2));
     const float e0 = expf(z0 - zm), e1 = expf(z1 - zm), e2 = expf(z2 - zm);

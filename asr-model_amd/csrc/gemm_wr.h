@@ -439,6 +439,9 @@ __device__ __forceinline__ void wr_load(const Params& p, WrStage<NJ, ABF>& st, i
   }
 }
 
+// (Raw buffer loads against a per-tile resource -- 32-bit offsets, out-of-range chunks read 0 -- were
+// measured against these zero-page-clamped global loads: 13.1 -> 14.9 us at M = 8192, N = K = 384 and
+// no change on the 192k-row launches, profiles/r03_gemm_micro_v2.txt.)
 // A image: [128 rows][4 chunks of 8 bf16] (64 B rows), W image: [BN rows][4 chunks], both with the
 // chunk XOR swizzle swb(row) (conflict-free ds_read_b128 fragment reads).
 template <int NJ, bool ABF>
@@ -502,8 +505,21 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
     const int j = s / nk;
     const int t = j * G + r;
     // past this workgroup's tiles (prefetch only) the raw index is kept: in range or beyond M
-    m0 = ((mlist && t < ntiles) ? mlist[t / nN] : t / nN) * BM;
-    n0 = (t % nN) * BN;
+    if constexpr (CE) {
+      // tied logits: row tiles fastest, so the 32 ranks of one XCD keep revisiting the same half of
+      // the (small) activation rows out of their L2 while the vocabulary's weight tiles stream past
+      // once per XCD pair (column-fastest re-streamed the whole bf16 vocabulary per ~2 row tiles)
+      const int nM = (p.M + BM - 1) / BM;
+      m0 = (t < ntiles ? t % nM : nM + t) * BM;
+      n0 = (t < ntiles ? t / nM : 0) * BN;
+    } else {
+      // the tile list is read through the constant address space: a uniform index then becomes a
+      // scalar load (lgkmcnt), where a vector load of it forced the compiler to drain every prefetch in
+      // flight (vmcnt(0)) at each k-step -- on every launch, list or not, since the wait follows the
+      // branch around the load
+      m0 = ((mlist && t < ntiles) ? ((const __attribute__((address_space(4))) int*)mlist)[t / nN] : t / nN) * BM;
+      n0 = (t % nN) * BN;
+    }
     k0 = (s - j * nk) * BK;
   };
   auto load = [&](int s, WrStage<NJ, ABF>& st) __attribute__((always_inline)) {
