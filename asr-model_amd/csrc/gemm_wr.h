@@ -501,40 +501,55 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
   const int lr = lane & 15, lk = lane >> 4;
   const bool vec = vec_ok(p);
 
-  auto coords = [&](int s, int& m0, int& n0, int& k0) __attribute__((always_inline)) {
-    const int j = s / nk;
-    const int t = j * G + r;
+  // Step -> (tile, k) coordinates are tracked incrementally by three cursors (the load cursor runs
+  // DEPTH steps ahead of the epilogue cursor, the store cursor one ahead): a tile's (m0, n0) is
+  // computed once when a cursor enters it.  Deriving them per k-step (s / nk, t / nN, t % nN with
+  // runtime divisors) cost ~250 scalar instructions per k-step and wave against 8-24 MFMAs -- the
+  // kernel was bound by instruction issue, not by MFMA or HBM (cursors: M = 8192, N = K = 384 14.9 ->
+  // 11.2 us, M = 192064 bf16-A 138 -> 105 us at nj 1; profiles/r03_gemm_micro_v3.txt).
+  struct Cur {
+    int j, kk, m0, n0;  // tile ordinal of this workgroup, k-step within the tile, tile origin
+  };
+  auto enter = [&](Cur& c) __attribute__((always_inline)) {
+    const int t = c.j * G + r;
     // past this workgroup's tiles (prefetch only) the raw index is kept: in range or beyond M
     if constexpr (CE) {
       // tied logits: row tiles fastest, so the 32 ranks of one XCD keep revisiting the same half of
       // the (small) activation rows out of their L2 while the vocabulary's weight tiles stream past
-      // once per XCD pair (column-fastest re-streamed the whole bf16 vocabulary per ~2 row tiles)
       const int nM = (p.M + BM - 1) / BM;
-      m0 = (t < ntiles ? t % nM : nM + t) * BM;
-      n0 = (t < ntiles ? t / nM : 0) * BN;
+      c.m0 = (t < ntiles ? t % nM : nM + t) * BM;
+      c.n0 = (t < ntiles ? t / nM : 0) * BN;
     } else {
       // the tile list is read through the constant address space: a uniform index then becomes a
-      // scalar load (lgkmcnt), where a vector load of it forced the compiler to drain every prefetch in
-      // flight (vmcnt(0)) at each k-step -- on every launch, list or not, since the wait follows the
-      // branch around the load
-      m0 = ((mlist && t < ntiles) ? ((const __attribute__((address_space(4))) int*)mlist)[t / nN] : t / nN) * BM;
-      n0 = (t % nN) * BN;
+      // scalar load (lgkmcnt) -- a vector load of it made the compiler drain every prefetch in flight
+      // (vmcnt(0)) behind the branch around the load
+      const int tm = t / nN;
+      c.m0 = ((mlist && t < ntiles) ? ((const __attribute__((address_space(4))) int*)mlist)[tm] : tm) * BM;
+      c.n0 = (t - tm * nN) * BN;
     }
-    k0 = (s - j * nk) * BK;
   };
-  auto load = [&](int s, WrStage<NJ, ABF>& st) __attribute__((always_inline)) {
-    int m0, n0, k0;
-    coords(s, m0, n0, k0);
-    wr_load<NJ, CONV, ABF>(p, st, m0, n0, k0);
+  auto advance = [&](Cur& c) __attribute__((always_inline)) {
+    if (++c.kk == nk) {
+      c.kk = 0;
+      ++c.j;
+      enter(c);
+    }
+  };
+  Cur cl{0, 0, 0, 0}, cs{0, 0, 0, 0}, ce{0, 0, 0, 0};  // load, store, epilogue cursors
+  enter(cl);
+  cs = cl;
+  ce = cl;
+  auto load = [&](WrStage<NJ, ABF>& st, bool issue) __attribute__((always_inline)) {
+    if (issue) wr_load<NJ, CONV, ABF>(p, st, cl.m0, cl.n0, cl.kk * BK);
+    advance(cl);
   };
   auto store = [&](int s, const WrStage<NJ, ABF>& st) __attribute__((always_inline)) {
     wr_store<NJ, ABF>(st, a_img[s & 1], b_img[s & 1]);
-    if (s % nk == 0) {  // first k-step of a tile: its bias slice (read by the tile's epilogue)
-      int m0, n0, k0;
-      coords(s, m0, n0, k0);
-      float* dst = bias_s[(s / nk) & 1];
-      for (int c = threadIdx.x; c < BN; c += NTHR) dst[c] = (p.bias && n0 + c < p.N) ? p.bias[n0 + c] : 0.f;
+    if (cs.kk == 0) {  // first k-step of a tile: its bias slice (read by the tile's epilogue)
+      float* dst = bias_s[cs.j & 1];
+      for (int c = threadIdx.x; c < BN; c += NTHR) dst[c] = (p.bias && cs.n0 + c < p.N) ? p.bias[cs.n0 + c] : 0.f;
     }
+    advance(cs);
   };
 
   f32x4 acc[4][NT];
@@ -548,13 +563,11 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
   constexpr int DEPTH = DEP ? DEP : WR_DEPTH;
   static_assert(DEPTH >= 3 && DEPTH <= 5, "stage sets are written out for depths 3..5");
   WrStage<NJ, ABF> st0, st1, st2, st3, st4;  // st3 / st4 unused (eliminated) below depth 4 / 5
-  if (S > 0) load(0, st0);
-  if (S > 1) load(1, st1);
-  if (S > 2) load(2, st2);
-  if constexpr (DEPTH >= 4)
-    if (S > 3) load(3, st3);
-  if constexpr (DEPTH >= 5)
-    if (S > 4) load(4, st4);
+  load(st0, S > 0);
+  load(st1, S > 1);
+  load(st2, S > 2);
+  if constexpr (DEPTH >= 4) load(st3, S > 3);
+  if constexpr (DEPTH >= 5) load(st4, S > 4);
   if (S > 0) store(0, st0);
   __syncthreads();
 
@@ -564,7 +577,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
     // unconditional: past the last step the A rows fall beyond M and read the zero page, so the
     // number of loads in flight is the same on every path and the compiler's vmcnt waits stay
     // counted (a conditional load here would force vmcnt(0) at every later wait)
-    load(s + DEPTH, cur);
+    load(cur, true);
     const char* At = a_img[s & 1];
     const char* Bt = b_img[s & 1];
     bf16x8 a[4], b[NT];
@@ -584,10 +597,9 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
       for (int nt = 0; nt < NT; ++nt)
         acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nt], a[mt], acc[mt][nt], 0, 0, 0);
     if (s + 1 < S) store(s + 1, nxt);
-    if (s % nk == nk - 1) {
-      int m0, n0, k0;
-      coords(s, m0, n0, k0);
-      const float* bsl = bias_s[(s / nk) & 1];
+    if (ce.kk == nk - 1) {
+      const int m0 = ce.m0, n0 = ce.n0;
+      const float* bsl = bias_s[ce.j & 1];
       if constexpr (RT) {
         epilogue_router<NJ>(p, acc, bsl, w2s, red, m0, wm, wn, lr, lk);
       } else if constexpr (CE) {
@@ -612,6 +624,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
 #pragma unroll
         for (int q = 0; q < NT; ++q) acc[i][q] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
+    advance(ce);
     __syncthreads();
   };
 
