@@ -213,7 +213,11 @@ def call(name: str, *args) -> None:
         import sys as _sys
 
         f = _sys._getframe(1)
-        key = (name, f"{os.path.basename(f.f_code.co_filename)}:{f.f_lineno}")
+        g = f.f_back
+        site = f"{os.path.basename(f.f_code.co_filename)}:{f.f_lineno}"
+        if g is not None:
+            site += f" <- {os.path.basename(g.f_code.co_filename)}:{g.f_lineno}"
+        key = (name, site)
         CENSUS[key + ("n",)] += 1
         CENSUS[key + ("size",)] += max((a for a in args if isinstance(a, int) and a < 1 << 40), default=0)
     check(getattr(load(), name)(*args), name)

@@ -469,11 +469,96 @@ __device__ __forceinline__ void wr_store(const WrStage<NJ, ABF>& st, char* At, c
   }
 }
 
+// 64-deep k-steps for the one-tile-column (nj = 1, no conv) launches: their k-step is 8 MFMAs per wave at
+// BK = 32, too little work to cover a step's fixed instruction overhead (loads, LDS, barrier, cursors);
+// at 64 each step carries 16 and a K-long reduction takes half the steps.  Images: rows of 128 B (8
+// chunks of 8 bf16) with the chunk XOR swizzle sw64(row) = (row >> 1) & 7, conflict-free for the 16-lane
+// ds_read_b128 groups (16 consecutive rows of one chunk column cover all 16 16-B bank slots of 256 B).
+template <bool ABF>
+struct WrStage64 {
+  float4 a[4];  // fp32 A: row q/16, k chunk of 4 q%16, q = tid + 512 i
+  u32x4 b[2];   // W: row q/8, k chunk of 8 q%8
+};
+template <>
+struct WrStage64<true> {
+  u32x4 a[2];  // bf16 A: row q/8, k chunk of 8 q%8
+  u32x4 b[2];
+};
+template <bool C, typename T, typename F>
+struct pick_t { typedef T type; };
+template <typename T, typename F>
+struct pick_t<false, T, F> { typedef F type; };
+
+__device__ __forceinline__ int sw64(int row) { return (row >> 1) & 7; }
+
+template <bool ABF>
+__device__ __forceinline__ void wr_load64(const Params& p, WrStage64<ABF>& st, int m0, int n0, int k0) {
+  const int t = threadIdx.x;
+  if constexpr (ABF) {
+    const unsigned short* Ah = reinterpret_cast<const unsigned short*>(p.A);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int q = t + NTHR * i;
+      const int r = m0 + (q >> 3), k = k0 + 8 * (q & 7);
+      st.a[i] = *reinterpret_cast<const u32x4*>((r < p.M && k < p.K) ? (const void*)(Ah + (int64_t)r * p.lda + k)
+                                                                     : (const void*)zero_page);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = t + NTHR * i;
+      const int r = m0 + (q >> 4), k = k0 + 4 * (q & 15);
+      st.a[i] = *reinterpret_cast<const float4*>((r < p.M && k < p.K) ? (const void*)(p.A + (int64_t)r * p.lda + k)
+                                                                      : (const void*)zero_page);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int q = t + NTHR * i;
+    const int n = n0 + (q >> 3), k = k0 + 8 * (q & 7);
+    st.b[i] = *reinterpret_cast<const u32x4*>((n < p.N && k < p.K) ? (const void*)(p.W + (int64_t)n * p.ldw + k)
+                                                                  : (const void*)zero_page);
+  }
+}
+
+template <bool ABF>
+__device__ __forceinline__ void wr_store64(const WrStage64<ABF>& st, char* At, char* Bt) {
+  const int t = threadIdx.x;
+  if constexpr (ABF) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int q = t + NTHR * i;
+      const int row = q >> 3, c = q & 7;
+      *reinterpret_cast<u32x4*>(At + row * 128 + 16 * (c ^ sw64(row))) = st.a[i];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = t + NTHR * i;
+      const int row = q >> 4, c = q & 15;
+      const float4 v = st.a[i];
+      typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+      bf16x4 h;
+      h[0] = (__bf16)v.x; h[1] = (__bf16)v.y; h[2] = (__bf16)v.z; h[3] = (__bf16)v.w;
+      *reinterpret_cast<bf16x4*>(At + row * 128 + 16 * ((c >> 1) ^ sw64(row)) + 8 * (c & 1)) = h;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int q = t + NTHR * i;
+    const int n = q >> 3, c = q & 7;
+    *reinterpret_cast<u32x4*>(Bt + n * 128 + 16 * (c ^ sw64(n))) = st.b[i];
+  }
+}
+
 template <int NJ, bool CONV, bool RT, int DEP = 0, bool ABF = false, bool CE = false, bool RES = false>
 __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) {  // ntiles: all tiles
   typedef Cfg<NJ> CF;
   constexpr int BN = CF::BN, NT = 2 * NJ, BNR = CF::BNR;
-  constexpr int AB = BM * BK * 2, BB = BN * BK * 2;  // bf16 images
+  constexpr bool K64 = NJ == 1 && !CONV;  // 64-deep k-steps (WrStage64)
+  constexpr int BKW = K64 ? 64 : BK;
+  typedef typename pick_t<K64, WrStage64<ABF>, WrStage<NJ, ABF>>::type Stg;
+  constexpr int AB = BM * BKW * 2, BB = BN * BKW * 2;  // bf16 images
   __shared__ __attribute__((aligned(16))) char a_img[2][AB];
   __shared__ __attribute__((aligned(16))) char b_img[2][BB];
   __shared__ __attribute__((aligned(16))) float bias_s[2][BNR];
@@ -488,7 +573,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
   }
 
   const int nN = (p.N + BN - 1) / BN;
-  const int nk = (p.K + BK - 1) / BK;
+  const int nk = (p.K + BKW - 1) / BKW;
   const int G = gridDim.x, bid = blockIdx.x;
   const int r = (G % 8 == 0) ? (bid & 7) * (G >> 3) + (bid >> 3) : bid;  // XCD-grouped tile ranks
   const int* mlist = p.mtiles;
@@ -539,12 +624,16 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
   enter(cl);
   cs = cl;
   ce = cl;
-  auto load = [&](WrStage<NJ, ABF>& st, bool issue) __attribute__((always_inline)) {
-    if (issue) wr_load<NJ, CONV, ABF>(p, st, cl.m0, cl.n0, cl.kk * BK);
+  auto load = [&](Stg& st, bool issue) __attribute__((always_inline)) {
+    if (issue) {
+      if constexpr (K64) wr_load64<ABF>(p, st, cl.m0, cl.n0, cl.kk * BKW);
+      else wr_load<NJ, CONV, ABF>(p, st, cl.m0, cl.n0, cl.kk * BK);
+    }
     advance(cl);
   };
-  auto store = [&](int s, const WrStage<NJ, ABF>& st) __attribute__((always_inline)) {
-    wr_store<NJ, ABF>(st, a_img[s & 1], b_img[s & 1]);
+  auto store = [&](int s, const Stg& st) __attribute__((always_inline)) {
+    if constexpr (K64) wr_store64<ABF>(st, a_img[s & 1], b_img[s & 1]);
+    else wr_store<NJ, ABF>(st, a_img[s & 1], b_img[s & 1]);
     if (cs.kk == 0) {  // first k-step of a tile: its bias slice (read by the tile's epilogue)
       float* dst = bias_s[cs.j & 1];
       for (int c = threadIdx.x; c < BN; c += NTHR) dst[c] = (p.bias && cs.n0 + c < p.N) ? p.bias[cs.n0 + c] : 0.f;
@@ -562,7 +651,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
   // ends up in scratch)
   constexpr int DEPTH = DEP ? DEP : WR_DEPTH;
   static_assert(DEPTH >= 3 && DEPTH <= 5, "stage sets are written out for depths 3..5");
-  WrStage<NJ, ABF> st0, st1, st2, st3, st4;  // st3 / st4 unused (eliminated) below depth 4 / 5
+  Stg st0, st1, st2, st3, st4;  // st3 / st4 unused (eliminated) below depth 4 / 5
   load(st0, S > 0);
   load(st1, S > 1);
   load(st2, S > 2);
@@ -573,29 +662,51 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
 
   // one k-step: `cur` held step s (already in LDS) and is refilled with step s + 3; `nxt` holds
   // step s + 1, which goes into the other LDS image after this step's MFMAs
-  auto kstep = [&](int s, WrStage<NJ, ABF>& cur, const WrStage<NJ, ABF>& nxt) __attribute__((always_inline)) {
+  auto kstep = [&](int s, Stg& cur, const Stg& nxt) __attribute__((always_inline)) {
     // unconditional: past the last step the A rows fall beyond M and read the zero page, so the
     // number of loads in flight is the same on every path and the compiler's vmcnt waits stay
     // counted (a conditional load here would force vmcnt(0) at every later wait)
     load(cur, true);
     const char* At = a_img[s & 1];
     const char* Bt = b_img[s & 1];
-    bf16x8 a[4], b[NT];
+    if constexpr (K64) {
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      const int rr = wm * 64 + mt * 16 + lr;
-      a[mt] = *reinterpret_cast<const bf16x8*>(At + rr * 64 + 16 * (lk ^ swb(rr)));
+      for (int h = 0; h < 2; ++h) {  // two 32-deep halves of the 64-deep step
+        bf16x8 a[4], b[NT];
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          const int rr = wm * 64 + mt * 16 + lr;
+          a[mt] = *reinterpret_cast<const bf16x8*>(At + rr * 128 + 16 * ((4 * h + lk) ^ sw64(rr)));
+        }
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          const int n = wn * 32 + nt * 16 + lr;
+          b[nt] = *reinterpret_cast<const bf16x8*>(Bt + n * 128 + 16 * ((4 * h + lk) ^ sw64(n)));
+        }
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt)
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nt], a[mt], acc[mt][nt], 0, 0, 0);
+      }
+    } else {
+      bf16x8 a[4], b[NT];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const int rr = wm * 64 + mt * 16 + lr;
+        a[mt] = *reinterpret_cast<const bf16x8*>(At + rr * 64 + 16 * (lk ^ swb(rr)));
+      }
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int n = wn * (32 * NJ) + nt * 16 + lr;
+        b[nt] = *reinterpret_cast<const bf16x8*>(Bt + n * 64 + 16 * (lk ^ swb(n)));
+      }
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nt], a[mt], acc[mt][nt], 0, 0, 0);
     }
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      const int n = wn * (32 * NJ) + nt * 16 + lr;
-      b[nt] = *reinterpret_cast<const bf16x8*>(Bt + n * 64 + 16 * (lk ^ swb(n)));
-    }
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nt], a[mt], acc[mt][nt], 0, 0, 0);
     if (s + 1 < S) store(s + 1, nxt);
     if (ce.kk == nk - 1) {
       const int m0 = ce.m0, n0 = ce.n0;
