@@ -263,11 +263,27 @@ def _splitk_for(m_rows: int, tiles: int) -> int:
     return int(max(1, min(want, m_rows // 256)))
 
 
-def _wgrad(A, lda, x2, out, M, K, rows):
+def _wgrad(A, lda, x2, out, M, K, rows, db=None):
     """out (M, K) += A^T x2 over `rows` rows (A: (rows, >= M) with row stride lda, x2: (rows, K), fp32 or
-    bf16-stored)."""
+    bf16-stored); db (M,): += the column sums of A (the bias gradient) -- in the same kernel pass on the
+    register-staged paths (asrx_wgrad_bias), a column-sum pass otherwise."""
     tiles = ((M + 127) // 128) * ((K + 127) // 128)
     sk = _splitk_for(rows, tiles)
+
+    def staged(a_bf16, b_bf16, name, *tag):
+        lib.require_gpu(A, x2, out)
+        e0 = probe.begin("gemm")
+        if db is not None:
+            lib.call("asrx_wgrad_bias", lib.ptr(A), a_bf16, lda, lib.ptr(x2), b_bf16, K, lib.ptr(out), out.stride(0),
+                     lib.ptr(db), M, K, rows, sk, lib.stream())
+        elif name == "asrx_wgrad_bf16":
+            lib.call(name, lib.ptr(A), lda, lib.ptr(x2), K, lib.ptr(out), out.stride(0), M, K, rows, sk, lib.stream())
+        else:
+            lib.call(name, lib.ptr(A), lda, lib.ptr(x2), b_bf16, K, lib.ptr(out), out.stride(0), M, K, rows, sk,
+                     lib.stream())
+        probe.end("gemm", e0, 2.0 * M * K * rows, ("wgrad", M, K, rows, sk) + tag)
+        return out
+
     if is_bf16(A):
         # a bf16-stored dY (the tied logits' gradient from the fused cross entropy, an activation's bf16
         # gradient from asrx_act_bwd_bias); X fp32 or bf16
@@ -275,35 +291,22 @@ def _wgrad(A, lda, x2, out, M, K, rows):
         if M % 8 or K % (8 if xb else 4) or lda % 8 or x2.stride(0) != K or A.data_ptr() % 16 or x2.data_ptr() % 16:
             A = A.float()
         else:
-            lib.require_gpu(A, x2, out)
-            e0 = probe.begin("gemm")
-            lib.call("asrx_wgrad_bf16_ab", lib.ptr(A), lda, lib.ptr(x2), int(xb), K, lib.ptr(out), out.stride(0), M, K,
-                     rows, sk, lib.stream())
-            probe.end("gemm", e0, 2.0 * M * K * rows, ("wgrad", M, K, rows, sk, 2 + int(xb)))
-            return out
+            return staged(1, int(xb), "asrx_wgrad_bf16_ab", 2 + int(xb))
     if is_bf16(x2):
         # a bf16-stored activation: the register-staged bf16 kernel at every shape (its X bytes halve)
         if M % 4 or K % 8 or lda % 4 or x2.stride(0) != K or A.data_ptr() % 16:
             x2 = x2.float()
         else:
-            lib.require_gpu(A, x2, out)
-            e0 = probe.begin("gemm")
-            lib.call("asrx_wgrad_bf16_ex", lib.ptr(A), lda, lib.ptr(x2), 1, K, lib.ptr(out), out.stride(0), M, K,
-                     rows, sk, lib.stream())
-            probe.end("gemm", e0, 2.0 * M * K * rows, ("wgrad", M, K, rows, sk, 1))
-            return out
+            return staged(0, 1, "asrx_wgrad_bf16_ex", 1)
     ok4 = M % 4 == 0 and K % 4 == 0 and lda % 4 == 0 and A.data_ptr() % 16 == 0 and x2.data_ptr() % 16 == 0
     # register-staged bf16 kernel with transpose reads (csrc/gemm_wg.hip): faster where the output
     # has few tiles (D x D weights, 1.2-2.6x on the 8192-row text side); the wide 1152/1536 outputs at
     # 192k rows stay on the split-K LDS-DMA kernel (5-12 % faster there, tools/wgrad_bench.py)
     if prec.get() == prec.PREC_BF16 and ok4 and x2.stride(0) == K and (tiles <= 9 or rows <= 16384):
-        lib.require_gpu(A, x2, out)
-        e0 = probe.begin("gemm")
-        lib.call("asrx_wgrad_bf16", lib.ptr(A), lda, lib.ptr(x2), K, lib.ptr(out), out.stride(0), M, K, rows, sk,
-                 lib.stream())
-        probe.end("gemm", e0, 2.0 * M * K * rows, ("wgrad", M, K, rows, sk))
-        return out
+        return staged(0, 0, "asrx_wgrad_bf16")
     gemm(A, x2, out, M=M, N=K, K=rows, lda=lda, ldb=K, ldc=K, a_kc=False, b_kc=False, beta=1.0, splitk=sk)
+    if db is not None:
+        lib.call("asrx_colsum_ld", lib.ptr(A), lda, lib.ptr(db), rows, M, lib.stream())
     return out
 
 
@@ -314,8 +317,9 @@ def wgrad_cols(dy, c0, n, x, out):
     return _wgrad(dy[:, c0:], ld, x, out, n, x.shape[1], rows)
 
 
-def linear_wgrad(dy, x, out=None, accumulate=False):
-    """dW = dy^T @ x (N, K) summed over all rows; accumulates into `out` when accumulate=True."""
+def linear_wgrad(dy, x, out=None, accumulate=False, db=None):
+    """dW = dy^T @ x (N, K) summed over all rows; accumulates into `out` when accumulate=True.  db (N,):
+    the bias gradient, += column sums of dy (fused into the weight-gradient pass where it can be)."""
     d2 = _rows(dy)
     x2 = _rows(x)
     if not d2.is_contiguous():
@@ -328,4 +332,4 @@ def linear_wgrad(dy, x, out=None, accumulate=False):
         out = torch.zeros(N, K, device=dy.device, dtype=torch.float32)
     elif not accumulate:
         out.zero_()
-    return _wgrad(d2, N, x2, out, N, K, M)
+    return _wgrad(d2, N, x2, out, N, K, M, db=db)

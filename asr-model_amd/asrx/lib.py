@@ -169,6 +169,7 @@ SIGNATURES = {
     "asrx_ce_part_fwd": (_i32, [_p, _i64] + [_p] * 6 + [_i64, _i64, _p]),
     "asrx_ce_bwd_bf16": (_i32, [_p] * 6 + [_i64, _i64, _p]),
     "asrx_wgrad_bf16_ab": (_i32, [_p, _i64, _p, _i32, _i64, _p, _i64, _i64, _i64, _i64, _i64, _p]),
+    "asrx_wgrad_bias": (_i32, [_p, _i32, _i64, _p, _i32, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _p]),
     "asrx_act_bwd_bias": (_i32, [_p, _p, _p, _p, _i64, _i64, _i32, _p]),
     "asrx_abby_fwd_res": (_i32, [_p] * 9 + [_i64] * 5 + [_u32, _i32, _p]),
     "asrx_gemm_wn_res": (_i32, [_p, _i64, _p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _i64, _i32, _p]),

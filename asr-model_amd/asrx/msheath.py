@@ -204,8 +204,7 @@ class MSheathFn(torch.autograd.Function):
                  _P(gb(mg.bias)), rows, D, 1, SIG, 1.0, st)
         m0, m2l = mod.mlp[0], mod.mlp[2]
         da1 = G.linear_dgrad(dhh, m2l.weight)
-        G.linear_wgrad(dhh, sv["a1"], out=gb(m2l.weight), accumulate=True)
-        ops.colsum(dhh.view(rows, D), out=gb(m2l.bias))
+        G.linear_wgrad(dhh, sv["a1"], out=gb(m2l.weight), accumulate=True, db=gb(m2l.bias))
         H1 = da1.shape[-1]
         if prec.get() == prec.PREC_BF16 and H1 % 8 == 0 and G.use_wide(H1):
             # perf mode: silu' applied, the gradient stored bf16 for both GEMMs, mlp[0]'s bias gradient
@@ -257,8 +256,7 @@ class MSheathFn(torch.autograd.Function):
             ad = lay["adapter"]
             if ad is not None:
                 dpx = G.linear_dgrad(dout, ad.weight, mtiles=s["mt"])  # rows off the layer: not read below
-                G.linear_wgrad(dout, s["px"], out=gb(ad.weight), accumulate=True)
-                ops.colsum(dout.view(rows, D), out=gb(ad.bias))
+                G.linear_wgrad(dout, s["px"], out=gb(ad.weight), accumulate=True, db=gb(ad.bias))
             else:
                 dpx = dout
             # LayerNorm + gate + |x| + v_gate backward in one row pass; dSH = [dS | dh]

@@ -300,14 +300,19 @@ class Linear(torch.autograd.Function):
             else:
                 dx = G.linear_dgrad(gz, W)
         dW = db = None
+        gb = None
+        if db_done is None and ctx.has_b and ctx.needs_input_grad[2]:
+            gb = _gbuf(b, True) if ctx.db else torch.zeros(N, device=gy.device)
         if ctx.needs_input_grad[1]:
             gW = _gbuf(W3, ctx.dW)
-            G.linear_wgrad(gz, x, out=gW.view(W.shape), accumulate=True)
+            G.linear_wgrad(gz, x, out=gW.view(W.shape), accumulate=True, db=gb)  # bias gradient in the same pass
             dW = _gret(W3, gW, ctx.dW)
+            if gb is not None:
+                db_done, gb = gb, None
         if db_done is not None:
             db = _gret(b, db_done, ctx.db)
-        elif ctx.has_b and ctx.needs_input_grad[2]:
-            db = _gret(b, colsum(gz, out=_gbuf(b, True) if ctx.db else None), ctx.db)
+        elif gb is not None:
+            db = _gret(b, colsum(gz, out=gb), ctx.db)
         return dx, dW, db, None, None, None, None, None
 
 
@@ -362,12 +367,17 @@ class LinearRes(torch.autograd.Function):
             else:
                 dx = G.linear_dgrad(gy, W)
         dW = db = None
+        gb = None
+        if ctx.has_b and ctx.needs_input_grad[3]:
+            gb = _gbuf(b, True) if ctx.db else torch.zeros(W.shape[0], device=gy.device)
         if ctx.needs_input_grad[2]:
             gW = _gbuf(W, ctx.dW)
-            G.linear_wgrad(gy, x, out=gW, accumulate=True)
+            G.linear_wgrad(gy, x, out=gW, accumulate=True, db=gb)  # bias gradient in the same pass
             dW = _gret(W, gW, ctx.dW)
-        if ctx.has_b and ctx.needs_input_grad[3]:
-            db = _gret(b, colsum(gy, out=_gbuf(b, True) if ctx.db else None), ctx.db)
+        elif gb is not None:
+            colsum(gy, out=gb)
+        if gb is not None:
+            db = _gret(b, gb, ctx.db)
         return gy if ctx.needs_input_grad[0] else None, dx, dW, db, None
 
 
@@ -426,11 +436,15 @@ class KVProjFn(torch.autograd.Function):
         dWf = dbf = None
         if ctx.needs_input_grad[1]:
             gW = _gbuf(W, ctx.dW)
+            gb = _gbuf(b, ctx.db) if ctx.needs_input_grad[2] else None
             for i, gpart in enumerate((dk, dv)):
                 if gpart is not None:
-                    G.linear_wgrad(gpart, x, out=gW[i * D:(i + 1) * D], accumulate=True)
+                    G.linear_wgrad(gpart, x, out=gW[i * D:(i + 1) * D], accumulate=True,
+                                   db=None if gb is None else gb[i * D:(i + 1) * D])
             dWf = _gret(W, gW, ctx.dW)
-        if ctx.needs_input_grad[2]:
+            if gb is not None:
+                dbf = _gret(b, gb, ctx.db)
+        elif ctx.needs_input_grad[2]:
             gb = _gbuf(b, ctx.db)
             for i, gpart in enumerate((dk, dv)):
                 if gpart is not None:
@@ -567,8 +581,8 @@ class AbbyNormalFn(torch.autograd.Function):
         G.linear_dgrad(dh, W1, out=dx, beta=1.0)
         if ctx.sink is not None:
             dx = None
-        dW1 = G.linear_wgrad(dh, x, out=_gbuf(W1, fW1), accumulate=True)
-        db1 = colsum(dh.view(-1, d), out=_gbuf(b1, fb1))
+        db1 = _gbuf(b1, fb1)  # bias gradient summed in the weight-gradient pass
+        dW1 = G.linear_wgrad(dh, x, out=_gbuf(W1, fW1), accumulate=True, db=db1)
         return (dx, _gret(W1, dW1, fW1), _gret(b1, db1, fb1), _gret(W2, dW2, fW2), _gret(b2, db2, fb2),
                 None, None, None, None, None, None, None, None, None, None, None, None,
                 gout if ctx.has_res and ctx.needs_input_grad[17] else None)
@@ -820,8 +834,8 @@ class VGateFn(torch.autograd.Function):
         G.linear_dgrad(dh, W1, out=dx, beta=1.0)
         lib.call("asrx_rownorm_bwd", _P(dnx), _P(x2), _P(nx), _P(dx), rows, D, _S())
         dmkeyn = G.linear_wgrad(dS, x2)
-        dW1 = G.linear_wgrad(dh, x2, out=_gbuf(W1, fW1), accumulate=True)
-        db1 = colsum(dh, out=_gbuf(b1, fb1))
+        db1 = _gbuf(b1, fb1)
+        dW1 = G.linear_wgrad(dh, x2, out=_gbuf(W1, fW1), accumulate=True, db=db1)
         return (dx.view(x.shape), dmkeyn, _gret(mval, dmval.view(M, 1), fmval), _gret(W1, dW1, fW1),
                 _gret(b1, db1, fb1), _gret(W2, dW2.view(1, Dh), fW2), _gret(b2, db2, fb2),
                 _gret(cw, dcw.view(1, 2), fcw), _gret(cb, dcb, fcb), None)

@@ -33,6 +33,9 @@ struct Params {
   int M, N;
   int64_t R, kchunk;
   int splitk;
+  // optional bias gradient (asrx_wgrad_bias): db[m] += sum over rows of dY[:, m], summed from the dY
+  // stages this kernel loads anyway (column tile 0 only), instead of a separate column-sum pass
+  float* db;
 };
 
 // byte offset of 16-B chunk ch (8 features) of k-row `row` in a [32][128] bf16 image
@@ -164,6 +167,30 @@ __device__ __forceinline__ int xcd_item(int bid, int nblk) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
+// per-thread column partials of a dY stage: fp32 dY -- features 4 (t & 31) .. +3 of rows (t >> 5) + 8 i;
+// bf16 dY -- features 8 (t & 15) .. +7 of rows (t >> 4) + 16 i (zero-page rows past the end add 0)
+template <bool ABF, bool BBF>
+__device__ __forceinline__ void colacc(const Stage<ABF, BBF>& st, float (&cs)[8]) {
+  if constexpr (ABF) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const unsigned u = st.ah[i][w];
+        cs[2 * w] += __builtin_bit_cast(float, u << 16);
+        cs[2 * w + 1] += __builtin_bit_cast(float, u & 0xffff0000u);
+      }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      cs[0] += st.a[i].x;
+      cs[1] += st.a[i].y;
+      cs[2] += st.a[i].z;
+      cs[3] += st.a[i].w;
+    }
+  }
+}
+
 template <bool ABF, bool BBF>
 __global__ __launch_bounds__(NT, 2) void wgrad_wr_kernel(Params p) {
   __shared__ __attribute__((aligned(16))) char Ai[2][TK * TM * 2];
@@ -185,8 +212,11 @@ __global__ __launch_bounds__(NT, 2) void wgrad_wr_kernel(Params p) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   Stage<ABF, BBF> s0, s1;
+  const bool dbon = p.db && n0 == 0;  // uniform
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   load(p, s0, rb, re, m0, n0);
   load(p, s1, rb + TK, re, m0, n0);
+  if (dbon && nk > 0) colacc(s0, cs);
   store(s0, Ai[0], Bi[0]);
   __syncthreads();
 
@@ -204,7 +234,10 @@ __global__ __launch_bounds__(NT, 2) void wgrad_wr_kernel(Params p) {
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt)
         acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt], b[nt], acc[mt][nt], 0, 0, 0);
-    if (s + 1 < nk) store(nxt, Ai[(s + 1) & 1], Bi[(s + 1) & 1]);
+    if (s + 1 < nk) {
+      if (dbon) colacc(nxt, cs);
+      store(nxt, Ai[(s + 1) & 1], Bi[(s + 1) & 1]);
+    }
     __syncthreads();
   };
   for (int s = 0; s < nk; s += 2) {
@@ -226,6 +259,28 @@ __global__ __launch_bounds__(NT, 2) void wgrad_wr_kernel(Params p) {
         if (m < p.M && nk > 0) atomicAdd(p.C + (int64_t)m * p.ldc + n, acc[mt][nt][r]);
       }
     }
+  if (dbon && nk > 0) {
+    // lanes sharing a feature group: fp32 dY -- t and t ^ 32 within a wave, then the 4 waves;
+    // bf16 dY -- t, t ^ 16, t ^ 32, t ^ 48, then the 4 waves (through the retired A images)
+    constexpr int F = ABF ? 8 : 4;
+#pragma unroll
+    for (int f = 0; f < F; ++f) {
+      cs[f] += __shfl_xor(cs[f], 32);
+      if (ABF) cs[f] += __shfl_xor(cs[f], 16);
+    }
+    __syncthreads();  // every wave is past its last LDS read of the images
+    float* red = reinterpret_cast<float*>(Ai[0]);  // [4 waves][128 features]
+    const int t = threadIdx.x, lane = t & 63;
+    const bool wr = ABF ? lane < 16 : lane < 32;
+    if (wr) {
+      const int f0 = ABF ? 8 * (lane & 15) : 4 * (lane & 31);
+#pragma unroll
+      for (int f = 0; f < F; ++f) red[(t >> 6) * TM + f0 + f] = cs[f];
+    }
+    __syncthreads();
+    if (t < TM && m0 + t < p.M)
+      atomicAdd(p.db + m0 + t, red[t] + red[TM + t] + red[2 * TM + t] + red[3 * TM + t]);
+  }
 }
 
 }  // namespace wg
@@ -237,7 +292,8 @@ using namespace asrx;
 // split over `splitk` work items (bf16 operands, fp32 accumulate).  M, N, lda, ldb multiples of 4,
 // 16-byte aligned operands.
 static int wgrad_launch(const void* A, int a_bf16, int64_t lda, const void* B, int b_bf16, int64_t ldb, float* C,
-                        int64_t ldc, int64_t M, int64_t N, int64_t R, int64_t splitk, hipStream_t stream) {
+                        int64_t ldc, int64_t M, int64_t N, int64_t R, int64_t splitk, hipStream_t stream,
+                        float* db = nullptr) {
   ASRX_REQUIRE(M > 0 && N > 0 && R >= 0, "asrx_wgrad_bf16: empty problem");
   ASRX_REQUIRE(M % 4 == 0 && N % 4 == 0 && lda % 4 == 0 && ldb % 4 == 0, "asrx_wgrad_bf16: M, N, lda, ldb %% 4 required");
   ASRX_REQUIRE(!b_bf16 || (N % 8 == 0 && ldb % 8 == 0), "asrx_wgrad_bf16: a bf16 X needs N, ldb %% 8");
@@ -248,7 +304,7 @@ static int wgrad_launch(const void* A, int a_bf16, int64_t lda, const void* B, i
   int64_t kchunk = (R + splitk - 1) / splitk;
   kchunk = (kchunk + wg::TK - 1) / wg::TK * wg::TK;
   splitk = (R + kchunk - 1) / kchunk;
-  wg::Params p{(const float*)A, (const float*)B, C, lda, ldb, ldc, (int)M, (int)N, R, kchunk, (int)splitk};
+  wg::Params p{(const float*)A, (const float*)B, C, lda, ldb, ldc, (int)M, (int)N, R, kchunk, (int)splitk, db};
   const int64_t items = ((M + wg::TM - 1) / wg::TM) * ((N + wg::TN - 1) / wg::TN) * splitk;
   ASRX_REQUIRE(items < (1LL << 31), "asrx_wgrad_bf16: too many work items");
   if (a_bf16 && b_bf16)
@@ -279,4 +335,14 @@ extern "C" int asrx_wgrad_bf16_ex(const float* A, int64_t lda, const void* B, in
 extern "C" int asrx_wgrad_bf16_ab(const void* A, int64_t lda, const void* B, int b_bf16, int64_t ldb, float* C,
                                   int64_t ldc, int64_t M, int64_t N, int64_t R, int64_t splitk, hipStream_t stream) {
   return wgrad_launch(A, 1, lda, B, b_bf16, ldb, C, ldc, M, N, R, splitk, stream);
+}
+
+// dW += dY^T X and db += column sums of dY in one pass (the bias gradient of y = x W^T + b summed from
+// the dY stages the weight-gradient kernel loads anyway; replaces a separate asrx_colsum over dY):
+// dY fp32 (a_bf16 = 0) or bf16 (1), X fp32 or bf16, as asrx_wgrad_bf16_ex / _ab.
+extern "C" int asrx_wgrad_bias(const void* A, int a_bf16, int64_t lda, const void* B, int b_bf16, int64_t ldb,
+                               float* C, int64_t ldc, float* db, int64_t M, int64_t N, int64_t R, int64_t splitk,
+                               hipStream_t stream) {
+  ASRX_REQUIRE(db, "asrx_wgrad_bias: db required");
+  return wgrad_launch(A, a_bf16, lda, B, b_bf16, ldb, C, ldc, M, N, R, splitk, stream, db);
 }

@@ -346,7 +346,7 @@ __global__ __launch_bounds__(64 * RW) void rownorm_kernel(const float* __restric
   for (int64_t r = row_begin(); r < rows; r += row_step()) {
     float s = 0.f;
     for (int j = lane; j < d; j += 64) s += x[r * d + j] * x[r * d + j];
-    s = wave_sum(s);
+    s = wave_sum_dpp(s);
     if (lane == 0) n[r] = sqrtf(s);
   }
 }
@@ -573,7 +573,8 @@ __global__ __launch_bounds__(64 * RW) void msheath_row_fwd_kernel(MSRowFwd p) {
   const float gbias = p.gb[0];
   const float mv_l = lane < p.M ? p.mval[lane] : 0.f;
   const float b2 = p.b2[0], cw0 = p.cw[0], cw1 = p.cw[1], cb = p.cb[0], tx = p.tx[0];
-  auto at_layer = [&](int64_t rr) { return !p.next_i || p.next_i[rr / p.L] == (float)p.layer; };
+  // 32-bit sample index (rows < 2^31): a 64-bit division by the runtime L cost ~3x the instructions
+  auto at_layer = [&](int64_t rr) { return !p.next_i || p.next_i[(unsigned)rr / (unsigned)p.L] == (float)p.layer; };
   // the next row's x AND its v_gate projections (S[lane], h) are loaded while this row is processed
   // (the SH row -- M + Dh floats -- was read only after the LayerNorm, its latency exposed per row)
   constexpr int HQ = (E + 1) / 2;  // h values per lane (Dh = D / 2 <= 64 HQ)
@@ -642,15 +643,15 @@ __global__ __launch_bounds__(64 * RW) void msheath_row_fwd_kernel(MSRowFwd p) {
     // v_gate
     const float inx = 1.0f / fmaxf(nrm, 1e-12f);
     const float z = lane < p.M ? sv * inx * p.inv_sqrt_d : -INFINITY;
-    const float zm = wave_max(z);
+    const float zm = wave_max_dpp(z);
     const float ez = lane < p.M ? expf(z - zm) : 0.f;
-    const float se = wave_sum(ez);
-    const float kv = wave_sum(lane < p.M ? ez / se * mv_l : 0.f);
+    const float se = wave_sum_dpp(ez);
+    const float kv = wave_sum_dpp(lane < p.M ? ez / se * mv_l : 0.f);
     float acc = 0.f;
 #pragma unroll
     for (int i = 0; i < HQ; ++i)
       if (lane + 64 * i < p.Dh) acc += silu_f(hv[i]) * p.w2[lane + 64 * i];
-    const float m2 = wave_sum(acc) + b2;
+    const float m2 = wave_sum_dpp(acc) + b2;
     const float xval = cw0 * kv + cw1 * m2 + cb;
     if (lane == 0) {
       p.mean[r] = mu;
@@ -710,7 +711,8 @@ __global__ __launch_bounds__(64 * RW) void msheath_row_bwd_kernel(MSRowBwd p) {
     float s, gi, nx, g, dg, mu, rs, kv, m2;
   };
   Pre nx_;
-  auto at_layer = [&](int64_t rr) { return !p.next_i || p.next_i[rr / p.L] == (float)p.layer; };
+  // 32-bit sample index (rows < 2^31): a 64-bit division by the runtime L cost ~3x the instructions
+  auto at_layer = [&](int64_t rr) { return !p.next_i || p.next_i[(unsigned)rr / (unsigned)p.L] == (float)p.layer; };
   auto fetch = [&](int64_t rr) __attribute__((always_inline)) {
     if (rr < p.rows && at_layer(rr)) {
       const float* S = p.SH + rr * p.ldsh;
@@ -749,18 +751,18 @@ __global__ __launch_bounds__(64 * RW) void msheath_row_bwd_kernel(MSRowBwd p) {
     float* dh = dS + M;
     const float sl = c.s;
     const float z = lane < M ? sl * inx * p.inv_sqrt_d : -INFINITY;
-    const float zm = wave_max(z);
+    const float zm = wave_max_dpp(z);
     const float ez = lane < M ? expf(z - zm) : 0.f;
-    const float key = ez / wave_sum(ez);
+    const float key = ez / wave_sum_dpp(ez);
     const float dkv = gi * cw0, dm2 = gi * cw1;
     const float dkey = lane < M ? dkv * mv_l : 0.f;
-    const float dot = wave_sum(key * dkey);
+    const float dot = wave_sum_dpp(key * dkey);
     const float dz = lane < M ? key * (dkey - dot) : 0.f;
     if (lane < M) {
       dS[lane] = dz * inx * p.inv_sqrt_d;
       pw[lane] += dkv * key;
     }
-    const float dinx = wave_sum(lane < M ? dz * sl * p.inv_sqrt_d : 0.f);
+    const float dinx = wave_sum_dpp(lane < M ? dz * sl * p.inv_sqrt_d : 0.f);
     const float dnx = nxr > 1e-12f ? -dinx * inx * inx : 0.f;
 #pragma unroll
     for (int i = 0; i < HQ; ++i) {
@@ -886,9 +888,9 @@ __global__ __launch_bounds__(64 * RW) void tgate_bwd_kernel(const float* __restr
       dg[D + j] = go * t1 * g1 * (1.f - g1);
       dg[2 * D + j] = go * t2 * g2 * (1.f - g2);
     }
-    a0 = wave_sum(a0);
-    a1 = wave_sum(a1);
-    a2 = wave_sum(a2);
+    a0 = wave_sum_dpp(a0);
+    a1 = wave_sum_dpp(a1);
+    a2 = wave_sum_dpp(a2);
     const float dot = t0 * a0 + t1 * a1 + t2 * a2;
     if (lane == 0) {
       dc[r * 3] = t0 * (a0 - dot);
@@ -926,7 +928,7 @@ __global__ __launch_bounds__(64 * RW) void axpy_row_bwd_kernel(const float* __re
       dy[r * d + j] = sc * gv;
       if (dxc) dxc[r * d + j] = gv;
     }
-    acc = wave_sum(acc);
+    acc = wave_sum_dpp(acc);
     if (lane == 0) ds[r] = acc;
   }
 }
@@ -1801,7 +1803,7 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const float* __restrict__ z
   const float* zr = z + r * V;
   float m = -INFINITY;
   for (int64_t j = threadIdx.x; j < V; j += 256) m = fmaxf(m, zr[j]);
-  m = wave_max(m);
+  m = wave_max_dpp(m);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();
   m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
@@ -1839,7 +1841,7 @@ __global__ __launch_bounds__(64 * RW) void row_normalize_kernel(const float* __r
   for (int64_t r = row_begin(); r < rows; r += row_step()) {
     float s = 0.f;
     for (int j = lane; j < d; j += 64) s += x[r * d + j] * x[r * d + j];
-    const float nn = fmaxf(sqrtf(wave_sum(s)), 1e-12f);
+    const float nn = fmaxf(sqrtf(wave_sum_dpp(s)), 1e-12f);
     for (int j = lane; j < d; j += 64) y[r * d + j] = x[r * d + j] / nn;
     if (lane == 0) n[r] = nn;
   }
@@ -1853,7 +1855,7 @@ __global__ __launch_bounds__(64 * RW) void row_normalize_bwd_kernel(const float*
     const float nn = n[r];
     float s = 0.f;
     for (int j = lane; j < d; j += 64) s += y[r * d + j] * dy[r * d + j];
-    s = wave_sum(s);
+    s = wave_sum_dpp(s);
     const bool clamped = nn <= 1e-12f;
     for (int j = lane; j < d; j += 64) {
       const float v = (dy[r * d + j] - (clamped ? 0.f : y[r * d + j] * s)) / nn;

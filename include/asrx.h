@@ -491,6 +491,11 @@ int asrx_act_bwd_bias(const float* g, const float* z, unsigned short* gz, float*
  * activation (asrx_act_bwd_bias). */
 int asrx_wgrad_bf16_ab(const void* A, int64_t lda, const void* B, int b_bf16, int64_t ldb, float* C, int64_t ldc,
                        int64_t M, int64_t N, int64_t R, int64_t splitk, asrx_stream_t stream);
+/* dW += dY^T X and db += column sums of dY in one pass (bias gradient of y = x W^T + b, replacing the
+ * nn.Linear backward's separate bias reduction; model.py Linear layers): dY fp32 (a_bf16 = 0) or bf16 (1),
+ * X fp32 (b_bf16 = 0) or bf16 (1), shapes as asrx_wgrad_bf16_ex / _ab. */
+int asrx_wgrad_bias(const void* A, int a_bf16, int64_t lda, const void* B, int b_bf16, int64_t ldb, float* C,
+                    int64_t ldc, float* db, int64_t M, int64_t N, int64_t R, int64_t splitk, asrx_stream_t stream);
 /* BatchNorm1d running statistics from per-clip (B, C) mean / rstd (ConvLite.bn, model.py:101);
  * nbt (num_batches_tracked, int64) may be NULL.  asrx_rsqrt_eps: eval-mode rstd. */
 int asrx_bn_running(const float* mean, const float* rstd, float* rm, float* rv, int64_t* nbt, int64_t B, int64_t C,

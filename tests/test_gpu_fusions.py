@@ -124,3 +124,34 @@ def test_abby_residual_matches_add(cuda, d, rows):
     for n in res[0][3]:
         a, c = res[0][3][n], res[1][3][n]
         assert float((a - c).abs().max() / c.abs().max().clamp_min(1e-30)) < 1e-5, n
+
+
+@pytest.mark.parametrize("a_bf16,b_bf16", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("R,M,N,splitk", [(5000, 384, 384, 4), (777, 200, 136, 1), (8192, 1536, 384, 8)])
+def test_wgrad_bias_matches_colsum(cuda, a_bf16, b_bf16, R, M, N, splitk):
+    """asrx_wgrad_bias (bias gradient summed from the weight-gradient kernel's dY stages) == the weight
+    gradient of asrx_wgrad_bf16* plus asrx_colsum of dY."""
+    from asrx import lib
+
+    if a_bf16 and M % 8 or b_bf16 and N % 8:
+        pytest.skip("bf16 operands need multiples of 8")
+    g = torch.Generator().manual_seed(R + M + N)
+    dy = torch.randn(R, M, generator=g).to(cuda)
+    x = torch.randn(R, N, generator=g).to(cuda)
+    dyb = dy.to(torch.bfloat16) if a_bf16 else dy
+    xb = x.to(torch.bfloat16) if b_bf16 else x
+    dw = torch.zeros(M, N, device=cuda)
+    db = torch.zeros(M, device=cuda)
+    lib.call("asrx_wgrad_bias", lib.ptr(dyb), a_bf16, M, lib.ptr(xb), b_bf16, N, lib.ptr(dw), N, lib.ptr(db), M, N, R,
+             splitk, lib.stream())
+    dw_ref = torch.zeros(M, N, device=cuda)
+    if a_bf16:
+        lib.call("asrx_wgrad_bf16_ab", lib.ptr(dyb), M, lib.ptr(xb), b_bf16, N, lib.ptr(dw_ref), N, M, N, R, splitk,
+                 lib.stream())
+    else:
+        lib.call("asrx_wgrad_bf16_ex", lib.ptr(dyb), M, lib.ptr(xb), b_bf16, N, lib.ptr(dw_ref), N, M, N, R, splitk,
+                 lib.stream())
+    db_ref = dyb.float().double().sum(0)
+    torch.cuda.synchronize()
+    assert float((dw - dw_ref).abs().max() / dw_ref.abs().max()) < 1e-5
+    assert float((db.double() - db_ref).abs().max() / db_ref.abs().max()) < 1e-5
