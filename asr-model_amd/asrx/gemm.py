@@ -263,6 +263,11 @@ def _splitk_for(m_rows: int, tiles: int) -> int:
     return int(max(1, min(want, m_rows // 256)))
 
 
+# bias gradients summed inside the weight-gradient kernel (False: a separate column-sum pass; the
+# fusion test compares the two on a whole model)
+FUSED_BIAS_GRAD = True
+
+
 def _wgrad(A, lda, x2, out, M, K, rows, db=None):
     """out (M, K) += A^T x2 over `rows` rows (A: (rows, >= M) with row stride lda, x2: (rows, K), fp32 or
     bf16-stored); db (M,): += the column sums of A (the bias gradient) -- in the same kernel pass on the
@@ -273,7 +278,11 @@ def _wgrad(A, lda, x2, out, M, K, rows, db=None):
     def staged(a_bf16, b_bf16, name, *tag):
         lib.require_gpu(A, x2, out)
         e0 = probe.begin("gemm")
-        if db is not None:
+        if db is not None and not FUSED_BIAS_GRAD:
+            staged_db, db_ = db, None
+        else:
+            staged_db, db_ = None, db
+        if db_ is not None:
             lib.call("asrx_wgrad_bias", lib.ptr(A), a_bf16, lda, lib.ptr(x2), b_bf16, K, lib.ptr(out), out.stride(0),
                      lib.ptr(db), M, K, rows, sk, lib.stream())
         elif name == "asrx_wgrad_bf16":
@@ -282,6 +291,10 @@ def _wgrad(A, lda, x2, out, M, K, rows, db=None):
             lib.call(name, lib.ptr(A), lda, lib.ptr(x2), b_bf16, K, lib.ptr(out), out.stride(0), M, K, rows, sk,
                      lib.stream())
         probe.end("gemm", e0, 2.0 * M * K * rows, ("wgrad", M, K, rows, sk) + tag)
+        if staged_db is not None:  # unfused reference: column sums of dY (fp32 copy when bf16-stored)
+            Af = A.float() if a_bf16 else A
+            lib.call("asrx_colsum_ld", lib.ptr(Af), Af.stride(0) if a_bf16 else lda, lib.ptr(staged_db), rows, M,
+                     lib.stream())
         return out
 
     if is_bf16(A):

@@ -155,3 +155,42 @@ def test_wgrad_bias_matches_colsum(cuda, a_bf16, b_bf16, R, M, N, splitk):
     torch.cuda.synchronize()
     assert float((dw - dw_ref).abs().max() / dw_ref.abs().max()) < 1e-5
     assert float((db.double() - db_ref).abs().max() / db_ref.abs().max()) < 1e-5
+
+
+def test_model_bias_grads_fused_match_colsum(cuda):
+    """A whole bf16 training step (tiny dims, 2 layers): every parameter gradient with the bias gradients
+    summed inside the weight-gradient kernel == with the separate column-sum pass (summation order only)."""
+    from asrx import gemm as G
+    from asrx import prec
+    from asrx.config import Dimensions
+    from asrx.model import Model
+
+    import model_parity as mp
+
+    cfg = Dimensions(tokens=1000, mels=128, dims=384, head=6, layer=2, act="gelu", n_type="AbbyNormal")
+    torch.manual_seed(0)
+    model = Model(cfg).to(cuda).train()
+    x = mp.inputs(1, 3.0, 32, cfg.tokens, 0)
+    res = []
+    for fused in (True, False):
+        G.FUSED_BIAS_GRAD = fused
+        try:
+            model.zero_grad(set_to_none=True)
+            model.set_noise(7, 3)
+            with prec.precision("bf16"):
+                out = model(labels=x["labels"].to(cuda), text_ids=x["text_ids"].to(cuda),
+                            spectrogram=x["spectrogram"].to(cuda), pitch=x["pitch"].to(cuda),
+                            waveform=x["waveform"].to(cuda))
+                out["loss"].backward()
+            torch.cuda.synchronize()
+        finally:
+            G.FUSED_BIAS_GRAD = True
+        res.append({n: p.grad.detach().clone() for n, p in model.named_parameters() if p.grad is not None})
+    assert set(res[0]) == set(res[1])
+    scale = max(float(g.abs().max()) for g in res[1].values())
+    nb = 0
+    for n in res[1]:
+        d = float((res[0][n] - res[1][n]).abs().max())
+        assert d <= 1e-4 * max(float(res[1][n].abs().max()), 1e-3 * scale), (n, d)
+        nb += n.endswith("bias")
+    assert nb > 10
