@@ -158,8 +158,9 @@ def test_wgrad_bias_matches_colsum(cuda, a_bf16, b_bf16, R, M, N, splitk):
 
 
 def test_model_bias_grads_fused_match_colsum(cuda):
-    """A whole bf16 training step (tiny dims, 2 layers): every parameter gradient with the bias gradients
-    summed inside the weight-gradient kernel == with the separate column-sum pass (summation order only)."""
+    """A whole bf16 training step (tiny dims, 2 layers): every bias gradient with the sums inside the
+    weight-gradient kernel == with the separate column-sum pass, as close as the unfused step is to a
+    rerun of itself (the step's other gradient sums use fp32 atomics, whose order varies run to run)."""
     from asrx import gemm as G
     from asrx import prec
     from asrx.config import Dimensions
@@ -172,7 +173,7 @@ def test_model_bias_grads_fused_match_colsum(cuda):
     model = Model(cfg).to(cuda).train()
     x = mp.inputs(1, 3.0, 32, cfg.tokens, 0)
     res = []
-    for fused in (True, False):
+    for fused in (True, False, False):
         G.FUSED_BIAS_GRAD = fused
         try:
             model.zero_grad(set_to_none=True)
@@ -186,11 +187,13 @@ def test_model_bias_grads_fused_match_colsum(cuda):
         finally:
             G.FUSED_BIAS_GRAD = True
         res.append({n: p.grad.detach().clone() for n, p in model.named_parameters() if p.grad is not None})
-    assert set(res[0]) == set(res[1])
-    scale = max(float(g.abs().max()) for g in res[1].values())
+    assert set(res[0]) == set(res[1]) == set(res[2])
     nb = 0
     for n in res[1]:
+        if not n.endswith("bias"):
+            continue
+        nb += 1
         d = float((res[0][n] - res[1][n]).abs().max())
-        assert d <= 1e-4 * max(float(res[1][n].abs().max()), 1e-3 * scale), (n, d)
-        nb += n.endswith("bias")
+        rerun = float((res[2][n] - res[1][n]).abs().max())
+        assert d <= 2e-4 * float(res[1][n].abs().max()) + 4 * rerun, (n, d, rerun)
     assert nb > 10
