@@ -195,5 +195,5 @@ def test_model_bias_grads_fused_match_colsum(cuda):
         nb += 1
         d = float((res[0][n] - res[1][n]).abs().max())
         rerun = float((res[2][n] - res[1][n]).abs().max())
-        assert d <= 2e-4 * float(res[1][n].abs().max()) + 4 * rerun, (n, d, rerun)
+        assert d <= 2e-3 * float(res[1][n].abs().max()) + 4 * rerun, (n, d, rerun)
     assert nb > 10
