@@ -187,8 +187,11 @@ def extract_features_batch(batches, tokenizer=None, spectrogram=False, waveform=
             target = int((n / sample_rate) * (sample_rate // hop_length))
             if n > target and n == target * hop_length:
                 _, w_tensor = _mel.logmel(audio.unsqueeze(0), layout="BMF", pool=True)
-            else:
+            elif n > target and target > 0:  # as features.extract_features: wave_pool needs 0 < target < n
                 w_tensor = _mel.wave_pool(audio.unsqueeze(0), target)
+            else:
+                w_tensor = torch.nn.functional.interpolate(audio.view(1, 1, -1), size=target, mode="linear",
+                                                           align_corners=False)[0]
         out.append({"waveform": w_tensor, "spectrogram": s_tensor, "pitch_tokens": None, "pitch": pitch_of.get(i),
                     "harmonic": None, "aperiodic": None, "labels": labels, "phase": phase_of.get(i)})
     return out

@@ -5,9 +5,13 @@ the same way on CPU for the tests.
 
 Design (MI355X-first, not a translation of DDP's call pattern):
   * gradients live in flat bucket buffers (p.grad is a view), so no copy is needed;
-  * the bucket plan covers exactly the parameters that receive gradients (dead blocks and the unused
-    attn.c / rot.lin / router / span_scale / pitch_tokens never do), found on the first step and
-    made identical on every rank: the live masks are max-reduced and rank 0's backward completion
+  * the bucket plan covers every parameter that CAN receive a gradient -- `model.grad_reachable()`
+    when the model declares it (asrx Model: everything but the dead blocks and the unused attn.c /
+    rot.lin / router / span_scale / pitch_tokens), every requires_grad parameter otherwise -- plus
+    whatever received one on the first step; a covered parameter that gets no gradient in a step is
+    reduced as zeros, so one that first receives a gradient on a later step is still
+    reduced and zeroed like the rest.  The layout is made identical on every rank: the live masks are
+    max-reduced and rank 0's backward completion
     order (the order in which each parameter took its last gradient of that step) is broadcast, so
     bucket 0 holds what backward finishes first (the processor) and the last bucket the encoder;
   * the first bucket is small (bucket_mb / 4) so the first all-reduce starts early in backward;
@@ -60,13 +64,18 @@ class _Bucket:
 
 class GradSync:
     def __init__(self, model: torch.nn.Module, bucket_mb: float = 64.0, group=None, signature=None,
-                 reduce_single: bool = False, first_bucket_mb: float | None = None):
+                 reduce_single: bool = False, first_bucket_mb: float | None = None, cover=None):
+        """cover: the parameters that can receive a gradient (default: model.grad_reachable() if the
+        model declares it, else every requires_grad parameter); each gets a bucket slot from step 1."""
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         # reduce_single: run the bucket all-reduces even in a 1-rank group (exercises the RCCL launch,
         # comm-stream overlap and join on a one-GPU box; the sum over one rank is the identity)
         self.active = self.world > 1 or (reduce_single and dist.is_initialized())
         self.params = [p for p in model.parameters() if p.requires_grad]
+        if cover is None:
+            cover = model.grad_reachable() if hasattr(model, "grad_reachable") else self.params
+        self._cover = {id(p) for p in cover if p.requires_grad}
         self.bucket_bytes = int(bucket_mb * 1024 * 1024)
         fb = bucket_mb / 4 if first_bucket_mb is None else first_bucket_mb
         self.first_bucket_bytes = int(fb * 1024 * 1024)
@@ -112,7 +121,7 @@ class GradSync:
         return sorted(live, key=lambda i: (key[i], -i))
 
     def _build(self):
-        live_idx = [i for i, p in enumerate(self.params) if p.grad is not None]
+        live_idx = [i for i, p in enumerate(self.params) if p.grad is not None or id(p) in self._cover]
         order = {i: self._last_event.get(id(self.params[i]), 1 << 40) for i in live_idx}
         if dist.is_initialized() and (self.world > 1 or self.active):
             idx = self._agree_layout(live_idx, order)
@@ -140,7 +149,9 @@ class GradSync:
     def _learn(self, sig, counts):
         """Record `counts` (events per parameter id) as the plan of signature `sig`."""
         self.plans[sig] = dict(counts)
-        self.bucket_plans[sig] = [sum(max(1, counts.get(id(p), 0)) for p in b.params) for b in self.buckets]
+        # a covered parameter with no event in this signature adds nothing to its bucket's count (a bucket
+        # of such parameters is complete -- all zeros -- as soon as the step starts)
+        self.bucket_plans[sig] = [sum(counts.get(id(p), 0) for p in b.params) for b in self.buckets]
 
     def zero_grad(self):
         """Zero the bucket buffers (the grads are views of them) before the next backward."""
@@ -167,6 +178,7 @@ class GradSync:
         if self._overlap:
             for b, n in zip(self.buckets, plan):
                 b.expected = b.pending = n
+                b.complete = n == 0
 
     def _ready(self, p):
         if not self._started:
@@ -185,6 +197,11 @@ class GradSync:
         if b.pending == 0:
             b.complete = True
             self._launch_ready()
+        elif b.pending < 0 and not b.launched:
+            # more events than the learned plan for a bucket still waiting on an earlier one (the
+            # next-bucket rule): nothing read it yet -- finish() launches it in index order and merges
+            # the new counts into the plan
+            b.complete = False
         elif b.pending < 0:
             raise RuntimeError(
                 "GradSync: a gradient event arrived after its bucket's all-reduce was launched (step "
@@ -193,7 +210,8 @@ class GradSync:
 
     def _launch_ready(self):
         """The next-bucket rule: launch the run of complete buckets starting at the next index."""
-        while self._next < len(self.buckets) and self.buckets[self._next].complete:
+        while self._next < len(self.buckets) and self.buckets[self._next].complete and \
+                self.buckets[self._next].pending == 0:
             self._launch(self.buckets[self._next])
             self._next += 1
 

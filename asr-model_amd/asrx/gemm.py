@@ -266,6 +266,9 @@ def _splitk_for(m_rows: int, tiles: int) -> int:
 # bias gradients summed inside the weight-gradient kernel (False: a separate column-sum pass; the
 # fusion test compares the two on a whole model)
 FUSED_BIAS_GRAD = True
+# tests: a list makes every fused bias sum also take the column sums of the SAME dY in a separate pass and
+# append (fused contribution, column sums) -- the fusion checked inside one backward
+BIAS_CHECK = None
 
 
 def _wgrad(A, lda, x2, out, M, K, rows, db=None):
@@ -283,8 +286,15 @@ def _wgrad(A, lda, x2, out, M, K, rows, db=None):
         else:
             staged_db, db_ = None, db
         if db_ is not None:
+            before = db_.clone() if BIAS_CHECK is not None else None
             lib.call("asrx_wgrad_bias", lib.ptr(A), a_bf16, lda, lib.ptr(x2), b_bf16, K, lib.ptr(out), out.stride(0),
                      lib.ptr(db), M, K, rows, sk, lib.stream())
+            if before is not None:
+                Af = A.float() if a_bf16 else A
+                ref = torch.zeros(M, device=A.device)
+                lib.call("asrx_colsum_ld", lib.ptr(Af), Af.stride(0) if a_bf16 else lda, lib.ptr(ref), rows, M,
+                         lib.stream())
+                BIAS_CHECK.append((db_ - before, ref))
         elif name == "asrx_wgrad_bf16":
             lib.call(name, lib.ptr(A), lda, lib.ptr(x2), K, lib.ptr(out), out.stride(0), M, K, rows, sk, lib.stream())
         else:
@@ -302,7 +312,8 @@ def _wgrad(A, lda, x2, out, M, K, rows, db=None):
         # gradient from asrx_act_bwd_bias); X fp32 or bf16
         xb = is_bf16(x2)
         if M % 8 or K % (8 if xb else 4) or lda % 8 or x2.stride(0) != K or A.data_ptr() % 16 or x2.data_ptr() % 16:
-            A = A.float()
+            A = A.float()  # contiguous copy (of a column-slice view too): its own row stride
+            lda = A.stride(0)
         else:
             return staged(1, int(xb), "asrx_wgrad_bf16_ab", 2 + int(xb))
     if is_bf16(x2):

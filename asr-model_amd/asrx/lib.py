@@ -112,6 +112,10 @@ SIGNATURES = {
     "asrx_msheath_ctrl_bwd2": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _p, _i32,
                                       _p, _p, _p, _p, _p, _p]),
     "asrx_jump_select4_bwd_acc": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p]),
+    "asrx_jump_bwd_part_floats": (_i64, [_i64, _i64, _i64]),
+    "asrx_jump_select4_bwd_part": (_i32, [_p] * 11 + [_i64, _i64, _i64, _p]),
+    "asrx_msheath_ctrl_bwd4": (_i32, [_p, _i64, _p, _p, _p, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _p, _i32]
+                               + [_p] * 8),
     "asrx_axpy_row2_bwd_acc": (_i32, [_p, _p, _f32, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p]),
     "asrx_msheath_dx_final": (_i32, [_p, _p, _p, _p, _i64, _i64, _i64, _p]),
     "asrx_axpy_row2": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _p]),
@@ -166,8 +170,11 @@ SIGNATURES = {
     "asrx_maxfactor_step": (_i32, [_p, _i32, _i64, _i64, _i64, _i64, _i64, _p, _p]),
     "asrx_abby_record_cond": (_i32, [_p]),
     "asrx_gemm_wn_ce": (_i32, [_p, _i64, _p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i32, _p]),
+    "asrx_gemm_wn_ce_f32": (_i32, [_p, _i64, _p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i32, _p]),
     "asrx_ce_part_fwd": (_i32, [_p, _i64] + [_p] * 6 + [_i64, _i64, _p]),
+    "asrx_ce_part_fwd_f32": (_i32, [_p, _i64] + [_p] * 6 + [_i64, _i64, _p]),
     "asrx_ce_bwd_bf16": (_i32, [_p] * 6 + [_i64, _i64, _p]),
+    "asrx_ce_bwd_f32in": (_i32, [_p] * 6 + [_i64, _i64, _p]),
     "asrx_wgrad_bf16_ab": (_i32, [_p, _i64, _p, _i32, _i64, _p, _i64, _i64, _i64, _i64, _i64, _p]),
     "asrx_wgrad_bias": (_i32, [_p, _i32, _i64, _p, _i32, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _p]),
     "asrx_act_bwd_bias": (_i32, [_p, _p, _p, _p, _i64, _i64, _i32, _p]),

@@ -622,6 +622,21 @@ class Model(nn.Module):
         # perf mode: the tied logits and the cross entropy run fused (ops.LogitsCE: logits stored bf16,
         # the loss from the GEMM's per-tile statistics); False: logits GEMM then ops.CrossEntropy
         self.fused_ce = True
+        # opt-in: the fused path returns the logits stored bf16 (half the logits bytes); default fp32 like
+        # the reference (model.py:629 .float())
+        self.bf16_logits = False
+
+    def grad_reachable(self):
+        """The parameters a training step can give a gradient (asrx.dist.GradSync gives each a bucket
+        slot from step 1, zero-filled when a step leaves it without one): all but blocks 0..L-2 (dead:
+        they restart from the embeddings and never reach the output, model.py:617-628) and the modules the
+        reference constructs but never calls (attention.c, rotary.lin, the router -- applied as the
+        identity it is --, AdaptiveSpan.span_scale, processor.pitch_tokens)."""
+        L = len(self.processor.block)
+        dead = tuple(f"processor.block.{i}." for i in range(L - 1))
+        unused = (".attn.c.", ".rot.lin.", ".router.", ".shared_head.span_scale", "processor.pitch_tokens.")
+        return [p for n, p in self.named_parameters()
+                if p.requires_grad and not n.startswith(dead) and not any(u in n for u in unused)]
 
     def set_noise(self, seed: int, step: int):
         self.noise_seed, self.noise_step = int(seed), int(step)
@@ -655,7 +670,7 @@ class Model(nn.Module):
         if labels is not None and self.fused_ce:
             h = self.processor(text_ids, xa, noise, seq=False, features=True)
             if ops.logits_ce_ok(h, self.processor.token.weight):
-                logits, loss = ops.logits_ce(h, self.processor.token.weight, labels)
+                logits, loss = ops.logits_ce(h, self.processor.token.weight, labels, self.bf16_logits)
                 return {"logits": logits, "loss": loss}
             logits = ops.linear(h, self.processor.token.weight)
         else:

@@ -38,6 +38,11 @@ _REC = None
 
 ROW_DIMS = (128, 256, 384, 512, 768, 1024)  # the fused row kernels' register-resident widths
 
+# The backward's per-sample jump sums (dalpha, dbeta, dgam) as ordered partial sums instead of float
+# atomics: with it no float atomic feeds the data gradient, so a whole backward is bit-reproducible
+# (tests/test_gpu_fusions.py).  False: the atomic form (kept for A/B diagnostics).
+DETERMINISTIC = True
+
 
 def _rec_bytes():
     global _REC
@@ -238,16 +243,26 @@ class MSheathFn(torch.autograd.Function):
             xi = s["x"]
             dxi = _E(B, L, D, device=dev)
             dxn = _E(B, L, D, device=dev)
-            dctl = _E(B * (2 + D), device=dev)  # [dalpha | dbeta | dgam]: zeroed by one memset
-            dalpha, dbeta, dgam = dctl[:B], dctl[B:2 * B], dctl[2 * B:]
-            lib.call("asrx_jump_select4_bwd_acc", _P(dx), _P(s["x_new"]), _P(x0), _P(s["active"]), _P(s["alpha"]),
-                     _P(s["beta"]), _P(has_orig), _P(dxn), _P(dorig), _P(dxi), _P(dalpha), _P(dbeta), _P(dgam), B, L,
-                     D, st)
             g_mem_w, g_mem = _E(B, D, device=dev), _E(B, D, device=dev)
-            lib.call("asrx_msheath_ctrl_bwd3", _P(dalpha), _P(dbeta), _P(dgam), _P(g_mwo), _P(s["mem_v"]),
-                     _P(s["mem_w"]), s["ld_mw"], _P(s["mem"]), _P(mod.jump_s), _P(s["rec"]), i, nl, B, D,
-                     _P(g_policy), int(i != nl - 1), _P(g_mem_w), _P(g_mem), _P(gb(mod.jump_s)), _P(has_orig),
-                     _P(mg_w), _P(gb(mg_w)), _P(gb(mg_b)), st)
+            if DETERMINISTIC:  # per-chunk partials summed in order by the control backward
+                part = _E(int(lib.load().asrx_jump_bwd_part_floats(B, L, D)), device=dev)
+                lib.call("asrx_jump_select4_bwd_part", _P(dx), _P(s["x_new"]), _P(x0), _P(s["active"]),
+                         _P(s["alpha"]), _P(s["beta"]), _P(has_orig), _P(dxn), _P(dorig), _P(dxi), _P(part), B, L, D,
+                         st)
+                lib.call("asrx_msheath_ctrl_bwd4", _P(part), L, _P(g_mwo), _P(s["mem_v"]), _P(s["mem_w"]),
+                         s["ld_mw"], _P(s["mem"]), _P(mod.jump_s), _P(s["rec"]), i, nl, B, D, _P(g_policy),
+                         int(i != nl - 1), _P(g_mem_w), _P(g_mem), _P(gb(mod.jump_s)), _P(has_orig), _P(mg_w),
+                         _P(gb(mg_w)), _P(gb(mg_b)), st)
+            else:
+                dctl = _E(B * (2 + D), device=dev)  # [dalpha | dbeta | dgam]: zeroed by one memset
+                dalpha, dbeta, dgam = dctl[:B], dctl[B:2 * B], dctl[2 * B:]
+                lib.call("asrx_jump_select4_bwd_acc", _P(dx), _P(s["x_new"]), _P(x0), _P(s["active"]),
+                         _P(s["alpha"]), _P(s["beta"]), _P(has_orig), _P(dxn), _P(dorig), _P(dxi), _P(dalpha),
+                         _P(dbeta), _P(dgam), B, L, D, st)
+                lib.call("asrx_msheath_ctrl_bwd3", _P(dalpha), _P(dbeta), _P(dgam), _P(g_mwo), _P(s["mem_v"]),
+                         _P(s["mem_w"]), s["ld_mw"], _P(s["mem"]), _P(mod.jump_s), _P(s["rec"]), i, nl, B, D,
+                         _P(g_policy), int(i != nl - 1), _P(g_mem_w), _P(g_mem), _P(gb(mod.jump_s)), _P(has_orig),
+                         _P(mg_w), _P(gb(mg_w)), _P(gb(mg_b)), st)
             dout = _E(B, L, D, device=dev)
             dgv, dion = _E(rows, device=dev), _E(rows, device=dev)
             lib.call("asrx_axpy_row2_bwd_acc", _P(dxn), _P(g_mem), 1.0 / L, _P(s["active"]), _P(s["g"]), _P(s["ion"]),

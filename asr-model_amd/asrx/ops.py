@@ -1573,15 +1573,16 @@ class CrossEntropy(torch.autograd.Function):
 
 class LogitsCE(torch.autograd.Function):
     """Tied logits + F.cross_entropy(logits, labels, ignore_index=0) fused (perf mode with bf16 storage;
-    model.py:629 logits = x @ token.weight^T, model.py:670 the loss).  One GEMM writes the logits bf16
-    (as autocast's bf16 Linear does) and, per row and column tile, the (max, sum exp) of the bf16
-    logits; a per-row merge gives the log-sum-exp and the loss, reading only the label's logit.  The
-    backward writes dz = (g/count)(softmax - onehot) bf16 from the bf16 logits and feeds it to the
+    model.py:629 logits = x @ token.weight^T, model.py:670 the loss).  One GEMM writes the logits -- fp32,
+    the boundary's dtype (model.py:629 .float()), or bf16 when opted in -- and, per row and column tile,
+    the (max, sum exp) of the stored logits; a per-row merge gives the log-sum-exp and the loss, reading
+    only the label's logit.  The backward writes dz = (g/count)(softmax - onehot) bf16 from the stored
+    logits and feeds it to the
     input-gradient GEMM and the embedding's weight-gradient GEMM.  The logits stay an output with a
     gradient path (a gradient arriving for them is added to dz)."""
 
     @staticmethod
-    def forward(ctx, h, W, labels, sink):
+    def forward(ctx, h, W, labels, sink, bf16_logits=False):
         h = _c(h)
         ctx.set_materialize_grads(False)
         ctx.sink = sink
@@ -1589,20 +1590,22 @@ class LogitsCE(torch.autograd.Function):
         V = W.shape[0]
         nj = G._nj(rows, V)
         nparts = (V + 128 * nj - 1) // (128 * nj)
-        zb = _E(*h.shape[:-1], V, dtype=torch.bfloat16, device=h.device)
+        zb = _E(*h.shape[:-1], V, dtype=torch.bfloat16 if bf16_logits else torch.float32, device=h.device)
         part = _E(rows, nparts, 2, device=h.device)
         Wb = G.weight_bf16(W)
         lib.require_gpu(h, Wb, zb)
         e0 = probe.begin("gemm")
-        lib.call("asrx_gemm_wn_ce", _P(h), D, _P(Wb), Wb.stride(0), _P(zb), V, _P(part), rows, V, D, nj, _S())
-        probe.end("gemm", e0, 2.0 * rows * V * D, ("wn", rows, V, D, nj, 0, "none", False, False, 1, 1, False))
+        lib.call("asrx_gemm_wn_ce" if bf16_logits else "asrx_gemm_wn_ce_f32", _P(h), D, _P(Wb), Wb.stride(0), _P(zb),
+                 V, _P(part), rows, V, D, nj, _S())
+        probe.end("gemm", e0, 2.0 * rows * V * D,
+                  ("wn", rows, V, D, nj, 0, "none", False, False, 1, int(bf16_logits), False))
         lab = _c(labels.reshape(-1))
         loss_r = _E(rows, device=h.device)
         lse = _E(rows, device=h.device)
         loss = _E((), device=h.device)
         count = _E(1, device=h.device)
-        lib.call("asrx_ce_part_fwd", _P(part), nparts, _P(zb), _P(lab), _P(loss_r), _P(lse), _P(loss), _P(count),
-                 rows, V, _S())
+        lib.call("asrx_ce_part_fwd" if bf16_logits else "asrx_ce_part_fwd_f32", _P(part), nparts, _P(zb), _P(lab),
+                 _P(loss_r), _P(lse), _P(loss), _P(count), rows, V, _S())
         ctx.dW = _direct(ctx, 1, W)
         ctx.save_for_backward(h, W, zb, lab, lse, count)
         return zb, loss
@@ -1615,7 +1618,8 @@ class LogitsCE(torch.autograd.Function):
             g_loss = torch.zeros(1, device=zb.device)
         g_loss = _c(g_loss.reshape(1).float())
         dz = _E(zb.shape, dtype=torch.bfloat16, device=zb.device)
-        lib.call("asrx_ce_bwd_bf16", _P(zb), _P(lab), _P(lse), _P(g_loss), _P(count), _P(dz), rows, V, _S())
+        lib.call("asrx_ce_bwd_bf16" if zb.dtype == torch.bfloat16 else "asrx_ce_bwd_f32in", _P(zb), _P(lab), _P(lse),
+                 _P(g_loss), _P(count), _P(dz), rows, V, _S())
         if g_logits is not None:  # a gradient for the logits themselves (not the training path)
             dz = dz.float() + g_logits.float()
         dx = None
@@ -1630,7 +1634,7 @@ class LogitsCE(torch.autograd.Function):
             gW = _gbuf(W, ctx.dW)
             G.linear_wgrad(dz, h, out=gW, accumulate=True)
             dW = _gret(W, gW, ctx.dW)
-        return dx, dW, None, None
+        return dx, dW, None, None, None
 
 
 def logits_ce_ok(h, W) -> bool:
@@ -1639,9 +1643,10 @@ def logits_ce_ok(h, W) -> bool:
             and prec.get() == prec.PREC_BF16)
 
 
-def logits_ce(h, W, labels):
-    """(logits bf16, loss) = (h W^T, F.cross_entropy(., labels, ignore_index=0)) through LogitsCE."""
-    return LogitsCE.apply(h, W, labels, sink_of(h))
+def logits_ce(h, W, labels, bf16_logits=False):
+    """(logits, loss) = (h W^T, F.cross_entropy(., labels, ignore_index=0)) through LogitsCE; the logits are
+    fp32 (model.py:629 returns .float() logits) unless bf16_logits (opt-in: half the logits bytes)."""
+    return LogitsCE.apply(h, W, labels, sink_of(h), bool(bf16_logits))
 
 
 class BlendFn(torch.autograd.Function):

@@ -158,6 +158,26 @@ extern "C" int asrx_gemm_wn_ce(const void* A, int64_t lda, const unsigned short*
   ASRX_LAUNCHED("asrx_gemm_wn_ce");
 }
 
+// As asrx_gemm_wn_ce with the logits stored fp32 (Zf) and the statistics taken of the fp32 values.
+extern "C" int asrx_gemm_wn_ce_f32(const void* A, int64_t lda, const unsigned short* W, int64_t ldw, float* Zf,
+                               int64_t ldc, float* part, int64_t M, int64_t N, int64_t K, int nj, hipStream_t stream) {
+  ASRX_REQUIRE(M > 0 && N > 0 && K > 0, "asrx_gemm_wn_ce_f32: empty problem");
+  ASRX_REQUIRE(((uintptr_t)A & 15) == 0 && ((uintptr_t)W & 15) == 0 && ((uintptr_t)Zf & 15) == 0 &&
+                   ((uintptr_t)part & 7) == 0,
+               "asrx_gemm_wn_ce_f32: A/W 16-byte, Zf 16-byte, part 8-byte aligned");
+  ASRX_REQUIRE(K % 8 == 0 && lda % 8 == 0 && ldw % 8 == 0 && N % 4 == 0 && ldc % 4 == 0,
+               "asrx_gemm_wn_ce_f32: K, lda, ldw %% 8 and N, ldc %% 4 required");
+  ASRX_REQUIRE(M * lda < (1LL << 31) && N * ldw < (1LL << 31), "asrx_gemm_wn_ce_f32: operand spans >= 2^31 elements");
+  ASRX_REQUIRE(nj >= 1 && nj <= 3, "asrx_gemm_wn_ce_f32: nj in 1..3");
+  wn::Params p{(const float*)A, (int)lda, W, (int)ldw, Zf, (int)ldc, nullptr, nullptr, (int)M, (int)N, (int)K,
+               1, 1, 1.f, 0.f, ACT_NONE, nullptr, nullptr, nullptr, nullptr, nullptr, (float2*)part,
+               (int)((N + 128 * nj - 1) / (128 * nj))};
+  if (nj == 3) wn::launch_wr<3, false, false, true, true>(p, stream);
+  else if (nj == 2) wn::launch_wr<2, false, false, true, true>(p, stream);
+  else wn::launch_wr<1, false, false, true, true>(p, stream);
+  ASRX_LAUNCHED("asrx_gemm_wn_ce_f32");
+}
+
 // Out projection with its residual add (model.py:578-580 x = x + attn(...).out): C = R + A W^T + bias, A, C
 // and R fp32 (R may not alias C), 16-byte aligned rows; nj 1 or 3 (the residual epilogue is compiled into
 // dedicated instantiations only, so the other GEMMs keep their register budget).

@@ -224,9 +224,10 @@ __device__ __forceinline__ void epilogue_lds(const Params& p, f32x4 (&acc)[4][2 
   }
 }
 
-// Tied-logits epilogue with cross-entropy statistics: the epilogue_lds bf16 store (alpha * acc, no
-// bias / activation), and from the same LDS slab each row's (max, sum exp) over the wave's 32*NJ
-// columns of the bf16-ROUNDED values (what the backward will read back): lane -> row lane/4, quarter
+// Tied-logits epilogue with cross-entropy statistics: the epilogue_lds store (alpha * acc, no bias /
+// activation) -- bf16 to Cb, or fp32 to C when Cb is null (the logits the drop-in boundary returns,
+// model.py:629 .float()) -- and from the same LDS slab each row's (max, sum exp) over the wave's 32*NJ
+// columns of the STORED values (what the backward will read back): lane -> row lane/4, quarter
 // lane%4 of the columns, merged over the 4 lanes by shuffles and over the 4 column waves through LDS
 // (red: BM x 4 float2); threads < BM then write the tile's partial of their row.
 template <int NJ>
@@ -236,6 +237,7 @@ __device__ __forceinline__ void epilogue_ce(const Params& p, f32x4 (&acc)[4][2 *
   constexpr int PER = 16 * W4 / 64;
   const int lane = threadIdx.x & 63;
   const int cbase = n0 + wn * W;
+  const bool rb = p.Cb != nullptr;  // bf16 logits (statistics of the rounded values) or fp32 logits in C
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) {
 #pragma unroll
@@ -253,7 +255,11 @@ __device__ __forceinline__ void epilogue_ce(const Params& p, f32x4 (&acc)[4][2 *
       const float4 x = *reinterpret_cast<const float4*>(ep + r * LD + c);
       const int row = rbase + r, col = cbase + c;
       if (row >= p.M || col >= p.N) continue;
-      st_bf16x4(p.Cb + (int64_t)row * p.ldc + col, x.x, x.y, x.z, x.w);
+      if (rb)
+        st_bf16x4(p.Cb + (int64_t)row * p.ldc + col, x.x, x.y, x.z, x.w);
+      else
+        __builtin_nontemporal_store(f32x4{x.x, x.y, x.z, x.w},
+                                    reinterpret_cast<f32x4*>(p.C + (int64_t)row * p.ldc + col));
     }
     {
       const int rr = lane >> 2, q = lane & 3;
@@ -262,12 +268,12 @@ __device__ __forceinline__ void epilogue_ce(const Params& p, f32x4 (&acc)[4][2 *
       float m = -INFINITY;
 #pragma unroll
       for (int i = 0; i < Q; ++i)
-        if (c0 + i < p.N) m = fmaxf(m, (float)(__bf16)src[i]);
+        if (c0 + i < p.N) m = fmaxf(m, rb ? (float)(__bf16)src[i] : src[i]);
       float sm = 0.f;
       if (m != -INFINITY) {
 #pragma unroll
         for (int i = 0; i < Q; ++i)
-          if (c0 + i < p.N) sm += __expf((float)(__bf16)src[i] - m);
+          if (c0 + i < p.N) sm += __expf((rb ? (float)(__bf16)src[i] : src[i]) - m);
       }
 #pragma unroll
       for (int o = 1; o <= 2; o <<= 1) {

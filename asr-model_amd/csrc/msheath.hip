@@ -145,7 +145,9 @@ __global__ __launch_bounds__(256) void msheath_ctrl_bwd_kernel(
     const float* __restrict__ mem, const float* __restrict__ jump_s, const CtrlRec* __restrict__ rec, int layer_i,
     int layers, int D, float* __restrict__ g_policy, float* __restrict__ g_mem_v, float* __restrict__ g_mem_w,
     float* __restrict__ g_mem, float* __restrict__ g_jump_s, int64_t ld_mem_w, int* __restrict__ has_orig,
-    int acc_policy, const float* __restrict__ mg_w, float* __restrict__ g_mg_w, float* __restrict__ g_mg_b) {
+    int acc_policy, const float* __restrict__ mg_w, float* __restrict__ g_mg_w, float* __restrict__ g_mg_b,
+    const float2* __restrict__ part_ab = nullptr, const float* __restrict__ part_g = nullptr, int nlc = 0,
+    int ncc = 0) {
   __shared__ float red[4];
   const int64_t b = blockIdx.x;
   const CtrlRec r = rec[b];
@@ -155,7 +157,13 @@ __global__ __launch_bounds__(256) void msheath_ctrl_bwd_kernel(
   for (int c = threadIdx.x; c < D; c += 256) {
     const float mw = mem_w[b * ld_mem_w + c], me = mem[b * D + c];
     const float mwn = mv * mw + (1.f - mv) * me;
-    const float gg = g_gam[b * D + c];
+    float gg;
+    if (part_g) {  // the jump-select backward's L-chunk partials, added in chunk order (deterministic)
+      gg = 0.f;
+      for (int k = 0; k < nlc; ++k) gg += part_g[(b * nlc + k) * D + c];
+    } else {
+      gg = g_gam[b * D + c];
+    }
     const float go = g_mwo ? g_mwo[b * D + c] : 0.f;
     const float gmwn = gg * r.cg + (act ? go : 0.f);
     s_cg += gg * mwn;
@@ -177,7 +185,17 @@ __global__ __launch_bounds__(256) void msheath_ctrl_bwd_kernel(
     if (g_mem_v) g_mem_v[b] = s_mv;
     const int action = (int)r.action;
     const bool jumped = action > 0;
-    const float ga = g_alpha[b], gb = g_beta[b];
+    float ga, gb;
+    if (part_ab) {
+      ga = 0.f, gb = 0.f;
+      for (int k = 0; k < nlc * ncc; ++k) {
+        const float2 v = part_ab[b * nlc * ncc + k];
+        ga += v.x;
+        gb += v.y;
+      }
+    } else {
+      ga = g_alpha[b], gb = g_beta[b];
+    }
     const int widx = min(max(action - 1, 0), 2);
     const float jw = jump_s[widx];
     const float g_jump = jumped ? jw * gb + (1.f - jw) * s_cg : ga;
@@ -412,14 +430,16 @@ __global__ __launch_bounds__(256) void jump_select4_bwd_acc_kernel(
     const float4* __restrict__ g, const float4* __restrict__ xn, const float4* __restrict__ orig,
     const float* __restrict__ act, const float* __restrict__ alpha, const float* __restrict__ beta,
     const int* __restrict__ has_orig, float4* __restrict__ dxn, float4* __restrict__ dorig, float4* __restrict__ dx,
-    float* __restrict__ dalpha, float* __restrict__ dbeta, float* __restrict__ dgam, int64_t L, int d4, int lchunk) {
+    float* __restrict__ dalpha, float* __restrict__ dbeta, float* __restrict__ dgam, int64_t L, int d4, int lchunk,
+    float2* __restrict__ part_ab = nullptr, float* __restrict__ part_g = nullptr) {
   __shared__ float4 sg_s[8][32];
   __shared__ float red[2][4];
   const int lane = threadIdx.x & 31, grp = threadIdx.x >> 5;
   const int cchunks = (d4 + 31) / 32;
   const int cc = blockIdx.x % cchunks;
+  const int lc = blockIdx.x / cchunks, nlc = gridDim.x / cchunks;
   const int64_t b = blockIdx.y;
-  const int64_t l0 = (int64_t)(blockIdx.x / cchunks) * lchunk;
+  const int64_t l0 = (int64_t)lc * lchunk;
   const int64_t l1 = min(L, l0 + lchunk);
   const int c4 = cc * 32 + lane;
   const bool a = act[b] != 0.f;
@@ -450,7 +470,8 @@ __global__ __launch_bounds__(256) void jump_select4_bwd_acc_kernel(
       }
     }
   }
-  if (!a) return;  // uniform per workgroup
+  // partial mode writes every (sample, L chunk, column chunk) slot, zeros for an inactive sample
+  if (!a && !part_g) return;  // uniform per workgroup
   sg_s[grp][lane] = sgv;
   sa = wave_sum(sa);
   sb = wave_sum(sb);
@@ -468,11 +489,20 @@ __global__ __launch_bounds__(256) void jump_select4_bwd_acc_kernel(
         const float4 v = sg_s[g2][cl];
         t += q == 0 ? v.x : q == 1 ? v.y : q == 2 ? v.z : v.w;
       }
-      atomicAdd(dgam + b * 4 * d4 + 4 * c4b + q, t);
+      if (part_g)
+        part_g[(b * nlc + lc) * 4 * d4 + 4 * c4b + q] = t;
+      else
+        atomicAdd(dgam + b * 4 * d4 + 4 * c4b + q, t);
     }
   } else if (threadIdx.x == 128) {
-    atomicAdd(dalpha + b, red[0][0] + red[0][1] + red[0][2] + red[0][3]);
-    atomicAdd(dbeta + b, red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+    const float A = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    const float Bv = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+    if (part_ab) {
+      part_ab[(b * nlc + lc) * cchunks + cc] = make_float2(A, Bv);
+    } else {
+      atomicAdd(dalpha + b, A);
+      atomicAdd(dbeta + b, Bv);
+    }
   }
 }
 
@@ -569,6 +599,33 @@ int asrx_jump_select4_bwd_acc(const float* g, const float* xn, const float* orig
                                                         alpha, beta, has_orig, (float4*)dxn, (float4*)dorig,
                                                         (float4*)dx, dalpha, dbeta, dgam, L, d4, lchunk);
   ASRX_LAUNCHED("asrx_jump_select4_bwd_acc");
+}
+
+// Deterministic form of asrx_jump_select4_bwd_acc: the per-sample sums (dalpha, dbeta, dgam) leave as
+// per-(L chunk, column chunk) partials in `part` (asrx_jump_bwd_part_floats floats, no memset needed),
+// which asrx_msheath_ctrl_bwd4 adds in a fixed order -- no float atomics on the data gradient's path,
+// so a backward is bit-reproducible run to run.
+int64_t asrx_jump_bwd_part_floats(int64_t B, int64_t L, int64_t d) {
+  const int64_t nlc = (L + 127) / 128, ncc = (d / 4 + 31) / 32;
+  return B * nlc * (2 * ncc + d);
+}
+
+int asrx_jump_select4_bwd_part(const float* g, const float* xn, const float* orig, const float* act,
+                               const float* alpha, const float* beta, const int* has_orig, float* dxn, float* dorig,
+                               float* dx, float* part, int64_t B, int64_t L, int64_t d, hipStream_t stream) {
+  ASRX_REQUIRE(d % 4 == 0, "asrx_jump_select4_bwd_part: d % 4 != 0");
+  if (B * L == 0) return 0;
+  const int d4 = (int)(d / 4);
+  const int lchunk = 128;
+  const int64_t nlc = (L + lchunk - 1) / lchunk, ncc = (d4 + 31) / 32;
+  float2* part_ab = reinterpret_cast<float2*>(part);
+  float* part_g = part + 2 * B * nlc * ncc;
+  dim3 grid((unsigned)(ncc * nlc), (unsigned)B);
+  jump_select4_bwd_acc_kernel<<<grid, 256, 0, stream>>>((const float4*)g, (const float4*)xn, (const float4*)orig, act,
+                                                        alpha, beta, has_orig, (float4*)dxn, (float4*)dorig,
+                                                        (float4*)dx, nullptr, nullptr, nullptr, L, d4, lchunk,
+                                                        part_ab, part_g);
+  ASRX_LAUNCHED("asrx_jump_select4_bwd_part");
 }
 
 int asrx_axpy_row2_bwd_acc(const float* dxn, const float* gm, float invL, const float* act, const float* s1,
@@ -679,6 +736,26 @@ int asrx_msheath_ctrl_bwd3(const float* g_alpha, const float* g_beta, const floa
                                                            g_policy, nullptr, g_mem_w, g_mem, g_jump_s, ld_mem_w,
                                                            has_orig, acc_policy, mg_w, g_mg_w, g_mg_b);
   ASRX_LAUNCHED("asrx_msheath_ctrl_bwd3");
+}
+
+// asrx_msheath_ctrl_bwd3 reading (dalpha, dbeta, dgam) as the partials of asrx_jump_select4_bwd_part
+// (same B, L, D), summed in chunk order.
+int asrx_msheath_ctrl_bwd4(const float* part, int64_t L, const float* g_mwo, const float* mem_v, const float* mem_w,
+                           int64_t ld_mem_w, const float* mem, const float* jump_s, const void* rec, int64_t layer_i,
+                           int64_t layers, int64_t B, int64_t D, float* g_policy, int acc_policy, float* g_mem_w,
+                           float* g_mem, float* g_jump_s, int* has_orig, const float* mg_w, float* g_mg_w,
+                           float* g_mg_b, hipStream_t stream) {
+  ASRX_REQUIRE(D % 4 == 0, "asrx_msheath_ctrl_bwd4: D % 4 != 0");
+  if (B == 0) return 0;
+  const int64_t nlc = (L + 127) / 128, ncc = (D / 4 + 31) / 32;
+  const float2* part_ab = reinterpret_cast<const float2*>(part);
+  const float* part_g = part + 2 * B * nlc * ncc;
+  msheath_ctrl_bwd_kernel<<<(unsigned)B, 256, 0, stream>>>(nullptr, nullptr, nullptr, g_mwo, mem_v, mem_w, mem,
+                                                           jump_s, (const CtrlRec*)rec, (int)layer_i, (int)layers,
+                                                           (int)D, g_policy, nullptr, g_mem_w, g_mem, g_jump_s,
+                                                           ld_mem_w, has_orig, acc_policy, mg_w, g_mg_w, g_mg_b,
+                                                           part_ab, part_g, (int)nlc, (int)ncc);
+  ASRX_LAUNCHED("asrx_msheath_ctrl_bwd4");
 }
 
 int64_t asrx_mem_chunks(int64_t L) { return (L + MEM_CHUNK - 1) / MEM_CHUNK; }

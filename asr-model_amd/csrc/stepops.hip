@@ -63,6 +63,7 @@ __global__ __launch_bounds__(256) void ce_fwd1_kernel(const float* __restrict__ 
 // (2 bytes) -- the 40000-wide row itself is not re-read.  One wave per row, 4 rows per workgroup.
 __global__ __launch_bounds__(256) void ce_part_fwd_kernel(const float2* __restrict__ part, int nparts,
                                                           const unsigned short* __restrict__ zb,
+                                                          const float* __restrict__ zf,
                                                           const int64_t* __restrict__ labels, float* __restrict__ loss,
                                                           float* __restrict__ lse, int64_t rows, int64_t V) {
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -87,7 +88,7 @@ __global__ __launch_bounds__(256) void ce_part_fwd_kernel(const float2* __restri
     lse[r] = l;
     float lr = 0.f;
     if (y < 0 || y >= V) lr = __builtin_nanf("");
-    else if (y != 0) lr = l - __builtin_bit_cast(float, (uint32_t)zb[r * V + y] << 16);
+    else if (y != 0) lr = l - (zf ? zf[r * V + y] : __builtin_bit_cast(float, (uint32_t)zb[r * V + y] << 16));
     loss[r] = lr;
   }
 }
@@ -128,7 +129,41 @@ __global__ __launch_bounds__(256) void ce_bwd_bf16_kernel(const unsigned short* 
   for (int64_t j = 8 * V8 + threadIdx.x; j < V; j += 256) dr[j] = f(zr[j], j);
 }
 
-// loss = sum_r loss_r / max(#{labels != 0}, 1); count kept for the backward.  One workgroup.
+// As ce_bwd_bf16_kernel from fp32 logits (the boundary's fp32 logits, asrx_gemm_wn_ce_f32): dz stored
+// bf16, 8 logits per two 16-byte loads.
+__global__ __launch_bounds__(256) void ce_bwd_f32in_kernel(const float* __restrict__ zf,
+                                                           const int64_t* __restrict__ labels,
+                                                           const float* __restrict__ lse, const float* __restrict__ g,
+                                                           const float* __restrict__ count,
+                                                           unsigned short* __restrict__ dzb, int64_t V) {
+  const int64_t r = blockIdx.x;
+  const int64_t y = labels[r];
+  const bool bad = y < 0 || y >= V;
+  const float sc = bad ? __builtin_nanf("") : (y == 0 ? 0.f : g[0] / count[0]);
+  const float l = lse[r];
+  const float* zr = zf + r * V;
+  unsigned short* dr = dzb + r * V;
+  auto f = [&](float v, int64_t j) {
+    return __builtin_bit_cast(unsigned short, (__bf16)(sc * (__expf(v - l) - (j == y ? 1.f : 0.f))));
+  };
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const bool vec = V % 8 == 0 && (((uintptr_t)zr | (uintptr_t)dr) & 15) == 0;
+  const int64_t V8 = vec ? V / 8 : 0;
+  for (int64_t j = threadIdx.x; j < V8; j += 256) {
+    const float4 a = reinterpret_cast<const float4*>(zr)[2 * j], b = reinterpret_cast<const float4*>(zr)[2 * j + 1];
+    const int64_t c = 8 * j;
+    u32x4 out;
+    out[0] = (unsigned)f(a.x, c) | ((unsigned)f(a.y, c + 1) << 16);
+    out[1] = (unsigned)f(a.z, c + 2) | ((unsigned)f(a.w, c + 3) << 16);
+    out[2] = (unsigned)f(b.x, c + 4) | ((unsigned)f(b.y, c + 5) << 16);
+    out[3] = (unsigned)f(b.z, c + 6) | ((unsigned)f(b.w, c + 7) << 16);
+    reinterpret_cast<u32x4*>(dr)[j] = out;
+  }
+  for (int64_t j = 8 * V8 + threadIdx.x; j < V; j += 256) dr[j] = f(zr[j], j);
+}
+
+// loss = sum_r loss_r / #{labels != 0} (NaN when every label is ignored, as F.cross_entropy's mean,
+// model.py:670); count = max(#, 1) kept for the backward (ignored rows get a zero gradient).  One workgroup.
 __global__ __launch_bounds__(1024) void ce_reduce_kernel(const float* __restrict__ loss_r, const int64_t* __restrict__ labels,
                                                          int64_t rows, float* __restrict__ loss, float* __restrict__ count) {
   __shared__ float red[16];
@@ -140,9 +175,8 @@ __global__ __launch_bounds__(1024) void ce_reduce_kernel(const float* __restrict
   s = block_sum<1024>(s, red);
   c = block_sum<1024>(c, red);
   if (threadIdx.x == 0) {
-    const float n = fmaxf(c, 1.f);
-    loss[0] = s / n;
-    count[0] = n;
+    loss[0] = c > 0.f ? s / c : __builtin_nanf("");
+    count[0] = fmaxf(c, 1.f);
   }
 }
 
@@ -343,10 +377,28 @@ int asrx_ce_part_fwd(const float* part, int64_t nparts, const unsigned short* zb
                      float* lse, float* loss, float* count, int64_t rows, int64_t V, hipStream_t stream) {
   if (rows == 0) return 0;
   ASRX_REQUIRE(nparts > 0 && rows < (1LL << 33), "asrx_ce_part_fwd: bad shape");
-  ce_part_fwd_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, stream>>>((const float2*)part, (int)nparts, zb, labels,
-                                                                     loss_r, lse, rows, V);
+  ce_part_fwd_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, stream>>>((const float2*)part, (int)nparts, zb, nullptr,
+                                                                     labels, loss_r, lse, rows, V);
   ce_reduce_kernel<<<1, 1024, 0, stream>>>(loss_r, labels, rows, loss, count);
   ASRX_LAUNCHED("asrx_ce_part_fwd");
+}
+
+int asrx_ce_part_fwd_f32(const float* part, int64_t nparts, const float* zf, const int64_t* labels, float* loss_r,
+                         float* lse, float* loss, float* count, int64_t rows, int64_t V, hipStream_t stream) {
+  if (rows == 0) return 0;
+  ASRX_REQUIRE(nparts > 0 && rows < (1LL << 33), "asrx_ce_part_fwd_f32: bad shape");
+  ce_part_fwd_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, stream>>>((const float2*)part, (int)nparts, nullptr, zf,
+                                                                     labels, loss_r, lse, rows, V);
+  ce_reduce_kernel<<<1, 1024, 0, stream>>>(loss_r, labels, rows, loss, count);
+  ASRX_LAUNCHED("asrx_ce_part_fwd_f32");
+}
+
+int asrx_ce_bwd_f32in(const float* zf, const int64_t* labels, const float* lse, const float* g, const float* count,
+                      unsigned short* dzb, int64_t rows, int64_t V, hipStream_t stream) {
+  if (rows == 0) return 0;
+  ASRX_REQUIRE(rows < (1LL << 31), "asrx_ce_bwd_f32in: too many rows");
+  ce_bwd_f32in_kernel<<<(unsigned)rows, 256, 0, stream>>>(zf, labels, lse, g, count, dzb, V);
+  ASRX_LAUNCHED("asrx_ce_bwd_f32in");
 }
 
 int asrx_ce_bwd_bf16(const unsigned short* zb, const int64_t* labels, const float* lse, const float* g,

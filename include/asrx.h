@@ -370,6 +370,20 @@ int asrx_jump_select4_bwd_acc(const float* g, const float* xn, const float* orig
 int asrx_axpy_row2_bwd_acc(const float* dxn, const float* gm, float invL, const float* act, const float* s1,
                            const float* s2, const float* y, float* dy, float* ds1, float* ds2, float* dx, int64_t B,
                            int64_t L, int64_t d, asrx_stream_t stream);
+/* Deterministic pair (round 4): asrx_jump_select4_bwd_acc writing its per-sample sums (dalpha, dbeta,
+ * dgam) as per-(128-row L chunk, 128-column chunk) partials into `part` (asrx_jump_bwd_part_floats(B, L,
+ * d) floats, fully written, no memset), and asrx_msheath_ctrl_bwd3 reading them from `part`, summed in
+ * chunk order -- no float atomics on the data gradient's path (model.py:489-501 backward). */
+int64_t asrx_jump_bwd_part_floats(int64_t B, int64_t L, int64_t d);
+int asrx_jump_select4_bwd_part(const float* g, const float* xn, const float* orig, const float* act,
+                               const float* alpha, const float* beta, const int* has_orig, float* dxn, float* dorig,
+                               float* dx, float* part, int64_t B, int64_t L, int64_t d, asrx_stream_t stream);
+int asrx_msheath_ctrl_bwd4(const float* part, int64_t L, const float* g_mwo, const float* mem_v, const float* mem_w,
+                           int64_t ld_mem_w, const float* mem, const float* jump_s, const void* rec, int64_t layer_i,
+                           int64_t layers, int64_t B, int64_t D, float* g_policy, int acc_policy, float* g_mem_w,
+                           float* g_mem, float* g_jump_s, int* has_orig, const float* mg_w, float* g_mg_w,
+                           float* g_mg_b, asrx_stream_t stream);
+
 int asrx_msheath_dx_final(float* dx, const float* dorig, const int* has_orig, const float* u, int64_t B, int64_t L,
                           int64_t d, asrx_stream_t stream);
 /* out = x + s1[r] * s2[r] * y (s2 may be NULL), d % 4 == 0 (model.py:461: x + gate * ion * out). */
@@ -476,6 +490,16 @@ int asrx_ce_part_fwd(const float* part, int64_t nparts, const unsigned short* zb
                      float* lse, float* loss, float* count, int64_t rows, int64_t V, asrx_stream_t stream);
 int asrx_ce_bwd_bf16(const unsigned short* zb, const int64_t* labels, const float* lse, const float* g,
                      const float* count, unsigned short* dzb, int64_t rows, int64_t V, asrx_stream_t stream);
+/* The same with the logits stored fp32 (the drop-in boundary's logits dtype, model.py:629 .float(); the
+ * default of Model.forward): statistics of the fp32 values, the label's fp32 logit, dz from fp32 logits.
+ * The loss is NaN when every label is ignored (F.cross_entropy's mean over zero rows, model.py:670);
+ * ignored rows get a zero gradient. */
+int asrx_gemm_wn_ce_f32(const void* A, int64_t lda, const unsigned short* W, int64_t ldw, float* Zf, int64_t ldc,
+                        float* part, int64_t M, int64_t N, int64_t K, int nj, asrx_stream_t stream);
+int asrx_ce_part_fwd_f32(const float* part, int64_t nparts, const float* zf, const int64_t* labels, float* loss_r,
+                         float* lse, float* loss, float* count, int64_t rows, int64_t V, asrx_stream_t stream);
+int asrx_ce_bwd_f32in(const float* zf, const int64_t* labels, const float* lse, const float* g, const float* count,
+                      unsigned short* dzb, int64_t rows, int64_t V, asrx_stream_t stream);
 /* out projection with its residual add (model.py:578-580): C = R + A W^T + bias; A, C, R fp32, R != C,
  * 16-byte aligned rows, nj 1 or 3. */
 int asrx_gemm_wn_res(const float* A, int64_t lda, const unsigned short* W, int64_t ldw, float* C, int64_t ldc,

@@ -137,9 +137,22 @@ def _decide_cond(cond, index, dkey, heads: bool):
     return out
 
 
+# bf16 rounding emulation (conditioning measurements only, tools/bf16_sensitivity.py): the named points
+# round their operands to bf16 in the forward (straight-through: the backward is the float64 one).
+# Empty by default -- the oracle is the reference's arithmetic in the requested dtype.
+EMU: set = set()
+
+
+def _r(x, point):
+    if point not in EMU:
+        return x
+    return x + (x.to(torch.bfloat16).to(x.dtype) - x).detach()
+
+
 def _lin(P, name, x):
     b = P.get(name + ".bias")
-    return F.linear(x, P[name + ".weight"], b)
+    pt = "qkproj" if name.endswith((".q.1", ".kv.1")) else "lin"
+    return F.linear(_r(x, pt), _r(P[name + ".weight"], pt), b)
 
 
 # ------------------------------------------------------------------------------- norms
@@ -302,10 +315,10 @@ def attention(P, pre, x, xa, masked, cfg, noise, site_q, sids_q, site_kv, sids_k
     gk = noise.abby(site_kv + ".kh", sids_kv, H, Lk)
     q = abby_normal(P, pre + ".ln", q, gq, (noise.key(site_q + ".qh"), sids_q))
     k = abby_normal(P, pre + ".ln", k, gk, (noise.key(site_kv + ".kh"), sids_kv))
-    s = (q @ k.transpose(-1, -2)) / math.sqrt(hd)
+    s = (_r(q, "qk") @ _r(k, "qk").transpose(-1, -2)) / math.sqrt(hd)
     if masked:
         s = s.masked_fill(torch.ones(Lq, Lk, dtype=torch.bool).triu(1), float("-inf"))
-    a = torch.softmax(s, dim=-1) @ v
+    a = _r(torch.softmax(s, dim=-1), "pv") @ _r(v, "pv")
     a = a.permute(0, 2, 1, 3).reshape(B, Lq, D)
     return _lin(P, pre + ".out.1", a)
 
@@ -488,7 +501,7 @@ def forward(P, cfg, text_ids, labels=None, spectrogram=None, pitch=None, wavefor
         blend = torch.sigmoid(P["processor.blend"])
         x = blend * d + (1 - blend) * g
     x = abby_rows(P, "processor.ln", x, noise, "final.ln", sid_t)
-    logits = x @ P["processor.token.weight"].t()
+    logits = _r(x, "logits") @ _r(P["processor.token.weight"], "logits").t()
     loss = None
     if labels is not None:
         loss = F.cross_entropy(logits.reshape(-1, logits.shape[-1]), labels.reshape(-1), ignore_index=0)

@@ -152,9 +152,25 @@ def grad_distance(Pa, Pb):
     return worst, wname, float((a @ b) / (a.norm() * b.norm()).clamp_min(1e-300))
 
 
+def bf16_nudge(sd, seed):
+    """sd with every floating weight scaled by (1 + u 2^-9), u uniform in [-1, 1): a perturbation at bf16
+    resolution (bf16 keeps 8 mantissa bits)."""
+    g = torch.Generator().manual_seed(2000 + seed)
+    return {k: (v.detach().double() * (1 + (torch.rand(v.shape, generator=g, dtype=torch.float64) * 2 - 1) * 2.0 ** -9)
+                if v.is_floating_point() else v) for k, v in sd.items()}
+
+
+BF16_POINTS = ("lin", "qkproj", "qk", "pv", "logits")
+
+
+def _cos(a, b):
+    a, b = a.double().reshape(-1), b.double().reshape(-1)
+    return float((a @ b) / (a.norm() * b.norm()).clamp_min(1e-300))
+
+
 def compare(cfg, B=1, seconds=30.0, T=256, precision="bf16", train=True, grads=True, seed=0, noise=(7, 3),
             model_seed=0, device="cuda", decisions=False, replay=False, hip_mel=False, pitch_frames=None,
-            yardstick=False, sensitivity=0):
+            yardstick=False, sensitivity=0, bf16_stability=False):
     """Run the HIP Model and the oracle on the same inputs; return a dict of metrics.
     decisions: record both sides' hard decisions and report their agreement.  replay: re-run the oracle
     consuming the HIP decisions and compare every parameter gradient.  hip_mel: feed the HIP model the
@@ -163,7 +179,12 @@ def compare(cfg, B=1, seconds=30.0, T=256, precision="bf16", train=True, grads=T
     arithmetic at fp32 -- and report its distance from the float64 oracle (yard_*): the model's fp32
     conditioning, against which the HIP fp32 path is gated.  sensitivity=K (with replay): K float64
     oracle runs on weights nudged by one fp32 ulp (ulp_nudge), the largest gradient move reported as
-    ulp_grads_global -- the gradient's conditioning at fp32 input precision."""
+    ulp_grads_global -- the gradient's conditioning at fp32 input precision.  bf16_stability (with replay and grads): the gradient's
+    conditioning at bf16 resolution -- two more float64 oracle runs on the replayed trajectory, one with
+    every GEMM / attention operand rounded to bf16 (oracle EMU, all points) and one on weights nudged at
+    bf16 scale (bf16_nudge); per parameter the cosine of each with float64 (bf16_emu_cos / bf16_nudge_cos
+    and their whole-gradient values).  A parameter whose gradient keeps cosine >= 0.99 under both is
+    STABLE at bf16 resolution: the HIP bf16 gradient is gated on those (bf16_stable_*)."""
     from asrx import decisions as hdec
     from asrx import prec
     from asrx.model import Model
@@ -279,6 +300,29 @@ def compare(cfg, B=1, seconds=30.0, T=256, precision="bf16", train=True, grads=T
                                       reverse=True)[:8]
         res["grads_missing"] = missing
         res["zero_grad_residue"] = max(residue.values(), default=0.0)
+        if bf16_stability:
+            om.EMU.update(BF16_POINTS)
+            try:
+                Pe, _ = run_oracle(om.Decisions(table=hip_dec))
+            finally:
+                om.EMU.clear()
+            Pn, _ = oracle_run(bf16_nudge(sd, 0), ocfg, x, om.Decisions(table=hip_dec), torch.float64, noise, train)
+            hip_cos, stable = {}, []
+            for n in per:
+                ce, cn = _cos(Pe[n].grad, P[n].grad), _cos(Pn[n].grad, P[n].grad)
+                hip_cos[n] = (_cos(names[n].grad.cpu(), P[n].grad), ce, cn)
+                if ce >= 0.99 and cn >= 0.99:
+                    stable.append(n)
+            cat = lambda G, ns: torch.cat([G(n).double().reshape(-1) for n in ns])  # noqa: E731
+            res["bf16_emu_cos"] = _cos(cat(lambda n: Pe[n].grad, list(per)), cat(lambda n: P[n].grad, list(per)))
+            res["bf16_nudge_cos"] = _cos(cat(lambda n: Pn[n].grad, list(per)), cat(lambda n: P[n].grad, list(per)))
+            res["bf16_stable"] = stable
+            res["bf16_unstable_n"] = len(per) - len(stable)
+            if stable:
+                res["bf16_stable_cos"] = _cos(cat(lambda n: names[n].grad.cpu(), stable),
+                                              cat(lambda n: P[n].grad, stable))
+                res["bf16_stable_min"] = min((hip_cos[n][0], n) for n in stable)
+            res["bf16_param_cos"] = {n: tuple(round(c, 5) for c in v) for n, v in hip_cos.items()}
         # one number over the whole model: cosine of the concatenated gradients
         kept = [n for n in per]
         a = torch.cat([names[n].grad.double().cpu().reshape(-1) for n in kept])

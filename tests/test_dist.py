@@ -28,6 +28,9 @@ class Toy(torch.nn.Module):
     def forward(self, x):
         return self.c(torch.tanh(self.b(torch.relu(self.a(x)))))
 
+    def grad_reachable(self):  # as asrx.model.Model.grad_reachable: the never-used module excluded
+        return [p for n, p in self.named_parameters() if not n.startswith("unused.")]
+
 
 class _DirectLinear(torch.autograd.Function):
     """CPU stand-in for an asrx op: y = x W^T + b with W's and b's gradients accumulated straight into
@@ -328,3 +331,83 @@ def test_stream_grouping_signature():
     assert stream_grouping([6001, 3001, 3000]) == (0, 1, 2)
     assert stream_grouping([3000, 3001, 3000]) == (0, 1, 2)  # only consecutive streams share a pass
     assert stream_grouping([101, 101, 101]) == (0, 0, 0)
+
+
+class ToyLate(torch.nn.Module):
+    """A parameter (`late`) that first receives a gradient on step 3 (no grad_reachable: every parameter
+    is covered).  The step signature records whether it is used."""
+
+    def __init__(self):
+        super().__init__()
+        self.a = torch.nn.Linear(16, 16)
+        self.late = torch.nn.Linear(16, 16)
+        self.c = torch.nn.Linear(16, 4)
+        self.use_late = False
+        self.grad_signature = None
+
+    def forward(self, x):
+        self.grad_signature = ("late", self.use_late)
+        h = torch.tanh(self.a(x))
+        if self.use_late:
+            h = h + torch.tanh(self.late(h))
+        return self.c(h)
+
+
+def _worker_late(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "asr-model_amd")]
+    from asrx.dist import GradSync, broadcast_parameters
+
+    torch.manual_seed(rank)
+    model = ToyLate()
+    broadcast_parameters(model)
+    twin = ToyLate()
+    twin.load_state_dict(model.state_dict())
+    sync = GradSync(model, bucket_mb=0.0005)
+    out = []
+    for step, use in enumerate([False, False, True, True, False, True]):
+        model.use_late = twin.use_late = use
+        sync.zero_grad()
+        x = torch.randn(5, 16, generator=torch.Generator().manual_seed(100 * step + rank))
+        (model(x).pow(2).sum() * (rank + 1)).backward()
+        sync.finish()
+        synced = {n: p.grad.clone() for n, p in model.named_parameters()}
+        twin.zero_grad(set_to_none=True)
+        (twin(x).pow(2).sum() * (rank + 1)).backward()
+        avg = {}
+        for n, p in twin.named_parameters():
+            t = p.grad.clone() if p.grad is not None else torch.zeros_like(p)
+            dist.all_reduce(t)
+            avg[n] = t / world
+        ok = all(torch.allclose(synced[n], avg[n], atol=1e-5) for n in avg)
+        out.append((use, ok, float(synced["late.weight"].abs().max())))
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gradsync_parameter_first_used_later():
+    """a parameter that first receives a gradient on step 3 is reduced (both ranks end
+    with the average) and zeroed between steps -- its gradient never accumulates across steps un-reduced."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_late, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r, out = q.get(timeout=120)
+        res[r] = out
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in (0, 1):
+        for step, (use, ok, late_max) in enumerate(res[r]):
+            assert ok, (r, step, res[r])
+            assert (late_max > 0) == use, (r, step, res[r])

@@ -157,23 +157,14 @@ def test_wgrad_bias_matches_colsum(cuda, a_bf16, b_bf16, R, M, N, splitk):
     assert float((db.double() - db_ref).abs().max() / db_ref.abs().max()) < 1e-5
 
 
-def test_model_bias_grads_fused_match_colsum(cuda):
-    """A whole bf16 training step (tiny dims, 2 layers): every bias gradient with the sums inside the
-    weight-gradient kernel == with the separate column-sum pass, as close as the unfused step is to a
-    rerun of itself (the step's other gradient sums use fp32 atomics, whose order varies run to run)."""
+def _tiny_step(cuda, model, x, n_runs_cfg):
+    """Run the bf16 training step once per entry of n_runs_cfg (FUSED_BIAS_GRAD value) with the same noise;
+    returns the parameter gradients of each run."""
     from asrx import gemm as G
     from asrx import prec
-    from asrx.config import Dimensions
-    from asrx.model import Model
 
-    import model_parity as mp
-
-    cfg = Dimensions(tokens=1000, mels=128, dims=384, head=6, layer=2, act="gelu", n_type="AbbyNormal")
-    torch.manual_seed(0)
-    model = Model(cfg).to(cuda).train()
-    x = mp.inputs(1, 3.0, 32, cfg.tokens, 0)
     res = []
-    for fused in (True, False, False):
+    for fused in n_runs_cfg:
         G.FUSED_BIAS_GRAD = fused
         try:
             model.zero_grad(set_to_none=True)
@@ -187,13 +178,62 @@ def test_model_bias_grads_fused_match_colsum(cuda):
         finally:
             G.FUSED_BIAS_GRAD = True
         res.append({n: p.grad.detach().clone() for n, p in model.named_parameters() if p.grad is not None})
-    assert set(res[0]) == set(res[1]) == set(res[2])
-    nb = 0
-    for n in res[1]:
-        if not n.endswith("bias"):
-            continue
-        nb += 1
-        d = float((res[0][n] - res[1][n]).abs().max())
-        rerun = float((res[2][n] - res[1][n]).abs().max())
-        assert d <= 2e-3 * float(res[1][n].abs().max()) + 4 * rerun, (n, d, rerun)
-    assert nb > 10
+    return res
+
+
+def _tiny_model(cuda):
+    from asrx.config import Dimensions
+    from asrx.model import Model
+
+    import model_parity as mp
+
+    cfg = Dimensions(tokens=1000, mels=128, dims=384, head=6, layer=2, act="gelu", n_type="AbbyNormal")
+    torch.manual_seed(0)
+    model = Model(cfg).to(cuda).train()
+    return model, mp.inputs(1, 3.0, 32, cfg.tokens, 0)
+
+
+def _grad_gap(a, b):
+    """max |a - b| / max |b| per parameter."""
+    return {n: float((a[n] - b[n]).abs().max() / b[n].abs().max().clamp_min(1e-30)) for n in b}
+
+
+def test_backward_is_reproducible(cuda):
+    """A whole bf16 training step run twice gives the same gradients up to the order of the parameter
+    gradients' own fp32 atomic sums: no float atomic feeds the data gradient (the MSheath jump backward's
+    per-sample sums are ordered partials, msheath.DETERMINISTIC), so nothing is amplified through the
+    backward's cancellations.  (With the atomic form, one rerun moved enc.conv1.0.bias by 2e-4 of its
+    max and another fused/unfused pair by 3.6e-3.)"""
+    model, x = _tiny_model(cuda)
+    r0, r1 = _tiny_step(cuda, model, x, (True, True))
+    assert set(r0) == set(r1)
+    gap = _grad_gap(r1, r0)
+    worst = sorted(gap.items(), key=lambda t: -t[1])[:5]
+    print("rerun gap (worst 5):", worst)
+    assert worst[0][1] < 1e-4, worst
+
+
+def test_model_bias_grads_fused_match_colsum(cuda):
+    """Fused bias gradients (summed inside the weight-gradient kernel) against the column sums of the SAME
+    dY, inside one backward (gemm.BIAS_CHECK): within 1e-5 of the bias's max.  Then the whole step with the
+    fused and with the separate column-sum pass: every parameter gradient within 1e-4 of its own max (the
+    data gradient is bit-reproducible, test_backward_is_reproducible; what is left is fp32 atomic order)."""
+    from asrx import gemm as G
+
+    model, x = _tiny_model(cuda)
+    G.BIAS_CHECK = []
+    try:
+        _tiny_step(cuda, model, x, (True,))
+        checks = G.BIAS_CHECK
+    finally:
+        G.BIAS_CHECK = None
+    assert len(checks) > 10, len(checks)
+    for k, (fused, ref) in enumerate(checks):
+        err = float((fused - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
+        assert err < 1e-5, (k, err, fused.shape)
+    res = _tiny_step(cuda, model, x, (True, False))
+    assert set(res[0]) == set(res[1])
+    gap = _grad_gap(res[0], res[1])
+    worst = sorted(gap.items(), key=lambda t: -t[1])[:5]
+    print("fused vs unfused gap (worst 5):", worst)
+    assert worst[0][1] < 1e-4, worst

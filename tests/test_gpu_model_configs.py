@@ -107,6 +107,31 @@ def test_model_parity_bf16_configs(cuda, name):
     assert r["loss"] < loss
 
 
+# bf16 gradients (VERDICT r03 missing 1 -- "make the bf16 gradient trustworthy, or show that it cannot be"):
+# the gradient of this model is not defined at bf16 resolution.  The float64 oracle itself, on the same
+# replayed trajectory, moves to whole-gradient cosine 0.34 with float64 when its weights are nudged by
+# 2^-9 (bf16 resolution), and to 0.35 when its GEMM / attention operands are rounded to bf16 (0.25 with
+# only the attention's q / k rounded, 0.57 with only the Linears other than q / kv, 0.72 with only P / v:
+# every rounding point feeds the near-tie attention scores of ~1e3-1e4); 129 of 150 parameters fall
+# below cosine 0.95 under that emulation (tools/bf16_sensitivity.py, profiles/r04_bf16_sensitivity.txt).
+# No bf16 implementation can therefore match the float64 gradient as a whole, and the fp32 parity mode
+# is the one for gradient fidelity.  What IS gated: the parameters whose float64 gradient keeps cosine >=
+# 0.99 under both bf16 perturbations (measured in the test itself, mp.compare(bf16_stability=True)) --
+# there the HIP bf16 gradient must reach cosine >= 0.95 per parameter and >= 0.99 over the set.
+BF16_STABLE_PARAM_COS = 0.95
+BF16_STABLE_SET_COS = 0.99
+
+
+@pytest.mark.parametrize("name", ["tiny_full", "refmain"])
+def test_bf16_gradient_on_bf16_stable_parameters(cuda, name):
+    r = _case(name, "bf16", True, replay=True, bf16_stability=True)
+    print(name, "emulated bf16 cos", r["bf16_emu_cos"], "bf16-nudged cos", r["bf16_nudge_cos"], "HIP cos",
+          r["grads_cos"], "stable", len(r["bf16_stable"]), "unstable", r["bf16_unstable_n"])
+    assert len(r["bf16_stable"]) >= 5, r["bf16_stable"]
+    assert r["bf16_stable_min"][0] >= BF16_STABLE_PARAM_COS, r["bf16_stable_min"]
+    assert r["bf16_stable_cos"] >= BF16_STABLE_SET_COS, r["bf16_stable_cos"]
+
+
 # Decision-aware parity (SURVEY §8(d) "gumbel decision agreement is reported"): both sides record every
 # hard decision (AbbyNormal mode per row and mode 2's max-vs-avg choice per feature, v_gate threshold per
 # position, MSheath action per sample and layer); the agreement rates are printed and gated (a flip
@@ -114,12 +139,10 @@ def test_model_parity_bf16_configs(cuda, name):
 # is compared: in fp32 through test_model_parity_fp32_configs' gates, in bf16 by the cosine of the whole
 # gradient (bf16 rounding of ~100 dependent ops times the fp32 conditioning above leaves single
 # parameters' gradients without a usable elementwise bound).  Measured: profiles/r03_parity_decisions.jsonl.
-# measured 0.21 (tiny_full) and 0.49 (refmain), then 0.03 (tiny_full) after two summation-order-only
-# changes (bias gradients summed inside the weight-gradient kernel, MSheath row reductions on DPP; the
-# fp32 gates above are unchanged): bf16 operand rounding (2^-8) meets the same near-singular attention
-# terms, so the whole bf16 gradient's direction is set by a few chaotic terms and is only gated to
-# point the same way as the float64 one
-BF16_GRAD_COS = 0.0
+# The whole bf16 gradient's cosine is not gated here: the float64 gradient itself only keeps cosine ~0.3
+# under bf16-resolution perturbations (see test_bf16_gradient_on_bf16_stable_parameters, which gates the
+# bf16-stable parameters); it is printed.
+BF16_GRAD_COS = -1.0
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
@@ -151,3 +174,8 @@ def test_hip_mel_end_to_end(cuda):
     assert r["logits_max"] < 3 * max(1e-3, YARD_FACTOR * r["yard_logits"]), (r["logits_max"], r["yard_logits"])
     assert r["argmax"] == 1.0
     assert r["loss"] < 1e-4
+    # gradients: the fp32 configs' gates, 3x for the same input perturbation
+    assert not r["grads_missing"], r["grads_missing"]
+    assert r["grads_all_global"] < 3 * max(1e-3, YARD_FACTOR * r["yard_grads_global"]), (
+        r["grads_all_global"], r["grads_all_global_worst"], r["yard_grads_global"])
+    assert r["grads_cos"] > 0.999, r["grads_cos"]
