@@ -294,7 +294,8 @@ def _wgrad(A, lda, x2, out, M, K, rows, db=None):
                 ref = torch.zeros(M, device=A.device)
                 lib.call("asrx_colsum_ld", lib.ptr(Af), Af.stride(0) if a_bf16 else lda, lib.ptr(ref), rows, M,
                          lib.stream())
-                BIAS_CHECK.append((db_ - before, ref))
+                absum = Af.as_strided((rows, M), (Af.stride(0) if a_bf16 else lda, 1)).abs().sum(0)
+                BIAS_CHECK.append((db_ - before, ref, absum))
         elif name == "asrx_wgrad_bf16":
             lib.call(name, lib.ptr(A), lda, lib.ptr(x2), K, lib.ptr(out), out.stride(0), M, K, rows, sk, lib.stream())
         else:

@@ -59,10 +59,13 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(model, cfg_name, budget_s=10.0, max_clips=3):
-    """The oracle (op-for-op CPU restatement of the reference forward, fp32) timed on the host cores
-    on a bounded sample of the same workload: whole 30 s clips through mel + forward + backward at
-    the same config, repeated until `budget_s` of CPU work has been done."""
+def cpu_baseline(model, cfg_name, warmup=1, runs=3):
+    """The oracle (op-for-op CPU restatement of the reference forward, fp32) timed on the host cores on a
+    bounded sample of the same workload: one 30 s clip through mel + forward + backward at the same
+    config, `warmup` untimed runs then the median of `runs` (warm-ups + median; a
+    30 s tiny clip costs ~5 s of CPU per run, so 1 + 3 keeps the sample near 20 s)."""
+    import statistics
+
     import numpy as np
 
     from asrx import synth
@@ -78,20 +81,77 @@ def cpu_baseline(model, cfg_name, budget_s=10.0, max_clips=3):
     wav = synth.waveform(1, CLIP_SECONDS)
     pitch = synth.pitch(1)
     ids, labels = synth.text(1)
-    clips, t_total = 0, 0.0
-    while clips < max_clips and (t_total < budget_s or clips == 0):
+    times = []
+    for i in range(warmup + runs):
+        for v in P.values():
+            v.grad = None
         t0 = time.perf_counter()
         spec = torch.from_numpy(omel.log_mel(wav[0].numpy().astype(np.float64))).float().unsqueeze(0)
         wf = torch.from_numpy(omel.waveform_feature(wav[0].numpy())).float().unsqueeze(0)
         out = om.forward(P, {"dims": cfg.dims, "head": cfg.head, "layer": cfg.layer}, ids, labels,
-                         spectrogram=spec, pitch=pitch, waveform=wf, seed=0, step=clips, dtype=torch.float32)
+                         spectrogram=spec, pitch=pitch, waveform=wf, seed=0, step=i, dtype=torch.float32)
         out["loss"].backward()
-        t_total += time.perf_counter() - t0
-        clips += 1
-    return {"value": clips * CLIP_SECONDS / t_total, "unit": "audio-sec/sec", "cores": torch.get_num_threads(),
+        if i >= warmup:
+            times.append(time.perf_counter() - t0)
+    med = statistics.median(times)
+    return {"value": CLIP_SECONDS / med, "unit": "audio-sec/sec", "cores": torch.get_num_threads(),
             "kind": "port",
-            "sample": f"{clips} x 30 s clip, {cfg_name} config, T=256, oracle mel + fwd + bwd, fp32, "
-                      f"batch 1, {t_total:.1f} s of CPU time"}
+            "sample": f"1 x 30 s clip, {cfg_name} config, T=256, oracle mel + fwd + bwd, fp32, batch 1: "
+                      f"{warmup} warm-up + median of {runs} ({med:.2f} s per clip)"}
+
+
+def plumbing_line(dev, warmup=3, runs=10):
+    """BASELINE configs[0]: one 1 s clip -> log-mel (128, 101) -> 2-layer D=256 AudioEncoder forward
+    (model.py:120-169, eval), on the CPU oracle (the reference's CPU plumbing case, fp32) and on the HIP
+    path (fp32 parity mode, the same chain) -- 3 warm-ups + the median of 10 each."""
+    import statistics
+
+    import numpy as np
+
+    from asrx import prec
+    from asrx.config import CONFIGS
+    from asrx.mel import logmel
+    from asrx.model import AudioEncoder
+    from asrx.noise import NoiseCtx
+    from oracle import mel as omel
+    from oracle import model as om
+
+    c = CONFIGS["plumbing"]
+    torch.manual_seed(0)
+    enc = AudioEncoder(c.mels, c.dims, c.head, c.layer, c.act, c.n_type).eval()
+    P = {"enc." + k: v.detach().clone() for k, v in enc.state_dict().items()}
+    g = np.random.default_rng(5)
+    audio = (0.5 * np.sin(2 * np.pi * 220.0 * np.arange(16000) / 16000) + 0.05 * g.standard_normal(16000))
+    audio = (audio / np.abs(audio).max()).astype(np.float32)
+
+    def cpu():
+        with torch.no_grad():
+            spec = torch.from_numpy(omel.log_mel(audio.astype(np.float64))).float().unsqueeze(0)
+            return om.encode_stream(P, spec, c.layer, om.Noise(0, 0, torch.float32), [0], training=False)
+
+    tc = []
+    for i in range(warmup + runs):
+        t0 = time.perf_counter()
+        ref = cpu()
+        if i >= warmup:
+            tc.append(time.perf_counter() - t0)
+    enc = enc.to(dev)
+    wav = torch.from_numpy(audio).to(dev).view(1, -1)
+    tg = []
+    with prec.precision("fp32"), torch.no_grad():
+        for i in range(warmup + runs):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            out = enc.layers(enc.stem(logmel(wav, layout="BMF")), NoiseCtx(0, 0, False), 0)
+            torch.cuda.synchronize()
+            if i >= warmup:
+                tg.append(time.perf_counter() - t0)
+    err = float((out.double().cpu() - ref.double()).abs().max() / ref.double().abs().max())
+    return {"workload": "BASELINE configs[0]: 1 x 1 s clip -> log-mel (128, 101) -> 2-layer d=256 encoder forward",
+            "cpu_oracle_ms": round(statistics.median(tc) * 1e3, 3), "cpu_threads": torch.get_num_threads(),
+            "hip_fp32_ms": round(statistics.median(tg) * 1e3, 3),
+            "hip_vs_oracle_max_rel": err, "timing": f"{warmup} warm-ups + median of {runs}",
+            "shape": list(out.shape)}
 
 
 def free_port():
@@ -306,7 +366,8 @@ def main():
             gbs = wn_bytes / wn_sec / 1e9
             result["roofline"] = {"kernel": "asrx::wn::gemm_wr_kernel (wide bf16-weight MFMA GEMM, fp32 / bf16-stored activations)",
                                   "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                  "frac": round(gbs / HBM_PEAK_GBS, 4), **pmc_traffic("gemm_wr_kernel"),
+                                  "frac": round(gbs / HBM_PEAK_GBS, 4),
+                                  **pmc_traffic("gemm_wr_kernel", args.config, args.batch, args.pitch_frames),
                                   "algorithmic_bytes_per_launch": round(wn_bytes / wn_n),
                                   "launches_per_step": wn_n // probe_steps,
                                   "avg_us": round(wn_sec / wn_n * 1e6, 2),
@@ -407,6 +468,7 @@ def main():
                     "specifies 3001-frame pitch)"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(model, args.config)
+        result["configs0_plumbing"] = plumbing_line(dev)
     if distributed:
         dist.barrier()
         dist.destroy_process_group()
@@ -414,19 +476,21 @@ def main():
         print(json.dumps(result), flush=True)
 
 
-def pmc_traffic(kernel_substr):
-    """HBM bytes per launch of a kernel from the newest committed PMC table (profiles/
-    rNN_pmc_traffic_vM.csv, newest round then version: separate rocprofv3 FETCH_SIZE and WRITE_SIZE passes over one eager step,
+def pmc_traffic(kernel_substr, config, batch, pitch_frames):
+    """HBM bytes per launch of a kernel from the newest committed PMC table OF THIS WORKLOAD (profiles/
+    rNN_pmc_traffic_<config>_b<batch>_p<pitch frames>_vM.csv: separate rocprofv3 FETCH_SIZE and WRITE_SIZE
+    passes over one eager step of `bench.py --config C --batch B --no-refpitch-line --no-dead-block-line`,
     FETCH doubled per the gfx950 note, see tools/pmc_traffic.py), launch-weighted over every template
-    instance whose name contains kernel_substr.  PMC counters cannot be read inside the timed run,
-    so the figure comes from the profiling pass of the same step; null when no table is present."""
+    instance whose name contains kernel_substr.  PMC counters cannot be read inside the timed run, so the
+    figure comes from the profiling pass of the same step; null when no table of this workload exists."""
     import csv
     import glob
-    tabs = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
-                                         "r*_pmc_traffic_v*.csv")),
-                  key=lambda p: tuple(int(v) for v in re.search(r"r(\d+)_pmc_traffic_v(\d+)\.csv$", p).groups()))
+    pat = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
+                       f"r*_pmc_traffic_{config}_b{batch}_p{pitch_frames}_v*.csv")
+    key = lambda p: tuple(int(v) for v in re.search(r"r(\d+)_pmc_traffic_.*_v(\d+)\.csv$", p).groups())  # noqa: E731
+    tabs = sorted(glob.glob(pat), key=key)
     if not tabs:
-        return {"traffic": None}
+        return {"traffic": None, "traffic_note": f"no PMC table for {config} B={batch} pitch {pitch_frames}"}
     n, tot = 0, 0.0
     for r in csv.DictReader(open(tabs[-1])):
         if kernel_substr in r["kernel"]:

@@ -149,10 +149,29 @@ def _r(x, point):
     return x + (x.to(torch.bfloat16).to(x.dtype) - x).detach()
 
 
+class _RoundGrad(torch.autograd.Function):
+    """Identity forward; the arriving gradient rounded to bf16 (the bf16 dY of a perf-mode backward GEMM)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).to(g.dtype)
+
+
+def _rg(x, point):
+    """With "bwd" in EMU: the gradient arriving at x rounded to bf16 at an enabled point."""
+    if point not in EMU or "bwd" not in EMU:
+        return x
+    return _RoundGrad.apply(x)
+
+
 def _lin(P, name, x):
     b = P.get(name + ".bias")
     pt = "qkproj" if name.endswith((".q.1", ".kv.1")) else "lin"
-    return F.linear(_r(x, pt), _r(P[name + ".weight"], pt), b)
+    return _rg(F.linear(_r(x, pt), _r(P[name + ".weight"], pt), b), pt)
 
 
 # ------------------------------------------------------------------------------- norms
@@ -315,10 +334,10 @@ def attention(P, pre, x, xa, masked, cfg, noise, site_q, sids_q, site_kv, sids_k
     gk = noise.abby(site_kv + ".kh", sids_kv, H, Lk)
     q = abby_normal(P, pre + ".ln", q, gq, (noise.key(site_q + ".qh"), sids_q))
     k = abby_normal(P, pre + ".ln", k, gk, (noise.key(site_kv + ".kh"), sids_kv))
-    s = (_r(q, "qk") @ _r(k, "qk").transpose(-1, -2)) / math.sqrt(hd)
+    s = _rg((_r(q, "qk") @ _r(k, "qk").transpose(-1, -2)) / math.sqrt(hd), "qk")  # bwd: dS rounded
     if masked:
         s = s.masked_fill(torch.ones(Lq, Lk, dtype=torch.bool).triu(1), float("-inf"))
-    a = _r(torch.softmax(s, dim=-1), "pv") @ _r(v, "pv")
+    a = _rg(_r(torch.softmax(s, dim=-1), "pv") @ _r(v, "pv"), "pv")  # bwd: dO rounded
     a = a.permute(0, 2, 1, 3).reshape(B, Lq, D)
     return _lin(P, pre + ".out.1", a)
 

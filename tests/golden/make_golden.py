@@ -1,9 +1,11 @@
 """Regenerate the golden fixtures in this directory from the oracle (oracle/): a 1 s log-mel +
-waveform-feature vector and a toy-model forward (D=128, H=2, layer=4, V=1000, B=2, T=8, S=101).
+waveform-feature vector, BASELINE configs[0]'s plumbing encoding of that clip (D=256, 2 layers), and a
+toy-model forward (D=128, H=2, layer=4, V=1000, B=2, T=8, S=101).
 The reference itself cannot be executed here, so these vectors pin the oracle
 restatement against regressions; parity with the reference is unpinned.
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py            (all)
+    python tests/golden/make_golden.py plumbing   (plumbing_1s.safetensors only)
 """
 import os
 import sys
@@ -46,6 +48,36 @@ def param_checksum(P):
                         dtype=torch.float64)
 
 
+def plumbing_params():
+    """BASELINE configs[0]'s encoder (asrx CONFIGS['plumbing']: D=256, 2 layers) at seed 0, reference names."""
+    from asrx.config import CONFIGS
+    from asrx.model import AudioEncoder
+
+    c = CONFIGS["plumbing"]
+    torch.manual_seed(0)
+    enc = AudioEncoder(c.mels, c.dims, c.head, c.layer, c.act, c.n_type)
+    return {"enc." + k: v.detach().clone() for k, v in enc.state_dict().items()}
+
+
+def plumbing_encoding(audio):
+    """configs[0]: 1 s clip -> float64 oracle log-mel (128, 101) -> 2-layer D=256 AudioEncoder forward (eval)
+    -> (1, 101, 256) (model.py:149-163)."""
+    from oracle import mel as omel
+    from oracle import model as om
+
+    spec = torch.from_numpy(omel.log_mel(np.asarray(audio, dtype=np.float64))).unsqueeze(0)
+    P = {k: v.double() if v.is_floating_point() else v for k, v in plumbing_params().items()}
+    return om.encode_stream(P, spec, 2, om.Noise(0, 0, torch.float64), [0], training=False)
+
+
+def write_plumbing():
+    from safetensors.torch import load_file
+
+    audio = load_file(os.path.join(HERE, "mel_1s.safetensors"))["audio"].numpy()
+    save_file({"encoding": plumbing_encoding(audio).contiguous(), "param_checksum": param_checksum(plumbing_params())},
+              os.path.join(HERE, "plumbing_1s.safetensors"))
+
+
 def main():
     from oracle import mel as omel
     from oracle import model as om
@@ -57,6 +89,7 @@ def main():
                "logmel": torch.from_numpy(omel.log_mel(audio.astype(np.float64))),
                "waveform": torch.from_numpy(omel.waveform_feature(audio.astype(np.float64)))},
               os.path.join(HERE, "mel_1s.safetensors"))
+    write_plumbing()
 
     spec, pitch, wav, ids, labels = toy_inputs()
     P = toy_params()
@@ -73,4 +106,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["plumbing"]:
+        write_plumbing()
+    else:
+        main()

