@@ -37,12 +37,11 @@ namespace asrx {
 constexpr int MEL_NFFT = 1024, MEL_HOP = 160, MEL_NBINS = 513, MEL_BANDS = 128, MEL_FBW = 32;
 constexpr int FB_A = 8, FB_B = 24;  // taps of a lane's two bands (see lane_filterbank in mel.py)
 constexpr int FB_QUADS = (FB_A + FB_B) / 4;
-constexpr int MEL_WAVES = 8;
-constexpr int MEL_THREADS = 64 * MEL_WAVES;
+constexpr int MEL_WAVES = 4;
 constexpr int MEL_FPT = 16;  // frames per tile
 constexpr int MEL_TSAMP = (MEL_FPT - 1) * MEL_HOP + MEL_NFFT;  // 3424 samples per tile
 constexpr int MEL_TSAMP4 = MEL_TSAMP / 4;                      // 856 float4
-constexpr int MEL_PF = (MEL_TSAMP4 + MEL_THREADS - 1) / MEL_THREADS;  // prefetch float4 per thread
+constexpr int MEL_PF = (MEL_TSAMP4 + 255) / 256;               // prefetch float4 per thread
 constexpr int FFT_SLOTS = 512 + 64 + 8;                        // padded cpx slots per wave
 static_assert(MEL_TSAMP % 4 == 0, "tile samples must be float4 aligned");
 
@@ -105,60 +104,6 @@ __device__ __forceinline__ void ds_rd64x4(uint32_t a, f2v (&o)[4]) {
   asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(o[0]), "+v"(o[1]), "+v"(o[2]), "+v"(o[3]) : : "memory");
 }
 
-// a frame's 8 sample pairs (b64 at base + 512 r bytes) and the matching window pairs (b64 at wbase +
-// 512 r bytes), one wait
-__device__ __forceinline__ void rd_samp_win(uint32_t a, uint32_t wa, f2v (&o)[8], f2v (&w)[8]) {
-  o[0] = ds_rd64<0>(a);
-  o[1] = ds_rd64<512>(a);
-  o[2] = ds_rd64<2 * 512>(a);
-  o[3] = ds_rd64<3 * 512>(a);
-  o[4] = ds_rd64<4 * 512>(a);
-  o[5] = ds_rd64<5 * 512>(a);
-  o[6] = ds_rd64<6 * 512>(a);
-  o[7] = ds_rd64<7 * 512>(a);
-  w[0] = ds_rd64<0>(wa);
-  w[1] = ds_rd64<512>(wa);
-  w[2] = ds_rd64<2 * 512>(wa);
-  w[3] = ds_rd64<3 * 512>(wa);
-  w[4] = ds_rd64<4 * 512>(wa);
-  w[5] = ds_rd64<5 * 512>(wa);
-  w[6] = ds_rd64<6 * 512>(wa);
-  w[7] = ds_rd64<7 * 512>(wa);
-  asm volatile("s_waitcnt lgkmcnt(0)"
-               : "+v"(o[0]), "+v"(o[1]), "+v"(o[2]), "+v"(o[3]), "+v"(o[4]), "+v"(o[5]), "+v"(o[6]), "+v"(o[7]),
-                 "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]), "+v"(w[4]), "+v"(w[5]), "+v"(w[6]), "+v"(w[7])
-               :
-               : "memory");
-}
-
-// the 8 transposed data slots (b64 at base + 576 r bytes) and the 7 twiddles of this lane (b64 at
-// tbase + 512 r bytes) in one batch of LDS reads, one wait
-__device__ __forceinline__ void rd_data_tw(uint32_t a, uint32_t ta, f2v (&o)[8], cpx (&tw)[7]) {
-  f2v t[7];
-  o[0] = ds_rd64<0>(a);
-  o[1] = ds_rd64<576>(a);
-  o[2] = ds_rd64<2 * 576>(a);
-  o[3] = ds_rd64<3 * 576>(a);
-  o[4] = ds_rd64<4 * 576>(a);
-  o[5] = ds_rd64<5 * 576>(a);
-  o[6] = ds_rd64<6 * 576>(a);
-  o[7] = ds_rd64<7 * 576>(a);
-  t[0] = ds_rd64<0>(ta);
-  t[1] = ds_rd64<512>(ta);
-  t[2] = ds_rd64<2 * 512>(ta);
-  t[3] = ds_rd64<3 * 512>(ta);
-  t[4] = ds_rd64<4 * 512>(ta);
-  t[5] = ds_rd64<5 * 512>(ta);
-  t[6] = ds_rd64<6 * 512>(ta);
-  asm volatile("s_waitcnt lgkmcnt(0)"
-               : "+v"(o[0]), "+v"(o[1]), "+v"(o[2]), "+v"(o[3]), "+v"(o[4]), "+v"(o[5]), "+v"(o[6]), "+v"(o[7]),
-                 "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]), "+v"(t[6])
-               :
-               : "memory");
-#pragma unroll
-  for (int r = 0; r < 7; ++r) tw[r] = cpx{t[r].x, t[r].y};
-}
-
 __device__ __forceinline__ void dft8_tw(cpx (&v)[8], const cpx (&tw)[7]) {
 #pragma unroll
   for (int r = 1; r < 8; ++r) v[r] = asrx_fft::cmul(v[r], tw[r - 1]);
@@ -172,8 +117,7 @@ __device__ __forceinline__ int xcd_block(int bid, int G) {
   return (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + q;
 }
 
-// 8 waves per workgroup, two workgroups per CU (78.8 KB LDS each), at most 128 VGPRs: 4 waves per SIMD
-__global__ __launch_bounds__(MEL_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4))) void logmel_tiles_kernel(
+__global__ __launch_bounds__(256, 3) void logmel_tiles_kernel(
     const float* __restrict__ wav, int64_t N, int64_t ld_wav, int vec_ok, int64_t F, int tiles_per_clip,
     int64_t n_tiles, int tiles_per_block, const float* __restrict__ consts, const float* __restrict__ fbw,
     const int* __restrict__ fbs, float* __restrict__ out, int layout, int64_t ld_out,
@@ -183,8 +127,6 @@ __global__ __launch_bounds__(MEL_THREADS) __attribute__((amdgpu_waves_per_eu(4, 
   __shared__ float melst[MEL_FPT][MEL_BANDS + 1];
   __shared__ float red[MEL_WAVES];
   __shared__ float4 fbw_s[FB_QUADS * 64];
-  __shared__ __attribute__((aligned(16))) cpx tw_s[2][7][64];  // pass-2 / pass-3 twiddles [pass][r-1][lane]
-  __shared__ __attribute__((aligned(16))) float2 win_s[8][64];  // window pairs (2n, 2n+1), n = lane + 64 r
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int64_t t_begin = (int64_t)xcd_block(blockIdx.x, gridDim.x) * tiles_per_block;
@@ -195,24 +137,21 @@ __global__ __launch_bounds__(MEL_THREADS) __attribute__((amdgpu_waves_per_eu(4, 
   const float* win = consts;
   const cpx* tw512 = reinterpret_cast<const cpx*>(consts + MEL_NFFT);
   const cpx* tw1024 = reinterpret_cast<const cpx*>(consts + MEL_NFFT + 1024);
-  for (int i = tid; i < 8 * 64; i += MEL_THREADS) win_s[i / 64][i % 64] = reinterpret_cast<const float2*>(win)[i];
-  cpx tu[8];  // untangle twiddles W1024^(lane + 64 r) = W1024^lane exp(-i pi r / 8), lane constants
-  {
-    const cpx tu0 = tw1024[lane];
+  float2 wv[8];
+  cpx t2[7], t3[7];
 #pragma unroll
-    for (int r = 0; r < 8; ++r) tu[r] = asrx_fft::cmul(tu0, cpx{kRot[r][0], kRot[r][1]});
-  }
-  // the pass-2 / pass-3 twiddles live in LDS (lane-contiguous, read with the transposed data): as lane
-  // constants they held 28 VGPRs (the window 16 more), the difference between 3 and 4 waves per SIMD
-  for (int i = tid; i < 2 * 7 * 64; i += MEL_THREADS) {
-    const int ps = i / 448, r = (i / 64) % 7 + 1, l = i % 64;
-    tw_s[ps][r - 1][l] = ps == 0 ? tw512[(r * (l & 7) * 8) & 511] : tw512[(r * l) & 511];
+  for (int r = 0; r < 8; ++r) wv[r] = *reinterpret_cast<const float2*>(win + 2 * (lane + 64 * r));
+  const cpx tu0 = tw1024[lane];
+#pragma unroll
+  for (int r = 1; r < 8; ++r) {
+    t2[r - 1] = tw512[(r * (lane & 7) * 8) & 511];
+    t3[r - 1] = tw512[(r * lane) & 511];
   }
   // lane-packed filterbank (asrx/mel.py lane_filterbank): lane m owns band_a (<= 8 taps from the
   // even bin sa) and band_b (<= 24 taps from the even bin sb); weights [tap/4][lane][4] in LDS
   const int band_a = fbs[lane], band_b = fbs[64 + lane];
   const int sa2 = fbs[128 + lane] >> 1, sb2 = fbs[192 + lane] >> 1;
-  for (int i = tid; i < FB_QUADS * 64; i += MEL_THREADS) fbw_s[i] = reinterpret_cast<const float4*>(fbw)[i];
+  for (int i = tid; i < FB_QUADS * 64; i += 256) fbw_s[i] = reinterpret_cast<const float4*>(fbw)[i];
 
   cpx* S = fbuf[wid];
   float* P = reinterpret_cast<float*>(S);
@@ -228,13 +167,13 @@ __global__ __launch_bounds__(MEL_THREADS) __attribute__((amdgpu_waves_per_eu(4, 
       const float4* x4 = reinterpret_cast<const float4*>(x);
 #pragma unroll
       for (int q = 0; q < MEL_PF; ++q) {
-        const int i4 = tid + MEL_THREADS * q;
+        const int i4 = tid + 256 * q;
         pf[q] = i4 < MEL_TSAMP4 ? x4[i4] : make_float4(0.f, 0.f, 0.f, 0.f);
       }
     } else {
 #pragma unroll
       for (int q = 0; q < MEL_PF; ++q) {
-        const int i4 = tid + MEL_THREADS * q;
+        const int i4 = tid + 256 * q;
         float e[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
@@ -254,7 +193,7 @@ __global__ __launch_bounds__(MEL_THREADS) __attribute__((amdgpu_waves_per_eu(4, 
     __syncthreads();  // the previous tile's readers are done with samp / melst
 #pragma unroll
     for (int q = 0; q < MEL_PF; ++q) {
-      const int i4 = tid + MEL_THREADS * q;
+      const int i4 = tid + 256 * q;
       if (i4 < MEL_TSAMP4) reinterpret_cast<float4*>(samp)[i4] = pf[q];
     }
     __syncthreads();
@@ -278,8 +217,8 @@ __global__ __launch_bounds__(MEL_THREADS) __attribute__((amdgpu_waves_per_eu(4, 
       const bool live = f0 + fi < F;  // wave-uniform
       cpx v[8];
       {
-        f2v sv[8], wv[8];
-        rd_samp_win(lds_off(samp + fi * MEL_HOP + 2 * lane), lds_off(&win_s[0][lane]), sv, wv);
+        f2v sv[8];
+        ds_rd64x8<0, 512>(lds_off(samp + fi * MEL_HOP + 2 * lane), sv);
 #pragma unroll
         for (int r = 0; r < 8; ++r) v[r] = cpx{sv[r].x * wv[r].x, sv[r].y * wv[r].y};
       }
@@ -288,28 +227,27 @@ __global__ __launch_bounds__(MEL_THREADS) __attribute__((amdgpu_waves_per_eu(4, 
 #pragma unroll
       for (int r = 0; r < 8; ++r) S[9 * lane + r] = v[r];
       wave_lds_sync();
-      cpx tw[7];
       {
         f2v t[8];
-        rd_data_tw(lds_off(S + pidx(lane)), lds_off(&tw_s[0][0][lane]), t, tw);
+        ds_rd64x8<0, 576>(lds_off(S + pidx(lane)), t);
 #pragma unroll
         for (int r = 0; r < 8; ++r) v[r] = cpx{t[r].x, t[r].y};
       }
       wave_lds_sync();
       // pass 2 (Ns = 8): out[(j/8)*64 + j%8 + 8r]
-      dft8_tw(v, tw);
+      dft8_tw(v, t2);
 #pragma unroll
       for (int r = 0; r < 8; ++r) S[72 * (lane >> 3) + (lane & 7) + 9 * r] = v[r];
       wave_lds_sync();
       {
         f2v t[8];
-        rd_data_tw(lds_off(S + pidx(lane)), lds_off(&tw_s[1][0][lane]), t, tw);
+        ds_rd64x8<0, 576>(lds_off(S + pidx(lane)), t);
 #pragma unroll
         for (int r = 0; r < 8; ++r) v[r] = cpx{t[r].x, t[r].y};
       }
       wave_lds_sync();
       // pass 3 (Ns = 64): out[j + 64 r] = Z[j + 64 r], kept in v
-      dft8_tw(v, tw);
+      dft8_tw(v, t3);
       // third exchange unpadded: the R-pattern writes and the mirrored reads are conflict-free
       // without padding (lane 0 also stores Z_0 at 512, the mirror of its r = 0 slot)
 #pragma unroll
@@ -326,7 +264,8 @@ __global__ __launch_bounds__(MEL_THREADS) __attribute__((amdgpu_waves_per_eu(4, 
         const cpx zk = v[r];
         const cpx e{zk.x + zn.x, zk.y - zn.y};
         const cpx o{zk.y + zn.y, zn.x - zk.x};
-        const cpx tt = asrx_fft::cmul(tu[r], o);
+        // W1024^(j + 64 r) = W1024^j * exp(-i pi r / 8)
+        const cpx tt = asrx_fft::cmul(asrx_fft::cmul(tu0, cpx{kRot[r][0], kRot[r][1]}), o);
         const float re = e.x + tt.x, im = e.y + tt.y;
         pw[r] = re * re + im * im;  // 4 |X_k|^2
       }
@@ -373,7 +312,7 @@ __global__ __launch_bounds__(MEL_THREADS) __attribute__((amdgpu_waves_per_eu(4, 
     // coalesced output of the staged block
     float* o = out + b * ld_out;
     if (layout == 0) {  // (B, F, 128): the tile is FPT contiguous rows of 128
-      for (int i = tid; i < MEL_FPT * MEL_BANDS / 4; i += MEL_THREADS) {
+      for (int i = tid; i < MEL_FPT * MEL_BANDS / 4; i += 256) {
         const int fi = i / (MEL_BANDS / 4), m4 = (i % (MEL_BANDS / 4)) * 4;
         if (f0 + fi < F) {
           const float* src = &melst[fi][m4];
@@ -381,7 +320,7 @@ __global__ __launch_bounds__(MEL_THREADS) __attribute__((amdgpu_waves_per_eu(4, 
         }
       }
     } else {  // (B, 128, F): each band's FPT frames contiguous
-      for (int i = tid; i < MEL_FPT * MEL_BANDS; i += MEL_THREADS) {
+      for (int i = tid; i < MEL_FPT * MEL_BANDS; i += 256) {
         const int m = i / MEL_FPT, fi = i % MEL_FPT;
         if (f0 + fi < F) o[m * F + f0 + fi] = melst[fi][m];
       }
@@ -446,12 +385,12 @@ extern "C" int asrx_logmel(const float* wav, int64_t B, int64_t N, int64_t ld_wa
                                                                    float_to_ordered(-3.0e38f));
   const int tiles_per_clip = (int)((F + MEL_FPT - 1) / MEL_FPT);
   const int64_t n_tiles = B * tiles_per_clip;
-  // 2 resident 8-wave workgroups per CU (128 VGPRs, 78.8 KB LDS) on 256 CUs; each takes a contiguous run
-  const int64_t slots = 256 * 2;
+  // 3 resident workgroups per CU (168 VGPRs, 48.8 KB LDS) on 256 CUs; each takes a contiguous run
+  const int64_t slots = 256 * 3;
   const int tiles_per_block = (int)std::max<int64_t>(1, (n_tiles + slots - 1) / slots);
   const int64_t grid = (n_tiles + tiles_per_block - 1) / tiles_per_block;
   const int vec_ok = (ld_wav % 4 == 0) && ((reinterpret_cast<uintptr_t>(wav) & 15) == 0);
-  logmel_tiles_kernel<<<(unsigned)grid, MEL_THREADS, 0, stream>>>(wav, N, ld_wav, vec_ok, F, tiles_per_clip, n_tiles,
+  logmel_tiles_kernel<<<(unsigned)grid, 256, 0, stream>>>(wav, N, ld_wav, vec_ok, F, tiles_per_clip, n_tiles,
                                                           tiles_per_block, consts, fbw, fbs, out, layout, ld_out,
                                                           clip_max_ws, pool, T_pool);
   const int64_t per_clip = F * MEL_BANDS;
