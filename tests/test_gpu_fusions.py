@@ -229,10 +229,15 @@ def test_model_bias_grads_fused_match_colsum(cuda):
     finally:
         G.BIAS_CHECK = None
     assert len(checks) > 10, len(checks)
-    for k, (fused, ref, absum) in enumerate(checks):
-        # two fp32 summation orders of the same column: within 1e-5 of the column's sum of |dY|
-        err = float(((fused - ref).abs() / absum.clamp_min(1e-30)).max())
-        assert err < 1e-5, (k, err, fused.shape)
+    bad = []
+    for k, (fused, ref, tol, args) in enumerate(checks):
+        # two fp32 summation orders of the same column: within 1e-5 of the column's sum of |dY| (plus the
+        # rounding of the += into what the bias gradient already held; gemm.BIAS_CHECK's tol)
+        e = (fused - ref).abs() / tol.clamp_min(1e-38)
+        c = int(e.argmax())
+        if float(e[c]) > 1.0:
+            bad.append((k, float(e[c]), c, float(fused[c]), float(ref[c]), float(tol[c]), args))
+    assert not bad, bad
     res = _tiny_step(cuda, model, x, (True, False))
     assert set(res[0]) == set(res[1])
     gap = _grad_gap(res[0], res[1])
