@@ -158,8 +158,8 @@ __device__ __forceinline__ void abby_row_stats(const float (&xv)[E], float& mu, 
   }
   s = wave_sum_dpp(s);
   sa = wave_sum_dpp(sa);
-  mu = s / D;
-  mabs = sa / D;
+  mu = s * (1.0f / D);
+  mabs = sa * (1.0f / D);
   float v = 0.f;
 #pragma unroll
   for (int e = 0; e < E; ++e) {
@@ -167,7 +167,7 @@ __device__ __forceinline__ void abby_row_stats(const float (&xv)[E], float& mu, 
     v += t * t;
   }
   v = wave_sum_dpp(v);
-  sd = sqrtf(v / (D - 1));
+  sd = sqrtf(v * (1.0f / (D - 1)));
 }
 
 // stage x^2 of this lane's features in the wave's padded LDS row and read back the halo
@@ -256,9 +256,11 @@ __device__ __forceinline__ void abby_wmax(const float (&h)[AbbyShape<E>::HL], fl
   }
 }
 
-__device__ __forceinline__ float abby_denom(float div, float& base) {
-  base = div * 1e-4f + 1.0f;
-  return __builtin_amdgcn_exp2f(0.75f * __builtin_amdgcn_logf(base));  // base^0.75, base >= 1
+// 1 / (1 + 1e-4 div)^0.75 = exp2(-0.75 log2(base)), base >= 1: the output is x times this (no IEEE
+// division -- ~10 instructions each -- per feature); lb = log2(base) for the backward's base^-1.75
+__device__ __forceinline__ float abby_idenom(float div, float& lb) {
+  lb = __builtin_amdgcn_logf(div * 1e-4f + 1.0f);
+  return __builtin_amdgcn_exp2f(-0.75f * lb);
 }
 
 template <int E, typename TO = float>
@@ -386,8 +388,8 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_fwd_kernel(const float* 
     }
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      float base;
-      drow[lane * E + e] = abby_denom(avg[e], base);
+      float lb;
+      drow[lane * E + e] = abby_idenom(avg[e], lb);  // inverse denominators
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -395,8 +397,8 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_fwd_kernel(const float* 
 #pragma unroll
     for (int j = 0; j < E / 2; ++j) {
       const float2 dn = *reinterpret_cast<const float2*>(drow + 128 * j + 2 * lane);
-      ov[2 * j] = xv[2 * j] / dn.x;
-      ov[2 * j + 1] = xv[2 * j + 1] / dn.y;
+      ov[2 * j] = xv[2 * j] * dn.x;
+      ov[2 * j + 1] = xv[2 * j + 1] * dn.y;
     }
     if (g.res) {
       float rv[E];
@@ -517,10 +519,11 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_bwd_kernel(
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const float div = sel == 1 ? m2[e] : avg[e];
-      float base;
-      const float denom = abby_denom(div, base);
-      dxv[e] = gv[e] / denom;
-      const float q = -gv[e] * xv[e] * (1e-4f * 0.75f) / (denom * base);
+      float lb;
+      const float idn = abby_idenom(div, lb);
+      dxv[e] = gv[e] * idn;
+      // d out / d div = -0.75e-4 x base^-1.75
+      const float q = -gv[e] * xv[e] * (1e-4f * 0.75f) * __builtin_amdgcn_exp2f(-1.75f * lb);
       dd0 += q * avg[e];
       dd1 += q * m2[e];
       const bool maxsel = sel == 1 && m2[e] != avg[e];
@@ -722,12 +725,12 @@ __device__ __forceinline__ void stats64(const float (&xv)[4], float& mu, float& 
   float sa = fabsf(xv[0]) + fabsf(xv[1]) + fabsf(xv[2]) + fabsf(xv[3]);
   s = row16_sum(s);
   sa = row16_sum(sa);
-  mu = s / 64.f;
-  mabs = sa / 64.f;
+  mu = s * (1.0f / 64.f);
+  mabs = sa * (1.0f / 64.f);
   float v = 0.f;
 #pragma unroll
   for (int e = 0; e < 4; ++e) v += (xv[e] - mu) * (xv[e] - mu);
-  sd = sqrtf(row16_sum(v) / 63.f);
+  sd = sqrtf(row16_sum(v) * (1.0f / 63.f));
 }
 
 template <typename TO = float>
@@ -804,7 +807,7 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_fwd64_kernel(const float
       const float div = (sel == 1 && mx > 2.0f * avg) ? mx : avg;
       if (g.cond && sel == 1) g.cond[r * 64 + 4 * l16 + e] = mx > 2.0f * avg ? 1 : 0;
       float base;
-      ov[e] = xv[e] / abby_denom(div, base);
+      ov[e] = xv[e] * abby_idenom(div, base);
     }
     st64(out + r * 64 + 4 * l16, ov);
   }
@@ -854,9 +857,9 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_bwd64_kernel(
       const float m2 = cnd ? mx : avg;
       const float div = sel == 1 ? m2 : avg;
       float base;
-      const float denom = abby_denom(div, base);
-      dxv[e] = gv[e] / denom;
-      const float q = -gv[e] * xv[e] * (1e-4f * 0.75f) / (denom * base);
+      const float idn = abby_idenom(div, base);  // base: log2 of the denominator's base here
+      dxv[e] = gv[e] * idn;
+      const float q = -gv[e] * xv[e] * (1e-4f * 0.75f) * __builtin_amdgcn_exp2f(-1.75f * base);
       dd0 += q * avg;
       dd1 += q * m2;
       const bool maxsel = sel == 1 && cnd;
@@ -892,7 +895,7 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_bwd64_kernel(
     const float dsd = dcv / den;
     const float dmabs = -dcv * sd / (den * den);
     const float csd = sd > 0.f ? dsd / (63.f * sd) : 0.f;
-    const float cma = dmabs / 64.f;
+    const float cma = dmabs * (1.0f / 64.f);
     float dh[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
