@@ -490,49 +490,64 @@ class processor(nn.Module):  # noqa: N801  (model.py:585-629)
         # launch-latency-bound kernels) runs on a second HIP stream under the next blocks' audio side
         # (bandwidth-bound, 192k-row calls).  Scheduling only: same kernels, same results.
         self.concurrent_dead_text = True
+        # All of blocks 0..L-2 on two side streams (their audio and text sides), concurrently with the live
+        # block's forward AND backward, joined at the end of the backward (round 4); False: the round-3
+        # schedule above (dead audio on the current stream, dead text beside it, joined per forward)
+        self.concurrent_dead_blocks = True
         self._side = None
+        self._pending = None
+        self._hold = []
 
     def forward(self, x, xa, noise: NoiseCtx, seq=False, features=False):
         """features: return the final norm's output instead of the tied logits (Model.forward then runs
         the logits fused with the cross entropy, ops.logits_ce)."""
         B, T = x.shape
+        self.join_dead_blocks()  # a previous forward's side work (no backward ran since)
         xe = ops.Embedding.apply(x, self.token.weight)
         x = ops.add_rows(xe, self.position)
         A_in = [xa["a"], xa["b"], xa["c"]]
         nblk = len(self.block)
-        side = None
-        keep = []  # cross-stream inputs stay referenced until the side stream is joined
-        for i, blk in enumerate(self.block):
-            if self.skip_dead_blocks and i < nblk - 1:
-                continue
-            dead = i < nblk - 1
-            conc = dead and self.concurrent_dead_text and x.is_cuda
-            with torch.no_grad() if dead and torch.is_grad_enabled() else contextlib.nullcontext():
+        live = nblk - 1
+        cuda = x.is_cuda
+        if not self.skip_dead_blocks and live > 0 and cuda and self.concurrent_dead_blocks:
+            # Blocks 0..L-2 depend on nothing but the embeddings and the encoder outputs (every block
+            # restarts from them) and nothing depends on them: they run on side streams, concurrently with
+            # the live block's forward and backward, and are joined at the end of the backward
+            # (Model.forward's hook) -- or right away without one.  Scheduling only: keyed noise, same
+            # kernels, same results.
+            main = torch.cuda.current_stream()
+            s_audio, s_text = self._side_streams(x.device)
+            s_audio.wait_stream(main)
+            s_text.wait_stream(main)
+            with torch.no_grad():
+                for i in range(live):
+                    self._dead_block(i, x, A_in, noise, B, s_audio, s_text)
+            self._pending = (s_audio, s_text, [x, xe] + A_in, main)
+        else:
+            side = None
+            keep = []  # cross-stream inputs stay referenced until the side stream is joined
+            for i in range(live):
+                if self.skip_dead_blocks:
+                    break
+                conc = self.concurrent_dead_text and cuda
                 if conc and side is None:
-                    if self._side is None or self._side.device != x.device:
-                        self._side = torch.cuda.Stream(device=x.device)
-                    side = self._side
+                    side = self._side_streams(x.device)[1]
                     side.wait_stream(torch.cuda.current_stream())
-                with torch.cuda.stream(side) if conc else contextlib.nullcontext():
-                    a = ops.fork(blk.call(x, noise, f"b{i}.ta", 0, masked=True))
-                A = self._audio(blk, A_in, noise, f"b{i}.audio", B, "call")
-                KV = self._audio(blk, A, noise, f"b{i}.xa", B, "xa")
-                if conc:
-                    ev = torch.cuda.Event()
-                    ev.record(torch.cuda.current_stream())
-                    keep.append(KV)
-                with torch.cuda.stream(side) if conc else contextlib.nullcontext():
-                    if conc:
-                        side.wait_event(ev)
-                    b_ = ops.fork(blk.call(a, noise, f"b{i}.tb", 0, kv=KV[0]))
-                    c_ = ops.fork(blk.call(b_, noise, f"b{i}.tc", 0, kv=KV[1]))
-                    d = ops.fork(blk.call(c_, noise, f"b{i}.td", 0, kv=KV[2]))
-                    e = ops.add(a, b_, c_)
-                    kve = blk.xa_side(e, noise, f"b{i}.tg.xa", 0)
-                    g = blk.call(d, noise, f"b{i}.tg", 0, kv=kve)
-        if side is not None:
-            torch.cuda.current_stream().wait_stream(side)
-        keep.clear()
+                with torch.no_grad() if torch.is_grad_enabled() else contextlib.nullcontext():
+                    self._dead_block(i, x, A_in, noise, B, None, side, keep)
+            if side is not None:
+                torch.cuda.current_stream().wait_stream(side)
+            keep.clear()
+        blk = self.block[live]
+        a = ops.fork(blk.call(x, noise, f"b{live}.ta", 0, masked=True))
+        A = self._audio(blk, A_in, noise, f"b{live}.audio", B, "call")
+        KV = self._audio(blk, A, noise, f"b{live}.xa", B, "xa")
+        b_ = ops.fork(blk.call(a, noise, f"b{live}.tb", 0, kv=KV[0]))
+        c_ = ops.fork(blk.call(b_, noise, f"b{live}.tc", 0, kv=KV[1]))
+        d = ops.fork(blk.call(c_, noise, f"b{live}.td", 0, kv=KV[2]))
+        e = ops.add(a, b_, c_)
+        kve = blk.xa_side(e, noise, f"b{live}.tg.xa", 0)
+        g = blk.call(d, noise, f"b{live}.tg", 0, kv=kve)
         if seq:
             out = g
         else:
@@ -541,6 +556,52 @@ class processor(nn.Module):  # noqa: N801  (model.py:585-629)
         if features:
             return out
         return ops.linear(out, self.token.weight)
+
+    def _side_streams(self, device):
+        if self._side is None or self._side[0].device != device:
+            self._side = (torch.cuda.Stream(device=device), torch.cuda.Stream(device=device))
+        return self._side
+
+    def _dead_block(self, i, x, A_in, noise, B, s_audio, s_text, keep=None):
+        """Block i < L-1 without autograd state (model.py:617-626; its output is discarded): the audio side
+        on s_audio (None: the current stream), the text side on s_text (None: the current stream) -- the
+        text self call first, the cross calls after the audio side's k / v (event)."""
+        blk = self.block[i]
+        cur = contextlib.nullcontext
+        with torch.cuda.stream(s_text) if s_text is not None else cur():
+            a = ops.fork(blk.call(x, noise, f"b{i}.ta", 0, masked=True))
+        with torch.cuda.stream(s_audio) if s_audio is not None else cur():
+            A = self._audio(blk, A_in, noise, f"b{i}.audio", B, "call")
+            KV = self._audio(blk, A, noise, f"b{i}.xa", B, "xa")
+            ev = None
+            if s_text is not None:
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream())
+        if keep is not None:
+            keep.append(KV)
+        with torch.cuda.stream(s_text) if s_text is not None else cur():
+            if ev is not None:
+                torch.cuda.current_stream().wait_event(ev)
+            b_ = ops.fork(blk.call(a, noise, f"b{i}.tb", 0, kv=KV[0]))
+            c_ = ops.fork(blk.call(b_, noise, f"b{i}.tc", 0, kv=KV[1]))
+            d = ops.fork(blk.call(c_, noise, f"b{i}.td", 0, kv=KV[2]))
+            e = ops.add(a, b_, c_)
+            kve = blk.xa_side(e, noise, f"b{i}.tg.xa", 0)
+            blk.call(d, noise, f"b{i}.tg", 0, kv=kve)
+        # tensors made on one stream and read on another stay referenced until the join
+        if keep is not None:
+            keep.append((A, KV, a, b_, c_, d, e, kve))
+        elif self._hold is not None:
+            self._hold.append((A, KV, a, b_, c_, d, e, kve))
+
+    def join_dead_blocks(self):
+        """Join the side streams of the concurrent dead blocks into the current stream (idempotent)."""
+        p, self._pending = self._pending, None
+        if p is not None:
+            s_audio, s_text, _, main = p  # the stream the forward (and so its backward) was issued on
+            main.wait_stream(s_audio)
+            main.wait_stream(s_text)
+        self._hold = []
 
     # ---- decoding (Model.generate): the y-independent audio side of the only live block, once
     def audio_cache(self, xa, noise: NoiseCtx, B: int):
@@ -667,18 +728,39 @@ class Model(nn.Module):
             self.noise_step += 1
         enc = self.enc.encode(streams, noise, B)
         xa = {"a": enc[0], "b": enc[1], "c": enc[2]}
+        loss = None
         if labels is not None and self.fused_ce:
             h = self.processor(text_ids, xa, noise, seq=False, features=True)
             if ops.logits_ce_ok(h, self.processor.token.weight):
                 logits, loss = ops.logits_ce(h, self.processor.token.weight, labels, self.bf16_logits)
-                return {"logits": logits, "loss": loss}
-            logits = ops.linear(h, self.processor.token.weight)
+            else:
+                logits = ops.linear(h, self.processor.token.weight)
         else:
             logits = self.processor(text_ids, xa, noise, seq=False)
-        loss = None
-        if labels is not None:
+        if labels is not None and loss is None:
             loss = ops.CrossEntropy.apply(logits, labels)
+        self._join_after_backward(logits, loss)
         return {"logits": logits, "loss": loss}
+
+    def _join_after_backward(self, *outs):
+        """The dead blocks run on side streams (processor.concurrent_dead_blocks): join them at the end of
+        the backward that follows this forward (an autograd final callback queued by a hook on the
+        outputs), so they overlap the live block's backward too and are complete before any optimizer
+        step; without a backward to come, join now."""
+        proc = self.processor
+        if proc._pending is None:
+            return
+        outs = [t for t in outs if t is not None and t.requires_grad]
+        if not (torch.is_grad_enabled() and outs):
+            proc.join_dead_blocks()
+            return
+
+        def hook(g):
+            torch.autograd.Variable._execution_engine.queue_callback(proc.join_dead_blocks)
+            return g
+
+        for t in outs:
+            t.register_hook(hook)
 
     @torch.no_grad()
     def generate(self, spectrogram=None, pitch=None, waveform=None, pitch_tokens=None, max_new_tokens=150):

@@ -275,9 +275,10 @@ def main():
         # captured graph): every rank runs the identical step (same kernels, shapes and inputs)
         # once more eagerly with the probe on, right after the timed steps
         probe.enable(("gemm", "logmel", "attn"))
-        model.processor.concurrent_dead_text = False  # per-kernel event times without a concurrent stream
+        # per-kernel event times without concurrent streams
+        model.processor.concurrent_dead_text = model.processor.concurrent_dead_blocks = False
         step()
-        model.processor.concurrent_dead_text = True
+        model.processor.concurrent_dead_text = model.processor.concurrent_dead_blocks = True
         torch.cuda.synchronize()
         recs = probe.disable()
         probe_steps = 1

@@ -78,8 +78,10 @@ def test_model_parity_fp32(cuda, train):
 def test_skip_dead_blocks_is_output_identical(cuda):
     """processor.skip_dead_blocks (the separately reported bench mode) skips blocks 0..L-2, which the
     reference computes and discards (model.py:617-628): logits, loss and every gradient are
-    identical to the faithful run (keyed noise leaves no RNG stream to keep in step).  So is the
-    faithful run with the dead blocks' text side on the main stream instead of the side stream."""
+    identical to the faithful run (keyed noise leaves no RNG stream to keep in step).  So are the faithful
+    runs with the dead blocks serially on one stream, and with the round-3 schedule (dead audio on the
+    main stream, dead text beside it); the default runs whole dead blocks on side streams, joined at the
+    end of the backward."""
     from asrx import prec
     from asrx.config import Dimensions
     from asrx.model import Model
@@ -89,17 +91,26 @@ def test_skip_dead_blocks_is_output_identical(cuda):
     model = Model(cfg).cuda().train()
     spec, pitch, wav, ids, labels = _toy_inputs()
     res = []
-    for skip, conc in ((False, True), (True, True), (False, False)):
+    # (skip, dead text beside the dead audio, whole dead blocks on side streams across the backward)
+    for skip, conc, blocks in ((False, True, True), (True, True, True), (False, False, False), (False, True, False)):
         model.processor.skip_dead_blocks = skip
         model.processor.concurrent_dead_text = conc
+        model.processor.concurrent_dead_blocks = blocks
         model.zero_grad(set_to_none=True)
         model.set_noise(3, 1)
         with prec.precision("bf16"):
             out = model(labels=labels.cuda(), text_ids=ids.cuda(), spectrogram=spec.cuda(), pitch=pitch.cuda(),
                         waveform=wav.cuda())
+            assert (model.processor._pending is not None) == (blocks and not skip)
             out["loss"].backward()
+        assert model.processor._pending is None  # joined at the end of the backward
         res.append((out["logits"].detach().clone(), {n: p.grad.clone() for n, p in model.named_parameters()
                                                      if p.grad is not None}))
+    with torch.no_grad(), prec.precision("bf16"):  # no backward to come: joined by the forward itself
+        model.processor.concurrent_dead_blocks = True
+        model(labels=labels.cuda(), text_ids=ids.cuda(), spectrogram=spec.cuda(), pitch=pitch.cuda(),
+              waveform=wav.cuda())
+        assert model.processor._pending is None
     model.processor.skip_dead_blocks = False
     model.processor.concurrent_dead_text = True
     for other in res[1:]:  # skipped dead blocks, and dead blocks run serially on one stream
