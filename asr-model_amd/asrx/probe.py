@@ -6,11 +6,17 @@ from __future__ import annotations
 import torch
 
 _active: dict | None = None
+_precise = 0
 
 
-def enable(kinds=("gemm", "logmel", "attn")):
-    global _active
+def enable(kinds=("gemm", "logmel", "attn"), precise_cycles=0):
+    """precise_cycles > 0: a spin kernel of that many cycles (torch.cuda._sleep) runs before every timed
+    launch, so the host has enqueued the start event, the launch and the end event before the GPU reaches
+    them -- in an eager step small kernels otherwise include the host's launch latency (tools/
+    gemm_table.py)."""
+    global _active, _precise
     _active = {k: [] for k in kinds}
+    _precise = int(precise_cycles)
 
 
 def disable():
@@ -22,6 +28,8 @@ def disable():
 def begin(kind):
     if _active is None or kind not in _active:
         return None
+    if _precise:
+        torch.cuda._sleep(_precise)
     e = torch.cuda.Event(enable_timing=True)
     e.record()
     return e

@@ -1,6 +1,9 @@
 """Per-shape GEMM / attention timing of one eager training step (GPU box; not part of the product).
 Runs the bench workload once eagerly with the HIP-event probe on and prints one row per GEMM shape:
-launches, avg us, TF/s, and the fp32-activation byte rate (A + C read/write, bf16 weights)."""
+launches, avg us, TF/s, and the fp32-activation byte rate (A + C read/write, bf16 weights).  Every timed
+launch is preceded by a spin kernel (probe precise mode, PRECISE cycles, default 60000), so small kernels
+are timed without the host's launch latency; the dead blocks run serially (no concurrent streams).
+usage: gemm_table.py [config] [B]"""
 import os
 import sys
 
@@ -21,6 +24,7 @@ cfg = CONFIGS[cfg_name]
 torch.manual_seed(0)
 model = Model(cfg).to(dev).train()
 model.set_noise(seed=0, step=0)
+model.processor.concurrent_dead_text = model.processor.concurrent_dead_blocks = False
 wav = synth.waveform(B, 30.0).to(dev)
 pitch = synth.pitch(B).to(dev)
 ids, labels = synth.text(B, 256, cfg.tokens)
@@ -37,7 +41,7 @@ def step():
 
 step()
 torch.cuda.synchronize()
-probe.enable(("gemm", "attn", "logmel"))
+probe.enable(("gemm", "attn", "logmel"), precise_cycles=int(os.environ.get("PRECISE", "60000")))
 t0 = torch.cuda.Event(enable_timing=True)
 t1 = torch.cuda.Event(enable_timing=True)
 t0.record()
@@ -46,7 +50,7 @@ t1.record()
 torch.cuda.synchronize()
 recs = probe.disable()
 total = t0.elapsed_time(t1) * 1e-3
-print(f"eager step {total*1e3:.1f} ms")
+print(f"eager step with spin kernels {total*1e3:.1f} ms (not a step time)")
 for kind in ("gemm", "attn", "logmel"):
     tab = probe.by_tag(recs[kind])
     tsum = sum(v[2] for v in tab.values())
