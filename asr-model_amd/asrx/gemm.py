@@ -92,12 +92,37 @@ def _build_plan():
     return (keys, srcs, views, table, max(sizes))
 
 
+# weights derived from parameters per step (tgate's concatenation, v_gate's combined projection), built
+# once per step and stream by their first user: parameters do not change inside a step, so the 7 calls
+# of one block's tgate (and the dead blocks' calls on the side streams) share one build per stream
+_DERIVED: dict = {}
+
+
+def derived(key, build):
+    """The per-step cached value of `key` on the current stream (build() makes it on first use)."""
+    k = (key, torch.cuda.current_stream().cuda_stream if torch.cuda.is_available() else 0)
+    v = _DERIVED.get(k)
+    if v is None:
+        v = _DERIVED[k] = build()
+    return v
+
+
+def end_step():
+    """End of a step (the backward, or a forward without one): drop the per-step copies.  The bulk
+    views are keyed by parameter address; once a step is over the parameters may be freed (their model
+    dropped) and another tensor allocated at the same address must not find them."""
+    _WCACHE.clear()
+    _BULK.clear()
+    _DERIVED.clear()
+
+
 def clear_weight_cache(owner=None):
     """Start of a step of `owner` (a Model): drop the per-step copies, then convert the weights this
     owner's previous steps used in one launch (its plan is recorded during its first wide step)."""
     global _OWNER
     _WCACHE.clear()
     _BULK.clear()
+    _DERIVED.clear()
     capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
     if _OWNER is not None and _SEEN and _OWNER not in _PLANS and not capturing:
         _PLANS[_OWNER] = _build_plan()  # the previous step of that owner recorded its weights

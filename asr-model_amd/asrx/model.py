@@ -739,24 +739,26 @@ class Model(nn.Module):
             logits = self.processor(text_ids, xa, noise, seq=False)
         if labels is not None and loss is None:
             loss = ops.CrossEntropy.apply(logits, labels)
-        self._join_after_backward(logits, loss)
+        self._end_step_after(logits, loss)
         return {"logits": logits, "loss": loss}
 
-    def _join_after_backward(self, *outs):
-        """The dead blocks run on side streams (processor.concurrent_dead_blocks): join them at the end of
-        the backward that follows this forward (an autograd final callback queued by a hook on the
-        outputs), so they overlap the live block's backward too and are complete before any optimizer
-        step; without a backward to come, join now."""
-        proc = self.processor
-        if proc._pending is None:
-            return
+    def _end_step(self):
+        """End of a step: join the dead blocks' side streams, drop the per-step weight copies."""
+        self.processor.join_dead_blocks()
+        gemm_mod.end_step()
+
+    def _end_step_after(self, *outs):
+        """The step ends with the backward that follows this forward (an autograd final callback queued
+        by a hook on the outputs): the dead blocks on side streams (processor.concurrent_dead_blocks)
+        overlap the live block's backward too and are joined before any optimizer step, and the
+        per-step weight copies live until then.  Without a backward to come, the step ends now."""
         outs = [t for t in outs if t is not None and t.requires_grad]
         if not (torch.is_grad_enabled() and outs):
-            proc.join_dead_blocks()
+            self._end_step()
             return
 
         def hook(g):
-            torch.autograd.Variable._execution_engine.queue_callback(proc.join_dead_blocks)
+            torch.autograd.Variable._execution_engine.queue_callback(self._end_step)
             return g
 
         for t in outs:
@@ -800,4 +802,5 @@ class Model(nn.Module):
             y = torch.cat((y, nxt), dim=1)
             if bool((nxt == 2).all()):
                 break
+        gemm_mod.end_step()
         return y

@@ -105,10 +105,16 @@ def forward(mod, x0, gpol, save, tag=None):
         M = vg.mkey.shape[0]
         N = M + Dh
         # SH = [x normalize(mkey)^T | mlp[0](x)]     model.py:346-349
-        Wc, bc, mkn = _E(N, D, device=dev), _E(N, device=dev), _E(M, device=dev)
-        wb = _E(N, D, dtype=torch.int16, device=dev) if wide else None
-        lib.call("asrx_vgate_weights", _P(vg.mkey), _P(vg.mlp[0].weight), _P(vg.mlp[0].bias), _P(Wc), _P(bc),
-                 _P(mkn), _P(wb), M, Dh, D, st)
+
+        def build(vg=vg, M=M, Dh=Dh, N=N):
+            Wc, bc, mkn = _E(N, D, device=dev), _E(N, device=dev), _E(M, device=dev)
+            wb = _E(N, D, dtype=torch.int16, device=dev) if wide else None
+            lib.call("asrx_vgate_weights", _P(vg.mkey), _P(vg.mlp[0].weight), _P(vg.mlp[0].bias), _P(Wc), _P(bc),
+                     _P(mkn), _P(wb), M, Dh, D, st)
+            return Wc, bc, mkn, wb
+
+        Wc, bc, mkn, wb = G.derived(("vgate", vg.mkey.data_ptr(), vg.mkey._version, vg.mlp[0].weight._version,
+                                     vg.mlp[0].bias._version, bool(wide)), build)
         # rows of samples not at this layer (next_i[b] != i; the reference never runs them) are skipped:
         # by whole 128-row tiles in the GEMMs, by row in the row kernels
         mt = G.row_tiles(next_i, i, L, rows) if (wide and next_i is not None) else None

@@ -863,10 +863,14 @@ class TGateFn(torch.autograd.Function):
         ctx.set_materialize_grads(False)
         D = x.shape[-1]
         rows = _rows(x)
-        Wcat = _E(3 * D, D, device=x.device)
-        bcat = _E(3 * D, device=x.device)
-        lib.call("asrx_cat3", _P(W0), _P(W1), _P(W2), D * D, _P(Wcat), _S())
-        lib.call("asrx_cat3", _P(b0), _P(b1), _P(b2), D, _P(bcat), _S())
+        def build():
+            Wc, bc = _E(3 * D, D, device=x.device), _E(3 * D, device=x.device)
+            lib.call("asrx_cat3", _P(W0), _P(W1), _P(W2), D * D, _P(Wc), _S())
+            lib.call("asrx_cat3", _P(b0), _P(b1), _P(b2), D, _P(bc), _S())
+            return Wc, bc
+
+        Wcat, bcat = G.derived(("tgate", W0.data_ptr(), W0._version, W1._version, W2._version, b0._version,
+                                b1._version, b2._version), build)
         Gs = G.linear_fwd(x, Wcat, bcat, act="sigmoid")
         if c_pre is not None:  # cs = Linear(D, 3)(x) evaluated by the producing AbbyNormal on fp32 x
             c = c_pre
