@@ -14,7 +14,19 @@ from asrx import lib  # noqa: E402
 calls = []
 lib.call = lambda name, *a: calls.append((name, a))
 lib.require_gpu = lambda *t: None
-lib.load = lambda: type("L", (), {"asrx_msheath_rec_bytes": staticmethod(lambda: 36)})()
+class _FakeLib:
+    """Size queries the host code makes (what the real library answers); everything else returns 64."""
+    asrx_msheath_rec_bytes = staticmethod(lambda: 36)
+    asrx_mem_chunks = staticmethod(lambda L: (L + 63) // 64)
+    asrx_row_tiles_max = staticmethod(lambda M: (M + 127) // 128 + 64)
+    asrx_jump_bwd_part_floats = staticmethod(lambda B, L, d: B * ((L + 127) // 128) * (2 * ((d // 4 + 31) // 32) + d))
+    asrx_wconv_entry_bytes = staticmethod(lambda: 40)
+
+    def __getattr__(self, name):
+        return lambda *a: 64
+
+
+lib.load = lambda: _FakeLib()
 
 from asrx import prec, synth  # noqa: E402
 from asrx.config import CONFIGS  # noqa: E402
@@ -22,7 +34,7 @@ from asrx.model import Model  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 2
 prec.set_precision("bf16")
-torch.cuda.current_stream = lambda: type("S", (), {"cuda_stream": 0})()
+torch.cuda.current_stream = lambda *a: type("S", (), {"cuda_stream": 0})()
 cfg = CONFIGS["tiny"]
 model = Model(cfg).train()
 model.set_noise(seed=0, step=0)
