@@ -269,7 +269,7 @@ class attention(nn.Module):  # noqa: N801
         '(kv h d)' -> k: scale + rotary(|src|) + per-head AbbyNormal."""
         B, L, D = src.shape
         H, hd = self.head, D // self.head
-        src = ops.fork(src)  # read by the kv AbbyNormal and rotary's |src|
+        src = ops.want_rownorm(ops.fork(src))  # read by the kv AbbyNormal and rotary's |src|
         kvn = self.kv[0].run(src, noise, site + ".kv", sid_base, L, out_bf16=True)
         k, v = ops.kv_proj(kvn, self.kv[1].weight, self.kv[1].bias)
         k = ops.rotary(k, src, rotary_freqs(D, H, masked, src.device), hd, self.scale)
@@ -282,7 +282,7 @@ class attention(nn.Module):  # noqa: N801
     def project_q(self, x, noise, site, sid_base, masked):
         B, L, D = x.shape
         H, hd = self.head, D // self.head
-        qn = self.q[0].run(x, noise, site + ".q", sid_base, L, out_bf16=True)
+        qn = self.q[0].run(ops.want_rownorm(x), noise, site + ".q", sid_base, L, out_bf16=True)
         q = ops.linear(qn, self.q[1].weight, self.q[1].bias)
         q = ops.rotary(q, x, rotary_freqs(D, H, masked, x.device), hd, self.scale)
         return self.ln.run(q.view(B, L, H, hd), noise, site + ".qh", sid_base, L, H, out_bf16=prec.attn_bf16_io())

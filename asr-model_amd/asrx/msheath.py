@@ -70,6 +70,9 @@ def _params(mod):
     return ps
 
 
+ACT_SOFTMAX = 16  # csrc/common.h
+
+
 def forward(mod, x0, gpol, save, tag=None):
     """MSheath forward on (B, L, D) x0 with policy noise gpol (B, layers, 3).  Returns (out, saved).
     tag: (noise site key, sid_base) of the call, for asrx.decisions."""
@@ -86,10 +89,9 @@ def forward(mod, x0, gpol, save, tag=None):
     net = mod.pnet.net
     zp = _E(B, net[0].weight.shape[0], device=dev) if save else None
     hp = G.linear_fwd(pooled, net[0].weight, net[0].bias, act="silu", preact=zp)
-    pl = _E(B, 3, device=dev)
-    lib.call("asrx_small_linear_fwd", _P(hp), _P(net[2].weight), _P(net[2].bias), _P(pl), B, hp.shape[1], 3, 0, st)
-    policy = _E(B, 3, device=dev)
-    lib.call("asrx_softmax_small", _P(pl), _P(policy), B, 3, st)
+    policy = _E(B, 3, device=dev)  # softmax(net[2](hp)) in one launch (act 16: the row softmax)
+    lib.call("asrx_small_linear_fwd", _P(hp), _P(net[2].weight), _P(net[2].bias), _P(policy), B, hp.shape[1], 3,
+             ACT_SOFTMAX, st)
     nl = len(mod.layers)
     wide = G.use_wide(D)
     mg = mod.mem_gate[0]

@@ -544,6 +544,15 @@ class AbbyNormalFn(torch.autograd.Function):
                 hpre, logits = G.linear_fwd(x, W1, b1), None
             lib.call("asrx_abby_fwd_res", _P(x), _P(hpre), _P(W2), _P(logits), _P(b2), _P(res), _P(out), _P(ys),
                      _P(idx), rows, d, L, H, sid_base, key & 0xFFFFFFFF, int(use_noise), _S())
+        elif side is not None and side.get("want_norm"):  # also ||x[r]|| for rotary's |src|
+            if G.use_wide(d) and d <= 384 and rows >= ROUTER_FUSED_MIN_ROWS:
+                hpre, logits = G.router_fwd(x.view(rows, d), W1, b1, W2, keep)
+            else:
+                hpre, logits = G.linear_fwd(x, W1, b1), None
+            nrm = _E(rows, device=x.device)
+            lib.call("asrx_abby_fwd3", _P(x), _P(hpre), _P(W2), _P(logits), _P(b2), _P(out), ob, _P(ys), _P(idx),
+                     rows, d, L, H, sid_base, key & 0xFFFFFFFF, int(use_noise), _P(tw), _P(tb), _P(tc), _P(nrm), _S())
+            side["rownorm"] = nrm
         elif G.use_wide(d) and d <= 384 and rows >= ROUTER_FUSED_MIN_ROWS:
             # perf mode: the router's d x d GEMM also applies SiLU and Linear(d, 3) in its epilogue,
             # so h_pre never makes the HBM round trip unless the backward needs it
@@ -605,11 +614,30 @@ def abby_normal(mod, x, L, H, sid_base, key, use_noise=True, out_bf16=False, tga
     if tgate is not None and H == 1 and x.shape[-1] >= 128:
         tw, tb = tgate.cs[0].weight, tgate.cs[0].bias
     side = {}
+    if (getattr(x, "_asrx_want_norm", False) and H == 1 and x.shape[-1] >= 128 and residual is None
+            and x.is_cuda and rownorm_of(x) is None):
+        side["want_norm"] = True
     y = AbbyNormalFn.apply(x, r[0].weight, r[0].bias, r[2].weight, r[2].bias, L, H, sid_base, key, use_noise,
                            keep, sink_of(x), out_bf16, osink, tw, tb, side, residual)
     if tw is not None:
         y._asrx_tgate_c = (side["tgate_c"], tw)  # tgate's cs logits of these rows, for ops.tgate
+    if "rownorm" in side:
+        x._asrx_rownorm = (x._version, _S(), side["rownorm"])
     return out_sink(y, osink)
+
+
+def want_rownorm(x):
+    """Ask the AbbyNormal that reads x next to also write ||x[r]|| (rotary's |src|, model.py:201)."""
+    x._asrx_want_norm = True
+    return x
+
+
+def rownorm_of(x):
+    """||x[r]|| (rows,) left on x by its AbbyNormal (want_rownorm), or None; the tensor's version
+    counter guards against an in-place change since, the stream against a read on another stream than
+    the one that wrote it (the processor runs blocks on side streams)."""
+    c = getattr(x, "_asrx_rownorm", None)
+    return c[2] if c is not None and c[0] == x._version and c[1] == _S() else None
 
 
 # =============================================================================== LayerNorm
@@ -747,13 +775,14 @@ class RotaryFn(torch.autograd.Function):
     """rotary.forward (model.py:198-214) fused with the hd^-0.25 scale: x, src (B, L, D)."""
 
     @staticmethod
-    def forward(ctx, x, src, freqs, hd, scale, sink=None):
+    def forward(ctx, x, src, freqs, hd, scale, sink=None, m=None):
         x = _c(x)
         src = _c(src)
         ctx.sink = sink
         B, L, D = x.shape
-        m = _E(B * L, device=x.device)
-        lib.call("asrx_rownorm", _P(src), _P(m), B * L, D, _S())
+        if m is None:  # else ||src[r]|| written by src's AbbyNormal (want_rownorm)
+            m = _E(B * L, device=x.device)
+            lib.call("asrx_rownorm", _P(src), _P(m), B * L, D, _S())
         y = _E(x.shape, device=x.device)
         lib.call("asrx_rotary_fwd", _P(x), _P(m), _P(freqs), _P(y), B * L, L, D, hd, float(scale), _S())
         ctx.hd, ctx.scale = hd, scale
@@ -777,11 +806,11 @@ class RotaryFn(torch.autograd.Function):
                 buf, acc = _E(src.shape, device=src.device), 0
             lib.call("asrx_rownorm_bwd2", _P(dm), _P(src), _P(m), _P(buf), B * L, D, acc, _S())
             dsrc = None if ctx.sink is not None else buf
-        return dx, dsrc, None, None, None, None
+        return dx, dsrc, None, None, None, None, None
 
 
 def rotary(x, src, freqs, hd, scale):
-    return RotaryFn.apply(x, src, freqs, hd, scale, sink_of(src))
+    return RotaryFn.apply(x, src, freqs, hd, scale, sink_of(src), rownorm_of(src))
 
 
 # =============================================================================== v_gate

@@ -36,6 +36,9 @@ struct AbbyGeom {
   // residual input (d >= 128 forward, fp32 out): out = res + x / denom -- the block's closing residual
   // add (model.py:583 x + mlp(x) with mlp's last AbbyNormal) without a separate add pass
   const float* res;
+  // row L2 norm output (optional, d >= 128 forward): ||x[r]|| for rotary's |src| (model.py:201), the
+  // rows' sum of squares taken from the values already in registers instead of a second pass over x
+  float* nrm;
 };
 
 // Per-row layout (MI355X design): lane l owns the E = d/64 CONSECUTIVE features [l E, l E + E), read
@@ -343,6 +346,13 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_fwd_kernel(const float* 
     }
     float mu, sd, mabs;
     abby_row_stats<E>(xv, mu, sd, mabs);
+    if (g.nrm) {
+      float ss = 0.f;
+#pragma unroll
+      for (int e = 0; e < E; ++e) ss += xv[e] * xv[e];
+      ss = wave_sum_dpp(ss);
+      if (lane == 0) g.nrm[r] = sqrtf(ss);
+    }
     const float cv = sd / (mabs + 1e-6f);
     float z0 = l0 + b2[0] + cv, z1 = l1 + b2[1] + cv, z2 = l2 + b2[2] + cv;
     if (g.use_noise) abby_gumbel3(g, r, lane, z0, z1, z2);
@@ -461,18 +471,29 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_bwd_kernel(
   int64_t r = (int64_t)blockIdx.x * ABBY_WAVES + wid;
   // x and dout of the next TWO rows (coalesced layout) are in flight while this row is processed
   // (one row ahead left the kernel latency-bound); past the end the last row is re-read
-  float xn1[E], gn1[E], xn2[E], gn2[E];
-  auto fetch = [&](int64_t rr, float (&xb)[E], float (&gb)[E]) __attribute__((always_inline)) {
+  // (the row's mode and softmax outputs travel with it: read at the top of the row they stalled every
+  // row for a full memory latency before the pools could start)
+  float xn1[E], gn1[E], xn2[E], gn2[E], yn1[3], yn2[3];
+  int sn1, sn2;
+  auto fetch = [&](int64_t rr, float (&xb)[E], float (&gb)[E], float (&yb)[3], int& sb) __attribute__((always_inline)) {
     const int64_t rc = rr < g.rows ? rr : g.rows - 1;
     ld_rowc<E>(x + rc * S::D, lane, xb);
     ld_rowc<E>(dout + rc * S::D, lane, gb);
+    yb[0] = ys[rc * 3 + 0];
+    yb[1] = ys[rc * 3 + 1];
+    yb[2] = ys[rc * 3 + 2];
+    sb = idx_in[rc];
   };
   if (r < g.rows) {
-    fetch(r, xn1, gn1);
-    fetch(r + stride, xn2, gn2);
+    fetch(r, xn1, gn1, yn1, sn1);
+    fetch(r + stride, xn2, gn2, yn2, sn2);
   }
   for (; r < g.rows; r += stride) {
     float xc[E], xv[E], gv[E];  // xc: coalesced layout; xv, gv: the lane's E consecutive features
+    // this row's later operands, issued now so their latency overlaps the pool work
+    float hv[E], old[E];
+    ld_rowc<E>(hpre + r * S::D, lane, hv);
+    if (g.acc) ld_rowc<E>(dx + r * S::D, lane, old);
 #pragma unroll
     for (int j = 0; j < E / 2; ++j) {
       xc[2 * j] = xn1[2 * j];
@@ -480,12 +501,17 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_bwd_kernel(
       *reinterpret_cast<float2*>(xr + 128 * j + 2 * lane) = make_float2(xn1[2 * j], xn1[2 * j + 1]);
       *reinterpret_cast<float2*>(gr + 128 * j + 2 * lane) = make_float2(gn1[2 * j], gn1[2 * j + 1]);
     }
+    const int sel = __builtin_amdgcn_readfirstlane(sn1);
+    const float y0 = yn1[0], y1 = yn1[1], y2 = yn1[2];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       xn1[e] = xn2[e];
       gn1[e] = gn2[e];
     }
-    fetch(r + 2 * stride, xn2, gn2);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) yn1[k] = yn2[k];
+    sn1 = sn2;
+    fetch(r + 2 * stride, xn2, gn2, yn2, sn2);
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
 #pragma unroll
@@ -493,8 +519,6 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_bwd_kernel(
       xv[e] = xr[lane * E + e];
       gv[e] = gr[lane * E + e];
     }
-    const int sel = idx_in[r];
-    const float y0 = ys[r * 3 + 0], y1 = ys[r * 3 + 1], y2 = ys[r * 3 + 2];
     // the pad entries of `row` hold -1 for the x^2 halo; the coefficient pass below re-pads with 0
     for (int i = lane; i < S::PAD; i += 64) {
       row[i] = -1.f;
@@ -605,14 +629,13 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_bwd_kernel(
     for (int e = 0; e < E; ++e) xr[lane * E + e] = dxv[e];
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    float dxc[E], hv[E], dh[E], w2v[3][E];
+    float dxc[E], dh[E], w2v[3][E];
 #pragma unroll
     for (int j = 0; j < E / 2; ++j) {
       const float2 t = *reinterpret_cast<const float2*>(xr + 128 * j + 2 * lane);
       dxc[2 * j] = t.x;
       dxc[2 * j + 1] = t.y;
     }
-    ld_rowc<E>(hpre + r * S::D, lane, hv);
 #pragma unroll
     for (int k = 0; k < 3; ++k) ld_rowc<E>(W2 + k * S::D, lane, w2v[k]);  // L1-resident
 #pragma unroll
@@ -627,8 +650,6 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_bwd_kernel(
       accW[2][e] += dz2 * hs;
     }
     if (g.acc) {
-      float old[E];
-      ld_rowc<E>(dx + r * S::D, lane, old);
 #pragma unroll
       for (int e = 0; e < E; ++e) dxc[e] += old[e];
     }
@@ -974,6 +995,7 @@ static AbbyGeom make_geom(int64_t rows, int64_t d, int64_t L, int64_t H, int64_t
   AbbyGeom g;
   g.cond = nullptr;
   g.res = nullptr;
+  g.nrm = nullptr;
   g.rows = rows;
   g.d = d;
   g.L = L > 0 ? L : 1;
@@ -1055,6 +1077,40 @@ extern "C" int asrx_abby_fwd_logits2(const float* x, const float* logits, const 
     ABBY_DISPATCH_T(abby_fwd_kernel, float, x, nullptr, nullptr, b2, (float*)out, ys, idx, g, logits, tw, tb, tc);
   }
   ASRX_LAUNCHED("asrx_abby_fwd_logits");
+}
+
+// asrx_abby_fwd2 (logits NULL) / asrx_abby_fwd_logits2 (logits given, hpre / W2 unused) that also writes
+// the input rows' L2 norms to nrm (rows,) when nrm is non-NULL (d >= 128).
+extern "C" int asrx_abby_fwd3(const float* x, const float* hpre, const float* W2, const float* logits,
+                              const float* b2, void* out, int out_bf16, float* ys, int* idx, int64_t rows, int64_t d,
+                              int64_t L, int64_t H, int64_t sid_base, uint32_t key, int use_noise, const float* tw,
+                              const float* tb, float* tc, float* nrm, hipStream_t stream) {
+  if (!nrm) {
+    if (logits)
+      return asrx_abby_fwd_logits2(x, logits, b2, out, out_bf16, ys, idx, rows, d, L, H, sid_base, key, use_noise, tw,
+                                   tb, tc, stream);
+    return asrx_abby_fwd2(x, hpre, W2, b2, out, out_bf16, ys, idx, rows, d, L, H, sid_base, key, use_noise, tw, tb,
+                          tc, stream);
+  }
+  ASRX_REQUIRE(!tw || d >= 128, "AbbyNormal: the fused tgate cs needs d >= 128");
+  ASRX_REQUIRE(d % 64 == 0 && d >= 128 && d <= 1024,
+               "asrx_abby_fwd3: d=%ld must be a multiple of 64 in [128,1024] with a norm output", (long)d);
+  ASRX_REQUIRE(logits || (hpre && W2), "asrx_abby_fwd3: logits or hpre/W2");
+  if (rows == 0) return 0;
+  const int E = (int)(d / 64);
+  AbbyGeom g = make_geom(rows, d, L, H, sid_base, key, use_noise);
+  g.cond = g_cond_record;
+  g.nrm = nrm;
+  const float* hp = logits ? nullptr : hpre;
+  const float* w2 = logits ? nullptr : W2;
+  const unsigned grid = (unsigned)std::min<int64_t>((rows + ABBY_WAVES - 1) / ABBY_WAVES, 4096);
+  if (out_bf16) {
+    ABBY_DISPATCH_T(abby_fwd_kernel, unsigned short, x, hp, w2, b2, (unsigned short*)out, ys, idx, g, logits, tw, tb,
+                    tc);
+  } else {
+    ABBY_DISPATCH_T(abby_fwd_kernel, float, x, hp, w2, b2, (float*)out, ys, idx, g, logits, tw, tb, tc);
+  }
+  ASRX_LAUNCHED("asrx_abby_fwd3");
 }
 
 // asrx_abby_fwd_logits2 / asrx_abby_fwd2 (hpre given, logits NULL) with a residual input: out = res +

@@ -22,6 +22,8 @@ namespace asrx {
 enum Prec : int { PREC_F32 = 0, PREC_BF16 = 1 };
 
 enum Act : int { ACT_NONE = 0, ACT_GELU = 1, ACT_SILU = 2, ACT_SIGMOID = 3, ACT_RELU = 4 };
+// small_linear only: softmax over the N outputs of each row (forward only; the caller differentiates it)
+constexpr int ACT_SOFTMAX = 16;
 
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
@@ -87,17 +89,33 @@ __device__ __forceinline__ float wave_sum(float v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
-// Wave sum with the in-row steps on DPP (VALU, no LDS round trip): xor 1 and xor 2 by quad_perm,
-// then the other quad of each 8 (row_half_mirror) and the other 8 of each 16 (row_mirror); the two
-// cross-row steps go through ds_bpermute.  Every lane ends with the full sum.
+// Cross-row exchanges on gfx950's v_permlane{16,32}_swap_b32 (VALU, no LDS round trip).  With both
+// operands holding v, the 16-lane swap leaves rows (r0, r0, r2, r2) in one and (r1, r1, r3, r3) in the
+// other, so a + b is v + v[lane ^ 16] in every lane; the 32-lane swap likewise pairs lane with lane ^ 32.
+// Inline asm: the ROCm 7.2 compiler returns the first result for both members of the builtin's pair.
+// The s_nop covers the VALU-write -> permlane-read hazard (the compiler cannot see into the asm).
+__device__ __forceinline__ void xrow16(float& a, float& b) {
+  asm("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+}
+__device__ __forceinline__ void xrow32(float& a, float& b) {
+  asm("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+}
+// Wave sum with the in-row steps on DPP: xor 1 and xor 2 by quad_perm, then the other quad of each 8
+// (row_half_mirror) and the other 8 of each 16 (row_mirror); the two cross-row steps by permlane
+// swaps.  Every lane ends with the full sum, bit-identical to the ds_bpermute (__shfl_xor) version
+// (each step adds the same two values; float addition commutes).
 __device__ __forceinline__ float wave_sum_dpp(float v) {
   v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
   v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
   v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
   v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));
-  v += __shfl_xor(v, 16, 64);
-  v += __shfl_xor(v, 32, 64);
-  return v;
+  float a = v, b = v;
+  xrow16(a, b);
+  v = a + b;
+  a = v;
+  b = v;
+  xrow32(a, b);
+  return a + b;
 }
 // wave_sum_dpp's pattern with max (exact, so the result equals wave_max's)
 __device__ __forceinline__ float wave_max_dpp(float v) {
@@ -105,9 +123,13 @@ __device__ __forceinline__ float wave_max_dpp(float v) {
   v = fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false)));
   v = fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false)));
   v = fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false)));
-  v = fmaxf(v, __shfl_xor(v, 16, 64));
-  v = fmaxf(v, __shfl_xor(v, 32, 64));
-  return v;
+  float a = v, b = v;
+  xrow16(a, b);
+  v = fmaxf(a, b);
+  a = v;
+  b = v;
+  xrow32(a, b);
+  return fmaxf(a, b);
 }
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll

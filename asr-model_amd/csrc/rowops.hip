@@ -282,6 +282,20 @@ __global__ __launch_bounds__(64 * RW) void small_linear_fwd_kernel(const TX* __r
 #pragma unroll
       for (int n = 0; n < NS; ++n) acc[n] += xv * W[n * K + k];
     }
+    if (act == ACT_SOFTMAX) {  // the row's softmax, in asrx_softmax_small's order of operations
+      float v[NS], m = -INFINITY, s = 0.f;
+#pragma unroll
+      for (int n = 0; n < NS; ++n) {
+        v[n] = wave_sum(acc[n]) + (b ? b[n] : 0.f);
+        m = fmaxf(m, v[n]);
+      }
+#pragma unroll
+      for (int n = 0; n < NS; ++n) s += expf(v[n] - m);
+#pragma unroll
+      for (int n = 0; n < NS; ++n)
+        if (lane == n) y[r * NS + n] = expf(v[n] - m) / s;
+      continue;
+    }
 #pragma unroll
     for (int n = 0; n < NS; ++n) {
       const float v = wave_sum(acc[n]) + (b ? b[n] : 0.f);

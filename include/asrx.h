@@ -153,6 +153,12 @@ int asrx_abby_fwd2(const float* x, const float* hpre, const float* W2, const flo
 int asrx_abby_fwd_logits2(const float* x, const float* logits, const float* b2, void* out, int out_bf16, float* ys,
                           int* idx, int64_t rows, int64_t d, int64_t L, int64_t H, int64_t sid_base, uint32_t key,
                           int use_noise, const float* tw, const float* tb, float* tc, asrx_stream_t stream);
+/* asrx_abby_fwd2 (logits NULL) / asrx_abby_fwd_logits2 (logits given) that also writes ||x[r]||_2 to nrm
+   (rows,) when nrm is non-NULL (d >= 128): the |src| of rotary (model.py:201) without a second pass. */
+int asrx_abby_fwd3(const float* x, const float* hpre, const float* W2, const float* logits, const float* b2,
+                   void* out, int out_bf16, float* ys, int* idx, int64_t rows, int64_t d, int64_t L, int64_t H,
+                   int64_t sid_base, uint32_t key, int use_noise, const float* tw, const float* tb, float* tc,
+                   float* nrm, asrx_stream_t stream);
 int asrx_abby_bwd(const float* dout, const float* x, const float* hpre, const float* W2, const float* ys,
                   const int* idx, float* dx, float* dhpre, float* dW2, float* db2, int64_t rows, int64_t d,
                   asrx_stream_t stream);
@@ -211,7 +217,8 @@ int asrx_layernorm_fwd3(const float* x, const float* w, const float* b, void* y,
 
 /* ---- small-N linear (N <= 4): gate / mem_gate / mlp_gate Linear(D,1) (model.py:398, 406, 420),
  *      v_gate.mlp[2] (341), tgate.cs Linear(D,3) (530), MPNet's Linear(128,3) (381).
- *      act: 0 none, 3 sigmoid.  Backward: dx = beta*dx + dz W; dW/db accumulated. ------------------ */
+ *      act: 0 none, 3 sigmoid; forward only: 16 = softmax over the N outputs of the row (MPNet + the
+ *      softmax of model.py:435 in one launch).  Backward: dx = beta*dx + dz W; dW/db accumulated. ------ */
 int asrx_small_linear_fwd(const float* x, const float* W, const float* b, float* y, int64_t rows, int64_t K,
                           int64_t N, int act, asrx_stream_t stream);
 int asrx_small_linear_bwd(const float* dy, const float* y, const float* x, const float* W, float* dx, float* dW,

@@ -118,30 +118,44 @@ def norm_bench():
 
 
 def abby_bench():
+    """AbbyNormal row kernels at the model's shapes; ck = float64 checksums of the outputs (compare two
+    builds with ASRX_LIB: the kernels are deterministic except the dW2 atomics)."""
     from asrx import lib
 
     dev = torch.device("cuda:0")
     P = lib.ptr
-    for rows, d in ((192064, 384), (1152384, 64), (48016, 768)):
-        x = torch.randn(rows, d, device=dev) * 3
-        lg = torch.randn(rows, 3, device=dev)
-        b2 = torch.randn(3, device=dev)
+    ck = lambda *ts: " ".join(f"{float(t.double().sum()):.9e}" for t in ts)  # noqa: E731
+    for rows, d in ((192064, 384), (96032, 384), (1152384, 64), (48016, 768)):
+        g0 = torch.Generator(device=dev).manual_seed(rows + d)
+        x = torch.randn(rows, d, device=dev, generator=g0) * 3
+        lg = torch.randn(rows, 3, device=dev, generator=g0)
+        b2 = torch.randn(3, device=dev, generator=g0)
         out = torch.empty_like(x)
+        outb = torch.empty(rows, d, device=dev, dtype=torch.bfloat16)
         ys = torch.empty(rows, 3, device=dev)
         idx = torch.empty(rows, dtype=torch.int32, device=dev)
         t = timeit(lambda: lib.call("asrx_abby_fwd_logits", P(x), P(lg), P(b2), P(out), P(ys), P(idx), rows, d, 1, 1,
                                     0, 7, 1, lib.stream()))
-        print(f"abby fwd rows={rows} d={d}: {t*1e6:.1f} us {2*rows*d*4/t/1e9:.0f} GB/s (x in, out)", flush=True)
-        h = torch.randn(rows, d, device=dev)
-        w2 = torch.randn(3, d, device=dev)
-        g = torch.randn(rows, d, device=dev)
+        print(f"abby fwd rows={rows} d={d}: {t*1e6:.1f} us {2*rows*d*4/t/1e9:.0f} GB/s (x in, out) ck {ck(out, ys)}",
+              flush=True)
+        t = timeit(lambda: lib.call("asrx_abby_fwd_logits2", P(x), P(lg), P(b2), P(outb), 1, P(ys), P(idx), rows, d,
+                                    1, 1, 0, 7, 1, None, None, None, lib.stream()))
+        print(f"abby fwd bf16-out rows={rows} d={d}: {t*1e6:.1f} us {rows*d*6/t/1e9:.0f} GB/s ck {ck(outb)}",
+              flush=True)
+        h = torch.randn(rows, d, device=dev, generator=g0)
+        w2 = torch.randn(3, d, device=dev, generator=g0)
+        g = torch.randn(rows, d, device=dev, generator=g0)
         dx, dh = torch.empty_like(x), torch.empty_like(x)
         dW2, db2 = torch.zeros(3, d, device=dev), torch.zeros(3, device=dev)
         t = timeit(lambda: lib.call("asrx_abby_bwd", P(g), P(x), P(h), P(w2), P(ys), P(idx), P(dx), P(dh), P(dW2),
                                     P(db2), rows, d, lib.stream()))
-        print(f"abby bwd rows={rows} d={d}: {t*1e6:.1f} us {5*rows*d*4/t/1e9:.0f} GB/s (g,x,h in; dx,dh out)",
-              flush=True)
-        del x, h, g, dx, dh, out
+        print(f"abby bwd rows={rows} d={d}: {t*1e6:.1f} us {5*rows*d*4/t/1e9:.0f} GB/s (g,x,h in; dx,dh out) "
+              f"ck {ck(dx, dh)}", flush=True)
+        dx.zero_()
+        t = timeit(lambda: lib.call("asrx_abby_bwd2", P(g), P(x), P(h), P(w2), P(ys), P(idx), P(dx), P(dh), P(dW2),
+                                    P(db2), rows, d, 1, lib.stream()), iters=1, warm=0)
+        print(f"abby bwd acc rows={rows} d={d}: {t*1e6:.1f} us (one launch, cold) ck {ck(dx, dh)}", flush=True)
+        del x, h, g, dx, dh, out, outb
 
 
 def attn_bench():
