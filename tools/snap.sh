@@ -4,6 +4,12 @@
 # usage: bash tools/snap.sh   then   gpurun -- 'cd .snap && bash tools/<script>.sh'
 set -e
 cd /root/repo
+# refuse a library older than its sources (a snapshot taken while `make` was relinking it is the likely
+# cause of round 3's one unexplained abort)
+so=asr-model_amd/asrx/libasrx.so
+if [ -n "$(find asr-model_amd/csrc include -newer $so -type f | head -1)" ]; then
+  echo "snap: $so is older than its sources; run make first" >&2; exit 1
+fi
 rm -rf .snap.new
 mkdir .snap.new
 tar --exclude=./.git --exclude=./gpurun_out --exclude=./.snap --exclude=./.snap.new --exclude=./asr-model_amd/build \
