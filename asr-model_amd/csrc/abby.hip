@@ -70,7 +70,7 @@ __device__ __forceinline__ uint32_t abby_noise_idx(const AbbyGeom& g, int64_t r,
 // third of the hash / log work of every lane computing all three
 __device__ __forceinline__ void abby_gumbel3(const AbbyGeom& g, int64_t r, int lane, float& z0, float& z1,
                                              float& z2) {
-  const float gk = noise_gumbel(g.key, abby_noise_idx(g, r, lane < 3 ? lane : 0));
+  const float gk = noise_gumbel_k(g.key, abby_noise_idx(g, r, lane < 3 ? lane : 0));  // key: noise_key'd
   const int gi = __builtin_bit_cast(int, gk);
   z0 += __builtin_bit_cast(float, __builtin_amdgcn_readlane(gi, 0));
   z1 += __builtin_bit_cast(float, __builtin_amdgcn_readlane(gi, 1));
@@ -300,34 +300,28 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_fwd_kernel(const float* 
   }
   const int64_t stride = (int64_t)gridDim.x * ABBY_WAVES;
   int64_t r = (int64_t)blockIdx.x * ABBY_WAVES + wid;
-  // the next TWO rows' x (coalesced layout) and router logits are in flight while this row is
-  // processed: one row of prefetch left the kernel latency-bound at ~2.5 TB/s (1.5 KB per wave in
-  // flight); loads past the end re-read the last row (unconditional, so the wait counts stay uniform)
-  float xn1[E], xn2[E], ln1[3] = {0.f, 0.f, 0.f}, ln2[3] = {0.f, 0.f, 0.f};
-  auto fetch = [&](int64_t rr, float (&xb)[E], float (&lb)[3]) __attribute__((always_inline)) {
+  g.key = noise_key(g.key);
+  // The next TWO rows' x (coalesced layout) and router logits are in flight while a row is processed,
+  // in two NAMED register sets used alternately (the loop is unrolled by two): rotating one set into
+  // the other (x1 = x2 at the top of each row) made the compiler wait for the newest prefetch at every
+  // row, i.e. one row of prefetch in effect.  Loads past the end re-read the last row (unconditional,
+  // so the wait counts stay uniform).
+  float xa[E], xb[E], la[3] = {0.f, 0.f, 0.f}, lb[3] = {0.f, 0.f, 0.f};
+  auto fetch = [&](int64_t rr, float (&xs)[E], float (&ls)[3]) __attribute__((always_inline)) {
     const int64_t rc = rr < g.rows ? rr : g.rows - 1;
-    ld_rowc<E>(x + rc * S::D, lane, xb);
+    ld_rowc<E>(x + rc * S::D, lane, xs);
     if (logits) {
-      lb[0] = logits[rc * 3 + 0];
-      lb[1] = logits[rc * 3 + 1];
-      lb[2] = logits[rc * 3 + 2];
+      ls[0] = logits[rc * 3 + 0];
+      ls[1] = logits[rc * 3 + 1];
+      ls[2] = logits[rc * 3 + 2];
     }
   };
   if (r < g.rows) {
-    fetch(r, xn1, ln1);
-    fetch(r + stride, xn2, ln2);
+    fetch(r, xa, la);
+    fetch(r + stride, xb, lb);
   }
-  for (; r < g.rows; r += stride) {
-    float xv[E];
-    float l0 = ln1[0], l1 = ln1[1], l2 = ln1[2];
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-      xv[e] = xn1[e];
-      xn1[e] = xn2[e];
-    }
-#pragma unroll
-    for (int k = 0; k < 3; ++k) ln1[k] = ln2[k];
-    fetch(r + 2 * stride, xn2, ln2);
+  // one row: xv / l0..l2 its x and router logits
+  auto row_body = [&](int64_t r, const float (&xv)[E], float l0, float l1, float l2) __attribute__((always_inline)) {
     if (!logits) {
       float hv[E];
       ld_rowc<E>(hpre + r * S::D, lane, hv);
@@ -436,6 +430,26 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_fwd_kernel(const float* 
     }
     __builtin_amdgcn_wave_barrier();  // the next row overwrites both LDS rows
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  };
+  for (; r < g.rows; r += 2 * stride) {
+    {
+      float xv[E];
+      const float l0 = la[0], l1 = la[1], l2 = la[2];
+#pragma unroll
+      for (int e = 0; e < E; ++e) xv[e] = xa[e];
+      fetch(r + 2 * stride, xa, la);
+      row_body(r, xv, l0, l1, l2);
+    }
+    const int64_t r2 = r + stride;
+    if (r2 >= g.rows) break;
+    {
+      float xv[E];
+      const float l0 = lb[0], l1 = lb[1], l2 = lb[2];
+#pragma unroll
+      for (int e = 0; e < E; ++e) xv[e] = xb[e];
+      fetch(r2 + 2 * stride, xb, lb);
+      row_body(r2, xv, l0, l1, l2);
+    }
   }
 }
 
@@ -488,7 +502,9 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_bwd_kernel(
     fetch(r, xn1, gn1, yn1, sn1);
     fetch(r + stride, xn2, gn2, yn2, sn2);
   }
-  for (; r < g.rows; r += stride) {
+  // one row from register set 1 or 2 (alternating, see abby_fwd_kernel), refilled with the row two
+  // strides ahead once its values are in LDS / locals
+  auto row_body = [&](int64_t r, float (&xs)[E], float (&gs)[E], float (&ysv)[3], int& ss) __attribute__((always_inline)) {
     float xc[E], xv[E], gv[E];  // xc: coalesced layout; xv, gv: the lane's E consecutive features
     // this row's later operands, issued now so their latency overlaps the pool work
     float hv[E], old[E];
@@ -496,22 +512,14 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_bwd_kernel(
     if (g.acc) ld_rowc<E>(dx + r * S::D, lane, old);
 #pragma unroll
     for (int j = 0; j < E / 2; ++j) {
-      xc[2 * j] = xn1[2 * j];
-      xc[2 * j + 1] = xn1[2 * j + 1];
-      *reinterpret_cast<float2*>(xr + 128 * j + 2 * lane) = make_float2(xn1[2 * j], xn1[2 * j + 1]);
-      *reinterpret_cast<float2*>(gr + 128 * j + 2 * lane) = make_float2(gn1[2 * j], gn1[2 * j + 1]);
+      xc[2 * j] = xs[2 * j];
+      xc[2 * j + 1] = xs[2 * j + 1];
+      *reinterpret_cast<float2*>(xr + 128 * j + 2 * lane) = make_float2(xs[2 * j], xs[2 * j + 1]);
+      *reinterpret_cast<float2*>(gr + 128 * j + 2 * lane) = make_float2(gs[2 * j], gs[2 * j + 1]);
     }
-    const int sel = __builtin_amdgcn_readfirstlane(sn1);
-    const float y0 = yn1[0], y1 = yn1[1], y2 = yn1[2];
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-      xn1[e] = xn2[e];
-      gn1[e] = gn2[e];
-    }
-#pragma unroll
-    for (int k = 0; k < 3; ++k) yn1[k] = yn2[k];
-    sn1 = sn2;
-    fetch(r + 2 * stride, xn2, gn2, yn2, sn2);
+    const int sel = __builtin_amdgcn_readfirstlane(ss);
+    const float y0 = ysv[0], y1 = ysv[1], y2 = ysv[2];
+    fetch(r + 2 * stride, xs, gs, ysv, ss);
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
 #pragma unroll
@@ -660,6 +668,11 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_bwd_kernel(
     accb[0] += dz0;
     accb[1] += dz1;
     accb[2] += dz2;
+  };
+  for (; r < g.rows; r += 2 * stride) {
+    row_body(r, xn1, gn1, yn1, sn1);
+    if (r + stride >= g.rows) break;
+    row_body(r + stride, xn2, gn2, yn2, sn2);
   }
   // workgroup reduction of dW2 / db2 through LDS, then one atomic per element
   __syncthreads();
@@ -764,6 +777,7 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_fwd64_kernel(const float
                                                                     const float* __restrict__ logits) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, l16 = lane & 15;
   const int64_t stride = (int64_t)gridDim.x * ABBY_WAVES * 4;
+  g.key = noise_key(g.key);
   for (int64_t r = ((int64_t)blockIdx.x * ABBY_WAVES + wid) * 4 + (lane >> 4); r < g.rows; r += stride) {
     // (rows is a multiple of nothing in particular: a 16-lane row past the end simply idles; the
     // DPP reductions never cross rows, so the live rows are unaffected)
@@ -794,7 +808,7 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_fwd64_kernel(const float
     const float cv = sd / (mabs + 1e-6f);
     float z0 = l0 + b2[0] + cv, z1 = l1 + b2[1] + cv, z2 = l2 + b2[2] + cv;
     if (g.use_noise) {  // lanes 0-2 of the 16-lane row draw one gumbel each, then broadcast in the row
-      const float gk = noise_gumbel(g.key, abby_noise_idx(g, r, l16 < 3 ? l16 : 0));
+      const float gk = noise_gumbel_k(g.key, abby_noise_idx(g, r, l16 < 3 ? l16 : 0));
       const int base = lane & 48;
       z0 += __shfl(gk, base + 0);
       z1 += __shfl(gk, base + 1);

@@ -222,17 +222,28 @@ __host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
 // keys exactly as oracle/keys.py computes them.  One copy per translation unit (no relocatable
 // device code); each noise-drawing TU exports its setter (ASRX_NOISE_EPOCH_SETTER).
 static __device__ uint32_t g_noise_epoch;
-__device__ __forceinline__ float noise_uniform(uint32_t key, uint32_t idx) {
-  const uint32_t ep = g_noise_epoch;
+// The site key with the epoch mixed in.  Row / element loops take it once before the loop: read per
+// draw, the epoch was a global load inside the loop whose wait (vmcnt counts in order) drained every
+// prefetch in flight on each row.  Read through the constant address space: a scalar load.
+__device__ __forceinline__ uint32_t noise_key(uint32_t key) {
+  const uint32_t ep = *(const __attribute__((address_space(4))) uint32_t*)&g_noise_epoch;
   if (ep != 0u) key ^= mix32(ep * 0x9E3779B9U + 0x7F4A7C15U);
+  return key;
+}
+// draws from a key already passed through noise_key
+__device__ __forceinline__ float noise_uniform_k(uint32_t key, uint32_t idx) {
   uint32_t h = mix32(mix32(idx ^ key) + (key * 0x9E3779B9U + 0x632BE5ABU));
   return ((float)(h >> 9) + 0.5f) * (1.0f / 8388608.0f);
 }
+__device__ __forceinline__ float noise_uniform(uint32_t key, uint32_t idx) {
+  return noise_uniform_k(noise_key(key), idx);
+}
 // Gumbel(0,1) sample g = -log(E), E = -log(u) ~ Exp(1).
-__device__ __forceinline__ float noise_gumbel(uint32_t key, uint32_t idx) {
-  float u = noise_uniform(key, idx);
+__device__ __forceinline__ float noise_gumbel_k(uint32_t key, uint32_t idx) {
+  float u = noise_uniform_k(key, idx);
   return -logf(-logf(u));
 }
+__device__ __forceinline__ float noise_gumbel(uint32_t key, uint32_t idx) { return noise_gumbel_k(noise_key(key), idx); }
 
 }  // namespace asrx
 

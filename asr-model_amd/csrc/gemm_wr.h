@@ -385,6 +385,9 @@ __device__ __forceinline__ void epilogue_router(const Params& p, f32x4 (&acc)[4]
 #ifndef WR_DEPTH
 #define WR_DEPTH 3  // register stages in flight (k-steps of prefetch)
 #endif
+#ifndef WR_PRIO
+#define WR_PRIO 0  // A/B switch: raise the wave's issue priority around each k-step's MFMA block
+#endif
 // DEP (template): register stages, 0 = WR_DEPTH
 
 // ABF: A is stored bf16 (M x K, lda in elements): one 16-byte chunk of 8 k per thread and k-step
@@ -707,11 +710,13 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
         const int n = wn * (32 * NJ) + nt * 16 + lr;
         b[nt] = *reinterpret_cast<const bf16x8*>(Bt + n * 64 + 16 * (lk ^ swb(n)));
       }
+      if (WR_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
           acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nt], a[mt], acc[mt][nt], 0, 0, 0);
+      if (WR_PRIO) __builtin_amdgcn_s_setprio(0);
     }
     if (s + 1 < S) store(s + 1, nxt);
     if (ce.kk == nk - 1) {

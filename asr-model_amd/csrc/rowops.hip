@@ -1213,12 +1213,13 @@ __global__ void dropout_kernel(const float* __restrict__ x, float* __restrict__ 
                                int64_t sid_base, uint32_t key, float p) {
   const int64_t total = B * T * C;
   const float sc = 1.0f / (1.0f - p);
+  key = noise_key(key);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t c = i % C;
     const int64_t t = (i / C) % T;
     const int64_t b = i / ((int64_t)T * C);
     const uint32_t idx = (uint32_t)(((sid_base + b) * C + c) * 8192 + t);
-    y[i] = noise_uniform(key, idx) >= p ? x[i] * sc : 0.f;
+    y[i] = noise_uniform_k(key, idx) >= p ? x[i] * sc : 0.f;
   }
 }
 
@@ -1250,6 +1251,7 @@ __global__ void act_dropout4_kernel(const float4* __restrict__ g, const float4* 
                                     uint32_t C4, uint32_t T, uint32_t C, uint32_t sid_base, uint32_t key, float p,
                                     int act, int act2) {
   const float sc = 1.0f / (1.0f - p);
+  key = noise_key(key);
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
     const uint32_t row = i / C4, c0 = (i - row * C4) * 4u;
     const uint32_t t = row % T, b = row / T;
@@ -1263,7 +1265,7 @@ __global__ void act_dropout4_kernel(const float4* __restrict__ g, const float4* 
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const bool keep = noise_uniform(key, base + (uint32_t)j * 8192u) >= p;
+      const bool keep = noise_uniform_k(key, base + (uint32_t)j * 8192u) >= p;
       if (BWD) {
         float gj = gg[j];
         if (act2 != ACT_NONE) gj = gj * act_grad(act2, keep ? apply_act(act, r[j]) * sc : 0.f);

@@ -15,13 +15,19 @@ prec.set_precision("bf16")
 dev = torch.device("cuda:0")
 SHAPES = [(8192, 384, 384), (8192, 384, 1536), (8192, 1536, 384), (8192, 1152, 384), (32, 128, 384),
           (192064, 384, 384), (192064, 1536, 384), (192064, 384, 1536)]
+# GEMM_SHAPES="M,N,K;M,N,K" / GEMM_NJ="3" / GEMM_ITERS / GEMM_ABF="0,1": a subset (PMC passes)
+if os.environ.get("GEMM_SHAPES"):
+    SHAPES = [tuple(int(v) for v in t.split(",")) for t in os.environ["GEMM_SHAPES"].split(";")]
+NJS = tuple(int(v) for v in os.environ.get("GEMM_NJ", "1,2,3").split(","))
+ABFS = tuple(bool(int(v)) for v in os.environ.get("GEMM_ABF", "0,1").split(","))
+ITERS = int(os.environ.get("GEMM_ITERS", "50"))
 for M, N, K in SHAPES:
-    for abf in (False, True):
+    for abf in ABFS:
         A = torch.randn(M, K, device=dev).to(torch.bfloat16 if abf else torch.float32)
         W = torch.randn(N, K, device=dev) * 0.05
         Wb = G.weight_bf16(W, cache=False)
         C = torch.empty(M, N, device=dev)
-        for nj in (1, 2, 3):
+        for nj in NJS:
             if 128 * nj > ((N + 127) // 128) * 128:
                 continue
             G._nj_override = nj
@@ -29,7 +35,7 @@ for M, N, K in SHAPES:
                 G.gemm_wn(A, Wb, C, M=M, N=N, K=K, lda=K, ldc=N)
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            n = 50
+            n = ITERS
             e0.record()
             for _ in range(n):
                 G.gemm_wn(A, Wb, C, M=M, N=N, K=K, lda=K, ldc=N)
