@@ -152,6 +152,9 @@ SIGNATURES = {
     "asrx_wgrad_bf16_ex": (_i32, [_p, _i64, _p, _i32, _i64, _p, _i64, _i64, _i64, _i64, _i64, _p]),
     "asrx_abby_fwd2": (_i32, [_p, _p, _p, _p, _p, _i32, _p, _p, _i64, _i64, _i64, _i64, _i64, _u32, _i32, _p, _p, _p,
                               _p]),
+    "asrx_rotary_table": (_i32, [_p, _p, _i64, _i64, _p]),
+    "asrx_rotary_fwd2": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _f32, _p]),
+    "asrx_rotary_bwd2": (_i32, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _f32, _p]),
     "asrx_abby_fwd3": (_i32, [_p, _p, _p, _p, _p, _p, _i32, _p, _p, _i64, _i64, _i64, _i64, _i64, _u32, _i32, _p, _p,
                                _p, _p, _p]),
     "asrx_abby_fwd_logits2": (_i32, [_p, _p, _p, _p, _i32, _p, _p, _i64, _i64, _i64, _i64, _i64, _u32, _i32, _p, _p,

@@ -784,19 +784,20 @@ class RotaryFn(torch.autograd.Function):
             m = _E(B * L, device=x.device)
             lib.call("asrx_rownorm", _P(src), _P(m), B * L, D, _S())
         y = _E(x.shape, device=x.device)
-        lib.call("asrx_rotary_fwd", _P(x), _P(m), _P(freqs), _P(y), B * L, L, D, hd, float(scale), _S())
+        tab = rotary_table(freqs, L, hd)
+        lib.call("asrx_rotary_fwd2", _P(x), _P(m), _P(freqs), _P(tab), _P(y), B * L, L, D, hd, float(scale), _S())
         ctx.hd, ctx.scale = hd, scale
-        ctx.save_for_backward(x, src, m, freqs)
+        ctx.save_for_backward(x, src, m, freqs, tab)
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        x, src, m, freqs = ctx.saved_tensors
+        x, src, m, freqs, tab = ctx.saved_tensors
         gy = _c(gy)
         B, L, D = x.shape
         dx = _E(x.shape, device=x.device)
         dm = _E(B * L, device=x.device)  # written by the kernel
-        lib.call("asrx_rotary_bwd", _P(gy), _P(x), _P(m), _P(freqs), _P(dx), _P(dm), B * L, L, D, ctx.hd,
+        lib.call("asrx_rotary_bwd2", _P(gy), _P(x), _P(m), _P(freqs), _P(tab), _P(dx), _P(dm), B * L, L, D, ctx.hd,
                  float(ctx.scale), _S())
         dsrc = None
         if ctx.needs_input_grad[1]:
@@ -807,6 +808,21 @@ class RotaryFn(torch.autograd.Function):
             lib.call("asrx_rownorm_bwd2", _P(dm), _P(src), _P(m), _P(buf), B * L, D, acc, _S())
             dsrc = None if ctx.sink is not None else buf
         return dx, dsrc, None, None, None, None, None
+
+
+_ROT_TABLES = {}
+
+
+def rotary_table(freqs, L, hd):
+    """(cos, sin) of position * freqs[j] for L positions (asrx_rotary_table), built once per (freqs, L) and kept:
+    freqs is a persistent per-(dims, heads, masked, device) tensor (model.rotary_freqs)."""
+    key = (freqs.data_ptr(), int(L), int(hd), str(freqs.device))
+    t = _ROT_TABLES.get(key)
+    if t is None:
+        t = _E(int(L), int(hd) // 2, 2, device=freqs.device)
+        lib.call("asrx_rotary_table", _P(freqs), _P(t), int(L), int(hd), _S())
+        _ROT_TABLES[key] = t
+    return t
 
 
 def rotary(x, src, freqs, hd, scale):

@@ -256,6 +256,14 @@ int asrx_rotary_fwd(const float* x, const float* m, const float* f, float* y, in
                     int64_t hd, float scale, asrx_stream_t stream);
 int asrx_rotary_bwd(const float* g, const float* x, const float* m, const float* f, float* dx, float* dm,
                     int64_t BL, int64_t L, int64_t D, int64_t hd, float scale, asrx_stream_t stream);
+/* The same with the (cos, sin) table of asrx_rotary_table (tab: L x hd/2 float2, NULL = sincosf in the
+   kernel): the angles depend only on (position, pair), so B samples x H heads share one table.  Results
+   are bit-identical to the direct form. */
+int asrx_rotary_table(const float* f, float* tab, int64_t L, int64_t hd, asrx_stream_t stream);
+int asrx_rotary_fwd2(const float* x, const float* m, const float* f, const float* tab, float* y, int64_t BL, int64_t L,
+                     int64_t D, int64_t hd, float scale, asrx_stream_t stream);
+int asrx_rotary_bwd2(const float* g, const float* x, const float* m, const float* f, const float* tab, float* dx,
+                     float* dm, int64_t BL, int64_t L, int64_t D, int64_t hd, float scale, asrx_stream_t stream);
 
 /* ---- v_gate (model.py:346-351): S = x mkey_n^T, h = mlp[0](x) pre-activation from asrx_gemm. ---- */
 int asrx_vgate_fwd(const float* S, const float* nx, const float* mval, const float* h, const float* w2,

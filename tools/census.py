@@ -43,9 +43,27 @@ pitch = synth.pitch(B)
 ids, labels = synth.text(B, 256, cfg.tokens)
 spec = torch.zeros(B, 128, 3001)
 wf = torch.zeros(B, 1, 3000)
-out = model(labels=labels, text_ids=ids, spectrogram=spec, pitch=pitch, waveform=wf)
-nf = len(calls)
-out["loss"].backward()
+from torch.profiler import ProfilerActivity, profile  # noqa: E402
+
+# torch-side device work of the step (copies, fills, cats, elementwise ops outside the library): on the
+# GPU every one of these aten ops is a kernel (or a copy / fill) launch of its own
+with profile(activities=[ProfilerActivity.CPU]) as prof:
+    out = model(labels=labels, text_ids=ids, spectrogram=spec, pitch=pitch, waveform=wf)
+    nf = len(calls)
+    out["loss"].backward()
+LAUNCHING = ("aten::copy_", "aten::fill_", "aten::zero_", "aten::cat", "aten::add_", "aten::mul", "aten::add",
+             "aten::sub", "aten::div", "aten::where", "aten::index", "aten::gather", "aten::scatter", "aten::sum",
+             "aten::mean", "aten::clamp", "aten::neg", "aten::exp", "aten::log", "aten::masked_fill_",
+             "aten::_to_copy", "aten::stack", "aten::index_put_", "aten::cumsum", "aten::ones_like",
+             "aten::zeros_like", "aten::mul_", "aten::div_", "aten::max", "aten::argmax", "aten::eq", "aten::ne",
+             "aten::lt", "aten::gt", "aten::ge", "aten::le", "aten::any", "aten::all", "aten::pow", "aten::sqrt")
+tops = collections.Counter()
+for ev in prof.key_averages():
+    if ev.key in LAUNCHING:
+        tops[ev.key] += ev.count
+print("torch ops that launch on a GPU (top-level counts include nested):", sum(tops.values()))
+for k, v in tops.most_common(20):
+    print(f"{v:6d} {k}")
 c = collections.Counter(n for n, _ in calls)
 print(f"calls fwd {nf} bwd {len(calls)-nf}")
 for n, v in c.most_common():

@@ -9,7 +9,7 @@ TAG=$1; shift
 mkdir -p $R/gpurun_out
 cd /tmp && export TMPDIR=/tmp
 B="$R/bench.py --no-cpu-baseline --no-probe --no-optimizer --no-dead-block-line --no-refpitch-line $*"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$TAG -o run --output-format csv -- python3 $B --steps 3 --warmup 1 > $R/gpurun_out/prof_$TAG.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$TAG -o run --output-format csv -- python3 $B --steps 3 --warmup 2 > $R/gpurun_out/prof_$TAG.log 2>&1
 tail -1 $R/gpurun_out/prof_$TAG.log | cut -c1-300
 if [ "$PMC" = 1 ]; then
 timeout -s KILL 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $R/gpurun_out/pmcf_$TAG -o run --output-format csv -- python3 $B --steps 1 --warmup 0 --eager > $R/gpurun_out/pmcf_$TAG.log 2>&1

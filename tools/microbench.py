@@ -158,6 +158,48 @@ def abby_bench():
         del x, h, g, dx, dh, out, outb
 
 
+def msrow_bench():
+    """MSheath layer row passes (asrx_msheath_row_fwd2 / _bwd) at the tiny config's shape (B=32 x 6002 rows, d=384,
+    M=64, Dh=192), all samples at the layer and half of them; ck = float64 checksums of the outputs."""
+    from asrx import lib
+
+    dev = torch.device("cuda:0")
+    P = lib.ptr
+    ck = lambda *ts: " ".join(f"{float(t.double().sum()):.9e}" for t in ts)  # noqa: E731
+    B, L, d, M, Dh = 32, 6002, 384, 64, 192
+    rows, N = B * L, M + Dh
+    g0 = torch.Generator(device=dev).manual_seed(5)
+    rn = lambda *s: torch.randn(*s, device=dev, generator=g0)  # noqa: E731
+    x, SH = rn(rows, d), rn(rows, N)
+    lnw, lnb, gw, gb = rn(d), rn(d), rn(d) * 0.05, rn(1)
+    mval, w2, b2, cw, cb = rn(M), rn(Dh) * 0.05, rn(1), rn(2), rn(1)
+    tx = torch.full((1,), 0.3, device=dev)
+    px = torch.empty(rows, d, device=dev)
+    sc = [torch.empty(rows, device=dev) for _ in range(7)]
+    for frac, tag in ((1.0, "all"), (0.5, "half")):
+        next_i = torch.where(torch.arange(B, device=dev) < int(B * frac), 1.0, 2.0).float()
+        fwd = lambda: lib.call("asrx_msheath_row_fwd2", P(x), P(lnw), P(lnb), P(gw), P(gb), P(SH), N, P(mval),  # noqa
+                               P(w2), P(b2), P(cw), P(cb), P(tx), P(px), 0, *[P(t) for t in sc], rows, d, M, Dh,
+                               1e-5, d ** -0.5, P(next_i), 1, L, lib.stream())
+        t = timeit(fwd)
+        nb = rows * frac * (2 * d + N) * 4
+        print(f"msheath row fwd {tag}: {t*1e6:.1f} us {nb/t/1e9:.0f} GB/s ck {ck(px, *sc)}", flush=True)
+        dpx, dg, dion = rn(rows, d), rn(rows), rn(rows)
+        dx = torch.zeros(rows, d, device=dev)
+        grads = [torch.zeros(n, device=dev) for n in (d, d, d, 1, M, Dh, 1, 2, 1, Dh)]
+        dSH = torch.empty(rows, N, device=dev)
+        bwd = lambda: lib.call("asrx_msheath_row_bwd", P(dpx), P(x), P(lnw), P(lnb), P(sc[0]), P(sc[1]), P(dg),  # noqa
+                               P(sc[3]), P(gw), P(dion), P(SH), N, P(sc[2]), P(mval), P(w2), P(cw), P(sc[5]),
+                               P(sc[6]), P(dx), P(grads[0]), P(grads[1]), P(grads[2]), P(grads[3]), P(dSH),
+                               P(grads[4]), P(grads[5]), P(grads[6]), P(grads[7]), P(grads[8]), P(grads[9]),
+                               rows, d, M, Dh, d ** -0.5, P(next_i), 1, L, lib.stream())
+        t = timeit(bwd)
+        nb = rows * frac * (4 * d + 2 * N) * 4
+        dx.zero_()
+        bwd()
+        print(f"msheath row bwd {tag}: {t*1e6:.1f} us {nb/t/1e9:.0f} GB/s ck {ck(dx, dSH)}", flush=True)
+
+
 def attn_bench():
     from asrx import ops, prec
 
@@ -232,3 +274,5 @@ if __name__ == "__main__":
         abby_bench()
     if "norm" in what:
         norm_bench()
+    if "msrow" in what:
+        msrow_bench()
