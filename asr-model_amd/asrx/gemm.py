@@ -203,6 +203,41 @@ def gemm_wn(A, Wb, C, *, M, N, K, lda, ldc, bias=None, Z=None, alpha=1.0, beta=0
     return C
 
 
+RECOMPUTE_ACT = True  # Linear + act in perf mode: the backward recomputes the pre-activation (gemm_wn_gact)
+
+
+def can_recompute_act(x, W, act):
+    """True when Linear(x, W) + act may skip storing its pre-activation: perf mode, gelu / silu / sigmoid, and
+    the shape the activation-gradient GEMM covers (the forward's tile width nj = 3, aligned rows)."""
+    if not RECOMPUTE_ACT or act not in ("gelu", "silu", "sigmoid") or not x.is_cuda:
+        return False
+    N, K = W.shape[0], W.shape[-1] if W.dim() == 2 else W.numel() // W.shape[0]
+    M = x.numel() // max(K, 1)
+    return (use_wide(K) and use_wide(N) and N % 8 == 0 and M > 0 and _nj(M, N) == 3
+            and (not is_bf16(x) or K % 8 == 0))
+
+
+def linear_gact(x, W, b, gy, gz, act, db=None):
+    """gz (bf16, gy's shape) = gy * act'(x W^T + b), the pre-activation recomputed by the GEMM; db (fp32, N)
+    += column sums of gz when given.  x as the forward saw it (fp32 or bf16-stored)."""
+    x2 = _rows(x)
+    if not x2.is_contiguous():
+        x2 = x2.contiguous()
+    M, K = x2.shape
+    N = W.shape[0]
+    Wb = weight_bf16(W.view(N, -1))
+    g2 = gy.reshape(M, N)
+    if g2.dtype != torch.float32 or not g2.is_contiguous():
+        g2 = g2.float().contiguous()
+    nj = _nj(M, N)
+    lib.require_gpu(x2, Wb, g2, gz)
+    e0 = probe.begin("gemm")
+    lib.call("asrx_gemm_wn_gact", lib.ptr(x2), int(is_bf16(x2)), K, lib.ptr(Wb), Wb.stride(0), lib.ptr(b),
+             lib.ptr(g2), N, lib.ptr(gz), N, lib.ptr(db), M, N, K, ACT[act], nj, lib.stream())
+    probe.end("gemm", e0, 2.0 * M * N * K, ("gact", M, N, K, nj, act, int(is_bf16(x2))))
+    return gz
+
+
 def router_fwd(x2, W1, b1, W2, keep_hpre):
     """AbbyNormal router in one GEMM pass: (hpre or None, logits (M, 3) without b2)."""
     M, K = x2.shape

@@ -152,6 +152,8 @@ SIGNATURES = {
     "asrx_wgrad_bf16_ex": (_i32, [_p, _i64, _p, _i32, _i64, _p, _i64, _i64, _i64, _i64, _i64, _p]),
     "asrx_abby_fwd2": (_i32, [_p, _p, _p, _p, _p, _i32, _p, _p, _i64, _i64, _i64, _i64, _i64, _u32, _i32, _p, _p, _p,
                               _p]),
+    "asrx_gemm_wn_gact": (_i32, [_p, _i32, _i64, _p, _i64, _p, _p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i32, _i32,
+                                 _p]),
     "asrx_rotary_table": (_i32, [_p, _p, _i64, _i64, _p]),
     "asrx_rotary_fwd2": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _f32, _p]),
     "asrx_rotary_bwd2": (_i32, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _f32, _p]),
@@ -199,6 +201,8 @@ def load() -> ctypes.CDLL:
             )
         lib = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("ASRX_LIB") and not hasattr(lib, name):
+                continue  # an older A/B build lacks entry points added since: bind what it has
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args

@@ -261,26 +261,35 @@ class Linear(torch.autograd.Function):
         ctx.set_materialize_grads(False)
         # the pre-activation is kept only for a backward that will run (none in the reference's dead
         # blocks, eval or decoding: an N-wide fp32 write saved per call)
-        z = _E(*x.shape[:-1], W.shape[0], device=x.device) if act != "none" and grad else None
+        # perf mode: the backward's GEMM recomputes the pre-activation (gemm_wn_gact) instead of reading it
+        ctx.recompute = grad and G.can_recompute_act(x, W, act)
+        z = _E(*x.shape[:-1], W.shape[0], device=x.device) if act != "none" and grad and not ctx.recompute else None
         y = G.linear_fwd(x, W.view(W.shape[0], -1), b, act=act, preact=z,  # (N, K, 1): a 1x1 Conv1d weight
                          out_bf16=out_bf16 and prec.bf16_storage())
         ctx.act = act
         ctx.has_b = b is not None
         if grad:
             ctx.dW, ctx.db = _direct(ctx, 1, W), _direct(ctx, 2, b)
-            ctx.save_for_backward(x, W, z, b if ctx.db else None)
+            # the bias itself (not only its gradient target) when the backward recomputes z = x W^T + b
+            ctx.save_for_backward(x, W, z, b if (ctx.db or ctx.recompute) else None)
         return y
 
     @staticmethod
     def backward(ctx, gy):
         x, W3, z, b = ctx.saved_tensors
         W = W3.view(W3.shape[0], -1)
+        ctx.bias_t = b if ctx.has_b else None
         gy = grad_in(gy, ctx.osink)
         if gy is None:
             return None, None, None, None, None, None, None, None
         db_done = None
         N = gy.shape[-1]
-        if ctx.act in ("gelu", "silu", "sigmoid") and prec.get() == prec.PREC_BF16 and N % 8 == 0 and G.use_wide(N):
+        if ctx.recompute:
+            gz = _E(gy.shape, dtype=torch.bfloat16, device=gy.device)
+            if ctx.has_b and ctx.needs_input_grad[2]:
+                db_done = _gbuf(b, True) if ctx.db else torch.zeros(N, device=gy.device)
+            G.linear_gact(x, W, ctx.bias_t, _c(gy), gz, ctx.act, db=db_done)
+        elif ctx.act in ("gelu", "silu", "sigmoid") and prec.get() == prec.PREC_BF16 and N % 8 == 0 and G.use_wide(N):
             # perf mode: act' applied, gz stored bf16 for the two GEMMs and the bias gradient summed in
             # the same pass (no fp32 gz round trip, no separate column-sum pass)
             gz = _E(gy.shape, dtype=torch.bfloat16, device=gy.device)

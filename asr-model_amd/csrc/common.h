@@ -61,7 +61,11 @@ namespace asrx {
 __device__ __forceinline__ float gelu_f(float x) {  // exact (erf) GELU, nn.GELU() default
   return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
 }
+// The activation derivatives are written without contractions in every translation unit (the row-kernel
+// units build with -ffp-contract=off, the GEMM units do not): the backward's activation-gradient GEMM
+// epilogue and asrx_act_bwd_bias then round identically.
 __device__ __forceinline__ float gelu_grad(float x) {
+#pragma clang fp contract(off)
   float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
   float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
   return cdf + x * pdf;
@@ -70,6 +74,7 @@ __device__ __forceinline__ float gelu_grad(float x) {
 __device__ __forceinline__ float sigmoid_f(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 __device__ __forceinline__ float silu_f(float x) { return x * sigmoid_f(x); }
 __device__ __forceinline__ float silu_grad(float x) {
+#pragma clang fp contract(off)
   float s = sigmoid_f(x);
   return s * (1.0f + x * (1.0f - s));
 }

@@ -200,6 +200,30 @@ extern "C" int asrx_gemm_wn_res(const float* A, int64_t lda, const unsigned shor
   ASRX_LAUNCHED("asrx_gemm_wn_res");
 }
 
+// Backward of y = act(A W^T + bias) (act gelu / silu / sigmoid) without a stored pre-activation: the GEMM
+// recomputes z = A W^T + bias with the forward's tile width (nj 3 only: the instantiation the forward's
+// shapes use) and writes gz = bf16(G * act'(z)) (M x N, ldc) from the output gradient G (fp32, ldg), adding
+// the column sums of gz into db when non-null.  A fp32 (a_bf16 = 0) or bf16 (1).
+extern "C" int asrx_gemm_wn_gact(const void* A, int a_bf16, int64_t lda, const unsigned short* W, int64_t ldw,
+                                 const float* bias, const float* G, int64_t ldg, unsigned short* gz, int64_t ldc,
+                                 float* db, int64_t M, int64_t N, int64_t K, int act, int nj, hipStream_t stream) {
+  ASRX_REQUIRE(M > 0 && N > 0 && K > 0, "asrx_gemm_wn_gact: empty problem");
+  ASRX_REQUIRE(nj == 3, "asrx_gemm_wn_gact: nj 3 only");
+  ASRX_REQUIRE(act == ACT_GELU || act == ACT_SILU || act == ACT_SIGMOID, "asrx_gemm_wn_gact: gelu/silu/sigmoid only");
+  ASRX_REQUIRE(((uintptr_t)A & 15) == 0 && ((uintptr_t)W & 15) == 0 && ((uintptr_t)G & 15) == 0 &&
+                   ((uintptr_t)gz & 7) == 0,
+               "asrx_gemm_wn_gact: A/W/G 16-byte, gz 8-byte aligned");
+  ASRX_REQUIRE(K % 8 == 0 && lda % (a_bf16 ? 8 : 4) == 0 && ldw % 8 == 0 && N % 4 == 0 && ldc % 4 == 0 &&
+                   ldg % 4 == 0,
+               "asrx_gemm_wn_gact: K, ldw %% 8; lda %% 4 (8 bf16); N, ldc, ldg %% 4");
+  ASRX_REQUIRE(M * lda < (1LL << 31) && N * ldw < (1LL << 31), "asrx_gemm_wn_gact: operand spans >= 2^31 elements");
+  wn::Params p{(const float*)A, (int)lda, W, (int)ldw, nullptr, (int)ldc, bias, nullptr, (int)M, (int)N, (int)K, 1,
+               1, 1.f, 0.f, act, nullptr, nullptr, nullptr, nullptr, gz, nullptr, 0, nullptr, 0, G, (int)ldg, db};
+  if (a_bf16) wn::launch_wr<3, false, false, true, false, false, true>(p, stream);
+  else wn::launch_wr<3, false, false, false, false, false, true>(p, stream);
+  ASRX_LAUNCHED("asrx_gemm_wn_gact");
+}
+
 // asrx_gemm_wn restricted to the BM-row tiles listed in mtiles (n_mtiles entries, both on the device,
 // from asrx_row_tiles); rows of other tiles are not written.
 extern "C" int asrx_gemm_wn_rows(const float* A, int64_t lda, const unsigned short* W, int64_t ldw, float* C,

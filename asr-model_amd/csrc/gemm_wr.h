@@ -66,6 +66,13 @@ struct Params {
   // around an out projection (model.py:578-580 x = x + attn(...)) without a separate add pass
   const float* Rres;
   int ldr;
+  // activation-gradient epilogue (gemm_wr_kernel<..., GA>): the GEMM recomputes the pre-activation
+  // z = alpha A W^T + bias of a Linear + act whose forward did not keep it, and stores
+  // gz = bf16(G * act'(z)) to Cb (G: the output gradient, fp32, row stride ldg) with the bias gradient's
+  // column sums of gz added into dB (nullable) -- the backward never reads a stored z
+  const float* G;
+  int ldg;
+  float* dB;
 };
 
 __device__ __forceinline__ void st_bf16x4(unsigned short* dst, float a, float b, float c, float d) {
@@ -221,6 +228,79 @@ __device__ __forceinline__ void epilogue_lds(const Params& p, f32x4 (&acc)[4][2 
                                   reinterpret_cast<f32x4*>(dst));
     }
     __builtin_amdgcn_wave_barrier();  // the next slice overwrites the slab
+  }
+}
+
+// Activation-gradient epilogue (Params::G): slab = z (as epilogue_lds stages it, so z is bit-identical to
+// the pre-activation the forward would have stored), then per coalesced float4: o = G * act'(z) (the
+// arithmetic of rowops.hip act_bwd_bias_kernel, up to the compiler's contractions), bf16 o to Cb and fp32
+// o back into the slab (0 outside M x N); each lane then sums columns lane, lane + 64 of the slice and
+// keeps the partials over the tile's 4 slices; one atomicAdd per column and wave into dB at the end.
+template <int ACT>
+__device__ __forceinline__ float dact_t(float v) {
+  if constexpr (ACT == ACT_GELU) return gelu_grad(v);
+  else if constexpr (ACT == ACT_SILU) return silu_grad(v);
+  else {
+    const float sg = sigmoid_f(v);
+    return sg * (1.f - sg);
+  }
+}
+template <int NJ, int ACT>
+__device__ __forceinline__ void epilogue_gact(const Params& p, f32x4 (&acc)[4][2 * NJ], const float* bsl, int m0,
+                                              int n0, int wm, int wn, int lr, int lk, float* ep) {
+  constexpr int NT = 2 * NJ, W = EpLds<NJ>::W, LD = EpLds<NJ>::LD, W4 = W / 4;
+  constexpr int PER = 16 * W4 / 64;
+  constexpr int CS = (W + 63) / 64;  // column-sum slots per lane
+  const int lane = threadIdx.x & 63;
+  const int cbase = n0 + wn * W;
+  float csum[CS];
+#pragma unroll
+  for (int i = 0; i < CS; ++i) csum[i] = 0.f;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int nl = nt * 16 + 4 * lk;
+      float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (p.bias) bv = *reinterpret_cast<const float4*>(bsl + wn * W + nl);
+      *reinterpret_cast<float4*>(ep + lr * LD + nl) =
+          make_float4(p.alpha * acc[mt][nt][0] + bv.x, p.alpha * acc[mt][nt][1] + bv.y,
+                      p.alpha * acc[mt][nt][2] + bv.z, p.alpha * acc[mt][nt][3] + bv.w);
+    }
+    __builtin_amdgcn_wave_barrier();
+    const int rbase = m0 + wm * 64 + mt * 16;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int f = j * 64 + lane, r = f / W4, c = 4 * (f % W4);
+      float* sl = ep + r * LD + c;
+      const float4 z = *reinterpret_cast<const float4*>(sl);
+      const int row = rbase + r, col = cbase + c;
+      float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (row < p.M && col < p.N) {
+        const float4 g = *reinterpret_cast<const float4*>(p.G + (int64_t)row * p.ldg + col);
+        o = make_float4(g.x * dact_t<ACT>(z.x), g.y * dact_t<ACT>(z.y), g.z * dact_t<ACT>(z.z),
+                        g.w * dact_t<ACT>(z.w));
+        st_bf16x4(p.Cb + (int64_t)row * p.ldc + col, o.x, o.y, o.z, o.w);
+      }
+      *reinterpret_cast<float4*>(sl) = o;
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int i = 0; i < CS; ++i) {
+      const int cc = lane + 64 * i;
+      if (cc < W) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) csum[i] += ep[r * LD + cc];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // the next slice overwrites the slab
+  }
+  if (p.dB) {
+#pragma unroll
+    for (int i = 0; i < CS; ++i) {
+      const int cc = lane + 64 * i;
+      if (cc < W && cbase + cc < p.N) atomicAdd(p.dB + cbase + cc, csum[i]);
+    }
   }
 }
 
@@ -384,9 +464,6 @@ __device__ __forceinline__ void epilogue_router(const Params& p, f32x4 (&acc)[4]
 #endif
 #ifndef WR_DEPTH
 #define WR_DEPTH 3  // register stages in flight (k-steps of prefetch)
-#endif
-#ifndef WR_PRIO
-#define WR_PRIO 0  // A/B switch: raise the wave's issue priority around each k-step's MFMA block
 #endif
 // DEP (template): register stages, 0 = WR_DEPTH
 
@@ -560,7 +637,8 @@ __device__ __forceinline__ void wr_store64(const WrStage64<ABF>& st, char* At, c
   }
 }
 
-template <int NJ, bool CONV, bool RT, int DEP = 0, bool ABF = false, bool CE = false, bool RES = false>
+template <int NJ, bool CONV, bool RT, int DEP = 0, bool ABF = false, bool CE = false, bool RES = false,
+          bool GA = false>
 __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) {  // ntiles: all tiles
   typedef Cfg<NJ> CF;
   constexpr int BN = CF::BN, NT = 2 * NJ, BNR = CF::BNR;
@@ -710,13 +788,11 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
         const int n = wn * (32 * NJ) + nt * 16 + lr;
         b[nt] = *reinterpret_cast<const bf16x8*>(Bt + n * 64 + 16 * (lk ^ swb(n)));
       }
-      if (WR_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
           acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nt], a[mt], acc[mt][nt], 0, 0, 0);
-      if (WR_PRIO) __builtin_amdgcn_s_setprio(0);
     }
     if (s + 1 < S) store(s + 1, nxt);
     if (ce.kk == nk - 1) {
@@ -728,6 +804,12 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
         epilogue_ce<NJ>(p, acc, m0, n0, wm, wn, lr, lk, ep, reinterpret_cast<float2*>(red));
       } else if constexpr (RES) {  // act none, vec_ok (checked by the launcher)
         epilogue_lds<NJ, ACT_NONE, true>(p, acc, bsl, m0, n0, wm, wn, lr, lk, ep);
+      } else if constexpr (GA) {  // gelu / silu / sigmoid (checked by the launcher)
+        switch (p.act) {
+          case ACT_GELU: epilogue_gact<NJ, ACT_GELU>(p, acc, bsl, m0, n0, wm, wn, lr, lk, ep); break;
+          case ACT_SILU: epilogue_gact<NJ, ACT_SILU>(p, acc, bsl, m0, n0, wm, wn, lr, lk, ep); break;
+          default: epilogue_gact<NJ, ACT_SIGMOID>(p, acc, bsl, m0, n0, wm, wn, lr, lk, ep); break;
+        }
       } else if (WR_EPI_LDS && vec) switch (p.act) {
         case ACT_GELU: epilogue_lds<NJ, ACT_GELU>(p, acc, bsl, m0, n0, wm, wn, lr, lk, ep); break;
         case ACT_SILU: epilogue_lds<NJ, ACT_SILU>(p, acc, bsl, m0, n0, wm, wn, lr, lk, ep); break;
@@ -777,10 +859,10 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
 template <bool ABF>
 constexpr int wr_dep() { return 0; }
 
-template <int NJ, bool CONV, bool RT = false, bool ABF = false, bool CE = false, bool RES = false>
+template <int NJ, bool CONV, bool RT = false, bool ABF = false, bool CE = false, bool RES = false, bool GA = false>
 void launch_wr(const Params& p, hipStream_t s) {
   static int resident = 0;
-  const void* fn = (const void*)gemm_wr_kernel<NJ, CONV, RT, wr_dep<ABF>(), ABF, CE, RES>;
+  const void* fn = (const void*)gemm_wr_kernel<NJ, CONV, RT, wr_dep<ABF>(), ABF, CE, RES, GA>;
   if (!resident) {
     int per_cu = 0, dev = 0, cus = 0;
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, NTHR, 0);
@@ -792,7 +874,7 @@ void launch_wr(const Params& p, hipStream_t s) {
   const int grid = std::min(tiles, resident);
   // a 5-deep pipeline (DEP = 5) for the one-wave 8192-row text-side launches measured 32.4 us vs
   // 30.1 us at depth 3 (profiles/r02_bench_v8_kernel_stats.csv): their time is not load latency
-  gemm_wr_kernel<NJ, CONV, RT, wr_dep<ABF>(), ABF, CE, RES><<<grid, NTHR, 0, s>>>(p, tiles);
+  gemm_wr_kernel<NJ, CONV, RT, wr_dep<ABF>(), ABF, CE, RES, GA><<<grid, NTHR, 0, s>>>(p, tiles);
 }
 
 }  // namespace wn
@@ -804,10 +886,12 @@ void launch_wr(const Params& p, hipStream_t s) {
 #define ASRX_WR_DECL(NJ, CONV, RT, ABF) extern template void asrx::wn::launch_wr<NJ, CONV, RT, ABF>(const asrx::wn::Params&, hipStream_t);
 #define ASRX_WR_DECL_CE(NJ) extern template void asrx::wn::launch_wr<NJ, false, false, true, true>(const asrx::wn::Params&, hipStream_t);
 #define ASRX_WR_DECL_RES(NJ) extern template void asrx::wn::launch_wr<NJ, false, false, false, false, true>(const asrx::wn::Params&, hipStream_t);
+#define ASRX_WR_DECL_GA(NJ, ABF) extern template void asrx::wn::launch_wr<NJ, false, false, ABF, false, false, true>(const asrx::wn::Params&, hipStream_t);
 #else
 #define ASRX_WR_DECL(NJ, CONV, RT, ABF) template void asrx::wn::launch_wr<NJ, CONV, RT, ABF>(const asrx::wn::Params&, hipStream_t);
 #define ASRX_WR_DECL_CE(NJ) template void asrx::wn::launch_wr<NJ, false, false, true, true>(const asrx::wn::Params&, hipStream_t);
 #define ASRX_WR_DECL_RES(NJ) template void asrx::wn::launch_wr<NJ, false, false, false, false, true>(const asrx::wn::Params&, hipStream_t);
+#define ASRX_WR_DECL_GA(NJ, ABF) template void asrx::wn::launch_wr<NJ, false, false, ABF, false, false, true>(const asrx::wn::Params&, hipStream_t);
 #endif
 #define ASRX_WR_SET(NJ) ASRX_WR_DECL(NJ, false, false, false) ASRX_WR_DECL(NJ, true, false, false) \
   ASRX_WR_DECL(NJ, false, false, true) ASRX_WR_DECL(NJ, true, false, true) ASRX_WR_DECL(NJ, false, true, false)
@@ -820,4 +904,6 @@ ASRX_WR_DECL_CE(2)
 ASRX_WR_DECL_CE(3)
 ASRX_WR_DECL_RES(1)
 ASRX_WR_DECL_RES(3)
+ASRX_WR_DECL_GA(3, false)
+ASRX_WR_DECL_GA(3, true)
 #endif

@@ -2420,7 +2420,7 @@ int asrx_msheath_row_bwd(const float* dpx, const float* x, const float* lnw, con
              L > 0 ? L : 1};
   const size_t nb = next_i ? (size_t)((rows + p.L - 1) / p.L) : 0;  // + the next_i copy
   const size_t shm = ((size_t)RW * (3 * d + M + 2 * Dh + 5) + nb) * sizeof(float);
-  ASRX_REQUIRE(shm <= 64 * 1024, "msheath_row_bwd: %ld samples exceed the LDS budget", (long)nb);
+  ASRX_REQUIRE(shm <= 160 * 1024, "msheath_row_bwd: %ld samples exceed the LDS budget", (long)nb);
   MS_DISPATCH(msheath_row_bwd_kernel, row_grid(rows, 1024), shm, p);
   ASRX_LAUNCHED("asrx_msheath_row_bwd");
 }

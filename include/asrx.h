@@ -517,6 +517,13 @@ int asrx_ce_bwd_f32in(const float* zf, const int64_t* labels, const float* lse, 
                       unsigned short* dzb, int64_t rows, int64_t V, asrx_stream_t stream);
 /* out projection with its residual add (model.py:578-580): C = R + A W^T + bias; A, C, R fp32, R != C,
  * 16-byte aligned rows, nj 1 or 3. */
+/* Backward of y = act(A W^T + bias), act gelu (1) / silu (2) / sigmoid (3), whose forward kept no pre-activation:
+   the GEMM recomputes z with the forward's tile width (nj 3) and writes gz = bf16(G * act'(z)) (M x N, ldc) from
+   the output gradient G (fp32, row stride ldg), adding gz's column sums into db when non-NULL.  A fp32
+   (a_bf16 = 0) or bf16 (1).  Replaces storing z in the forward and re-reading it (asrx_act_bwd_bias). */
+int asrx_gemm_wn_gact(const void* A, int a_bf16, int64_t lda, const unsigned short* W, int64_t ldw, const float* bias,
+                      const float* G, int64_t ldg, unsigned short* gz, int64_t ldc, float* db, int64_t M, int64_t N,
+                      int64_t K, int act, int nj, asrx_stream_t stream);
 int asrx_gemm_wn_res(const float* A, int64_t lda, const unsigned short* W, int64_t ldw, float* C, int64_t ldc,
                      const float* bias, const float* R, int64_t ldr, int64_t M, int64_t N, int64_t K, int nj,
                      asrx_stream_t stream);

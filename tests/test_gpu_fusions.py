@@ -44,6 +44,47 @@ def test_linear_residual_matches_add(cuda, M, N, K, fused_expected):
 
 
 @pytest.mark.parametrize("act", ["gelu", "silu", "sigmoid"])
+@pytest.mark.parametrize("M,N,K,abf", [(20000, 1536, 384, True), (9001, 1152, 384, False), (7000, 1536, 384, True)])
+def test_linear_act_recomputed_preact_matches_stored(cuda, act, M, N, K, abf):
+    """Linear + act in perf mode with the pre-activation recomputed by the backward's GEMM (gemm_wn_gact)
+    against the stored-pre-activation path (asrx_act_bwd_bias): the forward is the same launch without the
+    z store (bit-identical y); the recomputed z equals the stored one bit for bit (same tiles, same MFMA
+    order), so dx / dW match within the compilers' contraction differences of act' (<= 1e-5 of max) and the
+    bias gradient (column-sum order differs) within 1e-5 of the column sums of |gz|."""
+    from asrx import gemm as G
+    from asrx import ops, prec
+
+    assert G._nj(M, N) == 3
+    g = torch.Generator().manual_seed(M + N + K)
+    x = torch.randn(M, K, generator=g).to(cuda)
+    if abf:
+        x = x.to(torch.bfloat16)
+    W = (torch.randn(N, K, generator=g) * 0.05).to(cuda)
+    b = (torch.randn(N, generator=g) * 0.1).to(cuda)
+    gy = torch.randn(M, N, generator=g).to(cuda)
+    res = []
+    try:
+        for rec in (True, False):
+            G.RECOMPUTE_ACT = rec
+            xx = x.clone().requires_grad_(not abf)
+            WW = W.clone().requires_grad_(True)
+            bb = b.clone().requires_grad_(True)
+            with prec.precision("bf16"):
+                y = ops.linear(xx, WW, bb, act=act)
+                assert y.grad_fn is not None
+                y.backward(gy)
+            res.append((y.detach(), None if abf else xx.grad, WW.grad, bb.grad))
+    finally:
+        G.RECOMPUTE_ACT = True
+    assert torch.equal(res[0][0], res[1][0])
+    for a, c in zip(res[0][1:3], res[1][1:3]):
+        if a is not None:
+            assert float((a - c).abs().max() / c.abs().max()) < 1e-5
+    gabs = (gy * 1.2).abs().sum(0)  # |act'| <= 1.13 (gelu), 1.1 (silu), 0.25 (sigmoid)
+    assert float(((res[0][3] - res[1][3]).abs() / gabs.clamp_min(1e-30)).max()) < 1e-5
+
+
+@pytest.mark.parametrize("act", ["gelu", "silu", "sigmoid"])
 @pytest.mark.parametrize("rows,N", [(5000, 1536), (333, 1152), (64, 384)])
 def test_act_bwd_bias_matches_unfused(cuda, act, rows, N):
     from asrx import lib, ops
