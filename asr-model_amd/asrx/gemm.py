@@ -204,12 +204,18 @@ def gemm_wn(A, Wb, C, *, M, N, K, lda, ldc, bias=None, Z=None, alpha=1.0, beta=0
 
 
 RECOMPUTE_ACT = True  # Linear + act in perf mode: the backward recomputes the pre-activation (gemm_wn_gact)
+# Measured per forward + backward (tools/microbench.py gact, profiles/r04_gact_micro.txt): SiLU at
+# 192064 x 1536 1602 -> 1531 us and 8192 x 1536 147 -> 139 us, but 96000 x 1536 715 -> 759 us; GELU at
+# 192064 x 1152 1200 -> 1264 us (erf and exp inside the one-workgroup-per-CU GEMM's epilogue hold the
+# MFMA pipeline).  The recompute saves the pre-activation's HBM round trip (2 x 4 bytes per element) but is
+# time-neutral overall, so it is used for SiLU / sigmoid and not for GELU.
+RECOMPUTE_ACTS = ("silu", "sigmoid")
 
 
 def can_recompute_act(x, W, act):
-    """True when Linear(x, W) + act may skip storing its pre-activation: perf mode, gelu / silu / sigmoid, and
+    """True when Linear(x, W) + act may skip storing its pre-activation: perf mode, silu / sigmoid, and
     the shape the activation-gradient GEMM covers (the forward's tile width nj = 3, aligned rows)."""
-    if not RECOMPUTE_ACT or act not in ("gelu", "silu", "sigmoid") or not x.is_cuda:
+    if not RECOMPUTE_ACT or act not in RECOMPUTE_ACTS or not x.is_cuda:
         return False
     N, K = W.shape[0], W.shape[-1] if W.dim() == 2 else W.numel() // W.shape[0]
     M = x.numel() // max(K, 1)

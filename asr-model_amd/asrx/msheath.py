@@ -170,7 +170,9 @@ def forward(mod, x0, gpol, save, tag=None):
     lib.call("asrx_layernorm_fwd3", _P(x), _P(mod.mlp_ln.weight), _P(mod.mlp_ln.bias), _P(hln), hb, _P(mean2),
              _P(rstd2), None, _P(mod.mlp_gate[0].weight), _P(mod.mlp_gate[0].bias), _P(gate), 1, rows, D,
              float(mod.mlp_ln.eps), st)
-    z1 = _E(B, L, mod.mlp[0].weight.shape[0], device=dev) if save else None
+    # perf mode: the backward's GEMM recomputes mlp[0]'s pre-activation (gemm_wn_gact) -- no z1 store
+    rec1 = save and G.can_recompute_act(hln, mod.mlp[0].weight, "silu")
+    z1 = _E(B, L, mod.mlp[0].weight.shape[0], device=dev) if save and not rec1 else None
     a1 = G.linear_fwd(hln, mod.mlp[0].weight, mod.mlp[0].bias, act="silu", preact=z1,
                       out_bf16=prec.bf16_storage())
     hh = G.linear_fwd(a1, mod.mlp[2].weight, mod.mlp[2].bias)
@@ -219,7 +221,11 @@ class MSheathFn(torch.autograd.Function):
         da1 = G.linear_dgrad(dhh, m2l.weight)
         G.linear_wgrad(dhh, sv["a1"], out=gb(m2l.weight), accumulate=True, db=gb(m2l.bias))
         H1 = da1.shape[-1]
-        if prec.get() == prec.PREC_BF16 and H1 % 8 == 0 and G.use_wide(H1):
+        if sv["z1"] is None:  # pre-activation recomputed: gz = bf16(da1 * silu'(hln W0^T + b0)), db0 summed
+            ga1 = _E(da1.shape, dtype=torch.bfloat16, device=dev)
+            G.linear_gact(sv["hln"], m0.weight, m0.bias, da1, ga1, "silu", db=gb(m0.bias))
+            da1 = ga1
+        elif prec.get() == prec.PREC_BF16 and H1 % 8 == 0 and G.use_wide(H1):
             # perf mode: silu' applied, the gradient stored bf16 for both GEMMs, mlp[0]'s bias gradient
             # summed in the same pass
             ga1 = _E(da1.shape, dtype=torch.bfloat16, device=dev)

@@ -417,12 +417,25 @@ __global__ __launch_bounds__(64 * RW) void rotary_fwd_kernel(const float* __rest
     const float mm = m[r] * scale;
     const float2* xr = reinterpret_cast<const float2*>(x + r * D);
     float2* yr = reinterpret_cast<float2*>(y + r * D);
-    for (int p = lane; p < D / 2; p += 64) {
-      const int j = p % half;
-      float sn, cs;
-      rot_cs(f, tab, lpos, j, half, cs, sn);
-      const float2 v = xr[p];
-      yr[p] = make_float2(mm * (v.x * cs - v.y * sn), mm * (v.x * sn + v.y * cs));
+    // the row's pairs in groups of four per lane, every load of a group issued before any use (one pair
+    // per loop trip exposed a full load latency per pair)
+    for (int p0 = lane; p0 < D / 2; p0 += 256) {
+      float2 v[4], t[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int p = p0 + 64 * u;
+        const int pc = p < D / 2 ? p : p0;
+        v[u] = xr[pc];
+        float sn, cs;
+        rot_cs(f, tab, lpos, pc % half, half, cs, sn);
+        t[u] = make_float2(cs, sn);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int p = p0 + 64 * u;
+        const float cs = t[u].x, sn = t[u].y;
+        if (p < D / 2) yr[p] = make_float2(mm * (v[u].x * cs - v[u].y * sn), mm * (v[u].x * sn + v[u].y * cs));
+      }
     }
   }
 }
@@ -442,13 +455,26 @@ __global__ __launch_bounds__(64 * RW) void rotary_bwd_kernel(const float* __rest
     const float2* gr = reinterpret_cast<const float2*>(g + r * D);
     float2* dxr = reinterpret_cast<float2*>(dx + r * D);
     float acc = 0.f;
-    for (int p = lane; p < D / 2; p += 64) {
-      const int j = p % half;
-      float sn, cs;
-      rot_cs(f, tab, lpos, j, half, cs, sn);
-      const float2 v = xr[p], gg = gr[p];
-      dxr[p] = make_float2(mm * (gg.x * cs + gg.y * sn), mm * (-gg.x * sn + gg.y * cs));
-      acc += gg.x * (v.x * cs - v.y * sn) + gg.y * (v.x * sn + v.y * cs);
+    for (int p0 = lane; p0 < D / 2; p0 += 256) {  // groups of four pairs, loads first (rotary_fwd_kernel)
+      float2 v[4], gg[4], t[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int p = p0 + 64 * u;
+        const int pc = p < D / 2 ? p : p0;
+        v[u] = xr[pc];
+        gg[u] = gr[pc];
+        float sn, cs;
+        rot_cs(f, tab, lpos, pc % half, half, cs, sn);
+        t[u] = make_float2(cs, sn);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int p = p0 + 64 * u;
+        if (p >= D / 2) continue;
+        const float cs = t[u].x, sn = t[u].y;
+        dxr[p] = make_float2(mm * (gg[u].x * cs + gg[u].y * sn), mm * (-gg[u].x * sn + gg[u].y * cs));
+        acc += gg[u].x * (v[u].x * cs - v[u].y * sn) + gg[u].y * (v[u].x * sn + v[u].y * cs);
+      }
     }
     acc = wave_sum(acc) * scale;
     if (lane == 0) dm[r] = acc;  // written (one wave owns a row): no zero-filled dm needed

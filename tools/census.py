@@ -76,3 +76,13 @@ for n, a in calls:
         g[("gemm", a[16], a[17], a[18], a[19], a[4], a[9])] += 1  # M N K batch a_kc b_kc
 for k, v in sorted(g.items(), key=lambda kv: -kv[1] * kv[0][1] * kv[0][2] * kv[0][3]):
     print(v, k)
+ge = collections.Counter()
+for n, a in calls:
+    if n == "asrx_gemm_wn_ex" and a[18] != 0:
+        ge[("wn_ex act", a[13], a[14], a[15], a[18], "Z" if a[12] else "-", "ab" if a[1] else "a32")] += 1
+    elif n == "asrx_act_bwd_bias":
+        ge[("act_bwd_bias", a[4], a[5], a[6])] += 1
+    elif n == "asrx_gemm_wn_gact":
+        ge[("gact", a[11], a[12], a[13], a[14])] += 1
+for k, v in sorted(ge.items(), key=lambda kv: -kv[1]):
+    print(v, k)

@@ -200,6 +200,31 @@ def msrow_bench():
         print(f"msheath row bwd {tag}: {t*1e6:.1f} us {nb/t/1e9:.0f} GB/s ck {ck(dx, dSH)}", flush=True)
 
 
+def gact_bench():
+    """Linear + act forward and backward in perf mode with the pre-activation stored (asrx_act_bwd_bias) or
+    recomputed by the backward's GEMM (asrx_gemm_wn_gact), at the model's MLP shapes."""
+    from asrx import gemm as G
+    from asrx import ops, prec
+
+    ops.DIRECT = False  # torch.autograd.grad over parameters below
+    dev = torch.device("cuda:0")
+    for M, N, act in ((192064, 1536, "silu"), (192064, 1152, "gelu"), (96000, 1536, "silu"), (8192, 1536, "silu")):
+        x = torch.randn(M, 384, device=dev).to(torch.bfloat16)
+        W = (torch.randn(N, 384, device=dev) * 0.05).requires_grad_(True)
+        b = (torch.randn(N, device=dev) * 0.1).requires_grad_(True)
+        gy = torch.randn(M, N, device=dev)
+        for rec in (False, True):
+            G.RECOMPUTE_ACT = rec
+            with prec.precision("bf16"):
+                tf = timeit(lambda: ops.linear(x, W, b, act=act), iters=10)
+                y = ops.linear(x, W, b, act=act)
+                tb = timeit(lambda: torch.autograd.grad(y, (W, b), gy, retain_graph=True), iters=10)
+            print(f"linear+{act} M={M} N={N} recompute={rec}: fwd {tf*1e6:.1f} us  bwd {tb*1e6:.1f} us  "
+                  f"total {(tf+tb)*1e6:.1f} us", flush=True)
+        G.RECOMPUTE_ACT = True
+        del x, W, b, gy, y
+
+
 def attn_bench():
     from asrx import ops, prec
 
@@ -276,3 +301,5 @@ if __name__ == "__main__":
         norm_bench()
     if "msrow" in what:
         msrow_bench()
+    if "gact" in what:
+        gact_bench()
