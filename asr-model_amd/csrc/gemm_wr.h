@@ -525,6 +525,56 @@ __device__ __forceinline__ void wr_load(const Params& p, WrStage<NJ, ABF>& st, i
   }
 }
 
+// Fast operand addressing (non-conv launches whose operands span < 4 GiB and whose K is a multiple of the
+// k-step): each thread's row byte offsets are computed once per tile -- rows past M / N clamped to the last
+// row (they only feed accumulator rows / columns the epilogues never store) -- and a k-step's load is
+// base (SGPR) + offset + k bytes, one address add per load.  The general path selects between the row
+// address and the zero page per load and k-step (~15 instructions per load, exec-masked); the k-step is
+// issue-bound, and one extra load per k-step measured 5-12 % slower.
+#ifndef WR_FAST
+#define WR_FAST 1  // 0: every load takes the general (zero-page select) path -- A/B builds only
+#endif
+template <int NJ, bool ABF>
+struct WrOff {
+  uint32_t a[ABF ? 1 : 2];
+  uint32_t w[NJ];
+};
+template <int NJ, bool ABF>
+__device__ __forceinline__ void wr_offsets(const Params& p, WrOff<NJ, ABF>& o, int m0, int n0) {
+  const int t = threadIdx.x;
+  if constexpr (ABF) {
+    const int row = min(m0 + (t >> 2), p.M - 1);
+    o.a[0] = (uint32_t)(((int64_t)row * p.lda + 8 * (t & 3)) * 2);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int q = t + NTHR * i;
+      const int row = min(m0 + (q >> 3), p.M - 1);
+      o.a[i] = (uint32_t)(((int64_t)row * p.lda + 4 * (q & 7)) * 4);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NJ; ++i) {
+    const int q = t + NTHR * i;
+    const int n = min(n0 + (q >> 2), p.N - 1);
+    o.w[i] = (uint32_t)(((int64_t)n * p.ldw + 8 * (q & 3)) * 2);
+  }
+}
+template <int NJ, bool ABF>
+__device__ __forceinline__ void wr_load_fast(const Params& p, WrStage<NJ, ABF>& st, const WrOff<NJ, ABF>& o,
+                                             uint32_t ka, uint32_t kw) {
+  const char* A = reinterpret_cast<const char*>(p.A);
+  const char* W = reinterpret_cast<const char*>(p.W);
+  if constexpr (ABF) {
+    st.ah = *reinterpret_cast<const u32x4*>(A + (o.a[0] + ka));
+  } else {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) st.a[i] = *reinterpret_cast<const float4*>(A + (o.a[i] + ka));
+  }
+#pragma unroll
+  for (int i = 0; i < NJ; ++i) st.b[i] = *reinterpret_cast<const u32x4*>(W + (o.w[i] + kw));
+}
+
 // (Raw buffer loads against a per-tile resource -- 32-bit offsets, out-of-range chunks read 0 -- were
 // measured against these zero-page-clamped global loads: 13.1 -> 14.9 us at M = 8192, N = K = 384 and
 // no change on the 192k-row launches, profiles/r03_gemm_micro_v2.txt.)
@@ -637,6 +687,46 @@ __device__ __forceinline__ void wr_store64(const WrStage64<ABF>& st, char* At, c
   }
 }
 
+template <bool ABF>
+struct WrOff64 {
+  uint32_t a[ABF ? 2 : 4];
+  uint32_t w[2];
+};
+template <bool ABF>
+__device__ __forceinline__ void wr_offsets64(const Params& p, WrOff64<ABF>& o, int m0, int n0) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < (ABF ? 2 : 4); ++i) {
+    const int q = t + NTHR * i;
+    if constexpr (ABF) {
+      const int row = min(m0 + (q >> 3), p.M - 1);
+      o.a[i] = (uint32_t)(((int64_t)row * p.lda + 8 * (q & 7)) * 2);
+    } else {
+      const int row = min(m0 + (q >> 4), p.M - 1);
+      o.a[i] = (uint32_t)(((int64_t)row * p.lda + 4 * (q & 15)) * 4);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int q = t + NTHR * i;
+    const int n = min(n0 + (q >> 3), p.N - 1);
+    o.w[i] = (uint32_t)(((int64_t)n * p.ldw + 8 * (q & 7)) * 2);
+  }
+}
+template <bool ABF>
+__device__ __forceinline__ void wr_load64_fast(const Params& p, WrStage64<ABF>& st, const WrOff64<ABF>& o, uint32_t ka,
+                                               uint32_t kw) {
+  const char* A = reinterpret_cast<const char*>(p.A);
+  const char* W = reinterpret_cast<const char*>(p.W);
+#pragma unroll
+  for (int i = 0; i < (ABF ? 2 : 4); ++i) {
+    if constexpr (ABF) st.a[i] = *reinterpret_cast<const u32x4*>(A + (o.a[i] + ka));
+    else st.a[i] = *reinterpret_cast<const float4*>(A + (o.a[i] + ka));
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) st.b[i] = *reinterpret_cast<const u32x4*>(W + (o.w[i] + kw));
+}
+
 template <int NJ, bool CONV, bool RT, int DEP = 0, bool ABF = false, bool CE = false, bool RES = false,
           bool GA = false>
 __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) {  // ntiles: all tiles
@@ -711,10 +801,28 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
   enter(cl);
   cs = cl;
   ce = cl;
+  // fast operand addressing (wr_offsets) when the launch allows it; offsets of the load cursor's tile
+  constexpr int AES = ABF ? 2 : 4;
+  // nj = 1 (64-deep k-steps) only: measured 4-7 % faster there, but 10-14 % slower on the fp32-A nj = 3
+  // kernel (its five offsets at 253 VGPRs; profiles/r04_gemm_micro_fastaddr_ab.txt)
+  const bool fast = WR_FAST && K64 && p.K % BKW == 0 && (uint64_t)p.M * p.lda * AES < (1ull << 32) &&
+                    (uint64_t)p.N * p.ldw * 2 < (1ull << 32);
+  typedef typename pick_t<K64, WrOff64<ABF>, WrOff<NJ, ABF>>::type Off;
+  Off off;
   auto load = [&](Stg& st, bool issue) __attribute__((always_inline)) {
     if (issue) {
-      if constexpr (K64) wr_load64<ABF>(p, st, cl.m0, cl.n0, cl.kk * BKW);
-      else wr_load<NJ, CONV, ABF>(p, st, cl.m0, cl.n0, cl.kk * BK);
+      if (fast) {
+        if (cl.kk == 0) {
+          if constexpr (K64) wr_offsets64<ABF>(p, off, cl.m0, cl.n0);
+          else wr_offsets<NJ, ABF>(p, off, cl.m0, cl.n0);
+        }
+        const uint32_t k0 = (uint32_t)(cl.kk * BKW);
+        if constexpr (K64) wr_load64_fast<ABF>(p, st, off, k0 * AES, k0 * 2);
+        else wr_load_fast<NJ, ABF>(p, st, off, k0 * AES, k0 * 2);
+      } else {
+        if constexpr (K64) wr_load64<ABF>(p, st, cl.m0, cl.n0, cl.kk * BKW);
+        else wr_load<NJ, CONV, ABF>(p, st, cl.m0, cl.n0, cl.kk * BK);
+      }
     }
     advance(cl);
   };
