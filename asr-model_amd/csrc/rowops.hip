@@ -1031,6 +1031,24 @@ __global__ void axpy_row_kernel(const float* __restrict__ x, const float* __rest
   }
 }
 
+// float4 form (d % 4 == 0, aligned, rows * d / 4 < 2^31): two vectors per thread and trip, loads first,
+// 32-bit row index; the same x + s * y per element (bit-identical; this unit builds without contractions)
+__global__ void axpy_row4_kernel(const float4* __restrict__ x, const float* __restrict__ s,
+                                 const float4* __restrict__ y, float4* __restrict__ out, uint32_t n4, uint32_t d4) {
+  const uint32_t st = gridDim.x * blockDim.x;
+  auto one = [&](uint32_t i, float4 xv, float4 yv) __attribute__((always_inline)) {
+    const float sc = s ? s[i / d4] : 1.f;
+    out[i] = make_float4(xv.x + sc * yv.x, xv.y + sc * yv.y, xv.z + sc * yv.z, xv.w + sc * yv.w);
+  };
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + st < n4; i += 2 * st) {
+    const float4 x0 = x[i], x1 = x[i + st], y0 = y[i], y1 = y[i + st];
+    one(i, x0, y0);
+    one(i + st, x1, y1);
+  }
+  if (i < n4) one(i, x[i], y[i]);
+}
+
 // ds[r] = sum_j g[r,j] * y[r,j] ;  dy = s[r] * g  (dy may alias nothing)
 // (dxc, when non-null, receives a copy of g: x's pass-through gradient as a buffer the caller owns)
 __global__ __launch_bounds__(64 * RW) void axpy_row_bwd_kernel(const float* __restrict__ g, const float* __restrict__ s,
@@ -2476,7 +2494,14 @@ int asrx_tgate_bwd(const float* dout, const float* G, const float* c, float* dGz
 int asrx_axpy_row(const float* x, const float* s, const float* y, float* out, int64_t rows, int64_t d,
                   hipStream_t stream) {
   if (rows == 0) return 0;
-  LAUNCH_EW(axpy_row_kernel, rows * d, x, s, y, out, rows, (int)d);
+  if (d % 4 == 0 && rows * d / 4 < (1LL << 31) &&
+      ((((uintptr_t)x | (uintptr_t)y | (uintptr_t)out) & 15) == 0)) {
+    const int64_t n4 = rows * d / 4;
+    axpy_row4_kernel<<<ew_grid((n4 + 1) / 2, 8192), 256, 0, stream>>>((const float4*)x, s, (const float4*)y,
+                                                                      (float4*)out, (uint32_t)n4, (uint32_t)(d / 4));
+  } else {
+    LAUNCH_EW(axpy_row_kernel, rows * d, x, s, y, out, rows, (int)d);
+  }
   ASRX_LAUNCHED("asrx_axpy_row");
 }
 
