@@ -158,7 +158,7 @@ def logmel(wav: torch.Tensor, layout: str = "BFM", pool: bool = False):
         lay = 1
     else:
         raise ValueError(layout)
-    ws = torch.empty(B, dtype=torch.int32, device=wav.device)
+    ws = torch.empty(lib.load().asrx_logmel_ws_bytes(B, N) // 4, dtype=torch.float32, device=wav.device)
     pooled = None
     T = 0
     if pool:

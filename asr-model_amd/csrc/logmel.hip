@@ -38,11 +38,23 @@ constexpr int MEL_NFFT = 1024, MEL_HOP = 160, MEL_NBINS = 513, MEL_BANDS = 128, 
 constexpr int FB_A = 8, FB_B = 24;  // taps of a lane's two bands (see lane_filterbank in mel.py)
 constexpr int FB_QUADS = (FB_A + FB_B) / 4;
 constexpr int MEL_WAVES = 4;
-constexpr int MEL_FPT = 16;  // frames per tile
+#ifndef MEL_WPS
+#define MEL_WPS 3  // waves per SIMD (= resident 4-wave workgroups per CU)
+#endif
+#ifndef MEL_FPT_
+#define MEL_FPT_ 16
+#endif
+#ifndef MEL_NBUF0
+#define MEL_NBUF0 1  // sample buffers of the (B, F, 128) kernel (2: measured no faster, and 54 KB of LDS fits only 2 workgroups per CU)
+#endif
+#ifndef MEL_STAGE0
+#define MEL_STAGE0 0  // 1: (B, F, 128) output staged in LDS and stored as float4 rows
+#endif
+constexpr int MEL_FPT = MEL_FPT_;  // frames per tile
 constexpr int MEL_TSAMP = (MEL_FPT - 1) * MEL_HOP + MEL_NFFT;  // 3424 samples per tile
 constexpr int MEL_TSAMP4 = MEL_TSAMP / 4;                      // 856 float4
 constexpr int MEL_PF = (MEL_TSAMP4 + 255) / 256;               // prefetch float4 per thread
-constexpr int FFT_SLOTS = 512 + 64 + 8;                        // padded cpx slots per wave
+constexpr int FFT_SLOTS = 512 + 64 + 1;                        // zpad(0..512) cpx slots per wave
 static_assert(MEL_TSAMP % 4 == 0, "tile samples must be float4 aligned");
 
 __constant__ float kRot[8][2] = {
@@ -55,7 +67,86 @@ __constant__ float kRot[8][2] = {
     {-0.70710678118654746f, -0.70710678118654768f},
     {-0.92387953251128674f, -0.38268343236508989f}};
 
-__device__ __forceinline__ int pidx(int i) { return i + (i >> 3); }
+// Z slot of bin i: two pad slots every 16 bins (slot(i + 64) = slot(i) + 72), which makes the
+// digit-reversed Z stores conflict-free and leaves the mirrored reads 2-way
+__device__ __forceinline__ int zpad(int i) { return i + 2 * (i >> 4); }
+
+// 2 x 2 exchange between lane bit B and register bit: for every register pair (a, c) that differs
+// only in that register bit, lanes with the lane bit clear keep a and take the partner's a into c,
+// lanes with it set take the partner's c into a and keep c.  Bits 5 and 4 are one permlane swap per
+// VGPR pair; bits 3..0 read the partner through DPP (row_ror by 8 or 4/12 inside a 16-lane row,
+// quad_perm xor 2 / xor 1) and select.
+template <int B>
+__device__ __forceinline__ void xch_pair(float& a, float& c) {
+  if constexpr (B == 5) {
+    xrow32(a, c);
+  } else {
+    static_assert(B == 4, "bits 3..0 go through xch_dpp4");
+    xrow16(a, c);
+  }
+}
+// Bits 3..0, four register pairs at once: each output is one v_cndmask_b32 whose first source is
+// read through DPP (the select and the partner read in one instruction):
+//   c' = set ? c : partner(a)   with VCC = the lanes whose bit is set, DPP = UP
+//   a' = set ? partner(c) : a   with VCC = the lanes whose bit is clear, DPP = DN
+// UP: lane i reads lane i + 2^B (bit-clear lanes); DN: lane i - 2^B (bit-set lanes).  row_ror:n makes
+// lane i read lane (i - n) mod 16 of its row, so i + 4 is row_ror:12 and i - 4 row_ror:4; bits 1 and
+// 0 are quad_perm xor 2 / xor 1 both ways, bit 3 row_ror:8 both ways.  The leading s_nop 1 covers the
+// VALU-write -> DPP-read hazard on the inputs; the outputs are fresh registers.
+#define ASRX_XCH4(UPS, DNS)                                                                                    \
+  asm("s_mov_b64 vcc, %[ms]\n\ts_nop 1\n\t"                                                                 \
+      "v_cndmask_b32_dpp %[c0], %[a0i], %[c0i], vcc " UPS " row_mask:0xf bank_mask:0xf\n\t"                    \
+      "v_cndmask_b32_dpp %[c1], %[a1i], %[c1i], vcc " UPS " row_mask:0xf bank_mask:0xf\n\t"                    \
+      "v_cndmask_b32_dpp %[c2], %[a2i], %[c2i], vcc " UPS " row_mask:0xf bank_mask:0xf\n\t"                    \
+      "v_cndmask_b32_dpp %[c3], %[a3i], %[c3i], vcc " UPS " row_mask:0xf bank_mask:0xf\n\t"                    \
+      "s_mov_b64 vcc, %[mc]\n\t"                                                                             \
+      "v_cndmask_b32_dpp %[a0], %[c0i], %[a0i], vcc " DNS " row_mask:0xf bank_mask:0xf\n\t"                    \
+      "v_cndmask_b32_dpp %[a1], %[c1i], %[a1i], vcc " DNS " row_mask:0xf bank_mask:0xf\n\t"                    \
+      "v_cndmask_b32_dpp %[a2], %[c2i], %[a2i], vcc " DNS " row_mask:0xf bank_mask:0xf\n\t"                    \
+      "v_cndmask_b32_dpp %[a3], %[c3i], %[a3i], vcc " DNS " row_mask:0xf bank_mask:0xf"                          \
+      : [a0] "=&v"(a0), [a1] "=&v"(a1), [a2] "=&v"(a2), [a3] "=&v"(a3), [c0] "=&v"(c0), [c1] "=&v"(c1),          \
+        [c2] "=&v"(c2), [c3] "=&v"(c3)                                                                          \
+      : [a0i] "v"(*pa[0]), [a1i] "v"(*pa[1]), [a2i] "v"(*pa[2]), [a3i] "v"(*pa[3]), [c0i] "v"(*pc[0]),          \
+        [c1i] "v"(*pc[1]), [c2i] "v"(*pc[2]), [c3i] "v"(*pc[3]), [ms] "s"(mset), [mc] "s"(~mset)                \
+      : "vcc")
+template <int B>
+__device__ __forceinline__ void xch_dpp4(float* const (&pa)[4], float* const (&pc)[4]) {
+  constexpr uint64_t mset = B == 3 ? 0xFF00FF00FF00FF00ull
+                          : B == 2 ? 0xF0F0F0F0F0F0F0F0ull
+                          : B == 1 ? 0xCCCCCCCCCCCCCCCCull
+                                   : 0xAAAAAAAAAAAAAAAAull;
+  float a0, a1, a2, a3, c0, c1, c2, c3;
+  if constexpr (B == 3) ASRX_XCH4("row_ror:8", "row_ror:8");
+  else if constexpr (B == 2) ASRX_XCH4("row_ror:12", "row_ror:4");
+  else if constexpr (B == 1) ASRX_XCH4("quad_perm:[2,3,0,1]", "quad_perm:[2,3,0,1]");
+  else ASRX_XCH4("quad_perm:[1,0,3,2]", "quad_perm:[1,0,3,2]");
+  *pa[0] = a0; *pa[1] = a1; *pa[2] = a2; *pa[3] = a3;
+  *pc[0] = c0; *pc[1] = c1; *pc[2] = c2; *pc[3] = c3;
+}
+#undef ASRX_XCH4
+// lane bit B <-> register bit (B % 3): 5 and 2 pair registers r, r + 4; 4 and 1 pair r, r + 2; 3 and
+// 0 pair r, r + 1
+template <int B>
+__device__ __forceinline__ void xch_lanes(cpx (&v)[8]) {
+  constexpr int RB = 1 << (B % 3);
+  constexpr int R0 = RB == 1 ? 0 : 0, R1 = RB == 1 ? 2 : RB == 2 ? 1 : 1, R2 = RB == 1 ? 4 : RB == 2 ? 4 : 2,
+                R3 = RB == 1 ? 6 : RB == 2 ? 5 : 3;  // the four registers r with bit RB clear
+  if constexpr (B >= 4) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      if (r & RB) continue;
+      xch_pair<B>(v[r].x, v[r + RB].x);
+      xch_pair<B>(v[r].y, v[r + RB].y);
+    }
+  } else {
+    float* const ax[4] = {&v[R0].x, &v[R1].x, &v[R2].x, &v[R3].x};
+    float* const cx[4] = {&v[R0 + RB].x, &v[R1 + RB].x, &v[R2 + RB].x, &v[R3 + RB].x};
+    float* const ay[4] = {&v[R0].y, &v[R1].y, &v[R2].y, &v[R3].y};
+    float* const cy[4] = {&v[R0 + RB].y, &v[R1 + RB].y, &v[R2 + RB].y, &v[R3 + RB].y};
+    xch_dpp4<B>(ax, cx);
+    xch_dpp4<B>(ay, cy);
+  }
+}
 
 // Orders this wave's LDS accesses (the LDS unit executes one wave's DS instructions in order;
 // this only stops the compiler from moving them across the exchange point).
@@ -95,6 +186,16 @@ __device__ __forceinline__ void ds_rd64x8(uint32_t a, f2v (&o)[8]) {
                : "memory");
 }
 
+// the eight filterbank weight quads of this lane, re-read per frame (kept in VGPRs they would cost 32
+// registers for the whole kernel and a wave per SIMD)
+typedef float f4v __attribute__((ext_vector_type(4)));
+template <int OFF>
+__device__ __forceinline__ f4v ds_rd128(uint32_t a) {
+  f4v r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF) : "memory");
+  return r;
+}
+
 template <int OFF0, int STRIDE>
 __device__ __forceinline__ void ds_rd64x4(uint32_t a, f2v (&o)[4]) {
   o[0] = ds_rd64<OFF0>(a);
@@ -104,12 +205,6 @@ __device__ __forceinline__ void ds_rd64x4(uint32_t a, f2v (&o)[4]) {
   asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(o[0]), "+v"(o[1]), "+v"(o[2]), "+v"(o[3]) : : "memory");
 }
 
-__device__ __forceinline__ void dft8_tw(cpx (&v)[8], const cpx (&tw)[7]) {
-#pragma unroll
-  for (int r = 1; r < 8; ++r) v[r] = asrx_fft::cmul(v[r], tw[r - 1]);
-  asrx_fft::dft8(v);
-}
-
 // contiguous run of tiles per workgroup; consecutive runs on one XCD (blocks are dealt to the 8
 // XCDs round-robin by blockIdx)
 __device__ __forceinline__ int xcd_block(int bid, int G) {
@@ -117,15 +212,24 @@ __device__ __forceinline__ int xcd_block(int bid, int G) {
   return (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + q;
 }
 
-__global__ __launch_bounds__(256, 3) void logmel_tiles_kernel(
+// LAYOUT 0 (B, F, 128): every lane stores its two bands straight into the frame's 512-byte row (L2
+// merges the scattered dwords into whole lines), so no staging block is needed and the workgroup's
+// LDS (40.6 KB) lets 4 of them share a CU.  LAYOUT 1 (B, 128, F) stages the tile in LDS for
+// frame-contiguous stores.
+template <int LAYOUT>
+__global__ __launch_bounds__(256, MEL_WPS) void logmel_tiles_kernel(
     const float* __restrict__ wav, int64_t N, int64_t ld_wav, int vec_ok, int64_t F, int tiles_per_clip,
     int64_t n_tiles, int tiles_per_block, const float* __restrict__ consts, const float* __restrict__ fbw,
-    const int* __restrict__ fbs, float* __restrict__ out, int layout, int64_t ld_out,
-    int* __restrict__ clip_max, float* __restrict__ pool, int64_t T_pool) {
-  __shared__ __attribute__((aligned(16))) float samp[MEL_TSAMP];
+    const int* __restrict__ fbs, float* __restrict__ out, int64_t ld_out,
+    float* __restrict__ tstat, float* __restrict__ pool, int64_t T_pool) {
+  // (B, F, 128): two sample buffers, the next tile's samples land by LDS-DMA while this tile is
+  // transformed; (B, 128, F) keeps one (its staging block takes the room)
+  constexpr int NBUF = LAYOUT == 0 ? MEL_NBUF0 : 1;
+  constexpr bool STAGED = LAYOUT == 1 || MEL_STAGE0;
+  __shared__ __attribute__((aligned(16))) float samp_buf[NBUF][MEL_TSAMP];
   __shared__ __attribute__((aligned(16))) cpx fbuf[MEL_WAVES][FFT_SLOTS];
-  __shared__ float melst[MEL_FPT][MEL_BANDS + 1];
-  __shared__ float red[MEL_WAVES];
+  __shared__ float melst[STAGED ? MEL_FPT : 1][MEL_BANDS + 1];
+  __shared__ float red[2][MEL_WAVES];
   __shared__ float4 fbw_s[FB_QUADS * 64];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -138,14 +242,16 @@ __global__ __launch_bounds__(256, 3) void logmel_tiles_kernel(
   const cpx* tw512 = reinterpret_cast<const cpx*>(consts + MEL_NFFT);
   const cpx* tw1024 = reinterpret_cast<const cpx*>(consts + MEL_NFFT + 1024);
   float2 wv[8];
-  cpx t2[7], t3[7];
+  cpx twa[7], twb[7];
 #pragma unroll
   for (int r = 0; r < 8; ++r) wv[r] = *reinterpret_cast<const float2*>(win + 2 * (lane + 64 * r));
-  const cpx tu0 = tw1024[lane];
+  // the bin index lane j holds after the third stage: kj + 64 r, kj = (j >> 3) + 8 (j & 7)
+  const int kj = (lane >> 3) + 8 * (lane & 7);
+  const cpx tu0 = tw1024[kj];
 #pragma unroll
   for (int r = 1; r < 8; ++r) {
-    t2[r - 1] = tw512[(r * (lane & 7) * 8) & 511];
-    t3[r - 1] = tw512[(r * lane) & 511];
+    twa[r - 1] = tw512[(r * lane) & 511];            // W512^(j kA)
+    twb[r - 1] = tw512[(r * (lane & 7) * 8) & 511];  // W64^(n0 kB)
   }
   // lane-packed filterbank (asrx/mel.py lane_filterbank): lane m owns band_a (<= 8 taps from the
   // even bin sa) and band_b (<= 24 taps from the even bin sb); weights [tap/4][lane][4] in LDS
@@ -156,48 +262,45 @@ __global__ __launch_bounds__(256, 3) void logmel_tiles_kernel(
   cpx* S = fbuf[wid];
   float* P = reinterpret_cast<float*>(S);
 
-  // ---- sample prefetch (registers) for tile t; the bounds test is per tile (wave-uniform)
-  float4 pf[MEL_PF];
-  auto prefetch = [&](int64_t t) {
+  // tile t's samples -> dst.  Interior tiles: LDS-DMA (global_load_lds_dwordx4, 1 KB per wave
+  // instruction, no VGPRs held), completed by the s_waitcnt vmcnt(0) before the barrier that
+  // publishes the buffer.  Tiles that touch a clip edge (the test is per tile, so workgroup-uniform):
+  // element-wise with zero fill.
+  auto stage = [&](int64_t t, float* dst) {
     const int64_t b = t / tiles_per_clip;
-    const int64_t f0 = (t - b * tiles_per_clip) * MEL_FPT;
-    const int64_t g0 = f0 * MEL_HOP - MEL_NFFT / 2;
+    const int64_t g0 = (t - b * tiles_per_clip) * MEL_FPT * MEL_HOP - MEL_NFFT / 2;
     const float* x = wav + b * ld_wav + g0;
     if (vec_ok && g0 >= 0 && g0 + MEL_TSAMP <= N) {
       const float4* x4 = reinterpret_cast<const float4*>(x);
 #pragma unroll
       for (int q = 0; q < MEL_PF; ++q) {
-        const int i4 = tid + 256 * q;
-        pf[q] = i4 < MEL_TSAMP4 ? x4[i4] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const int c0 = 256 * q + 64 * wid;  // this wave's float4 chunk (wave-uniform)
+        if (c0 < MEL_TSAMP4 && c0 + lane < MEL_TSAMP4) glds16(x4 + c0 + lane, lds_addr(reinterpret_cast<float4*>(dst) + c0));
       }
     } else {
-#pragma unroll
-      for (int q = 0; q < MEL_PF; ++q) {
-        const int i4 = tid + 256 * q;
-        float e[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const int64_t g = g0 + 4 * i4 + c;
-          e[c] = (i4 < MEL_TSAMP4 && g >= 0 && g < N) ? x[4 * i4 + c] : 0.f;
-        }
-        pf[q] = make_float4(e[0], e[1], e[2], e[3]);
+#pragma unroll 1
+      for (int i = tid; i < MEL_TSAMP; i += 256) {
+        const int64_t g = g0 + i;
+        dst[i] = (g >= 0 && g < N) ? x[i] : 0.f;
       }
     }
   };
-  prefetch(t_begin);
+  if constexpr (NBUF == 2) stage(t_begin, samp_buf[0]);
 
 #pragma unroll 1
   for (int64_t t = t_begin; t < t_end; ++t) {
     const int64_t b = t / tiles_per_clip;
     const int64_t f0 = (t - b * tiles_per_clip) * MEL_FPT;
-    __syncthreads();  // the previous tile's readers are done with samp / melst
-#pragma unroll
-    for (int q = 0; q < MEL_PF; ++q) {
-      const int i4 = tid + 256 * q;
-      if (i4 < MEL_TSAMP4) reinterpret_cast<float4*>(samp)[i4] = pf[q];
+    float* samp = samp_buf[NBUF == 2 ? (int)((t - t_begin) & 1) : 0];
+    if constexpr (NBUF == 1) {
+      __syncthreads();  // the previous tile's readers are done with samp / melst
+      stage(t, samp);
     }
-    __syncthreads();
-    if (t + 1 < t_end) prefetch(t + 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // samp published; with two buffers also: every wave is done with the other one
+    if constexpr (NBUF == 2) {
+      if (t + 1 < t_end) stage(t + 1, samp_buf[(int)((t + 1 - t_begin) & 1)]);
+    }
 
     // fused waveform feature: exact 160-sample block means (pool index == frame index)
     if (pool) {
@@ -211,7 +314,7 @@ __global__ __launch_bounds__(256, 3) void logmel_tiles_kernel(
       }
     }
 
-    float lmax = -3.0e38f;
+    float lmax = -3.0e38f, lmin = 3.0e38f;
 #pragma unroll 1
     for (int fi = wid; fi < MEL_FPT; fi += MEL_WAVES) {
       const bool live = f0 + fi < F;  // wave-uniform
@@ -222,41 +325,38 @@ __global__ __launch_bounds__(256, 3) void logmel_tiles_kernel(
 #pragma unroll
         for (int r = 0; r < 8; ++r) v[r] = cpx{sv[r].x * wv[r].x, sv[r].y * wv[r].y};
       }
-      // pass 1 (Ns = 1): out[8j + r]
+      // stage A: DFT over n2 (registers) -> kA, twiddle W512^(j kA)
       asrx_fft::dft8(v);
 #pragma unroll
-      for (int r = 0; r < 8; ++r) S[9 * lane + r] = v[r];
-      wave_lds_sync();
-      {
-        f2v t[8];
-        ds_rd64x8<0, 576>(lds_off(S + pidx(lane)), t);
+      for (int r = 1; r < 8; ++r) v[r] = asrx_fft::cmul(v[r], twa[r - 1]);
+      // lane bits 3-5 (n1) <-> register bits 0-2 (kA): lane = n0 + 8 kA, registers n1
+      xch_lanes<5>(v);
+      xch_lanes<4>(v);
+      xch_lanes<3>(v);
+      // stage B: DFT over n1 -> kB, twiddle W64^(n0 kB)
+      asrx_fft::dft8(v);
 #pragma unroll
-        for (int r = 0; r < 8; ++r) v[r] = cpx{t[r].x, t[r].y};
-      }
-      wave_lds_sync();
-      // pass 2 (Ns = 8): out[(j/8)*64 + j%8 + 8r]
-      dft8_tw(v, t2);
+      for (int r = 1; r < 8; ++r) v[r] = asrx_fft::cmul(v[r], twb[r - 1]);
+      // lane bits 0-2 (n0) <-> register bits 0-2 (kB): lane = kB + 8 kA, registers n0
+      xch_lanes<2>(v);
+      xch_lanes<1>(v);
+      xch_lanes<0>(v);
+      // stage C: DFT over n0 -> kC; lane j register r now holds Z[kj + 64 r]
+      asrx_fft::dft8(v);
+      // the one LDS exchange: Z in natural order (padded, zpad), Z_0 also at slot
+      // zpad(512) for the mirror of lane 0's register 0
 #pragma unroll
-      for (int r = 0; r < 8; ++r) S[72 * (lane >> 3) + (lane & 7) + 9 * r] = v[r];
+      for (int r = 0; r < 8; ++r) S[zpad(kj) + 72 * r] = v[r];
+      if (lane == 0) S[zpad(512)] = v[0];
       wave_lds_sync();
-      {
-        f2v t[8];
-        ds_rd64x8<0, 576>(lds_off(S + pidx(lane)), t);
-#pragma unroll
-        for (int r = 0; r < 8; ++r) v[r] = cpx{t[r].x, t[r].y};
-      }
-      wave_lds_sync();
-      // pass 3 (Ns = 64): out[j + 64 r] = Z[j + 64 r], kept in v
-      dft8_tw(v, t3);
-      // third exchange unpadded: the R-pattern writes and the mirrored reads are conflict-free
-      // without padding (lane 0 also stores Z_0 at 512, the mirror of its r = 0 slot)
-#pragma unroll
-      for (int r = 0; r < 8; ++r) S[lane + 64 * r] = v[r];
-      if (lane == 0) S[512] = v[0];
-      wave_lds_sync();
-      f2v zm[8];  // zm[r] = Z[(512 - lane - 64 r) & 511] = S[64 - lane + 64 (7 - r)]
-      ds_rd64x8<0, 512>(lds_off(S + 64 - lane), zm);
+      f2v zm[8];  // zm[7 - r] = Z[(512 - kj - 64 r) & 511] = S[zpad(64 - kj) + 72 (7 - r)]
+      ds_rd64x8<0, 576>(lds_off(S + zpad(64 - kj)), zm);
       // real-FFT untangle: 2 X_k = (Z_k + conj Z_{512-k}) + W1024^k (-i)(Z_k - conj Z_{512-k})
+      // W1024^(kj + 64 r) = W1024^kj exp(-i pi r / 8) = u[r & 3] (-i)^(r >> 2)
+      cpx u[4];
+      u[0] = tu0;
+#pragma unroll
+      for (int r = 1; r < 4; ++r) u[r] = asrx_fft::cmul(tu0, cpx{kRot[r][0], kRot[r][1]});
       float pw[8];
 #pragma unroll
       for (int r = 0; r < 8; ++r) {
@@ -264,14 +364,13 @@ __global__ __launch_bounds__(256, 3) void logmel_tiles_kernel(
         const cpx zk = v[r];
         const cpx e{zk.x + zn.x, zk.y - zn.y};
         const cpx o{zk.y + zn.y, zn.x - zk.x};
-        // W1024^(j + 64 r) = W1024^j * exp(-i pi r / 8)
-        const cpx tt = asrx_fft::cmul(asrx_fft::cmul(tu0, cpx{kRot[r][0], kRot[r][1]}), o);
-        const float re = e.x + tt.x, im = e.y + tt.y;
+        const cpx w = asrx_fft::cmul(u[r & 3], o);
+        const float re = r < 4 ? e.x + w.x : e.x + w.y, im = r < 4 ? e.y + w.y : e.y - w.x;  // (-i) w = (w.y, -w.x)
         pw[r] = re * re + im * im;  // 4 |X_k|^2
       }
       wave_lds_sync();
 #pragma unroll
-      for (int r = 0; r < 8; ++r) P[lane + 64 * r] = pw[r];
+      for (int r = 0; r < 8; ++r) P[kj + 64 * r] = pw[r];
       if (lane < 16) {
         const float nyq = 2.0f * (v[0].x - v[0].y);  // lane 0: 2 X_512 = 2 (Re Z0 - Im Z0)
         P[512 + lane] = lane == 0 ? nyq * nyq : 0.f;  // bins past 512 are zero pads for the taps
@@ -279,39 +378,74 @@ __global__ __launch_bounds__(256, 3) void logmel_tiles_kernel(
       wave_lds_sync();
       // sparse filterbank (weights carry the 1/4; bins read in even-aligned pairs)
       static_assert(FB_A == 8 && FB_B == 24, "the filterbank reads below are written out for 8 + 24 taps");
-      f2v pa[4], pb[8], pc[4];  // bins sa .. sa+7 | sb .. sb+15 | sb+16 .. sb+23
-      ds_rd64x4<0, 8>(lds_off(P + 2 * sa2), pa);
-      ds_rd64x8<0, 8>(lds_off(P + 2 * sb2), pb);
-      ds_rd64x4<64, 8>(lds_off(P + 2 * sb2), pc);
+      // three read groups (bins | weight quads), each drained before the next, so at most 32 VGPRs
+      // of operands are live: band a (8 bins), band b taps 0-15, band b taps 16-23
+      const uint32_t wa = lds_off(fbw_s + lane);
       float acc_a = 0.f, acc_b = 0.f;
-#pragma unroll
-      for (int q = 0; q < FB_A / 4; ++q) {
-        const float4 wq = fbw_s[q * 64 + lane];
-        const f2v p0 = pa[2 * q], p1 = pa[2 * q + 1];
-        acc_a = fmaf(wq.x, p0.x, fmaf(wq.y, p0.y, fmaf(wq.z, p1.x, fmaf(wq.w, p1.y, acc_a))));
+      {
+        f2v p[4];
+        p[0] = ds_rd64<0>(lds_off(P + 2 * sa2));
+        p[1] = ds_rd64<8>(lds_off(P + 2 * sa2));
+        p[2] = ds_rd64<16>(lds_off(P + 2 * sa2));
+        p[3] = ds_rd64<24>(lds_off(P + 2 * sa2));
+        f4v w0 = ds_rd128<0>(wa), w1 = ds_rd128<1024>(wa);
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(p[0]), "+v"(p[1]), "+v"(p[2]), "+v"(p[3]), "+v"(w0), "+v"(w1) : : "memory");
+        acc_a = fmaf(w0.x, p[0].x, fmaf(w0.y, p[0].y, fmaf(w0.z, p[1].x, fmaf(w0.w, p[1].y, acc_a))));
+        acc_a = fmaf(w1.x, p[2].x, fmaf(w1.y, p[2].y, fmaf(w1.z, p[3].x, fmaf(w1.w, p[3].y, acc_a))));
       }
-#pragma unroll
-      for (int q = 0; q < FB_B / 4; ++q) {
-        const float4 wq = fbw_s[(FB_A / 4 + q) * 64 + lane];
-        const f2v p0 = q < 4 ? pb[2 * q] : pc[2 * (q - 4)], p1 = q < 4 ? pb[2 * q + 1] : pc[2 * (q - 4) + 1];
-        acc_b = fmaf(wq.x, p0.x, fmaf(wq.y, p0.y, fmaf(wq.z, p1.x, fmaf(wq.w, p1.y, acc_b))));
+      {
+        f2v p[8];
+        ds_rd64x8<0, 8>(lds_off(P + 2 * sb2), p);
+        f4v w0 = ds_rd128<2048>(wa), w1 = ds_rd128<3072>(wa), w2 = ds_rd128<4096>(wa), w3 = ds_rd128<5120>(wa);
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(w0), "+v"(w1), "+v"(w2), "+v"(w3) : : "memory");
+        acc_b = fmaf(w0.x, p[0].x, fmaf(w0.y, p[0].y, fmaf(w0.z, p[1].x, fmaf(w0.w, p[1].y, acc_b))));
+        acc_b = fmaf(w1.x, p[2].x, fmaf(w1.y, p[2].y, fmaf(w1.z, p[3].x, fmaf(w1.w, p[3].y, acc_b))));
+        acc_b = fmaf(w2.x, p[4].x, fmaf(w2.y, p[4].y, fmaf(w2.z, p[5].x, fmaf(w2.w, p[5].y, acc_b))));
+        acc_b = fmaf(w3.x, p[6].x, fmaf(w3.y, p[6].y, fmaf(w3.z, p[7].x, fmaf(w3.w, p[7].y, acc_b))));
+      }
+      {
+        f2v p[4];
+        ds_rd64x4<64, 8>(lds_off(P + 2 * sb2), p);
+        f4v w0 = ds_rd128<6144>(wa), w1 = ds_rd128<7168>(wa);
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(w0), "+v"(w1) : : "memory");
+        acc_b = fmaf(w0.x, p[0].x, fmaf(w0.y, p[0].y, fmaf(w0.z, p[1].x, fmaf(w0.w, p[1].y, acc_b))));
+        acc_b = fmaf(w1.x, p[2].x, fmaf(w1.y, p[2].y, fmaf(w1.z, p[3].x, fmaf(w1.w, p[3].y, acc_b))));
       }
       wave_lds_sync();
       // clamp(1e-10).log10(): the clamped value maps to exactly -10 like the correctly rounded
       // library log10; elsewhere log2 * log10(2) is within a few ulp
       const float l_a = acc_a <= 1e-10f ? -10.0f : __builtin_amdgcn_logf(acc_a) * 0.30102999566398120f;
       const float l_b = acc_b <= 1e-10f ? -10.0f : __builtin_amdgcn_logf(acc_b) * 0.30102999566398120f;
-      melst[fi][band_a] = l_a;
-      melst[fi][band_b] = l_b;
-      if (live) lmax = fmaxf(lmax, fmaxf(l_a, l_b));
+      // (x + 4) / 4 here; the clip-max floor is applied afterwards, only to the tiles holding a value
+      // below it (logmel_floor_kernel): (max(x, f) + 4) / 4 == max((x + 4) / 4, (f + 4) / 4) exactly,
+      // as x -> fl(x + 4) is monotone and / 4 is exact
+      const float y_a = (l_a + 4.0f) * 0.25f, y_b = (l_b + 4.0f) * 0.25f;
+      if constexpr (!STAGED) {
+        if (live) {
+          float* orow = out + b * ld_out + (f0 + fi) * MEL_BANDS;
+          orow[band_a] = y_a;
+          orow[band_b] = y_b;
+        }
+      } else {
+        melst[fi][band_a] = y_a;
+        melst[fi][band_b] = y_b;
+      }
+      if (live) {
+        lmax = fmaxf(lmax, fmaxf(l_a, l_b));
+        lmin = fminf(lmin, fminf(l_a, l_b));
+      }
     }
     lmax = wave_max(lmax);
-    if (lane == 0) red[wid] = lmax;
+    lmin = -wave_max(-lmin);
+    if (lane == 0) {
+      red[0][wid] = lmax;
+      red[1][wid] = lmin;
+    }
     __syncthreads();
 
     // coalesced output of the staged block
-    float* o = out + b * ld_out;
-    if (layout == 0) {  // (B, F, 128): the tile is FPT contiguous rows of 128
+    if constexpr (LAYOUT == 0 && STAGED) {  // (B, F, 128): the tile is FPT contiguous rows of 128
+      float* o = out + b * ld_out;
       for (int i = tid; i < MEL_FPT * MEL_BANDS / 4; i += 256) {
         const int fi = i / (MEL_BANDS / 4), m4 = (i % (MEL_BANDS / 4)) * 4;
         if (f0 + fi < F) {
@@ -319,46 +453,65 @@ __global__ __launch_bounds__(256, 3) void logmel_tiles_kernel(
           *reinterpret_cast<float4*>(o + (f0 + fi) * MEL_BANDS + m4) = make_float4(src[0], src[1], src[2], src[3]);
         }
       }
-    } else {  // (B, 128, F): each band's FPT frames contiguous
+    }
+    if constexpr (LAYOUT == 1) {  // (B, 128, F): each band's FPT frames contiguous
+      float* o = out + b * ld_out;
       for (int i = tid; i < MEL_FPT * MEL_BANDS; i += 256) {
         const int m = i / MEL_FPT, fi = i % MEL_FPT;
         if (f0 + fi < F) o[m * F + f0 + fi] = melst[fi][m];
       }
     }
-    if (tid == 0) {
-      float bm = red[0];
+    if (tid == 0) {  // this tile's max and min log value over its live frames (no atomics, no init)
+      float bm = red[0][0], bn = red[1][0];
 #pragma unroll
-      for (int w = 1; w < MEL_WAVES; ++w) bm = fmaxf(bm, red[w]);
-      atomicMax(clip_max + b, float_to_ordered(bm));
+      for (int w = 1; w < MEL_WAVES; ++w) {
+        bm = fmaxf(bm, red[0][w]);
+        bn = fminf(bn, red[1][w]);
+      }
+      tstat[t] = bm;
+      tstat[n_tiles + t] = bn;
     }
   }
 }
 
-__global__ void logmel_finalize_kernel(float* __restrict__ out, int64_t per_clip, int64_t ld_out,
-                                       const int* __restrict__ clip_max, int vec) {
-  const int b = blockIdx.y;
-  const float floor_v = ordered_to_float(clip_max[b]) - 8.0f;
+// Clip-max floor (maximum(x, max(x) - 8), essentials.py:485-488) on the (x + 4) / 4 values the tile
+// kernel wrote.  One workgroup per tile: the clip max is the max of the clip's tile maxima; a tile
+// whose minimum is not below the floor is left as it is (every value already final), any other is
+// rewritten as max(y, (f + 4) / 4).
+__global__ __launch_bounds__(256) void logmel_floor_kernel(float* __restrict__ out, int layout, int64_t F,
+                                                           int64_t ld_out, int tiles_per_clip, int64_t n_tiles,
+                                                           const float* __restrict__ tstat) {
+  __shared__ float red[4];
+  const int b = blockIdx.y, tl = blockIdx.x, tid = threadIdx.x;
+  const float* tm = tstat + (int64_t)b * tiles_per_clip;
+  float m = -3.0e38f;
+  for (int i = tid; i < tiles_per_clip; i += 256) m = fmaxf(m, tm[i]);
+  m = wave_max(m);
+  if ((tid & 63) == 0) red[tid >> 6] = m;
+  __syncthreads();
+  const float floor_v = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])) - 8.0f;
+  if (!(tstat[n_tiles + (int64_t)b * tiles_per_clip + tl] < floor_v)) return;  // workgroup-uniform
+  const float yf = (floor_v + 4.0f) * 0.25f;
+  const int64_t f0 = (int64_t)tl * MEL_FPT;
+  const int nf = (int)(F - f0 < MEL_FPT ? F - f0 : MEL_FPT);
   float* o = out + b * ld_out;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  if (vec) {
-    float4* o4 = reinterpret_cast<float4*>(o);
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < per_clip / 4; i += stride) {
+  if (layout == 0) {  // nf contiguous rows of 128
+    float4* o4 = reinterpret_cast<float4*>(o + f0 * MEL_BANDS);
+    for (int i = tid; i < nf * MEL_BANDS / 4; i += 256) {
       float4 v = o4[i];
-      v.x = (fmaxf(v.x, floor_v) + 4.0f) * 0.25f;
-      v.y = (fmaxf(v.y, floor_v) + 4.0f) * 0.25f;
-      v.z = (fmaxf(v.z, floor_v) + 4.0f) * 0.25f;
-      v.w = (fmaxf(v.w, floor_v) + 4.0f) * 0.25f;
+      v.x = fmaxf(v.x, yf);
+      v.y = fmaxf(v.y, yf);
+      v.z = fmaxf(v.z, yf);
+      v.w = fmaxf(v.w, yf);
       o4[i] = v;
     }
-  } else {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < per_clip; i += stride)
-      o[i] = (fmaxf(o[i], floor_v) + 4.0f) * 0.25f;
+  } else {  // 128 runs of nf frames at stride F
+    for (int i = tid; i < nf * MEL_BANDS; i += 256) {
+      const int mb = i / nf, fi = i - mb * nf;
+      float* q = o + mb * F + f0 + fi;
+      *q = fmaxf(*q, yf);
+    }
   }
-}
-
-__global__ void fill_int_kernel(int* p, int n, int v) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) p[i] = v;
 }
 
 }  // namespace asrx
@@ -366,37 +519,42 @@ __global__ void fill_int_kernel(int* p, int n, int v) {
 using namespace asrx;
 
 // wav: (B, N) rows at stride ld_wav.  out: (B, F, 128) if layout == 0 else (B, 128, F), clip stride
-// ld_out (>= 128*F).  clip_max_ws: int workspace of B entries (overwritten).  pool: (B, T_pool) or
-// null; the fused pool requires N == 160 * T_pool.  fbw/fbs: the lane-packed filterbank of
-// asrx/mel.py lane_filterbank: fbs = band_a[64] | band_b[64] | start_a[64] | start_b[64] (even
-// starts), fbw = weights [8 tap quads][64 lanes][4] (taps 0-7 band_a, 8-31 band_b, x 1/4).
+// ld_out (>= 128*F).  ws: float workspace of asrx_logmel_ws_bytes(B, N) bytes (per-tile max | min,
+// overwritten).  pool: (B, T_pool) or null; the fused pool requires N == 160 * T_pool.  fbw/fbs: the
+// lane-packed filterbank of asrx/mel.py lane_filterbank: fbs = band_a[64] | band_b[64] | start_a[64] |
+// start_b[64] (even starts), fbw = weights [8 tap quads][64 lanes][4] (taps 0-7 band_a, 8-31 band_b,
+// x 1/4).
+static int64_t mel_tiles_per_clip(int64_t N) { return (1 + N / MEL_HOP + MEL_FPT - 1) / MEL_FPT; }
+
+extern "C" int64_t asrx_logmel_ws_bytes(int64_t B, int64_t N) {
+  return 2 * B * mel_tiles_per_clip(N) * (int64_t)sizeof(float);
+}
+
 extern "C" int asrx_logmel(const float* wav, int64_t B, int64_t N, int64_t ld_wav, const float* consts,
                            const float* fbw, const int* fbs, float* out, int layout, int64_t ld_out,
-                           int* clip_max_ws, float* pool, int64_t T_pool, hipStream_t stream) {
+                           void* ws, float* pool, int64_t T_pool, hipStream_t stream) {
   ASRX_REQUIRE(B > 0 && N > 0, "asrx_logmel: empty input");
-  ASRX_REQUIRE(B < (1 << 24), "asrx_logmel: too many clips");
+  ASRX_REQUIRE(B < 65536, "asrx_logmel: too many clips (grid y)");
   const int64_t F = 1 + N / MEL_HOP;
   ASRX_REQUIRE(ld_out >= F * MEL_BANDS, "asrx_logmel: ld_out too small");
   ASRX_REQUIRE(layout != 0 || (ld_out % 4 == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0),
                "asrx_logmel: (B, F, 128) layout needs 16-byte aligned rows");
   ASRX_REQUIRE(!pool || N == (int64_t)MEL_HOP * T_pool,
                "asrx_logmel: fused pool needs N == 160*T_pool (N=%ld T=%ld)", (long)N, (long)T_pool);
-  fill_int_kernel<<<(unsigned)((B + 255) / 256), 256, 0, stream>>>(clip_max_ws, (int)B,
-                                                                   float_to_ordered(-3.0e38f));
-  const int tiles_per_clip = (int)((F + MEL_FPT - 1) / MEL_FPT);
+  const int tiles_per_clip = (int)mel_tiles_per_clip(N);
   const int64_t n_tiles = B * tiles_per_clip;
-  // 3 resident workgroups per CU (168 VGPRs, 48.8 KB LDS) on 256 CUs; each takes a contiguous run
-  const int64_t slots = 256 * 3;
+  float* tstat = static_cast<float*>(ws);
+  // MEL_WPS resident workgroups per CU (168 VGPRs; LDS 54 KB for (B, F, 128), 48.6 KB for (B, 128, F))
+  // on 256 CUs; each takes a contiguous run
+  const int64_t slots = 256 * MEL_WPS;
   const int tiles_per_block = (int)std::max<int64_t>(1, (n_tiles + slots - 1) / slots);
   const int64_t grid = (n_tiles + tiles_per_block - 1) / tiles_per_block;
   const int vec_ok = (ld_wav % 4 == 0) && ((reinterpret_cast<uintptr_t>(wav) & 15) == 0);
-  logmel_tiles_kernel<<<(unsigned)grid, 256, 0, stream>>>(wav, N, ld_wav, vec_ok, F, tiles_per_clip, n_tiles,
-                                                          tiles_per_block, consts, fbw, fbs, out, layout, ld_out,
-                                                          clip_max_ws, pool, T_pool);
-  const int64_t per_clip = F * MEL_BANDS;
-  const int vec = (ld_out % 4 == 0) && ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
-  const unsigned gx = (unsigned)std::min<int64_t>((per_clip / (vec ? 4 : 1) + 255) / 256, 96);
-  logmel_finalize_kernel<<<dim3(gx, (unsigned)B), 256, 0, stream>>>(out, per_clip, ld_out, clip_max_ws, vec);
+  auto kern = layout == 0 ? logmel_tiles_kernel<0> : logmel_tiles_kernel<1>;
+  kern<<<(unsigned)grid, 256, 0, stream>>>(wav, N, ld_wav, vec_ok, F, tiles_per_clip, n_tiles, tiles_per_block,
+                                           consts, fbw, fbs, out, ld_out, tstat, pool, T_pool);
+  logmel_floor_kernel<<<dim3((unsigned)tiles_per_clip, (unsigned)B), 256, 0, stream>>>(
+      out, layout, F, ld_out, tiles_per_clip, n_tiles, tstat);
   ASRX_LAUNCHED("asrx_logmel");
 }
 

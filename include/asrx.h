@@ -35,11 +35,14 @@ int asrx_mel_frames(int64_t n_samples); /* 1 + N/160 (host) */
 /* wav (B,N) at row stride ld_wav; consts = window|tw512|tw1024 (see asrx/mel.py); fbw/fbs the
  * lane-packed HTK filterbank of asrx/mel.py lane_filterbank (fbs int32[256] = band_a | band_b |
  * even start bins a | b, fbw float[8][64][4] = weights/4); out (B,F,128) when layout==0 or
- * (B,128,F) when layout==1, clip stride ld_out; clip_max_ws int32[B] workspace; pool (B,T_pool)
- * or NULL (needs N == 160*T_pool). */
+ * (B,128,F) when layout==1, clip stride ld_out; ws a device workspace of asrx_logmel_ws_bytes(B, N)
+ * bytes (per-tile max | min of the log values, overwritten); pool (B,T_pool) or NULL (needs
+ * N == 160*T_pool).  Two launches: the tile transform (writes (x+4)/4 and the tile stats) and the
+ * clip-max floor, which rewrites only the tiles holding a value below max - 8. */
+int64_t asrx_logmel_ws_bytes(int64_t B, int64_t N); /* host */
 int asrx_logmel(const float* wav, int64_t B, int64_t N, int64_t ld_wav, const float* consts,
                 const float* fbw, const int* fbs, float* out, int layout, int64_t ld_out,
-                int* clip_max_ws, float* pool, int64_t T_pool, asrx_stream_t stream);
+                void* ws, float* pool, int64_t T_pool, asrx_stream_t stream);
 /* waveform feature for any clip length: adaptive_avg_pool1d(audio, T) (essentials.py:493-510), bin i the
  * mean of samples [floor(i N / T), ceil((i + 1) N / T)); wav (B, N) at row stride ld_wav, out (B, T). */
 int asrx_wave_pool(const float* wav, int64_t B, int64_t N, int64_t ld_wav, int64_t T, float* out,
