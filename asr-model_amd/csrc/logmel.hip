@@ -7,26 +7,31 @@
 //   adaptive_avg_pool1d(audio, N/160)  (exact 160-sample block means when 160 | N)
 //
 // Kernel 1 (logmel_tiles): a tile is MEL_FPT consecutive frames of one clip; the (FPT-1)*160+1024
-// samples a tile touches are staged once in LDS (each sample re-used 6.4x by the overlapping
+// samples a tile touches land in LDS once (LDS-DMA; each sample is re-used 6.4x by the overlapping
 // windows), so HBM sees every input byte about once.  Workgroups are persistent over a contiguous
-// run of tiles (XCD-aware block order, so neighbouring tiles — which share 864 samples — stay in
-// one XCD's L2) and prefetch the next tile's samples into registers while the current one is
-// transformed.  Each wave owns one frame at a time and never synchronises with the other waves
+// run of tiles (XCD-aware block order, so neighbouring tiles -- which share 864 samples -- stay in
+// one XCD's L2).  Each wave owns one frame at a time and never synchronises with the other waves
 // inside a frame: per frame it
 //   * packs the windowed real frame as z[n] = x[2n] w[2n] + i x[2n+1] w[2n+1] (lane j holds
-//     n = j + 64 r, r = 0..7; the window values are lane constants kept in VGPRs),
-//   * runs a 512-point complex FFT as three radix-8 Stockham passes whose twiddles are lane
-//     constants in VGPRs; the two inter-pass transposes go through a per-wave LDS buffer padded
-//     with one slot every 8 (p(i) = i + i/8) so the stride-8 writes are bank-conflict free,
-//   * untangles the real spectrum (lane j already holds Z[j + 64 r]; only the mirrored Z[512-k]
-//     is read back) and forms 4|X_k|^2 (the factor 4 is folded into the filterbank weights),
-//   * applies the sparse filterbank: lane m owns bands m (<= FB_LO taps) and m + 64 (<= FB_HI
-//     taps) with the weights in VGPRs, reading the power bins by immediate LDS offsets,
-//   * takes log10 as log2 * log10(2) (v_log_f32).
-// Per tile the block stages the 128 x FPT log values in LDS, writes them with coalesced stores in
-// (B, F, 128) or (B, 128, F) layout and folds its maximum into the clip's ordered-int atomicMax.
-// The fused waveform pool reads the same LDS samples.
-// Kernel 2 (logmel_finalize): x -> (max(x, clipmax - 8) + 4) / 4 in place, float4.
+//     n = j + 64 r, r = 0..7, one complex value per aligned VGPR pair; the window values are lane
+//     constants),
+//   * runs the 512-point complex FFT as three radix-8 stages over the register index (n = j + 64 n2,
+//     j = n0 + 8 n1): DFT over n2 and twiddle W512^(j kA); swap lane bits 3-5 with the register bits;
+//     DFT over n1 and twiddle W64^(n0 kB); swap lane bits 0-2 with the register bits; DFT over n0.
+//     The lane/register swaps never touch LDS: bits 5 and 4 are v_permlane32/16_swap, bits 3..0 one
+//     v_cndmask_b32 with a DPP-read source per register (row_ror / quad_perm).  The complex arithmetic
+//     is packed FP32 (v_pk_add/mul/fma_f32 with op_sel / neg modifiers for the swaps and signs),
+//   * stores Z (digit-reversed in the lanes) to a padded per-wave LDS buffer in natural order, reads
+//     the mirrored Z[512-k] back, untangles the real spectrum and forms 4|X_k|^2 (the factor 4 is
+//     folded into the filterbank weights),
+//   * applies the sparse filterbank: lane m owns bands m (<= FB_A taps) and m + 64 (<= FB_B taps),
+//     weights re-read from LDS per frame, bins read by immediate LDS offsets, even and odd taps
+//     accumulated in the two halves of a packed pair,
+//   * takes log10 as log2 * log10(2) (v_log_f32) and stores (x + 4) / 4.
+// Per tile the block writes its max and min log value (over live frames) to a workspace; the fused
+// waveform pool reads the same LDS samples (16 threads per frame, DPP row sums).
+// Kernel 2 (logmel_floor): the clip-max floor, max(x, clipmax - 8), on the (x + 4) / 4 values; a tile
+// whose minimum is not below the floor is skipped.
 #include "common.h"
 #include "fft.h"
 
@@ -46,6 +51,10 @@ constexpr int MEL_WAVES = 4;
 #endif
 #ifndef MEL_NBUF0
 #define MEL_NBUF0 1  // sample buffers of the (B, F, 128) kernel (2: measured no faster, and 54 KB of LDS fits only 2 workgroups per CU)
+#endif
+#ifndef MEL_ABL
+#define MEL_ABL 0  // timing ablations (wrong results): 1 no sample loads, 2 no mirror exchange, 4 no filterbank
+                   // reads, 8 no lane exchanges (64 only bits 5-4, 128 only bits 3-0), 16 no stores, 32 no pool
 #endif
 #ifndef MEL_STAGE0
 #define MEL_STAGE0 0  // 1: (B, F, 128) output staged in LDS and stored as float4 rows
@@ -93,59 +102,150 @@ __device__ __forceinline__ void xch_pair(float& a, float& c) {
 // lane i read lane (i - n) mod 16 of its row, so i + 4 is row_ror:12 and i - 4 row_ror:4; bits 1 and
 // 0 are quad_perm xor 2 / xor 1 both ways, bit 3 row_ror:8 both ways.  The leading s_nop 1 covers the
 // VALU-write -> DPP-read hazard on the inputs; the outputs are fresh registers.
-#define ASRX_XCH4(UPS, DNS)                                                                                    \
+#define ASRX_XCH8(UPS, DNS)                                                                                    \
   asm("s_mov_b64 vcc, %[ms]\n\ts_nop 1\n\t"                                                                 \
-      "v_cndmask_b32_dpp %[c0], %[a0i], %[c0i], vcc " UPS " row_mask:0xf bank_mask:0xf\n\t"                    \
-      "v_cndmask_b32_dpp %[c1], %[a1i], %[c1i], vcc " UPS " row_mask:0xf bank_mask:0xf\n\t"                    \
-      "v_cndmask_b32_dpp %[c2], %[a2i], %[c2i], vcc " UPS " row_mask:0xf bank_mask:0xf\n\t"                    \
-      "v_cndmask_b32_dpp %[c3], %[a3i], %[c3i], vcc " UPS " row_mask:0xf bank_mask:0xf\n\t"                    \
+      "v_cndmask_b32_dpp %[c0], %[a0i], %[c0i], vcc " UPS " row_mask:0xf bank_mask:0xf\n\t"   \
+      "v_cndmask_b32_dpp %[c1], %[a1i], %[c1i], vcc " UPS " row_mask:0xf bank_mask:0xf\n\t"   \
+      "v_cndmask_b32_dpp %[c2], %[a2i], %[c2i], vcc " UPS " row_mask:0xf bank_mask:0xf\n\t"   \
+      "v_cndmask_b32_dpp %[c3], %[a3i], %[c3i], vcc " UPS " row_mask:0xf bank_mask:0xf\n\t"   \
+      "v_cndmask_b32_dpp %[c4], %[a4i], %[c4i], vcc " UPS " row_mask:0xf bank_mask:0xf\n\t"   \
+      "v_cndmask_b32_dpp %[c5], %[a5i], %[c5i], vcc " UPS " row_mask:0xf bank_mask:0xf\n\t"   \
+      "v_cndmask_b32_dpp %[c6], %[a6i], %[c6i], vcc " UPS " row_mask:0xf bank_mask:0xf\n\t"   \
+      "v_cndmask_b32_dpp %[c7], %[a7i], %[c7i], vcc " UPS " row_mask:0xf bank_mask:0xf\n\t"   \
       "s_mov_b64 vcc, %[mc]\n\t"                                                                             \
-      "v_cndmask_b32_dpp %[a0], %[c0i], %[a0i], vcc " DNS " row_mask:0xf bank_mask:0xf\n\t"                    \
-      "v_cndmask_b32_dpp %[a1], %[c1i], %[a1i], vcc " DNS " row_mask:0xf bank_mask:0xf\n\t"                    \
-      "v_cndmask_b32_dpp %[a2], %[c2i], %[a2i], vcc " DNS " row_mask:0xf bank_mask:0xf\n\t"                    \
-      "v_cndmask_b32_dpp %[a3], %[c3i], %[a3i], vcc " DNS " row_mask:0xf bank_mask:0xf"                          \
-      : [a0] "=&v"(a0), [a1] "=&v"(a1), [a2] "=&v"(a2), [a3] "=&v"(a3), [c0] "=&v"(c0), [c1] "=&v"(c1),          \
-        [c2] "=&v"(c2), [c3] "=&v"(c3)                                                                          \
-      : [a0i] "v"(*pa[0]), [a1i] "v"(*pa[1]), [a2i] "v"(*pa[2]), [a3i] "v"(*pa[3]), [c0i] "v"(*pc[0]),          \
-        [c1i] "v"(*pc[1]), [c2i] "v"(*pc[2]), [c3i] "v"(*pc[3]), [ms] "s"(mset), [mc] "s"(~mset)                \
+      "v_cndmask_b32_dpp %[a0], %[c0i], %[a0i], vcc " DNS " row_mask:0xf bank_mask:0xf\n\t"   \
+      "v_cndmask_b32_dpp %[a1], %[c1i], %[a1i], vcc " DNS " row_mask:0xf bank_mask:0xf\n\t"   \
+      "v_cndmask_b32_dpp %[a2], %[c2i], %[a2i], vcc " DNS " row_mask:0xf bank_mask:0xf\n\t"   \
+      "v_cndmask_b32_dpp %[a3], %[c3i], %[a3i], vcc " DNS " row_mask:0xf bank_mask:0xf\n\t"   \
+      "v_cndmask_b32_dpp %[a4], %[c4i], %[a4i], vcc " DNS " row_mask:0xf bank_mask:0xf\n\t"   \
+      "v_cndmask_b32_dpp %[a5], %[c5i], %[a5i], vcc " DNS " row_mask:0xf bank_mask:0xf\n\t"   \
+      "v_cndmask_b32_dpp %[a6], %[c6i], %[a6i], vcc " DNS " row_mask:0xf bank_mask:0xf\n\t"   \
+      "v_cndmask_b32_dpp %[a7], %[c7i], %[a7i], vcc " DNS " row_mask:0xf bank_mask:0xf"   \
+      : [a0] "=&v"(pa[0]), [a1] "=&v"(pa[1]), [a2] "=&v"(pa[2]), [a3] "=&v"(pa[3]), [a4] "=&v"(pa[4]), [a5] "=&v"(pa[5]), [a6] "=&v"(pa[6]), [a7] "=&v"(pa[7]), [c0] "=&v"(pc[0]), [c1] "=&v"(pc[1]), [c2] "=&v"(pc[2]), [c3] "=&v"(pc[3]), [c4] "=&v"(pc[4]), [c5] "=&v"(pc[5]), [c6] "=&v"(pc[6]), [c7] "=&v"(pc[7]) \
+      : [a0i] "v"(ia[0]), [a1i] "v"(ia[1]), [a2i] "v"(ia[2]), [a3i] "v"(ia[3]), [a4i] "v"(ia[4]), [a5i] "v"(ia[5]), [a6i] "v"(ia[6]), [a7i] "v"(ia[7]), [c0i] "v"(ic[0]), [c1i] "v"(ic[1]), [c2i] "v"(ic[2]), [c3i] "v"(ic[3]), [c4i] "v"(ic[4]), [c5i] "v"(ic[5]), [c6i] "v"(ic[6]), [c7i] "v"(ic[7]), [ms] "s"(mset), [mc] "s"(~mset) \
       : "vcc")
+// one stage, eight register pairs (x and y of four complex pairs) in one statement: two VCC loads and
+// one s_nop per stage
 template <int B>
-__device__ __forceinline__ void xch_dpp4(float* const (&pa)[4], float* const (&pc)[4]) {
+__device__ __forceinline__ void xch_dpp8(float (&pa)[8], float (&pc)[8]) {
   constexpr uint64_t mset = B == 3 ? 0xFF00FF00FF00FF00ull
                           : B == 2 ? 0xF0F0F0F0F0F0F0F0ull
                           : B == 1 ? 0xCCCCCCCCCCCCCCCCull
                                    : 0xAAAAAAAAAAAAAAAAull;
-  float a0, a1, a2, a3, c0, c1, c2, c3;
-  if constexpr (B == 3) ASRX_XCH4("row_ror:8", "row_ror:8");
-  else if constexpr (B == 2) ASRX_XCH4("row_ror:12", "row_ror:4");
-  else if constexpr (B == 1) ASRX_XCH4("quad_perm:[2,3,0,1]", "quad_perm:[2,3,0,1]");
-  else ASRX_XCH4("quad_perm:[1,0,3,2]", "quad_perm:[1,0,3,2]");
-  *pa[0] = a0; *pa[1] = a1; *pa[2] = a2; *pa[3] = a3;
-  *pc[0] = c0; *pc[1] = c1; *pc[2] = c2; *pc[3] = c3;
+  float ia[8], ic[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    ia[i] = pa[i];
+    ic[i] = pc[i];
+  }
+  if constexpr (B == 3) ASRX_XCH8("row_ror:8", "row_ror:8");
+  else if constexpr (B == 2) ASRX_XCH8("row_ror:12", "row_ror:4");
+  else if constexpr (B == 1) ASRX_XCH8("quad_perm:[2,3,0,1]", "quad_perm:[2,3,0,1]");
+  else ASRX_XCH8("quad_perm:[1,0,3,2]", "quad_perm:[1,0,3,2]");
 }
-#undef ASRX_XCH4
+#undef ASRX_XCH8
 // lane bit B <-> register bit (B % 3): 5 and 2 pair registers r, r + 4; 4 and 1 pair r, r + 2; 3 and
 // 0 pair r, r + 1
+typedef float f2v __attribute__((ext_vector_type(2)));
 template <int B>
-__device__ __forceinline__ void xch_lanes(cpx (&v)[8]) {
+__device__ __forceinline__ void xch_lanes(f2v (&v)[8]) {
   constexpr int RB = 1 << (B % 3);
-  constexpr int R0 = RB == 1 ? 0 : 0, R1 = RB == 1 ? 2 : RB == 2 ? 1 : 1, R2 = RB == 1 ? 4 : RB == 2 ? 4 : 2,
-                R3 = RB == 1 ? 6 : RB == 2 ? 5 : 3;  // the four registers r with bit RB clear
+  constexpr int R[4] = {0, RB == 1 ? 2 : 1, RB == 4 ? 2 : 4, RB == 1 ? 6 : RB == 2 ? 5 : 3};  // bit RB clear
   if constexpr (B >= 4) {
+    // the eight swaps of the stage in one statement behind one s_nop (no swap reads another's output)
+    float a[8], c[8];
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      if (r & RB) continue;
-      xch_pair<B>(v[r].x, v[r + RB].x);
-      xch_pair<B>(v[r].y, v[r + RB].y);
+    for (int i = 0; i < 4; ++i) {
+      a[2 * i] = v[R[i]].x;
+      a[2 * i + 1] = v[R[i]].y;
+      c[2 * i] = v[R[i] + RB].x;
+      c[2 * i + 1] = v[R[i] + RB].y;
+    }
+#define ASRX_SW(OP)                                                                                           \
+  asm("s_nop 1\n\t" OP " %0, %8\n\t" OP " %1, %9\n\t" OP " %2, %10\n\t" OP " %3, %11\n\t" OP " %4, %12\n\t" OP  \
+      " %5, %13\n\t" OP " %6, %14\n\t" OP " %7, %15"                                                             \
+      : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7]), "+v"(c[0]), \
+        "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]))
+    if constexpr (B == 5) ASRX_SW("v_permlane32_swap_b32");
+    else ASRX_SW("v_permlane16_swap_b32");
+#undef ASRX_SW
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[R[i]] = f2v{a[2 * i], a[2 * i + 1]};
+      v[R[i] + RB] = f2v{c[2 * i], c[2 * i + 1]};
     }
   } else {
-    float* const ax[4] = {&v[R0].x, &v[R1].x, &v[R2].x, &v[R3].x};
-    float* const cx[4] = {&v[R0 + RB].x, &v[R1 + RB].x, &v[R2 + RB].x, &v[R3 + RB].x};
-    float* const ay[4] = {&v[R0].y, &v[R1].y, &v[R2].y, &v[R3].y};
-    float* const cy[4] = {&v[R0 + RB].y, &v[R1 + RB].y, &v[R2 + RB].y, &v[R3 + RB].y};
-    xch_dpp4<B>(ax, cx);
-    xch_dpp4<B>(ay, cy);
+    float a[8], c[8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      a[2 * i] = v[R[i]].x;
+      a[2 * i + 1] = v[R[i]].y;
+      c[2 * i] = v[R[i] + RB].x;
+      c[2 * i + 1] = v[R[i] + RB].y;
+    }
+    xch_dpp8<B>(a, c);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[R[i]] = f2v{a[2 * i], a[2 * i + 1]};
+      v[R[i] + RB] = f2v{c[2 * i], c[2 * i + 1]};
+    }
   }
+}
+
+// ---- packed complex arithmetic (a complex value is one aligned VGPR pair: x = re, y = im).  Each
+// helper is one VOP3P instruction (v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32 with op_sel / neg
+// modifiers doing the swaps and sign flips), two for the general product.
+__device__ __forceinline__ f2v pk_cmul(f2v a, f2v b) {  // a b
+  f2v t, r;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "v"(b));  // (ax bx, ax by)
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,0,0]"  // (-ay by, ay bx) + t
+      : "=v"(r) : "v"(a), "v"(b), "v"(t));
+  return r;
+}
+__device__ __forceinline__ f2v pk_add_negi(f2v q, f2v d) {  // q + (-i) d = (qx + dy, qy - dx)
+  f2v r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(q), "v"(d));
+  return r;
+}
+__device__ __forceinline__ f2v pk_sub_negi(f2v q, f2v d) {  // q - (-i) d = (qx - dy, qy + dx)
+  f2v r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(q), "v"(d));
+  return r;
+}
+__device__ __forceinline__ f2v pk_conj_add(f2v a, f2v b) {  // a + conj b = (ax + bx, ay - by)
+  f2v r;
+  asm("v_pk_add_f32 %0, %1, %2 neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ f2v pk_untangle_odd(f2v zk, f2v zn) {  // (-i)(zk - conj zn) = (zk.y + zn.y, zn.x - zk.x)
+  f2v r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[0,0] neg_hi:[1,0]" : "=v"(r) : "v"(zk), "v"(zn));
+  return r;
+}
+// 8-point DFT over the registers, y[q] = sum_r x[r] exp(-2 pi i r q / 8) -- asrx_fft::dft8's
+// decimation-in-frequency graph on packed complex values (28 VOP3P instructions)
+__device__ __forceinline__ void pk_dft8(f2v (&v)[8]) {
+  const float h = 0.70710678118654752f;
+  const f2v a0 = v[0] + v[4], a1 = v[1] + v[5], a2 = v[2] + v[6], a3 = v[3] + v[7];
+  const f2v b0 = v[0] - v[4], b2 = v[2] - v[6];
+  f2v b1 = v[1] - v[5], b3 = v[3] - v[7];
+  {
+    f2v t1, t3;  // b1 (h - ih) = h (b1x + b1y, b1y - b1x); b3 (-h - ih) = -h (b3x - b3y, b3y + b3x)
+    asm("v_pk_add_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(t1) : "v"(b1));
+    asm("v_pk_add_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(t3) : "v"(b3));
+    b1 = t1 * f2v{h, h};
+    b3 = t3 * f2v{-h, -h};
+  }
+  const f2v p0 = a0 + a2, p1 = a1 + a3, q0 = a0 - a2, d = a1 - a3;
+  const f2v s0 = pk_add_negi(b0, b2), t0 = pk_sub_negi(b0, b2), s1 = b1 + b3, d2 = b1 - b3;
+  v[0] = p0 + p1;
+  v[4] = p0 - p1;
+  v[2] = pk_add_negi(q0, d);
+  v[6] = pk_sub_negi(q0, d);
+  v[1] = s0 + s1;
+  v[5] = s0 - s1;
+  v[3] = pk_add_negi(t0, d2);
+  v[7] = pk_sub_negi(t0, d2);
 }
 
 // Orders this wave's LDS accesses (the LDS unit executes one wave's DS instructions in order;
@@ -159,7 +259,6 @@ __device__ __forceinline__ void wave_lds_sync() {
 // of these reads into ds_read2_b64 / ds_read2st64_b64, which the LDS services at half the rate
 // (MI355X_MICROARCH.md LDS table).  The loads are issued back to back and completed by one
 // lgkmcnt(0) wait that also names every destination, so no use can be scheduled before it.
-typedef float f2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t lds_off(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
 }
@@ -241,17 +340,17 @@ __global__ __launch_bounds__(256, MEL_WPS) void logmel_tiles_kernel(
   const float* win = consts;
   const cpx* tw512 = reinterpret_cast<const cpx*>(consts + MEL_NFFT);
   const cpx* tw1024 = reinterpret_cast<const cpx*>(consts + MEL_NFFT + 1024);
-  float2 wv[8];
-  cpx twa[7], twb[7];
-#pragma unroll
-  for (int r = 0; r < 8; ++r) wv[r] = *reinterpret_cast<const float2*>(win + 2 * (lane + 64 * r));
+  const f2v* tw512v = reinterpret_cast<const f2v*>(tw512);
   // the bin index lane j holds after the third stage: kj + 64 r, kj = (j >> 3) + 8 (j & 7)
   const int kj = (lane >> 3) + 8 * (lane & 7);
-  const cpx tu0 = tw1024[kj];
+  f2v wv[8], twa[7], twb[7];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) wv[r] = *reinterpret_cast<const f2v*>(win + 2 * (lane + 64 * r));
+  const f2v tu0 = reinterpret_cast<const f2v*>(tw1024)[kj];
 #pragma unroll
   for (int r = 1; r < 8; ++r) {
-    twa[r - 1] = tw512[(r * lane) & 511];            // W512^(j kA)
-    twb[r - 1] = tw512[(r * (lane & 7) * 8) & 511];  // W64^(n0 kB)
+    twa[r - 1] = tw512v[(r * lane) & 511];            // W512^(j kA)
+    twb[r - 1] = tw512v[(r * (lane & 7) * 8) & 511];  // W64^(n0 kB)
   }
   // lane-packed filterbank (asrx/mel.py lane_filterbank): lane m owns band_a (<= 8 taps from the
   // even bin sa) and band_b (<= 24 taps from the even bin sb); weights [tap/4][lane][4] in LDS
@@ -260,6 +359,7 @@ __global__ __launch_bounds__(256, MEL_WPS) void logmel_tiles_kernel(
   for (int i = tid; i < FB_QUADS * 64; i += 256) fbw_s[i] = reinterpret_cast<const float4*>(fbw)[i];
 
   cpx* S = fbuf[wid];
+  f2v* Sv = reinterpret_cast<f2v*>(S);
   float* P = reinterpret_cast<float*>(S);
 
   // tile t's samples -> dst.  Interior tiles: LDS-DMA (global_load_lds_dwordx4, 1 KB per wave
@@ -294,7 +394,9 @@ __global__ __launch_bounds__(256, MEL_WPS) void logmel_tiles_kernel(
     float* samp = samp_buf[NBUF == 2 ? (int)((t - t_begin) & 1) : 0];
     if constexpr (NBUF == 1) {
       __syncthreads();  // the previous tile's readers are done with samp / melst
+#if !(MEL_ABL & 1)
       stage(t, samp);
+#endif
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // samp published; with two buffers also: every wave is done with the other one
@@ -302,15 +404,24 @@ __global__ __launch_bounds__(256, MEL_WPS) void logmel_tiles_kernel(
       if (t + 1 < t_end) stage(t + 1, samp_buf[(int)((t + 1 - t_begin) & 1)]);
     }
 
-    // fused waveform feature: exact 160-sample block means (pool index == frame index)
-    if (pool) {
-      for (int fi = wid; fi < MEL_FPT; fi += MEL_WAVES) {
+    // fused waveform feature: exact 160-sample block means (pool index == frame index).  Sixteen
+    // threads per frame, each summing 10 consecutive samples, then a DPP sum inside the 16-lane row
+    // (quad_perm xor 1, xor 2, row_half_mirror, row_mirror): no LDS round trips
+    static_assert(MEL_HOP == 16 * 10, "the pool splits a hop into 16 runs of 10 samples");
+    if (pool && !(MEL_ABL & 32)) {
+#pragma unroll 1
+      for (int i = tid; i < MEL_FPT * 16; i += 256) {
+        const int fi = i >> 4, part = i & 15;
+        const float* q = samp + MEL_NFFT / 2 + fi * MEL_HOP + part * 10;
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < 10; ++k) s += q[k];
+        s += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, s), 0xB1, 0xF, 0xF, false));
+        s += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, s), 0x4E, 0xF, 0xF, false));
+        s += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, s), 0x141, 0xF, 0xF, false));
+        s += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, s), 0x140, 0xF, 0xF, false));
         const int64_t f = f0 + fi;
-        if (f >= T_pool) break;
-        const int base = MEL_NFFT / 2 + fi * MEL_HOP;
-        float s = samp[base + lane] + samp[base + lane + 64] + (lane < 32 ? samp[base + lane + 128] : 0.f);
-        s = wave_sum(s);
-        if (lane == 0) pool[b * T_pool + f] = s * (1.0f / MEL_HOP);
+        if (part == 0 && f < T_pool) pool[b * T_pool + f] = s * (1.0f / MEL_HOP);
       }
     }
 
@@ -318,55 +429,67 @@ __global__ __launch_bounds__(256, MEL_WPS) void logmel_tiles_kernel(
 #pragma unroll 1
     for (int fi = wid; fi < MEL_FPT; fi += MEL_WAVES) {
       const bool live = f0 + fi < F;  // wave-uniform
-      cpx v[8];
-      {
-        f2v sv[8];
-        ds_rd64x8<0, 512>(lds_off(samp + fi * MEL_HOP + 2 * lane), sv);
+      f2v v[8];
+      ds_rd64x8<0, 512>(lds_off(samp + fi * MEL_HOP + 2 * lane), v);
 #pragma unroll
-        for (int r = 0; r < 8; ++r) v[r] = cpx{sv[r].x * wv[r].x, sv[r].y * wv[r].y};
-      }
+      for (int r = 0; r < 8; ++r) v[r] *= wv[r];
       // stage A: DFT over n2 (registers) -> kA, twiddle W512^(j kA)
-      asrx_fft::dft8(v);
+      pk_dft8(v);
 #pragma unroll
-      for (int r = 1; r < 8; ++r) v[r] = asrx_fft::cmul(v[r], twa[r - 1]);
+      for (int r = 1; r < 8; ++r) v[r] = pk_cmul(v[r], twa[r - 1]);
       // lane bits 3-5 (n1) <-> register bits 0-2 (kA): lane = n0 + 8 kA, registers n1
+#if !(MEL_ABL & (8 | 64))
       xch_lanes<5>(v);
+#endif
+#if !(MEL_ABL & (8 | 64))
       xch_lanes<4>(v);
+#endif
+#if !(MEL_ABL & (8 | 128))
       xch_lanes<3>(v);
+#endif
       // stage B: DFT over n1 -> kB, twiddle W64^(n0 kB)
-      asrx_fft::dft8(v);
+      pk_dft8(v);
 #pragma unroll
-      for (int r = 1; r < 8; ++r) v[r] = asrx_fft::cmul(v[r], twb[r - 1]);
+      for (int r = 1; r < 8; ++r) v[r] = pk_cmul(v[r], twb[r - 1]);
       // lane bits 0-2 (n0) <-> register bits 0-2 (kB): lane = kB + 8 kA, registers n0
+#if !(MEL_ABL & (8 | 128))
       xch_lanes<2>(v);
+#endif
+#if !(MEL_ABL & (8 | 128))
       xch_lanes<1>(v);
+#endif
+#if !(MEL_ABL & (8 | 128))
       xch_lanes<0>(v);
+#endif
       // stage C: DFT over n0 -> kC; lane j register r now holds Z[kj + 64 r]
-      asrx_fft::dft8(v);
+      pk_dft8(v);
       // the one LDS exchange: Z in natural order (padded, zpad), Z_0 also at slot
       // zpad(512) for the mirror of lane 0's register 0
 #pragma unroll
-      for (int r = 0; r < 8; ++r) S[zpad(kj) + 72 * r] = v[r];
-      if (lane == 0) S[zpad(512)] = v[0];
+      for (int r = 0; r < 8; ++r) Sv[zpad(kj) + 72 * r] = v[r];
+      if (lane == 0) Sv[zpad(512)] = v[0];
       wave_lds_sync();
       f2v zm[8];  // zm[7 - r] = Z[(512 - kj - 64 r) & 511] = S[zpad(64 - kj) + 72 (7 - r)]
+#if MEL_ABL & 2
+#pragma unroll
+      for (int r = 0; r < 8; ++r) zm[r] = v[7 - r] * 0.5f;
+#else
       ds_rd64x8<0, 576>(lds_off(S + zpad(64 - kj)), zm);
+#endif
       // real-FFT untangle: 2 X_k = (Z_k + conj Z_{512-k}) + W1024^k (-i)(Z_k - conj Z_{512-k})
       // W1024^(kj + 64 r) = W1024^kj exp(-i pi r / 8) = u[r & 3] (-i)^(r >> 2)
-      cpx u[4];
+      f2v u[4];
       u[0] = tu0;
 #pragma unroll
-      for (int r = 1; r < 4; ++r) u[r] = asrx_fft::cmul(tu0, cpx{kRot[r][0], kRot[r][1]});
+      for (int r = 1; r < 4; ++r) u[r] = pk_cmul(tu0, f2v{kRot[r][0], kRot[r][1]});
       float pw[8];
 #pragma unroll
       for (int r = 0; r < 8; ++r) {
-        const cpx zn{zm[7 - r].x, zm[7 - r].y};
-        const cpx zk = v[r];
-        const cpx e{zk.x + zn.x, zk.y - zn.y};
-        const cpx o{zk.y + zn.y, zn.x - zk.x};
-        const cpx w = asrx_fft::cmul(u[r & 3], o);
-        const float re = r < 4 ? e.x + w.x : e.x + w.y, im = r < 4 ? e.y + w.y : e.y - w.x;  // (-i) w = (w.y, -w.x)
-        pw[r] = re * re + im * im;  // 4 |X_k|^2
+        const f2v zn = zm[7 - r], zk = v[r];
+        const f2v e = pk_conj_add(zk, zn);                         // Z_k + conj Z_{512-k}
+        const f2v w = pk_cmul(u[r & 3], pk_untangle_odd(zk, zn));  // W (-i)(Z_k - conj Z_{512-k}), W = u (-i)^(r>>2)
+        const f2v x = r < 4 ? e + w : pk_add_negi(e, w);
+        pw[r] = fmaf(x.x, x.x, x.y * x.y);  // 4 |X_k|^2
       }
       wave_lds_sync();
 #pragma unroll
@@ -380,8 +503,13 @@ __global__ __launch_bounds__(256, MEL_WPS) void logmel_tiles_kernel(
       static_assert(FB_A == 8 && FB_B == 24, "the filterbank reads below are written out for 8 + 24 taps");
       // three read groups (bins | weight quads), each drained before the next, so at most 32 VGPRs
       // of operands are live: band a (8 bins), band b taps 0-15, band b taps 16-23
+#if MEL_ABL & 4
+      float acc_a = P[lane], acc_b = P[lane + 64];
+#else
       const uint32_t wa = lds_off(fbw_s + lane);
       float acc_a = 0.f, acc_b = 0.f;
+      // packed: the even and odd taps accumulate in the two halves, added at the end
+      f2v sa = {0.f, 0.f}, sb = {0.f, 0.f};
       {
         f2v p[4];
         p[0] = ds_rd64<0>(lds_off(P + 2 * sa2));
@@ -390,27 +518,38 @@ __global__ __launch_bounds__(256, MEL_WPS) void logmel_tiles_kernel(
         p[3] = ds_rd64<24>(lds_off(P + 2 * sa2));
         f4v w0 = ds_rd128<0>(wa), w1 = ds_rd128<1024>(wa);
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(p[0]), "+v"(p[1]), "+v"(p[2]), "+v"(p[3]), "+v"(w0), "+v"(w1) : : "memory");
-        acc_a = fmaf(w0.x, p[0].x, fmaf(w0.y, p[0].y, fmaf(w0.z, p[1].x, fmaf(w0.w, p[1].y, acc_a))));
-        acc_a = fmaf(w1.x, p[2].x, fmaf(w1.y, p[2].y, fmaf(w1.z, p[3].x, fmaf(w1.w, p[3].y, acc_a))));
+        sa = __builtin_elementwise_fma(w0.xy, p[0], sa);
+        sa = __builtin_elementwise_fma(w0.zw, p[1], sa);
+        sa = __builtin_elementwise_fma(w1.xy, p[2], sa);
+        sa = __builtin_elementwise_fma(w1.zw, p[3], sa);
       }
       {
         f2v p[8];
         ds_rd64x8<0, 8>(lds_off(P + 2 * sb2), p);
         f4v w0 = ds_rd128<2048>(wa), w1 = ds_rd128<3072>(wa), w2 = ds_rd128<4096>(wa), w3 = ds_rd128<5120>(wa);
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(w0), "+v"(w1), "+v"(w2), "+v"(w3) : : "memory");
-        acc_b = fmaf(w0.x, p[0].x, fmaf(w0.y, p[0].y, fmaf(w0.z, p[1].x, fmaf(w0.w, p[1].y, acc_b))));
-        acc_b = fmaf(w1.x, p[2].x, fmaf(w1.y, p[2].y, fmaf(w1.z, p[3].x, fmaf(w1.w, p[3].y, acc_b))));
-        acc_b = fmaf(w2.x, p[4].x, fmaf(w2.y, p[4].y, fmaf(w2.z, p[5].x, fmaf(w2.w, p[5].y, acc_b))));
-        acc_b = fmaf(w3.x, p[6].x, fmaf(w3.y, p[6].y, fmaf(w3.z, p[7].x, fmaf(w3.w, p[7].y, acc_b))));
+        sb = __builtin_elementwise_fma(w0.xy, p[0], sb);
+        sb = __builtin_elementwise_fma(w0.zw, p[1], sb);
+        sb = __builtin_elementwise_fma(w1.xy, p[2], sb);
+        sb = __builtin_elementwise_fma(w1.zw, p[3], sb);
+        sb = __builtin_elementwise_fma(w2.xy, p[4], sb);
+        sb = __builtin_elementwise_fma(w2.zw, p[5], sb);
+        sb = __builtin_elementwise_fma(w3.xy, p[6], sb);
+        sb = __builtin_elementwise_fma(w3.zw, p[7], sb);
       }
       {
         f2v p[4];
         ds_rd64x4<64, 8>(lds_off(P + 2 * sb2), p);
         f4v w0 = ds_rd128<6144>(wa), w1 = ds_rd128<7168>(wa);
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(w0), "+v"(w1) : : "memory");
-        acc_b = fmaf(w0.x, p[0].x, fmaf(w0.y, p[0].y, fmaf(w0.z, p[1].x, fmaf(w0.w, p[1].y, acc_b))));
-        acc_b = fmaf(w1.x, p[2].x, fmaf(w1.y, p[2].y, fmaf(w1.z, p[3].x, fmaf(w1.w, p[3].y, acc_b))));
+        sb = __builtin_elementwise_fma(w0.xy, p[0], sb);
+        sb = __builtin_elementwise_fma(w0.zw, p[1], sb);
+        sb = __builtin_elementwise_fma(w1.xy, p[2], sb);
+        sb = __builtin_elementwise_fma(w1.zw, p[3], sb);
       }
+      acc_a = sa.x + sa.y;
+      acc_b = sb.x + sb.y;
+#endif
       wave_lds_sync();
       // clamp(1e-10).log10(): the clamped value maps to exactly -10 like the correctly rounded
       // library log10; elsewhere log2 * log10(2) is within a few ulp
@@ -421,7 +560,7 @@ __global__ __launch_bounds__(256, MEL_WPS) void logmel_tiles_kernel(
       // as x -> fl(x + 4) is monotone and / 4 is exact
       const float y_a = (l_a + 4.0f) * 0.25f, y_b = (l_b + 4.0f) * 0.25f;
       if constexpr (!STAGED) {
-        if (live) {
+        if (live && !(MEL_ABL & 16)) {
           float* orow = out + b * ld_out + (f0 + fi) * MEL_BANDS;
           orow[band_a] = y_a;
           orow[band_b] = y_b;
@@ -435,8 +574,8 @@ __global__ __launch_bounds__(256, MEL_WPS) void logmel_tiles_kernel(
         lmin = fminf(lmin, fminf(l_a, l_b));
       }
     }
-    lmax = wave_max(lmax);
-    lmin = -wave_max(-lmin);
+    lmax = wave_max_dpp(lmax);
+    lmin = -wave_max_dpp(-lmin);
     if (lane == 0) {
       red[0][wid] = lmax;
       red[1][wid] = lmin;
