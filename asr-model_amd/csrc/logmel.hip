@@ -52,6 +52,9 @@ constexpr int MEL_WAVES = 4;
 #ifndef MEL_NBUF0
 #define MEL_NBUF0 1  // sample buffers of the (B, F, 128) kernel (2: measured no faster, and 54 KB of LDS fits only 2 workgroups per CU)
 #endif
+#ifndef MEL_ILP
+#define MEL_ILP 1  // frames per wave in flight at once
+#endif
 #ifndef MEL_ABL
 #define MEL_ABL 0  // timing ablations (wrong results): 1 no sample loads, 2 no mirror exchange, 4 no filterbank
                    // reads, 8 no lane exchanges (64 only bits 5-4, 128 only bits 3-0), 16 no stores, 32 no pool
@@ -295,6 +298,44 @@ __device__ __forceinline__ f4v ds_rd128(uint32_t a) {
   return r;
 }
 
+// the same reads without the wait: completed by lgkm_wait on every destination
+template <int OFF0, int STRIDE>
+__device__ __forceinline__ void ds_rd64x8_nw(uint32_t a, f2v (&o)[8]) {
+  o[0] = ds_rd64<OFF0>(a);
+  o[1] = ds_rd64<OFF0 + STRIDE>(a);
+  o[2] = ds_rd64<OFF0 + 2 * STRIDE>(a);
+  o[3] = ds_rd64<OFF0 + 3 * STRIDE>(a);
+  o[4] = ds_rd64<OFF0 + 4 * STRIDE>(a);
+  o[5] = ds_rd64<OFF0 + 5 * STRIDE>(a);
+  o[6] = ds_rd64<OFF0 + 6 * STRIDE>(a);
+  o[7] = ds_rd64<OFF0 + 7 * STRIDE>(a);
+}
+template <int OFF0, int STRIDE>
+__device__ __forceinline__ void ds_rd64x4_nw(uint32_t a, f2v (&o)[4]) {
+  o[0] = ds_rd64<OFF0>(a);
+  o[1] = ds_rd64<OFF0 + STRIDE>(a);
+  o[2] = ds_rd64<OFF0 + 2 * STRIDE>(a);
+  o[3] = ds_rd64<OFF0 + 3 * STRIDE>(a);
+}
+// s_waitcnt lgkmcnt(0) naming every register of the arrays, so no use is scheduled before it
+template <int N>
+__device__ __forceinline__ void lgkm_wait8(f2v (&o)[N]) {
+  static_assert(N == 8 || N == 4, "");
+  if constexpr (N == 8)
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(o[0]), "+v"(o[1]), "+v"(o[2]), "+v"(o[3]), "+v"(o[4]), "+v"(o[5]), "+v"(o[6]), "+v"(o[7])
+                 :
+                 : "memory");
+  else
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(o[0]), "+v"(o[1]), "+v"(o[2]), "+v"(o[3]) : : "memory");
+}
+template <int NQ, int N>
+__device__ __forceinline__ void lgkm_wait(f2v (&o)[NQ][N]) {
+  // the first call waits; the others only pin their registers behind it (lgkmcnt is already 0)
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) lgkm_wait8(o[q]);
+}
+
 template <int OFF0, int STRIDE>
 __device__ __forceinline__ void ds_rd64x4(uint32_t a, f2v (&o)[4]) {
   o[0] = ds_rd64<OFF0>(a);
@@ -326,7 +367,9 @@ __global__ __launch_bounds__(256, MEL_WPS) void logmel_tiles_kernel(
   constexpr int NBUF = LAYOUT == 0 ? MEL_NBUF0 : 1;
   constexpr bool STAGED = LAYOUT == 1 || MEL_STAGE0;
   __shared__ __attribute__((aligned(16))) float samp_buf[NBUF][MEL_TSAMP];
-  __shared__ __attribute__((aligned(16))) cpx fbuf[MEL_WAVES][FFT_SLOTS];
+  constexpr int NI = MEL_ILP;
+  static_assert(MEL_FPT % (MEL_WAVES * NI) == 0, "frames per tile must split evenly over waves x NI");
+  __shared__ __attribute__((aligned(16))) cpx fbuf[MEL_WAVES * NI][FFT_SLOTS];
   __shared__ float melst[STAGED ? MEL_FPT : 1][MEL_BANDS + 1];
   __shared__ float red[2][MEL_WAVES];
   __shared__ float4 fbw_s[FB_QUADS * 64];
@@ -358,9 +401,6 @@ __global__ __launch_bounds__(256, MEL_WPS) void logmel_tiles_kernel(
   const int sa2 = fbs[128 + lane] >> 1, sb2 = fbs[192 + lane] >> 1;
   for (int i = tid; i < FB_QUADS * 64; i += 256) fbw_s[i] = reinterpret_cast<const float4*>(fbw)[i];
 
-  cpx* S = fbuf[wid];
-  f2v* Sv = reinterpret_cast<f2v*>(S);
-  float* P = reinterpret_cast<float*>(S);
 
   // tile t's samples -> dst.  Interior tiles: LDS-DMA (global_load_lds_dwordx4, 1 KB per wave
   // instruction, no VGPRs held), completed by the s_waitcnt vmcnt(0) before the barrier that
@@ -426,55 +466,71 @@ __global__ __launch_bounds__(256, MEL_WPS) void logmel_tiles_kernel(
     }
 
     float lmax = -3.0e38f, lmin = 3.0e38f;
+    // NI frames per wave at a time (frames fi0 + q * MEL_WAVES): their dependency chains interleave
 #pragma unroll 1
-    for (int fi = wid; fi < MEL_FPT; fi += MEL_WAVES) {
-      const bool live = f0 + fi < F;  // wave-uniform
-      f2v v[8];
-      ds_rd64x8<0, 512>(lds_off(samp + fi * MEL_HOP + 2 * lane), v);
+    for (int fi0 = wid; fi0 < MEL_FPT; fi0 += MEL_WAVES * NI) {
+      f2v v[NI][8];
 #pragma unroll
-      for (int r = 0; r < 8; ++r) v[r] *= wv[r];
-      // stage A: DFT over n2 (registers) -> kA, twiddle W512^(j kA)
-      pk_dft8(v);
+      for (int q = 0; q < NI; ++q) ds_rd64x8_nw<0, 512>(lds_off(samp + (fi0 + q * MEL_WAVES) * MEL_HOP + 2 * lane), v[q]);
+      lgkm_wait(v);
 #pragma unroll
-      for (int r = 1; r < 8; ++r) v[r] = pk_cmul(v[r], twa[r - 1]);
+      for (int q = 0; q < NI; ++q) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) v[q][r] *= wv[r];
+        // stage A: DFT over n2 (registers) -> kA, twiddle W512^(j kA)
+        pk_dft8(v[q]);
+#pragma unroll
+        for (int r = 1; r < 8; ++r) v[q][r] = pk_cmul(v[q][r], twa[r - 1]);
+      }
       // lane bits 3-5 (n1) <-> register bits 0-2 (kA): lane = n0 + 8 kA, registers n1
+#pragma unroll
+      for (int q = 0; q < NI; ++q) {
 #if !(MEL_ABL & (8 | 64))
-      xch_lanes<5>(v);
-#endif
-#if !(MEL_ABL & (8 | 64))
-      xch_lanes<4>(v);
+        xch_lanes<5>(v[q]);
+        xch_lanes<4>(v[q]);
 #endif
 #if !(MEL_ABL & (8 | 128))
-      xch_lanes<3>(v);
+        xch_lanes<3>(v[q]);
 #endif
-      // stage B: DFT over n1 -> kB, twiddle W64^(n0 kB)
-      pk_dft8(v);
+      }
 #pragma unroll
-      for (int r = 1; r < 8; ++r) v[r] = pk_cmul(v[r], twb[r - 1]);
+      for (int q = 0; q < NI; ++q) {
+        // stage B: DFT over n1 -> kB, twiddle W64^(n0 kB)
+        pk_dft8(v[q]);
+#pragma unroll
+        for (int r = 1; r < 8; ++r) v[q][r] = pk_cmul(v[q][r], twb[r - 1]);
+      }
       // lane bits 0-2 (n0) <-> register bits 0-2 (kB): lane = kB + 8 kA, registers n0
-#if !(MEL_ABL & (8 | 128))
-      xch_lanes<2>(v);
-#endif
-#if !(MEL_ABL & (8 | 128))
-      xch_lanes<1>(v);
-#endif
-#if !(MEL_ABL & (8 | 128))
-      xch_lanes<0>(v);
-#endif
-      // stage C: DFT over n0 -> kC; lane j register r now holds Z[kj + 64 r]
-      pk_dft8(v);
-      // the one LDS exchange: Z in natural order (padded, zpad), Z_0 also at slot
-      // zpad(512) for the mirror of lane 0's register 0
 #pragma unroll
-      for (int r = 0; r < 8; ++r) Sv[zpad(kj) + 72 * r] = v[r];
-      if (lane == 0) Sv[zpad(512)] = v[0];
+      for (int q = 0; q < NI; ++q) {
+#if !(MEL_ABL & (8 | 128))
+        xch_lanes<2>(v[q]);
+        xch_lanes<1>(v[q]);
+        xch_lanes<0>(v[q]);
+#endif
+        // stage C: DFT over n0 -> kC; lane j register r now holds Z[kj + 64 r]
+        pk_dft8(v[q]);
+      }
+      // the one LDS exchange per frame: Z in natural order (padded, zpad), Z_0 also at slot zpad(512)
+      // for the mirror of lane 0's register 0
+#pragma unroll
+      for (int q = 0; q < NI; ++q) {
+        f2v* Sv = reinterpret_cast<f2v*>(fbuf[wid * NI + q]);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) Sv[zpad(kj) + 72 * r] = v[q][r];
+        if (lane == 0) Sv[zpad(512)] = v[q][0];
+      }
       wave_lds_sync();
-      f2v zm[8];  // zm[7 - r] = Z[(512 - kj - 64 r) & 511] = S[zpad(64 - kj) + 72 (7 - r)]
+      f2v zm[NI][8];  // zm[7 - r] = Z[(512 - kj - 64 r) & 511] = S[zpad(64 - kj) + 72 (7 - r)]
 #if MEL_ABL & 2
 #pragma unroll
-      for (int r = 0; r < 8; ++r) zm[r] = v[7 - r] * 0.5f;
+      for (int q = 0; q < NI; ++q)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) zm[q][r] = v[q][7 - r] * 0.5f;
 #else
-      ds_rd64x8<0, 576>(lds_off(S + zpad(64 - kj)), zm);
+#pragma unroll
+      for (int q = 0; q < NI; ++q) ds_rd64x8_nw<0, 576>(lds_off(fbuf[wid * NI + q] + zpad(64 - kj)), zm[q]);
+      lgkm_wait(zm);
 #endif
       // real-FFT untangle: 2 X_k = (Z_k + conj Z_{512-k}) + W1024^k (-i)(Z_k - conj Z_{512-k})
       // W1024^(kj + 64 r) = W1024^kj exp(-i pi r / 8) = u[r & 3] (-i)^(r >> 2)
@@ -482,96 +538,125 @@ __global__ __launch_bounds__(256, MEL_WPS) void logmel_tiles_kernel(
       u[0] = tu0;
 #pragma unroll
       for (int r = 1; r < 4; ++r) u[r] = pk_cmul(tu0, f2v{kRot[r][0], kRot[r][1]});
-      float pw[8];
+      float pw[NI][8];
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const f2v zn = zm[7 - r], zk = v[r];
-        const f2v e = pk_conj_add(zk, zn);                         // Z_k + conj Z_{512-k}
-        const f2v w = pk_cmul(u[r & 3], pk_untangle_odd(zk, zn));  // W (-i)(Z_k - conj Z_{512-k}), W = u (-i)^(r>>2)
-        const f2v x = r < 4 ? e + w : pk_add_negi(e, w);
-        pw[r] = fmaf(x.x, x.x, x.y * x.y);  // 4 |X_k|^2
-      }
+      for (int q = 0; q < NI; ++q)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const f2v zn = zm[q][7 - r], zk = v[q][r];
+          const f2v e = pk_conj_add(zk, zn);                         // Z_k + conj Z_{512-k}
+          const f2v w = pk_cmul(u[r & 3], pk_untangle_odd(zk, zn));  // W (-i)(Z_k - conj Z_{512-k}), W = u (-i)^(r>>2)
+          const f2v x = r < 4 ? e + w : pk_add_negi(e, w);
+          pw[q][r] = fmaf(x.x, x.x, x.y * x.y);  // 4 |X_k|^2
+        }
       wave_lds_sync();
 #pragma unroll
-      for (int r = 0; r < 8; ++r) P[kj + 64 * r] = pw[r];
-      if (lane < 16) {
-        const float nyq = 2.0f * (v[0].x - v[0].y);  // lane 0: 2 X_512 = 2 (Re Z0 - Im Z0)
-        P[512 + lane] = lane == 0 ? nyq * nyq : 0.f;  // bins past 512 are zero pads for the taps
+      for (int q = 0; q < NI; ++q) {
+        float* P = reinterpret_cast<float*>(fbuf[wid * NI + q]);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) P[kj + 64 * r] = pw[q][r];
+        if (lane < 16) {
+          const float nyq = 2.0f * (v[q][0].x - v[q][0].y);  // lane 0: 2 X_512 = 2 (Re Z0 - Im Z0)
+          P[512 + lane] = lane == 0 ? nyq * nyq : 0.f;        // bins past 512 are zero pads for the taps
+        }
       }
       wave_lds_sync();
-      // sparse filterbank (weights carry the 1/4; bins read in even-aligned pairs)
+      // sparse filterbank (weights carry the 1/4; bins read in even-aligned pairs), three read groups
+      // (bins | weight quads), each drained before the next: band a (8 bins), band b taps 0-15, band b
+      // taps 16-23; even and odd taps accumulate in the two halves of a packed pair
       static_assert(FB_A == 8 && FB_B == 24, "the filterbank reads below are written out for 8 + 24 taps");
-      // three read groups (bins | weight quads), each drained before the next, so at most 32 VGPRs
-      // of operands are live: band a (8 bins), band b taps 0-15, band b taps 16-23
+      float acc_a[NI], acc_b[NI];
 #if MEL_ABL & 4
-      float acc_a = P[lane], acc_b = P[lane + 64];
+#pragma unroll
+      for (int q = 0; q < NI; ++q) {
+        acc_a[q] = reinterpret_cast<float*>(fbuf[wid * NI + q])[lane];
+        acc_b[q] = reinterpret_cast<float*>(fbuf[wid * NI + q])[lane + 64];
+      }
 #else
       const uint32_t wa = lds_off(fbw_s + lane);
-      float acc_a = 0.f, acc_b = 0.f;
-      // packed: the even and odd taps accumulate in the two halves, added at the end
-      f2v sa = {0.f, 0.f}, sb = {0.f, 0.f};
+      f2v sa[NI], sb[NI];
       {
-        f2v p[4];
-        p[0] = ds_rd64<0>(lds_off(P + 2 * sa2));
-        p[1] = ds_rd64<8>(lds_off(P + 2 * sa2));
-        p[2] = ds_rd64<16>(lds_off(P + 2 * sa2));
-        p[3] = ds_rd64<24>(lds_off(P + 2 * sa2));
+        f2v p[NI][4];
+#pragma unroll
+        for (int q = 0; q < NI; ++q) ds_rd64x4_nw<0, 8>(lds_off(reinterpret_cast<float*>(fbuf[wid * NI + q]) + 2 * sa2), p[q]);
         f4v w0 = ds_rd128<0>(wa), w1 = ds_rd128<1024>(wa);
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(p[0]), "+v"(p[1]), "+v"(p[2]), "+v"(p[3]), "+v"(w0), "+v"(w1) : : "memory");
-        sa = __builtin_elementwise_fma(w0.xy, p[0], sa);
-        sa = __builtin_elementwise_fma(w0.zw, p[1], sa);
-        sa = __builtin_elementwise_fma(w1.xy, p[2], sa);
-        sa = __builtin_elementwise_fma(w1.zw, p[3], sa);
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(w0), "+v"(w1) : : "memory");
+        lgkm_wait(p);
+#pragma unroll
+        for (int q = 0; q < NI; ++q) {
+          sa[q] = w0.xy * p[q][0];
+          sa[q] = __builtin_elementwise_fma(w0.zw, p[q][1], sa[q]);
+          sa[q] = __builtin_elementwise_fma(w1.xy, p[q][2], sa[q]);
+          sa[q] = __builtin_elementwise_fma(w1.zw, p[q][3], sa[q]);
+        }
       }
       {
-        f2v p[8];
-        ds_rd64x8<0, 8>(lds_off(P + 2 * sb2), p);
+        f2v p[NI][8];
+#pragma unroll
+        for (int q = 0; q < NI; ++q) ds_rd64x8_nw<0, 8>(lds_off(reinterpret_cast<float*>(fbuf[wid * NI + q]) + 2 * sb2), p[q]);
         f4v w0 = ds_rd128<2048>(wa), w1 = ds_rd128<3072>(wa), w2 = ds_rd128<4096>(wa), w3 = ds_rd128<5120>(wa);
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(w0), "+v"(w1), "+v"(w2), "+v"(w3) : : "memory");
-        sb = __builtin_elementwise_fma(w0.xy, p[0], sb);
-        sb = __builtin_elementwise_fma(w0.zw, p[1], sb);
-        sb = __builtin_elementwise_fma(w1.xy, p[2], sb);
-        sb = __builtin_elementwise_fma(w1.zw, p[3], sb);
-        sb = __builtin_elementwise_fma(w2.xy, p[4], sb);
-        sb = __builtin_elementwise_fma(w2.zw, p[5], sb);
-        sb = __builtin_elementwise_fma(w3.xy, p[6], sb);
-        sb = __builtin_elementwise_fma(w3.zw, p[7], sb);
+        lgkm_wait(p);
+#pragma unroll
+        for (int q = 0; q < NI; ++q) {
+          sb[q] = w0.xy * p[q][0];
+          sb[q] = __builtin_elementwise_fma(w0.zw, p[q][1], sb[q]);
+          sb[q] = __builtin_elementwise_fma(w1.xy, p[q][2], sb[q]);
+          sb[q] = __builtin_elementwise_fma(w1.zw, p[q][3], sb[q]);
+          sb[q] = __builtin_elementwise_fma(w2.xy, p[q][4], sb[q]);
+          sb[q] = __builtin_elementwise_fma(w2.zw, p[q][5], sb[q]);
+          sb[q] = __builtin_elementwise_fma(w3.xy, p[q][6], sb[q]);
+          sb[q] = __builtin_elementwise_fma(w3.zw, p[q][7], sb[q]);
+        }
       }
       {
-        f2v p[4];
-        ds_rd64x4<64, 8>(lds_off(P + 2 * sb2), p);
+        f2v p[NI][4];
+#pragma unroll
+        for (int q = 0; q < NI; ++q) ds_rd64x4_nw<64, 8>(lds_off(reinterpret_cast<float*>(fbuf[wid * NI + q]) + 2 * sb2), p[q]);
         f4v w0 = ds_rd128<6144>(wa), w1 = ds_rd128<7168>(wa);
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(w0), "+v"(w1) : : "memory");
-        sb = __builtin_elementwise_fma(w0.xy, p[0], sb);
-        sb = __builtin_elementwise_fma(w0.zw, p[1], sb);
-        sb = __builtin_elementwise_fma(w1.xy, p[2], sb);
-        sb = __builtin_elementwise_fma(w1.zw, p[3], sb);
+        lgkm_wait(p);
+#pragma unroll
+        for (int q = 0; q < NI; ++q) {
+          sb[q] = __builtin_elementwise_fma(w0.xy, p[q][0], sb[q]);
+          sb[q] = __builtin_elementwise_fma(w0.zw, p[q][1], sb[q]);
+          sb[q] = __builtin_elementwise_fma(w1.xy, p[q][2], sb[q]);
+          sb[q] = __builtin_elementwise_fma(w1.zw, p[q][3], sb[q]);
+        }
       }
-      acc_a = sa.x + sa.y;
-      acc_b = sb.x + sb.y;
+#pragma unroll
+      for (int q = 0; q < NI; ++q) {
+        acc_a[q] = sa[q].x + sa[q].y;
+        acc_b[q] = sb[q].x + sb[q].y;
+      }
 #endif
       wave_lds_sync();
-      // clamp(1e-10).log10(): the clamped value maps to exactly -10 like the correctly rounded
-      // library log10; elsewhere log2 * log10(2) is within a few ulp
-      const float l_a = acc_a <= 1e-10f ? -10.0f : __builtin_amdgcn_logf(acc_a) * 0.30102999566398120f;
-      const float l_b = acc_b <= 1e-10f ? -10.0f : __builtin_amdgcn_logf(acc_b) * 0.30102999566398120f;
-      // (x + 4) / 4 here; the clip-max floor is applied afterwards, only to the tiles holding a value
-      // below it (logmel_floor_kernel): (max(x, f) + 4) / 4 == max((x + 4) / 4, (f + 4) / 4) exactly,
-      // as x -> fl(x + 4) is monotone and / 4 is exact
-      const float y_a = (l_a + 4.0f) * 0.25f, y_b = (l_b + 4.0f) * 0.25f;
-      if constexpr (!STAGED) {
-        if (live && !(MEL_ABL & 16)) {
-          float* orow = out + b * ld_out + (f0 + fi) * MEL_BANDS;
-          orow[band_a] = y_a;
-          orow[band_b] = y_b;
+#pragma unroll
+      for (int q = 0; q < NI; ++q) {
+        const int fi = fi0 + q * MEL_WAVES;
+        const bool live = f0 + fi < F;  // wave-uniform
+        // clamp(1e-10).log10(): the clamped value maps to exactly -10 like the correctly rounded
+        // library log10; elsewhere log2 * log10(2) is within a few ulp
+        const float l_a = acc_a[q] <= 1e-10f ? -10.0f : __builtin_amdgcn_logf(acc_a[q]) * 0.30102999566398120f;
+        const float l_b = acc_b[q] <= 1e-10f ? -10.0f : __builtin_amdgcn_logf(acc_b[q]) * 0.30102999566398120f;
+        // (x + 4) / 4 here; the clip-max floor is applied afterwards, only to the tiles holding a value
+        // below it (logmel_floor_kernel): (max(x, f) + 4) / 4 == max((x + 4) / 4, (f + 4) / 4) exactly,
+        // as x -> fl(x + 4) is monotone and / 4 is exact
+        const float y_a = (l_a + 4.0f) * 0.25f, y_b = (l_b + 4.0f) * 0.25f;
+        if constexpr (!STAGED) {
+          if (live && !(MEL_ABL & 16)) {
+            float* orow = out + b * ld_out + (f0 + fi) * MEL_BANDS;
+            orow[band_a] = y_a;
+            orow[band_b] = y_b;
+          }
+        } else {
+          melst[fi][band_a] = y_a;
+          melst[fi][band_b] = y_b;
         }
-      } else {
-        melst[fi][band_a] = y_a;
-        melst[fi][band_b] = y_b;
-      }
-      if (live) {
-        lmax = fmaxf(lmax, fmaxf(l_a, l_b));
-        lmin = fminf(lmin, fminf(l_a, l_b));
+        if (live) {
+          lmax = fmaxf(lmax, fmaxf(l_a, l_b));
+          lmin = fminf(lmin, fminf(l_a, l_b));
+        }
       }
     }
     lmax = wave_max_dpp(lmax);
