@@ -279,11 +279,7 @@ __global__ __launch_bounds__(NTHR, WPE) void attn_fwd_mf_kernel(const TI* __rest
         }
         tmax = fmaxf(tmax, x);
       }
-    {  // xor-32 partner by v_permlane32_swap (VALU) instead of a ds_bpermute round trip
-      float ta = tmax, tb = tmax;
-      xrow32(ta, tb);
-      tmax = fmaxf(ta, tb);
-    }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
     // lazy rescale: the running max moves only when a score passes it by more than 2^8 in the exp2
     // domain (p <= 256 otherwise, exact in the fp32 sums and fine in bf16), so most tiles skip the
     // O / l rescale; m = -inf (nothing seen yet) moves on the first finite score

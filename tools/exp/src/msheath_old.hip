@@ -315,21 +315,41 @@ __global__ void jump_select4_kernel(const float4* __restrict__ xn, const float4*
                                     const float4* __restrict__ xold, const float* __restrict__ act,
                                     const float* __restrict__ alpha, const float* __restrict__ beta,
                                     const float4* __restrict__ gam, float4* __restrict__ out, int64_t L, int d4) {
+  // grid (L chunks of MEM_CHUNK rows, B), thread (rl, c) as jump_axpy_inplace_kernel: no per-element
+  // 64-bit modulo for gam's column, four rows per trip with the loads first
   const int64_t b = blockIdx.y;
-  const int64_t n = L * d4;
-  const int64_t base = b * n;
-  const bool a = act[b] != 0.f;
+  const int nrl = 256 / d4;
+  const int c = threadIdx.x % d4, rl = threadIdx.x / d4;
+  if (rl >= nrl) return;
+  const int64_t l0 = (int64_t)blockIdx.x * MEM_CHUNK, l1 = min<int64_t>(L, l0 + MEM_CHUNK);
+  const int64_t rb = b * L;
+  if (act[b] == 0.f) {
+    for (int64_t l = l0 + rl; l < l1; l += nrl) out[(rb + l) * d4 + c] = xold[(rb + l) * d4 + c];
+    return;
+  }
   const float al = alpha[b], be = beta[b];
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    if (a) {
-      const float4 u = xn[base + i], v = orig[base + i], w = gam[b * d4 + i % d4];
-      out[base + i] = make_float4(__builtin_fmaf(al, u.x, __builtin_fmaf(be, v.x, w.x)),
-                                  __builtin_fmaf(al, u.y, __builtin_fmaf(be, v.y, w.y)),
-                                  __builtin_fmaf(al, u.z, __builtin_fmaf(be, v.z, w.z)),
-                                  __builtin_fmaf(al, u.w, __builtin_fmaf(be, v.w, w.w)));
-    } else {
-      out[base + i] = xold[base + i];
+  const float4 w = gam[b * d4 + c];
+  auto one = [&](float4 u, float4 v, int64_t i) __attribute__((always_inline)) {
+    out[i] = make_float4(__builtin_fmaf(al, u.x, __builtin_fmaf(be, v.x, w.x)),
+                         __builtin_fmaf(al, u.y, __builtin_fmaf(be, v.y, w.y)),
+                         __builtin_fmaf(al, u.z, __builtin_fmaf(be, v.z, w.z)),
+                         __builtin_fmaf(al, u.w, __builtin_fmaf(be, v.w, w.w)));
+  };
+  int64_t l = l0 + rl;
+  for (; l + 3 * nrl < l1; l += 4 * nrl) {
+    float4 u[4], v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t i = (rb + l + k * nrl) * d4 + c;
+      u[k] = xn[i];
+      v[k] = orig[i];
     }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) one(u[k], v[k], (rb + l + k * nrl) * d4 + c);
+  }
+  for (; l < l1; l += nrl) {
+    const int64_t i = (rb + l) * d4 + c;
+    one(xn[i], orig[i], i);
   }
 }
 
@@ -343,26 +363,48 @@ __global__ void jump_axpy_inplace_kernel(const float4* xin, float4* xout, const 
                                          const float4* __restrict__ orig, const float* __restrict__ act,
                                          const float* __restrict__ alpha, const float* __restrict__ beta,
                                          const float4* __restrict__ gam, int64_t L, int d4) {
+  // grid (L chunks of MEM_CHUNK rows, B); thread (rl, c): column c of rows l0 + rl, + nrl, ... -- no
+  // per-element 64-bit division for the row index (the flat form divided by d4 on every float4), four
+  // rows per trip with every load issued first
   const int64_t b = blockIdx.y;
-  const int64_t n = L * d4;
-  const int64_t base = b * n;
+  const int nrl = 256 / d4;
+  const int c = threadIdx.x % d4, rl = threadIdx.x / d4;
+  if (rl >= nrl) return;
+  const int64_t l0 = (int64_t)blockIdx.x * MEM_CHUNK, l1 = min<int64_t>(L, l0 + MEM_CHUNK);
+  const int64_t rb = b * L;
   if (act[b] == 0.f) {
     if (xin != xout)
-      for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        xout[base + i] = xin[base + i];
+      for (int64_t l = l0 + rl; l < l1; l += nrl) xout[(rb + l) * d4 + c] = xin[(rb + l) * d4 + c];
     return;
   }
   const float al = alpha[b], be = beta[b];
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = b * L + i / d4;
-    const float sc = s1[r] * s2[r];
-    const float4 a = xin[base + i], v = y[base + i], o = orig[base + i], w = gam[b * d4 + i % d4];
+  const float4 w = gam[b * d4 + c];
+  auto one = [&](float sc, float4 a, float4 v, float4 o, int64_t i) __attribute__((always_inline)) {
     const float4 u = make_float4(__builtin_fmaf(sc, v.x, a.x), __builtin_fmaf(sc, v.y, a.y), __builtin_fmaf(sc, v.z, a.z),
                                  __builtin_fmaf(sc, v.w, a.w));
-    xout[base + i] = make_float4(__builtin_fmaf(al, u.x, __builtin_fmaf(be, o.x, w.x)),
-                                 __builtin_fmaf(al, u.y, __builtin_fmaf(be, o.y, w.y)),
-                                 __builtin_fmaf(al, u.z, __builtin_fmaf(be, o.z, w.z)),
-                                 __builtin_fmaf(al, u.w, __builtin_fmaf(be, o.w, w.w)));
+    xout[i] = make_float4(__builtin_fmaf(al, u.x, __builtin_fmaf(be, o.x, w.x)),
+                          __builtin_fmaf(al, u.y, __builtin_fmaf(be, o.y, w.y)),
+                          __builtin_fmaf(al, u.z, __builtin_fmaf(be, o.z, w.z)),
+                          __builtin_fmaf(al, u.w, __builtin_fmaf(be, o.w, w.w)));
+  };
+  int64_t l = l0 + rl;
+  for (; l + 3 * nrl < l1; l += 4 * nrl) {
+    float sc[4];
+    float4 a[4], v[4], o[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t r = rb + l + u * nrl, i = r * d4 + c;
+      sc[u] = s1[r] * s2[r];
+      a[u] = xin[i];
+      v[u] = y[i];
+      o[u] = orig[i];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) one(sc[u], a[u], v[u], o[u], (rb + l + u * nrl) * d4 + c);
+  }
+  for (; l < l1; l += nrl) {
+    const int64_t r = rb + l, i = r * d4 + c;
+    one(s1[r] * s2[r], xin[i], y[i], orig[i], i);
   }
 }
 
@@ -816,8 +858,7 @@ int asrx_jump_axpy_inplace(const float* xin, float* xout, const float* s1, const
   ASRX_REQUIRE(xout != orig, "asrx_jump_axpy_inplace: xout must not alias orig");
   if (B * L == 0) return 0;
   ASRX_REQUIRE(d / 4 <= 256, "asrx_jump_axpy_inplace: d <= 1024 required");
-  // flat grid-stride (measured faster than 64- or 16-row chunk grids: profiles/r04_jump_ab.txt)
-  dim3 grid((unsigned)std::min<int64_t>((L * (d / 4) + 255) / 256, 512), (unsigned)B);
+  dim3 grid((unsigned)asrx_mem_chunks(L), (unsigned)B);
   jump_axpy_inplace_kernel<<<grid, 256, 0, stream>>>((const float4*)xin, (float4*)xout, s1, s2, (const float4*)y,
                                                      (const float4*)orig, act, alpha, beta, (const float4*)gam, L,
                                                      (int)(d / 4));
@@ -829,8 +870,7 @@ int asrx_jump_select4(const float* xn, const float* orig, const float* xold, con
                       hipStream_t stream) {
   ASRX_REQUIRE(d % 4 == 0 && d <= 1024, "asrx_jump_select4: d % 4 != 0 or d > 1024");
   if (B * L == 0) return 0;
-  // flat grid-stride (measured faster than 64- or 16-row chunk grids: profiles/r04_jump_ab.txt)
-  dim3 grid((unsigned)std::min<int64_t>((L * (d / 4) + 255) / 256, 512), (unsigned)B);
+  dim3 grid((unsigned)asrx_mem_chunks(L), (unsigned)B);
   jump_select4_kernel<<<grid, 256, 0, stream>>>((const float4*)xn, (const float4*)orig, (const float4*)xold, act,
                                                 alpha, beta, (const float4*)gam, (float4*)out, L, (int)(d / 4));
   ASRX_LAUNCHED("asrx_jump_select4");

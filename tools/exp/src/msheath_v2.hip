@@ -248,32 +248,16 @@ __global__ __launch_bounds__(256) void axpy_row2_colsum_kernel(const float4* __r
   }
   const int64_t l0 = (int64_t)blockIdx.y * MEM_CHUNK, l1 = min<int64_t>(L, l0 + MEM_CHUNK);
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  auto one = [&](float sc, float4 a, float4 v, int64_t i) __attribute__((always_inline)) {
-    const float4 o = make_float4(__builtin_fmaf(sc, v.x, a.x), __builtin_fmaf(sc, v.y, a.y),
-                                 __builtin_fmaf(sc, v.z, a.z), __builtin_fmaf(sc, v.w, a.w));
-    if (out) out[i] = o;  // null: column sums only (the in-place no-grad MSheath recomputes x_new)
-    acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
-  };
   if (rl < nrl) {
-    int64_t l = l0 + rl;
-    // four of the thread's rows per trip, every load issued first (one row per trip exposed a full load
-    // latency per row); the sums keep the row order, so the results are unchanged
-    for (; l + 3 * nrl < l1; l += 4 * nrl) {
-      float sc[4];
-      float4 a[4], v[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int64_t r = b * L + l + u * nrl;
-        sc[u] = s1[r] * s2[r];
-        a[u] = x[r * d4 + c];
-        v[u] = y[r * d4 + c];
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) one(sc[u], a[u], v[u], (b * L + l + u * nrl) * d4 + c);
-    }
-    for (; l < l1; l += nrl) {
+    for (int64_t l = l0 + rl; l < l1; l += nrl) {
       const int64_t r = b * L + l;
-      one(s1[r] * s2[r], x[r * d4 + c], y[r * d4 + c], r * d4 + c);
+      const float sc = s1[r] * s2[r];
+      const int64_t i = r * d4 + c;
+      const float4 a = x[i], v = y[i];
+      const float4 o = make_float4(__builtin_fmaf(sc, v.x, a.x), __builtin_fmaf(sc, v.y, a.y),
+                                   __builtin_fmaf(sc, v.z, a.z), __builtin_fmaf(sc, v.w, a.w));
+      if (out) out[i] = o;  // null: column sums only (the in-place no-grad MSheath recomputes x_new)
+      acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
     }
   }
   red[threadIdx.x] = acc;
@@ -815,9 +799,8 @@ int asrx_jump_axpy_inplace(const float* xin, float* xout, const float* s1, const
   ASRX_REQUIRE(d % 4 == 0, "asrx_jump_axpy_inplace: d % 4 != 0");
   ASRX_REQUIRE(xout != orig, "asrx_jump_axpy_inplace: xout must not alias orig");
   if (B * L == 0) return 0;
-  ASRX_REQUIRE(d / 4 <= 256, "asrx_jump_axpy_inplace: d <= 1024 required");
-  // flat grid-stride (measured faster than 64- or 16-row chunk grids: profiles/r04_jump_ab.txt)
-  dim3 grid((unsigned)std::min<int64_t>((L * (d / 4) + 255) / 256, 512), (unsigned)B);
+  const int64_t n = L * d / 4;
+  dim3 grid((unsigned)std::min<int64_t>((n + 255) / 256, 512), (unsigned)B);
   jump_axpy_inplace_kernel<<<grid, 256, 0, stream>>>((const float4*)xin, (float4*)xout, s1, s2, (const float4*)y,
                                                      (const float4*)orig, act, alpha, beta, (const float4*)gam, L,
                                                      (int)(d / 4));
@@ -827,10 +810,10 @@ int asrx_jump_axpy_inplace(const float* xin, float* xout, const float* s1, const
 int asrx_jump_select4(const float* xn, const float* orig, const float* xold, const float* act, const float* alpha,
                       const float* beta, const float* gam, float* out, int64_t B, int64_t L, int64_t d,
                       hipStream_t stream) {
-  ASRX_REQUIRE(d % 4 == 0 && d <= 1024, "asrx_jump_select4: d % 4 != 0 or d > 1024");
+  ASRX_REQUIRE(d % 4 == 0, "asrx_jump_select4: d % 4 != 0");
   if (B * L == 0) return 0;
-  // flat grid-stride (measured faster than 64- or 16-row chunk grids: profiles/r04_jump_ab.txt)
-  dim3 grid((unsigned)std::min<int64_t>((L * (d / 4) + 255) / 256, 512), (unsigned)B);
+  const int64_t n = L * d / 4;
+  dim3 grid((unsigned)std::min<int64_t>((n + 255) / 256, 512), (unsigned)B);
   jump_select4_kernel<<<grid, 256, 0, stream>>>((const float4*)xn, (const float4*)orig, (const float4*)xold, act,
                                                 alpha, beta, (const float4*)gam, (float4*)out, L, (int)(d / 4));
   ASRX_LAUNCHED("asrx_jump_select4");
