@@ -12,7 +12,21 @@ import torch  # noqa: E402
 from asrx import lib  # noqa: E402
 
 calls = []
-lib.call = lambda name, *a: calls.append((name, a))
+sites = []
+
+
+def _record(name, *a):
+    calls.append((name, a))
+    f, chain = sys._getframe(1), []
+    while f is not None and len(chain) < 3:
+        fn = os.path.basename(f.f_code.co_filename)
+        if fn not in ("gemm.py", "lib.py") and "torch" not in f.f_code.co_filename:
+            chain.append(f"{fn}:{f.f_lineno}")
+        f = f.f_back
+    sites.append(" <- ".join(chain))
+
+
+lib.call = _record
 lib.require_gpu = lambda *t: None
 class _FakeLib:
     """Size queries the host code makes (what the real library answers); everything else returns 64."""
@@ -87,10 +101,10 @@ for n, a in calls:
 for k, v in sorted(ge.items(), key=lambda kv: -kv[1]):
     print(v, k)
 gf = collections.Counter()
-for n, a in calls:
+for (n, a), site in zip(calls, sites):
     if n == "asrx_gemm_wn_ex" and not a[1] and a[13] >= 32768:
         gf[("fp32-A", a[13], a[14], a[15], "nj", a[19], "conv" if a[3] else "", "act", a[18], "Z" if a[12] else "",
-            "beta" if a[17] else "", "cb" if a[9] else "")] += 1
+            "beta" if a[17] else "", "cb" if a[9] else "", site)] += 1
     elif n in ("asrx_gemm_wn_res", "asrx_gemm_wn_router") and a[-5 if n == "asrx_gemm_wn_res" else -4] >= 32768:
         gf[(n,) + tuple(a[-5:-1])] += 1
 for k, v in sorted(gf.items(), key=lambda kv: -kv[1]):
