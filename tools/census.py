@@ -102,7 +102,7 @@ for k, v in sorted(ge.items(), key=lambda kv: -kv[1]):
     print(v, k)
 gf = collections.Counter()
 for (n, a), site in zip(calls, sites):
-    if n == "asrx_gemm_wn_ex" and not a[1] and a[13] >= 32768:
+    if n == "asrx_gemm_wn_ex" and not a[1] and (a[13] >= 32768 or os.environ.get("CENSUS_ALL")):
         gf[("fp32-A", a[13], a[14], a[15], "nj", a[19], "conv" if a[3] else "", "act", a[18], "Z" if a[12] else "",
             "beta" if a[17] else "", "cb" if a[9] else "", site)] += 1
     elif n in ("asrx_gemm_wn_res", "asrx_gemm_wn_router") and a[-5 if n == "asrx_gemm_wn_res" else -4] >= 32768:
