@@ -134,6 +134,37 @@ def test_logmel_matches_oracle(cuda, n):
         assert err < 2e-4, err
 
 
+def test_logmel_floor_on_some_tiles(cuda):
+    """The clip-max floor (essentials.py:485-488) is applied by a second pass only to the 16-frame tiles
+    that hold a value below max - 8 (asrx_logmel's logmel_floor_kernel): clips whose floor covers some
+    tiles and not others -- loud noise followed by near-silence, and a pure tone whose far bands fall
+    below the floor -- match the oracle, and the floored entries are exactly (max - 8 + 4) / 4."""
+    from asrx.mel import logmel
+    from oracle import mel as omel
+
+    n = 48000
+    t = np.arange(n) / 16000.0
+    rng = np.random.default_rng(3)
+    loud_then_quiet = np.where(t < 1.3, 0.5, 1e-6) * rng.standard_normal(n)  # broadband: no band floored while loud
+    pure = 0.9 * np.sin(2 * np.pi * 440 * t)
+    clips = np.stack([loud_then_quiet, pure, _clip(n, 11)]).astype(np.float32)
+    out_bfm = logmel(torch.from_numpy(clips).to(cuda), layout="BFM").cpu().numpy()
+    out_bmf = logmel(torch.from_numpy(clips).to(cuda), layout="BMF").cpu().numpy()
+    floored_tiles = []
+    for b in range(3):
+        ref = omel.log_mel(clips[b].astype(np.float64))
+        assert np.array_equal(out_bmf[b], out_bfm[b].T)
+        assert np.abs(out_bmf[b] - ref).max() < 2e-4
+        low = ref == ref.min()  # the floored entries (the floor is the clip's minimum)
+        fmin = out_bmf[b][low]
+        assert np.all(fmin == fmin[0]), "floored entries must share one value"
+        # frames (16 per tile) that hold a floored entry
+        tiles = np.unique(np.nonzero(low.any(axis=0))[0] // 16)
+        floored_tiles.append((len(tiles), (ref.shape[1] + 15) // 16))
+    # the quiet tail floors some tiles and leaves the loud ones alone
+    assert 0 < floored_tiles[0][0] < floored_tiles[0][1], floored_tiles
+
+
 def test_logmel_pool_and_silence(cuda):
     from asrx.mel import logmel
     from oracle import mel as omel
