@@ -487,6 +487,9 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_bwd_kernel(
   // (one row ahead left the kernel latency-bound); past the end the last row is re-read
   // (the row's mode and softmax outputs travel with it: read at the top of the row they stalled every
   // row for a full memory latency before the pools could start)
+  // d >= 768: one row ahead (two register sets of x and dout would not fit: 512 VGPRs and scratch
+  // spills at d = 1024)
+  constexpr int AHEAD = E >= 12 ? 1 : 2;
   float xn1[E], gn1[E], xn2[E], gn2[E], yn1[3], yn2[3];
   int sn1, sn2;
   auto fetch = [&](int64_t rr, float (&xb)[E], float (&gb)[E], float (&yb)[3], int& sb) __attribute__((always_inline)) {
@@ -500,7 +503,7 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_bwd_kernel(
   };
   if (r < g.rows) {
     fetch(r, xn1, gn1, yn1, sn1);
-    fetch(r + stride, xn2, gn2, yn2, sn2);
+    if constexpr (AHEAD == 2) fetch(r + stride, xn2, gn2, yn2, sn2);
   }
   // one row from register set 1 or 2 (alternating, see abby_fwd_kernel), refilled with the row two
   // strides ahead once its values are in LDS / locals
@@ -519,7 +522,7 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_bwd_kernel(
     }
     const int sel = __builtin_amdgcn_readfirstlane(ss);
     const float y0 = ysv[0], y1 = ysv[1], y2 = ysv[2];
-    fetch(r + 2 * stride, xs, gs, ysv, ss);
+    fetch(r + AHEAD * stride, xs, gs, ysv, ss);
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
 #pragma unroll
@@ -669,10 +672,14 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_bwd_kernel(
     accb[1] += dz1;
     accb[2] += dz2;
   };
-  for (; r < g.rows; r += 2 * stride) {
-    row_body(r, xn1, gn1, yn1, sn1);
-    if (r + stride >= g.rows) break;
-    row_body(r + stride, xn2, gn2, yn2, sn2);
+  if constexpr (AHEAD == 1) {
+    for (; r < g.rows; r += stride) row_body(r, xn1, gn1, yn1, sn1);
+  } else {
+    for (; r < g.rows; r += 2 * stride) {
+      row_body(r, xn1, gn1, yn1, sn1);
+      if (r + stride >= g.rows) break;
+      row_body(r + stride, xn2, gn2, yn2, sn2);
+    }
   }
   // workgroup reduction of dW2 / db2 through LDS, then one atomic per element
   __syncthreads();
