@@ -531,6 +531,9 @@ __device__ __forceinline__ void wr_load(const Params& p, WrStage<NJ, ABF>& st, i
 // base (SGPR) + offset + k bytes, one address add per load.  The general path selects between the row
 // address and the zero page per load and k-step (~15 instructions per load, exec-masked); the k-step is
 // issue-bound, and one extra load per k-step measured 5-12 % slower.
+#ifndef WR_ABL_EPI
+#define WR_ABL_EPI 0
+#endif
 #ifndef WR_FAST
 #define WR_FAST 1  // 0: every load takes the general (zero-page select) path -- A/B builds only
 #endif
@@ -906,6 +909,18 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
     if (ce.kk == nk - 1) {
       const int m0 = ce.m0, n0 = ce.n0;
       const float* bsl = bias_s[ce.j & 1];
+#if WR_ABL_EPI  // timing ablation (wrong results): no epilogue, the accumulators only feed a never-taken store
+      {
+        float t = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int q = 0; q < NT; ++q) t += acc[i][q][0] + acc[i][q][1] + acc[i][q][2] + acc[i][q][3];
+        if (t == 1.2345e-37f) p.C[m0] = t;
+      }
+      if constexpr (true) {
+      } else
+#endif
       if constexpr (RT) {
         epilogue_router<NJ>(p, acc, bsl, w2s, red, m0, wm, wn, lr, lk);
       } else if constexpr (CE) {
