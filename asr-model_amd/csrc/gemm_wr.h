@@ -170,6 +170,9 @@ __device__ __forceinline__ void epilogue(const Params& p, f32x4 (&acc)[4][2 * NJ
 // layout gives each lane 4 columns of one row, so a direct store instruction writes 16 rows x 64 B;
 // re-read from LDS, every store instruction writes whole contiguous row segments (32*NJ floats per
 // row: 384 B at NJ = 3).  Requires vec_ok(p) (float4-aligned C/Z, N % 4 == 0).
+#ifndef WR_ABL_EPI
+#define WR_ABL_EPI 0  // timing ablations (wrong results): 1 no epilogue, 2 epilogue without its global stores
+#endif
 constexpr int EP_PAD = 4;
 template <int NJ>
 struct EpLds {
@@ -204,6 +207,9 @@ __device__ __forceinline__ void epilogue_lds(const Params& p, f32x4 (&acc)[4][2 
       float4 x = *reinterpret_cast<const float4*>(ep + r * LD + c);
       const int row = rbase + r, col = cbase + c;
       if (row >= p.M || col >= p.N) continue;
+#if WR_ABL_EPI == 2  // timing ablation (wrong results): the epilogue without its global stores
+      if (x.x + x.y + x.z + x.w != 1.2345e-37f) continue;
+#endif
       if (p.Cb) {  // bf16 output (beta = 0)
         if (p.Z)
           __builtin_nontemporal_store(f32x4{x.x, x.y, x.z, x.w},
@@ -531,9 +537,6 @@ __device__ __forceinline__ void wr_load(const Params& p, WrStage<NJ, ABF>& st, i
 // base (SGPR) + offset + k bytes, one address add per load.  The general path selects between the row
 // address and the zero page per load and k-step (~15 instructions per load, exec-masked); the k-step is
 // issue-bound, and one extra load per k-step measured 5-12 % slower.
-#ifndef WR_ABL_EPI
-#define WR_ABL_EPI 0
-#endif
 #ifndef WR_FAST
 #define WR_FAST 1  // 0: every load takes the general (zero-page select) path -- A/B builds only
 #endif
@@ -909,7 +912,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
     if (ce.kk == nk - 1) {
       const int m0 = ce.m0, n0 = ce.n0;
       const float* bsl = bias_s[ce.j & 1];
-#if WR_ABL_EPI  // timing ablation (wrong results): no epilogue, the accumulators only feed a never-taken store
+#if WR_ABL_EPI == 1  // timing ablation (wrong results): no epilogue, the accumulators only feed a never-taken store
       {
         float t = 0.f;
 #pragma unroll
