@@ -27,18 +27,19 @@ for M, N, K in SHAPES:
         W = torch.randn(N, K, device=dev) * 0.05
         Wb = G.weight_bf16(W, cache=False)
         C = torch.empty(M, N, device=dev)
+        bias = torch.randn(N, device=dev) if os.environ.get("GEMM_BIAS") else None
         for nj in NJS:
             if 128 * nj > ((N + 127) // 128) * 128:
                 continue
             G._nj_override = nj
             for _ in range(3):
-                G.gemm_wn(A, Wb, C, M=M, N=N, K=K, lda=K, ldc=N)
+                G.gemm_wn(A, Wb, C, M=M, N=N, K=K, lda=K, ldc=N, bias=bias)
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             n = ITERS
             e0.record()
             for _ in range(n):
-                G.gemm_wn(A, Wb, C, M=M, N=N, K=K, lda=K, ldc=N)
+                G.gemm_wn(A, Wb, C, M=M, N=N, K=K, lda=K, ldc=N, bias=bias)
             e1.record()
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) * 1e3 / n
