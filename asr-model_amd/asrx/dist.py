@@ -32,7 +32,11 @@ Design (MI355X-first, not a translation of DDP's call pattern):
     partial gradient: that raises (it cannot happen while event counts are a function of the
     signature, and the check keeps it from ever passing silently);
   * finish() joins the comm stream; buckets a step left incomplete are reduced there with their
-    missing slots zero (variable unused parameters).
+    missing slots zero (SURVEY §7: variable unused parameters);
+  * BatchNorm running statistics (model.py:103 BatchNorm1d in ConvLite) are training state outside the
+    gradient: each rank's forward updates its own, so finish() also averages every floating-point
+    running_mean / running_var over the ranks (one small flat all-reduce behind the last bucket) and the
+    replicas' eval-mode outputs stay identical (DDP instead rebroadcasts rank 0's buffers each step).
 """
 from __future__ import annotations
 
@@ -95,6 +99,9 @@ class GradSync:
         self._reset_step()
         self._listener = weakref.WeakMethod(self._ready)
         ops.GRAD_LISTENERS.append(self._listener)
+        self._stat_bufs = [b for n, b in model.named_buffers()
+                           if b.is_floating_point() and n.rsplit(".", 1)[-1] in ("running_mean", "running_var")]
+        self._stat_flat = None
 
     def _reset_step(self):
         self._seen: dict[int, int] = {}  # events of the current step per parameter
@@ -178,7 +185,11 @@ class GradSync:
         if self._overlap:
             for b, n in zip(self.buckets, plan):
                 b.expected = b.pending = n
-                b.complete = n == 0
+                # a bucket the plan gives no event is NOT launched from the hooks: under the same signature
+                # a parameter of it may still take its first gradient later in this step (an event after
+                # the launch would mean a partial reduce); finish() launches it, and by the next-bucket
+                # rule the buckets behind it, once backward is done
+                b.complete = False
 
     def _ready(self, p):
         if not self._started:
@@ -211,7 +222,7 @@ class GradSync:
     def _launch_ready(self):
         """The next-bucket rule: launch the run of complete buckets starting at the next index."""
         while self._next < len(self.buckets) and self.buckets[self._next].complete and \
-                self.buckets[self._next].pending == 0:
+                self.buckets[self._next].pending == 0 and self.buckets[self._next].expected > 0:
             self._launch(self.buckets[self._next])
             self._next += 1
 
@@ -248,14 +259,37 @@ class GradSync:
             for b in self.buckets[self._next:]:  # the rest, in index order
                 self._launch(b)
             self._next = len(self.buckets)
+            stats = self._launch_stats()
             for b in self.buckets:
                 b.work.wait()
+            if stats is not None:
+                stats.wait()
             if self.cuda:
                 torch.cuda.current_stream().wait_stream(self.comm)
             inv = 1.0 / self.world
             for b in self.buckets:
                 b.buf.mul_(inv)
+            if stats is not None:
+                self._stat_flat.mul_(inv)
+                torch._foreach_copy_(self._stat_bufs, [v.view_as(t) for v, t in zip(
+                    self._stat_flat.split([t.numel() for t in self._stat_bufs]), self._stat_bufs)])
         self._reset_step()
+
+    def _launch_stats(self):
+        """All-reduce (sum) of the BatchNorm running statistics, flattened, after the last bucket."""
+        if not self._stat_bufs:
+            return None
+        n = sum(t.numel() for t in self._stat_bufs)
+        if self._stat_flat is None or self._stat_flat.numel() != n:
+            self._stat_flat = torch.empty(n, device=self._stat_bufs[0].device, dtype=torch.float32)
+        torch.cat([t.reshape(-1).float() for t in self._stat_bufs], out=self._stat_flat)
+        if self.cuda:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream())
+            with torch.cuda.stream(self.comm):
+                self.comm.wait_event(ev)
+                return dist.all_reduce(self._stat_flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        return dist.all_reduce(self._stat_flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
     def remove(self):
         for h in self.hooks:

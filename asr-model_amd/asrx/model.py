@@ -747,6 +747,15 @@ class Model(nn.Module):
         self.processor.join_dead_blocks()
         gemm_mod.end_step()
 
+    def end_step(self):
+        """End the current step explicitly.  A training step normally ends by itself at the end of the
+        backward that follows forward (_end_step_after); a forward run with grad enabled and NO backward
+        after it (validation under enable_grad, a step skipped on a NaN loss) otherwise keeps its side-stream
+        work and the per-step weight / derived caches (keyed by parameter address) alive until the next
+        forward or generate.  Call this before touching parameters directly (an optimizer step, a
+        load_state_dict) or before direct asrx.ops calls in such a window.  Idempotent."""
+        self._end_step()
+
     def _end_step_after(self, *outs):
         """The step ends with the backward that follows this forward (an autograd final callback queued
         by a hook on the outputs): the dead blocks on side streams (processor.concurrent_dead_blocks)

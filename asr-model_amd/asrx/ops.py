@@ -819,19 +819,37 @@ class RotaryFn(torch.autograd.Function):
         return dx, dsrc, None, None, None, None, None
 
 
-_ROT_TABLES = {}
+_ROT_TABLES = {}  # (freqs ptr, hd, device) -> (cap, hd/2, 2) table of positions [0, cap)
+_ROT_QUANTUM = 512
 
 
 def rotary_table(freqs, L, hd):
-    """(cos, sin) of position * freqs[j] for L positions (asrx_rotary_table), built once per (freqs, L) and kept:
-    freqs is a persistent per-(dims, heads, masked, device) tensor (model.rotary_freqs)."""
-    key = (freqs.data_ptr(), int(L), int(hd), str(freqs.device))
+    """(cos, sin) of position * freqs[j] for positions [0, cap >= L) (asrx_rotary_table).  Row l of the table
+    does not depend on the length it was built for, so ONE table per (freqs, hd) serves every length: it
+    grows (geometrically, in 512-position steps) when a longer sequence arrives, so variable-length
+    training keeps O(log) tables alive instead of one per distinct length.  freqs is a persistent
+    per-(dims, heads, masked, device) tensor (model.rotary_freqs).
+
+    Streams: the processor runs dead blocks on side streams, so the stream that first needs a table is not
+    the only one that reads it.  A table enters the cache only after the device has finished it and every
+    earlier read of the table it replaces (a host sync, once per growth), so a read from any stream sees a
+    complete table and no freed one.  Under graph
+    capture (no sync possible) a missing table is built on the capturing stream, used by that one call
+    and not cached (the bench warms up on the same shapes before it captures)."""
+    key = (freqs.data_ptr(), int(hd), str(freqs.device))
     t = _ROT_TABLES.get(key)
-    if t is None:
-        t = _E(int(L), int(hd) // 2, 2, device=freqs.device)
-        lib.call("asrx_rotary_table", _P(freqs), _P(t), int(L), int(hd), _S())
-        _ROT_TABLES[key] = t
-    return t
+    if t is not None and t.shape[0] >= L:
+        return t
+    cap = max(int(L), 2 * t.shape[0] if t is not None else 0)
+    cap = (cap + _ROT_QUANTUM - 1) // _ROT_QUANTUM * _ROT_QUANTUM
+    nt = _E(cap, int(hd) // 2, 2, device=freqs.device)
+    lib.call("asrx_rotary_table", _P(freqs), _P(nt), cap, int(hd), _S())
+    if torch.cuda.is_current_stream_capturing():
+        return nt
+    # device-wide: the side streams may still read the table this one replaces
+    torch.cuda.synchronize(freqs.device)
+    _ROT_TABLES[key] = nt
+    return nt
 
 
 def rotary(x, src, freqs, hd, scale):
