@@ -198,8 +198,10 @@ def gemm_wn(A, Wb, C, *, M, N, K, lda, ldc, bias=None, Z=None, alpha=1.0, beta=0
              lib.ptr(C), cb, ldc, lib.ptr(bias), lib.ptr(Z), M, N, K, float(alpha), float(beta), ACT[act], nj,
              lib.ptr(mtiles[0]) if mtiles is not None else None, lib.ptr(mtiles[1]) if mtiles is not None else None,
              lib.stream())
+    # row-list launches: the tag carries a probe snapshot of the device-built tile count (-1: all rows)
+    rl = probe.keep(mtiles[1]) if (mtiles is not None and probe.active()) else (-1 if mtiles is None else -2)
     probe.end("gemm", e0, 2.0 * M * N * K,
-              ("wn", M, N, K, nj, int(conv), act, Z is not None, beta != 0, ab, cb, mtiles is not None))
+              ("wn", M, N, K, nj, int(conv), act, Z is not None, beta != 0, ab, cb, rl))
     return C
 
 

@@ -356,7 +356,7 @@ class LinearRes(torch.autograd.Function):
         nj = G._nj(M, N)
         e0 = probe.begin("gemm")
         lib.call("asrx_gemm_wn_res", _P(x2), K, _P(Wb), Wb.stride(0), _P(y), N, _P(b), _P(r), N, M, N, K, nj, _S())
-        probe.end("gemm", e0, 2.0 * M * N * K, ("wn", M, N, K, nj, 0, "none", False, True, 0, 0, False))
+        probe.end("gemm", e0, 2.0 * M * N * K, ("wn", M, N, K, nj, 0, "none", False, True, 0, 0, -1))
         ctx.dW, ctx.db = _direct(ctx, 2, W), _direct(ctx, 3, b)
         ctx.save_for_backward(x, W, b if ctx.db else None)
         ctx.has_b = b is not None
@@ -1674,7 +1674,7 @@ class LogitsCE(torch.autograd.Function):
         lib.call("asrx_gemm_wn_ce" if bf16_logits else "asrx_gemm_wn_ce_f32", _P(h), D, _P(Wb), Wb.stride(0), _P(zb),
                  V, _P(part), rows, V, D, nj, _S())
         probe.end("gemm", e0, 2.0 * rows * V * D,
-                  ("wn", rows, V, D, nj, 0, "none", False, False, 1, int(bf16_logits), False))
+                  ("wn", rows, V, D, nj, 0, "none", False, False, 1, int(bf16_logits), -1))
         lab = _c(labels.reshape(-1))
         loss_r = _E(rows, device=h.device)
         lse = _E(rows, device=h.device)

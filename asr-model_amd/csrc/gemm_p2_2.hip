@@ -1,0 +1,7 @@
+// Explicit instantiations of the two-workgroups-per-CU wide GEMM (gemm_p2.h), one unit per group so
+// the build compiles them in parallel.
+#define ASRX_P2_INSTANTIATE
+#include "gemm_p2.h"
+
+ASRX_P2_DECL(2, false, false)
+ASRX_P2_DECL(2, true, false)

@@ -1,7 +1,29 @@
 // Entry points of the wide GEMM (kernel and design: gemm_wr.h), the bulk weight conversion to
 // bf16 and the MSheath row-tile lists.
 #include "gemm_wr.h"
+#include "gemm_p2.h"
 #include <string>
+
+// Which wide-GEMM kernel runs the plain / residual products that gemm_p2_kernel covers (asrx_set_gemm_variant):
+// 1 (default) gemm_p2_kernel (two workgroups per CU) for tile widths 3 and 2, 2 also for width 1 (the 128-column
+// tiles: gemm_p2's NJ = 2 tile is 128 x 128), 0 gemm_wr_kernel -- A/B measurements and the tests that compare them
+static int g_wide_variant = 1;
+extern "C" int asrx_set_gemm_variant(int v) {
+  const int old = g_wide_variant;
+  g_wide_variant = v;
+  return old;
+}
+// gemm_p2_kernel takes: no k3 conv, float4-aligned C / Z (LDS-staged epilogue), tile widths 3 and 2
+// (measured, profiles/r05_p2_micro.txt: bf16-stored A 5-10 % faster at every shape; fp32 A faster up to 96000
+// rows but 9-18 % slower at 192064 rows, where its four A loads per thread and k-step cost more than the
+// overlap gains -- so fp32 A at >= 131072 rows stays on gemm_wr_kernel)
+static bool p2_ok(const asrx::wn::Params& p, int conv, int nj, int a_bf16) {
+  if (!a_bf16 && p.M >= 131072) return false;
+  const bool vec = ((p.N | p.ldc) & 3) == 0 && ((uintptr_t)p.C & 15) == 0 && ((uintptr_t)p.Z & 15) == 0 &&
+                   ((uintptr_t)p.Cb & 7) == 0;
+  return g_wide_variant >= 1 && !conv && (nj == 3 || nj == 2 || (nj == 1 && g_wide_variant == 2)) && vec &&
+         p.K >= 64;
+}
 
 namespace asrx {
 namespace wn {
@@ -127,7 +149,10 @@ extern "C" int asrx_gemm_wn_ex(const void* A, int a_bf16, int64_t lda, int conv,
 #define ASRX_WN_EX(NJV)                                                                              \
   if (a_bf16) conv ? wn::launch_wr<NJV, true, false, true>(p, stream) : wn::launch_wr<NJV, false, false, true>(p, stream); \
   else conv ? wn::launch_wr<NJV, true>(p, stream) : wn::launch_wr<NJV, false>(p, stream);
-  if (nj == 3) { ASRX_WN_EX(3) }
+  if (p2_ok(p, conv, nj, a_bf16)) {
+    if (nj == 3) a_bf16 ? wn::launch_p2_act<3, true, false>(p, stream) : wn::launch_p2_act<3, false, false>(p, stream);
+    else a_bf16 ? wn::launch_p2_act<2, true, false>(p, stream) : wn::launch_p2_act<2, false, false>(p, stream);  // nj 2 / 1
+  } else if (nj == 3) { ASRX_WN_EX(3) }
   else if (nj == 2) { ASRX_WN_EX(2) }
   else { ASRX_WN_EX(1) }
 #undef ASRX_WN_EX
@@ -195,7 +220,8 @@ extern "C" int asrx_gemm_wn_res(const float* A, int64_t lda, const unsigned shor
   ASRX_REQUIRE(nj == 1 || nj == 3, "asrx_gemm_wn_res: nj 1 or 3");
   wn::Params p{A, (int)lda, W, (int)ldw, C, (int)ldc, bias, nullptr, (int)M, (int)N, (int)K, 1, 1, 1.f, 0.f,
                ACT_NONE, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, R, (int)ldr};
-  if (nj == 3) wn::launch_wr<3, false, false, false, false, true>(p, stream);
+  if (nj == 3 && p2_ok(p, 0, nj, 0)) wn::launch_p2_act<3, false, true>(p, stream);
+  else if (nj == 3) wn::launch_wr<3, false, false, false, false, true>(p, stream);
   else wn::launch_wr<1, false, false, false, false, true>(p, stream);
   ASRX_LAUNCHED("asrx_gemm_wn_res");
 }

@@ -341,40 +341,46 @@ def main():
         "loss": loss_v,
     }
     if recs is not None:
-        n, flops, sec = probe.summarize(recs["gemm"])
+        n, _, sec = probe.summarize(recs["gemm"])
+        flops = sum(probe.gemm_flops(tag, w) for w, _, _, tag in recs["gemm"])
         peak = BF16_PEAK_TFS if args.precision == "bf16" else F32_PEAK_TFS
         achieved = flops / sec / 1e12 if sec > 0 else 0.0
         step_s = elapsed / args.steps
-        # dominant kernel: the wide bf16-weight GEMM (asrx_gemm_wn -> gemm_wr_kernel, every activation x weight product
-        # of the forward and of the input gradients; the top kernel of the rocprof summary).  At K, N <= 1536 its
-        # arithmetic intensity is below the MI355X ridge point (2500 TF/s / 8 TB/s = 312 flop/B), so its roofline
-        # is HBM bandwidth: algorithmic bytes per launch = A (M K x 4 B fp32 / 2 B bf16-stored) + W (2 N K) +
-        # C (M N x 4 / 2 B) [+ the same again if beta != 0] [+ 4 M N if the fp32 pre-activation is saved].
-        wn_n, wn_bytes, wn_flops, wn_sec = 0, 0.0, 0.0, 0.0
-        for tag, (cnt, fl, sc) in probe.by_tag(recs["gemm"]).items():
-            if not tag or tag[0] != "wn":
+        # dominant kernel: gemm_wr_kernel, the wide bf16-weight GEMM behind every activation x weight product of
+        # the forward and of the input gradients -- EVERY instantiation (plain, MSheath row-list, residual,
+        # tied logits + CE statistics, AbbyNormal router, activation-gradient), i.e. the same launch set as the
+        # rocprof summary's gemm_wr_kernel rows and the PMC table's `traffic`.  At K, N <= 1536 its arithmetic
+        # intensity is below the MI355X ridge (2500 TF/s / 8 TB/s = 312 flop/B), so its roofline is HBM
+        # bandwidth; algorithmic bytes per launch: probe.gemm_wr_bytes (row-list launches use the tile count
+        # the device built, read back after the probed step)
+        wn_n, wn_bytes, wn_flops, wn_sec, unknown = 0, 0.0, 0.0, 0.0, 0
+        for w, e0, e1, tag in recs["gemm"]:
+            byts = probe.gemm_wr_bytes(tag)
+            if byts is None:
+                unknown += int(bool(tag) and tag[0] == "wn")
                 continue
-            _, M, N, K, _nj, _conv, _act, has_z, has_beta, a_bf16, c_bf16, row_list = tag
-            if row_list:  # MSheath launches over a device-built subset of row tiles: bytes not known here
-                continue
-            ea, ec = (2 if a_bf16 else 4), (2 if c_bf16 else 4)
-            per = ea * M * K + 2 * N * K + ec * M * N * (1 + int(has_beta)) + 4 * M * N * int(has_z)
-            wn_n += cnt
-            wn_bytes += cnt * per
-            wn_flops += fl
-            wn_sec += sc
+            wn_n += 1
+            wn_bytes += byts
+            wn_flops += probe.gemm_flops(tag, w)
+            wn_sec += e0.elapsed_time(e1) * 1e-3
+        probe.clear_aux()
         if wn_sec > 0:
             gbs = wn_bytes / wn_sec / 1e9
-            result["roofline"] = {"kernel": "asrx::wn::gemm_wr_kernel (wide bf16-weight MFMA GEMM, fp32 / bf16-stored activations)",
+            result["roofline"] = {"kernel": "asrx::wn::gemm_wr_kernel, every instantiation (wide bf16-weight MFMA GEMM: "
+                                            "plain, row-list, residual, tied logits, router, activation-gradient)",
                                   "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                   "frac": round(gbs / HBM_PEAK_GBS, 4),
                                   **pmc_traffic("gemm_wr_kernel", args.config, args.batch, args.pitch_frames),
                                   "algorithmic_bytes_per_launch": round(wn_bytes / wn_n),
+                                  "algorithmic_bytes_per_step": round(wn_bytes / probe_steps),
                                   "launches_per_step": wn_n // probe_steps,
+                                  **({"launches_unaccounted": unknown} if unknown else {}),
                                   "avg_us": round(wn_sec / wn_n * 1e6, 2),
                                   "share_of_step": round(wn_sec / probe_steps / step_s, 3),
                                   "mfma_achieved_tflops": round(wn_flops / wn_sec / 1e12, 2),
-                                  "mfma_frac": round(wn_flops / wn_sec / 1e12 / peak, 4)}
+                                  "mfma_frac": round(wn_flops / wn_sec / 1e12 / peak, 4),
+                                  "recompute": "frac = algorithmic_bytes_per_step / (gemm_wr_kernel time per step in "
+                                               "the rocprof summary) / peak"}
         result["gemm_all"] = {"kernel": "every asrx GEMM launch (wide, generic fp32/bf16 incl. wgrad, router)",
                               "bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                               "frac": round(achieved / peak, 4),

@@ -146,7 +146,12 @@ EMU: set = set()
 def _r(x, point):
     if point not in EMU:
         return x
-    return x + (x.to(torch.bfloat16).to(x.dtype) - x).detach()
+    r = x.to(torch.bfloat16).to(x.dtype)
+    if "x3" in EMU:
+        # split-bf16 ("bf16x3") operands: hi = bf16(x), lo = bf16(x - hi); the 3-MFMA product
+        # hi*hi + hi*lo + lo*hi sees x as hi + lo (the dropped lo*lo term is ~2^-16 of the product's ulp)
+        r = r + (x - r).to(torch.bfloat16).to(x.dtype)
+    return x + (r - x).detach()
 
 
 class _RoundGrad(torch.autograd.Function):

@@ -91,8 +91,12 @@ def test_skip_dead_blocks_is_output_identical(cuda):
     model = Model(cfg).cuda().train()
     spec, pitch, wav, ids, labels = _toy_inputs()
     res = []
-    # (skip, dead text beside the dead audio, whole dead blocks on side streams across the backward)
-    for skip, conc, blocks in ((False, True, True), (True, True, True), (False, False, False), (False, True, False)):
+    # (skip, dead text beside the dead audio, whole dead blocks on side streams across the backward); the
+    # default schedule runs three times: its reruns measure the spread the float-atomic parameter-gradient
+    # sums give ONE schedule, the yardstick of the schedule gaps
+    sched = ((False, True, True), (False, True, True), (False, True, True), (True, True, True),
+             (False, False, False), (False, True, False))
+    for skip, conc, blocks in sched:
         model.processor.skip_dead_blocks = skip
         model.processor.concurrent_dead_text = conc
         model.processor.concurrent_dead_blocks = blocks
@@ -113,16 +117,20 @@ def test_skip_dead_blocks_is_output_identical(cuda):
         assert model.processor._pending is None
     model.processor.skip_dead_blocks = False
     model.processor.concurrent_dead_text = True
-    for other in res[1:]:  # skipped dead blocks, and dead blocks run serially on one stream
+    # rerun spread of the default schedule, per parameter (the data gradient is deterministic; the parameter
+    # gradients' float-atomic sums are not)
+    spread = {n: max(_rel(res[i][1][n], res[0][1][n]) for i in (1, 2)) for n in res[0][1]}
+    worst_spread = max((v, n) for n, v in spread.items())
+    print("rerun spread of one schedule (worst):", worst_spread)
+    # a schedule may move a gradient by no more than a small multiple of what a rerun moves it (plus one fp32
+    # ulp of headroom at the gradient's scale, for parameters whose three reruns happened to agree bitwise)
+    bound = 4.0 * worst_spread[0] + 2.0 ** -23
+    for other in res[1:]:  # reruns, skipped dead blocks, dead blocks serially, the round-3 schedule
         assert torch.equal(res[0][0], other[0])
         assert set(res[0][1]) == set(other[1])
-        # gradients: equal up to the float-atomic accumulation order of the parameter-gradient sums (the
-        # data gradient is deterministic), so the bound is test_backward_is_reproducible's for two runs of
-        # ONE schedule: a schedule may not move a gradient more than a rerun may.  (Measured: up to 1.5e-5
-        # on processor.block.2.jump.mlp_gate.0.bias, a 192k-row atomic sum, profiles/r04_gpu_tests_v2.log.)
         worst = max((_rel(other[1][n], res[0][1][n]), n) for n in res[0][1])
-        print("schedule gap (worst):", worst)
-        assert worst[0] < 1e-4, worst
+        print("schedule gap (worst):", worst, "bound", bound)
+        assert worst[0] <= bound, (worst, worst_spread)
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])

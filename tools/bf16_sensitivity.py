@@ -4,7 +4,8 @@ straight-through), decisions replayed from the pure float64 run, and its gradien
 pure float64 gradient (whole-gradient cosine, worst parameter).  usage:
   bf16_sensitivity.py B seconds T [cfg] point[,point...] ...
 points: lin (every Linear's operands but q/kv), qkproj (the q / kv projections' operands), qk (the
-attention's q, k), pv (softmax P and v), logits (the tied logits' operands)."""
+attention's q, k), pv (softmax P and v), logits (the tied logits' operands); modifiers: x3 (operands as a
+split-bf16 hi + lo pair instead of one bf16), nudgeE (no rounding: weights nudged by relative 2^-E)."""
 import os
 import sys
 import time
@@ -30,11 +31,21 @@ rec = om.Decisions()
 t0 = time.time()
 P0, r0 = mp.oracle_run(sd, ocfg, x, rec, torch.float64)
 print(f"float64 reference run {time.time() - t0:.1f}s loss {r0['loss']:.6f}", flush=True)
+def nudged(sd, seed, rel):
+    g = torch.Generator().manual_seed(1000 + seed)
+    return {k: (v.detach().double() * (1 + (torch.rand(v.shape, generator=g, dtype=torch.float64) * 2 - 1) * rel)
+                if v.is_floating_point() else v) for k, v in sd.items()}
+
+
 for pts in sets:
     om.EMU.clear()
-    om.EMU.update(p for p in pts if p != "none")
+    # "nudgeE": no rounding, weights nudged by relative 2^-E uniform noise (E = 9: bf16 resolution; 17: the
+    # resolution of a split-bf16 hi + lo pair; 24: one fp32 ulp)
+    nud = [int(p[5:]) for p in pts if p.startswith("nudge")]
+    om.EMU.update(p for p in pts if p != "none" and not p.startswith("nudge"))
     t0 = time.time()
-    Pk, rk = mp.oracle_run(sd, ocfg, x, om.Decisions(table=rec.rec), torch.float64)
+    src = nudged(sd, 0, 2.0 ** -nud[0]) if nud else sd
+    Pk, rk = mp.oracle_run(src, ocfg, x, om.Decisions(table=rec.rec), torch.float64)
     om.EMU.clear()
     d = mp.grad_distance(Pk, P0)
     lg = float((rk["logits"] - r0["logits"]).abs().max() / r0["logits"].abs().max())

@@ -12,6 +12,9 @@ from asrx import gemm as G  # noqa: E402
 from asrx import prec  # noqa: E402
 
 prec.set_precision("bf16")
+if os.environ.get("GEMM_VARIANT"):  # 1: two-workgroups-per-CU kernel (default), 0: one workgroup per CU
+    from asrx import lib  # noqa: E402
+    lib.load().asrx_set_gemm_variant(int(os.environ["GEMM_VARIANT"]))
 dev = torch.device("cuda:0")
 SHAPES = [(8192, 384, 384), (8192, 384, 1536), (8192, 1536, 384), (8192, 1152, 384), (32, 128, 384),
           (192064, 384, 384), (192064, 1536, 384), (192064, 384, 1536)]

@@ -52,19 +52,17 @@ recs = probe.disable()
 total = t0.elapsed_time(t1) * 1e-3
 print(f"eager step with spin kernels {total*1e3:.1f} ms (not a step time)")
 for kind in ("gemm", "attn", "logmel"):
-    tab = probe.by_tag(recs[kind])
+    tab = {}
+    for w, e0, e1, tag in recs[kind]:
+        byts = probe.gemm_wr_bytes(tag) if kind == "gemm" else None
+        w = probe.gemm_flops(tag, w) if kind == "gemm" else w
+        if tag and tag[0] == "wn" and tag[11] >= 0:  # row-list launch: group by the rows it computed
+            tag = tag[:11] + (("rows", int(probe.aux(tag[11]).item()) * 128),)
+        n, wk, sec, b = tab.get(tag, (0, 0.0, 0.0, 0.0))
+        tab[tag] = (n + 1, wk + w, sec + e0.elapsed_time(e1) * 1e-3, None if (byts is None) else (b or 0.0) + byts)
     tsum = sum(v[2] for v in tab.values())
     print(f"== {kind}: {sum(v[0] for v in tab.values())} launches, {tsum*1e3:.1f} ms "
           f"({100*tsum/total:.1f}% of step), {sum(v[1] for v in tab.values())/max(tsum,1e-12)/1e12:.1f} TF/s")
-    for tag, (n, w, sec) in sorted(tab.items(), key=lambda kv: -kv[1][2]):
-        extra = ""
-        if kind == "gemm" and tag and tag[0] == "wn":
-            _, M, N, K, _nj, _conv, _act, has_z, has_beta, a_bf16, c_bf16, row_list = tag
-            ea, ec = (2 if a_bf16 else 4), (2 if c_bf16 else 4)
-            byts = ea * M * K + 2 * N * K + ec * M * N * (1 + int(has_beta)) + 4 * M * N * int(has_z)
-            extra = f" {byts*n/sec/1e9:7.0f} GB/s {byts/1e6:8.1f} MB"
-        elif kind == "gemm" and tag and tag[0] == "router":
-            M, N, K = tag[1], tag[2], tag[3]
-            byts = 4 * M * K + 2 * N * K + 12 * M + 4 * M * N * int(tag[4])
-            extra = f" {byts*n/sec/1e9:7.0f} GB/s {byts/1e6:8.1f} MB"
+    for tag, (n, w, sec, byts) in sorted(tab.items(), key=lambda kv: -kv[1][2]):
+        extra = f" {byts/sec/1e9:7.0f} GB/s {byts/n/1e6:8.1f} MB" if byts is not None else ""
         print(f"{n:5d} x {sec/n*1e6:8.1f} us = {sec*1e3:7.2f} ms  {w/sec/1e12:7.1f} TF/s{extra}  {tag}")
