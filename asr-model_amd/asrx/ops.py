@@ -721,7 +721,7 @@ class AttentionFn(torch.autograd.Function):
                  _P(lse), B, H, Lq, Lk, hd, int(causal), 1.0 / math.sqrt(hd), _S())
         probe.end("attn", e0, 4.0 * B * H * Lq * Lk * hd * (0.5 if causal else 1.0), ("attn", Lq, Lk, io))
         ctx.causal = causal
-        ctx.prec = prec.get()
+        ctx.prec = prec.attention_bwd_prec()
         ctx.io = io
         ctx.save_for_backward(q, k, v, o, lse)
         # merge: heads merged '(h d)' (model.py:316), the out projection's input

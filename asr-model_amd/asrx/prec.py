@@ -8,6 +8,11 @@
                 products are unchanged and the bytes halve; the residual stream, norm inputs and
                 everything a backward reads for its own arithmetic stay fp32.
 "fp32"  (parity): exact fp32 MFMA (v_mfma_f32_16x16x4_f32) everywhere.
+"x3"    (reference-faithful training): storage and every kernel as "fp32", but the GEMMs run split-bf16 products
+                (hi*hi + hi*lo + lo*hi of x = bf16 hi + bf16 lo, ~16-bit operands; csrc/gemm.hip PREC_X3) on the
+                bf16 MFMA; attention stays exact fp32.  The float64 oracle with every GEMM / attention operand
+                rounded to a hi + lo pair keeps the whole-gradient cosine at 0.993 where one bf16 rounding gives
+                0.35 (profiles/r05_split_bf16_sensitivity.txt): the gradient mode that follows the reference's.
 
 Attention mode (orthogonal, perf mode only): "fp8" runs the attention forward with QK^T on OCP e4m3
 (per-row scales, MX-rate MFMA; softmax and PV stay bf16) -- SURVEY.md §8(b) config 5 (fp8 attention,
@@ -22,14 +27,16 @@ import contextlib
 PREC_F32 = 0
 PREC_BF16 = 1
 PREC_FP8ATT = 2  # asrx_attn_fwd only
+PREC_X3 = 3  # asrx_gemm only (split-bf16 products); everything else runs as PREC_F32
+_NAMES = {"bf16": PREC_BF16, "fp32": PREC_F32, "x3": PREC_X3}
 
 _mode = {"prec": PREC_BF16, "attn": "bf16", "store": True}
 
 
 def set_precision(name: str) -> None:
-    if name not in ("bf16", "fp32"):
-        raise ValueError(f"precision must be 'bf16' or 'fp32', got {name!r}")
-    _mode["prec"] = PREC_BF16 if name == "bf16" else PREC_F32
+    if name not in _NAMES:
+        raise ValueError(f"precision must be 'bf16', 'fp32' or 'x3', got {name!r}")
+    _mode["prec"] = _NAMES[name]
 
 
 def get() -> int:
@@ -37,7 +44,7 @@ def get() -> int:
 
 
 def name() -> str:
-    return "bf16" if _mode["prec"] == PREC_BF16 else "fp32"
+    return {v: k for k, v in _NAMES.items()}[_mode["prec"]]
 
 
 @contextlib.contextmanager
@@ -78,10 +85,15 @@ def storage(on: bool):
 
 
 def attention_prec() -> int:
-    """Precision code for asrx_attn_fwd: fp8 only on top of the bf16 perf mode."""
+    """Precision code for asrx_attn_fwd: fp8 only on top of the bf16 perf mode; x3 runs exact fp32 attention."""
     if _mode["attn"] == "fp8" and _mode["prec"] == PREC_BF16:
         return PREC_FP8ATT
-    return _mode["prec"]
+    return attention_bwd_prec()
+
+
+def attention_bwd_prec() -> int:
+    """Precision code for asrx_attn_bwd (fp8 is forward only: its backward runs the bf16 kernels)."""
+    return PREC_F32 if _mode["prec"] == PREC_X3 else _mode["prec"]
 
 
 @contextlib.contextmanager

@@ -43,10 +43,12 @@ constexpr float LN2 = 0.6931471805599453f;
 __device__ __forceinline__ int kswz(int key) { return (key >> 1) & 7; }
 __device__ __forceinline__ int vswz(int key) { return ((key >> 1) & 1) << 2; }
 
+// two floats -> one packed bf16 pair (RNE) in ONE v_cvt_pk_bf16_f32 (converting them separately and
+// combining took a conversion, a shift and an or per pair)
 __device__ __forceinline__ unsigned pack2(float a, float b) {
-  const unsigned lo = __builtin_bit_cast(unsigned short, (__bf16)a);
-  const unsigned hi = __builtin_bit_cast(unsigned short, (__bf16)b);
-  return lo | (hi << 16);
+  typedef __attribute__((ext_vector_type(2))) float f2;
+  typedef __attribute__((ext_vector_type(2))) __bf16 b2;
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((f2){a, b}, b2));
 }
 
 __device__ __forceinline__ bf16x8 pack8(const float (&v)[8]) {
@@ -206,7 +208,7 @@ __global__ __launch_bounds__(NTHR, WPE) void attn_fwd_mf_kernel(const TI* __rest
     h = blockIdx.y;
     q0 = (int64_t)blockIdx.x * QB;
   }
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int j = lane & 31, hi = lane >> 5;
   const int64_t qi = q0 + wid * 32 + j;  // this lane's query row
   const TI* kb = k + b * sk.b + h * sk.h;
@@ -265,20 +267,25 @@ __global__ __launch_bounds__(NTHR, WPE) void attn_fwd_mf_kernel(const TI* __rest
     if (PRIO) __builtin_amdgcn_s_setprio(0);
 
     // ---- mask + online softmax (lane = query j, keys crow(r, hi) of each block)
-    const bool need_mask = (k0 + KT > Lk) || (causal && k0 + KT - 1 > q0 + wid * 32);
+    // wave-uniform (readfirstlane: the compiler cannot prove wid uniform, and a per-lane mask flag turned the
+    // block below into a 32-deep exec-masked branch chain run on EVERY tile, ~100 scalar instructions)
+    const bool need_mask =
+        __builtin_amdgcn_readfirstlane((int)((k0 + KT > Lk) || (causal && k0 + KT - 1 > q0 + wid * 32))) != 0;
+    if (need_mask) {  // keys of this tile at or past lim are masked: key >= Lk, or key > qi when causal
+      const int lim = (int)min(min(Lk - k0, (int64_t)KT), causal ? qi - k0 + 1 : (int64_t)KT);
+#pragma unroll
+      for (int kb2 = 0; kb2 < 2; ++kb2)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = 32 * kb2 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+          sacc[kb2][r] = key >= lim ? -INFINITY : sacc[kb2][r];
+        }
+    }
     float tmax = -INFINITY;
 #pragma unroll
     for (int kb2 = 0; kb2 < 2; ++kb2)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float x = sacc[kb2][r];
-        if (need_mask) {
-          const int64_t key = k0 + 32 * kb2 + (r & 3) + 8 * (r >> 2) + 4 * hi;
-          if (key >= Lk || (causal && key > qi)) x = -INFINITY;
-          sacc[kb2][r] = x;
-        }
-        tmax = fmaxf(tmax, x);
-      }
+      for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, sacc[kb2][r]);
     {  // xor-32 partner by v_permlane32_swap (VALU) instead of a ds_bpermute round trip
       float ta = tmax, tb = tmax;
       xrow32(ta, tb);
@@ -298,21 +305,30 @@ __global__ __launch_bounds__(NTHR, WPE) void attn_fwd_mf_kernel(const TI* __rest
         for (int r = 0; r < 16; ++r) oacc[d][r] *= alpha;
     }
     const float mc = m == -INFINITY ? 0.f : m * c;
+    // exp arguments and the row-sum partials two at a time on the packed FP32 ALU (v_pk_fma_f32 /
+    // v_pk_add_f32: half the issue of the scalar forms); four independent partial sums instead of one
+    // dependent chain of 32 adds
+    typedef __attribute__((ext_vector_type(2))) float f2;
+    const f2 c2 = {c, c}, m2 = {-mc, -mc};
     bf16x8 pb[2][2];
-    float lsum = 0.f;
+    f2 ls[2] = {{0.f, 0.f}, {0.f, 0.f}};
 #pragma unroll
     for (int kb2 = 0; kb2 < 2; ++kb2)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         float pv[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          pv[e] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[kb2][8 * s2 + e], c, -mc));
-          lsum += pv[e];
+        for (int e = 0; e < 8; e += 2) {
+          const f2 x = {sacc[kb2][8 * s2 + e], sacc[kb2][8 * s2 + e + 1]};
+          const f2 a = __builtin_elementwise_fma(x, c2, m2);
+          pv[e] = __builtin_amdgcn_exp2f(a.x);
+          pv[e + 1] = __builtin_amdgcn_exp2f(a.y);
+          ls[(e >> 1) & 1] += (f2){pv[e], pv[e + 1]};
         }
         pb[kb2][s2] = pack8(pv);
       }
-    l += lsum;
+    const f2 lt2 = ls[0] + ls[1];
+    l += lt2.x + lt2.y;
 
     // ---- O^T += V^T P^T
     if (PRIO) __builtin_amdgcn_s_setprio(1);
@@ -337,175 +353,6 @@ __global__ __launch_bounds__(NTHR, WPE) void attn_fwd_mf_kernel(const TI* __rest
   }
 
   // ---- finalize: l over both halves, O = O^T / l, lse in natural log
-  const float lt = l + __shfl_xor(l, 32);
-  if (qi < Lq) {
-    store_rowT<HD, TO>(o + b * so.b + h * so.h + qi * so.l, oacc, 1.0f / lt, hi);
-    if (hi == 0) lse[((int64_t)b * H + h) * Lq + qi] = (m * c + __builtin_amdgcn_logf(lt)) * LN2;
-  }
-}
-
-// --------------------------------------------------------------------------------------------
-// Software-pipelined forward (attn_fwd_pp_kernel): attn_fwd_mf_kernel's tiles, fragments and online
-// softmax, with the QK^T of tile t+1 issued BEFORE the softmax of tile t.  The softmax's VALU work (exp,
-// max, convert: ~19 VALU per MFMA, profiles/r04_attn_fwd_sq.txt) then runs while the matrix pipe works
-// on the next tile's scores, instead of between two MFMA phases that wait on it.  K is one tile ahead
-// of V: at iteration t the wave reads K(t+1) and V(t) while the block writes K(t+2) and V(t+1), so
-// each of the two double-buffered images is read and written on disjoint halves (one barrier per
-// tile, as before).  Bit-identical to attn_fwd_mf_kernel (same products in the same order).
-template <int HD, typename TI, typename TO>
-__global__ __launch_bounds__(NTHR, 1) void attn_fwd_pp_kernel(const TI* __restrict__ q, const TI* __restrict__ k,
-                                                             const TI* __restrict__ v, TO* __restrict__ o,
-                                                             float* __restrict__ lse, AttnStridesMF sq,
-                                                             AttnStridesMF sk, AttnStridesMF sv, AttnStridesMF so,
-                                                             int64_t H, int64_t Lq, int64_t Lk, int causal,
-                                                             float scale) {
-  constexpr int NH = HD / 64;
-  __shared__ __attribute__((aligned(16))) unsigned short Ks[2][NH * HALF];
-  __shared__ __attribute__((aligned(16))) unsigned short Vs[2][NH * HALF];
-
-  const int64_t nqb = (Lq + QB - 1) / QB;
-  const int64_t L = xcd_logical(blockIdx.x, (int64_t)gridDim.x);
-  const int64_t q0 = (L % nqb) * QB;
-  const int h = (int)((L / nqb) % H);
-  const int b = (int)(L / (nqb * H));
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int j = lane & 31, hi = lane >> 5;
-  const int64_t qi = q0 + wid * 32 + j;
-  const TI* kb = k + b * sk.b + h * sk.h;
-  const TI* vb = v + b * sv.b + h * sv.h;
-  const float c = scale * LOG2E;
-
-  bf16x8 qf[HD / 16];
-  row_frags<HD>(q + b * sq.b + h * sq.h, sq.l, qi, Lq, hi, qf);
-
-  int64_t kend = Lk;
-  if (causal) kend = min(Lk, q0 + QB);
-  const int ntiles = (int)((kend + KT - 1) / KT);
-  const int skey = tid >> 3, sc = tid & 7;
-
-  Row8<TI> ka[NH], va[NH];
-#pragma unroll
-  for (int hf = 0; hf < NH; ++hf) {  // K(0), V(0), K(1)
-    stage_load(kb, sk, skey, Lk, hf, sc, ka[hf]);
-    stage_load(vb, sv, skey, Lk, hf, sc, va[hf]);
-    stage_store(Ks[0] + hf * HALF, skey, sc ^ kswz(skey), ka[hf]);
-    stage_store(Vs[0] + hf * HALF, skey, sc ^ vswz(skey), va[hf]);
-  }
-  if (ntiles > 1) {
-#pragma unroll
-    for (int hf = 0; hf < NH; ++hf) {
-      stage_load(kb, sk, KT + skey, Lk, hf, sc, ka[hf]);
-      stage_store(Ks[1] + hf * HALF, skey, sc ^ kswz(skey), ka[hf]);
-    }
-  }
-  __syncthreads();
-
-  auto scores = [&](f32x16 (&s)[2], const unsigned short* Kt) __attribute__((always_inline)) {
-#pragma unroll
-    for (int kb2 = 0; kb2 < 2; ++kb2) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) s[kb2][r] = 0.f;
-      dot_rows<HD>(s[kb2], Kt, 32 * kb2 + j, hi, qf);
-    }
-  };
-  f32x16 sA[2], sB[2];
-  scores(sA, Ks[0]);
-  __syncthreads();  // every wave's K(0) reads done: iteration 0 overwrites Ks[0] with K(2)
-
-  f32x16 oacc[HD / 32];
-#pragma unroll
-  for (int d = 0; d < HD / 32; ++d)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) oacc[d][r] = 0.f;
-  float m = -INFINITY;
-  float l = 0.f;
-
-  auto iter = [&](int t, f32x16 (&sc_cur)[2], f32x16 (&sc_nxt)[2]) __attribute__((always_inline)) {
-    const int64_t k0 = (int64_t)t * KT;
-    // global loads for the images written at the end of this iteration: K(t+2), V(t+1)
-    if (t + 2 < ntiles) {
-#pragma unroll
-      for (int hf = 0; hf < NH; ++hf) stage_load(kb, sk, k0 + 2 * KT + skey, Lk, hf, sc, ka[hf]);
-    }
-    if (t + 1 < ntiles) {
-#pragma unroll
-      for (int hf = 0; hf < NH; ++hf) stage_load(vb, sv, k0 + KT + skey, Lk, hf, sc, va[hf]);
-    }
-    // the next tile's scores go to the matrix pipe first; the softmax below overlaps them
-    if (t + 1 < ntiles) scores(sc_nxt, Ks[(t + 1) & 1]);
-
-    const bool need_mask = (k0 + KT > Lk) || (causal && k0 + KT - 1 > q0 + wid * 32);
-    float tmax = -INFINITY;
-#pragma unroll
-    for (int kb2 = 0; kb2 < 2; ++kb2)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float x = sc_cur[kb2][r];
-        if (need_mask) {
-          const int64_t key = k0 + 32 * kb2 + (r & 3) + 8 * (r >> 2) + 4 * hi;
-          if (key >= Lk || (causal && key > qi)) x = -INFINITY;
-          sc_cur[kb2][r] = x;
-        }
-        tmax = fmaxf(tmax, x);
-      }
-    {
-      float ta = tmax, tb = tmax;
-      xrow32(ta, tb);
-      tmax = fmaxf(ta, tb);
-    }
-    const bool up = tmax * c > m * c + 8.f;
-    if (__any(up)) {
-      const float alpha = up ? __builtin_amdgcn_exp2f(m * c - tmax * c) : 1.f;
-      if (up) m = tmax;
-      l *= alpha;
-#pragma unroll
-      for (int d = 0; d < HD / 32; ++d)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) oacc[d][r] *= alpha;
-    }
-    const float mc = m == -INFINITY ? 0.f : m * c;
-    bf16x8 pb[2][2];
-    float lsum = 0.f;
-#pragma unroll
-    for (int kb2 = 0; kb2 < 2; ++kb2)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        float pv[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          pv[e] = __builtin_amdgcn_exp2f(__builtin_fmaf(sc_cur[kb2][8 * s2 + e], c, -mc));
-          lsum += pv[e];
-        }
-        pb[kb2][s2] = pack8(pv);
-      }
-    l += lsum;
-
-    const unsigned short* Vt = Vs[t & 1];
-#pragma unroll
-    for (int kb2 = 0; kb2 < 2; ++kb2)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int d = 0; d < HD / 32; ++d)
-          oacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Vt + (d >> 1) * HALF, lane, kb2, s2, d & 1),
-                                                            pb[kb2][s2], oacc[d], 0, 0, 0);
-    // K(t) was read in iteration t-1 and V(t-1) there too: both images are free to refill
-    if (t + 2 < ntiles) {
-#pragma unroll
-      for (int hf = 0; hf < NH; ++hf) stage_store(Ks[t & 1] + hf * HALF, skey, sc ^ kswz(skey), ka[hf]);
-    }
-    if (t + 1 < ntiles) {
-#pragma unroll
-      for (int hf = 0; hf < NH; ++hf) stage_store(Vs[(t + 1) & 1] + hf * HALF, skey, sc ^ vswz(skey), va[hf]);
-    }
-    __syncthreads();
-  };
-
-  for (int t = 0; t < ntiles; t += 2) {
-    iter(t, sA, sB);
-    if (t + 1 < ntiles) iter(t + 1, sB, sA);
-  }
-
   const float lt = l + __shfl_xor(l, 32);
   if (qi < Lq) {
     store_rowT<HD, TO>(o + b * so.b + h * so.h + qi * so.l, oacc, 1.0f / lt, hi);
@@ -554,7 +401,7 @@ __global__ __launch_bounds__(BwdCfg<HD>::NT, 1) void attn_bwd_dkdv_mf_kernel(
   const int64_t nkb = (Lk + 32 * C::NW - 1) / (32 * C::NW), L = xcd_logical(blockIdx.x, gridDim.x);
   const int b = (int)(L / (nkb * H)), h = (int)((L / nkb) % H);
   const int64_t k0 = (L % nkb) * (32 * C::NW);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int j = lane & 31, hi = lane >> 5;
   const int64_t key = k0 + wid * 32 + j;  // this lane's key
   const TI* qb = q + b * sq.b + h * sq.h;
@@ -619,7 +466,8 @@ __global__ __launch_bounds__(BwdCfg<HD>::NT, 1) void attn_bwd_dkdv_mf_kernel(
     const int buf = t & 1;
     const int64_t q0 = (qt0 + t) * BQT;
     if (t + 1 < ntiles) stage_ld(t + 1);
-    const bool need_mask = causal && q0 < k0 + wid * 32 + 32;
+    const bool need_mask = __builtin_amdgcn_readfirstlane((int)(causal && q0 < k0 + wid * 32 + 32)) != 0;
+    const int kq = (int)(key - q0);  // this lane's key relative to the tile's first query
     // one 32-query half at a time (keeps S / dP / P / dS of a single half live)
 #pragma unroll
     for (int qb2 = 0; qb2 < 2; ++qb2) {
@@ -642,13 +490,22 @@ __global__ __launch_bounds__(BwdCfg<HD>::NT, 1) void attn_bwd_dkdv_mf_kernel(
           const float4 lo = *reinterpret_cast<const float4*>(&LD[buf][ql]);
           const float4 hi4 = *reinterpret_cast<const float4*>(&LD[buf][ql + 2]);
           const float l2v[4] = {lo.x, lo.z, hi4.x, hi4.z}, dlv[4] = {lo.y, lo.w, hi4.y, hi4.w};
+          // two elements at a time on the packed FP32 ALU (exp stays scalar)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
+          for (int e = 0; e < 4; e += 2) {
+            typedef __attribute__((ext_vector_type(2))) float f2;
             const int r = 8 * s2 + 4 * e4 + e;
-            float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[r], c, -l2v[e]));
-            if (need_mask && key > q0 + ql + e) p = 0.f;
-            pv[4 * e4 + e] = p;
-            dsv[4 * e4 + e] = p * (pacc[r] - dlv[e]);
+            const f2 a = __builtin_elementwise_fma((f2){sacc[r], sacc[r + 1]}, (f2){c, c}, (f2){-l2v[e], -l2v[e + 1]});
+            f2 p = {__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
+            if (need_mask) {
+              p.x = kq > ql + e ? 0.f : p.x;
+              p.y = kq > ql + e + 1 ? 0.f : p.y;
+            }
+            const f2 ds = p * ((f2){pacc[r], pacc[r + 1]} - (f2){dlv[e], dlv[e + 1]});
+            pv[4 * e4 + e] = p.x;
+            pv[4 * e4 + e + 1] = p.y;
+            dsv[4 * e4 + e] = ds.x;
+            dsv[4 * e4 + e + 1] = ds.y;
           }
         }
         const bf16x8 pb = pack8(pv), sb = pack8(dsv);
@@ -686,7 +543,7 @@ __global__ __launch_bounds__(BwdCfg<HD>::NT, 1) void attn_bwd_dq_mf_kernel(
   const int64_t nqb = (Lq + 32 * C::NW - 1) / (32 * C::NW), L = xcd_logical(blockIdx.x, gridDim.x);
   const int b = (int)(L / (nqb * H)), h = (int)((L / nqb) % H);
   const int64_t q0 = (L % nqb) * (32 * C::NW);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int j = lane & 31, hi = lane >> 5;
   const int64_t qi = q0 + wid * 32 + j;  // this lane's query row
   const TI* kbp = k + b * sk.b + h * sk.h;
@@ -750,7 +607,9 @@ __global__ __launch_bounds__(BwdCfg<HD>::NT, 1) void attn_bwd_dq_mf_kernel(
       dot_rows<HD>(sacc[kb2], Kr[buf], 32 * kb2 + j, hi, qf);
       dot_rows<HD>(pacc[kb2], Vr[buf], 32 * kb2 + j, hi, gf);
     }
-    const bool need_mask = (k0 + KT > Lk) || (causal && k0 + KT - 1 > q0 + wid * 32);
+    const bool need_mask =
+        __builtin_amdgcn_readfirstlane((int)((k0 + KT > Lk) || (causal && k0 + KT - 1 > q0 + wid * 32))) != 0;
+    const int lim = need_mask ? (int)min(min(Lk - k0, (int64_t)KT), causal ? qi - k0 + 1 : (int64_t)KT) : KT;
     bf16x8 sb[2][2];
 #pragma unroll
     for (int kb2 = 0; kb2 < 2; ++kb2)
@@ -758,14 +617,18 @@ __global__ __launch_bounds__(BwdCfg<HD>::NT, 1) void attn_bwd_dq_mf_kernel(
       for (int s2 = 0; s2 < 2; ++s2) {
         float dsv[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
+        for (int e = 0; e < 8; e += 2) {  // two elements at a time on the packed FP32 ALU
+          typedef __attribute__((ext_vector_type(2))) float f2;
           const int r = 8 * s2 + e;
-          float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[kb2][r], c, -l2));
+          const f2 a = __builtin_elementwise_fma((f2){sacc[kb2][r], sacc[kb2][r + 1]}, (f2){c, c}, (f2){-l2, -l2});
+          f2 p = {__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
           if (need_mask) {
-            const int64_t kk = k0 + 32 * kb2 + (r & 3) + 8 * (r >> 2) + 4 * hi;
-            if (kk >= Lk || (causal && kk > qi)) p = 0.f;
+            p.x = (32 * kb2 + (r & 3) + 8 * (r >> 2) + 4 * hi) >= lim ? 0.f : p.x;
+            p.y = (32 * kb2 + ((r + 1) & 3) + 8 * ((r + 1) >> 2) + 4 * hi) >= lim ? 0.f : p.y;
           }
-          dsv[e] = p * (pacc[kb2][r] - dl);
+          const f2 ds = p * ((f2){pacc[kb2][r], pacc[kb2][r + 1]} - (f2){dl, dl});
+          dsv[e] = ds.x;
+          dsv[e + 1] = ds.y;
         }
         sb[kb2][s2] = pack8(dsv);
       }
@@ -786,13 +649,6 @@ __global__ __launch_bounds__(BwdCfg<HD>::NT, 1) void attn_bwd_dq_mf_kernel(
 
 }  // namespace amf
 
-// forward kernel selection (asrx_set_attn_variant): 1 the software-pipelined attn_fwd_pp_kernel for launches
-// of more than one query block, 0 (default) attn_fwd_mf_kernel -- bit-identical, an A/B switch.  Measured
-// (profiles/r05_attn_micro.txt): the pipelined kernel is 19-23 % SLOWER at the step's shapes (2185 vs 1775 us at
-// 64 x 6 heads x 3001^2): its second score set pushes it to 256 VGPRs with spills, and the exp / max chain
-// still waits on the scores it needs, so it stays behind the switch
-static int g_attn_variant = 0;
-
 template <int HD, typename TI, typename TO>
 static void attn_fwd_mf_t(const void* q, AttnStridesMF Sq, const void* k, AttnStridesMF Sk, const void* v,
                           AttnStridesMF Sv, void* o, AttnStridesMF So, float* lse, int64_t B, int64_t H, int64_t Lq,
@@ -803,10 +659,7 @@ static void attn_fwd_mf_t(const void* q, AttnStridesMF Sq, const void* k, AttnSt
   // query blocks of one (b, h) on one XCD when there are several (3.6 % at 3001 x 3001, H = 6,
   // B = 64; profiles/r02_attn_fwd_variants.txt, which also records the rejected 4-waves-per-SIMD
   // and s_setprio variants)
-  if (g_attn_variant == 1 && HD == 64 && g.x > 1)  // HD 128: the pipelined kernel spills
-    amf::attn_fwd_pp_kernel<HD, TI, TO><<<dim3((unsigned)((int64_t)g.x * g.y * g.z)), amf::NTHR, 0, stream>>>(
-        qq, kk, vv, oo, lse, Sq, Sk, Sv, So, H, Lq, Lk, causal, scale);
-  else if (HD == 64 && g.x > 1)
+  if (HD == 64 && g.x > 1)
     amf::attn_fwd_mf_kernel<HD, 1, true, false, TI, TO><<<dim3((unsigned)((int64_t)g.x * g.y * g.z)), amf::NTHR, 0,
                                                           stream>>>(qq, kk, vv, oo, lse, Sq, Sk, Sv, So, H, Lq, Lk,
                                                                     causal, scale);
@@ -891,9 +744,3 @@ int attn_bwd_mf(int io, const void* q, const int64_t* sq, const void* k, const i
 }
 
 }  // namespace asrx
-
-extern "C" int asrx_set_attn_variant(int v) {
-  const int old = asrx::g_attn_variant;
-  asrx::g_attn_variant = v;
-  return old;
-}

@@ -19,7 +19,9 @@ typedef __attribute__((ext_vector_type(16))) float f32x16;
 
 namespace asrx {
 
-enum Prec : int { PREC_F32 = 0, PREC_BF16 = 1 };
+// PREC_X3: fp32 storage with split-bf16 products (x = hi + lo, hi = bf16(x), lo = bf16(x - hi); a product is
+// hi*hi + hi*lo + lo*hi on the bf16 MFMA, ~2^-16 relative per operand) -- asrx_gemm only
+enum Prec : int { PREC_F32 = 0, PREC_BF16 = 1, PREC_X3 = 3 };
 
 enum Act : int { ACT_NONE = 0, ACT_GELU = 1, ACT_SILU = 2, ACT_SIGMOID = 3, ACT_RELU = 4 };
 // small_linear only: softmax over the N outputs of each row (forward only; the caller differentiates it)

@@ -12,7 +12,13 @@
 //
 // PREC_BF16: operands are rounded to bf16 while staging into LDS and multiplied with
 //            v_mfma_f32_16x16x32_bf16 (fp32 accumulate)          — the perf mode;
-// PREC_F32:  exact fp32 v_mfma_f32_16x16x4_f32                    — the parity mode.
+// PREC_F32:  exact fp32 v_mfma_f32_16x16x4_f32                    — the parity mode;
+// PREC_X3:   split bf16 ("bf16x3"): each fp32 fragment value x is split into hi = bf16(x) and
+//            lo = bf16(x - hi) when it is read from LDS, and the product is lo*hi + hi*lo + hi*hi on
+//            v_mfma_f32_16x16x32_bf16 (the lo*lo term, ~2^-16 of an operand's ulp, is dropped): ~16-bit
+//            operand precision at 3/16 of the fp32 MFMA's cycles -- the reference-faithful training mode
+//            (tools/bf16_sensitivity.py x3: whole-gradient cosine 0.993 with float64 where one bf16
+//            rounding gives 0.35, profiles/r05_split_bf16_sensitivity.txt).
 //
 // Tiling: 128x128 block tile, 256 threads = 4 waves (2x2), 64x64 per wave = 4x4 MFMA 16x16 tiles,
 // BK = 32.  fp32 tiles stream HBM -> LDS by LDS-DMA (global_load_lds_dwordx4, 8 x 1 KB per wave per
@@ -157,6 +163,16 @@ __device__ __forceinline__ bf16x8 to_bf16x8(const float (&f)[8]) {
   return r;
 }
 
+// x = hi + lo to ~16 bits: hi = bf16(x) (RNE), lo = bf16(x - hi) (x - hi is exact in fp32)
+__device__ __forceinline__ void split_bf16x8(const float (&f)[8], bf16x8& hi, bf16x8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 h = (__bf16)f[j];
+    hi[j] = h;
+    lo[j] = (__bf16)(f[j] - (float)h);
+  }
+}
+
 // acc[mt][nt] += A(wave rows, 32 k) * B(wave cols, 32 k)^T from one stage.
 template <int PREC, bool A_KC, bool B_KC>
 __device__ __forceinline__ void mma_stage(f32x4 (&acc)[4][4], const char* At, const char* Bt, int wm, int wn) {
@@ -181,6 +197,29 @@ __device__ __forceinline__ void mma_stage(f32x4 (&acc)[4][4], const char* At, co
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt)
         acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt], b[nt], acc[mt][nt], 0, 0, 0);
+  } else if constexpr (PREC == PREC_X3) {
+    bf16x8 ah[4], al[4], bh[4], bl[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      float f[8];
+      read8<A_KC>(At, wm * 64 + mt * 16 + lr, 8 * lk, f);
+      split_bf16x8(f, ah[mt], al[mt]);
+    }
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      float f[8];
+      read8<B_KC>(Bt, wn * 64 + nt * 16 + lr, 8 * lk, f);
+      split_bf16x8(f, bh[nt], bl[nt]);
+    }
+    // small terms first: they are added to the accumulator before the leading product
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[mt], bh[nt], acc[mt][nt], 0, 0, 0);
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[mt], bl[nt], acc[mt][nt], 0, 0, 0);
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[mt], bh[nt], acc[mt][nt], 0, 0, 0);
+      }
   } else {
 #pragma unroll
     for (int ks = 0; ks < BK / 4; ++ks) {
@@ -353,7 +392,7 @@ extern "C" int asrx_gemm(int prec, const float* A, int64_t lda, int64_t sA, int 
                          int64_t ldc, int64_t sC, const float* bias, float* Z, int64_t M, int64_t N,
                          int64_t K, int64_t batch, float alpha, float beta, int act, int64_t conv_F,
                          int64_t conv_C, int splitk, hipStream_t stream) {
-  ASRX_REQUIRE(prec == PREC_F32 || prec == PREC_BF16, "asrx_gemm: bad precision %d", prec);
+  ASRX_REQUIRE(prec == PREC_F32 || prec == PREC_BF16 || prec == PREC_X3, "asrx_gemm: bad precision %d", prec);
   ASRX_REQUIRE(M > 0 && N > 0 && K > 0 && batch > 0, "asrx_gemm: empty problem M=%ld N=%ld K=%ld",
                (long)M, (long)N, (long)K);
   ASRX_REQUIRE(aligned16(A) && aligned16(B), "asrx_gemm: A/B must be 16-byte aligned");
@@ -403,6 +442,7 @@ extern "C" int asrx_gemm(int prec, const float* A, int64_t lda, int64_t sA, int 
   ASRX_REQUIRE(spanA < (1LL << 31) && spanB < (1LL << 31) && K < (1LL << 31),
                "asrx_gemm: operand spans >= 2^31 elements");
   if (prec == PREC_BF16) launch_prec<PREC_BF16>(p, a_kc, b_kc, conv_a, conv_b, g, stream);
+  else if (prec == PREC_X3) launch_prec<PREC_X3>(p, a_kc, b_kc, conv_a, conv_b, g, stream);
   else launch_prec<PREC_F32>(p, a_kc, b_kc, conv_a, conv_b, g, stream);
   ASRX_LAUNCHED("asrx_gemm");
 }

@@ -63,6 +63,42 @@ __device__ __forceinline__ void load(const Params& p, Stage<NJ, ABF>& st, int m0
   }
 }
 
+// Fast addressing (launches whose operands span < 4 GiB and whose K is a multiple of the k-step): each
+// thread's row byte offsets are computed once per tile (rows past M / N clamped to the last row: they only
+// feed accumulator rows / columns the epilogue never stores), and a k-step's load is a uniform base
+// (operand + k bytes, SGPR) plus that offset -- one address add per load instead of the general path's
+// ~15 instructions of row / zero-page selection, which made the k-step issue-bound.
+template <int NJ, bool ABF>
+struct Off {
+  uint32_t a[Geo<NJ, ABF>::ACH];
+  uint32_t w[Geo<NJ, ABF>::WCH];
+};
+template <int NJ, bool ABF>
+__device__ __forceinline__ void offsets(const Params& p, Off<NJ, ABF>& o, int m0, int n0) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < Geo<NJ, ABF>::ACH; ++i) {
+    const int q = t + NT2 * i;
+    const int row = min(m0 + (ABF ? (q >> 2) : (q >> 3)), p.M - 1), c = ABF ? (q & 3) : (q & 7);
+    o.a[i] = ABF ? (uint32_t)(((int64_t)row * p.lda + 8 * c) * 2) : (uint32_t)(((int64_t)row * p.lda + 4 * c) * 4);
+  }
+#pragma unroll
+  for (int i = 0; i < Geo<NJ, ABF>::WCH; ++i) {
+    const int q = t + NT2 * i;
+    const int n = min(n0 + (q >> 2), p.N - 1);
+    o.w[i] = (uint32_t)(((int64_t)n * p.ldw + 8 * (q & 3)) * 2);
+  }
+}
+template <int NJ, bool ABF>
+__device__ __forceinline__ void load_fast(const Params& p, Stage<NJ, ABF>& st, const Off<NJ, ABF>& o, int k0) {
+  const char* A = reinterpret_cast<const char*>(p.A) + (size_t)k0 * (ABF ? 2 : 4);
+  const char* W = reinterpret_cast<const char*>(p.W) + (size_t)k0 * 2;
+#pragma unroll
+  for (int i = 0; i < Geo<NJ, ABF>::ACH; ++i) st.a[i] = *reinterpret_cast<const u32x4*>(A + o.a[i]);
+#pragma unroll
+  for (int i = 0; i < Geo<NJ, ABF>::WCH; ++i) st.b[i] = *reinterpret_cast<const u32x4*>(W + o.w[i]);
+}
+
 // registers -> LDS images ([rows][4 chunks of 8 bf16], chunk XOR swb(row), as gemm_wr.h wr_store)
 template <int NJ, bool ABF>
 __device__ __forceinline__ void store(const Stage<NJ, ABF>& st, char* At, char* Bt) {
@@ -91,6 +127,12 @@ __device__ __forceinline__ void store(const Stage<NJ, ABF>& st, char* At, char* 
 }
 }  // namespace p2
 
+#ifndef P2_ABL
+#define P2_ABL 0  // timing ablations (wrong results): 1 no global loads, 2 no LDS image writes, 4 no MFMA, 8 no epilogue
+#endif
+#ifndef P2_FAST
+#define P2_FAST 1  // 0: every load takes the general (zero-page select) path -- A/B builds only
+#endif
 #ifndef P2_DEPTH
 #define P2_DEPTH 3  // register stages in flight (k-steps of prefetch)
 #endif
@@ -142,8 +184,19 @@ __global__ __launch_bounds__(p2::NT2, 2) void gemm_p2_kernel(Params p, int ntile
   cs = cl;
   ce = cl;
   typedef Stage<NJ, ABF> Stg;
+  // past this workgroup's last tile the load cursor's rows lie beyond M: the fast path clamps them to row
+  // M - 1 (in bounds; the data feeds no stored output), the general path reads the zero page
+  // (not for fp32 A at NJ = 3: its seven offsets push the kernel into scratch)
+  const bool fast = P2_FAST && (ABF || NJ < 3) && p.K % BK == 0 && (uint64_t)p.M * p.lda * (ABF ? 2 : 4) < (1ull << 32) &&
+                    (uint64_t)p.N * p.ldw * 2 < (1ull << 32);
+  Off<NJ, ABF> off;
   auto ld = [&](Stg& st) __attribute__((always_inline)) {
-    load<NJ, ABF>(p, st, cl.m0, cl.n0, cl.kk * BK);
+    if (fast) {
+      if (cl.kk == 0) offsets<NJ, ABF>(p, off, cl.m0, cl.n0);
+      load_fast<NJ, ABF>(p, st, off, cl.kk * BK);
+    } else {
+      load<NJ, ABF>(p, st, cl.m0, cl.n0, cl.kk * BK);
+    }
     advance(cl);
   };
   auto st_lds = [&](int s, const Stg& st) __attribute__((always_inline)) {
@@ -170,7 +223,11 @@ __global__ __launch_bounds__(p2::NT2, 2) void gemm_p2_kernel(Params p, int ntile
   __syncthreads();
 
   auto kstep = [&](int s, Stg& cur, const Stg& nxt) __attribute__((always_inline)) {
+#if !(P2_ABL & 1)
     ld(cur);  // step s + 3 (unconditional: past the last step the rows read the zero page)
+#else
+    advance(cl);
+#endif
     const char* At = a_img[s & 1];
     const char* Bt = b_img[s & 1];
     bf16x8 a[4], b[NT];
@@ -188,10 +245,29 @@ __global__ __launch_bounds__(p2::NT2, 2) void gemm_p2_kernel(Params p, int ntile
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt)
+#if !(P2_ABL & 4)
         acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nt], a[mt], acc[mt][nt], 0, 0, 0);
+#else
+        acc[mt][nt][0] += (float)a[mt][0] * (float)b[nt][0];
+#endif
+#if !(P2_ABL & 2)
     if (s + 1 < S) st_lds(s + 1, nxt);
+#else
+    advance(cs);
+#endif
     if (ce.kk == nk - 1) {
+#if !(P2_ABL & 8)
       epilogue_lds<NJ, ACT, RES>(p, acc, bias_s[ce.j & 1], ce.m0, ce.n0, wm, wn, lr, lk, ep);
+#else
+      {  // the accumulators feed a never-taken store
+        float t = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int q = 0; q < NT; ++q) t += acc[i][q][0] + acc[i][q][1] + acc[i][q][2] + acc[i][q][3];
+        if (t == 1.2345e-37f) p.C[ce.m0] = t;
+      }
+#endif
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll

@@ -38,7 +38,9 @@ def parse():
     ap.add_argument("--config", default="tiny")
     ap.add_argument("--batch", type=int, default=32, help="clips per GPU")
     ap.add_argument("--text-len", type=int, default=256)
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32", "x3"],
+                    help="bf16: the perf mode (headline); fp32: exact fp32 MFMA (parity); x3: fp32 storage with "
+                         "split-bf16 GEMM products and fp32 attention (the gradient mode that follows the reference)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true", help="skip the live per-kernel event probe")
     ap.add_argument("--no-optimizer", action="store_true", help="skip timing the fused MaxFactor step")
@@ -343,7 +345,10 @@ def main():
     if recs is not None:
         n, _, sec = probe.summarize(recs["gemm"])
         flops = sum(probe.gemm_flops(tag, w) for w, _, _, tag in recs["gemm"])
-        peak = BF16_PEAK_TFS if args.precision == "bf16" else F32_PEAK_TFS
+        # x3: a split-bf16 product costs three bf16 MFMAs, so its GEMM ceiling is a third of the bf16 peak in
+        # useful (fp32-equivalent) flops; its attention runs the fp32 kernels
+        peak = {"bf16": BF16_PEAK_TFS, "fp32": F32_PEAK_TFS, "x3": BF16_PEAK_TFS / 3}[args.precision]
+        apeak = {"bf16": BF16_PEAK_TFS, "fp32": F32_PEAK_TFS, "x3": F32_PEAK_TFS}[args.precision]
         achieved = flops / sec / 1e12 if sec > 0 else 0.0
         step_s = elapsed / args.steps
         # dominant kernel: gemm_wr_kernel, the wide bf16-weight GEMM behind every activation x weight product of
@@ -366,11 +371,13 @@ def main():
         probe.clear_aux()
         if wn_sec > 0:
             gbs = wn_bytes / wn_sec / 1e9
-            result["roofline"] = {"kernel": "asrx::wn::gemm_wr_kernel, every instantiation (wide bf16-weight MFMA GEMM: "
-                                            "plain, row-list, residual, tied logits, router, activation-gradient)",
+            result["roofline"] = {"kernel": "asrx::wn::gemm_wr_kernel + gemm_p2_kernel, every instantiation (the wide "
+                                            "bf16-weight MFMA GEMM: plain, row-list, residual, tied logits, router, "
+                                            "activation-gradient; gemm_p2 = its two-workgroups-per-CU form)",
                                   "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                   "frac": round(gbs / HBM_PEAK_GBS, 4),
-                                  **pmc_traffic("gemm_wr_kernel", args.config, args.batch, args.pitch_frames),
+                                  **pmc_traffic(("gemm_wr_kernel", "gemm_p2_kernel"), args.config, args.batch,
+                                                args.pitch_frames),
                                   "algorithmic_bytes_per_launch": round(wn_bytes / wn_n),
                                   "algorithmic_bytes_per_step": round(wn_bytes / probe_steps),
                                   "launches_per_step": wn_n // probe_steps,
@@ -379,8 +386,8 @@ def main():
                                   "share_of_step": round(wn_sec / probe_steps / step_s, 3),
                                   "mfma_achieved_tflops": round(wn_flops / wn_sec / 1e12, 2),
                                   "mfma_frac": round(wn_flops / wn_sec / 1e12 / peak, 4),
-                                  "recompute": "frac = algorithmic_bytes_per_step / (gemm_wr_kernel time per step in "
-                                               "the rocprof summary) / peak"}
+                                  "recompute": "frac = algorithmic_bytes_per_step / (gemm_wr_kernel + gemm_p2_kernel "
+                                               "time per step in the rocprof summary) / peak"}
         result["gemm_all"] = {"kernel": "every asrx GEMM launch (wide, generic fp32/bf16 incl. wgrad, router)",
                               "bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                               "frac": round(achieved / peak, 4),
@@ -397,8 +404,8 @@ def main():
                                       "avg_us": round(sec2 / n2 * 1e6, 1)}
         n3, af, sec3 = probe.summarize(recs["attn"])
         if sec3 > 0:
-            result["attn_fwd"] = {"achieved": round(af / sec3 / 1e12, 2), "unit": "TFLOP/s",
-                                  "frac": round(af / sec3 / 1e12 / peak, 4),
+            result["attn_fwd"] = {"achieved": round(af / sec3 / 1e12, 2), "unit": "TFLOP/s", "peak": apeak,
+                                  "frac": round(af / sec3 / 1e12 / apeak, 4),
                                   "share_of_step": round(sec3 / probe_steps / step_s, 3)}
     if opt_ms is not None:
         result["maxfactor_step_ms"] = round(opt_ms, 3)
@@ -483,12 +490,12 @@ def main():
         print(json.dumps(result), flush=True)
 
 
-def pmc_traffic(kernel_substr, config, batch, pitch_frames):
+def pmc_traffic(kernel_substrs, config, batch, pitch_frames):
     """HBM bytes per launch of a kernel from the newest committed PMC table OF THIS WORKLOAD (profiles/
     rNN_pmc_traffic_<config>_b<batch>_p<pitch frames>_vM.csv: separate rocprofv3 FETCH_SIZE and WRITE_SIZE
     passes over one eager step of `bench.py --config C --batch B --no-refpitch-line --no-dead-block-line`,
     FETCH doubled per the gfx950 note, see tools/pmc_traffic.py), launch-weighted over every template
-    instance whose name contains kernel_substr.  PMC counters cannot be read inside the timed run, so the
+    instance whose name contains one of kernel_substrs.  PMC counters cannot be read inside the timed run, so the
     figure comes from the profiling pass of the same step; null when no table of this workload exists."""
     import csv
     import glob
@@ -500,7 +507,7 @@ def pmc_traffic(kernel_substr, config, batch, pitch_frames):
         return {"traffic": None, "traffic_note": f"no PMC table for {config} B={batch} pitch {pitch_frames}"}
     n, tot = 0, 0.0
     for r in csv.DictReader(open(tabs[-1])):
-        if kernel_substr in r["kernel"]:
+        if any(k in r["kernel"] for k in kernel_substrs):
             n += int(r["launches"])
             tot += int(r["launches"]) * float(r["avg_hbm_bytes"])
     if n == 0:

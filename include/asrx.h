@@ -32,9 +32,6 @@ int asrx_set_noise_epoch(uint32_t epoch, asrx_stream_t stream);
  * stream-ordered): 1 (default) the two-workgroups-per-CU kernel, 0 the one-workgroup-per-CU kernel.
  * Same results bit for bit; an A/B switch for measurements and tests.  Returns the previous value. */
 int asrx_set_gemm_variant(int variant);
-/* Flash-attention forward kernel selection (host state): 1 the software-pipelined kernel (the next key tile's
- * QK^T issued before this tile's softmax), 0 (default) the unpipelined one.  Bit-identical; A/B switch. */
-int asrx_set_attn_variant(int variant);
 
 /* ---- log-mel front end: replaces torchaudio MelSpectrogram + log10 + clip-max floor,
  *      essentials.py:469-491, and the waveform adaptive_avg_pool1d, essentials.py:493-510 -------- */
