@@ -494,6 +494,10 @@ class processor(nn.Module):  # noqa: N801  (model.py:585-629)
         # block's forward AND backward, joined at the end of the backward (round 4); False: the round-3
         # schedule above (dead audio on the current stream, dead text beside it, joined per forward)
         self.concurrent_dead_blocks = True
+        # where the concurrent dead blocks are enqueued: "start" (before the live block: they share the GPU with
+        # the live forward), "mid" (after the live audio side: beside the live text side, the cross entropy and
+        # the backward) or "end" (after the live forward: beside the cross entropy and the backward)
+        self.dead_blocks_at = "end"  # measured: end 5108-5111, mid 5097-5114, start 5061-5072 audio-s/s (profiles/r05_dead_at_ab.txt)
         self._side = None
         self._pending = None
         self._hold = []
@@ -509,21 +513,10 @@ class processor(nn.Module):  # noqa: N801  (model.py:585-629)
         nblk = len(self.block)
         live = nblk - 1
         cuda = x.is_cuda
-        if not self.skip_dead_blocks and live > 0 and cuda and self.concurrent_dead_blocks:
-            # Blocks 0..L-2 depend on nothing but the embeddings and the encoder outputs (every block
-            # restarts from them) and nothing depends on them: they run on side streams, concurrently with
-            # the live block's forward and backward, and are joined at the end of the backward
-            # (Model.forward's hook) -- or right away without one.  Scheduling only: keyed noise, same
-            # kernels, same results.
-            main = torch.cuda.current_stream()
-            s_audio, s_text = self._side_streams(x.device)
-            s_audio.wait_stream(main)
-            s_text.wait_stream(main)
-            with torch.no_grad():
-                for i in range(live):
-                    self._dead_block(i, x, A_in, noise, B, s_audio, s_text)
-            self._pending = (s_audio, s_text, [x, xe] + A_in, main)
-        else:
+        conc_dead = not self.skip_dead_blocks and live > 0 and cuda and self.concurrent_dead_blocks
+        if conc_dead and self.dead_blocks_at == "start":
+            self._enqueue_dead(live, x, xe, A_in, noise, B)
+        elif not conc_dead:
             side = None
             keep = []  # cross-stream inputs stay referenced until the side stream is joined
             for i in range(live):
@@ -542,12 +535,16 @@ class processor(nn.Module):  # noqa: N801  (model.py:585-629)
         a = ops.fork(blk.call(x, noise, f"b{live}.ta", 0, masked=True))
         A = self._audio(blk, A_in, noise, f"b{live}.audio", B, "call")
         KV = self._audio(blk, A, noise, f"b{live}.xa", B, "xa")
+        if conc_dead and self.dead_blocks_at == "mid":  # after the live audio side, beside its text side
+            self._enqueue_dead(live, x, xe, A_in, noise, B)
         b_ = ops.fork(blk.call(a, noise, f"b{live}.tb", 0, kv=KV[0]))
         c_ = ops.fork(blk.call(b_, noise, f"b{live}.tc", 0, kv=KV[1]))
         d = ops.fork(blk.call(c_, noise, f"b{live}.td", 0, kv=KV[2]))
         e = ops.add(a, b_, c_)
         kve = blk.xa_side(e, noise, f"b{live}.tg.xa", 0)
         g = blk.call(d, noise, f"b{live}.tg", 0, kv=kve)
+        if conc_dead and self.dead_blocks_at == "end":
+            self._enqueue_dead(live, x, xe, A_in, noise, B)
         if seq:
             out = g
         else:
@@ -556,6 +553,20 @@ class processor(nn.Module):  # noqa: N801  (model.py:585-629)
         if features:
             return out
         return ops.linear(out, self.token.weight)
+
+    def _enqueue_dead(self, live, x, xe, A_in, noise, B):
+        """Blocks 0..L-2 depend on nothing but the embeddings and the encoder outputs (every block restarts
+        from them) and nothing depends on them: they run on side streams, concurrently with the rest of the
+        step, and are joined at the end of the backward (Model.forward's hook) -- or right away without one.
+        Scheduling only: keyed noise, same kernels, same results."""
+        main = torch.cuda.current_stream()
+        s_audio, s_text = self._side_streams(x.device)
+        s_audio.wait_stream(main)
+        s_text.wait_stream(main)
+        with torch.no_grad():
+            for i in range(live):
+                self._dead_block(i, x, A_in, noise, B, s_audio, s_text)
+        self._pending = (s_audio, s_text, [x, xe] + A_in, main)
 
     def _side_streams(self, device):
         if self._side is None or self._side[0].device != device:

@@ -47,8 +47,10 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", help="process-group backend for N > 1 (nccl = RCCL); "
                     "gloo + --same-device is a one-GPU rehearsal of the multi-rank path")
     ap.add_argument("--same-device", action="store_true", help="every rank on cuda:0 (rehearsal only)")
-    ap.add_argument("--eager", action="store_true", help="launch every kernel from Python instead of replaying "
-                    "the captured HIP graph of the step")
+    ap.add_argument("--graph", action="store_true", help="N=1 only: capture the step in one HIP graph and replay it "
+                    "(measured 5 %% SLOWER than eager launches: the replay runs the side streams' kernels mostly one "
+                    "at a time, profiles/r05_eager_vs_graph.txt)")
+    ap.add_argument("--eager", action="store_true", help="eager launches (the default; kept for old scripts)")
     ap.add_argument("--dist-single", action="store_true", help="N=1 through the N>1 code path: a 1-rank "
                     "process group (RCCL) and GradSync's bucket all-reduces on the comm stream (a rehearsal of "
                     "the multi-GPU step on a one-GPU box; never the headline)")
@@ -56,6 +58,8 @@ def parse():
                     "(3001: SURVEY.md §8(d)'s synthetic spec, = the spectrogram's frames)")
     ap.add_argument("--no-refpitch-line", action="store_true", help="skip the side line at the reference's own "
                     "pitch shape (6001 frames: pw.dio's 5 ms frames, essentials.py:451-455)")
+    ap.add_argument("--dead-at", default=None, choices=["start", "mid", "end"], help="where the dead blocks' side-stream "
+                    "work is enqueued (asrx.model.processor.dead_blocks_at; default: the model's)")
     ap.add_argument("--no-dead-block-line", action="store_true", help="skip the extra measurement with the "
                     "reference's dead decoder blocks eliminated (reported beside, never as, the headline)")
     return ap.parse_args()
@@ -214,6 +218,8 @@ def main():
     cfg = CONFIGS[args.config]
     torch.manual_seed(0)
     model = Model(cfg).to(dev).train()
+    if args.dead_at:
+        model.processor.dead_blocks_at = args.dead_at
     if distributed:
         broadcast_parameters(model)
     gsync = GradSync(model, reduce_single=args.dist_single)
@@ -236,7 +242,9 @@ def main():
         gsync.finish()
         return out["loss"]
 
-    use_graph = not args.eager and not distributed
+    # eager launches at every N: the N = 1 point of a 1 -> 8 curve runs the same code path as N > 1, and
+    # eager is the faster one (profiles/r05_eager_vs_graph.txt)
+    use_graph = args.graph and not args.eager and not distributed
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):  # warmup off the default stream (graph-capture requirement)

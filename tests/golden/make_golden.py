@@ -18,6 +18,28 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "asr-model_amd")]
 
+def pinned_threads():
+    """One BLAS / torch intra-op thread while making or checking a fixture: the float64 oracle's reductions
+    (matmul, FFT filterbank) are then summed in one order on every host -- with the host's default thread
+    count the toy model's logits moved by ~1e-6 relative between an 8- and a 16-CPU container (its hard
+    decisions amplify reduction-order ulps), which no rtol-1e-9 pin can absorb."""
+    import contextlib
+
+    from threadpoolctl import threadpool_limits
+
+    @contextlib.contextmanager
+    def ctx():
+        n = torch.get_num_threads()
+        torch.set_num_threads(1)
+        try:
+            with threadpool_limits(1):
+                yield
+        finally:
+            torch.set_num_threads(n)
+
+    return ctx()
+
+
 TOY = dict(tokens=1000, mels=128, dims=128, head=2, layer=4, act="gelu", n_type="AbbyNormal")
 
 
@@ -106,7 +128,8 @@ def main():
 
 
 if __name__ == "__main__":
-    if sys.argv[1:] == ["plumbing"]:
-        write_plumbing()
-    else:
-        main()
+    with pinned_threads():
+        if sys.argv[1:] == ["plumbing"]:
+            write_plumbing()
+        else:
+            main()

@@ -12,7 +12,7 @@ def _err(c, ref):
     return float((c.double() - ref).abs().max() / ref.abs().max())
 
 
-@pytest.mark.parametrize("M,N,K", [(1000, 384, 384), (257, 200, 96), (4096, 1536, 1152)])
+@pytest.mark.parametrize("M,N,K", [(1000, 384, 384), (260, 200, 96), (4096, 1536, 1152)])
 @pytest.mark.parametrize("a_kc,b_kc", [(True, True), (False, True), (True, False), (False, False)])
 def test_x3_gemm_precision(cuda, M, N, K, a_kc, b_kc):
     from asrx import gemm as G
@@ -22,7 +22,7 @@ def test_x3_gemm_precision(cuda, M, N, K, a_kc, b_kc):
     A = torch.randn(M, K, generator=g, dtype=torch.float64)
     Bm = torch.randn(K, N, generator=g, dtype=torch.float64) / K ** 0.5
     ref = A @ Bm
-    Ad = (A if a_kc else A.t()).contiguous().float().to(cuda)  # K-contiguous: (M, K); else stored (K, M)
+    Ad = (A if a_kc else A.t()).contiguous().float().to(cuda)  # K-contiguous: (M, K); else stored (K, M) (leading dims: multiples of 4)
     Bd = (Bm.t() if b_kc else Bm).contiguous().float().to(cuda)  # K-contiguous: stored (N, K); else (K, N)
     out = {}
     for p in (prec.PREC_X3, prec.PREC_BF16, prec.PREC_F32):
