@@ -306,6 +306,27 @@ def linear_fwd(x, W, b=None, act="none", out=None, preact=None, wbf=None, mtiles
     return y
 
 
+def linear_rot_fwd(x, W, b, m, tab, L, hd, scale, preact=None):
+    """rotary(x @ W^T + b) in one wide GEMM (perf mode, asrx_gemm_wn_rot): x (B, L, K) fp32 or bf16-stored, W
+    (N, K), m (B L,) the rotary magnitudes (||src|| per row), tab the (cos, sin) table of rotary_table;
+    preact (B, L, N) fp32 receives the unrotated product when given.  -> (B, L, N) fp32."""
+    x2 = _rows(x)
+    if not x2.is_contiguous():
+        x2 = x2.contiguous()
+    M, K = x2.shape
+    N = W.shape[0]
+    Wb = weight_bf16(W)
+    y = torch.empty(*x.shape[:-1], N, device=x.device)
+    nj = _nj(M, N)
+    ab = int(is_bf16(x2))
+    lib.require_gpu(x2, Wb, y, m, tab)
+    e0 = probe.begin("gemm")
+    lib.call("asrx_gemm_wn_rot", lib.ptr(x2), ab, K, lib.ptr(Wb), Wb.stride(0), lib.ptr(y), lib.ptr(preact), N,
+             lib.ptr(b), lib.ptr(m), lib.ptr(tab), L, hd, float(scale), M, N, K, nj, lib.stream())
+    probe.end("gemm", e0, 2.0 * M * N * K, ("wn", M, N, K, nj, 0, "rot", preact is not None, False, ab, 0, -1))
+    return y
+
+
 def linear_dgrad(dy, W, out=None, beta=0.0, mtiles=None):
     """dx = dy @ W (fp32 dx)."""
     """dx = dy @ W for dy (..., N), W (N, K); mtiles as in linear_fwd."""

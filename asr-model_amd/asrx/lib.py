@@ -189,6 +189,8 @@ SIGNATURES = {
     "asrx_act_bwd_bias": (_i32, [_p, _p, _p, _p, _i64, _i64, _i32, _p]),
     "asrx_abby_fwd_res": (_i32, [_p] * 9 + [_i64] * 5 + [_u32, _i32, _p]),
     "asrx_gemm_wn_res": (_i32, [_p, _i64, _p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _i64, _i32, _p]),
+    "asrx_gemm_wn_rot": (_i32, [_p, _i32, _i64, _p, _i64, _p, _p, _i64, _p, _p, _p, _i64, _i64, _f32, _i64, _i64,
+                                _i64, _i32, _p]),
 }
 
 _lib = None

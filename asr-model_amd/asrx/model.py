@@ -271,8 +271,8 @@ class attention(nn.Module):  # noqa: N801
         H, hd = self.head, D // self.head
         src = ops.want_rownorm(ops.fork(src))  # read by the kv AbbyNormal and rotary's |src|
         kvn = self.kv[0].run(src, noise, site + ".kv", sid_base, L, out_bf16=True)
-        k, v = ops.kv_proj(kvn, self.kv[1].weight, self.kv[1].bias)
-        k = ops.rotary(k, src, rotary_freqs(D, H, masked, src.device), hd, self.scale)
+        k, v = ops.kv_proj_rotary(kvn, self.kv[1].weight, self.kv[1].bias, src,
+                                  rotary_freqs(D, H, masked, src.device), hd, self.scale)
         k = self.ln.run(k.view(B, L, H, hd), noise, site + ".kh", sid_base, L, H, out_bf16=prec.attn_bf16_io())
         vh = v.view(B, L, H, hd)
         if ops.sink_of(v) is not None:  # v is bf16-stored: attention adds its gradient into v's sink
@@ -283,8 +283,8 @@ class attention(nn.Module):  # noqa: N801
         B, L, D = x.shape
         H, hd = self.head, D // self.head
         qn = self.q[0].run(ops.want_rownorm(x), noise, site + ".q", sid_base, L, out_bf16=True)
-        q = ops.linear(qn, self.q[1].weight, self.q[1].bias)
-        q = ops.rotary(q, x, rotary_freqs(D, H, masked, x.device), hd, self.scale)
+        q = ops.linear_rotary(qn, self.q[1].weight, self.q[1].bias, x, rotary_freqs(D, H, masked, x.device), hd,
+                              self.scale)
         return self.ln.run(q.view(B, L, H, hd), noise, site + ".qh", sid_base, L, H, out_bf16=prec.attn_bf16_io())
 
     def run(self, x, kv, noise, site, sid_base, masked, residual=None):

@@ -407,10 +407,26 @@ class KVProjFn(torch.autograd.Function):
     (beta = 1) and the weight / bias gradients written into the blocks of p.grad."""
 
     @staticmethod
-    def forward(ctx, x, W, b, sink, v_bf16=False, vsink=None):
+    def forward(ctx, x, W, b, sink, v_bf16=False, vsink=None, src=None, rot=None, grad=False):
+        """rot: (freqs, hd, scale, src sink, ||src|| or None) -- k leaves the GEMM rotated (asrx_gemm_wn_rot,
+        model.py:304's rotary of k on the kv source src), its unrotated product kept for the backward."""
         x = _c(x)
         D = W.shape[0] // 2
-        k = G.linear_fwd(x, W[:D], b[:D])
+        ctx.rot = rot is not None
+        if rot is not None:
+            freqs, hd, scale, ctx.src_sink, m = rot
+            src = _c(src)
+            L = x.shape[1]
+            if m is None:
+                m = _E(_rows(src), device=x.device)
+                lib.call("asrx_rownorm", _P(src), _P(m), _rows(src), src.shape[-1], _S())
+            tab = rotary_table(freqs, L, hd)
+            kz = _E(*x.shape[:-1], D, device=x.device) if grad else None
+            k = G.linear_rot_fwd(x, W[:D], b[:D], m, tab, L, hd, scale, preact=kz)
+            ctx.hd, ctx.scale = hd, scale
+            ctx.rot_saved = (kz, src, m, freqs, tab) if grad else None
+        else:
+            k = G.linear_fwd(x, W[:D], b[:D])
         v = G.linear_fwd(x, W[D:], b[D:], out_bf16=v_bf16)  # v only feeds attention
         ctx.vsink = vsink
         ctx.set_materialize_grads(False)
@@ -425,6 +441,9 @@ class KVProjFn(torch.autograd.Function):
         D = W.shape[0] // 2
         dk = _f32(dk)
         dv = grad_in(dv, ctx.vsink)
+        dsrc = None
+        if ctx.rot and dk is not None:
+            dk, dsrc = _rotary_bwd(ctx, dk, *ctx.rot_saved, ctx.needs_input_grad[6], ctx.src_sink)
         if dk is not None:
             dk = dk.reshape(*x.shape[:-1], D)
         if dv is not None:
@@ -459,13 +478,35 @@ class KVProjFn(torch.autograd.Function):
                 if gpart is not None:
                     colsum(gpart.view(-1, D), out=gb[i * D:(i + 1) * D])
             dbf = _gret(b, gb, ctx.db)
-        return dx, dWf, dbf, None, None, None
+        return dx, dWf, dbf, None, None, None, dsrc, None, None
 
 
 def kv_proj(x, W, b):
     vb = prec.attn_bf16_io()
     vsink = new_sink(vb) if _grad_needed(x, W, b) else None
     k, v = KVProjFn.apply(x, W, b, sink_of(x), vb, vsink)
+    return k, out_sink(v, vsink)
+
+
+def _rot_fusable(x, N, hd):
+    """The rotary can ride in the projection GEMM's epilogue (asrx_gemm_wn_rot): perf mode, a (B, L, K) CUDA
+    input, and a tile width the rotary instantiations cover (nj 1 or 3)."""
+    K = x.shape[-1]
+    return (ROT_FUSED and prec.get() == prec.PREC_BF16 and G.use_wide(K) and x.is_cuda and x.dim() == 3
+            and N % 4 == 0 and hd % 4 == 0 and N % hd == 0 and G._nj(_rows(x), N) in (1, 3))
+
+
+def kv_proj_rotary(x, W, b, src, freqs, hd, scale):
+    """(rotary(k, src), v) of kv_proj(x, W, b): the rotary of k fused into its GEMM in perf mode."""
+    D = W.shape[0] // 2
+    if not _rot_fusable(x, D, hd):
+        k, v = kv_proj(x, W, b)
+        return rotary(k, src, freqs, hd, scale), v
+    vb = prec.attn_bf16_io()
+    grad = _grad_needed(x, W, b, src)
+    vsink = new_sink(vb) if grad else None
+    k, v = KVProjFn.apply(x, W, b, sink_of(x), vb, vsink, src, (freqs, hd, scale, sink_of(src), rownorm_of(src)),
+                          grad)
     return k, out_sink(v, vsink)
 
 
@@ -817,6 +858,92 @@ class RotaryFn(torch.autograd.Function):
             lib.call("asrx_rownorm_bwd2", _P(dm), _P(src), _P(m), _P(buf), B * L, D, acc, _S())
             dsrc = None if ctx.sink is not None else buf
         return dx, dsrc, None, None, None, None, None
+
+
+def _rotary_bwd(ctx, gy, x, src, m, freqs, tab, want_src, src_sink):
+    """RotaryFn.backward's arithmetic: -> (dx, dsrc or None); dsrc lands in src_sink when there is one."""
+    gy = _c(gy)
+    B, L, D = x.shape
+    dx = _E(x.shape, device=x.device)
+    dm = _E(B * L, device=x.device)  # written by the kernel
+    lib.call("asrx_rotary_bwd2", _P(gy), _P(x), _P(m), _P(freqs), _P(tab), _P(dx), _P(dm), B * L, L, D, ctx.hd,
+             float(ctx.scale), _S())
+    dsrc = None
+    if want_src:
+        if src_sink is not None:
+            buf, acc = src_sink.target(src)
+        else:
+            buf, acc = _E(src.shape, device=src.device), 0
+        lib.call("asrx_rownorm_bwd2", _P(dm), _P(src), _P(m), _P(buf), B * L, src.shape[-1], acc, _S())
+        dsrc = None if src_sink is not None else buf
+    return dx, dsrc
+
+
+# perf mode: the q / k projections apply the rotary in their GEMM's epilogue (LinearRotFn, KVProjFn rot);
+# False: the projection GEMM then RotaryFn's separate pass (same results, bit for bit)
+ROT_FUSED = True
+
+
+class LinearRotFn(torch.autograd.Function):
+    """rotary(Linear(x), src) -- the q projection (model.py:242-245) and its rotary (model.py:198-214, with the
+    hd^-0.25 scale of model.py:303) in one GEMM whose epilogue rotates the product before storing it
+    (asrx_gemm_wn_rot): the unrotated projection reaches HBM only as the backward's saved input.  Backward:
+    RotaryFn's, then Linear's (act none), with the same sinks."""
+
+    @staticmethod
+    def forward(ctx, x, W, b, src, freqs, hd, scale, grad=False, sink=None, src_sink=None, m=None):
+        x = _c(x)
+        src = _c(src)
+        ctx.sink, ctx.src_sink = sink, src_sink
+        ctx.set_materialize_grads(False)
+        L = x.shape[1]
+        if m is None:
+            m = _E(_rows(src), device=x.device)
+            lib.call("asrx_rownorm", _P(src), _P(m), _rows(src), src.shape[-1], _S())
+        tab = rotary_table(freqs, L, hd)
+        z = _E(*x.shape[:-1], W.shape[0], device=x.device) if grad else None
+        y = G.linear_rot_fwd(x, W, b, m, tab, L, hd, scale, preact=z)
+        ctx.hd, ctx.scale = hd, scale
+        ctx.has_b = b is not None
+        if grad:
+            ctx.dW, ctx.db = _direct(ctx, 1, W), _direct(ctx, 2, b)
+            ctx.save_for_backward(x, W, b, z, src, m, freqs, tab)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, W, b, z, src, m, freqs, tab = ctx.saved_tensors
+        if gy is None:
+            return (None,) * 11
+        dq, dsrc = _rotary_bwd(ctx, _f32(gy), z, src, m, freqs, tab, ctx.needs_input_grad[3], ctx.src_sink)
+        N = W.shape[0]
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if ctx.sink is not None:
+                buf, acc = ctx.sink.target(x)
+                G.linear_dgrad(dq, W, out=buf, beta=float(acc))
+            else:
+                dx = G.linear_dgrad(dq, W)
+        dW = db = gb = None
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            gb = _gbuf(b, True) if ctx.db else torch.zeros(N, device=dq.device)
+        if ctx.needs_input_grad[1]:
+            gW = _gbuf(W, ctx.dW)
+            G.linear_wgrad(dq, x, out=gW, accumulate=True, db=gb)  # bias gradient in the same pass
+            dW = _gret(W, gW, ctx.dW)
+        elif gb is not None:
+            colsum(dq.view(-1, N), out=gb)
+        if gb is not None:
+            db = _gret(b, gb, ctx.db)
+        return dx, dW, db, dsrc, None, None, None, None, None, None, None
+
+
+def linear_rotary(x, W, b, src, freqs, hd, scale):
+    """rotary(linear(x, W, b), src, freqs, hd, scale) -- one fused GEMM in perf mode (LinearRotFn)."""
+    if not _rot_fusable(x, W.shape[0], hd):
+        return rotary(linear(x, W, b), src, freqs, hd, scale)
+    grad = _grad_needed(x, W, b, src)
+    return LinearRotFn.apply(x, W, b, src, freqs, hd, scale, grad, sink_of(x), sink_of(src), rownorm_of(src))
 
 
 _ROT_TABLES = {}  # (freqs ptr, hd, device) -> (cap, hd/2, 2) table of positions [0, cap)

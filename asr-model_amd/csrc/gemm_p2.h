@@ -137,7 +137,7 @@ __device__ __forceinline__ void store(const Stage<NJ, ABF>& st, char* At, char* 
 #define P2_DEPTH 3  // register stages in flight (k-steps of prefetch)
 #endif
 
-template <int NJ, bool ABF, int ACT, bool RES>
+template <int NJ, bool ABF, int ACT, bool RES, bool ROT = false>
 __global__ __launch_bounds__(p2::NT2, 2) void gemm_p2_kernel(Params p, int ntiles) {
   using namespace p2;
   typedef Geo<NJ, ABF> GE;
@@ -257,7 +257,7 @@ __global__ __launch_bounds__(p2::NT2, 2) void gemm_p2_kernel(Params p, int ntile
 #endif
     if (ce.kk == nk - 1) {
 #if !(P2_ABL & 8)
-      epilogue_lds<NJ, ACT, RES>(p, acc, bias_s[ce.j & 1], ce.m0, ce.n0, wm, wn, lr, lk, ep);
+      epilogue_lds<NJ, ACT, RES, ROT>(p, acc, bias_s[ce.j & 1], ce.m0, ce.n0, wm, wn, lr, lk, ep);
 #else
       {  // the accumulators feed a never-taken store
         float t = 0.f;
@@ -285,10 +285,10 @@ __global__ __launch_bounds__(p2::NT2, 2) void gemm_p2_kernel(Params p, int ntile
 }
 
 // launch: resident workgroups (2 per CU) walk the tiles persistently
-template <int NJ, bool ABF, int ACT, bool RES>
+template <int NJ, bool ABF, int ACT, bool RES, bool ROT = false>
 void launch_p2(const Params& p, hipStream_t s) {
   static int resident = 0;
-  const void* fn = (const void*)gemm_p2_kernel<NJ, ABF, ACT, RES>;
+  const void* fn = (const void*)gemm_p2_kernel<NJ, ABF, ACT, RES, ROT>;
   if (!resident) {
     int per_cu = 0, dev = 0, cus = 0;
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, p2::NT2, 0);
@@ -298,7 +298,7 @@ void launch_p2(const Params& p, hipStream_t s) {
   }
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + p2::Geo<NJ, ABF>::BN - 1) / p2::Geo<NJ, ABF>::BN);
   const int grid = std::min(tiles, resident);
-  gemm_p2_kernel<NJ, ABF, ACT, RES><<<grid, p2::NT2, 0, s>>>(p, tiles);
+  gemm_p2_kernel<NJ, ABF, ACT, RES, ROT><<<grid, p2::NT2, 0, s>>>(p, tiles);
 }
 
 // dispatch over the activation (runtime act -> template)
@@ -326,6 +326,13 @@ void launch_p2_act(const Params& p, hipStream_t s) {
 #define ASRX_P2_DECL(NJ, ABF, RES) template void asrx::wn::launch_p2_act<NJ, ABF, RES>(const asrx::wn::Params&, hipStream_t);
 #endif
 #ifndef ASRX_P2_INSTANTIATE
+#define ASRX_P2_DECL_ROT(NJ, ABF) extern template void asrx::wn::launch_p2<NJ, ABF, asrx::ACT_NONE, false, true>(const asrx::wn::Params&, hipStream_t);
+#else
+#define ASRX_P2_DECL_ROT(NJ, ABF) template void asrx::wn::launch_p2<NJ, ABF, asrx::ACT_NONE, false, true>(const asrx::wn::Params&, hipStream_t);
+#endif
+#ifndef ASRX_P2_INSTANTIATE
+ASRX_P2_DECL_ROT(3, true)
+ASRX_P2_DECL_ROT(3, false)
 ASRX_P2_DECL(3, false, false)
 ASRX_P2_DECL(3, true, false)
 ASRX_P2_DECL(2, false, false)

@@ -226,6 +226,40 @@ extern "C" int asrx_gemm_wn_res(const float* A, int64_t lda, const unsigned shor
   ASRX_LAUNCHED("asrx_gemm_wn_res");
 }
 
+// q / k projection with rotary fused (model.py:242-245 then 198-214, with the hd^-0.25 scale of model.py:303-304):
+// C = rot(A W^T + bias), i.e. each head's pairs (2j, 2j+1) of the product times polar(scale * m[row], angle(row %
+// L, j)) from the (cos, sin) table tab (positions >= L, hd / 2) float2 -- asrx_rotary_fwd2's arithmetic, so C is
+// bit-identical to the GEMM followed by that pass; Z (nullable) receives the unrotated product (what the rotary
+// backward reads).  A fp32 (a_bf16 = 0) or bf16 (1); C, Z fp32, 16-byte aligned rows; nj 1 or 3.
+extern "C" int asrx_gemm_wn_rot(const void* A, int a_bf16, int64_t lda, const unsigned short* W, int64_t ldw,
+                                float* C, float* Z, int64_t ldc, const float* bias, const float* m, const float* tab,
+                                int64_t L, int64_t hd, float scale, int64_t M, int64_t N, int64_t K, int nj,
+                                hipStream_t stream) {
+  ASRX_REQUIRE(M > 0 && N > 0 && K > 0 && L > 0, "asrx_gemm_wn_rot: empty problem");
+  ASRX_REQUIRE(((uintptr_t)A & 15) == 0 && ((uintptr_t)W & 15) == 0 && ((uintptr_t)C & 15) == 0 &&
+                   ((uintptr_t)Z & 15) == 0 && ((uintptr_t)tab & 15) == 0,
+               "asrx_gemm_wn_rot: A/W/C/Z/tab must be 16-byte aligned");
+  ASRX_REQUIRE(K % 8 == 0 && lda % (a_bf16 ? 8 : 4) == 0 && ldw % 8 == 0 && N % 4 == 0 && ldc % 4 == 0,
+               "asrx_gemm_wn_rot: K, ldw %% 8; lda %% 4 (8 bf16); N, ldc %% 4");
+  ASRX_REQUIRE(hd >= 4 && hd % 4 == 0 && N % hd == 0, "asrx_gemm_wn_rot: head dim %% 4, N %% hd");
+  ASRX_REQUIRE(M * lda < (1LL << 31) && N * ldw < (1LL << 31), "asrx_gemm_wn_rot: operand spans >= 2^31 elements");
+  ASRX_REQUIRE(m && tab, "asrx_gemm_wn_rot: row norms and angle table required");
+  ASRX_REQUIRE(nj == 1 || nj == 3, "asrx_gemm_wn_rot: nj 1 or 3");
+  wn::Params p{(const float*)A, (int)lda, W, (int)ldw, C, (int)ldc, bias, Z, (int)M, (int)N, (int)K, 1, 1, 1.f, 0.f,
+               ACT_NONE};
+  p.rot_m = m;
+  p.rot_tab = reinterpret_cast<const float2*>(tab);
+  p.rot_L = (int)L;
+  p.rot_half = (int)(hd / 2);
+  p.rot_scale = scale;
+  ASRX_REQUIRE(nj == 1 || g_wide_variant >= 1, "asrx_gemm_wn_rot: nj 3 runs on gemm_p2 only (variant >= 1)");
+  if (nj == 3) a_bf16 ? wn::launch_p2<3, true, ACT_NONE, false, true>(p, stream)
+                      : wn::launch_p2<3, false, ACT_NONE, false, true>(p, stream);
+  else a_bf16 ? wn::launch_wr<1, false, false, true, false, false, false, true>(p, stream)
+              : wn::launch_wr<1, false, false, false, false, false, false, true>(p, stream);
+  ASRX_LAUNCHED("asrx_gemm_wn_rot");
+}
+
 // Backward of y = act(A W^T + bias) (act gelu / silu / sigmoid) without a stored pre-activation: the GEMM
 // recomputes z = A W^T + bias with the forward's tile width (nj 3 only: the instantiation the forward's
 // shapes use) and writes gz = bf16(G * act'(z)) (M x N, ldc) from the output gradient G (fp32, ldg), adding

@@ -73,6 +73,15 @@ struct Params {
   const float* G;
   int ldg;
   float* dB;
+  // rotary epilogue (ROT instantiations, act none, fp32 C): the q / k projection's rotary (model.py:198-214)
+  // applied to the product before it is stored -- C = rot(alpha A W^T + bias), the pairs (2j, 2j+1) of each
+  // head times polar(rot_scale * rot_m[row], angle(row % rot_L, j)) from the (cos, sin) table rot_tab
+  // ((positions, rot_half) float2, asrx_rotary_table); Z, when non-null, receives the unrotated product
+  // (the rotary backward's input)
+  const float* rot_m;
+  const float2* rot_tab;
+  int rot_L, rot_half;
+  float rot_scale;
 };
 
 __device__ __forceinline__ void st_bf16x4(unsigned short* dst, float a, float b, float c, float d) {
@@ -180,7 +189,19 @@ struct EpLds {
   static constexpr int LD = W + EP_PAD;       // slab row stride (floats)
   static constexpr int FLOATS = 16 * LD;      // one 16-row slice
 };
-template <int NJ, int ACT, bool RES = false>
+// rot_apply: rotary's complex product on one float4 of columns (col % 4 == 0, so two whole pairs), with the
+// arithmetic of rowops.hip rotary_fwd_kernel (no contractions: bit-identical to the separate pass)
+__device__ __forceinline__ float4 rot_apply(const Params& p, float4 x, int row, int col) {
+#pragma clang fp contract(off)
+  const int hd = 2 * p.rot_half;
+  const int j = (col % hd) >> 1;
+  const float4 t = *reinterpret_cast<const float4*>(p.rot_tab + (int64_t)(row % p.rot_L) * p.rot_half + j);
+  const float mm = p.rot_m[row] * p.rot_scale;
+  return make_float4(mm * (x.x * t.x - x.y * t.y), mm * (x.x * t.y + x.y * t.x), mm * (x.z * t.z - x.w * t.w),
+                     mm * (x.z * t.w + x.w * t.z));
+}
+
+template <int NJ, int ACT, bool RES = false, bool ROT = false>
 __device__ __forceinline__ void epilogue_lds(const Params& p, f32x4 (&acc)[4][2 * NJ], const float* bsl, int m0,
                                              int n0, int wm, int wn, int lr, int lk, float* ep) {
   constexpr int NT = 2 * NJ, W = EpLds<NJ>::W, LD = EpLds<NJ>::LD, W4 = W / 4;
@@ -230,6 +251,7 @@ __device__ __forceinline__ void epilogue_lds(const Params& p, f32x4 (&acc)[4][2 
       if (p.Z)
         __builtin_nontemporal_store(f32x4{x.x, x.y, x.z, x.w},
                                     reinterpret_cast<f32x4*>(p.Z + (int64_t)row * p.ldc + col));
+      if constexpr (ROT) x = rot_apply(p, x, row, col);  // act none (ROT instantiations)
       __builtin_nontemporal_store(f32x4{act_t<ACT>(x.x), act_t<ACT>(x.y), act_t<ACT>(x.z), act_t<ACT>(x.w)},
                                   reinterpret_cast<f32x4*>(dst));
     }
@@ -734,7 +756,7 @@ __device__ __forceinline__ void wr_load64_fast(const Params& p, WrStage64<ABF>& 
 }
 
 template <int NJ, bool CONV, bool RT, int DEP = 0, bool ABF = false, bool CE = false, bool RES = false,
-          bool GA = false>
+          bool GA = false, bool ROT = false>
 __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) {  // ntiles: all tiles
   typedef Cfg<NJ> CF;
   constexpr int BN = CF::BN, NT = 2 * NJ, BNR = CF::BNR;
@@ -930,6 +952,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
         epilogue_ce<NJ>(p, acc, m0, n0, wm, wn, lr, lk, ep, reinterpret_cast<float2*>(red));
       } else if constexpr (RES) {  // act none, vec_ok (checked by the launcher)
         epilogue_lds<NJ, ACT_NONE, true>(p, acc, bsl, m0, n0, wm, wn, lr, lk, ep);
+      } else if constexpr (ROT) {  // act none, fp32 C, vec_ok (checked by the launcher)
+        epilogue_lds<NJ, ACT_NONE, false, true>(p, acc, bsl, m0, n0, wm, wn, lr, lk, ep);
       } else if constexpr (GA) {  // gelu / silu / sigmoid (checked by the launcher)
         switch (p.act) {
           case ACT_GELU: epilogue_gact<NJ, ACT_GELU>(p, acc, bsl, m0, n0, wm, wn, lr, lk, ep); break;
@@ -985,10 +1009,11 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_wr_kernel(Params p, int ntiles) 
 template <bool ABF>
 constexpr int wr_dep() { return 0; }
 
-template <int NJ, bool CONV, bool RT = false, bool ABF = false, bool CE = false, bool RES = false, bool GA = false>
+template <int NJ, bool CONV, bool RT = false, bool ABF = false, bool CE = false, bool RES = false, bool GA = false,
+          bool ROT = false>
 void launch_wr(const Params& p, hipStream_t s) {
   static int resident = 0;
-  const void* fn = (const void*)gemm_wr_kernel<NJ, CONV, RT, wr_dep<ABF>(), ABF, CE, RES, GA>;
+  const void* fn = (const void*)gemm_wr_kernel<NJ, CONV, RT, wr_dep<ABF>(), ABF, CE, RES, GA, ROT>;
   if (!resident) {
     int per_cu = 0, dev = 0, cus = 0;
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, NTHR, 0);
@@ -1000,7 +1025,7 @@ void launch_wr(const Params& p, hipStream_t s) {
   const int grid = std::min(tiles, resident);
   // a 5-deep pipeline (DEP = 5) for the one-wave 8192-row text-side launches measured 32.4 us vs
   // 30.1 us at depth 3 (profiles/r02_bench_v8_kernel_stats.csv): their time is not load latency
-  gemm_wr_kernel<NJ, CONV, RT, wr_dep<ABF>(), ABF, CE, RES, GA><<<grid, NTHR, 0, s>>>(p, tiles);
+  gemm_wr_kernel<NJ, CONV, RT, wr_dep<ABF>(), ABF, CE, RES, GA, ROT><<<grid, NTHR, 0, s>>>(p, tiles);
 }
 
 }  // namespace wn
@@ -1013,11 +1038,13 @@ void launch_wr(const Params& p, hipStream_t s) {
 #define ASRX_WR_DECL_CE(NJ) extern template void asrx::wn::launch_wr<NJ, false, false, true, true>(const asrx::wn::Params&, hipStream_t);
 #define ASRX_WR_DECL_RES(NJ) extern template void asrx::wn::launch_wr<NJ, false, false, false, false, true>(const asrx::wn::Params&, hipStream_t);
 #define ASRX_WR_DECL_GA(NJ, ABF) extern template void asrx::wn::launch_wr<NJ, false, false, ABF, false, false, true>(const asrx::wn::Params&, hipStream_t);
+#define ASRX_WR_DECL_ROT(NJ, ABF) extern template void asrx::wn::launch_wr<NJ, false, false, ABF, false, false, false, true>(const asrx::wn::Params&, hipStream_t);
 #else
 #define ASRX_WR_DECL(NJ, CONV, RT, ABF) template void asrx::wn::launch_wr<NJ, CONV, RT, ABF>(const asrx::wn::Params&, hipStream_t);
 #define ASRX_WR_DECL_CE(NJ) template void asrx::wn::launch_wr<NJ, false, false, true, true>(const asrx::wn::Params&, hipStream_t);
 #define ASRX_WR_DECL_RES(NJ) template void asrx::wn::launch_wr<NJ, false, false, false, false, true>(const asrx::wn::Params&, hipStream_t);
 #define ASRX_WR_DECL_GA(NJ, ABF) template void asrx::wn::launch_wr<NJ, false, false, ABF, false, false, true>(const asrx::wn::Params&, hipStream_t);
+#define ASRX_WR_DECL_ROT(NJ, ABF) template void asrx::wn::launch_wr<NJ, false, false, ABF, false, false, false, true>(const asrx::wn::Params&, hipStream_t);
 #endif
 #define ASRX_WR_SET(NJ) ASRX_WR_DECL(NJ, false, false, false) ASRX_WR_DECL(NJ, true, false, false) \
   ASRX_WR_DECL(NJ, false, false, true) ASRX_WR_DECL(NJ, true, false, true) ASRX_WR_DECL(NJ, false, true, false)
@@ -1032,4 +1059,6 @@ ASRX_WR_DECL_RES(1)
 ASRX_WR_DECL_RES(3)
 ASRX_WR_DECL_GA(3, false)
 ASRX_WR_DECL_GA(3, true)
+ASRX_WR_DECL_ROT(1, true)
+ASRX_WR_DECL_ROT(1, false)
 #endif

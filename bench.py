@@ -266,7 +266,9 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     from asrx import lib
+    host_s = 0.0  # host time spent issuing the steps (eager: Python + launches); ~ms_per_step means host-bound
     for i in range(args.steps):
+        h0 = time.perf_counter()
         if graph is not None:
             # the captured launches carry the capture step's noise keys: a new epoch per replay gives
             # every timed step its own dropout masks and gumbel draws (stream-ordered, outside the graph)
@@ -274,6 +276,7 @@ def main():
             graph.replay()
         else:
             loss = step()
+        host_s += time.perf_counter() - h0
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
@@ -345,6 +348,7 @@ def main():
                    "pitch_frames": args.pitch_frames,
                    "parallelism": f"dp{world}"},
         "per_gpu": round(value / world, 3),
+        "host_issue_ms_per_step": round(host_s / args.steps * 1e3, 3),
         **({"grad_sync_rel_spread": grad_spread} if distributed else {}),
         **({"dist_single": "1-rank RCCL group through the N>1 path (eager, bucket all-reduces on the comm "
                            "stream); a rehearsal, not the headline"} if args.dist_single else {}),

@@ -531,6 +531,15 @@ int asrx_ce_bwd_f32in(const float* zf, const int64_t* labels, const float* lse, 
 int asrx_gemm_wn_gact(const void* A, int a_bf16, int64_t lda, const unsigned short* W, int64_t ldw, const float* bias,
                       const float* G, int64_t ldg, unsigned short* gz, int64_t ldc, float* db, int64_t M, int64_t N,
                       int64_t K, int act, int nj, asrx_stream_t stream);
+/* q / k projection with its rotary fused (model.py:242-245 / 261, then model.py:198-214 with the hd^-0.25 scale of
+ * model.py:303-304): C = rot(A W^T + bias) -- each head's pairs (2j, 2j+1) times polar(scale * m[row],
+ * angle(row % L, j)) from tab ((positions >= L) x hd/2 float2 (cos, sin), asrx_rotary_table); bit-identical to
+ * asrx_gemm_wn_ex followed by asrx_rotary_fwd2.  Z (nullable) receives the unrotated product.  A fp32 (a_bf16 = 0)
+ * or bf16 (1); C, Z, tab 16-byte aligned; N % hd == 0, hd % 4 == 0; nj 1 or 3.  Replaces the rotary pass over
+ * the projection's output (its fp32 write and re-read). */
+int asrx_gemm_wn_rot(const void* A, int a_bf16, int64_t lda, const unsigned short* W, int64_t ldw, float* C, float* Z,
+                     int64_t ldc, const float* bias, const float* m, const float* tab, int64_t L, int64_t hd,
+                     float scale, int64_t M, int64_t N, int64_t K, int nj, asrx_stream_t stream);
 int asrx_gemm_wn_res(const float* A, int64_t lda, const unsigned short* W, int64_t ldw, float* C, int64_t ldc,
                      const float* bias, const float* R, int64_t ldr, int64_t M, int64_t N, int64_t K, int nj,
                      asrx_stream_t stream);
