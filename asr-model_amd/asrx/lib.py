@@ -211,7 +211,25 @@ def load() -> ctypes.CDLL:
             fn.restype = res
             fn.argtypes = args
         _lib = lib
+        _bind_fast(lib)
     return _lib
+
+
+def _bind_fast(lib) -> None:
+    """call() goes through asrx/_asrxcall.so (gen_fastcall.py: one METH_FASTCALL wrapper per entry point, bound
+    to the addresses of THIS ctypes handle's functions) when it was built; ctypes otherwise.  Same C-ABI, same
+    library instance -- only the Python-side argument conversion differs (~1 us instead of ~10 us per launch)."""
+    if os.environ.get("ASRX_CTYPES"):
+        return
+    try:
+        from . import _asrxcall
+    except ImportError:
+        return
+    for name in SIGNATURES:
+        if not hasattr(lib, name):
+            continue
+        if _asrxcall.bind(name, ctypes.cast(getattr(lib, name), ctypes.c_void_p).value):
+            _FN[name] = getattr(_asrxcall, name)
 
 
 def exported_symbols() -> list[str]:
@@ -241,11 +259,25 @@ def call(name: str, *args) -> None:
         key = (name, site)
         CENSUS[key + ("n",)] += 1
         CENSUS[key + ("size",)] += max((a for a in args if isinstance(a, int) and a < 1 << 40), default=0)
-    check(getattr(load(), name)(*args), name)
+    fn = _FN.get(name)
+    if fn is None:
+        lib = load()  # binds the FASTCALL wrappers into _FN on first use
+        fn = _FN.get(name) or _FN.setdefault(name, getattr(lib, name))
+    rc = fn(*args)
+    if rc:
+        check(rc, name)
+
+
+_FN: dict = {}  # entry point name -> callable (FASTCALL wrapper, or the bound ctypes function)
+_raw_stream = torch._C._cuda_getCurrentRawStream
+_get_device = torch._C._cuda_getDevice
 
 
 def stream() -> int:
-    return torch.cuda.current_stream().cuda_stream
+    """The current HIP stream of the current device as a raw pointer (what torch.cuda.current_stream().cuda_stream
+    returns, without building a Stream object per launch -- the step issues ~4000 launches, and the eager step is
+    close to host-bound)."""
+    return _raw_stream(_get_device())
 
 
 def ptr(t) -> int | None:

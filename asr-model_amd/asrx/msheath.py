@@ -338,7 +338,13 @@ class MSheathFn(torch.autograd.Function):
 def msheath(mod, x, gpol, tag=None):
     """Fused MSheath call.  Without autograd (the reference's dead blocks, eval, decoding) the forward
     runs without saving anything for a backward.  tag: (noise site key, sid_base) for asrx.decisions."""
-    params = _params(mod)
-    if not torch.is_grad_enabled() or not (x.requires_grad or any(p.requires_grad for p in params)):
+    if not torch.is_grad_enabled():
+        return forward(mod, x if x.is_contiguous() else x.contiguous(), gpol, save=False, tag=tag)[0]
+    # the parameter list (~60 nn.Module attribute walks) is made once per module: the module tree is fixed
+    params = mod.__dict__.get("_asrx_params")
+    if params is None or params[4] is not mod.mem_w or params[7] is not mod.jump_s:  # (replaced parameters)
+        params = _params(mod)
+        mod.__dict__["_asrx_params"] = params
+    if not (x.requires_grad or any(p.requires_grad for p in params)):
         return forward(mod, x if x.is_contiguous() else x.contiguous(), gpol, save=False, tag=tag)[0]
     return MSheathFn.apply(x, gpol, mod, tag, *params)

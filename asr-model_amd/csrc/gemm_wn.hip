@@ -2,12 +2,18 @@
 // bf16 and the MSheath row-tile lists.
 #include "gemm_wr.h"
 #include "gemm_p2.h"
+#include "gemm_ws.h"
 #include <string>
 
 // Which wide-GEMM kernel runs the plain / residual products that gemm_p2_kernel covers (asrx_set_gemm_variant):
-// 1 (default) gemm_p2_kernel (two workgroups per CU) for tile widths 3 and 2, 2 also for width 1 (the 128-column
-// tiles: gemm_p2's NJ = 2 tile is 128 x 128), 0 gemm_wr_kernel -- A/B measurements and the tests that compare them
-static int g_wide_variant = 1;
+// 1 gemm_p2_kernel (two workgroups per CU) for tile widths 3 and 2, 2 also for width 1 (the 128-column
+// tiles: gemm_p2's NJ = 2 tile is 128 x 128), 0 gemm_wr_kernel -- A/B measurements and the tests that compare them;
+// + 4: the weight-stationary gemm_ws_kernel first for the launches it takes (ws_ok: K <= 384, >= 32768 rows, the
+// shapes where it measured faster).
+// Default 5.
+static int g_wide_variant = 5;
+static bool ws_on() { return (g_wide_variant & 4) != 0; }
+static bool ws_any() { return (g_wide_variant & 8) != 0; }  // + 8: every shape gemm_ws can run (tests)
 extern "C" int asrx_set_gemm_variant(int v) {
   const int old = g_wide_variant;
   g_wide_variant = v;
@@ -21,8 +27,8 @@ static bool p2_ok(const asrx::wn::Params& p, int conv, int nj, int a_bf16) {
   if (!a_bf16 && p.M >= 131072) return false;
   const bool vec = ((p.N | p.ldc) & 3) == 0 && ((uintptr_t)p.C & 15) == 0 && ((uintptr_t)p.Z & 15) == 0 &&
                    ((uintptr_t)p.Cb & 7) == 0;
-  return g_wide_variant >= 1 && !conv && (nj == 3 || nj == 2 || (nj == 1 && g_wide_variant == 2)) && vec &&
-         p.K >= 64;
+  return (g_wide_variant & 3) >= 1 && !conv && (nj == 3 || nj == 2 || (nj == 1 && (g_wide_variant & 3) == 2)) &&
+         vec && p.K >= 64;
 }
 
 namespace asrx {
@@ -149,7 +155,9 @@ extern "C" int asrx_gemm_wn_ex(const void* A, int a_bf16, int64_t lda, int conv,
 #define ASRX_WN_EX(NJV)                                                                              \
   if (a_bf16) conv ? wn::launch_wr<NJV, true, false, true>(p, stream) : wn::launch_wr<NJV, false, false, true>(p, stream); \
   else conv ? wn::launch_wr<NJV, true>(p, stream) : wn::launch_wr<NJV, false>(p, stream);
-  if (p2_ok(p, conv, nj, a_bf16)) {
+  if (ws_on() && !conv && wn::ws_ok(p, a_bf16, ws_any())) {
+    a_bf16 ? wn::launch_ws_act<true>(p, stream) : wn::launch_ws_act<false>(p, stream);
+  } else if (p2_ok(p, conv, nj, a_bf16)) {
     if (nj == 3) a_bf16 ? wn::launch_p2_act<3, true, false>(p, stream) : wn::launch_p2_act<3, false, false>(p, stream);
     else a_bf16 ? wn::launch_p2_act<2, true, false>(p, stream) : wn::launch_p2_act<2, false, false>(p, stream);  // nj 2 / 1
   } else if (nj == 3) { ASRX_WN_EX(3) }
@@ -220,7 +228,8 @@ extern "C" int asrx_gemm_wn_res(const float* A, int64_t lda, const unsigned shor
   ASRX_REQUIRE(nj == 1 || nj == 3, "asrx_gemm_wn_res: nj 1 or 3");
   wn::Params p{A, (int)lda, W, (int)ldw, C, (int)ldc, bias, nullptr, (int)M, (int)N, (int)K, 1, 1, 1.f, 0.f,
                ACT_NONE, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, R, (int)ldr};
-  if (nj == 3 && p2_ok(p, 0, nj, 0)) wn::launch_p2_act<3, false, true>(p, stream);
+  if (ws_on() && wn::ws_ok(p, false, ws_any())) wn::launch_ws<false, ACT_NONE, true, false>(p, stream);
+  else if (nj == 3 && p2_ok(p, 0, nj, 0)) wn::launch_p2_act<3, false, true>(p, stream);
   else if (nj == 3) wn::launch_wr<3, false, false, false, false, true>(p, stream);
   else wn::launch_wr<1, false, false, false, false, true>(p, stream);
   ASRX_LAUNCHED("asrx_gemm_wn_res");
@@ -252,8 +261,10 @@ extern "C" int asrx_gemm_wn_rot(const void* A, int a_bf16, int64_t lda, const un
   p.rot_L = (int)L;
   p.rot_half = (int)(hd / 2);
   p.rot_scale = scale;
-  ASRX_REQUIRE(nj == 1 || g_wide_variant >= 1, "asrx_gemm_wn_rot: nj 3 runs on gemm_p2 only (variant >= 1)");
-  if (nj == 3) a_bf16 ? wn::launch_p2<3, true, ACT_NONE, false, true>(p, stream)
+  ASRX_REQUIRE(nj == 1 || (g_wide_variant & 3) >= 1, "asrx_gemm_wn_rot: nj 3 runs on gemm_p2 only (variant >= 1)");
+  if (ws_on() && wn::ws_ok(p, a_bf16, ws_any())) a_bf16 ? wn::launch_ws<true, ACT_NONE, false, true>(p, stream)
+                                      : wn::launch_ws<false, ACT_NONE, false, true>(p, stream);
+  else if (nj == 3) a_bf16 ? wn::launch_p2<3, true, ACT_NONE, false, true>(p, stream)
                       : wn::launch_p2<3, false, ACT_NONE, false, true>(p, stream);
   else a_bf16 ? wn::launch_wr<1, false, false, true, false, false, false, true>(p, stream)
               : wn::launch_wr<1, false, false, false, false, false, false, true>(p, stream);

@@ -29,7 +29,7 @@ for M, N, K in SHAPES:
         A = torch.randn(M, K, device=dev).to(torch.bfloat16 if abf else torch.float32)
         W = torch.randn(N, K, device=dev) * 0.05
         Wb = G.weight_bf16(W, cache=False)
-        C = torch.empty(M, N, device=dev)
+        C = torch.empty(M, N, device=dev, dtype=torch.bfloat16 if os.environ.get("GEMM_CBF") else torch.float32)
         bias = torch.randn(N, device=dev) if os.environ.get("GEMM_BIAS") else None
         for nj in NJS:
             if 128 * nj > ((N + 127) // 128) * 128:
