@@ -24,25 +24,26 @@ if os.environ.get("GEMM_SHAPES"):
 NJS = tuple(int(v) for v in os.environ.get("GEMM_NJ", "1,2,3").split(","))
 ABFS = tuple(bool(int(v)) for v in os.environ.get("GEMM_ABF", "0,1").split(","))
 ITERS = int(os.environ.get("GEMM_ITERS", "50"))
+BETA = float(os.environ.get("GEMM_BETA", "0"))  # 1: the accumulating input-gradient launches (C += A W^T)
 for M, N, K in SHAPES:
     for abf in ABFS:
         A = torch.randn(M, K, device=dev).to(torch.bfloat16 if abf else torch.float32)
         W = torch.randn(N, K, device=dev) * 0.05
         Wb = G.weight_bf16(W, cache=False)
-        C = torch.empty(M, N, device=dev, dtype=torch.bfloat16 if os.environ.get("GEMM_CBF") else torch.float32)
+        C = torch.zeros(M, N, device=dev, dtype=torch.bfloat16 if os.environ.get("GEMM_CBF") else torch.float32)
         bias = torch.randn(N, device=dev) if os.environ.get("GEMM_BIAS") else None
         for nj in NJS:
             if 128 * nj > ((N + 127) // 128) * 128:
                 continue
             G._nj_override = nj
             for _ in range(3):
-                G.gemm_wn(A, Wb, C, M=M, N=N, K=K, lda=K, ldc=N, bias=bias)
+                G.gemm_wn(A, Wb, C, M=M, N=N, K=K, lda=K, ldc=N, bias=bias, beta=BETA)
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             n = ITERS
             e0.record()
             for _ in range(n):
-                G.gemm_wn(A, Wb, C, M=M, N=N, K=K, lda=K, ldc=N, bias=bias)
+                G.gemm_wn(A, Wb, C, M=M, N=N, K=K, lda=K, ldc=N, bias=bias, beta=BETA)
             e1.record()
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) * 1e3 / n
