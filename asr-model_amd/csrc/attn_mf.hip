@@ -360,6 +360,178 @@ __global__ __launch_bounds__(NTHR, WPE) void attn_fwd_mf_kernel(const TI* __rest
   }
 }
 
+// Software-pipelined forward (HD = 64; asrx_set_attn_variant, 1 = this kernel, the default): the same
+// per-element arithmetic in the same order as attn_fwd_mf_kernel (bit-identical outputs), re-timed so the
+// score MFMAs of tile t + 1 share one basic block with the softmax VALU of tile t and the compiler can
+// put the exp / convert / sum work in the MFMA gaps (one wave alone had nothing to issue under its
+// score MFMAs, and the softmax had no MFMA to hide under).  K runs one tile ahead of V: iteration t
+// reads K(t + 1) and V(t), and writes K(t + 2) into K(t)'s buffer and V(t + 1) into V(t - 1)'s, so one
+// barrier per tile still separates every write from the reads of its buffer.  The boundary mask of a
+// tile is applied when its scores are made (end of the previous iteration), outside the interleaved
+// block; loads past the last tile are clamped (stage_load) and their scores never used.  Two named
+// score sets (loop unrolled by two) instead of a runtime index, which would go to scratch.
+template <bool XCD, typename TI, typename TO>
+__global__ __launch_bounds__(NTHR, 1) void attn_fwd_sp_kernel(const TI* __restrict__ q, const TI* __restrict__ k,
+                                                            const TI* __restrict__ v, TO* __restrict__ o,
+                                                            float* __restrict__ lse, AttnStridesMF sq,
+                                                            AttnStridesMF sk, AttnStridesMF sv, AttnStridesMF so,
+                                                            int64_t H, int64_t Lq, int64_t Lk, int causal,
+                                                            float scale) {
+  constexpr int HD = 64;
+  __shared__ __attribute__((aligned(16))) unsigned short Ks[2][HALF];
+  __shared__ __attribute__((aligned(16))) unsigned short Vs[2][HALF];
+
+  int b, h;
+  int64_t q0;
+  if (XCD) {
+    const int64_t nqb = (Lq + QB - 1) / QB;
+    const int64_t G = (int64_t)gridDim.x, L = xcd_logical(blockIdx.x, G);
+    q0 = (L % nqb) * QB;
+    h = (int)((L / nqb) % H);
+    b = (int)(L / (nqb * H));
+  } else {
+    b = blockIdx.z;
+    h = blockIdx.y;
+    q0 = (int64_t)blockIdx.x * QB;
+  }
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int j = lane & 31, hi = lane >> 5;
+  const int64_t qi = q0 + wid * 32 + j;
+  const TI* kb = k + b * sk.b + h * sk.h;
+  const TI* vb = v + b * sv.b + h * sv.h;
+  const float c = scale * LOG2E;
+
+  bf16x8 qf[HD / 16];
+  row_frags<HD>(q + b * sq.b + h * sq.h, sq.l, qi, Lq, hi, qf);
+
+  int64_t kend = Lk;
+  if (causal) kend = min(Lk, q0 + QB);
+  const int ntiles = (int)((kend + KT - 1) / KT);
+  const int skey = tid >> 3, sc = tid & 7;
+
+  Row8<TI> ka, va;
+  stage_load(kb, sk, skey, Lk, 0, sc, ka);
+  stage_load(vb, sv, skey, Lk, 0, sc, va);
+  stage_store(Ks[0], skey, sc ^ kswz(skey), ka);
+  stage_store(Vs[0], skey, sc ^ vswz(skey), va);
+  stage_load(kb, sk, KT + skey, Lk, 0, sc, ka);
+  stage_store(Ks[1], skey, sc ^ kswz(skey), ka);
+  __syncthreads();
+
+  // scores of tile tt (K image Kt) into s, boundary keys masked (wave-uniform test, as attn_fwd_mf_kernel)
+  auto scores = [&](f32x16 (&s)[2], const unsigned short* Kt, int tt) {
+#pragma unroll
+    for (int kb2 = 0; kb2 < 2; ++kb2) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[kb2][r] = 0.f;
+      dot_rows<HD>(s[kb2], Kt, 32 * kb2 + j, hi, qf);
+    }
+  };
+  auto mask = [&](f32x16 (&s)[2], int tt) {
+    const int64_t k0 = (int64_t)tt * KT;
+    const bool need_mask =
+        __builtin_amdgcn_readfirstlane((int)((k0 + KT > Lk) || (causal && k0 + KT - 1 > q0 + wid * 32))) != 0;
+    if (need_mask) {
+      const int lim = (int)min(min(Lk - k0, (int64_t)KT), causal ? qi - k0 + 1 : (int64_t)KT);
+#pragma unroll
+      for (int kb2 = 0; kb2 < 2; ++kb2)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = 32 * kb2 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+          s[kb2][r] = key >= lim ? -INFINITY : s[kb2][r];
+        }
+    }
+  };
+
+  f32x16 sA[2], sB[2];
+  scores(sA, Ks[0], 0);
+  mask(sA, 0);
+
+  f32x16 oacc[HD / 32];
+#pragma unroll
+  for (int d = 0; d < HD / 32; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) oacc[d][r] = 0.f;
+  float m = -INFINITY;
+  float l = 0.f;
+
+  auto step = [&](int t, f32x16 (&cur)[2], f32x16 (&nxt)[2]) {
+    const int buf = t & 1;
+    const int64_t k0 = (int64_t)t * KT;
+    stage_load(vb, sv, k0 + KT + skey, Lk, 0, sc, va);      // V(t + 1)
+    stage_load(kb, sk, k0 + 2 * KT + skey, Lk, 0, sc, ka);  // K(t + 2)
+
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int kb2 = 0; kb2 < 2; ++kb2)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, cur[kb2][r]);
+    {
+      float ta = tmax, tb = tmax;
+      xrow32(ta, tb);
+      tmax = fmaxf(ta, tb);
+    }
+    const bool up = tmax * c > m * c + 8.f;
+    if (__any(up)) {
+      const float alpha = up ? __builtin_amdgcn_exp2f(m * c - tmax * c) : 1.f;
+      if (up) m = tmax;
+      l *= alpha;
+#pragma unroll
+      for (int d = 0; d < HD / 32; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oacc[d][r] *= alpha;
+    }
+    const float mc = m == -INFINITY ? 0.f : m * c;
+
+    scores(nxt, Ks[buf ^ 1], t + 1);  // tile t + 1 (unused past the last tile)
+
+    // exp arguments and row-sum partials as single (not packed) FP32 ops: the same roundings as the packed
+    // forms, and the packed forms cost more than two singles beside MFMAs (MI355X_MICROARCH.md)
+    bf16x8 pb[2][2];
+    float l0x = 0.f, l0y = 0.f, l1x = 0.f, l1y = 0.f;
+#pragma unroll
+    for (int kb2 = 0; kb2 < 2; ++kb2)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        float pv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) pv[e] = __builtin_amdgcn_exp2f(__builtin_fmaf(cur[kb2][8 * s2 + e], c, -mc));
+        l0x += pv[0]; l0y += pv[1]; l1x += pv[2]; l1y += pv[3];
+        l0x += pv[4]; l0y += pv[5]; l1x += pv[6]; l1y += pv[7];
+        pb[kb2][s2] = pack8(pv);
+      }
+    const float ltx = l0x + l1x, lty = l0y + l1y;
+    l += ltx + lty;
+
+#pragma unroll
+    for (int kb2 = 0; kb2 < 2; ++kb2)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int d = 0; d < HD / 32; ++d)
+          oacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Vs[buf], lane, kb2, s2, d & 1), pb[kb2][s2],
+                                                            oacc[d], 0, 0, 0);
+
+    mask(nxt, t + 1);
+    stage_store(Ks[buf], skey, sc ^ kswz(skey), ka);
+    stage_store(Vs[buf ^ 1], skey, sc ^ vswz(skey), va);
+    __syncthreads();
+  };
+
+  int t = 0;
+  for (; t + 2 <= ntiles; t += 2) {
+    step(t, sA, sB);
+    step(t + 1, sB, sA);
+  }
+  if (t < ntiles) step(t, sA, sB);
+
+  const float lt = l + __shfl_xor(l, 32);
+  if (qi < Lq) {
+    store_rowT<HD, TO>(o + b * so.b + h * so.h + qi * so.l, oacc, 1.0f / lt, hi);
+    if (hi == 0) lse[((int64_t)b * H + h) * Lq + qi] = (m * c + __builtin_amdgcn_logf(lt)) * LN2;
+  }
+}
+
 // ============================================================================================
 // Backward (perf mode), the same operand tricks as the forward:
 //   Delta_i = rowsum(dO_i * O_i) (attn_delta_kernel), P = exp(S * scale - lse), dS = P (dP - Delta)
@@ -649,6 +821,9 @@ __global__ __launch_bounds__(BwdCfg<HD>::NT, 1) void attn_bwd_dq_mf_kernel(
 
 }  // namespace amf
 
+// forward kernel for HD = 64 (asrx_set_attn_variant): 1 attn_fwd_sp_kernel (default), 0 attn_fwd_mf_kernel
+static int g_attn_fwd_variant = 1;
+
 template <int HD, typename TI, typename TO>
 static void attn_fwd_mf_t(const void* q, AttnStridesMF Sq, const void* k, AttnStridesMF Sk, const void* v,
                           AttnStridesMF Sv, void* o, AttnStridesMF So, float* lse, int64_t B, int64_t H, int64_t Lq,
@@ -659,7 +834,14 @@ static void attn_fwd_mf_t(const void* q, AttnStridesMF Sq, const void* k, AttnSt
   // query blocks of one (b, h) on one XCD when there are several (3.6 % at 3001 x 3001, H = 6,
   // B = 64; profiles/r02_attn_fwd_variants.txt, which also records the rejected 4-waves-per-SIMD
   // and s_setprio variants)
-  if (HD == 64 && g.x > 1)
+  if (HD == 64 && g_attn_fwd_variant == 1) {
+    if (g.x > 1)
+      amf::attn_fwd_sp_kernel<true, TI, TO><<<dim3((unsigned)((int64_t)g.x * g.y * g.z)), amf::NTHR, 0, stream>>>(
+          qq, kk, vv, oo, lse, Sq, Sk, Sv, So, H, Lq, Lk, causal, scale);
+    else
+      amf::attn_fwd_sp_kernel<false, TI, TO><<<g, amf::NTHR, 0, stream>>>(qq, kk, vv, oo, lse, Sq, Sk, Sv, So, H, Lq,
+                                                                          Lk, causal, scale);
+  } else if (HD == 64 && g.x > 1)
     amf::attn_fwd_mf_kernel<HD, 1, true, false, TI, TO><<<dim3((unsigned)((int64_t)g.x * g.y * g.z)), amf::NTHR, 0,
                                                           stream>>>(qq, kk, vv, oo, lse, Sq, Sk, Sv, So, H, Lq, Lk,
                                                                     causal, scale);
@@ -744,3 +926,11 @@ int attn_bwd_mf(int io, const void* q, const int64_t* sq, const void* k, const i
 }
 
 }  // namespace asrx
+
+// A / B switch of the HD = 64 forward kernel (host state): 1 the software-pipelined kernel (default), 0 the
+// round-4 kernel.  Bit-identical outputs.  Returns the previous value.
+extern "C" int asrx_set_attn_variant(int v) {
+  const int old = asrx::g_attn_fwd_variant;
+  asrx::g_attn_fwd_variant = v;
+  return old;
+}

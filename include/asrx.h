@@ -32,6 +32,10 @@ int asrx_set_noise_epoch(uint32_t epoch, asrx_stream_t stream);
  * stream-ordered): 1 (default) the two-workgroups-per-CU kernel, 0 the one-workgroup-per-CU kernel.
  * Same results bit for bit; an A/B switch for measurements and tests.  Returns the previous value. */
 int asrx_set_gemm_variant(int variant);
+/* Attention forward kernel selection at head dim 64 (host state): 1 (default) the software-pipelined kernel
+ * (scores of the next key tile computed beside this tile's softmax), 0 the round-4 kernel.  Same results bit
+ * for bit; an A/B switch for measurements and tests.  Returns the previous value. */
+int asrx_set_attn_variant(int variant);
 
 /* ---- log-mel front end: replaces torchaudio MelSpectrogram + log10 + clip-max floor,
  *      essentials.py:469-491, and the waveform adaptive_avg_pool1d, essentials.py:493-510 -------- */

@@ -10,6 +10,9 @@ from microbench import timeit  # noqa: E402
 from asrx import ops, prec  # noqa: E402
 
 dev = torch.device("cuda:0")
+if os.environ.get("ATTN_VARIANT"):  # asrx_set_attn_variant: 1 software-pipelined forward (default), 0 round-4
+    from asrx import lib  # noqa: E402
+    lib.load().asrx_set_attn_variant(int(os.environ["ATTN_VARIANT"]))
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 2
 shapes = [(64, 6, 3001, 3001, False), (32, 6, 3000, 3000, False), (32, 6, 256, 3001, False), (16, 12, 3001, 3001, False)]
 for rep in range(reps):
