@@ -10,6 +10,7 @@
 // tiles: gemm_p2's NJ = 2 tile is 128 x 128), 0 gemm_wr_kernel -- A/B measurements and the tests that compare them;
 // + 4: the weight-stationary gemm_ws_kernel first for the launches it takes (ws_ok: K <= 384, >= 32768 rows, the
 // shapes where it measured faster).
+// + 16: the AbbyNormal router at d = 64 on gemm_wr_kernel instead of router64_kernel (A/B, tests).
 // Default 5.
 static int g_wide_variant = 5;
 static bool ws_on() { return (g_wide_variant & 4) != 0; }
@@ -366,6 +367,119 @@ extern "C" int asrx_row_tiles(const float* next_i, int64_t layer, int64_t L, int
 
 // AbbyNormal router (essentials.py:155-161) in one pass: h_pre = A W1^T + b1 (kept in hpre when
 // non-null, for the backward) and logits = SiLU(h_pre) W2^T (M x 3, without b2), for d <= 384.
+namespace asrx {
+namespace wn {
+
+// AbbyNormal router at d = 64 (the per-head norms of model.py:303-304's q / k; essentials.py:155-161):
+// logits = SiLU(x W1^T + b1) W2^T over 1.15 M rows of 64 features at the tiny config.  gemm_wr_kernel ran it on
+// a 128-column tile with half the columns empty and two k-steps per 128-row tile (prologue and epilogue bound,
+// 1.8 TB/s).  Here a wave streams 16-row groups straight from global memory into MFMA fragments: W1 (64 x 64 bf16)
+// sits in 32 registers as the row operand for the whole launch, each group is 8 v_mfma_f32_16x16x32_bf16, and the
+// epilogue reduces in registers.  The fragment layout, k order, epilogue expressions and the logit sum order
+// (each 32-column group over its lane's columns, xor-16 / xor-32 partners, then the groups in order, plus the
+// two empty groups' +0.0) are gemm_wr_kernel's (epilogue_router), so h_pre and the logits are bit-identical.
+// The next group's x is in flight while a group is computed (two named register sets, loop unrolled by two).
+struct R64X {
+  float4 v[4];  // lane (row l & 15): k 8 (l >> 4) .. + 7 of k-halves 0 and 1
+};
+__global__ __launch_bounds__(256) void router64_kernel(Params p) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lr = lane & 15, lk = lane >> 4;
+  bf16x8 wf[4][2];
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+      wf[nb][kb] = *reinterpret_cast<const bf16x8*>(p.W + (int64_t)(16 * nb + lr) * p.ldw + 32 * kb + 8 * lk);
+  float bv[4][4], w2v[3][4][4];
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int n = 16 * nb + 4 * lk + q;
+      bv[nb][q] = p.bias ? p.bias[n] : 0.f;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) w2v[k][nb][q] = p.W2[k * 64 + n];
+    }
+  const int64_t ngroups = ((int64_t)p.M + 15) / 16;
+  const int64_t step = (int64_t)gridDim.x * 4;
+  const float* A = reinterpret_cast<const float*>(p.A);
+  auto fetch = [&](int64_t g, R64X& x) __attribute__((always_inline)) {
+    const int64_t row = min(g * 16 + lr, (int64_t)p.M - 1);  // past the end: a valid row, results dropped
+    const float* src = A + row * p.lda + 8 * lk;
+    x.v[0] = *reinterpret_cast<const float4*>(src);
+    x.v[1] = *reinterpret_cast<const float4*>(src + 4);
+    x.v[2] = *reinterpret_cast<const float4*>(src + 32);
+    x.v[3] = *reinterpret_cast<const float4*>(src + 36);
+  };
+  auto group = [&](int64_t g, const R64X& x) __attribute__((always_inline)) {
+    bf16x8 xf[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      const float4 a = x.v[2 * kb], b = x.v[2 * kb + 1];
+      xf[kb] = bf16x8{(__bf16)a.x, (__bf16)a.y, (__bf16)a.z, (__bf16)a.w,
+                      (__bf16)b.x, (__bf16)b.y, (__bf16)b.z, (__bf16)b.w};
+    }
+    f32x4 acc[4];
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[nb][kb], xf[kb], acc[nb], 0, 0, 0);
+    const int64_t row = g * 16 + lr;
+    float s[2][3];
+#pragma unroll
+    for (int grp = 0; grp < 2; ++grp) {
+      float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const int nb = 2 * grp + nt;
+        const float v[4] = {p.alpha * acc[nb][0] + bv[nb][0], p.alpha * acc[nb][1] + bv[nb][1],
+                            p.alpha * acc[nb][2] + bv[nb][2], p.alpha * acc[nb][3] + bv[nb][3]};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float h = silu_f(v[q]);
+          s0 += h * w2v[0][nb][q];
+          s1 += h * w2v[1][nb][q];
+          s2 += h * w2v[2][nb][q];
+        }
+        if (p.C && row < p.M)
+          *reinterpret_cast<float4*>(p.C + row * p.ldc + 16 * nb + 4 * lk) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+      s0 += __shfl_xor(s0, 16); s1 += __shfl_xor(s1, 16); s2 += __shfl_xor(s2, 16);
+      s0 += __shfl_xor(s0, 32); s1 += __shfl_xor(s1, 32); s2 += __shfl_xor(s2, 32);
+      s[grp][0] = s0; s[grp][1] = s1; s[grp][2] = s2;
+    }
+    if (lk == 0 && row < p.M) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) p.R[row * 3 + k] = s[0][k] + s[1][k] + 0.f + 0.f;
+    }
+  };
+  int64_t g = (int64_t)blockIdx.x * 4 + wid;
+  if (g >= ngroups) return;
+  R64X xa, xb;
+  fetch(g, xa);
+  fetch(g + step, xb);
+  for (;; g += 2 * step) {
+    {
+      const R64X x = xa;
+      fetch(g + 2 * step, xa);
+      group(g, x);
+    }
+    if (g + step >= ngroups) break;
+    {
+      const R64X x = xb;
+      fetch(g + 3 * step, xb);
+      group(g + step, x);
+    }
+    if (g + 2 * step >= ngroups) break;
+  }
+}
+
+}  // namespace wn
+}  // namespace asrx
+
 extern "C" int asrx_gemm_wn_router(const float* A, int64_t lda, const unsigned short* W1, int64_t ldw,
                                    const float* b1, const float* W2, float* hpre, int64_t ldc, float* logits,
                                    int64_t M, int64_t N, int64_t K, hipStream_t stream) {
@@ -376,7 +490,20 @@ extern "C" int asrx_gemm_wn_router(const float* A, int64_t lda, const unsigned s
   ASRX_REQUIRE(M * lda < (1LL << 31), "asrx_gemm_wn_router: operand spans >= 2^31 elements");
   wn::Params p{A, (int)lda, W1, (int)ldw, hpre, (int)ldc, b1, nullptr, (int)M, (int)N, (int)K, 1, 1, 1.f, 0.f,
                ACT_NONE, W2, logits};
-  if (N <= 128) wn::launch_wr<1, false, true>(p, stream);
+  const bool r64 = N == 64 && K == 64 && W2 && (g_wide_variant & 16) == 0 && ldw % 8 == 0 &&
+                   (!hpre || (ldc % 4 == 0 && ((uintptr_t)hpre & 15) == 0));
+  if (r64) {
+    static int cus = 0;
+    if (!cus) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      cus = std::max(1, cus);
+    }
+    const int64_t groups = (M + 15) / 16;
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((groups + 3) / 4, (int64_t)cus * 8));
+    wn::router64_kernel<<<grid, 256, 0, stream>>>(p);
+  } else if (N <= 128) wn::launch_wr<1, false, true>(p, stream);
   else if (N <= 256) wn::launch_wr<2, false, true>(p, stream);
   else wn::launch_wr<3, false, true>(p, stream);
   ASRX_LAUNCHED("asrx_gemm_wn_router");
