@@ -98,13 +98,20 @@ def _build_plan():
 _DERIVED: dict = {}
 
 
-def derived(key, build):
-    """The per-step cached value of `key` on the current stream (build() makes it on first use)."""
-    k = (key, torch.cuda.current_stream().cuda_stream if torch.cuda.is_available() else 0)
+def derived(key, build, refs=()):
+    """The per-step cached value of `key` on the current stream (build() makes it on first use).  refs: the
+    tensors the value is derived from; their addresses, shapes and versions join the key and the entry holds
+    them, so their memory cannot be recycled for another tensor that would then hit a stale entry of a
+    different shape (a standalone module used without end_step() -- the MSheath op test after a smaller
+    one -- read such an entry out of bounds)."""
+    k = (key, tuple((t.data_ptr(), tuple(t.shape), t._version) for t in refs),
+         torch.cuda.current_stream().cuda_stream if torch.cuda.is_available() else 0)
     v = _DERIVED.get(k)
     if v is None:
-        v = _DERIVED[k] = build()
-    return v
+        v = build()
+        _DERIVED[k] = (v, tuple(refs))
+        return v
+    return v[0]
 
 
 def end_step():

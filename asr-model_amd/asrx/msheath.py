@@ -115,8 +115,7 @@ def forward(mod, x0, gpol, save, tag=None):
                      _P(mkn), _P(wb), M, Dh, D, st)
             return Wc, bc, mkn, wb
 
-        Wc, bc, mkn, wb = G.derived(("vgate", vg.mkey.data_ptr(), vg.mkey._version, vg.mlp[0].weight._version,
-                                     vg.mlp[0].bias._version, bool(wide)), build)
+        Wc, bc, mkn, wb = G.derived(("vgate", bool(wide)), build, (vg.mkey, vg.mlp[0].weight, vg.mlp[0].bias))
         # rows of samples not at this layer (next_i[b] != i; the reference never runs them) are skipped:
         # by whole 128-row tiles in the GEMMs, by row in the row kernels
         mt = G.row_tiles(next_i, i, L, rows) if (wide and next_i is not None) else None

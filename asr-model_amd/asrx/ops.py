@@ -1068,8 +1068,7 @@ class TGateFn(torch.autograd.Function):
             lib.call("asrx_cat3", _P(b0), _P(b1), _P(b2), D, _P(bc), _S())
             return Wc, bc
 
-        Wcat, bcat = G.derived(("tgate", W0.data_ptr(), W0._version, W1._version, W2._version, b0._version,
-                                b1._version, b2._version), build)
+        Wcat, bcat = G.derived(("tgate",), build, (W0, W1, W2, b0, b1, b2))
         Gs = G.linear_fwd(x, Wcat, bcat, act="sigmoid")
         if c_pre is not None:  # cs = Linear(D, 3)(x) evaluated by the producing AbbyNormal on fp32 x
             c = c_pre

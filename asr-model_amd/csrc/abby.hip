@@ -159,8 +159,7 @@ __device__ __forceinline__ void abby_row_stats(const float (&xv)[E], float& mu, 
     s += xv[e];
     sa += fabsf(xv[e]);
   }
-  s = wave_sum_dpp(s);
-  sa = wave_sum_dpp(sa);
+  wave_sum2_dpp(s, sa);
   mu = s * (1.0f / D);
   mabs = sa * (1.0f / D);
   float v = 0.f;
@@ -187,17 +186,20 @@ __device__ __forceinline__ void abby_halo(float* row, int lane, const float (&xv
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
 }
 
-// window sums (zero padding) of the halo for the lane's E outputs
-template <int E>
+// window sums (zero padding) of the halo for the lane's E outputs.  ZPAD: the halo's pads already hold 0 (the
+// forward's rows; the backward's hold -1 for its argmax), so the fmax(., 0) that maps a -1 pad to the zero
+// padding is skipped -- x^2 >= 0, so the sums are identical
+template <int E, bool ZPAD = false>
 __device__ __forceinline__ void abby_wsum(const float (&h)[AbbyShape<E>::HL], float (&avg)[E]) {
   typedef AbbyShape<E> S;
+  auto z = [](float v) __attribute__((always_inline)) { return ZPAD ? v : fmaxf(v, 0.f); };
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < S::W; ++i) s += fmaxf(h[i], 0.f);
+  for (int i = 0; i < S::W; ++i) s += z(h[i]);
   avg[0] = s * (1.0f / S::W);
 #pragma unroll
   for (int e = 1; e < E; ++e) {
-    s += fmaxf(h[e + S::W - 1], 0.f) - fmaxf(h[e - 1], 0.f);
+    s += z(h[e + S::W - 1]) - z(h[e - 1]);
     avg[e] = s * (1.0f / S::W);
   }
 }
@@ -286,17 +288,23 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_fwd_kernel(const float* 
     for (int k = 0; k < 3; ++k) ld_rowc<E>(tw + k * S::D, threadIdx.x & 63, twv[k]);
   }
   // x^2 row: feature f at P0 + f (P0 = PAD rounded up to even, so the coalesced float2 writes stay
-  // 8-byte aligned), pads of -1 (below every x^2) on both sides; den row: the denominators by feature
+  // 8-byte aligned), pads of 0 on both sides (the avg pool's zero padding; for the max pool a 0 pad equals
+  // the reference's -inf one: every window holds a real x^2 >= 0 and the forward takes no argmax); den row:
+  // the denominators by feature.  The halo is read as float2 from the even index at or below its start
+  // (HS = the offset of the halo in that read), so the row stride is even too.
   constexpr int P0 = (S::PAD + 1) & ~1;
-  constexpr int ROWC = P0 + S::D + S::PAD + 1;
+  constexpr int HS = (P0 - S::PAD) & 1;
+  constexpr int HR = (S::HL + HS + 1) / 2;  // float2 reads per lane
+  constexpr int ROWC = (P0 + S::D + S::PAD + 1 + 1) & ~1;
+  static_assert(P0 - S::PAD - HS >= 0 && P0 - S::PAD - HS + 63 * E + 2 * HR <= ROWC, "halo read inside the row");
   __shared__ __attribute__((aligned(16))) float rows_all[ABBY_WAVES][ROWC];
   __shared__ __attribute__((aligned(16))) float den_all[ABBY_WAVES][S::D];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   float* row = rows_all[wid];
   float* drow = den_all[wid];
   for (int i = lane; i < S::PAD; i += 64) {
-    row[P0 - S::PAD + i] = -1.f;
-    row[P0 + S::D + i] = -1.f;
+    row[P0 - S::PAD + i] = 0.f;
+    row[P0 + S::D + i] = 0.f;
   }
   const int64_t stride = (int64_t)gridDim.x * ABBY_WAVES;
   int64_t r = (int64_t)blockIdx.x * ABBY_WAVES + wid;
@@ -334,9 +342,7 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_fwd_kernel(const float* 
         l1 += hs * W2[S::D + j];
         l2 += hs * W2[2 * S::D + j];
       }
-      l0 = wave_sum_dpp(l0);
-      l1 = wave_sum_dpp(l1);
-      l2 = wave_sum_dpp(l2);
+      wave_sum3_dpp(l0, l1, l2);
     }
     float mu, sd, mabs;
     abby_row_stats<E>(xv, mu, sd, mabs);
@@ -374,11 +380,18 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_fwd_kernel(const float* 
           make_float2(xv[2 * j] * xv[2 * j], xv[2 * j + 1] * xv[2 * j + 1]);
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    float hh[2 * HR];
+#pragma unroll
+    for (int i = 0; i < HR; ++i) {
+      const float2 t = *reinterpret_cast<const float2*>(row + P0 - S::PAD - HS + lane * E + 2 * i);
+      hh[2 * i] = t.x;
+      hh[2 * i + 1] = t.y;
+    }
     float h[S::HL];
 #pragma unroll
-    for (int i = 0; i < S::HL; ++i) h[i] = row[P0 - S::PAD + lane * E + i];
+    for (int i = 0; i < S::HL; ++i) h[i] = hh[i + HS];
     float avg[E];
-    abby_wsum<E>(h, avg);
+    abby_wsum<E, true>(h, avg);
     if (sel == 1) {  // wave-uniform: mode 2 (max pool where max > 2 avg)
       float mx[E];
       int am[E];
@@ -419,9 +432,7 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_fwd_kernel(const float* 
         c1 += ov[e] * twv[1][e];
         c2 += ov[e] * twv[2][e];
       }
-      c0 = wave_sum_dpp(c0);
-      c1 = wave_sum_dpp(c1);
-      c2 = wave_sum_dpp(c2);
+      wave_sum3_dpp(c0, c1, c2);
       if (lane == 0) {
         tc[r * 3 + 0] = c0 + tb[0];
         tc[r * 3 + 1] = c1 + tb[1];
@@ -565,8 +576,7 @@ __global__ __launch_bounds__(64 * ABBY_WAVES) void abby_bwd_kernel(
       qa[e] = maxsel ? 0.f : q * (1.0f / S::W);
       qm[e] = maxsel ? q : 0.f;
     }
-    dd0 = wave_sum_dpp(dd0);
-    dd1 = wave_sum_dpp(dd1);
+    wave_sum2_dpp(dd0, dd1);
     const float dd2 = dd0;
     // pool backward in gather form: dsq_i = sum_{j in win(i)} qa_j + sum_{j in win(i), am_j == i} qm_j
     for (int i = lane; i < S::PAD; i += 64) {

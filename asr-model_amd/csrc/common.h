@@ -107,6 +107,77 @@ __device__ __forceinline__ void xrow16(float& a, float& b) {
 __device__ __forceinline__ void xrow32(float& a, float& b) {
   asm("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
 }
+// two / three independent swaps behind one s_nop (the second and third read registers no swap wrote)
+__device__ __forceinline__ void xrow16x2(float& a0, float& b0, float& a1, float& b1) {
+  asm("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\tv_permlane16_swap_b32 %2, %3" : "+v"(a0), "+v"(b0), "+v"(a1), "+v"(b1));
+}
+__device__ __forceinline__ void xrow32x2(float& a0, float& b0, float& a1, float& b1) {
+  asm("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\tv_permlane32_swap_b32 %2, %3" : "+v"(a0), "+v"(b0), "+v"(a1), "+v"(b1));
+}
+__device__ __forceinline__ void xrow16x3(float& a0, float& b0, float& a1, float& b1, float& a2, float& b2) {
+  asm("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\tv_permlane16_swap_b32 %2, %3\n\tv_permlane16_swap_b32 %4, %5"
+      : "+v"(a0), "+v"(b0), "+v"(a1), "+v"(b1), "+v"(a2), "+v"(b2));
+}
+__device__ __forceinline__ void xrow32x3(float& a0, float& b0, float& a1, float& b1, float& a2, float& b2) {
+  asm("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\tv_permlane32_swap_b32 %2, %3\n\tv_permlane32_swap_b32 %4, %5"
+      : "+v"(a0), "+v"(b0), "+v"(a1), "+v"(b1), "+v"(a2), "+v"(b2));
+}
+__device__ __forceinline__ float dpp_row_sum(float v) {  // the 4 in-row DPP steps of wave_sum_dpp
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));
+  return v;
+}
+// wave_sum_dpp of two / three independent values (each bit-identical to wave_sum_dpp of it), their chains
+// interleaved and their cross-row swaps sharing one hazard s_nop
+__device__ __forceinline__ void wave_sum2_dpp(float& x, float& y) {
+  x = dpp_row_sum(x);
+  y = dpp_row_sum(y);
+  float a0 = x, b0 = x, a1 = y, b1 = y;
+  xrow16x2(a0, b0, a1, b1);
+  x = a0 + b0;
+  y = a1 + b1;
+  a0 = b0 = x;
+  a1 = b1 = y;
+  xrow32x2(a0, b0, a1, b1);
+  x = a0 + b0;
+  y = a1 + b1;
+}
+__device__ __forceinline__ void wave_sum3_dpp(float& x, float& y, float& z) {
+  x = dpp_row_sum(x);
+  y = dpp_row_sum(y);
+  z = dpp_row_sum(z);
+  float a0 = x, b0 = x, a1 = y, b1 = y, a2 = z, b2 = z;
+  xrow16x3(a0, b0, a1, b1, a2, b2);
+  x = a0 + b0;
+  y = a1 + b1;
+  z = a2 + b2;
+  a0 = b0 = x;
+  a1 = b1 = y;
+  a2 = b2 = z;
+  xrow32x3(a0, b0, a1, b1, a2, b2);
+  x = a0 + b0;
+  y = a1 + b1;
+  z = a2 + b2;
+}
+// wave_sum_dpp of x beside wave_max_dpp of y (bit-identical to each alone), one hazard s_nop per swap pair
+__device__ __forceinline__ void wave_sum_max_dpp(float& x, float& y) {
+  x = dpp_row_sum(x);
+  y = fmaxf(y, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, y), 0xB1, 0xF, 0xF, false)));
+  y = fmaxf(y, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, y), 0x4E, 0xF, 0xF, false)));
+  y = fmaxf(y, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, y), 0x141, 0xF, 0xF, false)));
+  y = fmaxf(y, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, y), 0x140, 0xF, 0xF, false)));
+  float a0 = x, b0 = x, a1 = y, b1 = y;
+  xrow16x2(a0, b0, a1, b1);
+  x = a0 + b0;
+  y = fmaxf(a1, b1);
+  a0 = b0 = x;
+  a1 = b1 = y;
+  xrow32x2(a0, b0, a1, b1);
+  x = a0 + b0;
+  y = fmaxf(a1, b1);
+}
 // Wave sum with the in-row steps on DPP: xor 1 and xor 2 by quad_perm, then the other quad of each 8
 // (row_half_mirror) and the other 8 of each 16 (row_mirror); the two cross-row steps by permlane
 // swaps.  Every lane ends with the full sum, bit-identical to the ds_bpermute (__shfl_xor) version

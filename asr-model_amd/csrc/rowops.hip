@@ -164,8 +164,9 @@ __global__ __launch_bounds__(64 * RW) void ln_bwd_t_kernel(const float* __restri
       aw[e] += gv[e] * xv[e];
       ab[e] += gv[e];
     }
-    s1 = wave_sum_dpp(s1) * (1.0f / D);
-    s2 = wave_sum_dpp(s2) * (1.0f / D);
+    wave_sum2_dpp(s1, s2);
+    s1 *= (1.0f / D);
+    s2 *= (1.0f / D);
     float dv[E];
     if (acc) ld_lane<E>(dx + r * D, lane, dv);
 #pragma unroll
@@ -686,21 +687,35 @@ __global__ __launch_bounds__(64 * RW) void msheath_row_fwd_kernel(MSRowFwd p) {
       }
       return;
     }
+    // Eight wave reductions in four dependent levels (the values and their arithmetic are the one-at-a-time
+    // order's; independent chains share a level so their DPP / permlane latencies overlap):
+    // (sum x, sum x^2, SiLU(h) . w2) -> (variance, max of the key scores) -> (gate dot, sum exp) -> key mix
     float s = 0.f, q = 0.f;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       s += xv[e];
       q += xv[e] * xv[e];
     }
-    const float mu = wave_sum_dpp(s) * (1.0f / D);
-    const float nrm = sqrtf(wave_sum_dpp(q));
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < HQ; ++i)
+      if (lane + 64 * i < p.Dh) acc += silu_f(hv[i]) * w2v[i];
+    wave_sum3_dpp(s, q, acc);
+    const float mu = s * (1.0f / D);
+    const float nrm = sqrtf(q);
+    const float m2 = acc + b2;
     float v = 0.f;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const float t = xv[e] - mu;
       v += t * t;
     }
-    const float rs = rsqrtf(wave_sum_dpp(v) * (1.0f / D) + p.eps);
+    // v_gate's key scores
+    const float inx = 1.0f / fmaxf(nrm, 1e-12f);
+    const float z = lane < p.M ? sv * inx * p.inv_sqrt_d : -INFINITY;
+    float zm = z;
+    wave_sum_max_dpp(v, zm);
+    const float rs = rsqrtf(v * (1.0f / D) + p.eps);
     float yv[E], gd = 0.f;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -709,19 +724,11 @@ __global__ __launch_bounds__(64 * RW) void msheath_row_fwd_kernel(MSRowFwd p) {
     }
     if (p.pxb) st_lane<E>(p.pxb + r * D, lane, yv);
     else st_lane<E>(p.px + r * D, lane, yv);
-    const float gate = sigmoid_f(wave_sum_dpp(gd) + gbias);
-    // v_gate
-    const float inx = 1.0f / fmaxf(nrm, 1e-12f);
-    const float z = lane < p.M ? sv * inx * p.inv_sqrt_d : -INFINITY;
-    const float zm = wave_max_dpp(z);
     const float ez = lane < p.M ? expf(z - zm) : 0.f;
-    const float se = wave_sum_dpp(ez);
+    float se = ez;
+    wave_sum2_dpp(gd, se);
+    const float gate = sigmoid_f(gd + gbias);
     const float kv = wave_sum_dpp(lane < p.M ? ez / se * mv_l : 0.f);
-    float acc = 0.f;
-#pragma unroll
-    for (int i = 0; i < HQ; ++i)
-      if (lane + 64 * i < p.Dh) acc += silu_f(hv[i]) * w2v[i];
-    const float m2 = wave_sum_dpp(acc) + b2;
     const float xval = cw0 * kv + cw1 * m2 + cb;
     if (lane == 0) {
       p.mean[r] = mu;
@@ -919,8 +926,9 @@ __global__ __launch_bounds__(64 * RW) void msheath_row_bwd_kernel(MSRowBwd p) {
       ab[e] += gv[e];
       ag[e] += dzg * (xh[e] * wv[e] + bv[e]);
     }
-    s1 = wave_sum_dpp(s1) * (1.0f / D);
-    s2 = wave_sum_dpp(s2) * (1.0f / D);
+    wave_sum2_dpp(s1, s2);
+    s1 *= (1.0f / D);
+    s2 *= (1.0f / D);
     float dv[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) dv[e] = c.dx[e] + rs * (gv[e] * wv[e] - s1 - xh[e] * s2) + cn * xv[e];
@@ -1007,9 +1015,7 @@ __global__ __launch_bounds__(64 * RW) void tgate_bwd_kernel(const float* __restr
       dg[D + j] = go * t1 * g1 * (1.f - g1);
       dg[2 * D + j] = go * t2 * g2 * (1.f - g2);
     }
-    a0 = wave_sum_dpp(a0);
-    a1 = wave_sum_dpp(a1);
-    a2 = wave_sum_dpp(a2);
+    wave_sum3_dpp(a0, a1, a2);
     const float dot = t0 * a0 + t1 * a1 + t2 * a2;
     if (lane == 0) {
       dc[r * 3] = t0 * (a0 - dot);
