@@ -31,6 +31,7 @@ SIGNATURES = {
     "asrx_set_noise_epoch": (_i32, [_u32, _p]),
     "asrx_set_gemm_variant": (_i32, [_i32]),
     "asrx_set_attn_variant": (_i32, [_i32]),
+    "asrx_set_wgrad_variant": (_i32, [_i32]),
     "asrx_mel_frames": (_i32, [_i64]),
     "asrx_logmel_ws_bytes": (_i64, [_i64, _i64]),
     "asrx_flac_info": (_i32, [_p, _i64, _p, _p, _p, _p, _p]),

@@ -36,6 +36,10 @@ int asrx_set_gemm_variant(int variant);
  * (scores of the next key tile computed beside this tile's softmax), 0 the round-4 kernel.  Same results bit
  * for bit; an A/B switch for measurements and tests.  Returns the previous value. */
 int asrx_set_attn_variant(int variant);
+/* Weight-gradient kernel selection for fp32 dY with bf16 X and N % 384 == 0 (host state): 1 (default) the
+ * 128 x 384 work items of wgrad_w3_kernel, 0 the 128 x 128 items of wgrad_wr_kernel.  Same products, summed
+ * over K slices by float atomics in either case (fp32 reassociation only).  Returns the previous value. */
+int asrx_set_wgrad_variant(int variant);
 
 /* ---- log-mel front end: replaces torchaudio MelSpectrogram + log10 + clip-max floor,
  *      essentials.py:469-491, and the waveform adaptive_avg_pool1d, essentials.py:493-510 -------- */
