@@ -50,7 +50,7 @@ def _rows(x):
 # forward -- before any side stream forks -- so the entries serve every stream.  Weights derived per
 # step (tgate's concatenation, v_gate's normalised keys) keep the lazy per-call conversion.
 _WCACHE: dict = {}
-_BULK: dict = {}       # (ptr, shape, stride, trans) -> bf16 arena view, valid for the current step
+_BULK: dict = {}       # (ptr, shape, stride, trans) -> (source, bf16 arena view), valid for the current step
 _SEEN: dict = {}       # plan being recorded for the current owner: key -> (source tensor,)
 _PLANS: dict = {}      # id(owner model) -> (keys, sources, arena views, table, max_elems)
 _OWNER = None          # id of the model whose step is running (set by clear_weight_cache)
@@ -149,7 +149,10 @@ def clear_weight_cache(owner=None):
         del _PLANS[_OWNER]
         return
     lib.call("asrx_weights_to_bf16", lib.ptr(table), len(keys), mx, lib.stream())
-    _BULK.update(zip(keys, views))
+    # the entries hold their source weights: until the next clear their memory cannot be recycled for another
+    # tensor that would hit a stale entry (a model dropped after its forward, then ops on new weights: the
+    # fused-residual test after the model tests read the dropped model's bf16 copy)
+    _BULK.update((k, (s, v)) for k, s, v in zip(keys, srcs, views))
 
 
 def weight_bf16(W, trans=False, cache=True):
@@ -158,7 +161,7 @@ def weight_bf16(W, trans=False, cache=True):
     if cache and _BULK:
         hit = _BULK.get(_bulk_key(W, trans))
         if hit is not None:
-            return hit
+            return hit[1]
     key = (W.data_ptr(), tuple(W.shape), tuple(W.stride()), bool(trans), W._version,
            torch.cuda.current_stream(W.device).cuda_stream if W.is_cuda else 0) if cache else None
     if key is not None and key in _WCACHE:
@@ -277,12 +280,14 @@ def gemm_wn_rows(A, Wb, C, *, M, N, K, lda, ldc, mtiles, bias=None, alpha=1.0, b
     return gemm_wn(A, Wb, C, M=M, N=N, K=K, lda=lda, ldc=ldc, bias=bias, alpha=alpha, beta=beta, mtiles=mtiles)
 
 
-def row_tiles(next_i, layer, L, M):
+def row_tiles(next_i, layer, L, M, device=None):
     """(list, count) of the 128-row tiles of an M-row activation holding rows of samples at MSheath
-    layer `layer` (next_i[b] == layer, L rows per sample), built on the device."""
+    layer `layer` (next_i[b] == layer, L rows per sample), built on the device.  next_i: a tensor, or a device
+    address with `device` given."""
     n = int(lib.load().asrx_row_tiles_max(M))
-    tl = torch.empty(n, dtype=torch.int32, device=next_i.device)
-    cnt = torch.empty(1, dtype=torch.int32, device=next_i.device)
+    dev = device if device is not None else next_i.device
+    tl = torch.empty(n, dtype=torch.int32, device=dev)
+    cnt = torch.empty(1, dtype=torch.int32, device=dev)
     lib.call("asrx_row_tiles", lib.ptr(next_i), layer, L, M, lib.ptr(tl), lib.ptr(cnt), lib.stream())
     return tl, cnt
 

@@ -283,8 +283,12 @@ def stream() -> int:
 
 
 def ptr(t) -> int | None:
+    """Device address of a tensor; an int is an address already (per-call workspaces hand out offsets into one
+    allocation instead of a tensor view per buffer)."""
     if t is None:
         return None
+    if isinstance(t, int):
+        return t
     return t.data_ptr()
 
 

@@ -99,6 +99,16 @@ def forward(mod, x0, gpol, save, tag=None):
     next_i = None
     x = x0
     rec_bytes = _rec_bytes()
+    # the layers' small per-row / per-sample outputs live in four per-call workspaces, handed to the kernels as
+    # addresses (the kernels take raw pointers): ~16 tensor allocations per layer were ~10 % of the host's issue
+    # time on the host-bound small config (tools/host_prof.py)
+    wsr = _E(nl, 7, rows, device=dev)                       # mean, rstd, nx, g, ion, kv, m2
+    wsb = _E(nl, 5, B, device=dev)                          # alpha, beta, active, next_out, mem_v
+    wsd = _E(nl, 3, B, D, device=dev)                       # gam, mwo, mem
+    wsc = _E(nl, B * rec_bytes, dtype=torch.uint8, device=dev)  # control records
+    a_r, a_b, a_d, a_c = wsr.data_ptr(), wsb.data_ptr(), wsd.data_ptr(), wsc.data_ptr()
+    if save:
+        sv["ws"] = (wsr, wsb, wsd, wsc)
     inv_sqrt_d = 1.0 / math.sqrt(D)
     layers = []
     for i, lay in enumerate(mod.layers):
@@ -118,7 +128,7 @@ def forward(mod, x0, gpol, save, tag=None):
         Wc, bc, mkn, wb = G.derived(("vgate", bool(wide)), build, (vg.mkey, vg.mlp[0].weight, vg.mlp[0].bias))
         # rows of samples not at this layer (next_i[b] != i; the reference never runs them) are skipped:
         # by whole 128-row tiles in the GEMMs, by row in the row kernels
-        mt = G.row_tiles(next_i, i, L, rows) if (wide and next_i is not None) else None
+        mt = G.row_tiles(next_i, i, L, rows, dev) if (wide and next_i is not None) else None
         SH = G.linear_fwd(x, Wc, bc, wbf=wb, mtiles=mt)
         # px = LayerNorm(x), |x|, g = sigmoid(gate(px)), ion = v_gate(x)   (346-351, 452-460)
         ln, gt = lay["ln"], lay["gate"][0]
@@ -126,7 +136,7 @@ def forward(mod, x0, gpol, save, tag=None):
         # px feeds only the adapter GEMM on even layers (bf16-stored); on odd layers it is the update itself
         pxb = int(ad is not None and wide and prec.bf16_storage())
         px = _E(B, L, D, device=dev, dtype=torch.bfloat16 if pxb else torch.float32)
-        mean, rstd, nx, gv, ion, kv, m2 = (_E(rows, device=dev) for _ in range(7))
+        mean, rstd, nx, gv, ion, kv, m2 = (a_r + 4 * rows * (7 * i + j) for j in range(7))
         lib.call("asrx_msheath_row_fwd2", _P(x), _P(ln.weight), _P(ln.bias), _P(gt.weight), _P(gt.bias), _P(SH), N,
                  _P(vg.mval), _P(vg.mlp[2].weight), _P(vg.mlp[2].bias), _P(vg.concat.weight), _P(vg.concat.bias),
                  _P(vg.tx), _P(px), pxb, _P(mean), _P(rstd), _P(nx), _P(gv), _P(ion), _P(kv), _P(m2), rows, D, M, Dh,
@@ -138,15 +148,15 @@ def forward(mod, x0, gpol, save, tag=None):
         lib.call("asrx_axpy_row2_colsum", _P(x), _P(gv), _P(ion), _P(out), _P(x_new), _P(part[i]), B, L, D,
                  _P(next_i), i, st)
         # mem_v = sigmoid(mem_gate(mem)); control; jump select   (464-501)
-        alpha, beta, active, next_out, mem_v = (_E(B, device=dev) for _ in range(5))
-        gam, mwo, mem = _E(B, D, device=dev), _E(B, D, device=dev), _E(B, D, device=dev)
-        rec = _E(B * rec_bytes, dtype=torch.uint8, device=dev)
+        alpha, beta, active, next_out, mem_v = (a_b + 4 * B * (5 * i + j) for j in range(5))
+        gam, mwo, mem = (a_d + 4 * B * D * (3 * i + j) for j in range(3))
+        rec = a_c + B * rec_bytes * i
         gp = gpol[:, i]
         lib.call("asrx_msheath_ctrl_fwd3", _P(policy), _P(gp), gp.stride(0), _P(ion), _P(mg.weight), _P(mg.bias),
                  _P(mem_v), _P(mem_w), ld_mw, _P(part[i]), _P(mem), _P(mod.jump_s), _P(next_i), i, nl, B, L, D,
                  _P(alpha), _P(beta), _P(gam), _P(mwo), _P(active), _P(next_out), _P(rec), st)
         if tag is not None and decisions.active():
-            decisions.msheath_layer(tag[0], tag[1], i, ion.view(B, L), rec.view(torch.float32).view(B, -1))
+            decisions.msheath_layer(tag[0], tag[1], i, wsr[i, 4].view(B, L), wsc[i].view(torch.float32).view(B, -1))
         if save:
             x_out = _E(B, L, D, device=dev)
             lib.call("asrx_jump_select4", _P(x_new), _P(x0), _P(x), _P(active), _P(alpha), _P(beta), _P(gam),

@@ -2,6 +2,9 @@
 // row reduction is needed, grid-stride elementwise otherwise).  Each kernel names the reference
 // op(s) it replaces.
 #include "common.h"
+#include <algorithm>
+#include <mutex>
+#include <unordered_map>
 
 namespace asrx {
 
@@ -310,7 +313,7 @@ template <int NS, typename TX = float>
 __global__ __launch_bounds__(64 * RW) void small_linear_bwd_kernel(
     const float* __restrict__ dy, const float* __restrict__ y, const TX* __restrict__ x,
     const float* __restrict__ W, float* __restrict__ dx, float* __restrict__ dW, float* __restrict__ db,
-    int64_t rows, int K, int act, float beta) {
+    int64_t rows, int K, int act, float beta, float* __restrict__ ws) {
   extern __shared__ float part[];  // [RW][NS*K + NS]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int PN = NS * K + NS;
@@ -345,11 +348,27 @@ __global__ __launch_bounds__(64 * RW) void small_linear_bwd_kernel(
     }
   }
   __syncthreads();
+  // Deterministic parameter gradients: each workgroup writes its partial to ws[blockIdx.x] and
+  // small_linear_colsum_kernel adds the partials in a fixed order into dW / db.  Float atomics summed them in
+  // completion order, which made e.g. MSheath's mlp_gate bias gradient differ between two schedules of the
+  // same step by more than the rerun spread the dead-block test measures.
   for (int j = threadIdx.x; j < PN; j += 64 * RW) {
     float s = 0.f;
     for (int ww = 0; ww < RW; ++ww) s += part[ww * PN + j];
-    if (j < NS * K) atomicAdd(dW + j, s);
-    else if (db) atomicAdd(db + (j - NS * K), s);
+    ws[(int64_t)blockIdx.x * PN + j] = s;
+  }
+}
+
+// one wave per column j of the nb x PN partials: lane l sums rows l, l + 64, ... in order, then a fixed wave tree
+__global__ __launch_bounds__(64) void small_linear_colsum_kernel(const float* __restrict__ ws, int nb, int PN, int NSK,
+                                                                 float* __restrict__ dW, float* __restrict__ db) {
+  const int j = blockIdx.x, lane = threadIdx.x;
+  float s = 0.f;
+  for (int bb = lane; bb < nb; bb += 64) s += ws[(int64_t)bb * PN + j];
+  s = wave_sum(s);
+  if (lane == 0) {
+    if (j < NSK) dW[j] += s;
+    else if (db) db[j - NSK] += s;
   }
 }
 
@@ -2245,19 +2264,53 @@ int asrx_small_linear_fwd(const float* x, const float* W, const float* b, float*
 }
 
 }  // extern "C"
+// per-stream partial buffer of small_linear_bwd_kernel (grown on demand outside any graph capture: the first
+// backward runs eagerly; launches on one stream reuse it in stream order)
+struct SlWs {
+  float* buf = nullptr;
+  size_t bytes = 0;
+};
+static int sl_workspace(hipStream_t stream, size_t bytes, float** ws) {
+  static std::unordered_map<hipStream_t, SlWs> pool;
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lk(mu);
+  SlWs& w = pool[stream];
+  if (w.bytes < bytes) {
+    if (w.buf) {
+      (void)hipStreamSynchronize(stream);  // earlier launches on this stream may still read the old buffer
+      (void)hipFree(w.buf);
+    }
+    const size_t nb = std::max(bytes, (size_t)1 << 20);
+    hipError_t e = hipMalloc(&w.buf, nb);
+    if (e != hipSuccess) {
+      w.buf = nullptr;
+      w.bytes = 0;
+      asrx::set_error("small_linear_bwd workspace: %s", hipGetErrorString(e));
+      return (int)e;
+    }
+    w.bytes = nb;
+  }
+  *ws = w.buf;
+  return 0;
+}
+
 template <typename TX>
 static int small_linear_bwd_t(const float* dy, const float* y, const TX* x, const float* W, float* dx, float* dW,
                               float* db, int64_t rows, int64_t K, int64_t N, int act, float beta, hipStream_t stream) {
   const size_t shm = (size_t)RW * (N * K + N) * sizeof(float);
   ASRX_REQUIRE(shm <= 64 * 1024, "small_linear_bwd: K too large");
   const unsigned g = row_grid(rows, 1024);
+  float* ws = nullptr;
+  const int rc = sl_workspace(stream, (size_t)g * (N * K + N) * sizeof(float), &ws);
+  if (rc) return rc;
   switch (N) {
-    case 1: small_linear_bwd_kernel<1, TX><<<g, 64 * RW, shm, stream>>>(dy, y, x, W, dx, dW, db, rows, (int)K, act, beta); break;
-    case 2: small_linear_bwd_kernel<2, TX><<<g, 64 * RW, shm, stream>>>(dy, y, x, W, dx, dW, db, rows, (int)K, act, beta); break;
-    case 3: small_linear_bwd_kernel<3, TX><<<g, 64 * RW, shm, stream>>>(dy, y, x, W, dx, dW, db, rows, (int)K, act, beta); break;
-    case 4: small_linear_bwd_kernel<4, TX><<<g, 64 * RW, shm, stream>>>(dy, y, x, W, dx, dW, db, rows, (int)K, act, beta); break;
+    case 1: small_linear_bwd_kernel<1, TX><<<g, 64 * RW, shm, stream>>>(dy, y, x, W, dx, dW, db, rows, (int)K, act, beta, ws); break;
+    case 2: small_linear_bwd_kernel<2, TX><<<g, 64 * RW, shm, stream>>>(dy, y, x, W, dx, dW, db, rows, (int)K, act, beta, ws); break;
+    case 3: small_linear_bwd_kernel<3, TX><<<g, 64 * RW, shm, stream>>>(dy, y, x, W, dx, dW, db, rows, (int)K, act, beta, ws); break;
+    case 4: small_linear_bwd_kernel<4, TX><<<g, 64 * RW, shm, stream>>>(dy, y, x, W, dx, dW, db, rows, (int)K, act, beta, ws); break;
     default: ASRX_REQUIRE(false, "small_linear: N=%ld not in 1..4", (long)N);
   }
+  small_linear_colsum_kernel<<<(unsigned)(N * K + N), 64, 0, stream>>>(ws, (int)g, (int)(N * K + N), (int)(N * K), dW, db);
   return 0;
 }
 

@@ -10,3 +10,8 @@ timeout -k 10 600 python -u bench.py --config small --batch 8 --no-cpu-baseline 
 cut -c1-200 gpurun_out/${T}_small.json
 timeout -k 10 600 python -u bench.py --config medium --batch 8 --no-cpu-baseline > gpurun_out/${T}_medium.json 2> gpurun_out/${T}_medium.err || { tail -20 gpurun_out/${T}_medium.err; exit 1; }
 cut -c1-200 gpurun_out/${T}_medium.json
+# host-bound configs: the same steps replayed from one captured graph (no per-launch host cost)
+timeout -k 10 600 python -u bench.py --config small --batch 8 --no-cpu-baseline --graph --no-refpitch-line > gpurun_out/${T}_small_graph.json 2> gpurun_out/${T}_small_graph.err || { tail -20 gpurun_out/${T}_small_graph.err; exit 1; }
+cut -c1-200 gpurun_out/${T}_small_graph.json
+timeout -k 10 600 python -u bench.py --config medium --batch 8 --no-cpu-baseline --graph --no-refpitch-line > gpurun_out/${T}_medium_graph.json 2> gpurun_out/${T}_medium_graph.err || { tail -20 gpurun_out/${T}_medium_graph.err; exit 1; }
+cut -c1-200 gpurun_out/${T}_medium_graph.json
