@@ -5,6 +5,7 @@
 //   control: potential, gumbel policy, action, alpha/beta/gam, mem_w, next layer  msheath_ctrl
 //   x = act ? alpha*x_new + beta*orig + gam : x                                     jump_select
 // instead of ~25 small tensor ops forward and ~40 backward.
+#include <type_traits>
 #include "common.h"
 
 namespace asrx {
@@ -256,21 +257,27 @@ __global__ __launch_bounds__(256) void axpy_row2_colsum_kernel(const float4* __r
   };
   if (rl < nrl) {
     int64_t l = l0 + rl;
-    // four of the thread's rows per trip, every load issued first (one row per trip exposed a full load
-    // latency per row); the sums keep the row order, so the results are unchanged
-    for (; l + 3 * nrl < l1; l += 4 * nrl) {
-      float sc[4];
-      float4 a[4], v[4];
+    // U of the thread's rows per trip, every load issued first (one row per trip exposed a full load
+    // latency per row; most launches have few samples at the layer, so few waves per SIMD, and the
+    // bytes in flight per wave set the rate); the sums keep the row order, so the results are unchanged
+    auto trips = [&](auto UC) __attribute__((always_inline)) {
+      constexpr int U = decltype(UC)::value;
+      for (; l + (U - 1) * nrl < l1; l += U * nrl) {
+        float sc[U];
+        float4 a[U], v[U];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int64_t r = b * L + l + u * nrl;
-        sc[u] = s1[r] * s2[r];
-        a[u] = x[r * d4 + c];
-        v[u] = y[r * d4 + c];
+        for (int u = 0; u < U; ++u) {
+          const int64_t r = b * L + l + u * nrl;
+          sc[u] = s1[r] * s2[r];
+          a[u] = x[r * d4 + c];
+          v[u] = y[r * d4 + c];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) one(sc[u], a[u], v[u], (b * L + l + u * nrl) * d4 + c);
       }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) one(sc[u], a[u], v[u], (b * L + l + u * nrl) * d4 + c);
-    }
+    };
+    trips(std::integral_constant<int, 8>{});
+    trips(std::integral_constant<int, 4>{});
     for (; l < l1; l += nrl) {
       const int64_t r = b * L + l;
       one(s1[r] * s2[r], x[r * d4 + c], y[r * d4 + c], r * d4 + c);
