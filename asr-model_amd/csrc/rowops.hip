@@ -2264,33 +2264,29 @@ int asrx_small_linear_fwd(const float* x, const float* W, const float* b, float*
 }
 
 }  // extern "C"
-// per-stream partial buffer of small_linear_bwd_kernel (grown on demand outside any graph capture: the first
-// backward runs eagerly; launches on one stream reuse it in stream order)
-struct SlWs {
-  float* buf = nullptr;
-  size_t bytes = 0;
-};
-static int sl_workspace(hipStream_t stream, size_t bytes, float** ws) {
-  static std::unordered_map<hipStream_t, SlWs> pool;
+// per-stream partial buffer of small_linear_bwd_kernel, allocated once at its largest size (grid <= 1024
+// workgroups x (N K + N) <= 64 KB / RW floats: 16 MB) so it never grows: a stream's launches reuse it in stream
+// order, and nothing is freed or synchronised while a graph capture may be running.  A stream's first use may
+// come inside a capture (bench.py --graph captures on its own stream), so the allocation runs in relaxed
+// capture mode, as PyTorch's allocator does; the buffer outlives the graph that records its address.
+constexpr size_t SL_WS_BYTES = (size_t)1024 * (64 * 1024 / RW);
+static int sl_workspace(hipStream_t stream, float** ws) {
+  static std::unordered_map<hipStream_t, float*> pool;
   static std::mutex mu;
   std::lock_guard<std::mutex> lk(mu);
-  SlWs& w = pool[stream];
-  if (w.bytes < bytes) {
-    if (w.buf) {
-      (void)hipStreamSynchronize(stream);  // earlier launches on this stream may still read the old buffer
-      (void)hipFree(w.buf);
-    }
-    const size_t nb = std::max(bytes, (size_t)1 << 20);
-    hipError_t e = hipMalloc(&w.buf, nb);
+  float*& buf = pool[stream];
+  if (!buf) {
+    hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+    (void)hipThreadExchangeStreamCaptureMode(&mode);
+    const hipError_t e = hipMalloc(&buf, SL_WS_BYTES);
+    (void)hipThreadExchangeStreamCaptureMode(&mode);
     if (e != hipSuccess) {
-      w.buf = nullptr;
-      w.bytes = 0;
+      buf = nullptr;
       asrx::set_error("small_linear_bwd workspace: %s", hipGetErrorString(e));
       return (int)e;
     }
-    w.bytes = nb;
   }
-  *ws = w.buf;
+  *ws = buf;
   return 0;
 }
 
@@ -2300,8 +2296,9 @@ static int small_linear_bwd_t(const float* dy, const float* y, const TX* x, cons
   const size_t shm = (size_t)RW * (N * K + N) * sizeof(float);
   ASRX_REQUIRE(shm <= 64 * 1024, "small_linear_bwd: K too large");
   const unsigned g = row_grid(rows, 1024);
+  ASRX_REQUIRE((size_t)g * (N * K + N) * sizeof(float) <= SL_WS_BYTES, "small_linear_bwd: partials exceed the workspace");
   float* ws = nullptr;
-  const int rc = sl_workspace(stream, (size_t)g * (N * K + N) * sizeof(float), &ws);
+  const int rc = sl_workspace(stream, &ws);
   if (rc) return rc;
   switch (N) {
     case 1: small_linear_bwd_kernel<1, TX><<<g, 64 * RW, shm, stream>>>(dy, y, x, W, dx, dW, db, rows, (int)K, act, beta, ws); break;
