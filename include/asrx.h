@@ -233,7 +233,9 @@ int asrx_layernorm_fwd3(const float* x, const float* w, const float* b, void* y,
 /* ---- small-N linear (N <= 4): gate / mem_gate / mlp_gate Linear(D,1) (model.py:398, 406, 420),
  *      v_gate.mlp[2] (341), tgate.cs Linear(D,3) (530), MPNet's Linear(128,3) (381).
  *      act: 0 none, 3 sigmoid; forward only: 16 = softmax over the N outputs of the row (MPNet + the
- *      softmax of model.py:435 in one launch).  Backward: dx = beta*dx + dz W; dW/db accumulated. ------ */
+ *      softmax of model.py:435 in one launch).  Backward: dx = beta*dx + dz W; dW/db accumulated from
+ *      per-workgroup partials in a fixed order (deterministic; a 16 MB partial buffer per stream, allocated on
+ *      the stream's first call, capture-safe, kept for the process lifetime). ------ */
 int asrx_small_linear_fwd(const float* x, const float* W, const float* b, float* y, int64_t rows, int64_t K,
                           int64_t N, int act, asrx_stream_t stream);
 int asrx_small_linear_bwd(const float* dy, const float* y, const float* x, const float* W, float* dx, float* dW,
