@@ -38,19 +38,32 @@ __global__ __launch_bounds__(256) void msheath_ctrl_fwd_kernel(
     // the chunk partials are loaded 16 at a time before they are added (in chunk order, so the sum
     // is bit-identical to the sequential loop): a dependent load-add chain over ~47 chunks left
     // every load's latency exposed (24 us per launch at B = 32)
+    // (a thread's two columns c0 and c0 + 256 in flight together, and the last partial group loaded from
+    // clamped addresses like the full ones: its serial remainder loop and the second column's separate pass
+    // exposed ~20 load latencies per launch)
     const float* mp = mem_part + (int64_t)b * nchunk * D;
-    for (int c = threadIdx.x; c < D; c += 256) {
-      float t = 0.f;
-      int k = 0;
-      for (; k + 16 <= nchunk; k += 16) {
-        float v[16];
+    for (int c0 = threadIdx.x; c0 < D; c0 += 512) {
+      const int c1 = c0 + 256;
+      const bool two = c1 < D;
+      const int c1c = two ? c1 : c0;
+      float t0 = 0.f, t1 = 0.f;
+      for (int k = 0; k < nchunk; k += 16) {
+        float v0[16], v1[16];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) v[j] = mp[(int64_t)(k + j) * D + c];
+        for (int j = 0; j < 16; ++j) {
+          const int64_t kk = min(k + j, nchunk - 1);
+          v0[j] = mp[kk * D + c0];
+          v1[j] = mp[kk * D + c1c];
+        }
 #pragma unroll
-        for (int j = 0; j < 16; ++j) t += v[j];
+        for (int j = 0; j < 16; ++j)
+          if (k + j < nchunk) {
+            t0 += v0[j];
+            t1 += v1[j];
+          }
       }
-      for (; k < nchunk; ++k) t += mp[(int64_t)k * D + c];
-      mem_out[b * D + c] = t * (1.0f / (float)L);
+      mem_out[b * D + c0] = t0 * (1.0f / (float)L);
+      if (two) mem_out[b * D + c1] = t1 * (1.0f / (float)L);
     }
     __syncthreads();
     mem = mem_out;
@@ -58,15 +71,14 @@ __global__ __launch_bounds__(256) void msheath_ctrl_fwd_kernel(
   float s = 0.f;
   {
     const float* ib = ion + b * L;
-    int64_t l = threadIdx.x;
-    for (; l + 7 * 256 < L; l += 8 * 256) {  // 8 loads in flight, added in the same order
-      float v[8];
+    for (int64_t l = threadIdx.x; l < L; l += 8 * 256) {  // 8 loads in flight (the tail's from clamped
+      float v[8];                                          // addresses), added in the same order
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = ib[l + 256 * j];
+      for (int j = 0; j < 8; ++j) v[j] = ib[min<int64_t>(l + 256 * j, L - 1)];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s += v[j];
+      for (int j = 0; j < 8; ++j)
+        if (l + 256 * j < L) s += v[j];
     }
-    for (; l < L; l += 256) s += ib[l];
   }
   const float potential = block_sum<256>(s, red) / (float)L;  // ion.mean(dim=1), model.py:466
   float mv;
@@ -159,9 +171,16 @@ __global__ __launch_bounds__(256) void msheath_ctrl_bwd_kernel(
     const float mw = mem_w[b * ld_mem_w + c], me = mem[b * D + c];
     const float mwn = mv * mw + (1.f - mv) * me;
     float gg;
-    if (part_g) {  // the jump-select backward's L-chunk partials, added in chunk order (deterministic)
-      gg = 0.f;
-      for (int k = 0; k < nlc; ++k) gg += part_g[(b * nlc + k) * D + c];
+    if (part_g) {  // the jump-select backward's L-chunk partials, added in chunk order (deterministic;
+      gg = 0.f;      // 16 loads in flight, the last group's from clamped addresses)
+      for (int k = 0; k < nlc; k += 16) {
+        float v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = part_g[(b * nlc + min(k + j, nlc - 1)) * D + c];
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          if (k + j < nlc) gg += v[j];
+      }
     } else {
       gg = g_gam[b * D + c];
     }
@@ -187,12 +206,20 @@ __global__ __launch_bounds__(256) void msheath_ctrl_bwd_kernel(
     const int action = (int)r.action;
     const bool jumped = action > 0;
     float ga, gb;
-    if (part_ab) {
+    if (part_ab) {  // in order, 16 loads in flight (a dependent chain of ~100 loads cost ~10 us per launch)
       ga = 0.f, gb = 0.f;
-      for (int k = 0; k < nlc * ncc; ++k) {
-        const float2 v = part_ab[b * nlc * ncc + k];
-        ga += v.x;
-        gb += v.y;
+      const int n = nlc * ncc;
+      const float2* pb = part_ab + b * n;
+      for (int k = 0; k < n; k += 16) {
+        float2 v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = pb[min(k + j, n - 1)];
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          if (k + j < n) {
+            ga += v[j].x;
+            gb += v[j].y;
+          }
       }
     } else {
       ga = g_alpha[b], gb = g_beta[b];
