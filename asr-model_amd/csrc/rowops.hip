@@ -1208,7 +1208,14 @@ __global__ void seg_reduce_kernel(const float* __restrict__ part, float* __restr
   if (i >= (int64_t)B * d) return;
   const int64_t b = i / d, c = i % d;
   float t = 0.f;
-  for (int k = 0; k < nchunk; ++k) t += part[(b * nchunk + k) * d + c];
+  for (int k = 0; k < nchunk; k += 16) {  // in chunk order, 16 loads in flight (the last group's clamped)
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = part[(b * nchunk + min(k + j, nchunk - 1)) * d + c];
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (k + j < nchunk) t += v[j];
+  }
   out[i] = t * scale;
 }
 
