@@ -2117,8 +2117,32 @@ __global__ __launch_bounds__(64 * RW) void row_normalize_bwd_kernel(const float*
                                                                     const float* __restrict__ n, float* __restrict__ dx,
                                                                     int64_t rows, int d, int acc) {
   const int lane = threadIdx.x & 63;
+  constexpr int C = 16;  // d <= 64 C: every operand of the row (y, dy, the accumulated dx) loaded at once
   for (int64_t r = row_begin(); r < rows; r += row_step()) {
     const float nn = n[r];
+    if (d <= 64 * C) {  // same arithmetic and order as the general loop below, one load round trip per row
+      float yv[C], gv[C], ov[C];
+#pragma unroll
+      for (int i = 0; i < C; ++i) {
+        const int j = lane + 64 * i;
+        const bool ok = j < d;
+        yv[i] = ok ? y[r * d + j] : 0.f;
+        gv[i] = ok ? dy[r * d + j] : 0.f;
+        ov[i] = ok && acc ? dx[r * d + j] : 0.f;
+      }
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < C; ++i)
+        if (lane + 64 * i < d) s += yv[i] * gv[i];
+      s = wave_sum_dpp(s);
+      const bool clamped = nn <= 1e-12f;
+#pragma unroll
+      for (int i = 0; i < C; ++i) {
+        const int j = lane + 64 * i;
+        if (j < d) dx[r * d + j] = ov[i] + (gv[i] - (clamped ? 0.f : yv[i] * s)) / nn;
+      }
+      continue;
+    }
     float s = 0.f;
     for (int j = lane; j < d; j += 64) s += y[r * d + j] * dy[r * d + j];
     s = wave_sum_dpp(s);
