@@ -34,6 +34,16 @@ __global__ __launch_bounds__(256) void msheath_ctrl_fwd_kernel(
     const float* __restrict__ mem_part, int nchunk, float* __restrict__ mem_out) {
   __shared__ float red[4];
   const int64_t b = blockIdx.x;
+  // the sample's ion values (L <= 24 * 256: the configurations' 3001 / 6002 frames) are requested first, so
+  // their loads are in flight together with the mem partials' instead of after them
+  constexpr int IQ = 24;
+  const float* ib = ion + b * L;
+  const bool ion_pre = L <= (int64_t)IQ * 256;
+  float iv[IQ];
+  if (ion_pre) {
+#pragma unroll
+    for (int j = 0; j < IQ; ++j) iv[j] = ib[min<int64_t>(threadIdx.x + 256 * j, L - 1)];
+  }
   if (mem_part) {  // mem = (1/L) sum over the row chunks of x_new, in chunk order (deterministic)
     // the chunk partials are loaded 16 at a time before they are added (in chunk order, so the sum
     // is bit-identical to the sequential loop): a dependent load-add chain over ~47 chunks left
@@ -69,8 +79,11 @@ __global__ __launch_bounds__(256) void msheath_ctrl_fwd_kernel(
     mem = mem_out;
   }
   float s = 0.f;
-  {
-    const float* ib = ion + b * L;
+  if (ion_pre) {  // the thread's values in the order of the loop below
+#pragma unroll
+    for (int j = 0; j < IQ; ++j)
+      if (threadIdx.x + 256 * j < L) s += iv[j];
+  } else {
     for (int64_t l = threadIdx.x; l < L; l += 8 * 256) {  // 8 loads in flight (the tail's from clamped
       float v[8];                                          // addresses), added in the same order
 #pragma unroll
