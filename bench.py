@@ -383,13 +383,15 @@ def main():
         probe.clear_aux()
         if wn_sec > 0:
             gbs = wn_bytes / wn_sec / 1e9
-            result["roofline"] = {"kernel": "asrx::wn::gemm_wr_kernel + gemm_p2_kernel + gemm_ws_kernel, every "
-                                            "instantiation (the wide bf16-weight MFMA GEMM: plain, row-list, residual, "
-                                            "rotary, tied logits, router, activation-gradient; gemm_p2 = its "
-                                            "two-workgroups-per-CU form, gemm_ws = its weight-stationary form)",
+            result["roofline"] = {"kernel": "asrx::wn::gemm_wr_kernel + gemm_p2_kernel + gemm_ws_kernel + "
+                                            "router64_kernel, every instantiation (the wide bf16-weight MFMA GEMM: "
+                                            "plain, row-list, residual, rotary, tied logits, router, "
+                                            "activation-gradient; gemm_p2 = its two-workgroups-per-CU form, gemm_ws = "
+                                            "its weight-stationary form, router64 = the d = 64 router launches)",
                                   "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                   "frac": round(gbs / HBM_PEAK_GBS, 4),
-                                  **pmc_traffic(("gemm_wr_kernel", "gemm_p2_kernel", "gemm_ws_kernel"), args.config,
+                                  **pmc_traffic(("gemm_wr_kernel", "gemm_p2_kernel", "gemm_ws_kernel", "router64_kernel"),
+                                                args.config,
                                                 args.batch, args.pitch_frames),
                                   "algorithmic_bytes_per_launch": round(wn_bytes / wn_n),
                                   "algorithmic_bytes_per_step": round(wn_bytes / probe_steps),
@@ -400,7 +402,8 @@ def main():
                                   "mfma_achieved_tflops": round(wn_flops / wn_sec / 1e12, 2),
                                   "mfma_frac": round(wn_flops / wn_sec / 1e12 / peak, 4),
                                   "recompute": "frac = algorithmic_bytes_per_step / (gemm_wr_kernel + gemm_p2_kernel + "
-                                               "gemm_ws_kernel time per step in the rocprof summary) / peak"}
+                                               "gemm_ws_kernel + router64_kernel time per step in the rocprof summary) "
+                                               "/ peak"}
         result["gemm_all"] = {"kernel": "every asrx GEMM launch (wide, generic fp32/bf16 incl. wgrad, router)",
                               "bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                               "frac": round(achieved / peak, 4),
