@@ -155,6 +155,27 @@ def clear_weight_cache(owner=None):
     _BULK.update((k, (s, v)) for k, s, v in zip(keys, srcs, views))
 
 
+def plan_token():
+    """Identity of the running step's bulk bf16 arena (None before its owner's plan exists): a recorded launch
+    sequence that reads the arena's views (a dead-block graph) is valid only while this token is unchanged."""
+    plan = _PLANS.get(_OWNER) if _OWNER is not None else None
+    return None if not plan or not plan[2] else (_OWNER, plan[2][0].data_ptr())
+
+
+def plan_refs():
+    """The tensors of the running step's bulk plan (arena views, entry table): held by a graph that reads them."""
+    plan = _PLANS.get(_OWNER) if _OWNER is not None else None
+    return () if not plan else tuple(plan[2]) + (plan[3],)
+
+
+def forget_stream(stream_id):
+    """Drop the per-step cache entries made on one stream (after a graph capture on it: their values live in the
+    graph's pool and hold the right contents only after a replay)."""
+    for d in (_WCACHE, _DERIVED):
+        for k in [k for k in d if k[-1] == stream_id]:
+            del d[k]
+
+
 def weight_bf16(W, trans=False, cache=True):
     """bf16 N x K copy of a weight: W is (N, K) (trans=False) or (K, N) (trans=True).  Cached per
     stream: a copy converted on one stream is never read by another before it is complete."""

@@ -498,6 +498,19 @@ class processor(nn.Module):  # noqa: N801  (model.py:585-629)
         # the live forward), "mid" (after the live audio side: beside the live text side, the cross entropy and
         # the backward) or "end" (after the live forward: beside the cross entropy and the backward)
         self.dead_blocks_at = "end"  # measured: end 5108-5111, mid 5097-5114, start 5061-5072 audio-s/s (profiles/r05_dead_at_ab.txt)
+        # Opt-in: the concurrent dead blocks replayed from HIP graphs, one set per step signature (shapes,
+        # grouping, precision switches, the bulk bf16 arena), so their launches cost one graph launch of host time
+        # instead of ~30-45 us of Python each.  Same kernels, same shapes, same work; the replays reuse the capture
+        # step's noise keys -- the dead blocks' outputs never reach the loss (model.py:617-628).  Off by default:
+        # the steps it was built for turned out GPU-bound, not host-bound, and the replays run the side streams'
+        # kernels with less overlap than eager launches (profiles/r06_host_vs_gpu.txt: small B = 8 452 vs 418 ms
+        # per step, tiny B = 32 180 vs 180 ms, with the forward's host time 30 vs 260 ms and 18 vs 47 ms).
+        self.graph_dead_blocks = False
+        self.graph_dead_max = 4  # graphs kept per processor (each holds its own memory pool)
+        self._dgraphs = {}
+        self._dseen = set()
+        self.keep_dead_out = False  # tests: dead_out = the last dead block's output (graph vs eager)
+        self.dead_out = None
         self._side = None
         self._pending = None
         self._hold = []
@@ -561,29 +574,152 @@ class processor(nn.Module):  # noqa: N801  (model.py:585-629)
         Scheduling only: keyed noise, same kernels, same results."""
         main = torch.cuda.current_stream()
         s_audio, s_text = self._side_streams(x.device)
+        if self._replay_dead(live, x, A_in, noise, B, main, s_audio, s_text):
+            self._pending = (s_audio, s_text, [x, xe] + A_in, main)
+            return
         s_audio.wait_stream(main)
         s_text.wait_stream(main)
         with torch.no_grad():
             for i in range(live):
-                self._dead_block(i, x, A_in, noise, B, s_audio, s_text)
+                g = self._dead_block(i, x, A_in, noise, B, s_audio, s_text)
+        if self.keep_dead_out:
+            self.dead_out = g
         self._pending = (s_audio, s_text, [x, xe] + A_in, main)
+
+    def _dead_signature(self, live, x, A_in, groups, B):
+        from . import msheath
+        return (live, tuple(x.shape), x.dtype, tuple((tuple(a.shape), a.dtype) for a in A_in), tuple(groups), B,
+                str(x.device), prec.state(), self.training, ops.ROT_FUSED, ops.DIRECT, MSheath.fused,
+                msheath.DETERMINISTIC, gemm_mod._nj_override, gemm_mod.plan_token())
+
+    def _replay_dead(self, live, x, A_in, noise, B, main, s_audio, s_text):
+        """Blocks 0..L-2 from the signature's HIP graphs (see graph_dead_blocks).  False: run them eagerly
+        (graphs off, a first sighting, decisions recorded or kernels probed -- both need eager launches --, or
+        the graph budget spent).
+
+        Three graphs keep the eager schedule's two side streams: the text self calls of every dead block on
+        s_text, the audio sides (self calls and cross k / v) on s_audio, then -- after an event on the audio
+        graph -- the text cross calls on s_text.  One graph per stream, so no captured fork / join (whose
+        branches the replay maps onto one hardware queue, profiles/r05_eager_vs_graph.txt): the 2048-8192-row
+        text-side kernels keep running beside the audio side's 48k-192k-row ones."""
+        from . import decisions, probe
+        if (not self.graph_dead_blocks or self.graph_dead_max <= 0 or decisions.active() or probe.active()
+                or torch.cuda.is_current_stream_capturing()):
+            return False
+        groups, i = [], 0  # runs of equal-length streams, batched as processor._audio batches them
+        while i < len(A_in):
+            j = i + 1
+            while j < len(A_in) and A_in[j].shape[1] == A_in[i].shape[1]:
+                j += 1
+            groups.append((i, j))
+            i = j
+        sig = self._dead_signature(live, x, A_in, groups, B)
+        ent = self._dgraphs.get(sig)
+        if ent is None:
+            # capture on a signature's second sighting -- or on its first once the bulk bf16 arena exists, when the
+            # live forward ran first (its tables and lazy buffers then exist; bench.py's warm-up steps capture)
+            ready = sig in self._dseen or (sig[-1] is not None and self.dead_blocks_at == "end")
+            self._dseen.add(sig)
+            if not ready or len(self._dgraphs) >= self.graph_dead_max:
+                return False
+        with torch.no_grad():
+            if ent is None:  # static inputs: the graphs read their inputs from fixed addresses
+                ent = {"sx": torch.empty(x.shape, dtype=x.dtype, device=x.device), "gbufs": []}
+                views = [None] * len(A_in)
+                for i, j in groups:
+                    src = A_in[i]
+                    buf = torch.empty((src.shape[0] * (j - i),) + tuple(src.shape[1:]), dtype=src.dtype,
+                                      device=src.device)
+                    ent["gbufs"].append(buf)
+                    views[i:j] = ops.split_rows(buf, j - i)
+                ent["views"] = views
+                new = True
+            else:
+                new = False
+            s_audio.wait_stream(main)
+            s_text.wait_stream(main)
+            with torch.cuda.stream(s_text):
+                ent["sx"].copy_(x)
+            with torch.cuda.stream(s_audio):
+                for (i, j), buf in zip(groups, ent["gbufs"]):
+                    buf.copy_(ops.group(A_in[i:j]))
+            if new:
+                self._capture_dead(ent, live, noise, B, s_audio, s_text)
+                self._dgraphs[sig] = ent
+            with torch.cuda.stream(s_text):
+                ent["text_self"].replay()
+            with torch.cuda.stream(s_audio):
+                ent["audio"].replay()
+                ev = torch.cuda.Event()
+                ev.record(s_audio)
+            with torch.cuda.stream(s_text):
+                s_text.wait_event(ev)
+                ent["text_cross"].replay()
+        if self.keep_dead_out:
+            self.dead_out = ent["out"]
+        return True
+
+    def _capture_dead(self, ent, live, noise, B, s_audio, s_text):
+        """Record the three dead-block graphs of one signature (inputs: ent's static buffers)."""
+        sx, views = ent["sx"], ent["views"]
+        graphs = [torch.cuda.CUDAGraph() for _ in range(3)]
+        # each graph captured on the stream it replays on (per-stream buffers and caches are that stream's)
+        with torch.cuda.graph(graphs[0], stream=s_text, capture_error_mode="thread_local"):
+            As = [self._dead_text_self(i, sx, noise) for i in range(live)]
+        with torch.cuda.graph(graphs[1], stream=s_audio, capture_error_mode="thread_local"):
+            KVs = [self._dead_audio(i, views, noise, B)[1] for i in range(live)]
+        with torch.cuda.graph(graphs[2], stream=s_text, capture_error_mode="thread_local"):
+            out = [self._dead_text_cross(i, As[i], KVs[i], noise)[-1] for i in range(live)][-1]
+        for s in (s_audio, s_text):
+            gemm_mod.forget_stream(s.cuda_stream)
+        ent.update(text_self=graphs[0], audio=graphs[1], text_cross=graphs[2], out=out,
+                   # read across graphs: the text self calls' outputs and the audio side's k / v (each lives in
+                   # its producer graph's pool, held here)
+                   cross=(As, KVs),
+                   # made outside the capture, read by the graphs, droppable by a cache: rotary tables (replaced
+                   # when a longer sequence grows them) and the bulk bf16 arena
+                   refs=(tuple(ops._ROT_TABLES.values()), gemm_mod.plan_refs()))
+
+    def reset_dead_graphs(self):
+        """Drop the captured dead-block graphs (after changing a switch the signature does not cover, e.g. the
+        C-side kernel variants of asrx_set_gemm_variant)."""
+        self.join_dead_blocks()
+        torch.cuda.synchronize()
+        self._dgraphs.clear()
+        self._dseen.clear()
 
     def _side_streams(self, device):
         if self._side is None or self._side[0].device != device:
             self._side = (torch.cuda.Stream(device=device), torch.cuda.Stream(device=device))
         return self._side
 
+    def _dead_text_self(self, i, x, noise):
+        return ops.fork(self.block[i].call(x, noise, f"b{i}.ta", 0, masked=True))
+
+    def _dead_audio(self, i, A_in, noise, B):
+        blk = self.block[i]
+        A = self._audio(blk, A_in, noise, f"b{i}.audio", B, "call")
+        return A, self._audio(blk, A, noise, f"b{i}.xa", B, "xa")
+
+    def _dead_text_cross(self, i, a, KV, noise):
+        blk = self.block[i]
+        b_ = ops.fork(blk.call(a, noise, f"b{i}.tb", 0, kv=KV[0]))
+        c_ = ops.fork(blk.call(b_, noise, f"b{i}.tc", 0, kv=KV[1]))
+        d = ops.fork(blk.call(c_, noise, f"b{i}.td", 0, kv=KV[2]))
+        e = ops.add(a, b_, c_)
+        kve = blk.xa_side(e, noise, f"b{i}.tg.xa", 0)
+        return b_, c_, d, e, kve, blk.call(d, noise, f"b{i}.tg", 0, kv=kve)
+
     def _dead_block(self, i, x, A_in, noise, B, s_audio, s_text, keep=None):
         """Block i < L-1 without autograd state (model.py:617-626; its output is discarded): the audio side
         on s_audio (None: the current stream), the text side on s_text (None: the current stream) -- the
-        text self call first, the cross calls after the audio side's k / v (event)."""
-        blk = self.block[i]
+        text self call first, the cross calls after the audio side's k / v (event).  Returns the block's last
+        output."""
         cur = contextlib.nullcontext
         with torch.cuda.stream(s_text) if s_text is not None else cur():
-            a = ops.fork(blk.call(x, noise, f"b{i}.ta", 0, masked=True))
+            a = self._dead_text_self(i, x, noise)
         with torch.cuda.stream(s_audio) if s_audio is not None else cur():
-            A = self._audio(blk, A_in, noise, f"b{i}.audio", B, "call")
-            KV = self._audio(blk, A, noise, f"b{i}.xa", B, "xa")
+            A, KV = self._dead_audio(i, A_in, noise, B)
             ev = None
             if s_text is not None:
                 ev = torch.cuda.Event()
@@ -593,17 +729,13 @@ class processor(nn.Module):  # noqa: N801  (model.py:585-629)
         with torch.cuda.stream(s_text) if s_text is not None else cur():
             if ev is not None:
                 torch.cuda.current_stream().wait_event(ev)
-            b_ = ops.fork(blk.call(a, noise, f"b{i}.tb", 0, kv=KV[0]))
-            c_ = ops.fork(blk.call(b_, noise, f"b{i}.tc", 0, kv=KV[1]))
-            d = ops.fork(blk.call(c_, noise, f"b{i}.td", 0, kv=KV[2]))
-            e = ops.add(a, b_, c_)
-            kve = blk.xa_side(e, noise, f"b{i}.tg.xa", 0)
-            blk.call(d, noise, f"b{i}.tg", 0, kv=kve)
+            rest = self._dead_text_cross(i, a, KV, noise)
         # tensors made on one stream and read on another stay referenced until the join
         if keep is not None:
-            keep.append((A, KV, a, b_, c_, d, e, kve))
+            keep.append((A, KV, a) + rest)
         elif self._hold is not None:
-            self._hold.append((A, KV, a, b_, c_, d, e, kve))
+            self._hold.append((A, KV, a) + rest)
+        return rest[-1]
 
     def join_dead_blocks(self):
         """Join the side streams of the concurrent dead blocks into the current stream (idempotent)."""

@@ -424,26 +424,29 @@ class KVProjFn(torch.autograd.Function):
             kz = _E(*x.shape[:-1], D, device=x.device) if grad else None
             k = G.linear_rot_fwd(x, W[:D], b[:D], m, tab, L, hd, scale, preact=kz)
             ctx.hd, ctx.scale = hd, scale
-            ctx.rot_saved = (kz, src, m, freqs, tab) if grad else None
+            # (kz, src, m, freqs, tab) through save_for_backward like LinearRotFn: autograd's version check
+            # then catches an in-place change of src or its row norm between forward and backward
+            rsaved = (kz, src, m, freqs, tab) if grad else (None,) * 5
         else:
             k = G.linear_fwd(x, W[:D], b[:D])
+            rsaved = (None,) * 5
         v = G.linear_fwd(x, W[D:], b[D:], out_bf16=v_bf16)  # v only feeds attention
         ctx.vsink = vsink
         ctx.set_materialize_grads(False)
         ctx.sink = sink
         ctx.dW, ctx.db = _direct(ctx, 1, W), _direct(ctx, 2, b)
-        ctx.save_for_backward(x, W, b)
+        ctx.save_for_backward(x, W, b, *rsaved)
         return k, v
 
     @staticmethod
     def backward(ctx, dk, dv):
-        x, W, b = ctx.saved_tensors
+        x, W, b, *rsaved = ctx.saved_tensors
         D = W.shape[0] // 2
         dk = _f32(dk)
         dv = grad_in(dv, ctx.vsink)
         dsrc = None
-        if ctx.rot and dk is not None:
-            dk, dsrc = _rotary_bwd(ctx, dk, *ctx.rot_saved, ctx.needs_input_grad[6], ctx.src_sink)
+        if ctx.rot and dk is not None and rsaved[1] is not None:
+            dk, dsrc = _rotary_bwd(ctx, dk, *rsaved, ctx.needs_input_grad[6], ctx.src_sink)
         if dk is not None:
             dk = dk.reshape(*x.shape[:-1], D)
         if dv is not None:

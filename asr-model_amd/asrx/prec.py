@@ -43,6 +43,12 @@ def get() -> int:
     return _mode["prec"]
 
 
+def state() -> tuple:
+    """Every switch of this module (a key for launch sequences recorded under one mode, e.g. the dead-block
+    graphs of asrx.model.processor)."""
+    return tuple(sorted(_mode.items()))
+
+
 def name() -> str:
     return {v: k for k, v in _NAMES.items()}[_mode["prec"]]
 

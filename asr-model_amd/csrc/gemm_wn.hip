@@ -262,11 +262,14 @@ extern "C" int asrx_gemm_wn_rot(const void* A, int a_bf16, int64_t lda, const un
   p.rot_L = (int)L;
   p.rot_half = (int)(hd / 2);
   p.rot_scale = scale;
-  ASRX_REQUIRE(nj == 1 || (g_wide_variant & 3) >= 1, "asrx_gemm_wn_rot: nj 3 runs on gemm_p2 only (variant >= 1)");
+  // the same kernel choice as asrx_gemm_wn_ex: gemm_ws where it takes the shape, gemm_p2 where p2_ok (so fp32 A at
+  // >= 131072 rows and gemm variant 0 stay on gemm_wr), gemm_wr otherwise -- every form bit-identical
   if (ws_on() && wn::ws_ok(p, a_bf16, ws_any())) a_bf16 ? wn::launch_ws<true, ACT_NONE, false, true>(p, stream)
                                       : wn::launch_ws<false, ACT_NONE, false, true>(p, stream);
-  else if (nj == 3) a_bf16 ? wn::launch_p2<3, true, ACT_NONE, false, true>(p, stream)
-                      : wn::launch_p2<3, false, ACT_NONE, false, true>(p, stream);
+  else if (nj == 3 && p2_ok(p, 0, nj, a_bf16)) a_bf16 ? wn::launch_p2<3, true, ACT_NONE, false, true>(p, stream)
+                                                   : wn::launch_p2<3, false, ACT_NONE, false, true>(p, stream);
+  else if (nj == 3) a_bf16 ? wn::launch_wr<3, false, false, true, false, false, false, true>(p, stream)
+                           : wn::launch_wr<3, false, false, false, false, false, false, true>(p, stream);
   else a_bf16 ? wn::launch_wr<1, false, false, true, false, false, false, true>(p, stream)
               : wn::launch_wr<1, false, false, false, false, false, false, true>(p, stream);
   ASRX_LAUNCHED("asrx_gemm_wn_rot");

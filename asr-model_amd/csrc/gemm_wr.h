@@ -1061,4 +1061,6 @@ ASRX_WR_DECL_GA(3, false)
 ASRX_WR_DECL_GA(3, true)
 ASRX_WR_DECL_ROT(1, true)
 ASRX_WR_DECL_ROT(1, false)
+ASRX_WR_DECL_ROT(3, true)
+ASRX_WR_DECL_ROT(3, false)
 #endif

@@ -4,7 +4,9 @@
 #include "common.h"
 #include <algorithm>
 #include <mutex>
+#include <map>
 #include <unordered_map>
+#include <utility>
 
 namespace asrx {
 
@@ -2301,11 +2303,19 @@ int asrx_small_linear_fwd(const float* x, const float* W, const float* b, float*
 // come inside a capture (bench.py --graph captures on its own stream), so the allocation runs in relaxed
 // capture mode, as PyTorch's allocator does; the buffer outlives the graph that records its address.
 constexpr size_t SL_WS_BYTES = (size_t)1024 * (64 * 1024 / RW);
+// Keyed by (device, stream): the null stream's handle is the same on every device, and a destroyed stream's
+// handle can come back on another device, so the handle alone could hand one device's buffer to another.
 static int sl_workspace(hipStream_t stream, float** ws) {
-  static std::unordered_map<hipStream_t, float*> pool;
+  static std::map<std::pair<int, hipStream_t>, float*> pool;
   static std::mutex mu;
+  int dev = 0;
+  const hipError_t de = hipGetDevice(&dev);
+  if (de != hipSuccess) {
+    asrx::set_error("small_linear_bwd workspace: hipGetDevice: %s", hipGetErrorString(de));
+    return (int)de;
+  }
   std::lock_guard<std::mutex> lk(mu);
-  float*& buf = pool[stream];
+  float*& buf = pool[std::make_pair(dev, stream)];
   if (!buf) {
     hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
     (void)hipThreadExchangeStreamCaptureMode(&mode);

@@ -60,6 +60,8 @@ def parse():
                     "pitch shape (6001 frames: pw.dio's 5 ms frames, essentials.py:451-455)")
     ap.add_argument("--dead-at", default=None, choices=["start", "mid", "end"], help="where the dead blocks' side-stream "
                     "work is enqueued (asrx.model.processor.dead_blocks_at; default: the model's)")
+    ap.add_argument("--graph-dead", action="store_true", help="replay the dead blocks from HIP graphs "
+                    "(asrx.model.processor.graph_dead_blocks; off by default, profiles/r06_host_vs_gpu.txt)")
     ap.add_argument("--no-dead-block-line", action="store_true", help="skip the extra measurement with the "
                     "reference's dead decoder blocks eliminated (reported beside, never as, the headline)")
     return ap.parse_args()
@@ -220,6 +222,7 @@ def main():
     model = Model(cfg).to(dev).train()
     if args.dead_at:
         model.processor.dead_blocks_at = args.dead_at
+    model.processor.graph_dead_blocks = args.graph_dead
     if distributed:
         broadcast_parameters(model)
     gsync = GradSync(model, reduce_single=args.dist_single)
@@ -283,6 +286,20 @@ def main():
     elapsed = time.perf_counter() - t0
     if graph is not None:
         lib.call("asrx_set_noise_epoch", 0, lib.stream())
+    # host_issue_ms_per_step above includes the time the host spends BLOCKED in launches once the GPU's queues are
+    # full, so it approaches ms_per_step whenever the GPU is the bound too.  Issue time without that back-pressure:
+    # steps started from an idle GPU (synchronised before each), the host's own time to issue one step, beside
+    # that step's wall time -- issue well below wall means the step is GPU-bound (profiles/r06_host_vs_gpu.txt)
+    free_issue, free_wall = [], []
+    if graph is None:
+        for _ in range(2):
+            torch.cuda.synchronize()
+            h0 = time.perf_counter()
+            step()
+            h1 = time.perf_counter()
+            torch.cuda.synchronize()
+            free_issue.append(h1 - h0)
+            free_wall.append(time.perf_counter() - h0)
     if not args.no_probe:
         # per-kernel HIP events stay out of the timed region (and cannot be read back from inside a
         # captured graph): every rank runs the identical step (same kernels, shapes and inputs)
@@ -349,6 +366,12 @@ def main():
                    "parallelism": f"dp{world}"},
         "per_gpu": round(value / world, 3),
         "host_issue_ms_per_step": round(host_s / args.steps * 1e3, 3),
+        **({"host_issue_from_idle_ms": round(min(free_issue) * 1e3, 3),
+            "step_from_idle_ms": round(min(free_wall) * 1e3, 3),
+            "host_issue_note": "host_issue_ms_per_step includes launches blocked on full GPU queues; "
+                               "host_issue_from_idle_ms is one step issued from an idle GPU (min of 2) beside that "
+                               "step's wall time step_from_idle_ms: issue < wall means the GPU is the bound"}
+           if free_issue else {}),
         **({"grad_sync_rel_spread": grad_spread} if distributed else {}),
         **({"dist_single": "1-rank RCCL group through the N>1 path (eager, bucket all-reduces on the comm "
                            "stream); a rehearsal, not the headline"} if args.dist_single else {}),

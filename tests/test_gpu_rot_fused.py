@@ -116,3 +116,36 @@ def test_kv_proj_rotary_autograd_matches_unfused(cuda, B, L):
         assert torch.equal(a, c)
     for gf, gu in zip(g_f, g_u):
         assert _rel(gf, gu) < 1e-5
+
+
+@pytest.mark.parametrize("variant,B,L,abf", [(0, 16, 3001, True), (0, 16, 3001, False), (1, 48, 3001, False)])
+def test_gemm_rot_every_wide_variant(cuda, variant, B, L, abf):
+    """asrx_gemm_wn_rot under the A/B switch asrx_set_gemm_variant: variant 0 (gemm_wr only) and fp32 A at >= 131072
+    rows (which gemm_p2 does not take) run the nj = 3 rotary epilogue on gemm_wr_kernel -- bit-identical to the
+    GEMM + rotary pass like every other form (nj = 3 used to raise under variant 0)."""
+    from asrx import gemm as G
+    from asrx import lib, ops
+    from asrx.model import rotary_freqs
+
+    D, H = 384, 6
+    hd = D // H
+    x, src, W, b = _inputs(cuda, B, L, D, abf, 91 + variant + abf)
+    freqs = rotary_freqs(D, H, False, cuda)
+    scale = hd ** -0.25
+    m = torch.empty(B * L, device=cuda)
+    lib.call("asrx_rownorm", lib.ptr(src), lib.ptr(m), B * L, D, lib.stream())
+    tab = ops.rotary_table(freqs, L, hd)
+    old = lib.load().asrx_set_gemm_variant(variant)
+    try:
+        assert G._nj(B * L, D) == 3
+        z = torch.empty(B, L, D, device=cuda)
+        y = G.linear_rot_fwd(x, W, b, m, tab, L, hd, scale, preact=z)
+        q = G.linear_fwd(x, W, b)
+    finally:
+        lib.load().asrx_set_gemm_variant(old)
+    ref = torch.empty_like(q)
+    lib.call("asrx_rotary_fwd2", lib.ptr(q), lib.ptr(m), lib.ptr(freqs), lib.ptr(tab), lib.ptr(ref), B * L, L, D, hd,
+             float(scale), lib.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(z, q)
+    assert torch.equal(y, ref)
