@@ -21,6 +21,7 @@ with mem_gate inside it (asrx_msheath_ctrl_fwd3) and the jump select.  The backw
 """
 from __future__ import annotations
 
+import ctypes
 import math
 
 import torch
@@ -344,16 +345,117 @@ class MSheathFn(torch.autograd.Function):
         return (dx, None, None, None) + (None,) * len(ctx.needs_input_grad[4:])
 
 
+# ------------------------------------------------------------------------------------------------ no-save composite
+# forward(save=False) -- the reference's dead blocks, eval and decoding -- as ONE C-ABI call (asrx_msheath_fwd,
+# csrc/msheath_plan.cpp) that enqueues the same launches from C++: the per-layer Python around ~7 launches cost
+# ~30 us of host time each (profiles/r06_host_vs_gpu.txt).  The per-module constants travel as an
+# asrx_msheath_plan, built once per step and stream (the v_gate projections and bf16 weight copies it points at
+# are per-step values).  False: the Python loop above (same kernels, bit-identical results).
+COMPOSITE = True
+
+
+class _Layer(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("ln_w", "ln_b", "gate_w", "gate_b", "mval", "vw2", "vb2", "cw", "cb",
+                                                "tx", "bc", "wcb", "ad_wb", "ad_b")] + \
+               [("M", ctypes.c_int64), ("Dh", ctypes.c_int64), ("ln_eps", ctypes.c_float), ("px_bf16", ctypes.c_int32)]
+
+
+class _Plan(ctypes.Structure):
+    _fields_ = [("p0_wb", ctypes.c_void_p), ("p0_b", ctypes.c_void_p), ("p2_w", ctypes.c_void_p),
+                ("p2_b", ctypes.c_void_p), ("p_hidden", ctypes.c_int64), ("mem_w", ctypes.c_void_p),
+                ("mg_w", ctypes.c_void_p), ("mg_b", ctypes.c_void_p), ("jump_s", ctypes.c_void_p),
+                ("mln_w", ctypes.c_void_p), ("mln_b", ctypes.c_void_p), ("mln_eps", ctypes.c_float),
+                ("hln_bf16", ctypes.c_int32), ("mgate_w", ctypes.c_void_p), ("mgate_b", ctypes.c_void_p),
+                ("m0_wb", ctypes.c_void_p), ("m0_b", ctypes.c_void_p), ("m2_wb", ctypes.c_void_p),
+                ("m2_b", ctypes.c_void_p), ("H1", ctypes.c_int64), ("a1_bf16", ctypes.c_int32),
+                ("n_layers", ctypes.c_int32), ("layers", ctypes.c_void_p)]
+
+
+def _composite_ok(mod, x, gpol, tag):
+    from . import probe
+    D = x.shape[-1]
+    H1 = mod.mlp[0].weight.shape[0]
+    return (COMPOSITE and prec.get() == prec.PREC_BF16 and G.use_wide(D) and G.use_wide(H1) and H1 % 4 == 0
+            and G._nj_override is None and not probe.active() and not (tag is not None and decisions.active())
+            and x.is_cuda and gpol.is_contiguous() and gpol.dtype == torch.float32 and x.dtype == torch.float32)
+
+
+def _build_plan(mod, D):
+    dev = mod.mem_w.device
+    st = _S()
+    wide = True
+    store = prec.bf16_storage()
+    keep = []  # every tensor the plan points at (bf16 copies, derived weights): alive while the plan is
+
+    def a(t):
+        if t is None:
+            return None
+        keep.append(t)
+        return t.data_ptr()
+
+    layers = (_Layer * len(mod.layers))()
+    for i, lay in enumerate(mod.layers):
+        vg = lay["v_gate"]
+        Dh, M = vg.mlp[0].weight.shape[0], vg.mkey.shape[0]
+        N = M + Dh
+
+        def build(vg=vg, M=M, Dh=Dh, N=N):  # the same derived entry as forward()
+            Wc, bc, mkn = _E(N, D, device=dev), _E(N, device=dev), _E(M, device=dev)
+            wb = _E(N, D, dtype=torch.int16, device=dev) if wide else None
+            lib.call("asrx_vgate_weights", _P(vg.mkey), _P(vg.mlp[0].weight), _P(vg.mlp[0].bias), _P(Wc), _P(bc),
+                     _P(mkn), _P(wb), M, Dh, D, st)
+            return Wc, bc, mkn, wb
+
+        Wc, bc, mkn, wb = G.derived(("vgate", bool(wide)), build, (vg.mkey, vg.mlp[0].weight, vg.mlp[0].bias))
+        ad = lay["adapter"]
+        ln, gt = lay["ln"], lay["gate"][0]
+        layers[i] = _Layer(a(ln.weight), a(ln.bias), a(gt.weight), a(gt.bias), a(vg.mval), a(vg.mlp[2].weight),
+                           a(vg.mlp[2].bias), a(vg.concat.weight), a(vg.concat.bias), a(vg.tx), a(bc), a(wb),
+                           a(G.weight_bf16(ad.weight)) if ad is not None else None,
+                           a(ad.bias) if ad is not None else None, M, Dh, float(ln.eps),
+                           int(ad is not None and store))
+    net = mod.pnet.net
+    H1 = mod.mlp[0].weight.shape[0]
+    plan = _Plan(a(G.weight_bf16(net[0].weight)), a(net[0].bias), a(net[2].weight), a(net[2].bias),
+                 net[0].weight.shape[0], a(mod.mem_w), a(mod.mem_gate[0].weight), a(mod.mem_gate[0].bias),
+                 a(mod.jump_s), a(mod.mlp_ln.weight), a(mod.mlp_ln.bias), float(mod.mlp_ln.eps), int(store),
+                 a(mod.mlp_gate[0].weight), a(mod.mlp_gate[0].bias), a(G.weight_bf16(mod.mlp[0].weight)),
+                 a(mod.mlp[0].bias), a(G.weight_bf16(mod.mlp[2].weight)), a(mod.mlp[2].bias), H1,
+                 int(store and H1 % 4 == 0), len(mod.layers), ctypes.addressof(layers))
+    return {"plan": plan, "layers": layers, "keep": keep, "ws": {}}
+
+
+def _forward_composite(mod, x0, gpol):
+    B, L, D = x0.shape
+    pl = G.derived(("msheath_plan", id(mod), prec.bf16_storage()), lambda: _build_plan(mod, D), (mod.jump_s,))
+    L_ = lib.load()
+    nb = pl["ws"].get((B, L))
+    if nb is None:
+        nb = pl["ws"][(B, L)] = int(L_.asrx_msheath_fwd_ws_bytes(ctypes.byref(pl["plan"]), B, L, D))
+    ws = _E(nb, dtype=torch.uint8, device=x0.device)
+    y = _E(B, L, D, device=x0.device)
+    lib.call("asrx_msheath_fwd", ctypes.addressof(pl["plan"]), _P(x0), _P(gpol), gpol.stride(0), _P(y), _P(ws), nb,
+             B, L, D, _S())
+    return y
+
+
 def msheath(mod, x, gpol, tag=None):
     """Fused MSheath call.  Without autograd (the reference's dead blocks, eval, decoding) the forward
-    runs without saving anything for a backward.  tag: (noise site key, sid_base) for asrx.decisions."""
+    runs without saving anything for a backward -- from C++ in one call where it can (_forward_composite).
+    tag: (noise site key, sid_base) for asrx.decisions."""
     if not torch.is_grad_enabled():
-        return forward(mod, x if x.is_contiguous() else x.contiguous(), gpol, save=False, tag=tag)[0]
+        x = x if x.is_contiguous() else x.contiguous()
+        if _composite_ok(mod, x, gpol, tag):
+            return _forward_composite(mod, x, gpol)
+        return forward(mod, x, gpol, save=False, tag=tag)[0]
     # the parameter list (~60 nn.Module attribute walks) is made once per module: the module tree is fixed
     params = mod.__dict__.get("_asrx_params")
     if params is None or params[4] is not mod.mem_w or params[7] is not mod.jump_s:  # (replaced parameters)
         params = _params(mod)
         mod.__dict__["_asrx_params"] = params
     if not (x.requires_grad or any(p.requires_grad for p in params)):
-        return forward(mod, x if x.is_contiguous() else x.contiguous(), gpol, save=False, tag=tag)[0]
+        x = x if x.is_contiguous() else x.contiguous()
+        if _composite_ok(mod, x, gpol, tag):
+            return _forward_composite(mod, x, gpol)
+        return forward(mod, x, gpol, save=False, tag=tag)[0]
     return MSheathFn.apply(x, gpol, mod, tag, *params)

@@ -248,9 +248,13 @@ def main():
     # eager launches at every N: the N = 1 point of a 1 -> 8 curve runs the same code path as N > 1, and
     # eager is the faster one (profiles/r05_eager_vs_graph.txt)
     use_graph = args.graph and not args.eager and not distributed
-    side = torch.cuda.Stream()
+    # warm-up on the stream the timed steps run on: the caching allocator keeps freed blocks per stream, so a
+    # warm-up on another stream leaves the first timed steps to allocate (hipMalloc) their whole working set --
+    # ~0.7 s per step of a 3-step medium run (profiles/r06_host_vs_gpu.txt).  A graph capture needs its warm-up
+    # off the default stream, and then captures and replays there too.
+    side = torch.cuda.Stream() if use_graph else torch.cuda.current_stream()
     side.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(side):  # warmup off the default stream (graph-capture requirement)
+    with torch.cuda.stream(side):
         for _ in range(max(args.warmup, 1 if use_graph else 0)):
             step()
     torch.cuda.current_stream().wait_stream(side)

@@ -418,6 +418,47 @@ int asrx_msheath_ctrl_bwd4(const float* part, int64_t L, const float* g_mwo, con
 
 int asrx_msheath_dx_final(float* dx, const float* dorig, const int* has_orig, const float* u, int64_t B, int64_t L,
                           int64_t d, asrx_stream_t stream);
+
+/* ---- MSheath.forward without a backward in ONE call (model.py:429-507; the reference's dead blocks,
+ *      model.py:617-626, eval and decoding): enqueues asrx/msheath.py forward(save=False)'s launches from C++
+ *      -- policy (seg_colsum_det, MPNet GEMM, small_linear softmax), per layer row_tiles, the v_gate projection
+ *      GEMM, msheath_row_fwd2, the adapter GEMM, axpy_row2_colsum, msheath_ctrl_fwd3, jump_axpy_inplace, then
+ *      layernorm_fwd3, the two MLP GEMMs and axpy_row -- bit-identical to issuing them one by one.  bf16 perf
+ *      mode (wide GEMM, bf16 weight copies N x K contiguous).  The plan holds the module's constant addresses
+ *      (parameters, the bf16 copies, v_gate's combined projection from asrx_vgate_weights); x0, y (B, L, D)
+ *      fp32 contiguous and distinct; gpol (B, layers, 3) policy noise with row stride ld_gpol floats; ws: a device
+ *      workspace of asrx_msheath_fwd_ws_bytes(plan, B, L, D) bytes.  The plan and layer structs are HOST memory
+ *      read during the call only. */
+typedef struct asrx_msheath_layer {
+  const float *ln_w, *ln_b, *gate_w, *gate_b, *mval, *vw2, *vb2, *cw, *cb, *tx, *bc;
+  const unsigned short *wcb;   /* bf16 [normalize(mkey); v_gate.mlp[0].weight] (M + Dh, D) */
+  const unsigned short *ad_wb; /* bf16 adapter weight (D, D); NULL on odd layers */
+  const float *ad_b;
+  int64_t M, Dh;
+  float ln_eps;
+  int32_t px_bf16;
+} asrx_msheath_layer;
+typedef struct asrx_msheath_plan {
+  const unsigned short *p0_wb;
+  const float *p0_b, *p2_w, *p2_b;
+  int64_t p_hidden;
+  const float *mem_w, *mg_w, *mg_b, *jump_s, *mln_w, *mln_b;
+  float mln_eps;
+  int32_t hln_bf16;
+  const float *mgate_w, *mgate_b;
+  const unsigned short *m0_wb;
+  const float *m0_b;
+  const unsigned short *m2_wb;
+  const float *m2_b;
+  int64_t H1;
+  int32_t a1_bf16, n_layers;
+  const asrx_msheath_layer* layers;
+} asrx_msheath_plan;
+int64_t asrx_msheath_plan_bytes(void);
+int64_t asrx_msheath_layer_bytes(void);
+int64_t asrx_msheath_fwd_ws_bytes(const asrx_msheath_plan* plan, int64_t B, int64_t L, int64_t D);
+int asrx_msheath_fwd(const asrx_msheath_plan* plan, const float* x0, const float* gpol, int64_t ld_gpol, float* y,
+                     void* ws, int64_t ws_bytes, int64_t B, int64_t L, int64_t D, asrx_stream_t stream);
 /* out = x + s1[r] * s2[r] * y (s2 may be NULL), d % 4 == 0 (model.py:461: x + gate * ion * out). */
 int asrx_axpy_row2(const float* x, const float* s1, const float* s2, const float* y, float* out, int64_t rows,
                    int64_t d, asrx_stream_t stream);

@@ -104,3 +104,21 @@ def test_keyed_noise_index_guards():
         ops._noise_rows_ok(2, 384, 8193)
     with pytest.raises(ValueError, match="32-bit"):
         ops._noise_rows_ok(2000, 1024, 3001)
+
+
+def test_msheath_plan_struct_layout():
+    """The ctypes mirror of asrx_msheath_plan / asrx_msheath_layer (asrx/msheath.py) has the C structs' sizes and
+    the workspace query runs on the host (no GPU): the composite no-save MSheath forward reads them by layout."""
+    import ctypes
+
+    from asrx import lib, msheath
+
+    L = lib.load()
+    assert L.asrx_msheath_plan_bytes() == ctypes.sizeof(msheath._Plan)
+    assert L.asrx_msheath_layer_bytes() == ctypes.sizeof(msheath._Layer)
+    layers = (msheath._Layer * 2)()
+    for i in range(2):
+        layers[i].M, layers[i].Dh = 64, 192
+    plan = msheath._Plan(p_hidden=128, H1=1536, n_layers=2, layers=ctypes.addressof(layers))
+    n = L.asrx_msheath_fwd_ws_bytes(ctypes.byref(plan), 2, 3001, 384)
+    assert n > 4 * 2 * 3001 * 384 * 6  # at least the running x, px, out, hln, hh and SH rows
