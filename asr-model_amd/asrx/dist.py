@@ -36,7 +36,11 @@ Design (MI355X-first, not a translation of DDP's call pattern):
   * BatchNorm running statistics (model.py:103 BatchNorm1d in ConvLite) are training state outside the
     gradient: each rank's forward updates its own, so finish() also averages every floating-point
     running_mean / running_var over the ranks (one small flat all-reduce behind the last bucket) and the
-    replicas' eval-mode outputs stay identical (DDP instead rebroadcasts rank 0's buffers each step).
+    replicas' eval-mode outputs stay identical (DDP instead rebroadcasts rank 0's buffers each step);
+  * opt-in bf16 wire format (comm_dtype=torch.bfloat16): a bucket is rounded to bf16 into its own comm
+    buffer on the comm stream, all-reduced as bf16 (half the bytes over xGMI: medium's ~1 GB of gradient per step
+    becomes ~0.5 GB) and widened back to fp32 before the average.  The gradients stay fp32 everywhere else;
+    the rounding adds ~2^-9 relative error per element and rank (tests/test_dist.py bounds it against fp32).
 """
 from __future__ import annotations
 
@@ -49,7 +53,7 @@ from . import ops
 
 
 class _Bucket:
-    __slots__ = ("params", "buf", "pending", "expected", "work", "launched", "complete", "offsets")
+    __slots__ = ("params", "buf", "pending", "expected", "work", "launched", "complete", "offsets", "cbuf")
 
     def __init__(self, params, device):
         self.params = params
@@ -64,13 +68,19 @@ class _Bucket:
         self.work = None
         self.launched = False
         self.complete = False
+        self.cbuf = None  # bf16 wire copy (GradSync comm_dtype=torch.bfloat16)
 
 
 class GradSync:
     def __init__(self, model: torch.nn.Module, bucket_mb: float = 64.0, group=None, signature=None,
-                 reduce_single: bool = False, first_bucket_mb: float | None = None, cover=None):
+                 reduce_single: bool = False, first_bucket_mb: float | None = None, cover=None,
+                 comm_dtype=torch.float32):
         """cover: the parameters that can receive a gradient (default: model.grad_reachable() if the
-        model declares it, else every requires_grad parameter); each gets a bucket slot from step 1."""
+        model declares it, else every requires_grad parameter); each gets a bucket slot from step 1.
+        comm_dtype: the all-reduce's wire format, torch.float32 (default) or torch.bfloat16 (opt-in)."""
+        if comm_dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError(f"GradSync comm_dtype must be torch.float32 or torch.bfloat16, got {comm_dtype}")
+        self.comm_dtype = comm_dtype
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         # reduce_single: run the bucket all-reduces even in a 1-rank group (exercises the RCCL launch,
@@ -235,9 +245,19 @@ class GradSync:
             ev.record(torch.cuda.current_stream())
             with torch.cuda.stream(self.comm):
                 self.comm.wait_event(ev)
-                b.work = dist.all_reduce(b.buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+                b.work = dist.all_reduce(self._wire(b), op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         else:
-            b.work = dist.all_reduce(b.buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            b.work = dist.all_reduce(self._wire(b), op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+
+    def _wire(self, b: _Bucket):
+        """The tensor the all-reduce moves: the bucket itself, or its bf16 copy (made on the current stream --
+        the comm stream on the GPU -- into a buffer the bucket keeps)."""
+        if self.comm_dtype == torch.float32:
+            return b.buf
+        if b.cbuf is None or b.cbuf.numel() != b.buf.numel():
+            b.cbuf = torch.empty(b.buf.numel(), dtype=self.comm_dtype, device=b.buf.device)
+        b.cbuf.copy_(b.buf)
+        return b.cbuf
 
     def finish(self):
         """Join every bucket's all-reduce and average.  Call after backward, before the optimizer."""
@@ -268,6 +288,8 @@ class GradSync:
                 torch.cuda.current_stream().wait_stream(self.comm)
             inv = 1.0 / self.world
             for b in self.buckets:
+                if b.cbuf is not None and self.comm_dtype != torch.float32:
+                    b.buf.copy_(b.cbuf)  # widen the reduced bf16 sum back into the fp32 gradients
                 b.buf.mul_(inv)
             if stats is not None:
                 self._stat_flat.mul_(inv)

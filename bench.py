@@ -62,6 +62,12 @@ def parse():
                     "work is enqueued (asrx.model.processor.dead_blocks_at; default: the model's)")
     ap.add_argument("--graph-dead", action="store_true", help="replay the dead blocks from HIP graphs "
                     "(asrx.model.processor.graph_dead_blocks; off by default, profiles/r06_host_vs_gpu.txt)")
+    ap.add_argument("--no-pin", action="store_true", help="N > 1: do not pin each rank to its own slice of the CPUs")
+    ap.add_argument("--bf16-grads", action="store_true", help="N > 1: all-reduce the gradient buckets in bf16 "
+                    "(asrx.dist.GradSync comm_dtype; opt-in, fp32 by default)")
+    ap.add_argument("--no-fp32-line", action="store_true", help="skip the side line in the fp32 parity mode "
+                    "(same workload; the mode that meets north_star's parity gate)")
+    ap.add_argument("--fp32-steps", type=int, default=3)
     ap.add_argument("--no-dead-block-line", action="store_true", help="skip the extra measurement with the "
                     "reference's dead decoder blocks eliminated (reported beside, never as, the headline)")
     return ap.parse_args()
@@ -199,6 +205,19 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     if args.same_device:
         local = 0
+    # one issue thread per rank: pin each rank's process (its Python issue thread and the HIP runtime's threads) to its
+    # own contiguous slice of the CPUs this job may use, before anything touches the GPU, so eight ranks' host
+    # issue does not migrate across each other's cores (local ranks map to GPUs in order, and contiguous core
+    # slices keep a rank on one socket when the GPUs are numbered socket by socket)
+    cores = None
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    if world > 1 and not args.no_pin and hasattr(os, "sched_setaffinity"):
+        avail = sorted(os.sched_getaffinity(0))
+        per = len(avail) // max(local_world, 1)
+        slot = int(os.environ.get("LOCAL_RANK", "0"))
+        if per >= 1:
+            cores = avail[slot * per:(slot + 1) * per]
+            os.sched_setaffinity(0, cores)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     distributed = world > 1 or args.dist_single
@@ -225,7 +244,8 @@ def main():
     model.processor.graph_dead_blocks = args.graph_dead
     if distributed:
         broadcast_parameters(model)
-    gsync = GradSync(model, reduce_single=args.dist_single)
+    gsync = GradSync(model, reduce_single=args.dist_single,
+                     comm_dtype=torch.bfloat16 if args.bf16_grads else torch.float32)
     model.set_noise(seed=0, step=rank * 1_000_000)
 
     B = args.batch
@@ -345,6 +365,9 @@ def main():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        core_map = [None] * world
+        dist.all_gather_object(core_map, None if cores is None else f"{cores[0]}-{cores[-1]}" if cores == list(
+            range(cores[0], cores[-1] + 1)) else ",".join(map(str, cores)))
     loss_v = float(loss.item())
 
     audio_s = world * B * CLIP_SECONDS * args.steps
@@ -376,7 +399,8 @@ def main():
                                "host_issue_from_idle_ms is one step issued from an idle GPU (min of 2) beside that "
                                "step's wall time step_from_idle_ms: issue < wall means the GPU is the bound"}
            if free_issue else {}),
-        **({"grad_sync_rel_spread": grad_spread} if distributed else {}),
+        **({"grad_sync_rel_spread": grad_spread, "cpu_affinity_by_rank": core_map,
+            "grad_wire_dtype": "bf16" if args.bf16_grads else "fp32"} if distributed else {}),
         **({"dist_single": "1-rank RCCL group through the N>1 path (eager, bucket all-reduces on the comm "
                            "stream); a rehearsal, not the headline"} if args.dist_single else {}),
         "loss": loss_v,
@@ -523,6 +547,45 @@ def main():
             "note": "reference extract_args workload: pitch at dio's 5 ms frames (essentials.py:451-455), "
                     "the step the reference's own feature path produces; NOT the headline (SURVEY.md §8(d) "
                     "specifies 3001-frame pitch)"}
+    if not args.no_fp32_line and not distributed and args.precision == "bf16":
+        # the fp32 parity mode -- the mode that meets north_star's parity gate (argmax ids
+        # bit-exact, logits within 1e-3 of the reference; tests/test_gpu_model_configs.py) -- on the same config,
+        # batch and clips, timed here so the driver observes it; its GEMMs priced against the fp32 MFMA peak
+        prec.set_precision("fp32")
+        try:
+            step()  # warm-up: fp32 storage allocates a different working set
+            torch.cuda.synchronize()
+            t4 = time.perf_counter()
+            for _ in range(args.fp32_steps):
+                step()
+            torch.cuda.synchronize()
+            el4 = time.perf_counter() - t4
+            f32 = {"value": round(B * CLIP_SECONDS * args.fp32_steps / el4, 3), "unit": "audio-sec/sec",
+                   "ms_per_step": round(el4 / args.fp32_steps * 1e3, 3), "steps": args.fp32_steps, "warmup": 1,
+                   "dtype": "fp32",
+                   "note": "same workload in the fp32 parity mode (exact fp32 MFMA, fp32 storage): the mode gated at "
+                           "north_star's argmax-exact / logits 1e-3 (tests/test_gpu_model_configs.py); NOT the headline"}
+            if not args.no_probe:
+                probe.enable(("gemm", "attn"))
+                model.processor.concurrent_dead_text = model.processor.concurrent_dead_blocks = False
+                step()
+                model.processor.concurrent_dead_text = model.processor.concurrent_dead_blocks = True
+                torch.cuda.synchronize()
+                r4 = probe.disable()
+                n4, _, s4 = probe.summarize(r4["gemm"])
+                fl4 = sum(probe.gemm_flops(tag, w) for w, _, _, tag in r4["gemm"])
+                probe.clear_aux()
+                if s4 > 0:
+                    f32["gemm_all"] = {"bound": "mfma", "achieved": round(fl4 / s4 / 1e12, 2), "peak": F32_PEAK_TFS,
+                                       "unit": "TFLOP/s", "frac": round(fl4 / s4 / 1e12 / F32_PEAK_TFS, 4),
+                                       "launches_per_step": n4, "share_of_step": round(s4 / (el4 / args.fp32_steps), 3)}
+                na, fa, sa = probe.summarize(r4["attn"])
+                if sa > 0:
+                    f32["attn_fwd"] = {"achieved": round(fa / sa / 1e12, 2), "unit": "TFLOP/s", "peak": F32_PEAK_TFS,
+                                       "frac": round(fa / sa / 1e12 / F32_PEAK_TFS, 4)}
+            result["fp32_workload"] = f32
+        finally:
+            prec.set_precision(args.precision)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(model, args.config)
         result["configs0_plumbing"] = plumbing_line(dev)

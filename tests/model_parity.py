@@ -54,6 +54,34 @@ def inputs(B: int, seconds: float, T: int, vocab: int, seed: int = 0, pitch_fram
 _ORACLE_CACHE: dict = {}
 
 
+def record(case: str, precision: str, res: dict, path=None) -> None:
+    """Append one parity case's measured metrics (every scalar / small entry of compare()'s result, the per-
+    parameter gradient table left out) as a JSON line to $ASRX_PARITY_LOG (the GPU suite's collector, e.g.
+    profiles/r06_parity_metrics.jsonl); a no-op when the variable is unset."""
+    import json
+    import os
+
+    path = path or os.environ.get("ASRX_PARITY_LOG")
+    if not path:
+        return
+
+    def clean(v):
+        if isinstance(v, dict):
+            return {str(k): clean(x) for k, x in v.items()}
+        if isinstance(v, (list, tuple)):
+            return [clean(x) for x in v][:64]
+        if isinstance(v, (np.floating, np.integer)):
+            return v.item()
+        if isinstance(v, torch.Tensor):
+            return v.item() if v.numel() == 1 else None
+        return v if isinstance(v, (int, float, str, bool)) or v is None else str(v)
+
+    line = {"case": case, "precision": precision, "time": time.strftime("%Y-%m-%dT%H:%M:%S"),
+            **{k: clean(v) for k, v in res.items() if k != "grads"}}
+    with open(path, "a") as f:
+        f.write(json.dumps(line) + "\n")
+
+
 def _rel_max(a, b):
     return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
 

@@ -239,7 +239,7 @@ def test_gradsync_event_plans_per_signature(sig_override):
         assert all(o[2] for o in out)
 
 
-def _worker_mixed(rank, world, port, q, schedule):
+def _worker_mixed(rank, world, port, q, schedule, comm_dtype=None):
     """Ranks whose step signatures differ IN THE SAME STEP (one rank's batch needs 3 passes of the
     shared weight, the other's 1; one rank knows its signature, the other sees it for the first time):
     both must issue the same all-reduce sequence (next-bucket rule), complete, and end with the
@@ -258,7 +258,7 @@ def _worker_mixed(rank, world, port, q, schedule):
     broadcast_parameters(model)
     twin = ToyVarying()  # local gradients (no hooks)
     twin.load_state_dict(model.state_dict())
-    sync = GradSync(model, bucket_mb=0.0005)
+    sync = GradSync(model, bucket_mb=0.0005, comm_dtype=comm_dtype or torch.float32)
     launches = []
     orig_launch = sync._launch
 
@@ -279,13 +279,21 @@ def _worker_mixed(rank, world, port, q, schedule):
         synced = {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None}
         twin.zero_grad(set_to_none=True)
         (twin(x).pow(2).sum() * (rank + 1)).backward()
-        avg = {}
+        avg, absavg = {}, {}
         for n, p in twin.named_parameters():
             t = p.grad.clone()
             dist.all_reduce(t)
             avg[n] = t / world
-        ok = set(synced) == set(avg) and all(torch.allclose(synced[n], avg[n], atol=1e-5) for n in avg)
-        out.append((passes_by_rank[rank], overlapped, ok, list(launches[-1]), len(sync.buckets)))
+            a = p.grad.abs()
+            dist.all_reduce(a)
+            absavg[n] = a / world
+        if comm_dtype is None:
+            ok = set(synced) == set(avg) and all(torch.allclose(synced[n], avg[n], atol=1e-5) for n in avg)
+            rel = 0.0
+        else:  # bf16 wire: one rounding per rank's bucket plus the bf16 sum's, each ~2^-9 of the magnitudes
+            rel = max(float(((synced[n] - avg[n]).abs() / (absavg[n] + 1e-12)).max()) for n in avg)
+            ok = set(synced) == set(avg) and rel <= world * 2.0 ** -8
+        out.append((passes_by_rank[rank], overlapped, ok, list(launches[-1]), len(sync.buckets), rel))
     q.put((rank, out))
     dist.barrier()
     dist.destroy_process_group()
@@ -309,7 +317,7 @@ def test_gradsync_ranks_with_different_signatures_same_step():
         p.join(timeout=60)
         assert p.exitcode == 0
     for r in (0, 1):
-        for step, (passes, overlapped, ok, order, nb) in enumerate(res[r]):
+        for step, (passes, overlapped, ok, order, nb, _) in enumerate(res[r]):
             assert ok, (r, step, res[r])
             assert order == list(range(nb)), (r, step, order)  # every rank: index order, every bucket
     # a rank that knows its signature launches from backward even when the other rank does not
@@ -317,6 +325,58 @@ def test_gradsync_ranks_with_different_signatures_same_step():
     assert res[0][2][1] > 0 and res[1][2][1] == 0, res
     assert res[0][3][1] > 0 and res[1][3][1] > 0, res
     assert res[0][4][1] == 0 and res[1][4][1] == 0, res
+
+
+def _run_mixed(world, schedule, comm_dtype=None):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_mixed, args=(r, world, port, q, schedule, comm_dtype)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, out = q.get(timeout=180)
+        res[r] = out
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+def test_gradsync_world4_mixed_signatures():
+    """Four ranks, each step a different mix of known and new step signatures across the ranks (the 8-GPU run
+    pads every rank's batch to its own maximum, so signatures differ between ranks in one step): every rank issues
+    every bucket's all-reduce in index order, the steps complete and every rank ends with the average of the four
+    local gradients; a rank that knows its signature overlaps even when the others do not."""
+    schedule = [(1, 1, 1, 1), (3, 1, 2, 1), (1, 3, 2, 2), (3, 1, 2, 1), (2, 2, 3, 3), (1, 3, 2, 2)]
+    res = _run_mixed(4, schedule)
+    for r in range(4):
+        for step, (passes, overlapped, ok, order, nb, _) in enumerate(res[r]):
+            assert ok, (r, step, res[r])
+            assert order == list(range(nb)), (r, step, order)
+    # a rank launches from the backward hooks exactly when it has seen its own signature before, whatever the other
+    # ranks' signatures are in that step
+    for r in range(4):
+        seen = set()
+        for step, passes in enumerate(p[r] for p in schedule):
+            assert (res[r][step][1] > 0) == (passes in seen), (r, step, res[r])
+            seen.add(passes)
+
+
+def test_gradsync_bf16_wire_error_bounded():
+    """comm_dtype=torch.bfloat16 (the opt-in bf16 all-reduce): the averaged gradients stay within world x 2^-8 of
+    the fp32 average relative to the ranks' mean |g| per element, and differ from it (the wire format is used)."""
+    schedule = [(1, 1, 1, 1), (3, 1, 2, 1), (3, 1, 2, 1)]
+    res = _run_mixed(4, schedule, torch.bfloat16)
+    rels = []
+    for r in range(4):
+        for step, (passes, overlapped, ok, order, nb, rel) in enumerate(res[r]):
+            assert ok, (r, step, rel)
+            assert order == list(range(nb))
+            rels.append(rel)
+    assert max(rels) > 0.0  # bf16 rounding happened
+    print("bf16 wire, worst relative error:", max(rels))
 
 
 def test_stream_grouping_signature():

@@ -80,6 +80,7 @@ def _case(name, precision, grads, **kw):  # noqa: D103
     pf = CASES[name][4] if len(CASES[name]) > 4 else None
     r = mp.compare(CONFIGS[cfg], B=B, seconds=sec, T=T, precision=precision, grads=grads, pitch_frames=pf, **kw)
     print(name, precision, {k: v for k, v in r.items() if k != "grads"})
+    mp.record(name + "".join(f"+{k}" for k in sorted(kw) if k in ("decisions", "bf16_stability")), precision, r)
     return r
 
 
@@ -190,6 +191,7 @@ def test_hip_mel_end_to_end(cuda):
     r = mp.compare(CONFIGS["tiny"], B=1, seconds=10.0, T=64, precision="fp32", grads=True, replay=True,
                    hip_mel=True, yardstick=True)
     print({k: v for k, v in r.items() if k != "grads"})
+    mp.record("tiny_10s_hip_mel", "fp32", r)
     assert r["replayed"] > 0
     # the HIP mel differs from the float64 mel by ~1e-4 (log10 via log2, fp32 FFT): an input perturbation
     # on top of the fp32 arithmetic, hence 3x the fp32-config bound
