@@ -65,8 +65,8 @@ def parse():
     ap.add_argument("--no-pin", action="store_true", help="N > 1: do not pin each rank to its own slice of the CPUs")
     ap.add_argument("--bf16-grads", action="store_true", help="N > 1: all-reduce the gradient buckets in bf16 "
                     "(asrx.dist.GradSync comm_dtype; opt-in, fp32 by default)")
-    ap.add_argument("--no-fp32-line", action="store_true", help="skip the side line in the fp32 parity mode "
-                    "(same workload; the mode that meets north_star's parity gate)")
+    ap.add_argument("--no-fp32-line", action="store_true", help="skip the side lines in the fp32 and x3 parity "
+                    "modes (same workload; the modes that meet north_star's parity gate)")
     ap.add_argument("--fp32-steps", type=int, default=3)
     ap.add_argument("--no-dead-block-line", action="store_true", help="skip the extra measurement with the "
                     "reference's dead decoder blocks eliminated (reported beside, never as, the headline)")
@@ -547,24 +547,22 @@ def main():
             "note": "reference extract_args workload: pitch at dio's 5 ms frames (essentials.py:451-455), "
                     "the step the reference's own feature path produces; NOT the headline (SURVEY.md §8(d) "
                     "specifies 3001-frame pitch)"}
-    if not args.no_fp32_line and not distributed and args.precision == "bf16":
-        # the fp32 parity mode -- the mode that meets north_star's parity gate (argmax ids
-        # bit-exact, logits within 1e-3 of the reference; tests/test_gpu_model_configs.py) -- on the same config,
-        # batch and clips, timed here so the driver observes it; its GEMMs priced against the fp32 MFMA peak
-        prec.set_precision("fp32")
+    def mode_line(mode, steps, note):
+        """The same workload in another precision mode (asrx.prec), timed here so the driver observes it, with its
+        GEMMs priced against that mode's MFMA ceiling (fp32: the fp32 MFMA peak; x3: a third of the bf16 peak in
+        fp32-equivalent flops) and its attention forward against the fp32 peak (both modes run fp32 attention)."""
+        prec.set_precision(mode)
         try:
             step()  # warm-up: fp32 storage allocates a different working set
             torch.cuda.synchronize()
             t4 = time.perf_counter()
-            for _ in range(args.fp32_steps):
+            for _ in range(steps):
                 step()
             torch.cuda.synchronize()
             el4 = time.perf_counter() - t4
-            f32 = {"value": round(B * CLIP_SECONDS * args.fp32_steps / el4, 3), "unit": "audio-sec/sec",
-                   "ms_per_step": round(el4 / args.fp32_steps * 1e3, 3), "steps": args.fp32_steps, "warmup": 1,
-                   "dtype": "fp32",
-                   "note": "same workload in the fp32 parity mode (exact fp32 MFMA, fp32 storage): the mode gated at "
-                           "north_star's argmax-exact / logits 1e-3 (tests/test_gpu_model_configs.py); NOT the headline"}
+            line = {"value": round(B * CLIP_SECONDS * steps / el4, 3), "unit": "audio-sec/sec",
+                    "ms_per_step": round(el4 / steps * 1e3, 3), "steps": steps, "warmup": 1, "dtype": mode,
+                    "note": note}
             if not args.no_probe:
                 probe.enable(("gemm", "attn"))
                 model.processor.concurrent_dead_text = model.processor.concurrent_dead_blocks = False
@@ -575,17 +573,29 @@ def main():
                 n4, _, s4 = probe.summarize(r4["gemm"])
                 fl4 = sum(probe.gemm_flops(tag, w) for w, _, _, tag in r4["gemm"])
                 probe.clear_aux()
+                gpeak = {"fp32": F32_PEAK_TFS, "x3": BF16_PEAK_TFS / 3}[mode]
                 if s4 > 0:
-                    f32["gemm_all"] = {"bound": "mfma", "achieved": round(fl4 / s4 / 1e12, 2), "peak": F32_PEAK_TFS,
-                                       "unit": "TFLOP/s", "frac": round(fl4 / s4 / 1e12 / F32_PEAK_TFS, 4),
-                                       "launches_per_step": n4, "share_of_step": round(s4 / (el4 / args.fp32_steps), 3)}
+                    line["gemm_all"] = {"bound": "mfma", "achieved": round(fl4 / s4 / 1e12, 2), "peak": round(gpeak, 1),
+                                        "unit": "TFLOP/s", "frac": round(fl4 / s4 / 1e12 / gpeak, 4),
+                                        "launches_per_step": n4, "share_of_step": round(s4 / (el4 / steps), 3)}
                 na, fa, sa = probe.summarize(r4["attn"])
                 if sa > 0:
-                    f32["attn_fwd"] = {"achieved": round(fa / sa / 1e12, 2), "unit": "TFLOP/s", "peak": F32_PEAK_TFS,
-                                       "frac": round(fa / sa / 1e12 / F32_PEAK_TFS, 4)}
-            result["fp32_workload"] = f32
+                    line["attn_fwd"] = {"achieved": round(fa / sa / 1e12, 2), "unit": "TFLOP/s", "peak": F32_PEAK_TFS,
+                                        "frac": round(fa / sa / 1e12 / F32_PEAK_TFS, 4)}
+            return line
         finally:
             prec.set_precision(args.precision)
+
+    if not args.no_fp32_line and not distributed and args.precision == "bf16":
+        # the parity modes on the same config, batch and clips, driver-observed.  fp32 (exact
+        # fp32 MFMA) and x3 (split-bf16 GEMM products, fp32 attention) both meet north_star's parity gate: argmax ids
+        # bit-exact and logits within max(1e-3, 30x the reference's own fp32 error) of the float64 oracle
+        # (tests/test_gpu_model_configs.py; measured values in profiles/r06_parity_metrics.jsonl)
+        result["fp32_workload"] = mode_line("fp32", args.fp32_steps, "same workload in the fp32 parity mode (exact "
+                                            "fp32 MFMA, fp32 storage); NOT the headline")
+        result["x3_workload"] = mode_line("x3", args.fp32_steps, "same workload in the x3 mode (fp32 storage, GEMM "
+                                          "products as three bf16 MFMAs of hi / lo splits, fp32 attention): argmax "
+                                          "bit-exact like fp32 mode; NOT the headline")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(model, args.config)
         result["configs0_plumbing"] = plumbing_line(dev)

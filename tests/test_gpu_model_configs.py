@@ -101,18 +101,21 @@ def test_model_parity_fp32_configs(cuda, name):
 # x3 (split-bf16 GEMM products, fp32 storage, fp32 attention; asrx.prec "x3"): the gradient mode that follows
 # the reference.  tools/bf16_sensitivity.py x3 (profiles/r05_split_bf16_sensitivity.txt): the float64 oracle
 # with every GEMM / attention operand rounded to a bf16 hi + lo pair keeps whole-gradient cosine 0.993 with
-# float64 (one bf16 rounding: 0.35; weights nudged at 2^-17: 0.999), so the whole gradient is gated at 0.99,
-# the forward at the fp32 gates scaled by the operand precision (2^-16 vs fp32's 2^-24 relative per operand).
+# float64 (one bf16 rounding: 0.35; weights nudged at 2^-17: 0.999), so the whole gradient is gated at 0.99.
+# The forward meets north_star's gate the way fp32 mode does (round 6, profiles/r06_parity_metrics.jsonl): argmax
+# ids bit-exact in every case, logits within max(1e-3, YARD_FACTOR x the reference's own fp32 error) -- measured
+# 3.6e-3 at tiny_full (yardstick 1.4e-4: 30x = 4.2e-3), 4.6e-4 tiny_b2, 2.2e-4 refmain, 5.4e-6 small -- and the
+# loss within 2.5e-5.
 X3_GRAD_COS = 0.99
 
 
 @pytest.mark.parametrize("name", ["tiny_full", "tiny_b2", "refmain", "small"])
 def test_model_parity_x3_configs(cuda, name):
-    r = _case(name, "x3", True, replay=True)
+    r = _case(name, "x3", True, replay=True, yardstick=True)
     assert r["replayed"] > 0
-    assert r["argmax"] >= 0.99, r["argmax"]
-    assert r["logits_max"] < 2e-2, r["logits_max"]
-    assert r["loss"] < 1e-3, r["loss"]
+    assert r["argmax"] == 1.0, r["argmax"]
+    assert r["logits_max"] < max(1e-3, YARD_FACTOR * r["yard_logits"]), (r["logits_max"], r["yard_logits"])
+    assert r["loss"] < 1e-4, r["loss"]
     assert not r["grads_missing"], r["grads_missing"]
     assert r["grads_cos"] > X3_GRAD_COS, r["grads_cos"]
 
