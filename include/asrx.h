@@ -28,9 +28,12 @@ uint32_t asrx_noise_hash(uint32_t key, uint32_t idx);
  * of a training step draws fresh dropout masks / gumbel noise per replay (the reference draws fresh
  * noise every step, essentials.py:751-824); 0 (default) = the keys of oracle/keys.py. */
 int asrx_set_noise_epoch(uint32_t epoch, asrx_stream_t stream);
-/* Wide-GEMM kernel selection for the plain / residual activation x weight products (host state, not
- * stream-ordered): 1 (default) the two-workgroups-per-CU kernel, 0 the one-workgroup-per-CU kernel.
- * Same results bit for bit; an A/B switch for measurements and tests.  Returns the previous value. */
+/* Wide-GEMM kernel selection for the activation x weight products (host state, not stream-ordered), a bit set:
+ * low two bits 0 = gemm_wr_kernel (one workgroup per CU) only, 1 = gemm_p2_kernel (two per CU) for 384- and
+ * 256-column tiles, 2 = also for 128-column tiles; + 4 the weight-stationary gemm_ws_kernel first where it measured
+ * faster, + 8 gemm_ws on every shape it can run (tests), + 16 the d = 64 AbbyNormal router on gemm_wr_kernel instead
+ * of router64_kernel.  Default 5 (gemm_p2 + gemm_ws).  Same results bit for bit in every setting; an A/B switch for
+ * measurements and tests.  Returns the previous value. */
 int asrx_set_gemm_variant(int variant);
 /* Attention forward kernel selection at head dim 64 (host state): 1 (default) the software-pipelined kernel
  * (scores of the next key tile computed beside this tile's softmax), 0 the round-4 kernel.  Same results bit

@@ -1,5 +1,6 @@
 """Launches and kernel time per headline step from a rocprofv3 kernel trace of tools/gpu_prof.sh: the
-trace is split at each step's log-mel tile launch; the last three segments are the graph replays.
+trace is split at each step's log-mel tile launch; the last three segments are the timed steps (eager launches
+since round 5; graph replays before, and with bench.py --graph).
 usage: replay_step.py run_kernel_trace.csv [tag]"""
 import collections
 import csv
@@ -14,8 +15,8 @@ for r in rows:
         segs.append(cur)
     if cur is not None:
         cur.append(r)
-print(f"rocprofv3 kernel trace of tools/gpu_prof.sh {tag} (2 eager warm-ups + 3 graph replays of the headline step);")
-print("per-step numbers below are the mean of the 3 replays (segments start at each step's logmel_tiles launch)")
+print(f"rocprofv3 kernel trace of tools/gpu_prof.sh {tag} (2 warm-ups + 3 timed steps of the headline step);")
+print("per-step numbers below are the mean of the 3 timed steps (segments start at each step's logmel_tiles launch)")
 for s in segs:
     print("segment launches", len(s))
 rep = segs[-3:]
