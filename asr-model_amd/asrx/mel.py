@@ -135,6 +135,17 @@ def algorithmic_bytes(B: int, N: int, pool: bool) -> float:
     return float(B * (N * 4 + N_MELS * F * 4 + ((N // HOP) * 4 if pool else 0)))
 
 
+def algorithmic_flops(B: int, N: int) -> float:
+    """fp32 flops of the log-mel per batch, counted for the textbook algorithm the kernel implements: per frame the
+    Hann window (1024 mul), the 1024-point real FFT as a 512-point complex FFT (5 n log2 n = 23040) plus the real
+    untangle (~10 per bin, 5120), the power (3 per bin, 1539), the 128-band HTK filterbank (one multiply-add per
+    tap, every bin in at most two bands: 2052) and the log / scale (~3 per band): 33159 per frame.  At ~29 flop per
+    algorithmic HBM byte the kernel sits right of the fp32 ridge (157 TF/s / 8 TB/s = 19.7 flop/B): its binding
+    roofline is the fp32 vector rate, not HBM."""
+    per_frame = 1024 + 5 * 512 * 9 + 10 * 512 + 3 * 513 + 2 * 1026 + 3 * N_MELS
+    return float(B * n_frames(N) * per_frame)
+
+
 def logmel(wav: torch.Tensor, layout: str = "BFM", pool: bool = False):
     """Batched log-mel of (B, N) float32 device audio.
 

@@ -232,7 +232,7 @@ def main():
     from asrx import prec, probe, synth
     from asrx.config import CONFIGS
     from asrx.dist import GradSync, broadcast_parameters
-    from asrx.mel import algorithmic_bytes, logmel
+    from asrx.mel import algorithmic_bytes, algorithmic_flops, logmel
     from asrx.model import Model
 
     prec.set_precision(args.precision)
@@ -464,11 +464,17 @@ def main():
         n2, byts, sec2 = probe.summarize(recs["logmel"])
         if sec2 > 0:
             gbs = byts / sec2 / 1e9
+            mfl = algorithmic_flops(B, wav.shape[1]) * n2  # one probe record per asrx_logmel call
             result["mel_roofline"] = {"kernel": "asrx_logmel (frames + finalize)", "bound": "hbm",
                                       "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                       "frac": round(gbs / HBM_PEAK_GBS, 4),
                                       "algorithmic_bytes": algorithmic_bytes(B, wav.shape[1], True),
-                                      "avg_us": round(sec2 / n2 * 1e6, 1)}
+                                      "avg_us": round(sec2 / n2 * 1e6, 1),
+                                      # the same launches against the fp32 vector roofline (the binding one:
+                                      # 33 kflop per 1.15 KB frame, right of the ridge; asrx.mel.algorithmic_flops)
+                                      "valu_achieved_tflops": round(mfl / sec2 / 1e12, 2), "valu_peak": F32_PEAK_TFS,
+                                      "valu_frac": round(mfl / sec2 / 1e12 / F32_PEAK_TFS, 4),
+                                      "algorithmic_flops": algorithmic_flops(B, wav.shape[1])}
         n3, af, sec3 = probe.summarize(recs["attn"])
         if sec3 > 0:
             result["attn_fwd"] = {"achieved": round(af / sec3 / 1e12, 2), "unit": "TFLOP/s", "peak": apeak,
