@@ -109,6 +109,11 @@ class GradSync:
         self._reset_step()
         self._listener = weakref.WeakMethod(self._ready)
         ops.GRAD_LISTENERS.append(self._listener)
+        # per step: how many buckets the backward hooks launched and how many were left to finish() (a bucket whose
+        # learned plan has no event holds back every later bucket under the next-bucket rule) -- the
+        # last step's counts, and per known signature the largest number its overlapped steps left to finish()
+        self.last_overlap = None
+        self.left_to_finish: dict = {}
         self._stat_bufs = [b for n, b in model.named_buffers()
                            if b.is_floating_point() and n.rsplit(".", 1)[-1] in ("running_mean", "running_var")]
         self._stat_flat = None
@@ -276,9 +281,16 @@ class GradSync:
                     merged[i] = max(n, merged.get(i, 0))
                 self._learn(self._sig, merged)
         if self.active:
+            hooked = self._next
             for b in self.buckets[self._next:]:  # the rest, in index order
                 self._launch(b)
             self._next = len(self.buckets)
+            zero = [i for i, b in enumerate(self.buckets) if self._overlap and b.expected == 0]
+            self.last_overlap = {"buckets": len(self.buckets), "from_hooks": hooked,
+                                 "from_finish": len(self.buckets) - hooked, "overlap": self._overlap,
+                                 "first_zero_plan_bucket": zero[0] if zero else None}
+            if self._overlap:  # (a first sighting launches everything from finish() by design)
+                self.left_to_finish[self._sig] = max(self.left_to_finish.get(self._sig, 0), len(self.buckets) - hooked)
             stats = self._launch_stats()
             for b in self.buckets:
                 b.work.wait()
@@ -318,6 +330,17 @@ class GradSync:
             h.remove()
         if self._listener in ops.GRAD_LISTENERS:
             ops.GRAD_LISTENERS.remove(self._listener)
+
+
+def rank_cores(avail, slot: int, local_world: int):
+    """The CPUs one local rank pins its process to: the slot-th of local_world contiguous, equal slices of the
+    sorted usable CPUs (a contiguous slice keeps a rank on one socket when GPUs are numbered socket by socket);
+    None when there are fewer CPUs than ranks (no pinning)."""
+    avail = sorted(avail)
+    per = len(avail) // max(int(local_world), 1)
+    if per < 1 or not 0 <= slot < local_world:
+        return None
+    return avail[slot * per:(slot + 1) * per]
 
 
 def broadcast_parameters(model: torch.nn.Module, src: int = 0):

@@ -212,11 +212,9 @@ def main():
     cores = None
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
     if world > 1 and not args.no_pin and hasattr(os, "sched_setaffinity"):
-        avail = sorted(os.sched_getaffinity(0))
-        per = len(avail) // max(local_world, 1)
-        slot = int(os.environ.get("LOCAL_RANK", "0"))
-        if per >= 1:
-            cores = avail[slot * per:(slot + 1) * per]
+        from asrx.dist import rank_cores  # (no GPU touched by the import)
+        cores = rank_cores(os.sched_getaffinity(0), int(os.environ.get("LOCAL_RANK", "0")), local_world)
+        if cores:
             os.sched_setaffinity(0, cores)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)

@@ -616,3 +616,100 @@ def test_gradsync_batchnorm_running_stats_synced():
     assert torch.equal(m0, m1) and torch.equal(v0, v1)
     assert torch.allclose(m0, tm, atol=1e-6) and torch.allclose(v0, tv, atol=1e-6)
     assert float(m0.abs().max()) > 0  # the stats did move
+
+
+class ToyMid(torch.nn.Module):
+    """`mid` sits between `a` and `c` in the backward order; a step signature that leaves it unused gives its bucket
+    no event in that signature's plan."""
+
+    def __init__(self):
+        super().__init__()
+        self.a = torch.nn.Linear(16, 16)
+        self.mid = torch.nn.Linear(16, 16)
+        self.c = torch.nn.Linear(16, 4)
+        self.use_mid = True
+
+    def forward(self, x):
+        self.grad_signature = ("mid", self.use_mid)
+        h = torch.tanh(self.a(x))
+        if self.use_mid:
+            h = h + torch.tanh(self.mid(h))
+        return self.c(h)
+
+
+def _worker_mid(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "asr-model_amd")]
+    from asrx.dist import GradSync, broadcast_parameters
+
+    torch.manual_seed(rank)
+    model = ToyMid()
+    broadcast_parameters(model)
+    sync = GradSync(model, bucket_mb=0.0005)
+    out = []
+    for step, use in enumerate([True, False, False, True]):
+        model.use_mid = use
+        sync.zero_grad()
+        x = torch.randn(5, 16, generator=torch.Generator().manual_seed(100 * step + rank))
+        model(x).pow(2).sum().backward()
+        sync.finish()
+        pos = {n: sync.buckets.index(sync.where[id(p)][0]) for n, p in model.named_parameters()}
+        out.append((use, dict(sync.last_overlap), pos["mid.weight"], pos["mid.bias"]))
+    q.put((rank, out, dict((str(k), v) for k, v in sync.left_to_finish.items())))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gradsync_zero_plan_bucket_holds_back_later_buckets():
+    """under a known signature whose plan gives a mid-layout bucket no event, that bucket is not
+    launched from the hooks (a parameter of it could still take a first gradient) and, by the next-bucket rule, holds
+    back every later bucket until finish().  GradSync reports it per step (last_overlap) and per signature
+    (left_to_finish), and the loss is bounded by the buckets from the first zero-plan bucket on."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_mid, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r, out, left = q.get(timeout=120)
+        res[r] = (out, left)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in (0, 1):
+        out, left = res[r]
+        use, st, mid_w, mid_b = out[2]  # signature (mid, False) known since step 1: overlap engaged
+        assert st["overlap"] and st["first_zero_plan_bucket"] is not None, st
+        z = st["first_zero_plan_bucket"]
+        assert min(mid_w, mid_b) >= z  # mid's buckets are the zero-plan ones
+        assert st["from_finish"] == st["buckets"] - z, st  # exactly the buckets from the first zero-plan one on
+        assert st["from_hooks"] == z, st
+        use, st3, _, _ = out[3]  # (mid, True) was learned on step 0: every bucket from the hooks
+        assert st3["overlap"] and st3["from_finish"] == 0, st3
+        assert left["('mid', False)"] == st["buckets"] - z
+
+
+def test_rank_cores_partition():
+    """bench.py's per-rank pinning (asrx.dist.rank_cores): disjoint, equal, contiguous slices covering the usable
+    CPUs in order; no pinning with fewer CPUs than ranks."""
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "asr-model_amd")]
+    from asrx.dist import rank_cores
+
+    avail = set(range(256))
+    slices = [rank_cores(avail, r, 8) for r in range(8)]
+    assert [s[0] for s in slices] == list(range(0, 256, 32)) and all(len(s) == 32 for s in slices)
+    assert sorted(c for s in slices for c in s) == list(range(256))
+    odd = {3, 5, 7, 9, 11, 13, 15}  # a restricted, non-contiguous affinity set: slices of the sorted list
+    assert rank_cores(odd, 0, 2) == [3, 5, 7] and rank_cores(odd, 1, 2) == [9, 11, 13]
+    assert rank_cores({0, 1, 2}, 0, 8) is None
+    assert rank_cores(avail, 8, 8) is None
