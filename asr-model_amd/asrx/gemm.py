@@ -205,14 +205,22 @@ def weight_bf16(W, trans=False, cache=True):
 _nj_override = None
 
 
+# Minimum tile counts (in 128 x 128 nj units) for the 384- and 256-column tile widths.  Large activations (the audio
+# side, >= 16384 rows): the widest width that still gives >= 200 tiles.  Below that (the text side's 2048-8192-row
+# launches) a wider tile wins with fewer tiles: nj = 3 from 180, nj = 2 from 144 (profiles/r06_small_m_nj_sweep_*.txt:
+# 45 text-side shapes, 1099 -> ~1025 us summed, e.g. 2048 x 3072 x 1024 37.0 -> 26.5 us, 8192 x 768 x 384 18.8 ->
+# 14.7 us).  Every tile width runs the same k order per output element, so the products are bit-identical.
+NJ_MIN_TILES = {"large": (200, 200), "small": (180, 144)}
+
+
 def _nj(M, N):
-    """Tile width 128*nj of the persistent wide GEMM: the widest that still gives >= 200 tiles
-    (most of the 256 CUs busy); narrow tiles run two workgroups per CU."""
+    """Tile width 128*nj of the persistent wide GEMM (NJ_MIN_TILES); narrow tiles run two workgroups per CU."""
     if _nj_override:
         return _nj_override
     tm = (M + 127) // 128
-    for nj in (3, 2):
-        if 128 * nj <= ((N + 127) // 128) * 128 and tm * ((N + 128 * nj - 1) // (128 * nj)) >= 200:
+    t3, t2 = NJ_MIN_TILES["large" if M >= 16384 else "small"]
+    for nj, th in ((3, t3), (2, t2)):
+        if 128 * nj <= ((N + 127) // 128) * 128 and tm * ((N + 128 * nj - 1) // (128 * nj)) >= th:
             return nj
     return 1
 

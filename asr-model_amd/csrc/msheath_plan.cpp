@@ -4,7 +4,8 @@
 // sequence of asrx/msheath.py forward(save=False), entry point for entry point, so the results are
 // bit-identical.  A call that runs eagerly from Python costs ~7 Python-side launches of ~30 us of host time
 // per layer; the dead blocks (model.py:617-626) and decoding run ~5700 such layers per medium-config step
-// (profiles/r06_medium_b8_kernel_stats.csv), which made the medium step's host issue (~2 s) its bound.
+// (profiles/r06_medium_b8_kernel_stats.csv).  (The steps turned out GPU-bound: the host time saved here is now spent
+// waiting on full GPU queues, profiles/r06_host_vs_gpu.txt.)
 //
 // The per-module constants (parameter addresses, the bf16 weight copies, v_gate's combined projection) arrive as
 // an asrx_msheath_plan the caller builds once per step and stream; the per-call buffers are carved from one
@@ -93,11 +94,15 @@ struct asrx_msheath_plan {
 
 namespace {
 
-// asrx/gemm.py _nj: the widest 128 * nj tile that still gives >= 200 tiles
+// asrx/gemm.py _nj (NJ_MIN_TILES): the widest 128 * nj tile with enough tiles -- 200 for either width at >= 16384
+// rows, 180 (nj 3) / 144 (nj 2) below
 int wide_nj(int64_t M, int64_t N) {
   const int64_t tm = (M + 127) / 128;
-  for (int nj = 3; nj >= 2; --nj)
-    if (128 * nj <= ((N + 127) / 128) * 128 && tm * ((N + 128 * nj - 1) / (128 * nj)) >= 200) return nj;
+  const bool large = M >= 16384;
+  for (int nj = 3; nj >= 2; --nj) {
+    const int64_t th = large ? 200 : (nj == 3 ? 180 : 144);
+    if (128 * nj <= ((N + 127) / 128) * 128 && tm * ((N + 128 * nj - 1) / (128 * nj)) >= th) return nj;
+  }
   return 1;
 }
 
