@@ -225,13 +225,33 @@ def _nj(M, N):
     return 1
 
 
+# Plain bf16-activation products go to the vendor library (hipBLASLt, asrx_gemm_lt) where it measured faster than the
+# wide GEMM: K >= 768 at >= 16384 rows, 25-40 % (profiles/r06_blaslt_vs_wide.txt); every fused epilogue, fp32
+# activations, row-tile lists and K = 384 stay on the hand-written kernels.  False: the wide GEMM everywhere.
+LIBRARY_GEMM = __import__("os").environ.get("ASRX_LIBRARY_GEMM", "1") != "0"
+LIB_MIN_K, LIB_MIN_M = 768, 16384
+
+
+def _lib_ok(A, Wb, C, M, N, K, lda, ldc, Z, act, conv, mtiles, beta):
+    return (LIBRARY_GEMM and is_bf16(A) and not conv and mtiles is None and act == "none" and Z is None
+            and K >= LIB_MIN_K and M >= LIB_MIN_M and (beta == 0.0 or not is_bf16(C))
+            and A.data_ptr() % 16 == 0 and Wb.data_ptr() % 16 == 0 and C.data_ptr() % 16 == 0)
+
+
 def gemm_wn(A, Wb, C, *, M, N, K, lda, ldc, bias=None, Z=None, alpha=1.0, beta=0.0, act="none",
             conv=False, conv_F=0, conv_C=0, mtiles=None):
     """C = act(alpha A Wb^T + beta C + bias); Wb bf16 (N, K) from weight_bf16.  A and C are stored fp32
-    or bf16 (their dtype; a bf16 C takes beta = 0); mtiles: only these 128-row tiles (row_tiles)."""
+    or bf16 (their dtype; a bf16 C takes beta = 0); mtiles: only these 128-row tiles (row_tiles).  Plain
+    bf16-A products at the library's shapes run on hipBLASLt (LIBRARY_GEMM)."""
     lib.require_gpu(A, Wb, C)
-    nj = _nj(M, N)
     ab, cb = int(is_bf16(A)), int(is_bf16(C))
+    if _lib_ok(A, Wb, C, M, N, K, lda, ldc, Z, act, conv, mtiles, beta):
+        e0 = probe.begin("gemm")
+        lib.call("asrx_gemm_lt", lib.ptr(A), lda, lib.ptr(Wb), Wb.stride(0), lib.ptr(C), cb, ldc, lib.ptr(bias), M, N,
+                 K, float(alpha), float(beta), lib.stream())
+        probe.end("gemm", e0, 2.0 * M * N * K, ("lt", M, N, K, cb, beta != 0))
+        return C
+    nj = _nj(M, N)
     e0 = probe.begin("gemm")
     lib.call("asrx_gemm_wn_ex", lib.ptr(A), ab, lda, int(conv), conv_F, conv_C, lib.ptr(Wb), Wb.stride(0),
              lib.ptr(C), cb, ldc, lib.ptr(bias), lib.ptr(Z), M, N, K, float(alpha), float(beta), ACT[act], nj,

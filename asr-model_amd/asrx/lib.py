@@ -197,6 +197,7 @@ SIGNATURES = {
     "asrx_msheath_layer_bytes": (_i64, []),
     "asrx_msheath_fwd_ws_bytes": (_i64, [_p, _i64, _i64, _i64]),
     "asrx_msheath_fwd": (_i32, [_p, _p, _p, _i64, _p, _p, _i64, _i64, _i64, _i64, _p]),
+    "asrx_gemm_lt": (_i32, [_p, _i64, _p, _i64, _p, _i32, _i64, _p, _i64, _i64, _i64, _f32, _f32, _p]),
 }
 
 _lib = None

@@ -594,6 +594,13 @@ int asrx_gemm_wn_gact(const void* A, int a_bf16, int64_t lda, const unsigned sho
 int asrx_gemm_wn_rot(const void* A, int a_bf16, int64_t lda, const unsigned short* W, int64_t ldw, float* C, float* Z,
                      int64_t ldc, const float* bias, const float* m, const float* tab, int64_t L, int64_t hd,
                      float scale, int64_t M, int64_t N, int64_t K, int nj, asrx_stream_t stream);
+/* Plain bf16 product on the vendor GEMM library (hipBLASLt; round 6): Y (M x N, ldc; fp32, or bf16 with c_bf16) =
+ * alpha A W^T + bias + beta Y for a bf16-stored activation A (M x K, lda) and bf16 weight W (N x K, ldw), bias fp32
+ * or NULL -- no other epilogue.  asrx/gemm.py routes the shapes where the library measured faster than the wide GEMM
+ * (K >= 768, >= 16384 rows; profiles/r06_blaslt_vs_wide.txt).  Replaces nn.Linear's forward / input gradient at
+ * those shapes (model.py:573-574 MLP down projection, 505 MSheath MLP, their input gradients). */
+int asrx_gemm_lt(const void* A, int64_t lda, const unsigned short* W, int64_t ldw, void* C, int c_bf16, int64_t ldc,
+                 const float* bias, int64_t M, int64_t N, int64_t K, float alpha, float beta, asrx_stream_t stream);
 int asrx_gemm_wn_res(const float* A, int64_t lda, const unsigned short* W, int64_t ldw, float* C, int64_t ldc,
                      const float* bias, const float* R, int64_t ldr, int64_t M, int64_t N, int64_t K, int nj,
                      asrx_stream_t stream);
