@@ -213,13 +213,18 @@ _nj_override = None
 NJ_MIN_TILES = {"large": (200, 200), "small": (180, 144)}
 
 
-def _nj(M, N):
-    """Tile width 128*nj of the persistent wide GEMM (NJ_MIN_TILES); narrow tiles run two workgroups per CU."""
+def _nj(M, N, a_bf16=True):
+    """Tile width 128*nj of the persistent wide GEMM (NJ_MIN_TILES); narrow tiles run two workgroups per CU.  An fp32
+    activation whose N leaves the last 384-wide tile partly empty takes the 256-wide tile (N = M + Dh of the MSheath
+    product: 448 at small, 576 at medium -- 48016 x 448 x 768 93 -> 69 us, 24000 x 576 x 1024 74 -> 52 us; a bf16
+    activation is within 3 % either way, profiles/r06_nj_pad.txt)."""
     if _nj_override:
         return _nj_override
     tm = (M + 127) // 128
     t3, t2 = NJ_MIN_TILES["large" if M >= 16384 else "small"]
     for nj, th in ((3, t3), (2, t2)):
+        if nj == 3 and not a_bf16 and N % 384:
+            continue
         if 128 * nj <= ((N + 127) // 128) * 128 and tm * ((N + 128 * nj - 1) // (128 * nj)) >= th:
             return nj
     return 1
@@ -251,7 +256,7 @@ def gemm_wn(A, Wb, C, *, M, N, K, lda, ldc, bias=None, Z=None, alpha=1.0, beta=0
                  K, float(alpha), float(beta), lib.stream())
         probe.end("gemm", e0, 2.0 * M * N * K, ("lt", M, N, K, cb, beta != 0))
         return C
-    nj = _nj(M, N)
+    nj = _nj(M, N, ab)
     e0 = probe.begin("gemm")
     lib.call("asrx_gemm_wn_ex", lib.ptr(A), ab, lda, int(conv), conv_F, conv_C, lib.ptr(Wb), Wb.stride(0),
              lib.ptr(C), cb, ldc, lib.ptr(bias), lib.ptr(Z), M, N, K, float(alpha), float(beta), ACT[act], nj,
@@ -480,8 +485,11 @@ def _wgrad(A, lda, x2, out, M, K, rows, db=None):
     ok4 = M % 4 == 0 and K % 4 == 0 and lda % 4 == 0 and A.data_ptr() % 16 == 0 and x2.data_ptr() % 16 == 0
     # register-staged bf16 kernel with transpose reads (csrc/gemm_wg.hip): faster where the output
     # has few tiles (D x D weights, 1.2-2.6x on the 8192-row text side); the wide 1152/1536 outputs at
-    # 192k rows stay on the split-K LDS-DMA kernel (5-12 % faster there, tools/wgrad_bench.py)
-    if prec.get() == prec.PREC_BF16 and ok4 and x2.stride(0) == K and (tiles <= 9 or rows <= 16384):
+    # 192k rows stay on the split-K LDS-DMA kernel (5-12 % faster there, tools/wgrad_bench.py); at 24-48k rows
+    # (small / medium B=8) every output up to 72 tiles is 5-25 % faster on the staged kernel, 768 x 3072 is not
+    # (profiles/r06_wgrad_bench.txt)
+    if prec.get() == prec.PREC_BF16 and ok4 and x2.stride(0) == K and (tiles <= 9 or rows <= 16384
+                                                                        or (rows <= 50000 and tiles <= 72)):
         return staged(0, 0, "asrx_wgrad_bf16")
     gemm(A, x2, out, M=M, N=K, K=rows, lda=lda, ldb=K, ldc=K, a_kc=False, b_kc=False, beta=1.0, splitk=sk)
     if db is not None:

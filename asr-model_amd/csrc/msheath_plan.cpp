@@ -96,10 +96,11 @@ namespace {
 
 // asrx/gemm.py _nj (NJ_MIN_TILES): the widest 128 * nj tile with enough tiles -- 200 for either width at >= 16384
 // rows, 180 (nj 3) / 144 (nj 2) below
-int wide_nj(int64_t M, int64_t N) {
+int wide_nj(int64_t M, int64_t N, bool a_bf16) {
   const int64_t tm = (M + 127) / 128;
   const bool large = M >= 16384;
   for (int nj = 3; nj >= 2; --nj) {
+    if (nj == 3 && !a_bf16 && N % 384) continue;  // an fp32 activation skips a partly empty 384-wide tile
     const int64_t th = large ? 200 : (nj == 3 ? 180 : 144);
     if (128 * nj <= ((N + 127) / 128) * 128 && tm * ((N + 128 * nj - 1) / (128 * nj)) >= th) return nj;
   }
@@ -193,7 +194,7 @@ int asrx_msheath_fwd(const asrx_msheath_plan* plan, const float* x0, const float
   float* part_last = b.part + nl * B * nchunk * D;
   MS_CALL(asrx_seg_colsum_det(x0, part_last, b.pooled, B, L, D, (float)(1.0 / (double)L), st));
   MS_CALL(asrx_gemm_wn_ex(b.pooled, 0, D, 0, 0, 0, P.p0_wb, D, b.hp, 0, P.p_hidden, P.p0_b, nullptr, B, P.p_hidden, D,
-                          1.f, 0.f, asrx::ACT_SILU, wide_nj(B, P.p_hidden), nullptr, nullptr, st));
+                          1.f, 0.f, asrx::ACT_SILU, wide_nj(B, P.p_hidden, false), nullptr, nullptr, st));
   MS_CALL(asrx_small_linear_fwd(b.hp, P.p2_w, P.p2_b, b.policy, B, P.p_hidden, 3, asrx::ACT_SOFTMAX, st));
   const float* mem_w = P.mem_w;
   int64_t ld_mw = 0;
@@ -212,7 +213,7 @@ int asrx_msheath_fwd(const asrx_msheath_plan* plan, const float* x0, const float
     }
     // SH = [x normalize(mkey)^T | mlp[0](x)]     model.py:346-349
     MS_CALL(asrx_gemm_wn_ex(x, 0, D, 0, 0, 0, Ly.wcb, D, b.SH, 0, N, Ly.bc, nullptr, rows, N, D, 1.f, 0.f,
-                            asrx::ACT_NONE, wide_nj(rows, N), tl, cnt, st));
+                            asrx::ACT_NONE, wide_nj(rows, N, false), tl, cnt, st));
     float* wr = b.wsr + 7 * rows * i;  // mean, rstd, nx, g, ion, kv, m2
     float *mean = wr, *rstd = wr + rows, *nx = wr + 2 * rows, *gv = wr + 3 * rows, *ion = wr + 4 * rows,
           *kv = wr + 5 * rows, *m2 = wr + 6 * rows;
@@ -223,7 +224,7 @@ int asrx_msheath_fwd(const asrx_msheath_plan* plan, const float* x0, const float
     const float* out = (const float*)b.px;
     if (Ly.ad_wb) {
       MS_CALL(asrx_gemm_wn_ex(b.px, pxb, D, 0, 0, 0, Ly.ad_wb, D, b.out, 0, D, Ly.ad_b, nullptr, rows, D, D, 1.f, 0.f,
-                              asrx::ACT_NONE, wide_nj(rows, D), tl, cnt, st));
+                              asrx::ACT_NONE, wide_nj(rows, D, pxb != 0), tl, cnt, st));
       out = b.out;
     }
     float* part_i = b.part + i * B * nchunk * D;
@@ -246,9 +247,9 @@ int asrx_msheath_fwd(const asrx_msheath_plan* plan, const float* x0, const float
   MS_CALL(asrx_layernorm_fwd3(x, P.mln_w, P.mln_b, b.hln, P.hln_bf16, b.mean2, b.rstd2, nullptr, P.mgate_w,
                               P.mgate_b, b.gate, 1, rows, D, P.mln_eps, st));
   MS_CALL(asrx_gemm_wn_ex(b.hln, P.hln_bf16, D, 0, 0, 0, P.m0_wb, D, b.a1, P.a1_bf16, P.H1, P.m0_b, nullptr, rows,
-                          P.H1, D, 1.f, 0.f, asrx::ACT_SILU, wide_nj(rows, P.H1), nullptr, nullptr, st));
+                          P.H1, D, 1.f, 0.f, asrx::ACT_SILU, wide_nj(rows, P.H1, P.hln_bf16 != 0), nullptr, nullptr, st));
   MS_CALL(asrx_gemm_wn_ex(b.a1, P.a1_bf16, P.H1, 0, 0, 0, P.m2_wb, P.H1, b.hh, 0, D, P.m2_b, nullptr, rows, D, P.H1,
-                          1.f, 0.f, asrx::ACT_NONE, wide_nj(rows, D), nullptr, nullptr, st));
+                          1.f, 0.f, asrx::ACT_NONE, wide_nj(rows, D, P.a1_bf16 != 0), nullptr, nullptr, st));
   MS_CALL(asrx_axpy_row(x, b.gate, b.hh, y, rows, D, st));
   return 0;
 }
