@@ -91,8 +91,6 @@ SIGNATURES = {
     "asrx_weights_to_bf16": (_i32, [_p, _i64, _i64, _p]),
     "asrx_row_tiles": (_i32, [_p, _i64, _i64, _i64, _p, _p, _p]),
     "asrx_msheath_ctrl_fwd3": (_i32, [_p, _p, _i64, _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p] + [_i64] * 5 + [_p] * 8),
-    "asrx_msheath_ctrl_fwd4": (_i32, [_p, _p, _i64, _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p] + [_i64] * 5 + [_p] * 7
-                               + [_i64, _p, _p, _p]),
     "asrx_mem_chunks": (_i64, [_i64]),
     "asrx_seg_colsum_det": (_i32, [_p, _p, _p, _i64, _i64, _i64, _f32, _p]),
     "asrx_msheath_ctrl_bwd3": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _p, _p, _p] + [_i64] * 4 + [_p, _i32] + [_p] * 8),

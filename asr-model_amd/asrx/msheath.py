@@ -112,8 +112,6 @@ def forward(mod, x0, gpol, save, tag=None):
         sv["ws"] = (wsr, wsb, wsd, wsc)
     inv_sqrt_d = 1.0 / math.sqrt(D)
     layers = []
-    mt_next = None
-    n_tiles = int(lib.load().asrx_row_tiles_max(rows)) if wide else 0
     for i, lay in enumerate(mod.layers):
         vg = lay["v_gate"]
         Dh = vg.mlp[0].weight.shape[0]
@@ -131,8 +129,7 @@ def forward(mod, x0, gpol, save, tag=None):
         Wc, bc, mkn, wb = G.derived(("vgate", bool(wide)), build, (vg.mkey, vg.mlp[0].weight, vg.mlp[0].bias))
         # rows of samples not at this layer (next_i[b] != i; the reference never runs them) are skipped:
         # by whole 128-row tiles in the GEMMs, by row in the row kernels
-        # (built by the previous layer's control kernel, asrx_msheath_ctrl_fwd4)
-        mt = mt_next if (wide and next_i is not None) else None
+        mt = G.row_tiles(next_i, i, L, rows, dev) if (wide and next_i is not None) else None
         SH = G.linear_fwd(x, Wc, bc, wbf=wb, mtiles=mt)
         # px = LayerNorm(x), |x|, g = sigmoid(gate(px)), ion = v_gate(x)   (346-351, 452-460)
         ln, gt = lay["ln"], lay["gate"][0]
@@ -156,16 +153,9 @@ def forward(mod, x0, gpol, save, tag=None):
         gam, mwo, mem = (a_d + 4 * B * D * (3 * i + j) for j in range(3))
         rec = a_c + B * rec_bytes * i
         gp = gpol[:, i]
-        if wide and i + 1 < nl:  # also layer i + 1's row tiles, from the last workgroup (no row_tiles launch)
-            mt_next = (torch.empty(n_tiles, dtype=torch.int32, device=dev), torch.empty(1, dtype=torch.int32, device=dev))
-            lib.call("asrx_msheath_ctrl_fwd4", _P(policy), _P(gp), gp.stride(0), _P(ion), _P(mg.weight), _P(mg.bias),
-                     _P(mem_v), _P(mem_w), ld_mw, _P(part[i]), _P(mem), _P(mod.jump_s), _P(next_i), i, nl, B, L, D,
-                     _P(alpha), _P(beta), _P(gam), _P(mwo), _P(active), _P(next_out), _P(rec), rows, _P(mt_next[0]),
-                     _P(mt_next[1]), st)
-        else:
-            lib.call("asrx_msheath_ctrl_fwd3", _P(policy), _P(gp), gp.stride(0), _P(ion), _P(mg.weight), _P(mg.bias),
-                     _P(mem_v), _P(mem_w), ld_mw, _P(part[i]), _P(mem), _P(mod.jump_s), _P(next_i), i, nl, B, L, D,
-                     _P(alpha), _P(beta), _P(gam), _P(mwo), _P(active), _P(next_out), _P(rec), st)
+        lib.call("asrx_msheath_ctrl_fwd3", _P(policy), _P(gp), gp.stride(0), _P(ion), _P(mg.weight), _P(mg.bias),
+                 _P(mem_v), _P(mem_w), ld_mw, _P(part[i]), _P(mem), _P(mod.jump_s), _P(next_i), i, nl, B, L, D,
+                 _P(alpha), _P(beta), _P(gam), _P(mwo), _P(active), _P(next_out), _P(rec), st)
         if tag is not None and decisions.active():
             decisions.msheath_layer(tag[0], tag[1], i, wsr[i, 4].view(B, L), wsc[i].view(torch.float32).view(B, -1))
         if save:

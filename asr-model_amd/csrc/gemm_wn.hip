@@ -3,7 +3,6 @@
 #include "gemm_wr.h"
 #include "gemm_p2.h"
 #include "gemm_ws.h"
-#include "row_tiles.h"
 #include <string>
 
 // Which wide-GEMM kernel runs the plain / residual products that gemm_p2_kernel covers (asrx_set_gemm_variant):
@@ -319,12 +318,44 @@ extern "C" int asrx_gemm_wn_rows(const float* A, int64_t lda, const unsigned sho
   ASRX_LAUNCHED("asrx_gemm_wn_rows");
 }
 
-// The BM-row tiles of an M-row activation at MSheath layer `layer` (row_tiles.h).  One workgroup.
+// The BM-row tiles of an M-row activation whose rows r belong to a sample b = r / L that is at MSheath
+// layer `layer` (next_i[b] == layer): mtiles[0 .. *n_mtiles) in increasing order.  One workgroup.
 namespace asrx {
-static_assert(wn::BM == RT_BM, "row tiles are the wide GEMM's row tiles");
 __global__ __launch_bounds__(1024) void row_tiles_kernel(const float* __restrict__ next_i, int layer, int64_t L,
                                                          int64_t M, int* __restrict__ mtiles, int* __restrict__ n_out) {
-  build_row_tiles<1024, false>(next_i, layer, L, M, mtiles, n_out);
+  __shared__ int wsum[16];
+  __shared__ int base;
+  const int nm = (int)((M + wn::BM - 1) / wn::BM);
+  if (threadIdx.x == 0) base = 0;
+  __syncthreads();
+  for (int t0 = 0; t0 < nm; t0 += 1024) {
+    const int t = t0 + threadIdx.x;
+    int act = 0;
+    if (t < nm) {
+      const int64_t r0 = (int64_t)t * wn::BM, r1 = min<int64_t>(r0 + wn::BM, M) - 1;
+      for (int64_t b = r0 / L; b <= r1 / L && !act; ++b) act = next_i[b] == (float)layer;
+    }
+    // block exclusive scan of act
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int v = act;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = __shfl_up(v, o);
+      if (lane >= o) v += u;
+    }
+    if (lane == 63) wsum[w] = v;
+    __syncthreads();
+    int off = base;
+    for (int k = 0; k < w; ++k) off += wsum[k];
+    if (act) mtiles[off + v - 1] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int tot = 0;
+      for (int k = 0; k < 16; ++k) tot += wsum[k];
+      base += tot;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) n_out[0] = base;
 }
 }  // namespace asrx
 

@@ -5,12 +5,8 @@
 //   control: potential, gumbel policy, action, alpha/beta/gam, mem_w, next layer  msheath_ctrl
 //   x = act ? alpha*x_new + beta*orig + gam : x                                     jump_select
 // instead of ~25 small tensor ops forward and ~40 backward.
-#include <map>
-#include <mutex>
 #include <type_traits>
-#include <utility>
 #include "common.h"
-#include "row_tiles.h"
 
 namespace asrx {
 
@@ -35,8 +31,7 @@ __global__ __launch_bounds__(256) void msheath_ctrl_fwd_kernel(
     float* __restrict__ alpha, float* __restrict__ beta, float* __restrict__ gam, float* __restrict__ mem_w_out,
     float* __restrict__ active, float* __restrict__ next_out, CtrlRec* __restrict__ rec, int64_t ld_mem_w,
     const float* __restrict__ mg_w, const float* __restrict__ mg_b, float* __restrict__ mem_v_out,
-    const float* __restrict__ mem_part, int nchunk, float* __restrict__ mem_out, int64_t M_rows = 0,
-    int* __restrict__ tl_next = nullptr, int* __restrict__ cnt_next = nullptr, unsigned* __restrict__ counter = nullptr) {
+    const float* __restrict__ mem_part, int nchunk, float* __restrict__ mem_out) {
   __shared__ float red[4];
   const int64_t b = blockIdx.x;
   // the sample's ion values (L <= 24 * 256: the configurations' 3001 / 6002 frames) are requested first, so
@@ -165,19 +160,6 @@ __global__ __launch_bounds__(256) void msheath_ctrl_fwd_kernel(
     r.cg = cg;
     r.act = act;
     rec[b] = r;
-  }
-  if (tl_next) {  // the next layer's row tiles (row_tiles.h), built by the last workgroup to finish
-    __shared__ int last;
-    if (threadIdx.x == 0) {
-      __threadfence();  // this sample's next_out visible device-wide before it is counted
-      last = atomicAdd(counter, 1u) == gridDim.x - 1;
-    }
-    __syncthreads();
-    if (last) {
-      __threadfence();
-      build_row_tiles<256, true>(next_out, layer_i + 1, L, M_rows, tl_next, cnt_next);
-      if (threadIdx.x == 0) *counter = 0u;  // ready for the next launch on this stream
-    }
   }
 }
 
@@ -775,51 +757,6 @@ int asrx_msheath_ctrl_fwd3(const float* policy, const float* gpol, int64_t ld_gp
                                                            gam, mem_w_out, active, next_out, (CtrlRec*)rec, ld_mem_w,
                                                            mg_w, mg_b, mem_v_out, mem_part, nchunk, mem);
   ASRX_LAUNCHED("asrx_msheath_ctrl_fwd3");
-}
-
-// The launch counter of asrx_msheath_ctrl_fwd4's last-workgroup step, one per (device, stream): launches on one
-// stream are ordered and the last workgroup resets it, so it is zero at every launch's start.  Allocated (and
-// zeroed on the stream) on first use, in relaxed capture mode like the small-linear partials.
-static unsigned* ctrl_counter(hipStream_t stream) {
-  static std::mutex mu;
-  static std::map<std::pair<int, hipStream_t>, unsigned*> pool;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  std::lock_guard<std::mutex> lk(mu);
-  unsigned*& p = pool[std::make_pair(dev, stream)];
-  if (!p) {
-    hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
-    (void)hipThreadExchangeStreamCaptureMode(&mode);
-    const hipError_t e = hipMalloc(&p, 64);
-    (void)hipThreadExchangeStreamCaptureMode(&mode);
-    if (e != hipSuccess || hipMemsetAsync(p, 0, 64, stream) != hipSuccess) {
-      p = nullptr;
-      return nullptr;
-    }
-  }
-  return p;
-}
-
-// asrx_msheath_ctrl_fwd3 that also writes layer layer_i + 1's row-tile list of the M_rows-row activation
-// (asrx_row_tiles' output: tl_next[asrx_row_tiles_max(M_rows)], cnt_next[1]) from next_out, in its last workgroup
-// to finish: one launch fewer per MSheath layer.
-int asrx_msheath_ctrl_fwd4(const float* policy, const float* gpol, int64_t ld_gpol, const float* ion,
-                           const float* mg_w, const float* mg_b, float* mem_v_out, const float* mem_w,
-                           int64_t ld_mem_w, const float* mem_part, float* mem, const float* jump_s,
-                           const float* next_i, int64_t layer_i, int64_t layers, int64_t B, int64_t L, int64_t D,
-                           float* alpha, float* beta, float* gam, float* mem_w_out, float* active, float* next_out,
-                           void* rec, int64_t M_rows, int* tl_next, int* cnt_next, hipStream_t stream) {
-  if (B == 0) return 0;
-  ASRX_REQUIRE(tl_next && cnt_next && M_rows == B * L, "asrx_msheath_ctrl_fwd4: row-tile outputs and M_rows = B L");
-  unsigned* counter = ctrl_counter(stream);
-  ASRX_REQUIRE(counter, "asrx_msheath_ctrl_fwd4: counter allocation failed");
-  const int nchunk = (int)((L + MEM_CHUNK - 1) / MEM_CHUNK);
-  msheath_ctrl_fwd_kernel<<<(unsigned)B, 256, 0, stream>>>(policy, gpol, ld_gpol, ion, nullptr, mem_w, mem, jump_s,
-                                                           next_i, (int)layer_i, (int)layers, L, (int)D, alpha, beta,
-                                                           gam, mem_w_out, active, next_out, (CtrlRec*)rec, ld_mem_w,
-                                                           mg_w, mg_b, mem_v_out, mem_part, nchunk, mem, M_rows,
-                                                           tl_next, cnt_next, counter);
-  ASRX_LAUNCHED("asrx_msheath_ctrl_fwd4");
 }
 
 int asrx_msheath_ctrl_bwd(const float* g_alpha, const float* g_beta, const float* g_gam, const float* g_mwo,

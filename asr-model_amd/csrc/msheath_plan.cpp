@@ -25,6 +25,8 @@ int asrx_gemm_wn_ex(const void* A, int a_bf16, int64_t lda, int conv, int64_t co
 int asrx_small_linear_fwd(const float* x, const float* W, const float* b, float* y, int64_t rows, int64_t K,
                           int64_t N, int act, hipStream_t stream);
 int64_t asrx_row_tiles_max(int64_t M);
+int asrx_row_tiles(const float* next_i, int64_t layer, int64_t L, int64_t M, int* mtiles, int* n_mtiles,
+                   hipStream_t stream);
 int asrx_msheath_row_fwd2(const float* x, const float* lnw, const float* lnb, const float* gw, const float* gb,
                           const float* SH, int64_t ldsh, const float* mval, const float* w2, const float* b2,
                           const float* cw, const float* cb, const float* tx, void* px, int px_bf16, float* mean,
@@ -41,12 +43,6 @@ int asrx_msheath_ctrl_fwd3(const float* policy, const float* gpol, int64_t ld_gp
                            const float* next_i, int64_t layer_i, int64_t layers, int64_t B, int64_t L, int64_t D,
                            float* alpha, float* beta, float* gam, float* mem_w_out, float* active, float* next_out,
                            void* rec, hipStream_t stream);
-int asrx_msheath_ctrl_fwd4(const float* policy, const float* gpol, int64_t ld_gpol, const float* ion,
-                           const float* mg_w, const float* mg_b, float* mem_v_out, const float* mem_w,
-                           int64_t ld_mem_w, const float* mem_part, float* mem, const float* jump_s,
-                           const float* next_i, int64_t layer_i, int64_t layers, int64_t B, int64_t L, int64_t D,
-                           float* alpha, float* beta, float* gam, float* mem_w_out, float* active, float* next_out,
-                           void* rec, int64_t M_rows, int* tl_next, int* cnt_next, hipStream_t stream);
 int asrx_jump_axpy_inplace(const float* xin, float* xout, const float* s1, const float* s2, const float* y,
                            const float* orig, const float* act, const float* alpha, const float* beta, const float* gam,
                            int64_t B, int64_t L, int64_t d, hipStream_t stream);
@@ -210,7 +206,8 @@ int asrx_msheath_fwd(const asrx_msheath_plan* plan, const float* x0, const float
     // rows of samples not at this layer are skipped: by whole 128-row tiles in the GEMMs, by row in the row kernels
     const int* tl = nullptr;
     const int* cnt = nullptr;
-    if (next_i) {  // written by the previous layer's control step (asrx_msheath_ctrl_fwd4)
+    if (next_i) {
+      MS_CALL(asrx_row_tiles(next_i, i, L, rows, b.tl, b.cnt, st));
       tl = b.tl;
       cnt = b.cnt;
     }
@@ -236,15 +233,9 @@ int asrx_msheath_fwd(const asrx_msheath_plan* plan, const float* x0, const float
     float *alpha = wb5, *beta = wb5 + B, *active = wb5 + 2 * B, *next_out = wb5 + 3 * B, *mem_v = wb5 + 4 * B;
     float* wd3 = b.wsd + 3 * B * D * i;  // gam, mwo, mem
     float *gam = wd3, *mwo = wd3 + B * D, *mem = wd3 + 2 * B * D;
-    // layer i + 1's row tiles from the same launch: b.tl is free again (both GEMMs of layer i are ahead on the stream)
-    if (i + 1 < nl)
-      MS_CALL(asrx_msheath_ctrl_fwd4(b.policy, gpol + 3 * i, ld_gpol, ion, P.mg_w, P.mg_b, mem_v, mem_w, ld_mw, part_i,
-                                     mem, P.jump_s, next_i, i, nl, B, L, D, alpha, beta, gam, mwo, active, next_out,
-                                     b.wsc + rec_bytes * B * i, rows, b.tl, b.cnt, st));
-    else
-      MS_CALL(asrx_msheath_ctrl_fwd3(b.policy, gpol + 3 * i, ld_gpol, ion, P.mg_w, P.mg_b, mem_v, mem_w, ld_mw, part_i,
-                                     mem, P.jump_s, next_i, i, nl, B, L, D, alpha, beta, gam, mwo, active, next_out,
-                                     b.wsc + rec_bytes * B * i, st));
+    MS_CALL(asrx_msheath_ctrl_fwd3(b.policy, gpol + 3 * i, ld_gpol, ion, P.mg_w, P.mg_b, mem_v, mem_w, ld_mw, part_i,
+                                   mem, P.jump_s, next_i, i, nl, B, L, D, alpha, beta, gam, mwo, active, next_out,
+                                   b.wsc + rec_bytes * B * i, st));
     // one pass, in place from layer 1 on (samples not at the layer keep their rows untouched)
     MS_CALL(asrx_jump_axpy_inplace(x, b.xrun, gv, ion, out, x0, active, alpha, beta, gam, B, L, D, st));
     mem_w = mwo;

@@ -385,15 +385,6 @@ int asrx_msheath_ctrl_fwd3(const float* policy, const float* gpol, int64_t ld_gp
                            const float* next_i, int64_t layer_i, int64_t layers, int64_t B, int64_t L, int64_t D,
                            float* alpha, float* beta, float* gam, float* mem_w_out, float* active, float* next_out,
                            void* rec, asrx_stream_t stream);
-/* asrx_msheath_ctrl_fwd3 that also writes the next layer's row-tile list (asrx_row_tiles(next_out, layer_i + 1, L,
- * M_rows, tl_next, cnt_next)) from its last workgroup to finish -- one launch fewer per MSheath layer.  M_rows = B L;
- * tl_next holds asrx_row_tiles_max(M_rows) ints.  A device counter per (device, stream) is kept by the library. */
-int asrx_msheath_ctrl_fwd4(const float* policy, const float* gpol, int64_t ld_gpol, const float* ion,
-                           const float* mg_w, const float* mg_b, float* mem_v_out, const float* mem_w,
-                           int64_t ld_mem_w, const float* mem_part, float* mem, const float* jump_s,
-                           const float* next_i, int64_t layer_i, int64_t layers, int64_t B, int64_t L, int64_t D,
-                           float* alpha, float* beta, float* gam, float* mem_w_out, float* active, float* next_out,
-                           void* rec, int64_t M_rows, int* tl_next, int* cnt_next, asrx_stream_t stream);
 int asrx_msheath_ctrl_bwd3(const float* g_alpha, const float* g_beta, const float* g_gam, const float* g_mwo,
                            const float* mem_v, const float* mem_w, int64_t ld_mem_w, const float* mem,
                            const float* jump_s, const void* rec, int64_t layer_i, int64_t layers, int64_t B, int64_t D,
