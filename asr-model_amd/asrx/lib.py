@@ -174,6 +174,7 @@ SIGNATURES = {
     "asrx_tgate_fwd2": (_i32, [_p, _p, _p, _i32, _i64, _i64, _p]),
     "asrx_msheath_row_fwd2": (_i32, [_p] * 6 + [_i64] + [_p] * 7 + [_i32] + [_p] * 7 + [_i64] * 4
                                     + [_f32, _f32, _p, _i64, _i64, _p]),
+    "asrx_msheath_row_fwd3": (_i32, [_p] * 6 + [_i64] + [_p] * 16 + [_i64] * 4 + [_f32, _f32, _p, _i64, _i64, _p]),
     "asrx_layernorm_fwd3": (_i32, [_p, _p, _p, _p, _i32] + [_p] * 6 + [_i32, _i64, _i64, _f32, _p]),
     "asrx_jump_axpy_inplace": (_i32, [_p] * 10 + [_i64, _i64, _i64, _p]),
     "asrx_wave_pool": (_i32, [_p, _i64, _i64, _i64, _i64, _p, _p]),

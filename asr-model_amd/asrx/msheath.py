@@ -43,6 +43,9 @@ ROW_DIMS = (128, 256, 384, 512, 768, 1024)  # the fused row kernels' register-re
 # atomics: with it no float atomic feeds the data gradient, so a whole backward is bit-reproducible
 # (tests/test_gpu_fusions.py).  False: the atomic form (kept for A/B diagnostics).
 DETERMINISTIC = True
+# A layer without adapter (its update is px itself) forms x_new and the per-chunk column sums in its row pass
+# (asrx_msheath_row_fwd3) instead of a separate asrx_axpy_row2_colsum launch.  False: the two-launch form.
+ROW_COLSUM = __import__("os").environ.get("ASRX_ROW_COLSUM", "1") != "0"
 
 
 def _rec_bytes():
@@ -138,16 +141,23 @@ def forward(mod, x0, gpol, save, tag=None):
         pxb = int(ad is not None and wide and prec.bf16_storage())
         px = _E(B, L, D, device=dev, dtype=torch.bfloat16 if pxb else torch.float32)
         mean, rstd, nx, gv, ion, kv, m2 = (a_r + 4 * rows * (7 * i + j) for j in range(7))
-        lib.call("asrx_msheath_row_fwd2", _P(x), _P(ln.weight), _P(ln.bias), _P(gt.weight), _P(gt.bias), _P(SH), N,
-                 _P(vg.mval), _P(vg.mlp[2].weight), _P(vg.mlp[2].bias), _P(vg.concat.weight), _P(vg.concat.bias),
-                 _P(vg.tx), _P(px), pxb, _P(mean), _P(rstd), _P(nx), _P(gv), _P(ion), _P(kv), _P(m2), rows, D, M, Dh,
-                 float(ln.eps), inv_sqrt_d, _P(next_i), i, L, st)
-        out = G.linear_fwd(px, ad.weight, ad.bias, mtiles=mt) if ad is not None else px
         # x_new = x + g * ion * out; mem = mean_l x_new   (461-463).  Without a backward x_new is not
-        # materialised: the column sums are taken here and the jump step below recomputes it
+        # materialised: the column sums are taken and the jump step below recomputes it
         x_new = _E(B, L, D, device=dev) if save else None
-        lib.call("asrx_axpy_row2_colsum", _P(x), _P(gv), _P(ion), _P(out), _P(x_new), _P(part[i]), B, L, D,
-                 _P(next_i), i, st)
+        if ad is None and ROW_COLSUM:  # out = px: the row pass forms x_new and its column sums itself
+            lib.call("asrx_msheath_row_fwd3", _P(x), _P(ln.weight), _P(ln.bias), _P(gt.weight), _P(gt.bias), _P(SH),
+                     N, _P(vg.mval), _P(vg.mlp[2].weight), _P(vg.mlp[2].bias), _P(vg.concat.weight),
+                     _P(vg.concat.bias), _P(vg.tx), _P(px), _P(mean), _P(rstd), _P(nx), _P(gv), _P(ion), _P(kv), _P(m2),
+                     _P(x_new), _P(part[i]), rows, D, M, Dh, float(ln.eps), inv_sqrt_d, _P(next_i), i, L, st)
+            out = px
+        else:
+            lib.call("asrx_msheath_row_fwd2", _P(x), _P(ln.weight), _P(ln.bias), _P(gt.weight), _P(gt.bias), _P(SH),
+                     N, _P(vg.mval), _P(vg.mlp[2].weight), _P(vg.mlp[2].bias), _P(vg.concat.weight),
+                     _P(vg.concat.bias), _P(vg.tx), _P(px), pxb, _P(mean), _P(rstd), _P(nx), _P(gv), _P(ion), _P(kv),
+                     _P(m2), rows, D, M, Dh, float(ln.eps), inv_sqrt_d, _P(next_i), i, L, st)
+            out = G.linear_fwd(px, ad.weight, ad.bias, mtiles=mt) if ad is not None else px
+            lib.call("asrx_axpy_row2_colsum", _P(x), _P(gv), _P(ion), _P(out), _P(x_new), _P(part[i]), B, L, D,
+                     _P(next_i), i, st)
         # mem_v = sigmoid(mem_gate(mem)); control; jump select   (464-501)
         alpha, beta, active, next_out, mem_v = (a_b + 4 * B * (5 * i + j) for j in range(5))
         gam, mwo, mem = (a_d + 4 * B * D * (3 * i + j) for j in range(3))
@@ -375,7 +385,7 @@ def _composite_ok(mod, x, gpol, tag):
     from . import probe
     D = x.shape[-1]
     H1 = mod.mlp[0].weight.shape[0]
-    return (COMPOSITE and prec.get() == prec.PREC_BF16 and G.use_wide(D) and G.use_wide(H1) and H1 % 4 == 0
+    return (COMPOSITE and ROW_COLSUM and prec.get() == prec.PREC_BF16 and G.use_wide(D) and G.use_wide(H1) and H1 % 4 == 0
             and G._nj_override is None and not probe.active() and not (tag is not None and decisions.active())
             and x.is_cuda and gpol.is_contiguous() and gpol.dtype == torch.float32 and x.dtype == torch.float32)
 

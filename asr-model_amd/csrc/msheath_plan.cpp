@@ -35,6 +35,12 @@ int asrx_msheath_row_fwd2(const float* x, const float* lnw, const float* lnb, co
                           int64_t L, hipStream_t stream);
 int64_t asrx_mem_chunks(int64_t L);
 int64_t asrx_msheath_rec_bytes(void);
+int asrx_msheath_row_fwd3(const float* x, const float* lnw, const float* lnb, const float* gw, const float* gb,
+                          const float* SH, int64_t ldsh, const float* mval, const float* w2, const float* b2,
+                          const float* cw, const float* cb, const float* tx, float* px, float* mean, float* rstd,
+                          float* nx, float* g, float* ion, float* kv, float* m2, float* xnew, float* part, int64_t rows,
+                          int64_t d, int64_t M, int64_t Dh, float eps, float inv_sqrt_d, const float* next_i,
+                          int64_t layer, int64_t L, hipStream_t stream);
 int asrx_axpy_row2_colsum(const float* x, const float* s1, const float* s2, const float* y, float* out, float* part,
                           int64_t B, int64_t L, int64_t d, const float* next_i, int64_t layer, hipStream_t stream);
 int asrx_msheath_ctrl_fwd3(const float* policy, const float* gpol, int64_t ld_gpol, const float* ion,
@@ -218,17 +224,21 @@ int asrx_msheath_fwd(const asrx_msheath_plan* plan, const float* x0, const float
     float *mean = wr, *rstd = wr + rows, *nx = wr + 2 * rows, *gv = wr + 3 * rows, *ion = wr + 4 * rows,
           *kv = wr + 5 * rows, *m2 = wr + 6 * rows;
     const int pxb = Ly.ad_wb ? Ly.px_bf16 : 0;
-    MS_CALL(asrx_msheath_row_fwd2(x, Ly.ln_w, Ly.ln_b, Ly.gate_w, Ly.gate_b, b.SH, N, Ly.mval, Ly.vw2, Ly.vb2, Ly.cw,
-                                  Ly.cb, Ly.tx, b.px, pxb, mean, rstd, nx, gv, ion, kv, m2, rows, D, Ly.M, Ly.Dh,
-                                  Ly.ln_eps, inv_sqrt_d, next_i, i, L, st));
     const float* out = (const float*)b.px;
+    float* part_i = b.part + i * B * nchunk * D;
     if (Ly.ad_wb) {
+      MS_CALL(asrx_msheath_row_fwd2(x, Ly.ln_w, Ly.ln_b, Ly.gate_w, Ly.gate_b, b.SH, N, Ly.mval, Ly.vw2, Ly.vb2,
+                                    Ly.cw, Ly.cb, Ly.tx, b.px, pxb, mean, rstd, nx, gv, ion, kv, m2, rows, D, Ly.M, Ly.Dh,
+                                    Ly.ln_eps, inv_sqrt_d, next_i, i, L, st));
       MS_CALL(asrx_gemm_wn_ex(b.px, pxb, D, 0, 0, 0, Ly.ad_wb, D, b.out, 0, D, Ly.ad_b, nullptr, rows, D, D, 1.f, 0.f,
                               asrx::ACT_NONE, wide_nj(rows, D, pxb != 0), tl, cnt, st));
       out = b.out;
+      MS_CALL(asrx_axpy_row2_colsum(x, gv, ion, out, nullptr, part_i, B, L, D, next_i, i, st));
+    } else {  // out = px: the row pass takes the column sums of x_new itself (asrx.msheath.ROW_COLSUM)
+      MS_CALL(asrx_msheath_row_fwd3(x, Ly.ln_w, Ly.ln_b, Ly.gate_w, Ly.gate_b, b.SH, N, Ly.mval, Ly.vw2, Ly.vb2,
+                                    Ly.cw, Ly.cb, Ly.tx, (float*)b.px, mean, rstd, nx, gv, ion, kv, m2, nullptr, part_i,
+                                    rows, D, Ly.M, Ly.Dh, Ly.ln_eps, inv_sqrt_d, next_i, i, L, st));
     }
-    float* part_i = b.part + i * B * nchunk * D;
-    MS_CALL(asrx_axpy_row2_colsum(x, gv, ion, out, nullptr, part_i, B, L, D, next_i, i, st));
     float* wb5 = b.wsb + 5 * B * i;  // alpha, beta, active, next_out, mem_v
     float *alpha = wb5, *beta = wb5 + B, *active = wb5 + 2 * B, *next_out = wb5 + 3 * B, *mem_v = wb5 + 4 * B;
     float* wd3 = b.wsd + 3 * B * D * i;  // gam, mwo, mem

@@ -645,6 +645,13 @@ struct MSRowFwd {
   int layer;
   int64_t L;
   unsigned short* pxb;  // non-null: px stored bf16 here instead (it only feeds the adapter GEMM)
+  // non-null (a layer without adapter, whose update is px itself): x_new = x + g ion px (model.py:461) is formed
+  // per row and its per-sample column sums over 64-row chunks go to part[b][chunk][:] -- the work of
+  // axpy_row2_colsum (msheath.hip) in this pass; each wave then owns whole chunks (rows in order), and xnew (when
+  // non-null) receives x_new
+  float* part;
+  float* xnew;
+  int nchunk;
 };
 
 // Per row: px = LayerNorm(x); nx = |x|; g = sigmoid(px . gw + gb); v_gate from SH and nx (as
@@ -677,6 +684,7 @@ __global__ __launch_bounds__(64 * RW) void msheath_row_fwd_kernel(MSRowFwd p) {
   float w2v[HQ];
 #pragma unroll
   for (int i = 0; i < HQ; ++i) w2v[i] = lane + 64 * i < p.Dh ? p.w2[lane + 64 * i] : 0.f;
+  float csum[E];  // chunk mode (p.part): this wave's column sums of x_new over its current chunk
   // The rows two strides ahead -- x AND the v_gate projections (S[lane], h) -- are in flight in two
   // named register sets used alternately (see abby_fwd_kernel: rotating one set into the other made the
   // compiler wait for the newest loads every row).  Loads are unconditional: past the end, or for a
@@ -751,6 +759,16 @@ __global__ __launch_bounds__(64 * RW) void msheath_row_fwd_kernel(MSRowFwd p) {
     const float gate = sigmoid_f(gd + gbias);
     const float kv = wave_sum_dpp(lane < p.M ? ez / se * mv_l : 0.f);
     const float xval = cw0 * kv + cw1 * m2 + cb;
+    if (p.part) {  // x_new = x + (g ion) px, as axpy_row2_colsum forms it; column sums in row order
+      const float sc = gate * (xval > tx ? 1.f : 0.f);
+      float xn[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        xn[e] = __builtin_fmaf(sc, yv[e], xv[e]);
+        csum[e] += xn[e];
+      }
+      if (p.xnew) st_lane<E>(p.xnew + r * D, lane, xn);
+    }
     if (lane == 0) {
       p.mean[r] = mu;
       p.rstd[r] = rs;
@@ -761,6 +779,53 @@ __global__ __launch_bounds__(64 * RW) void msheath_row_fwd_kernel(MSRowFwd p) {
       p.m2[r] = m2;
     }
   };
+  if (p.part) {
+    // one workgroup per 64-row chunk of one sample (chunks never straddle samples): wave w takes the chunk's
+    // rows w, w + RW, ... in order with the next row's loads in flight, and the RW waves' column sums are added
+    // in wave order through LDS (deterministic)
+    float* red = ni_s + (p.next_i ? (p.rows + p.L - 1) / p.L : 0);  // RW x D floats after the next_i copy
+    const int w = threadIdx.x >> 6;
+    const int64_t nb = (p.rows + p.L - 1) / p.L, nc = (int64_t)nb * p.nchunk;
+    for (int64_t cid = blockIdx.x; cid < nc; cid += gridDim.x) {
+      const int64_t b = cid / p.nchunk, c = cid - b * p.nchunk;
+      const int64_t r0 = b * p.L + c * 64, r1 = min(min(r0 + 64, (b + 1) * p.L), p.rows);
+#pragma unroll
+      for (int e = 0; e < E; ++e) csum[e] = 0.f;
+      const bool act = r0 < r1 && at_layer(r0);  // workgroup-uniform
+      if (act) {
+        float xa[E], sa, ha[HQ];
+        fetch(r0 + w, xa, sa, ha);
+        for (int64_t r = r0 + w; r < r1; r += RW) {
+          float xv[E], hv[HQ];
+#pragma unroll
+          for (int e = 0; e < E; ++e) xv[e] = xa[e];
+#pragma unroll
+          for (int i = 0; i < HQ; ++i) hv[i] = ha[i];
+          const float sv = sa;
+          fetch(r + RW < r1 ? r + RW : r0, xa, sa, ha);
+          row_body(r, xv, sv, hv);
+        }
+      } else {
+        float xv[E], hv[HQ];
+        for (int64_t r = r0 + w; r < r1; r += RW) row_body(r, xv, 0.f, hv);  // not at this layer: zero rows
+      }
+      if (act) {
+        st_lane<E>(red + w * D, lane, csum);
+        __syncthreads();
+        if (w == 0) {
+          for (int k = 1; k < RW; ++k) {
+            float t[E];
+            ld_lane<E>(red + k * D, lane, t);
+#pragma unroll
+            for (int e = 0; e < E; ++e) csum[e] += t[e];
+          }
+        }
+        __syncthreads();  // red is rewritten by the next chunk
+      }
+      if (w == 0) st_lane<E>(p.part + cid * D, lane, csum);  // (b, chunk) row; zeros for a sample not at the layer
+    }
+    return;
+  }
   const int64_t st = row_step();
   int64_t r = row_begin();
   float xa[E], xb[E], sa, sb, ha[HQ], hb[HQ];
@@ -2530,6 +2595,31 @@ int asrx_msheath_row_fwd2(const float* x, const float* lnw, const float* lnb, co
   ASRX_REQUIRE(shm <= 48 * 1024, "msheath_row_fwd: %ld samples exceed the next_i LDS copy", (long)(shm / 4));
   MS_DISPATCH(msheath_row_fwd_kernel, row_grid(rows), shm, p);
   ASRX_LAUNCHED("asrx_msheath_row_fwd");
+}
+
+// asrx_msheath_row_fwd2 for a layer without adapter (px fp32, the update itself) that also does
+// asrx_axpy_row2_colsum's work: x_new = x + g ion px into xnew (when non-null) and the per-sample 64-row chunk
+// column sums into part (B x asrx_mem_chunks(L) x d) -- one launch and one pass over x and px fewer per layer.
+int asrx_msheath_row_fwd3(const float* x, const float* lnw, const float* lnb, const float* gw, const float* gb,
+                          const float* SH, int64_t ldsh, const float* mval, const float* w2, const float* b2,
+                          const float* cw, const float* cb, const float* tx, float* px, float* mean, float* rstd,
+                          float* nx, float* g, float* ion, float* kv, float* m2, float* xnew, float* part, int64_t rows,
+                          int64_t d, int64_t M, int64_t Dh, float eps, float inv_sqrt_d, const float* next_i,
+                          int64_t layer, int64_t L, hipStream_t stream) {
+  ASRX_REQUIRE(M <= 64 && ldsh >= M + Dh, "asrx_msheath_row_fwd3: M <= 64 and ldsh >= M + Dh required");
+  ASRX_REQUIRE(Dh <= 64 * ((d / 64 + 1) / 2), "asrx_msheath_row_fwd3: v_gate hidden size Dh <= d / 2 required");
+  ASRX_REQUIRE(ms_aligned({x, lnw, lnb, gw, (const float*)px, (const float*)xnew, (const float*)part}),
+               "asrx_msheath_row_fwd3: 8-byte aligned rows required");
+  ASRX_REQUIRE(part && L > 0 && rows % L == 0, "asrx_msheath_row_fwd3: part and rows = B L required");
+  if (rows == 0) return 0;
+  MSRowFwd p{x, lnw, lnb, gw, gb, SH, mval, w2, b2, cw, cb, tx, px, mean, rstd, nx, g, ion, kv, m2, rows, ldsh,
+             (int)M, (int)Dh, eps, inv_sqrt_d, next_i, (int)layer, L, nullptr, part, xnew, (int)((L + 63) / 64)};
+  // next_i copy, then the RW waves' column sums of a chunk
+  const size_t shm = (next_i ? (size_t)(rows / L) : 0) * sizeof(float) + (size_t)RW * d * sizeof(float);
+  ASRX_REQUIRE(shm <= 48 * 1024, "msheath_row_fwd3: %ld samples exceed the next_i LDS copy", (long)(rows / L));
+  const int64_t chunks = (rows / L) * p.nchunk;
+  MS_DISPATCH(msheath_row_fwd_kernel, (unsigned)std::min<int64_t>(chunks, 65535), shm, p);
+  ASRX_LAUNCHED("asrx_msheath_row_fwd3");
 }
 
 int asrx_msheath_row_fwd(const float* x, const float* lnw, const float* lnb, const float* gw, const float* gb,

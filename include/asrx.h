@@ -320,6 +320,16 @@ int asrx_msheath_row_fwd2(const float* x, const float* lnw, const float* lnb, co
                           float* rstd, float* nx, float* g, float* ion, float* kv, float* m2, int64_t rows, int64_t d,
                           int64_t M, int64_t Dh, float eps, float inv_sqrt_d, const float* next_i, int64_t layer,
                           int64_t L, asrx_stream_t stream);
+/* asrx_msheath_row_fwd2 for a layer without adapter (px fp32, the update itself) that also forms x_new = x + g ion px
+ * (model.py:461) into xnew (when non-null) and its per-sample 64-row chunk column sums into part (B x
+ * asrx_mem_chunks(L) x d, zeros for a sample not at the layer) -- asrx_axpy_row2_colsum's work in the same pass.
+ * rows = B L. */
+int asrx_msheath_row_fwd3(const float* x, const float* lnw, const float* lnb, const float* gw, const float* gb,
+                          const float* SH, int64_t ldsh, const float* mval, const float* w2, const float* b2,
+                          const float* cw, const float* cb, const float* tx, float* px, float* mean, float* rstd,
+                          float* nx, float* g, float* ion, float* kv, float* m2, float* xnew, float* part, int64_t rows,
+                          int64_t d, int64_t M, int64_t Dh, float eps, float inv_sqrt_d, const float* next_i,
+                          int64_t layer, int64_t L, asrx_stream_t stream);
 int asrx_msheath_row_bwd(const float* dpx, const float* x, const float* lnw, const float* lnb, const float* mean,
                          const float* rstd, const float* dg, const float* g, const float* gw, const float* dion,
                          const float* SH, int64_t ldsh, const float* nx, const float* mval, const float* w2,
