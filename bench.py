@@ -203,6 +203,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # stdout carries exactly one JSON line: everything else written to fd 1 from here on -- the RCCL version banner
+    # of communicator init, library messages, our own progress prints -- goes to stderr, and the line is written to
+    # the original stdout at the end
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     if args.same_device:
         local = 0
     # one issue thread per rank: pin each rank's process (its Python issue thread and the HIP runtime's threads) to its
@@ -607,7 +613,9 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(result) + "\n").encode())
+    os.close(json_fd)
 
 
 def pmc_traffic(kernel_substrs, config, batch, pitch_frames):
