@@ -63,6 +63,8 @@ def parse():
     ap.add_argument("--graph-dead", action="store_true", help="replay the dead blocks from HIP graphs "
                     "(asrx.model.processor.graph_dead_blocks; off by default, profiles/r06_host_vs_gpu.txt)")
     ap.add_argument("--no-pin", action="store_true", help="N > 1: do not pin each rank to its own slice of the CPUs")
+    ap.add_argument("--bucket-mb", type=float, default=64.0, help="N > 1: GradSync bucket size in MB (the first bucket "
+                    "a quarter of it)")
     ap.add_argument("--bf16-grads", action="store_true", help="N > 1: all-reduce the gradient buckets in bf16 "
                     "(asrx.dist.GradSync comm_dtype; opt-in, fp32 by default)")
     ap.add_argument("--no-fp32-line", action="store_true", help="skip the side lines in the fp32 and x3 parity "
@@ -229,7 +231,11 @@ def main():
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), RANK="0", WORLD_SIZE="1")
     if distributed:
         if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            # no device_id: RCCL's communicator is then created at the first collective (the parameter broadcast)
+            # on the device set above.  The eager form (device_id=dev) measured 12 ms slower per tiny step in
+            # every later step, with or without collectives in them -- 1-rank group, 192.5 vs 180.5 ms, the
+            # lazy form at the N = 1 step time (profiles/r06_rccl_eager_init_ab.txt)
+            dist.init_process_group("nccl")
         else:
             dist.init_process_group(args.dist_backend)
 
@@ -248,7 +254,7 @@ def main():
     model.processor.graph_dead_blocks = args.graph_dead
     if distributed:
         broadcast_parameters(model)
-    gsync = GradSync(model, reduce_single=args.dist_single,
+    gsync = GradSync(model, bucket_mb=args.bucket_mb, reduce_single=args.dist_single,
                      comm_dtype=torch.bfloat16 if args.bf16_grads else torch.float32)
     model.set_noise(seed=0, step=rank * 1_000_000)
 
