@@ -24,7 +24,11 @@ struct CtrlRec {
 // this layer), ion (B,L) the v_gate output, mem_v (B) sigmoid(mem_gate(mem)), mem_w / mem (B,D),
 // jump_s (3), next_i (B) float layer index.  Outputs alpha, beta (B), gam (B,D), mem_w_out (B,D),
 // active (B), next_out (B), rec (B).
-__global__ __launch_bounds__(256) void msheath_ctrl_fwd_kernel(
+// CT: threads of the forward control kernel (one workgroup per sample): above D = 512 the mem-partial loads of 512
+// threads take half the dependent trips of 256 (8.6 vs 11.2 us at B = 8, L = 6002, D = 768); at D <= 512 the
+// 256-thread kernel is as fast or faster (7.8 vs 8.6 us at B = 32, D = 384; profiles/r06_ctrl_ab.txt)
+template <int CT>
+__global__ __launch_bounds__(CT) void msheath_ctrl_fwd_kernel(
     const float* __restrict__ policy, const float* __restrict__ gpol, int64_t ld_gpol, const float* __restrict__ ion,
     const float* __restrict__ mem_v, const float* __restrict__ mem_w, const float* __restrict__ mem,
     const float* __restrict__ jump_s, const float* __restrict__ next_i, int layer_i, int layers, int64_t L, int D,
@@ -32,28 +36,28 @@ __global__ __launch_bounds__(256) void msheath_ctrl_fwd_kernel(
     float* __restrict__ active, float* __restrict__ next_out, CtrlRec* __restrict__ rec, int64_t ld_mem_w,
     const float* __restrict__ mg_w, const float* __restrict__ mg_b, float* __restrict__ mem_v_out,
     const float* __restrict__ mem_part, int nchunk, float* __restrict__ mem_out) {
-  __shared__ float red[4];
+  __shared__ float red[CT / 64];
   const int64_t b = blockIdx.x;
-  // the sample's ion values (L <= 24 * 256: the configurations' 3001 / 6002 frames) are requested first, so
+  // the sample's ion values (L <= 12 * 512: the configurations' 3001 / 6002 frames) are requested first, so
   // their loads are in flight together with the mem partials' instead of after them
-  constexpr int IQ = 24;
+  constexpr int IQ = 6144 / CT;
   const float* ib = ion + b * L;
-  const bool ion_pre = L <= (int64_t)IQ * 256;
+  const bool ion_pre = L <= (int64_t)IQ * CT;
   float iv[IQ];
   if (ion_pre) {
 #pragma unroll
-    for (int j = 0; j < IQ; ++j) iv[j] = ib[min<int64_t>(threadIdx.x + 256 * j, L - 1)];
+    for (int j = 0; j < IQ; ++j) iv[j] = ib[min<int64_t>(threadIdx.x + CT * j, L - 1)];
   }
   if (mem_part) {  // mem = (1/L) sum over the row chunks of x_new, in chunk order (deterministic)
     // the chunk partials are loaded 16 at a time before they are added (in chunk order, so the sum
     // is bit-identical to the sequential loop): a dependent load-add chain over ~47 chunks left
     // every load's latency exposed (24 us per launch at B = 32)
-    // (a thread's two columns c0 and c0 + 256 in flight together, and the last partial group loaded from
+    // (a thread's two columns c0 and c0 + CT in flight together, and the last partial group loaded from
     // clamped addresses like the full ones: its serial remainder loop and the second column's separate pass
     // exposed ~20 load latencies per launch)
     const float* mp = mem_part + (int64_t)b * nchunk * D;
-    for (int c0 = threadIdx.x; c0 < D; c0 += 512) {
-      const int c1 = c0 + 256;
+    for (int c0 = threadIdx.x; c0 < D; c0 += 2 * CT) {
+      const int c1 = c0 + CT;
       const bool two = c1 < D;
       const int c1c = two ? c1 : c0;
       float t0 = 0.f, t1 = 0.f;
@@ -82,23 +86,23 @@ __global__ __launch_bounds__(256) void msheath_ctrl_fwd_kernel(
   if (ion_pre) {  // the thread's values in the order of the loop below
 #pragma unroll
     for (int j = 0; j < IQ; ++j)
-      if (threadIdx.x + 256 * j < L) s += iv[j];
+      if (threadIdx.x + CT * j < L) s += iv[j];
   } else {
-    for (int64_t l = threadIdx.x; l < L; l += 8 * 256) {  // 8 loads in flight (the tail's from clamped
+    for (int64_t l = threadIdx.x; l < L; l += 8 * CT) {  // 8 loads in flight (the tail's from clamped
       float v[8];                                          // addresses), added in the same order
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = ib[min<int64_t>(l + 256 * j, L - 1)];
+      for (int j = 0; j < 8; ++j) v[j] = ib[min<int64_t>(l + CT * j, L - 1)];
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        if (l + 256 * j < L) s += v[j];
+        if (l + CT * j < L) s += v[j];
     }
   }
-  const float potential = block_sum<256>(s, red) / (float)L;  // ion.mean(dim=1), model.py:466
+  const float potential = block_sum<CT>(s, red) / (float)L;  // ion.mean(dim=1), model.py:466
   float mv;
   if (mg_w) {  // mem_v = sigmoid(mem_gate(mem)) computed here (model.py:464)
     float t = 0.f;
-    for (int c = threadIdx.x; c < D; c += 256) t += mem[b * D + c] * mg_w[c];
-    mv = sigmoid_f(block_sum<256>(t, red) + mg_b[0]);
+    for (int c = threadIdx.x; c < D; c += CT) t += mem[b * D + c] * mg_w[c];
+    mv = sigmoid_f(block_sum<CT>(t, red) + mg_b[0]);
     if (threadIdx.x == 0) mem_v_out[b] = mv;
   } else {
     mv = mem_v[b];
@@ -138,7 +142,7 @@ __global__ __launch_bounds__(256) void msheath_ctrl_fwd_kernel(
   const float al = jumped ? 1.f : jump_g;
   const float be = jumped ? jw * jump_g : 0.f;
   const float cg = jumped ? (1.f - jw) * jump_g : 0.f;
-  for (int c = threadIdx.x; c < D; c += 256) {
+  for (int c = threadIdx.x; c < D; c += CT) {
     const float mw = mem_w[b * ld_mem_w + c];                 // ld 0: the (1, 1, D) parameter broadcast
     const float mwn = mv * mw + (1.f - mv) * mem[b * D + c];  // model.py:464
     gam[b * D + c] = cg * mwn;
@@ -640,6 +644,14 @@ __global__ void msheath_dx_final_kernel(float4* __restrict__ dx, const float4* _
 
 using namespace asrx;
 
+
+// the forward control kernel at its thread count for D (CT above)
+template <typename... A>
+static void ctrl_fwd_launch(int64_t D, int64_t B, hipStream_t stream, A... a) {
+  if (D > 512) msheath_ctrl_fwd_kernel<512><<<(unsigned)B, 512, 0, stream>>>(a...);
+  else msheath_ctrl_fwd_kernel<256><<<(unsigned)B, 256, 0, stream>>>(a...);
+}
+
 extern "C" {
 
 int asrx_jump_select4_bwd_acc(const float* g, const float* xn, const float* orig, const float* act,
@@ -719,7 +731,7 @@ int asrx_msheath_ctrl_fwd(const float* policy, const float* gpol, int64_t ld_gpo
                           float* alpha, float* beta, float* gam, float* mem_w_out, float* active, float* next_out,
                           void* rec, hipStream_t stream) {
   if (B == 0) return 0;
-  msheath_ctrl_fwd_kernel<<<(unsigned)B, 256, 0, stream>>>(policy, gpol, ld_gpol, ion, mem_v, mem_w, mem, jump_s,
+  ctrl_fwd_launch(D, B, stream, policy, gpol, ld_gpol, ion, mem_v, mem_w, mem, jump_s,
                                                            next_i, (int)layer_i, (int)layers, L, (int)D, alpha, beta,
                                                            gam, mem_w_out, active, next_out, (CtrlRec*)rec, D, nullptr,
                                                            nullptr, nullptr, nullptr, 0, nullptr);
@@ -734,7 +746,7 @@ int asrx_msheath_ctrl_fwd2(const float* policy, const float* gpol, int64_t ld_gp
                            int64_t L, int64_t D, float* alpha, float* beta, float* gam, float* mem_w_out, float* active,
                            float* next_out, void* rec, hipStream_t stream) {
   if (B == 0) return 0;
-  msheath_ctrl_fwd_kernel<<<(unsigned)B, 256, 0, stream>>>(policy, gpol, ld_gpol, ion, mem_v, mem_w, mem, jump_s,
+  ctrl_fwd_launch(D, B, stream, policy, gpol, ld_gpol, ion, mem_v, mem_w, mem, jump_s,
                                                            next_i, (int)layer_i, (int)layers, L, (int)D, alpha, beta,
                                                            gam, mem_w_out, active, next_out, (CtrlRec*)rec, ld_mem_w,
                                                            nullptr, nullptr, nullptr, nullptr, 0, nullptr);
@@ -752,7 +764,7 @@ int asrx_msheath_ctrl_fwd3(const float* policy, const float* gpol, int64_t ld_gp
                            void* rec, hipStream_t stream) {
   if (B == 0) return 0;
   const int nchunk = (int)((L + MEM_CHUNK - 1) / MEM_CHUNK);
-  msheath_ctrl_fwd_kernel<<<(unsigned)B, 256, 0, stream>>>(policy, gpol, ld_gpol, ion, nullptr, mem_w, mem, jump_s,
+  ctrl_fwd_launch(D, B, stream, policy, gpol, ld_gpol, ion, nullptr, mem_w, mem, jump_s,
                                                            next_i, (int)layer_i, (int)layers, L, (int)D, alpha, beta,
                                                            gam, mem_w_out, active, next_out, (CtrlRec*)rec, ld_mem_w,
                                                            mg_w, mg_b, mem_v_out, mem_part, nchunk, mem);
