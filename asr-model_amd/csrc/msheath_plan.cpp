@@ -13,6 +13,8 @@
 // weights); the caller keeps the Python path for the other modes.
 #include "common.h"
 
+#include <cstdlib>
+
 #include <cmath>
 
 extern "C" {
@@ -98,7 +100,22 @@ struct asrx_msheath_plan {
   const asrx_msheath_layer* layers;
 };
 
+namespace asrx {
+void set_msheath_row_nofill(bool on);  // rowops.hip
+}
+
 namespace {
+
+// The composite's row passes leave the rows of samples not at a layer unwritten (nothing in a no-grad forward reads
+// them; the Python path, whose saved tensors a backward reads, keeps zeroing them).  ASRX_ROW_NOFILL=0: zero them
+// here too (A/B).  Reset on every exit from asrx_msheath_fwd.
+struct RowNoFill {
+  RowNoFill() {
+    const char* e = std::getenv("ASRX_ROW_NOFILL");
+    asrx::set_msheath_row_nofill(!(e && e[0] == '0'));
+  }
+  ~RowNoFill() { asrx::set_msheath_row_nofill(false); }
+};
 
 // asrx/gemm.py _nj (NJ_MIN_TILES): the widest 128 * nj tile with enough tiles -- 200 for either width at >= 16384
 // rows, 180 (nj 3) / 144 (nj 2) below
@@ -195,6 +212,7 @@ int asrx_msheath_fwd(const asrx_msheath_plan* plan, const float* x0, const float
   ASRX_REQUIRE(ws && ws_bytes >= need, "asrx_msheath_fwd: workspace %ld < %ld bytes", (long)ws_bytes, (long)need);
   const int64_t rows = B * L, nl = P.n_layers, nchunk = asrx_mem_chunks(L);
   const int64_t rec_bytes = asrx_msheath_rec_bytes();
+  const RowNoFill nofill;
   const float inv_sqrt_d = (float)(1.0 / std::sqrt((double)D));
   // policy = softmax(MPNet(mean_l x0))   model.py:432-435, 375-385
   float* part_last = b.part + nl * B * nchunk * D;

@@ -652,6 +652,10 @@ struct MSRowFwd {
   float* part;
   float* xnew;
   int nchunk;
+  // rows of samples not at this layer are left unwritten instead of zeroed (no-grad composite forward only:
+  // nothing there reads them -- no backward, the row-list GEMMs' outputs of such rows are never consumed, the
+  // column sums and the jump skip such samples)
+  int nofill;
 };
 
 // Per row: px = LayerNorm(x); nx = |x|; g = sigmoid(px . gw + gb); v_gate from SH and nx (as
@@ -700,6 +704,7 @@ __global__ __launch_bounds__(64 * RW) void msheath_row_fwd_kernel(MSRowFwd p) {
   };
   auto row_body = [&](int64_t r, const float (&xv)[E], float sv, const float (&hv)[HQ]) __attribute__((always_inline)) {
     if (!at_layer(r)) {  // sample not at this layer: no reads; zeros keep every later consumer finite
+      if (p.nofill) return;
       float z[E];
 #pragma unroll
       for (int e = 0; e < E; ++e) z[e] = 0.f;
@@ -2576,6 +2581,14 @@ static bool ms_aligned(std::initializer_list<const void*> ps) {
   return true;
 }
 
+}  // extern "C"
+namespace asrx {
+static bool g_row_nofill = false;
+// asrx_msheath_fwd (msheath_plan.cpp, the no-grad composite) sets this around its layer loop
+void set_msheath_row_nofill(bool on) { g_row_nofill = on; }
+}  // namespace asrx
+extern "C" {
+
 // Fused MSheath layer row pass (msheath_row_fwd_kernel); SH = [S | h] with row stride ldsh >= M + Dh.
 int asrx_msheath_row_fwd2(const float* x, const float* lnw, const float* lnb, const float* gw, const float* gb,
                           const float* SH, int64_t ldsh, const float* mval, const float* w2, const float* b2,
@@ -2590,7 +2603,7 @@ int asrx_msheath_row_fwd2(const float* x, const float* lnw, const float* lnb, co
   if (rows == 0) return 0;
   MSRowFwd p{x, lnw, lnb, gw, gb, SH, mval, w2, b2, cw, cb, tx, px_bf16 ? nullptr : (float*)px, mean, rstd, nx, g,
              ion, kv, m2, rows, ldsh, (int)M, (int)Dh, eps, inv_sqrt_d, next_i, (int)layer, L > 0 ? L : 1,
-             px_bf16 ? (unsigned short*)px : nullptr};
+             px_bf16 ? (unsigned short*)px : nullptr, nullptr, nullptr, 0, asrx::g_row_nofill ? 1 : 0};
   const size_t shm = next_i ? (size_t)((rows + p.L - 1) / p.L) * sizeof(float) : 0;  // next_i copy
   ASRX_REQUIRE(shm <= 48 * 1024, "msheath_row_fwd: %ld samples exceed the next_i LDS copy", (long)(shm / 4));
   MS_DISPATCH(msheath_row_fwd_kernel, row_grid(rows), shm, p);
@@ -2613,7 +2626,8 @@ int asrx_msheath_row_fwd3(const float* x, const float* lnw, const float* lnb, co
   ASRX_REQUIRE(part && L > 0 && rows % L == 0, "asrx_msheath_row_fwd3: part and rows = B L required");
   if (rows == 0) return 0;
   MSRowFwd p{x, lnw, lnb, gw, gb, SH, mval, w2, b2, cw, cb, tx, px, mean, rstd, nx, g, ion, kv, m2, rows, ldsh,
-             (int)M, (int)Dh, eps, inv_sqrt_d, next_i, (int)layer, L, nullptr, part, xnew, (int)((L + 63) / 64)};
+             (int)M, (int)Dh, eps, inv_sqrt_d, next_i, (int)layer, L, nullptr, part, xnew, (int)((L + 63) / 64),
+             asrx::g_row_nofill ? 1 : 0};
   // next_i copy, then the RW waves' column sums of a chunk
   const size_t shm = (next_i ? (size_t)(rows / L) : 0) * sizeof(float) + (size_t)RW * d * sizeof(float);
   ASRX_REQUIRE(shm <= 48 * 1024, "msheath_row_fwd3: %ld samples exceed the next_i LDS copy", (long)(rows / L));
