@@ -788,7 +788,8 @@ __global__ __launch_bounds__(64 * RW) void msheath_row_fwd_kernel(MSRowFwd p) {
     // one workgroup per 64-row chunk of one sample (chunks never straddle samples): wave w takes the chunk's
     // rows w, w + RW, ... in order with the next row's loads in flight, and the RW waves' column sums are added
     // in wave order through LDS (deterministic)
-    float* red = ni_s + (p.next_i ? (p.rows + p.L - 1) / p.L : 0);  // RW x D floats after the next_i copy
+    // RW x D floats after the next_i copy, 16-byte aligned (the float2 lane accesses need 8)
+    float* red = ni_s + (p.next_i ? (((p.rows + p.L - 1) / p.L + 3) & ~(int64_t)3) : 0);
     const int w = threadIdx.x >> 6;
     const int64_t nb = (p.rows + p.L - 1) / p.L, nc = (int64_t)nb * p.nchunk;
     for (int64_t cid = blockIdx.x; cid < nc; cid += gridDim.x) {
@@ -2629,7 +2630,7 @@ int asrx_msheath_row_fwd3(const float* x, const float* lnw, const float* lnb, co
              (int)M, (int)Dh, eps, inv_sqrt_d, next_i, (int)layer, L, nullptr, part, xnew, (int)((L + 63) / 64),
              asrx::g_row_nofill ? 1 : 0};
   // next_i copy, then the RW waves' column sums of a chunk
-  const size_t shm = (next_i ? (size_t)(rows / L) : 0) * sizeof(float) + (size_t)RW * d * sizeof(float);
+  const size_t shm = (next_i ? (size_t)((rows / L + 3) & ~(int64_t)3) : 0) * sizeof(float) + (size_t)RW * d * sizeof(float);
   ASRX_REQUIRE(shm <= 48 * 1024, "msheath_row_fwd3: %ld samples exceed the next_i LDS copy", (long)(rows / L));
   const int64_t chunks = (rows / L) * p.nchunk;
   MS_DISPATCH(msheath_row_fwd_kernel, (unsigned)std::min<int64_t>(chunks, 65535), shm, p);

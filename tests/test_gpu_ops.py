@@ -363,8 +363,9 @@ def test_fork_sink_and_stream_groups(cuda):
     assert _rel(z.grad, ref) < 1e-6
 
 
-@pytest.mark.parametrize("fused,D", [(True, 128), (True, 384), (False, 128), (False, 192)])
-def test_msheath(cuda, fused, D):
+@pytest.mark.parametrize("fused,D,B", [(True, 128, 4), (True, 384, 4), (True, 384, 3), (False, 128, 4),
+                                       (False, 192, 4)])
+def test_msheath(cuda, fused, D, B):
     """MSheath (model.py:387-507), the fused single-node path (asrx/msheath.py, hand-written backward)
     and the per-op composition, against the oracle's per-sample while-loop: output, input gradient and
     every parameter's gradient, with potentials spread around the 0.1 threshold so samples take
@@ -383,7 +384,7 @@ def test_msheath(cuda, fused, D):
     with torch.no_grad():
         for i in range(layer):  # spread x_val around the 0.3 threshold so potentials vary per sample
             mod.layers[i]["v_gate"].concat.bias.fill_(0.3 + 0.1 * (i - 1))
-    B, L = 4, 30
+    L = 30  # B = 3: an odd sample count (the row pass's LDS layout after the per-sample next_i copy)
     x = torch.randn(B, L, D)
     x[1] *= 0.1
     trainable = {n for n, p in mod.named_parameters() if p.requires_grad}  # v_gate.tx is frozen
